@@ -1,0 +1,195 @@
+/*
+ * mrt.h -- C-ABI of the MI355X ray engine (libmrt.so).
+ *
+ * Drop-in boundary for the hot path of bitfrozen/rendering-algorithms-raytracer
+ * ("Miro"): per-pixel ray generation -> QBVH traversal -> Moller-Trumbore ->
+ * Lambert/Blinn shade + shadow rays.  Plain C types only (no torch / HIP types in
+ * the signatures; streams are passed as void*).  Every entry point cites the
+ * reference interface it replaces (paths relative to the reference repo).
+ *
+ * Conventions
+ *  - Return value: 0 (MRT_OK) or a negative MRT_ERR_* code; mrt_last_error()
+ *    gives a thread-local message.  No C++ exception crosses this ABI
+ *    (reference: bool returns + printf, src/TriangleMeshLoad.cpp:53-57).
+ *  - Ownership: the library copies every input array; the caller keeps its
+ *    buffers.  The scene owns its device memory; mrt_scene_destroy frees all
+ *    (reference: Scene never frees Objects, src/Scene.h:17-21).
+ *  - Frames are W*H, row 0 = bottom (reference src/Image.cpp:78-87,137-154).
+ *  - Numerics are the reference's x86 SSE contract:
+ *    hit t/a/b/prim and float RGB are bit-identical to the CPU restatement.
+ */
+#ifndef MRT_H
+#define MRT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MRT_ABI_VERSION 1
+
+enum {
+    MRT_OK = 0,
+    MRT_ERR_INVALID = -1,   /* bad argument / handle                              */
+    MRT_ERR_IO = -2,        /* file could not be read / parsed                    */
+    MRT_ERR_HIP = -3,       /* HIP runtime failure (device, alloc, launch)        */
+    MRT_ERR_BUILD = -4,     /* BVH build failed (degenerate input)                */
+    MRT_ERR_NOT_BUILT = -5, /* scene used before mrt_scene_build_bvh              */
+    MRT_ERR_OVERFLOW = -6,  /* traversal stack overflow detected on the device    */
+    MRT_ERR_NO_DEVICE = -7  /* no HIP device visible                              */
+};
+
+enum { MRT_LAMBERT = 0, MRT_BLINN = 1 };                 /* src/Lambert.h, src/Blinn.h */
+enum { MRT_POINT_LIGHT = 0, MRT_RECT_LIGHT = 1 };        /* src/Light.h:13 lightType_t  */
+
+typedef struct mrt_scene mrt_scene;
+
+/* Material as data (replaces virtual Material::shade, src/Material.h:18). */
+typedef struct {
+    int32_t type;            /* MRT_LAMBERT | MRT_BLINN                               */
+    float kd[3], ka[3], ks[3];
+    float spec_exp, spec_amt;/* Blinn m_specExp / m_specAmt (src/Blinn.h:59-61)       */
+} mrt_material;
+
+/* Light as data (replaces virtual Light::sampleLight, src/Light.h:35). */
+typedef struct {
+    int32_t type;            /* MRT_POINT_LIGHT | MRT_RECT_LIGHT                       */
+    float pos[3];            /* PointLight::setPosition                                */
+    float v1[3], v2[3], v3[3];/* RectangleLight::setVertices                           */
+    float power;             /* Light::setPower (area scaling applied internally)      */
+    int32_t samples;         /* Light::setSamples                                      */
+    float noise_threshold;   /* Light::setNoiseThreshold (default 0.001)               */
+    int32_t cast_shadows;    /* Light::setCastShadows                                  */
+} mrt_light;
+
+/* Camera (src/Camera.h:26-45): eye, lookAt, up, vertical FOV in degrees. */
+typedef struct {
+    float eye[3], look_at[3], up[3];
+    float fov_deg;
+} mrt_camera;
+
+/* Raw triangle mesh (TriangleMesh arrays, src/TriangleMesh.h:36-47). */
+typedef struct {
+    const float* verts;      /* nv*3                                                    */
+    const float* normals;    /* nn*3                                                    */
+    const uint32_t* vidx;    /* nt*3 vertex indices                                     */
+    const uint32_t* nidx;    /* nt*3 normal indices                                     */
+    int32_t nv, nn, nt;
+} mrt_mesh;
+
+typedef struct {             /* HitInfo (src/Ray.h:185-200); obj -> prim id           */
+    float t, a, b;
+    int32_t prim;            /* global triangle id in scene order, -1 = miss           */
+} mrt_hit;
+
+typedef struct {
+    int32_t nodes, leaves, prims;       /* QBVH nodes / 4-triangle leaf packets / tris */
+    int32_t bin_nodes, bin_leaves;      /* binary BVH before the 4-wide collapse       */
+    int32_t max_depth;
+    double build_ms;
+    uint64_t device_bytes;              /* node + leaf + shading arrays in HBM         */
+} mrt_bvh_info;
+
+typedef struct {
+    int32_t width, height;   /* frame size                                              */
+    int32_t device;          /* HIP device ordinal                                      */
+    int32_t count_visits;    /* 1: instrumented launch (node/leaf visit counters)       */
+    int32_t want_rgb8;       /* 1: also write tone-mapped 8-bit RGB (Image::Map)        */
+    int32_t want_hits;       /* 1: also write primary mrt_hit per pixel (debug/parity)  */
+    uint32_t seed;           /* stochastic configs only (counter RNG stream)            */
+} mrt_render_opts;
+
+typedef struct {
+    uint64_t primary_rays, shadow_rays;
+    uint64_t node_visits, leaf_visits;   /* all rays; valid when count_visits was set   */
+    uint64_t primary_node_visits, primary_leaf_visits; /* primary-ray launch share     */
+    uint64_t primary_hits;               /* primary rays that hit geometry               */
+    float kernel_ms;                     /* device time of the last frame (all launches)*/
+    float primary_ms, shade_ms;          /* per launch: primary rays / shade + shadows  */
+    int32_t max_stack;                   /* deepest traversal stack seen (count mode)   */
+} mrt_stats;
+
+const char* mrt_last_error(void);
+int mrt_abi_version(void);
+/* Number of visible HIP devices (0 when none); never initialises a context. */
+int mrt_device_count(void);
+
+/* ---- scene construction: Scene::addObject/addLight/preCalc (src/Scene.h:17-28) */
+mrt_scene* mrt_scene_create(void);
+void mrt_scene_destroy(mrt_scene* s);
+/* returns material id >= 0 */
+int mrt_scene_add_material(mrt_scene* s, const mrt_material* m);
+/* returns light id >= 0 */
+int mrt_scene_add_light(mrt_scene* s, const mrt_light* l);
+/* TriangleMesh::load(file, ctm) + makeMeshObjs (src/TriangleMeshLoad.cpp:50-214).
+ * ctm16: row-major 4x4 or NULL (identity).  Returns mesh id >= 0. */
+int mrt_scene_add_obj(mrt_scene* s, const char* path, const float* ctm16, int material);
+/* Raw mesh (TriangleMesh::createSingleTriangle + setV1..3 / setN1..3, src/TriangleMesh.cpp:11-42). */
+int mrt_scene_add_mesh(mrt_scene* s, const mrt_mesh* mesh, int material);
+int mrt_scene_mesh_info(const mrt_scene* s, int mesh, int32_t* nv, int32_t* nn, int32_t* nt);
+int mrt_scene_mesh_export(const mrt_scene* s, int mesh, float* verts, float* normals,
+                          uint32_t* vidx, uint32_t* nidx);
+/* Scene::setBGColor (src/Scene.h:37) */
+int mrt_scene_set_background(mrt_scene* s, const float rgb[3]);
+/* Scene::m_numPaths (src/Scene.h:61): shade() calls per primary hit */
+int mrt_scene_set_num_paths(mrt_scene* s, int num_paths);
+/* Scene::preCalc -> BVH::build (src/Scene.cpp:62-79, src/BVH.cpp:457-575):
+ * binned SAH, 4-wide collapse, host-side; then uploads to the device lazily. */
+int mrt_scene_build_bvh(mrt_scene* s);
+int mrt_scene_bvh_info(const mrt_scene* s, mrt_bvh_info* info);
+/* Canonical QBVH arrays: node_boxes[24*nodes] (minX4 minY4 minZ4 maxX4 maxY4 maxZ4),
+ * node_child[4*nodes] (>=0 inner node, ~leaf for a leaf slot, INT32_MIN empty),
+ * leaf_tris[36*leaves] (Ax4 Ay4 Az4 e0x4 e0y4 e0z4 e1x4 e1y4 e1z4),
+ * leaf_prims[4*leaves] (-1 empty).  (QBVH_Node / TriCache4, src/BVH.h:37-109) */
+int mrt_scene_bvh_export(const mrt_scene* s, float* node_boxes, int32_t* node_child,
+                         float* leaf_tris, int32_t* leaf_prims);
+/* Replace the built hierarchy with given canonical arrays (identical-BVH tests). */
+int mrt_scene_bvh_import(mrt_scene* s, int32_t nodes, int32_t leaves, const float* node_boxes,
+                         const int32_t* node_child, const float* leaf_tris, const int32_t* leaf_prims);
+/* Copy the scene to device `device` (done implicitly by render/trace). */
+int mrt_scene_upload(mrt_scene* s, int device);
+
+/* ---- frame entry: Scene::raytraceImage(Camera*, Image*) (src/Scene.cpp:85-217).
+ * Synchronous, host buffers: rgb (W*H*3 floats, before Map) and rgb8 (W*H*3,
+ * after Image::Map; nullable); hits (W*H, nullable).  1 spp primary + shadow. */
+int mrt_render(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
+               float* rgb, uint8_t* rgb8, mrt_hit* hits);
+
+/* ---- bucketed device render for multi-GPU tiling (src/Scene.cpp:90-174 buckets).
+ * Renders the 32x32 buckets listed in d_buckets (device int32 ids, row-major
+ * bucket grid) into d_tiles: n_buckets * 32*32*3 floats, bucket-major, pixels
+ * row-major inside a bucket (pixels outside the frame left untouched).
+ * Everything is enqueued on `stream` (hipStream_t, NULL = default); returns
+ * without synchronising.  Device pointers come from the caller (e.g. torch). */
+int mrt_render_buckets_async(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
+                             const int32_t* d_buckets, int32_t n_buckets, float* d_tiles,
+                             void* stream);
+/* Scatter bucket tiles into a W*H*3 float frame (and optional W*H*3 rgb8). */
+int mrt_unpack_buckets_async(const int32_t* d_buckets, int32_t n_buckets, const float* d_tiles,
+                             int32_t width, int32_t height, float* d_frame, uint8_t* d_frame8,
+                             const mrt_scene* s_for_lut, void* stream);
+/* Whole frame straight into device buffers (N = 1 fast path, no tiles). */
+int mrt_render_frame_async(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
+                           float* d_rgb, uint8_t* d_rgb8, void* stream);
+
+/* ---- batched ray query: Scene::trace / BVH::intersect (src/Scene.cpp:295-298,
+ * src/BVH.cpp:1112-1178).  o,d: n*3 floats; tmin,tmax: n floats.  any_hit=1
+ * stops at the first accepted triangle (shadow rays; occlusion result is
+ * identical to the reference's closest-hit shadow traversal). */
+int mrt_trace(mrt_scene* s, const float* o, const float* d, const float* tmin, const float* tmax,
+              size_t n, int any_hit, mrt_hit* out);
+int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const float* d_tmin,
+                    const float* d_tmax, size_t n, int any_hit, mrt_hit* d_out, void* stream);
+
+/* Counters of the last render on this scene (ray counts, visits, kernel time). */
+int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
+
+/* Numerics probes (x86 RCPSS/RSQRTSS emulation + one Newton step, SSE.h:67-101). */
+float mrt_rcp_nr(float x);
+float mrt_rsqrt_nr(float x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MRT_H */

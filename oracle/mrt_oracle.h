@@ -1,0 +1,116 @@
+/*
+ * mrt_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C CPU restatement of the reference (bitfrozen/rendering-algorithms-raytracer)
+ * hot path: OBJ load -> binned-SAH BVH -> QBVH collapse -> stack traversal ->
+ * 4-wide Moller-Trumbore -> Lambert/Blinn direct shading + PointLight /
+ * RectangleLight shadow rays -> gamma-LUT tone map.  Every function cites the
+ * reference file:line it restates.
+ *
+ * It is the CHECKER for the MI355X product (rendering-algorithms-raytracer_amd/),
+ * never part of it: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.
+ *
+ * PARITY UNPINNED against reference outputs: the reference cannot be compiled in
+ * this image without stand-ins for headers the image lacks (<GL/glut.h>,
+ * <Windows.h>; reference src/OpenGL.h:13, src/Scene.cpp:8) and it ships no tests,
+ * golden images or fixtures.  What IS pinned: the x86 RCPSS/RSQRTSS emulation
+ * (exhaustively, all 2^32 inputs, against live instructions), the OBJ-loader
+ * scaling facts and the QBVH node/leaf counts measured from the reference in
+ * SURVEY.md (tests/test_oracle_pins.py).
+ */
+#ifndef MRT_ORACLE_H
+#define MRT_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oro_scene oro_scene;
+
+enum { ORO_LAMBERT = 0, ORO_BLINN = 1 };
+enum { ORO_POINT_LIGHT = 0, ORO_RECT_LIGHT = 1 };
+
+typedef struct {
+    int type;               /* ORO_LAMBERT / ORO_BLINN                        */
+    float kd[3], ka[3], ks[3];
+    float specExp, specAmt; /* Blinn only (reference src/Blinn.h:11-22)       */
+} oro_material;
+
+typedef struct {
+    int type;               /* ORO_POINT_LIGHT / ORO_RECT_LIGHT               */
+    float pos[3];           /* point light position                            */
+    float v1[3], v2[3], v3[3]; /* rect light parallelogram                     */
+    float power;            /* as passed to setPower()                         */
+    int samples;            /* rect light samples (Light::m_numSamples)        */
+    float noiseThreshold;   /* Light::m_noiseThreshold (default epsilon)       */
+    int castShadows;
+} oro_light;
+
+typedef struct {
+    float eye[3], up[3], lookAt[3];
+    float fov;              /* degrees, as setFOV()                            */
+} oro_camera;
+
+typedef struct {
+    float t, a, b;
+    int32_t prim;           /* -1 on miss                                      */
+} oro_hit;
+
+/* mesh-level helpers ------------------------------------------------------- */
+/* Load an OBJ exactly as TriangleMesh::loadObj (src/TriangleMeshLoad.cpp:99-214).
+ * ctm: 16 floats row-major (m11..m44) or NULL for identity.
+ * Returns a mesh handle index inside the scene (>=0) or negative on error. */
+int oro_scene_add_obj(oro_scene* s, const char* path, const float* ctm, int material);
+/* Raw triangle mesh (TriangleMesh::createSingleTriangle-style: no ctm, no rcp). */
+int oro_scene_add_mesh(oro_scene* s, int nv, const float* verts, int nn, const float* normals,
+                       int nt, const uint32_t* vidx, const uint32_t* nidx, int material);
+int oro_mesh_info(const oro_scene* s, int mesh, int* nv, int* nn, int* nt);
+int oro_mesh_export(const oro_scene* s, int mesh, float* verts, float* normals,
+                    uint32_t* vidx, uint32_t* nidx);
+
+oro_scene* oro_scene_create(void);
+void oro_scene_destroy(oro_scene* s);
+int oro_scene_add_material(oro_scene* s, const oro_material* m);
+int oro_scene_add_light(oro_scene* s, const oro_light* l);
+void oro_scene_set_bg(oro_scene* s, float r, float g, float b);
+void oro_scene_set_num_paths(oro_scene* s, int n);
+/* Scene::preCalc -> BVH::build (src/Scene.cpp:62-79, src/BVH.cpp:457-575). */
+int oro_scene_build(oro_scene* s);
+/* Canonical QBVH export (preorder node numbering, leaf numbering = nodeNum). */
+int oro_qbvh_info(const oro_scene* s, int* n_nodes, int* n_leaves, int* n_prims,
+                  int* bin_nodes, int* bin_leaves, int* max_depth);
+int oro_qbvh_export(const oro_scene* s, float* node_boxes /*24/node*/, int32_t* node_child /*4/node*/,
+                    float* leaf_tris /*36/leaf*/, int32_t* leaf_prims /*4/leaf*/);
+
+/* Scene::trace for a batch (closest hit; reference src/BVH.cpp:1112-1178). */
+int oro_trace(const oro_scene* s, size_t n, const float* o /*3n*/, const float* d /*3n*/,
+              const float* tmin, const float* tmax, oro_hit* out,
+              uint32_t* node_visits, uint32_t* leaf_visits);
+
+/* Render rows [y0,y1) x columns [x0,x1) of a W x H frame (row 0 = bottom),
+ * 1 spp, Scene::adaptiveSampleScene with min=max subdivs=1 (src/Scene.cpp:252-293).
+ * rgb: W*H*3 floats (before Image::Map), rgb8: W*H*3 (after Map), hit: W*H
+ * primary hit records, shadow: W*H bitmask of occluded lights, may be NULL.
+ * counters[4] (nullable) += {primary rays, shadow rays, node visits, leaf visits}.
+ * n_threads > 1 uses OpenMP over rows (the oracle is deterministic per pixel). */
+int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H,
+               int x0, int y0, int x1, int y1,
+               float* rgb, uint8_t* rgb8, oro_hit* hit, uint32_t* shadow,
+               uint64_t* counters, int n_threads);
+
+/* numerics probes (for tests) */
+float oro_x86_rcp(float x);
+float oro_x86_rsqrt(float x);
+float oro_rcp_nr(float x);
+float oro_rsqrt_nr(float x);
+void oro_gamma_table(uint8_t* lut32769);
+/* counter-based RNG used in place of the reference's global MT pool */
+float oro_rand(uint32_t pixel, uint32_t sample, uint32_t dim, uint32_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

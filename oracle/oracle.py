@@ -1,0 +1,247 @@
+"""ctypes wrapper for the CPU oracle (oracle/_build/libmrt_oracle.so).
+
+TEST INFRASTRUCTURE ONLY.  Importable only from tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg.  The oracle is the checker, never the product.
+PARITY UNPINNED against reference outputs (see mrt_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libmrt_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = C.CDLL(_LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+class Material(C.Structure):
+    _fields_ = [("type", C.c_int), ("kd", C.c_float * 3), ("ka", C.c_float * 3), ("ks", C.c_float * 3),
+                ("specExp", C.c_float), ("specAmt", C.c_float)]
+
+
+class Light(C.Structure):
+    _fields_ = [("type", C.c_int), ("pos", C.c_float * 3), ("v1", C.c_float * 3), ("v2", C.c_float * 3),
+                ("v3", C.c_float * 3), ("power", C.c_float), ("samples", C.c_int),
+                ("noiseThreshold", C.c_float), ("castShadows", C.c_int)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("eye", C.c_float * 3), ("up", C.c_float * 3), ("lookAt", C.c_float * 3), ("fov", C.c_float)]
+
+
+class Hit(C.Structure):
+    _fields_ = [("t", C.c_float), ("a", C.c_float), ("b", C.c_float), ("prim", C.c_int32)]
+
+
+HIT_DTYPE = np.dtype([("t", "<f4"), ("a", "<f4"), ("b", "<f4"), ("prim", "<i4")])
+
+_fp = C.POINTER(C.c_float)
+_u32p = C.POINTER(C.c_uint32)
+_i32p = C.POINTER(C.c_int32)
+_u8p = C.POINTER(C.c_uint8)
+_u64p = C.POINTER(C.c_uint64)
+
+
+def _declare(L):
+    L.oro_scene_create.restype = C.c_void_p
+    L.oro_scene_destroy.argtypes = [C.c_void_p]
+    L.oro_scene_add_obj.argtypes = [C.c_void_p, C.c_char_p, _fp, C.c_int]
+    L.oro_scene_add_mesh.argtypes = [C.c_void_p, C.c_int, _fp, C.c_int, _fp, C.c_int, _u32p, _u32p, C.c_int]
+    L.oro_mesh_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.oro_mesh_export.argtypes = [C.c_void_p, C.c_int, _fp, _fp, _u32p, _u32p]
+    L.oro_scene_add_material.argtypes = [C.c_void_p, C.POINTER(Material)]
+    L.oro_scene_add_light.argtypes = [C.c_void_p, C.POINTER(Light)]
+    L.oro_scene_set_bg.argtypes = [C.c_void_p, C.c_float, C.c_float, C.c_float]
+    L.oro_scene_set_num_paths.argtypes = [C.c_void_p, C.c_int]
+    L.oro_scene_build.argtypes = [C.c_void_p]
+    L.oro_qbvh_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 6
+    L.oro_qbvh_export.argtypes = [C.c_void_p, _fp, _i32p, _fp, _i32p]
+    L.oro_trace.argtypes = [C.c_void_p, C.c_size_t, _fp, _fp, _fp, _fp, C.c_void_p, _u32p, _u32p]
+    L.oro_render.argtypes = [C.c_void_p, C.POINTER(Camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                             _fp, _u8p, C.c_void_p, _u32p, _u64p, C.c_int]
+    for n in ("oro_x86_rcp", "oro_x86_rsqrt", "oro_rcp_nr", "oro_rsqrt_nr"):
+        getattr(L, n).argtypes = [C.c_float]
+        getattr(L, n).restype = C.c_float
+    L.oro_gamma_table.argtypes = [_u8p]
+    L.oro_rand.argtypes = [C.c_uint32] * 4
+    L.oro_rand.restype = C.c_float
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _v3(x):
+    return (C.c_float * 3)(*[float(v) for v in x])
+
+
+class OracleScene:
+    """Scene builder mirroring the reference scene scripts (src/assignment2.h)."""
+
+    def __init__(self):
+        self.L = lib()
+        self.h = self.L.oro_scene_create()
+        self.n_lights = 0
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.L.oro_scene_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def add_material(self, kind="lambert", kd=(1, 1, 1), ka=(0, 0, 0), ks=(1, 1, 1), specExp=1.0, specAmt=0.0):
+        m = Material(0 if kind == "lambert" else 1, _v3(kd), _v3(ka), _v3(ks), specExp, specAmt)
+        return self.L.oro_scene_add_material(self.h, C.byref(m))
+
+    def add_obj(self, path, material, ctm=None):
+        ctm_p = None
+        if ctm is not None:
+            arr = np.ascontiguousarray(np.asarray(ctm, np.float32).reshape(16))
+            ctm_p = _p(arr, _fp)
+        r = self.L.oro_scene_add_obj(self.h, path.encode(), ctm_p, material)
+        if r < 0:
+            raise RuntimeError(f"oracle OBJ load failed ({r}): {path}")
+        return r
+
+    def add_mesh(self, verts, normals, vidx, nidx, material):
+        v = np.ascontiguousarray(verts, np.float32).reshape(-1, 3)
+        n = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
+        vi = np.ascontiguousarray(vidx, np.uint32).reshape(-1, 3)
+        ni = np.ascontiguousarray(nidx, np.uint32).reshape(-1, 3)
+        r = self.L.oro_scene_add_mesh(self.h, len(v), _p(v, _fp), len(n), _p(n, _fp), len(vi),
+                                      _p(vi, _u32p), _p(ni, _u32p), material)
+        if r < 0:
+            raise RuntimeError("oracle add_mesh failed")
+        return r
+
+    def mesh_arrays(self, mesh):
+        nv, nn, nt = C.c_int(), C.c_int(), C.c_int()
+        self.L.oro_mesh_info(self.h, mesh, C.byref(nv), C.byref(nn), C.byref(nt))
+        v = np.zeros((nv.value, 3), np.float32)
+        n = np.zeros((nn.value, 3), np.float32)
+        vi = np.zeros((nt.value, 3), np.uint32)
+        ni = np.zeros((nt.value, 3), np.uint32)
+        self.L.oro_mesh_export(self.h, mesh, _p(v, _fp), _p(n, _fp), _p(vi, _u32p), _p(ni, _u32p))
+        return v, n, vi, ni
+
+    def add_point_light(self, pos, power, cast_shadows=True):
+        l = Light()
+        l.type = 0
+        l.pos = _v3(pos)
+        l.power = power
+        l.samples = 1
+        l.noiseThreshold = 0.001
+        l.castShadows = int(cast_shadows)
+        self.n_lights += 1
+        return self.L.oro_scene_add_light(self.h, C.byref(l))
+
+    def add_rect_light(self, v1, v2, v3, power, samples=1, noise=0.001, cast_shadows=True):
+        l = Light()
+        l.type = 1
+        l.v1, l.v2, l.v3 = _v3(v1), _v3(v2), _v3(v3)
+        l.power = power
+        l.samples = samples
+        l.noiseThreshold = noise
+        l.castShadows = int(cast_shadows)
+        self.n_lights += 1
+        return self.L.oro_scene_add_light(self.h, C.byref(l))
+
+    def set_bg(self, rgb):
+        self.L.oro_scene_set_bg(self.h, *[float(x) for x in rgb])
+
+    def set_num_paths(self, n):
+        self.L.oro_scene_set_num_paths(self.h, int(n))
+
+    def build(self):
+        r = self.L.oro_scene_build(self.h)
+        if r != 0:
+            raise RuntimeError(f"oracle BVH build failed ({r})")
+
+    def qbvh_info(self):
+        vals = [C.c_int() for _ in range(6)]
+        self.L.oro_qbvh_info(self.h, *[C.byref(v) for v in vals])
+        keys = ("nodes", "leaves", "prims", "bin_nodes", "bin_leaves", "max_depth")
+        return {k: v.value for k, v in zip(keys, vals)}
+
+    def qbvh_export(self):
+        info = self.qbvh_info()
+        nb = np.zeros((info["nodes"], 24), np.float32)
+        nc = np.zeros((info["nodes"], 4), np.int32)
+        lt = np.zeros((info["leaves"], 36), np.float32)
+        lp = np.zeros((info["leaves"], 4), np.int32)
+        self.L.oro_qbvh_export(self.h, _p(nb, _fp), _p(nc, _i32p), _p(lt, _fp), _p(lp, _i32p))
+        return nb, nc, lt, lp
+
+    def trace(self, o, d, tmin, tmax):
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        n = len(o)
+        tmin = np.ascontiguousarray(np.broadcast_to(np.float32(tmin), (n,)) if np.ndim(tmin) == 0 else tmin, np.float32)
+        tmax = np.ascontiguousarray(np.broadcast_to(np.float32(tmax), (n,)) if np.ndim(tmax) == 0 else tmax, np.float32)
+        out = np.zeros(n, HIT_DTYPE)
+        nv = np.zeros(n, np.uint32)
+        lv = np.zeros(n, np.uint32)
+        r = self.L.oro_trace(self.h, n, _p(o, _fp), _p(d, _fp), _p(tmin, _fp), _p(tmax, _fp),
+                             out.ctypes.data, _p(nv, _u32p), _p(lv, _u32p))
+        if r != 0:
+            raise RuntimeError(f"oracle trace failed ({r})")
+        return out, nv, lv
+
+    def render(self, cam, W, H, rect=None, threads=1, want_hits=True):
+        """cam: dict(eye, lookAt, up, fov).  Returns dict of numpy arrays."""
+        c = Camera(_v3(cam["eye"]), _v3(cam.get("up", (0, 1, 0))), _v3(cam["lookAt"]), float(cam["fov"]))
+        x0, y0, x1, y1 = rect if rect is not None else (0, 0, W, H)
+        rgb = np.zeros((H, W, 3), np.float32)
+        rgb8 = np.zeros((H, W, 3), np.uint8)
+        hits = np.zeros((H, W), HIT_DTYPE) if want_hits else None
+        shadow = np.zeros((H, W), np.uint32)
+        counters = np.zeros(4, np.uint64)
+        r = self.L.oro_render(self.h, C.byref(c), W, H, x0, y0, x1, y1, _p(rgb, _fp), _p(rgb8, _u8p),
+                              hits.ctypes.data if hits is not None else None, _p(shadow, _u32p),
+                              _p(counters, _u64p), int(threads))
+        if r != 0:
+            raise RuntimeError(f"oracle render failed ({r})")
+        return {"rgb": rgb, "rgb8": rgb8, "hits": hits, "shadow": shadow,
+                "primary_rays": int(counters[0]), "shadow_rays": int(counters[1]),
+                "node_visits": int(counters[2]), "leaf_visits": int(counters[3])}
+
+
+def x86_rcp(x):
+    return lib().oro_x86_rcp(float(x))
+
+
+def x86_rsqrt(x):
+    return lib().oro_x86_rsqrt(float(x))
+
+
+def rcp_nr(x):
+    return lib().oro_rcp_nr(float(x))
+
+
+def rsqrt_nr(x):
+    return lib().oro_rsqrt_nr(float(x))
+
+
+def gamma_table():
+    t = np.zeros(32769, np.uint8)
+    lib().oro_gamma_table(_p(t, _u8p))
+    return t

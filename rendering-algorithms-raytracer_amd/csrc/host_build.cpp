@@ -1,0 +1,567 @@
+// host_build.cpp -- OBJ loading and QBVH construction (host side of libmrt).
+//
+// Restates the reference's scene-build semantics so that the device traverses
+// the same hierarchy the reference would build for the same input:
+//   TriangleMesh::loadObj           src/TriangleMeshLoad.cpp:99-214
+//   BVH::build (USE_BINS, USE_QBVH) src/BVH.cpp:457-575
+//   BVH_Node::buildBin              src/BVH.cpp:625-689
+//   BVH_Node::partitionSweepBin     src/BVH.cpp:691-901
+//   BVH_Node::calcSAHCost           src/BVH.cpp:1076-1106
+//   QBVH_Node::build / buildTriBundle src/BVH.cpp:64-389
+// The binary tree is built into a flat arena and collapsed in one pass into the
+// HBM layout (mrt_types.h).  Quirks of the reference that shape the tree are
+// kept on purpose (they are pinned by SURVEY.md's explosion01 node/leaf counts):
+//   * the loose partition does not swap bin ids with the objects it moves;
+//   * the <128-object sweep's left/right areas skip the first/last object;
+//   * qsort is glibc's stable merge sort (so std::stable_sort).
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+
+#include "mrt_scene.h"
+
+#define MRT_TABLE_QUAL static const
+#include "x86_approx_tables.inc"
+
+namespace mrt {
+
+namespace {
+struct Tables {
+    uint16_t rcp[2048], rsq[2048];
+    uint8_t gamma[32769];
+    Tables() {
+        for (int i = 0; i < 2048; i++) {
+            rcp[i] = (uint16_t)((MRT_RCP_TABLE[i] >> 11) & 0xFFFu);
+            rsq[i] = (uint16_t)((MRT_RSQRT_TABLE[i] >> 11) & 0xFFFu);
+        }
+        // Image::generateGammaTables (src/Image.cpp:19-35): float pow, double tail.
+        const float GAMMA = 2.2f;
+        for (int i = 0; i < 32769; i++) {
+            float r2 = (float)((double)powf(i / 32768.0f, 1 / GAMMA) * 255.0 + 0.5);
+            gamma[i] = (uint8_t)(int)r2;
+        }
+    }
+};
+const Tables& tables() {
+    static Tables t;
+    return t;
+}
+}  // namespace
+
+const uint16_t* host_rcp_table() { return tables().rcp; }
+const uint16_t* host_rsqrt_table() { return tables().rsq; }
+const uint8_t* host_gamma_lut() { return tables().gamma; }
+
+// ------------------------------------------------------------------ Matrix4x4
+namespace {
+struct Mat4 {
+    float m[4][4];
+};
+Mat4 identity() {
+    Mat4 M{};
+    M.m[0][0] = M.m[1][1] = M.m[2][2] = M.m[3][3] = 1.0f;
+    return M;
+}
+// Matrix4x4::invert (src/Matrix4x4.h:353-412): cofactors, 1/det in double.
+Mat4 inverse(const Mat4& A) {
+    const float(*a)[4] = A.m;
+    auto t2 = [](float p, float q, float r, float s) { return p * q - r * s; };
+    float T34_12 = t2(a[2][0], a[3][1], a[2][1], a[3][0]), T34_13 = t2(a[2][0], a[3][2], a[2][2], a[3][0]);
+    float T34_14 = t2(a[2][0], a[3][3], a[2][3], a[3][0]), T34_23 = t2(a[2][1], a[3][2], a[2][2], a[3][1]);
+    float T34_24 = t2(a[2][1], a[3][3], a[2][3], a[3][1]), T34_34 = t2(a[2][2], a[3][3], a[2][3], a[3][2]);
+    float T24_12 = t2(a[1][0], a[3][1], a[1][1], a[3][0]), T24_13 = t2(a[1][0], a[3][2], a[1][2], a[3][0]);
+    float T24_14 = t2(a[1][0], a[3][3], a[1][3], a[3][0]), T24_23 = t2(a[1][1], a[3][2], a[1][2], a[3][1]);
+    float T24_24 = t2(a[1][1], a[3][3], a[1][3], a[3][1]), T24_34 = t2(a[1][2], a[3][3], a[1][3], a[3][2]);
+    float T23_12 = t2(a[1][0], a[2][1], a[1][1], a[2][0]), T23_13 = t2(a[1][0], a[2][2], a[1][2], a[2][0]);
+    float T23_14 = t2(a[1][0], a[2][3], a[1][3], a[2][0]), T23_23 = t2(a[1][1], a[2][2], a[1][2], a[2][1]);
+    float T23_24 = t2(a[1][1], a[2][3], a[1][3], a[2][1]), T23_34 = t2(a[1][2], a[2][3], a[1][3], a[2][2]);
+    auto s3 = [](float p, float q, float r, float s, float u, float v) { return p * q - r * s + u * v; };
+    float sd11 = s3(a[1][1], T34_34, a[1][2], T34_24, a[1][3], T34_23);
+    float sd12 = s3(a[1][0], T34_34, a[1][2], T34_14, a[1][3], T34_13);
+    float sd13 = s3(a[1][0], T34_24, a[1][1], T34_14, a[1][3], T34_12);
+    float sd14 = s3(a[1][0], T34_23, a[1][1], T34_13, a[1][2], T34_12);
+    float sd21 = s3(a[0][1], T34_34, a[0][2], T34_24, a[0][3], T34_23);
+    float sd22 = s3(a[0][0], T34_34, a[0][2], T34_14, a[0][3], T34_13);
+    float sd23 = s3(a[0][0], T34_24, a[0][1], T34_14, a[0][3], T34_12);
+    float sd24 = s3(a[0][0], T34_23, a[0][1], T34_13, a[0][2], T34_12);
+    float sd31 = s3(a[0][1], T24_34, a[0][2], T24_24, a[0][3], T24_23);
+    float sd32 = s3(a[0][0], T24_34, a[0][2], T24_14, a[0][3], T24_13);
+    float sd33 = s3(a[0][0], T24_24, a[0][1], T24_14, a[0][3], T24_12);
+    float sd34 = s3(a[0][0], T24_23, a[0][1], T24_13, a[0][2], T24_12);
+    float sd41 = s3(a[0][1], T23_34, a[0][2], T23_24, a[0][3], T23_23);
+    float sd42 = s3(a[0][0], T23_34, a[0][2], T23_14, a[0][3], T23_13);
+    float sd43 = s3(a[0][0], T23_24, a[0][1], T23_14, a[0][3], T23_12);
+    float sd44 = s3(a[0][0], T23_23, a[0][1], T23_13, a[0][2], T23_12);
+    float det = a[0][0] * sd11 - a[0][1] * sd12 + a[0][2] * sd13 - a[0][3] * sd14;
+    float di = (float)(1.0 / (double)det);
+    Mat4 R;
+    const float sd[4][4] = {{sd11, sd12, sd13, sd14}, {sd21, sd22, sd23, sd24},
+                            {sd31, sd32, sd33, sd34}, {sd41, sd42, sd43, sd44}};
+    // R(r,c) = (-1)^(r+c) * sd[c][r] * di
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) R.m[r][c] = (((r + c) & 1) ? -sd[c][r] : sd[c][r]) * di;
+    return R;
+}
+Mat4 transpose(const Mat4& A) {
+    Mat4 R;
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) R.m[r][c] = A.m[c][r];
+    return R;
+}
+// DPPS 0xFF: (p0 + p1) + (p2 + p3)
+inline float dp4(const float* row, const float* u) {
+    float p0 = row[0] * u[0], p1 = row[1] * u[1], p2 = row[2] * u[2], p3 = row[3] * u[3];
+    return (p0 + p1) + (p2 + p3);
+}
+// multiplyAndDivideByW(__m128 (x,y,z,1)), src/Matrix4x4.h:744-748
+v3 xform_point(const Mat4& M, v3 p) {
+    const float u[4] = {p.x, p.y, p.z, 1.0f};
+    float w = rcp_nr(dp4(M.m[3], u), host_rcp_table());
+    return mk(w * dp4(M.m[0], u), w * dp4(M.m[1], u), w * dp4(M.m[2], u));
+}
+// operator*(Matrix4x4, Vector3), src/Matrix4x4.h:693-704 (non-SSE path)
+v3 xform_dir(const Mat4& M, v3 u) {
+    return mk(M.m[0][0] * u.x + M.m[0][1] * u.y + M.m[0][2] * u.z,
+              M.m[1][0] * u.x + M.m[1][1] * u.y + M.m[1][2] * u.z,
+              M.m[2][0] * u.x + M.m[2][1] * u.y + M.m[2][2] * u.z);
+}
+
+// getIndices, src/TriangleMeshLoad.cpp:67-97
+void split_indices(char* word, int& vi, int& ti, int& ni) {
+    static char blank[] = " ";
+    char* tp = blank;
+    char* np = blank;
+    for (char* p = word; *p; ++p) {
+        if (*p != '/') continue;
+        if (tp == blank) tp = p + 1;
+        else np = p + 1;
+        *p = '\0';
+    }
+    vi = atoi(word);
+    ti = atoi(tp);
+    ni = atoi(np);
+}
+}  // namespace
+
+// TriangleMesh::loadObj, src/TriangleMeshLoad.cpp:99-214.  Two passes over
+// 79-character fgets chunks; vertices through ctm with the rcp_nr w-divide;
+// normals through the inverse transpose and renormalised; a face without a
+// normal on its last corner gets a face normal appended at slot `nn`
+// (the reference also stores its index triple at m_normalIndices[nn]).
+// Reference UB (negative / out-of-range indices, slot overflow) -> MRT_ERR_IO.
+int load_obj(const char* path, const float* ctm16, Mesh& out, std::string& err) {
+    FILE* fp = fopen(path, "rb");
+    if (!fp) {
+        err = std::string("cannot open ") + path;
+        return MRT_ERR_IO;
+    }
+    Mat4 ctm = identity();
+    if (ctm16) memcpy(ctm.m, ctm16, sizeof(float) * 16);
+    const Mat4 nctm = transpose(inverse(ctm));
+    const uint16_t* RS = host_rsqrt_table();
+
+    char line[81];
+    int nv = 0, nt = 0, nn = 0, nf = 0;
+    while (fgets(line, 80, fp)) {
+        if (line[0] == 'v') {
+            if (line[1] == 'n') nn++;
+            else if (line[1] == 't') nt++;
+            else nv++;
+        } else if (line[0] == 'f') {
+            nf++;
+        }
+    }
+    (void)nt;
+    fseek(fp, 0, SEEK_SET);
+    out.verts.assign((size_t)nv, v3{0, 0, 0});
+    out.normals.assign((size_t)3 * nv + 1, v3{0, 0, 0});
+    out.vidx.assign((size_t)3 * nf, 0u);
+    out.nidx.assign((size_t)3 * nf, 0u);
+    int nverts = 0, nnorm = 0, ntris = 0;
+    int rc = MRT_OK;
+    while (rc == MRT_OK && fgets(line, 80, fp)) {
+        if (line[0] == 'v') {
+            float x = 0, y = 0, z = 0;
+            if (line[1] == 'n') {
+                sscanf(&line[2], "%f %f %f\n", &x, &y, &z);
+                if (nnorm >= 3 * nv + 1) { rc = MRT_ERR_IO; err = "too many normals"; break; }
+                out.normals[nnorm++] = normalized(xform_dir(nctm, mk(x, y, z)), RS);
+            } else if (line[1] != 't') {
+                sscanf(&line[1], "%f %f %f\n", &x, &y, &z);
+                out.verts[nverts++] = xform_point(ctm, mk(x, y, z));
+            }
+        } else if (line[0] == 'f') {
+            char tok[3][32];
+            tok[0][0] = tok[1][0] = tok[2][0] = 0;
+            sscanf(&line[1], "%31s %31s %31s\n", tok[0], tok[1], tok[2]);
+            int v = 0, t = 0, n = 0;
+            for (int k = 0; k < 3; k++) {
+                split_indices(tok[k], v, t, n);
+                if (v <= 0 || v > nv) { rc = MRT_ERR_IO; err = "face vertex index out of range"; break; }
+                out.vidx[3 * ntris + k] = (uint32_t)(v - 1);
+                if (n) out.nidx[3 * ntris + k] = (uint32_t)(n - 1);
+            }
+            if (rc != MRT_OK) break;
+            if (!n) {
+                if (nn >= nf || nn >= 3 * nv) { rc = MRT_ERR_IO; err = "face-normal slot overflow"; break; }
+                const uint32_t* f = &out.vidx[3 * ntris];
+                v3 e1 = sub(out.verts[f[1]], out.verts[f[0]]);
+                v3 e2 = sub(out.verts[f[2]], out.verts[f[0]]);
+                out.normals[nn] = normalized(cross(e1, e2), RS);
+                out.nidx[3 * nn + 0] = out.nidx[3 * nn + 1] = out.nidx[3 * nn + 2] = (uint32_t)nn;
+                nn++;
+            }
+            ntris++;
+        }
+    }
+    fclose(fp);
+    if (rc != MRT_OK) return rc;
+    out.normals.resize((size_t)std::max(nn, 1));
+    out.vidx.resize((size_t)3 * ntris);
+    out.nidx.resize((size_t)3 * ntris);
+    for (uint32_t i : out.nidx)
+        if (i >= out.normals.size()) { err = "normal index out of range"; return MRT_ERR_IO; }
+    return MRT_OK;
+}
+
+// ------------------------------------------------------------------ BVH
+namespace {
+
+struct Box {
+    float mn[3], mx[3];
+};
+inline Box empty_box() {  // AABB(): bbMin(MIRO_TMAX), bbMax(-MIRO_TMAX), src/Object.h:13
+    return Box{{1e12f, 1e12f, 1e12f}, {-1e12f, -1e12f, -1e12f}};
+}
+inline Box merge(const Box& a, const Box& b) {  // AABB(bb1, bb2), src/Object.h:16-23
+    Box r;
+    for (int k = 0; k < 3; k++) {
+        r.mn[k] = std_min(a.mn[k], b.mn[k]);
+        r.mx[k] = std_max(a.mx[k], b.mx[k]);
+    }
+    return r;
+}
+inline float area(const Box& b) {  // AABB::getArea, src/Object.h:32-34
+    float dx = b.mx[0] - b.mn[0];
+    float s = ((dx + b.mx[2]) - b.mn[2]) * (b.mx[1] - b.mn[1]);
+    return 2.0f * (s + dx * (b.mx[2] - b.mn[2]));
+}
+inline float sah(int ln, float la, int rn, float ra) {  // calcSAHCost, src/BVH.cpp:1076-1106
+    if (ln + rn >= 32) return ((float)ln) * la + ((float)rn) * ra;
+    auto pen = [](int n) { return n % 4 == 0 ? 0.5f : n % 3 == 0 ? 10.f : n % 2 == 0 ? 100.f : 1000.f; };
+    return ((float)ln) * la * pen(ln) + ((float)rn) * ra * pen(rn);
+}
+// cvttss2si: out-of-range / NaN -> INT_MIN
+inline int trunc_x86(float f) {
+    if (!(f >= -2147483648.0f && f < 2147483648.0f)) return (int)0x80000000u;
+    return (int)f;
+}
+
+struct BNode {
+    Box box;
+    int32_t left = -1;   // children are left, left+1
+    int32_t start = 0, count = 0;
+    bool leaf = false;
+};
+
+class Builder {
+   public:
+    Builder(Scene& s) : s_(s) {}
+
+    int run(std::string& err) {
+        const int n = (int)s_.obj_mesh.size();
+        tri_box_.resize(n);
+        cen_obj_.resize((size_t)3 * n);
+        for (int i = 0; i < n; i++) {
+            tri_box_[i] = tri_aabb(i);
+            for (int k = 0; k < 3; k++) cen_obj_[3 * i + k] = (tri_box_[i].mn[k] + tri_box_[i].mx[k]) * 0.5f;
+        }
+        objs_.resize(n);
+        pre_.resize(n);
+        cen_.resize((size_t)3 * n);
+        bin_ids_.resize(n);
+        for (int i = 0; i < n; i++) {
+            objs_[i] = i;
+            pre_[i] = tri_box_[i];
+            for (int k = 0; k < 3; k++) cen_[3 * i + k] = cen_obj_[3 * i + k];
+        }
+        bn_.reserve((size_t)2 * n + 2);
+        bn_.emplace_back();
+        build_bin(0, 0, n);
+        if (fail_) {
+            err = fail_msg_;
+            return MRT_ERR_BUILD;
+        }
+        collapse();
+        return MRT_OK;
+    }
+
+    int bin_leaves = 0, bin_depth = 0, q_depth = 0;
+
+   private:
+    Box tri_aabb(int o) const {  // TriangleMesh::getAABB, src/TriangleMesh.cpp:156-195
+        const Mesh& m = s_.meshes[s_.obj_mesh[o]];
+        const uint32_t* f = &m.vidx[3 * (size_t)s_.obj_tri[o]];
+        v3 A = m.verts[f[0]], B = m.verts[f[1]], C = m.verts[f[2]];
+        return Box{{std_min(A.x, std_min(B.x, C.x)), std_min(A.y, std_min(B.y, C.y)), std_min(A.z, std_min(B.z, C.z))},
+                   {std_max(A.x, std_max(B.x, C.x)), std_max(A.y, std_max(B.y, C.y)), std_max(A.z, std_max(B.z, C.z))}};
+    }
+
+    // qsort(objs, n, sizeof(Object*), Object::sortBy{X,Y,Z}Component): glibc msort is
+    // stable, so std::stable_sort with the same three-way comparator.
+    void sort_by_axis(int start, int n, int axis) {
+        const float* c = cen_obj_.data();
+        std::stable_sort(objs_.begin() + start, objs_.begin() + start + n,
+                         [c, axis](int a, int b) { return c[3 * a + axis] < c[3 * b + axis]; });
+    }
+
+    // BVH_Node::buildBin, src/BVH.cpp:625-689
+    void build_bin(int node, int start, int n) {
+        if (fail_) return;
+        Box b = empty_box();
+        for (int i = 0; i < n; i++) b = merge(b, tri_box_[objs_[start + i]]);
+        bn_[node].box = b;
+        if (n <= 4) {
+            bn_[node].leaf = true;
+            bn_[node].start = start;
+            bn_[node].count = n;
+            bin_leaves++;
+            return;
+        }
+        depth_++;
+        bin_depth = std::max(bin_depth, depth_);
+        unsigned part = 0;
+        partition(start, n, part);
+        if (fail_) return;
+        unsigned ln = part + 1u, rn = (unsigned)n - part - 1u;
+        if (ln == 0u || rn == 0u || ln > (unsigned)n) {
+            fail("BVH partition produced an empty side (reference would recurse forever)");
+            return;
+        }
+        int32_t l = (int32_t)bn_.size();
+        bn_.emplace_back();
+        bn_.emplace_back();
+        bn_[node].left = l;
+        build_bin(l, start, (int)ln);
+        build_bin(l + 1, start + (int)ln, (int)rn);
+        depth_--;
+    }
+
+    // BVH_Node::partitionSweepBin, src/BVH.cpp:691-901
+    void partition(int start, int n, unsigned& partPt) {
+        float best = INFINITY;
+        unsigned bestAxis = 0;
+        int binPart = 0;
+        int* objs = objs_.data() + start;
+        Box* pre = pre_.data() + start;
+        float* cen = cen_.data() + 3 * (size_t)start;
+        if (n >= 128) {
+            Box bb = empty_box();
+            for (int i = 0; i < n; i++)
+                for (int k = 0; k < 3; k++) {
+                    bb.mn[k] = std_min(bb.mn[k], cen[3 * i + k]);
+                    bb.mx[k] = std_max(bb.mx[k], cen[3 * i + k]);
+                }
+            float len[3] = {bb.mx[0] - bb.mn[0], bb.mx[1] - bb.mn[1], bb.mx[2] - bb.mn[2]};
+            bool any = false;
+            for (int axis = 0; axis < 3; axis++) {
+                // Reference UB guard: a zero extent gives kl = inf and NaN bins.
+                if (!(len[axis] > 0.0f)) continue;
+                any = true;
+                float kl = (float)8 * (1.0f - 0.001f) / len[axis], ko = bb.mn[axis];
+                Box bins[8];
+                int cnt[8] = {0};
+                for (int i = 0; i < 8; i++) bins[i] = empty_box();
+                for (int i = 0; i < n; i++) {
+                    int id = trunc_x86(kl * (cen[3 * i + axis] - ko));
+                    if (id < 0 || id > 7) { fail("bin id out of range"); return; }
+                    bins[id] = merge(bins[id], pre[i]);
+                    cnt[id]++;
+                }
+                float la[8], ra[8];
+                Box acc = empty_box();
+                for (int i = 0; i < 7; i++) { acc = merge(acc, bins[i]); la[i] = area(acc); }
+                acc = empty_box();
+                int rnum = 0;
+                for (int i = 7; i > 0; i--) {
+                    rnum += cnt[i];
+                    acc = merge(acc, bins[i]);
+                    ra[i] = area(acc);
+                    float c = sah(n - rnum, la[i - 1], rnum, ra[i]);
+                    if (c < best) { best = c; binPart = i; bestAxis = (unsigned)axis; }
+                }
+            }
+            if (!any) { partPt = (unsigned)(n / 2 - 1); return; }
+            float kl = (float)8 * (1.0f - 0.001f) / len[bestAxis], ko = bb.mn[bestAxis];
+            int* ids = bin_ids_.data();
+            for (int i = 0; i < n; i++) ids[i] = trunc_x86(kl * (cen[3 * i + bestAxis] - ko));
+            // Loose in-place partition, src/BVH.cpp:769-792 (ids are NOT swapped).
+            int rev = n - 1;
+            for (int i = 0; i < n; i++) {
+                if (ids[i] < binPart) continue;
+                while (rev >= 0 && ids[rev] >= binPart) rev--;
+                if (rev <= i) { partPt = (unsigned)(i - 1); return; }
+                std::swap(pre[i], pre[rev]);
+                for (int k = 0; k < 3; k++) std::swap(cen[3 * i + k], cen[3 * rev + k]);
+                std::swap(objs[i], objs[rev]);
+                rev--;
+            }
+            return;
+        }
+        // Small nodes: full sweep per axis, src/BVH.cpp:794-899.
+        float la[128], ra[128];
+        for (int axis = 0; axis < 3; axis++) {
+            sort_by_axis(start, n, axis);
+            Box acc = empty_box();
+            la[0] = INFINITY;
+            for (int i = 1; i < n; i++) { acc = merge(acc, tri_box_[objs[i]]); la[i] = area(acc); }
+            acc = empty_box();
+            ra[n - 1] = INFINITY;
+            for (int i = n - 2; i >= 0; i--) {
+                acc = merge(acc, tri_box_[objs[i]]);
+                ra[i] = area(acc);
+                float c = sah(i + 1, la[i], n - i - 1, ra[i]);
+                if (c < best) { best = c; partPt = (unsigned)i; bestAxis = (unsigned)axis; }
+            }
+        }
+        if (bestAxis < 2) sort_by_axis(start, n, (int)bestAxis);
+    }
+
+    // QBVH_Node::build, src/BVH.cpp:100-389 -- preorder node numbering, leaf
+    // packets numbered in creation order (nodeNum).
+    int32_t new_node() {
+        QNode q{};
+        for (int k = 0; k < 4; k++) q.child[k] = kEmptySlot;
+        s_.nodes.push_back(q);
+        return (int32_t)s_.nodes.size() - 1;
+    }
+    void set_box(int32_t qi, int slot, int32_t b) {
+        const Box& x = bn_[b].box;
+        float* box = s_.nodes[qi].box;
+        box[0 + slot] = x.mn[0]; box[4 + slot] = x.mn[1]; box[8 + slot] = x.mn[2];
+        box[12 + slot] = x.mx[0]; box[16 + slot] = x.mx[1]; box[20 + slot] = x.mx[2];
+    }
+    int32_t make_leaf(int32_t b) {  // buildTriBundle, src/BVH.cpp:64-98
+        QLeaf L{};
+        for (int i = 0; i < 4; i++) L.prim[i] = -1;
+        for (int i = 0; i < bn_[b].count; i++) {
+            int o = objs_[bn_[b].start + i];
+            const Mesh& m = s_.meshes[s_.obj_mesh[o]];
+            const uint32_t* f = &m.vidx[3 * (size_t)s_.obj_tri[o]];
+            v3 A = m.verts[f[0]], B = m.verts[f[1]], C = m.verts[f[2]];
+            L.t[0 + i] = A.x; L.t[4 + i] = A.y; L.t[8 + i] = A.z;
+            L.t[12 + i] = B.x - A.x; L.t[16 + i] = B.y - A.y; L.t[20 + i] = B.z - A.z;
+            L.t[24 + i] = C.x - A.x; L.t[28 + i] = C.y - A.y; L.t[32 + i] = C.z - A.z;
+            L.prim[i] = o;
+        }
+        s_.leaves.push_back(L);
+        return ~(int32_t)(s_.leaves.size() - 1);
+    }
+    // slot <- binary node b: leaf packet now, or a new 4-wide node built recursively
+    void fill(int32_t qi, int slot, int32_t b, int depth) {
+        if (bn_[b].leaf) {
+            int32_t c = make_leaf(b);
+            s_.nodes[qi].child[slot] = c;
+        } else {
+            int32_t c = new_node();
+            s_.nodes[qi].child[slot] = c;
+            qbuild(c, b, depth + 1);
+        }
+    }
+    void qbuild(int32_t qi, int32_t b, int depth) {
+        q_depth = std::max(q_depth, depth);
+        const BNode& n = bn_[b];
+        if (n.leaf) {  // only the root can be a leaf
+            set_box(qi, 0, b);
+            fill(qi, 0, b, depth);
+            return;
+        }
+        const int32_t c0 = n.left, c1 = n.left + 1;
+        const bool l0 = bn_[c0].leaf, l1 = bn_[c1].leaf;
+        if (l0 && l1) {
+            set_box(qi, 0, c0);
+            set_box(qi, 1, c1);
+            fill(qi, 0, c0, depth);
+            fill(qi, 1, c1, depth);
+        } else if (l0) {  // leaf, then child 1's two children in slots 1, 2
+            const int32_t g0 = bn_[c1].left, g1 = g0 + 1;
+            set_box(qi, 0, c0); set_box(qi, 1, g0); set_box(qi, 2, g1);
+            fill(qi, 0, c0, depth);
+            fill(qi, 1, g0, depth);
+            fill(qi, 2, g1, depth);
+        } else if (l1) {  // child 0's two children in slots 0, 1, leaf in slot 2 (leaf first)
+            const int32_t g0 = bn_[c0].left, g1 = g0 + 1;
+            set_box(qi, 0, g0); set_box(qi, 1, g1); set_box(qi, 2, c1);
+            fill(qi, 2, c1, depth);
+            fill(qi, 0, g0, depth);
+            fill(qi, 1, g1, depth);
+        } else {
+            const int32_t g[4] = {bn_[c0].left, bn_[c0].left + 1, bn_[c1].left, bn_[c1].left + 1};
+            for (int k = 0; k < 4; k++) set_box(qi, k, g[k]);
+            for (int k = 0; k < 4; k++) fill(qi, k, g[k], depth);
+        }
+    }
+    void collapse() {
+        s_.nodes.clear();
+        s_.leaves.clear();
+        s_.nodes.reserve(bn_.size() / 4 + 4);
+        s_.leaves.reserve((size_t)bin_leaves);
+        int32_t root = new_node();
+        qbuild(root, 0, 1);
+    }
+
+    void fail(const char* m) {
+        if (!fail_) fail_msg_ = m;
+        fail_ = true;
+    }
+
+    Scene& s_;
+    std::vector<Box> tri_box_, pre_;
+    std::vector<float> cen_obj_, cen_;
+    std::vector<int> objs_, bin_ids_;
+    std::vector<BNode> bn_;
+    int depth_ = 0;
+    bool fail_ = false;
+    std::string fail_msg_;
+
+   public:
+    int32_t bin_nodes() const { return (int32_t)bn_.size(); }
+};
+
+}  // namespace
+
+// Scene::preCalc -> BVH::build, src/Scene.cpp:62-79 + src/BVH.cpp:457-575.
+int build_qbvh(Scene& s, std::string& err) {
+    auto t0 = std::chrono::steady_clock::now();
+    s.obj_mesh.clear();
+    s.obj_tri.clear();
+    for (size_t m = 0; m < s.meshes.size(); m++)
+        for (int32_t t = 0; t < s.meshes[m].nt(); t++) {
+            s.obj_mesh.push_back((int32_t)m);
+            s.obj_tri.push_back(t);
+        }
+    if (s.obj_mesh.empty()) {
+        err = "scene has no triangles";
+        return MRT_ERR_BUILD;
+    }
+    Builder b(s);
+    int rc = b.run(err);
+    if (rc != MRT_OK) return rc;
+    auto t1 = std::chrono::steady_clock::now();
+    s.info.nodes = (int32_t)s.nodes.size();
+    s.info.leaves = (int32_t)s.leaves.size();
+    s.info.prims = (int32_t)s.obj_mesh.size();
+    s.info.bin_nodes = b.bin_nodes();
+    s.info.bin_leaves = b.bin_leaves;
+    s.info.max_depth = b.q_depth;
+    s.info.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    s.built = true;
+    s.dev_dirty = true;
+    return MRT_OK;
+}
+
+}  // namespace mrt

@@ -1,0 +1,943 @@
+// mrt_device.hip -- kernels + C-ABI of libmrt (MI355X / gfx950).
+//
+// Render kernel: persistent workgroups of 4 waves; a wave renders one 8x8
+// pixel tile per step (one lane per pixel), so a wave's rays are coherent.
+// Per lane: camera ray (Camera::eyeRayAdaptive, src/Camera.cpp:116-157) ->
+// closest-hit traversal -> Lambert/Blinn shading (src/Lambert.cpp:19-53,
+// src/Blinn.cpp:91-237) with PointLight / RectangleLight shadow rays traced
+// any-hit (same occlusion boolean as the reference's closest-hit shadow rays)
+// -> float RGB (+ Image::Map 8-bit).  The rcp/rsqrt tables (8 KB) and the
+// traversal stacks live in LDS.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "mrt_kernels.h"
+#include "mrt_scene.h"
+
+namespace mrt {
+
+static thread_local std::string g_err;
+void set_error(const std::string& m) { g_err = m; }
+
+#define HIP_OK(expr)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));               \
+            return MRT_ERR_HIP;                                                         \
+        }                                                                               \
+    } while (0)
+
+enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLOW = 4, CTR_NODES_P = 5, CTR_LEAVES_P = 6, CTR_HITS = 7, CTR_N = 8 };
+
+struct RenderParams {
+    const QNode* nodes;
+    const DLeaf* leaves;
+    const PrimShade* prims;
+    const float4* verts;
+    const float4* normals;
+    const DevMaterial* mats;
+    const DevLight* lights;
+    const uint16_t* tables;  // rcp[2048] | rsqrt[2048]
+    const uint8_t* gamma;
+    int32_t* gstack;
+    uint32_t gstride;        // total threads in the launch
+    unsigned long long* ctr;
+    CamParams cam;
+    float bg[3];
+    int32_t n_lights, num_paths;
+    uint32_t seed;
+    // work: 8x8 tiles
+    int32_t tiles_x, n_tiles;    // frame mode: tiles_x = ceil(W/8)
+    const int32_t* buckets;      // bucket mode: bucket ids (row-major bucket grid)
+    int32_t buckets_x;           // ceil(W/32)
+    int32_t mode;                // 0 frame, 1 buckets
+    float* out_rgb;              // frame: W*H*3; buckets: n_buckets*1024*3
+    uint8_t* out_rgb8;           // same slots as out_rgb (nullable)
+    float4* hits;                // per slot: t, a, b, prim bits (kernel 1 -> kernel 2)
+    float4* dirs;                // per slot: primary direction
+};
+
+struct Shader {
+    const RenderParams& P;
+    const Trav& T;
+    const uint16_t* rcpT;
+    const uint16_t* rsqT;
+    TravStats& st;
+    uint32_t pixel, dim;
+    uint32_t shadow_rays;
+
+    __device__ float next_rand() { return rng(pixel, 0, dim++, P.seed); }
+
+    template <bool COUNT>
+    __device__ bool occluded(v3 from, v3 L, float tMax) {
+        DRay r = make_ray(from, L);
+        DHit h{tMax, 0.f, 0.f, -1};
+        shadow_rays++;
+        return traverse<true, COUNT>(T, r, 0.001f, h, st);
+    }
+
+    // PointLight::sampleLight, src/PointLight.cpp:8-81
+    template <bool COUNT>
+    __device__ float point_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec) {
+        v3 L = sub(mk(l.pos[0], l.pos[1], l.pos[2]), from);
+        float nDotL = dot(normal, L);
+        if (!(nDotL > 0.0f)) { outSpec = 0.f; return 0.0f; }
+        float falloff = dot(L, L);
+        float distanceRecip = rsqrt_nr(falloff, rsqT);
+        falloff = rcp_nr(falloff, rcpT);
+        float distance = rcp_nr(distanceRecip, rcpT);
+        L = scale(L, distanceRecip);
+        nDotL *= distanceRecip;
+        float attenuate = 1.0f;
+        if (l.cast_shadows && occluded<COUNT>(from, L, distance)) attenuate = 0.0f;
+        attenuate *= nDotL;
+        outSpec = std_max(0.f, dot(rVec, L)) * attenuate;
+        return ((l.power * falloff) * (0.25f / 3.1415926f)) * attenuate;
+    }
+
+    // RectangleLight::sampleLight, src/RectangleLight.cpp:42-136 (fast shadows)
+    template <bool COUNT>
+    __device__ v3 rect_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec) {
+        v3 v1 = mk(l.v1[0], l.v1[1], l.v1[2]), v2 = mk(l.v2[0], l.v2[1], l.v2[2]), w3 = mk(l.v3[0], l.v3[1], l.v3[2]);
+        v3 acc = mk(0, 0, 0);
+        float tmpSpec = 0.f, recip = 1.0f, falloff = 1.0f;
+        int done = 0;
+        bool cut = false;
+        do {
+            float e1 = next_rand();
+            float e2 = next_rand();
+            e2 = ((double)e2 > 0.99) ? (float)0.99 : e2;
+            v3 rd = sub(add(add(v1, scale(sub(v2, v1), e1)), scale(sub(w3, v1), e2)), from);
+            float nDotL = dot(normal, rd);
+            float att = 1.0f;
+            if (nDotL > 0.001f) {
+                falloff = dot(rd, rd);
+                float dr = rsqrt_nr(falloff, rsqT);
+                falloff = rcp_nr(falloff, rcpT);
+                float dist = rcp_nr(dr, rcpT);
+                rd = scale(rd, dr);
+                if (l.cast_shadows && occluded<COUNT>(from, rd, dist - 0.001f)) att = 0.0f;
+            } else {
+                att = 0.0f;
+            }
+            float E = (l.power * falloff) * (0.25f / 3.1415926f);
+            done++;
+            recip = 1.0f / (float)done;
+            float Es = E * recip;
+            cut = ((Es + Es + Es) * 0.333333f) < l.noise;
+            float Ea = E * att;
+            acc = add(acc, mk(Ea, Ea, Ea));
+            tmpSpec += std_max(0.f, dot(rVec, rd)) * att;
+        } while (done < l.samples && !cut);
+        outSpec = tmpSpec * recip;
+        return scale(acc, recip);
+    }
+
+    template <bool COUNT>
+    __device__ v3 sample_light(int li, v3 from, v3 normal, v3 rVec, float& spec) {
+        const DevLight& l = P.lights[li];
+        if (l.type == MRT_POINT_LIGHT) {
+            float e = point_light<COUNT>(l, from, normal, rVec, spec);
+            return mk(e, e, e);
+        }
+        return rect_light<COUNT>(l, from, normal, rVec, spec);
+    }
+
+    // HitInfo::getAllInfos (normals), src/Ray.cpp:5-49
+    __device__ void normals(const DHit& h, v3& N, v3& geoN, uint32_t& mat) {
+        PrimShade ps = P.prims[h.prim];
+        float4 A = P.verts[ps.v[0]], B = P.verts[ps.v[1]], C = P.verts[ps.v[2]];
+        geoN = normalized(cross(mk(B.x - A.x, B.y - A.y, B.z - A.z), mk(C.x - A.x, C.y - A.y, C.z - A.z)), rsqT);
+        float c = 1.0f - h.a - h.b;
+        float4 n0 = P.normals[ps.n[0]], n1 = P.normals[ps.n[1]], n2 = P.normals[ps.n[2]];
+        v3 s = add(add(scale(mk(n0.x, n0.y, n0.z), c), scale(mk(n1.x, n1.y, n1.z), h.a)), scale(mk(n2.x, n2.y, n2.z), h.b));
+        N = normalized(s, rsqT);
+        mat = ps.mat;
+    }
+
+    // Scene::sampleScene hit branch (src/Scene.cpp:224-233)
+    template <bool COUNT>
+    __device__ v3 shade(const DRay& r, const DHit& h) {
+        v3 N, geoN;
+        uint32_t mi;
+        normals(h, N, geoN, mi);
+        const DevMaterial& M = P.mats[mi];
+        v3 P_ = mk(r.o[0] + h.t * r.d[0], r.o[1] + h.t * r.d[1], r.o[2] + h.t * r.d[2]);  // Ray::getPoint
+        v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+        v3 result = mk(0, 0, 0);
+        for (int path = 0; path < P.num_paths; path++) {
+            v3 sh;
+            if (M.type == MRT_LAMBERT) {  // Lambert::shade
+                v3 L = mk(0, 0, 0);
+                for (int i = 0; i < P.n_lights; i++) {
+                    float discard;
+                    v3 E = sample_light<COUNT>(i, P_, N, mk(0, 0, 0), discard);
+                    L = add(L, mul(E, kd));
+                }
+                sh = add(L, ka);
+            } else {  // Blinn::shade, direct branch
+                v3 rayD = mk(r.d[0], r.d[1], r.d[2]);
+                v3 viewDir = neg(rayD);
+                float vDotN = dot(viewDir, N), vDotGeoN = dot(viewDir, geoN);
+                bool same = (vDotN * vDotGeoN) >= 0.0f;
+                v3 n = same ? N : geoN;
+                vDotN = same ? vDotN : vDotGeoN;
+                if (vDotN < 0.0f) { vDotN = -vDotN; n = neg(n); }
+                v3 rVec = add(rayD, scale(n, 2.0f * vDotN));
+                (void)next_rand();  // Russian-roulette draw (src/Blinn.cpp:195); weight 1
+                v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
+                v3 Ld = mk(0, 0, 0), Ls = mk(0, 0, 0);
+                for (int i = 0; i < P.n_lights; i++) {
+                    float spec = 0.f;
+                    v3 E = sample_light<COUNT>(i, P_, n, rVec, spec);
+                    float pw = (M.spec_exp == 1.0f) ? spec : powf(spec, M.spec_exp);
+                    Ls = add(Ls, scale(scale(mul(E, ks), M.spec_amt), pw));
+                    Ld = add(Ld, mul(E, kd));
+                }
+                Ld = add(Ld, ka);
+                v3 z = mk(0, 0, 0);
+                sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), z);
+            }
+            result = add(result, sh);
+        }
+        return scale(result, 1.0f / (float)P.num_paths);
+    }
+};
+
+__device__ __forceinline__ uint8_t map8(const uint8_t* lut, float v) { return lut[map_index(v)]; }
+
+// work item (8x8 tile) + lane -> pixel (x, y) and output slot
+__device__ __forceinline__ bool item_pixel(const RenderParams& P, int item, int lane, int& x, int& y, size_t& slot) {
+    if (P.mode == 0) {
+        int tx = item % P.tiles_x, ty = item / P.tiles_x;
+        x = tx * 8 + (lane & 7);
+        y = ty * 8 + (lane >> 3);
+        slot = (size_t)y * P.cam.W + x;
+    } else {
+        int bslot = item >> 4, sub = item & 15;
+        int b = P.buckets[bslot];
+        int bx = b % P.buckets_x, by = b / P.buckets_x;
+        int lx = (sub & 3) * 8 + (lane & 7), ly = (sub >> 2) * 8 + (lane >> 3);
+        x = bx * 32 + lx;
+        y = by * 32 + ly;
+        slot = (size_t)bslot * 1024 + ly * 32 + lx;
+    }
+    return x < P.cam.W && y < P.cam.H;
+}
+
+__device__ __forceinline__ void load_tables(const uint16_t* g, uint16_t* s, int words32) {
+    for (int i = threadIdx.x; i < words32; i += kWG) reinterpret_cast<uint32_t*>(s)[i] = reinterpret_cast<const uint32_t*>(g)[i];
+    __syncthreads();
+}
+
+template <bool COUNT, bool PRIMARY = false>
+__device__ __forceinline__ void flush_stats(const RenderParams& P, const TravStats& st, uint32_t shadow, int lane) {
+    // shadow rays (shade kernel) or primary hits (primary kernel), always counted
+    unsigned long long sh = shadow;
+    for (int off = 32; off > 0; off >>= 1) sh += __shfl_down(sh, off);
+    if (lane == 0 && sh) atomicAdd(&P.ctr[PRIMARY ? CTR_HITS : CTR_SHADOW], sh);
+    if (COUNT) {
+        unsigned long long nv = st.nodes, lv = st.leaves;
+        int msp = st.max_sp;
+        for (int off = 32; off > 0; off >>= 1) {
+            nv += __shfl_down(nv, off);
+            lv += __shfl_down(lv, off);
+            msp = max(msp, __shfl_down(msp, off));
+        }
+        if (lane == 0) {
+            atomicAdd(&P.ctr[CTR_NODES], nv);
+            atomicAdd(&P.ctr[CTR_LEAVES], lv);
+            if (PRIMARY) {
+                atomicAdd(&P.ctr[CTR_NODES_P], nv);
+                atomicAdd(&P.ctr[CTR_LEAVES_P], lv);
+            }
+            atomicMax(&P.ctr[CTR_MAXSP], (unsigned long long)msp);
+        }
+    }
+    if (st.overflow) atomicOr(&P.ctr[CTR_OVERFLOW], 1ull);
+}
+
+// Kernel 1: Camera::eyeRayAdaptive + closest-hit BVH::intersect per pixel.
+// Writes the HitInfo record (t, a, b, prim) to P.hits[slot].
+template <bool COUNT>
+__global__ void __launch_bounds__(kWG) primary_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[kTableWords];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    load_tables(P.tables, s_tab, kTableWords / 2);
+    const uint16_t* rcpT = s_tab;
+    const uint16_t* rsqT = s_tab + 2048;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    Trav T{P.nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    TravStats st;
+    uint32_t nhits = 0;
+    const CamParams& cam = P.cam;
+    const v3 U = mk(cam.u[0], cam.u[1], cam.u[2]), Vv = mk(cam.v[0], cam.v[1], cam.v[2]),
+             W = mk(cam.w[0], cam.w[1], cam.w[2]), eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
+    for (int item = blockIdx.x * 4 + wave; item < P.n_tiles; item += gridDim.x * 4) {
+        int x, y;
+        size_t slot;
+        if (!item_pixel(P, item, lane, x, y, slot)) continue;
+        const uint32_t pixel = (uint32_t)(y * cam.W + x);
+        // eyeRayAdaptive(x, y, .5, .5, .5, .5): two jitter draws + one time draw (dims 0..2)
+        float ur = rng(pixel, 0, 0, P.seed), vr = rng(pixel, 0, 1, P.seed);
+        float xo = (0.5f - 0.5f) * ur + 0.5f, yo = (0.5f - 0.5f) * vr + 0.5f;
+        float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
+        float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
+        v3 dir = normalized(sub(add(scale(U, Up), scale(Vv, Vp)), W), rsqT);
+        DRay r = make_ray(eye, dir);
+        DHit h{1e12f, 0.f, 0.f, -1};
+        if (!traverse<false, COUNT>(T, r, 0.001f, h, st)) h.prim = -1;
+        else nhits++;
+        P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(h.prim));
+        P.dirs[slot] = make_float4(dir.x, dir.y, dir.z, 0.f);
+    }
+    flush_stats<COUNT, true>(P, st, nhits, lane);
+}
+
+// Kernel 2: Scene::sampleScene shading of the primary hit with shadow rays.
+template <bool COUNT>
+__global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[kTableWords];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    load_tables(P.tables, s_tab, kTableWords / 2);
+    const uint16_t* rcpT = s_tab;
+    const uint16_t* rsqT = s_tab + 2048;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    Trav T{P.nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    TravStats st;
+    uint32_t shadow_total = 0;
+    const CamParams& cam = P.cam;
+    const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
+    for (int item = blockIdx.x * 4 + wave; item < P.n_tiles; item += gridDim.x * 4) {
+        int x, y;
+        size_t slot;
+        if (!item_pixel(P, item, lane, x, y, slot)) continue;
+        float4 hv = P.hits[slot];
+        DHit h{hv.x, hv.y, hv.z, __float_as_int(hv.w)};
+        v3 col;
+        if (h.prim >= 0) {
+            float4 dv = P.dirs[slot];
+            DRay r = make_ray(eye, mk(dv.x, dv.y, dv.z));
+            Shader S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u};
+            col = S.shade<COUNT>(r, h);
+            shadow_total += S.shadow_rays;
+        } else {
+            col = mk(P.bg[0], P.bg[1], P.bg[2]);
+        }
+        float* o = P.out_rgb + 3 * slot;
+        o[0] = col.x; o[1] = col.y; o[2] = col.z;
+        if (P.out_rgb8) {
+            uint8_t* o8 = P.out_rgb8 + 3 * slot;
+            o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
+        }
+    }
+    flush_stats<COUNT>(P, st, shadow_total, lane);
+}
+
+// Batched Scene::trace: one lane per query ray.
+template <bool ANY>
+__global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DLeaf* leaves, const uint16_t* tables,
+                                                    int32_t* gstack, uint32_t gstride, const float* o, const float* d,
+                                                    const float* tmin, const float* tmax, size_t n, mrt_hit* out,
+                                                    unsigned long long* ctr) {
+    __shared__ uint16_t s_tab[2048];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 1024; i += kWG) reinterpret_cast<uint32_t*>(s_tab)[i] = reinterpret_cast<const uint32_t*>(tables)[i];
+    __syncthreads();
+    const uint32_t gtid = blockIdx.x * kWG + tid;
+    Trav T{nodes, leaves, s_tab, s_stack + tid, gstack + gtid, gstride};
+    TravStats st;
+    for (size_t i = (size_t)blockIdx.x * kWG + tid; i < n; i += (size_t)gridDim.x * kWG) {
+        DRay r = make_ray(mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]));
+        DHit h{tmax[i], 0.f, 0.f, -1};
+        bool hit = traverse<ANY, false>(T, r, tmin[i], h, st);
+        mrt_hit res;
+        res.t = h.t; res.a = h.a; res.b = h.b; res.prim = hit ? (ANY ? 0 : h.prim) : -1;
+        if (ANY && hit) res.prim = 1;  // any-hit: occluded flag only
+        out[i] = res;
+    }
+    if (st.overflow) atomicOr(&ctr[CTR_OVERFLOW], 1ull);
+}
+
+__global__ void unpack_kernel(const int32_t* buckets, int32_t n_buckets, const float* tiles, int32_t W, int32_t H,
+                              int32_t buckets_x, float* frame, uint8_t* frame8, const uint8_t* gamma) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)n_buckets * 1024) return;
+    int bslot = (int)(i >> 10), p = (int)(i & 1023);
+    int b = buckets[bslot];
+    int x = (b % buckets_x) * 32 + (p & 31), y = (b / buckets_x) * 32 + (p >> 5);
+    if (x >= W || y >= H) return;
+    size_t q = (size_t)y * W + x;
+    float r = tiles[3 * i], g = tiles[3 * i + 1], bl = tiles[3 * i + 2];
+    frame[3 * q] = r; frame[3 * q + 1] = g; frame[3 * q + 2] = bl;
+    if (frame8) { frame8[3 * q] = map8(gamma, r); frame8[3 * q + 1] = map8(gamma, g); frame8[3 * q + 2] = map8(gamma, bl); }
+}
+
+// ------------------------------------------------------------------ device state
+struct DeviceState {
+    int device = -1;
+    QNode* nodes = nullptr;
+    DLeaf* leaves = nullptr;
+    PrimShade* prims = nullptr;
+    float4* verts = nullptr;
+    float4* normals = nullptr;
+    DevMaterial* mats = nullptr;
+    DevLight* lights = nullptr;
+    uint16_t* tables = nullptr;
+    uint8_t* gamma = nullptr;
+    int32_t* gstack = nullptr;
+    uint32_t gthreads = 0;
+    int grid = 0;
+    unsigned long long* ctr = nullptr;
+    // scratch for the synchronous API
+    float* d_rgb = nullptr;
+    uint8_t* d_rgb8 = nullptr;
+    size_t frame_px = 0;
+    // kernel 1 -> kernel 2 hand-off (per output slot)
+    float4* hitbuf = nullptr;
+    float4* dirbuf = nullptr;
+    size_t hit_slots = 0;
+    int grid_primary = 0, grid_shade = 0;
+    bool last_was_render = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
+    size_t bytes = 0;
+};
+
+static void free_device(DeviceState* d) {
+    if (!d) return;
+    if (d->device >= 0) (void)hipSetDevice(d->device);
+    void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->tables,
+                    d->gamma, d->gstack, d->ctr, d->d_rgb, d->d_rgb8, d->hitbuf, d->dirbuf};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (d->ev0) (void)hipEventDestroy(d->ev0);
+    if (d->ev1) (void)hipEventDestroy(d->ev1);
+    if (d->evm) (void)hipEventDestroy(d->evm);
+    delete d;
+}
+
+template <typename T>
+static int upload(T*& dst, const void* src, size_t bytes, size_t& total) {
+    HIP_OK(hipMalloc((void**)&dst, bytes ? bytes : 16));
+    if (bytes) HIP_OK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    total += bytes;
+    return MRT_OK;
+}
+
+static int ensure_device(Scene& s, int device) {
+    if (!s.built) { set_error("scene not built"); return MRT_ERR_NOT_BUILT; }
+    if (s.dev && !s.dev_dirty && s.dev->device == device) return MRT_OK;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) { set_error("no HIP device"); return MRT_ERR_NO_DEVICE; }
+    if (device < 0 || device >= n) { set_error("bad device ordinal"); return MRT_ERR_INVALID; }
+    if (s.lights.size() > (size_t)kMaxLights) { set_error("too many lights"); return MRT_ERR_INVALID; }
+    free_device(s.dev);
+    s.dev = new DeviceState();
+    DeviceState& d = *s.dev;
+    d.device = device;
+    HIP_OK(hipSetDevice(device));
+    // shading arrays: concatenate meshes
+    std::vector<float4> V, N;
+    std::vector<uint32_t> vbase(s.meshes.size()), nbase(s.meshes.size());
+    for (size_t m = 0; m < s.meshes.size(); m++) {
+        vbase[m] = (uint32_t)V.size();
+        nbase[m] = (uint32_t)N.size();
+        for (auto& p : s.meshes[m].verts) V.push_back(make_float4(p.x, p.y, p.z, 1.f));
+        for (auto& p : s.meshes[m].normals) N.push_back(make_float4(p.x, p.y, p.z, 0.f));
+    }
+    std::vector<PrimShade> PS(s.obj_mesh.size());
+    for (size_t i = 0; i < PS.size(); i++) {
+        const Mesh& m = s.meshes[s.obj_mesh[i]];
+        size_t t = (size_t)s.obj_tri[i];
+        for (int k = 0; k < 3; k++) {
+            PS[i].v[k] = vbase[s.obj_mesh[i]] + m.vidx[3 * t + k];
+            PS[i].n[k] = nbase[s.obj_mesh[i]] + m.nidx[3 * t + k];
+        }
+        PS[i].mat = (uint32_t)m.material;
+        PS[i].pad = 0;
+    }
+    std::vector<uint16_t> tab(4096);
+    memcpy(tab.data(), host_rcp_table(), 4096);
+    memcpy(tab.data() + 2048, host_rsqrt_table(), 4096);
+    size_t total = 0;
+    int rc;
+    if ((rc = upload(d.nodes, s.nodes.data(), s.nodes.size() * sizeof(QNode), total))) return rc;
+    std::vector<DLeaf> DL(s.leaves.size());
+    for (size_t i = 0; i < DL.size(); i++) {
+        for (int k = 0; k < 4; k++) {
+            for (int c = 0; c < 9; c++) DL[i].tri[k][c] = s.leaves[i].t[4 * c + k];
+            DL[i].prim[k] = s.leaves[i].prim[k];
+        }
+    }
+    if ((rc = upload(d.leaves, DL.data(), DL.size() * sizeof(DLeaf), total))) return rc;
+    if ((rc = upload(d.prims, PS.data(), PS.size() * sizeof(PrimShade), total))) return rc;
+    if ((rc = upload(d.verts, V.data(), V.size() * sizeof(float4), total))) return rc;
+    if ((rc = upload(d.normals, N.data(), N.size() * sizeof(float4), total))) return rc;
+    if ((rc = upload(d.mats, s.materials.data(), s.materials.size() * sizeof(DevMaterial), total))) return rc;
+    if ((rc = upload(d.lights, s.lights.data(), s.lights.size() * sizeof(DevLight), total))) return rc;
+    if ((rc = upload(d.tables, tab.data(), tab.size() * sizeof(uint16_t), total))) return rc;
+    if ((rc = upload(d.gamma, host_gamma_lut(), 32769, total))) return rc;
+    d.bytes = total;
+    // persistent grid: resident workgroups on every CU
+    hipDeviceProp_t prop;
+    HIP_OK(hipGetDeviceProperties(&prop, device));
+    int per_cu1 = 0, per_cu2 = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu1, primary_kernel<false>, kWG, 0));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, shade_kernel<false>, kWG, 0));
+    d.grid_primary = prop.multiProcessorCount * std::max(per_cu1, 1);
+    d.grid_shade = prop.multiProcessorCount * std::max(per_cu2, 1);
+    d.grid = std::max(d.grid_primary, d.grid_shade);
+    d.gthreads = (uint32_t)d.grid * kWG;
+    HIP_OK(hipMalloc((void**)&d.gstack, (size_t)kGlobalStack * d.gthreads * sizeof(int32_t)));
+    HIP_OK(hipMalloc((void**)&d.ctr, CTR_N * sizeof(unsigned long long)));
+    HIP_OK(hipEventCreate(&d.ev0));
+    HIP_OK(hipEventCreate(&d.ev1));
+    HIP_OK(hipEventCreate(&d.evm));
+    s.info.device_bytes = total;
+    s.dev_dirty = false;
+    return MRT_OK;
+}
+
+static int host_camera(const mrt_camera* c, int W, int H, CamParams& out) {
+    if (!c || W <= 0 || H <= 0) { set_error("bad camera/frame"); return MRT_ERR_INVALID; }
+    const uint16_t* RS = host_rsqrt_table();
+    // Camera::setEye/setLookAt/setUp (src/Camera.h:82-124), eyeRayAdaptive basis
+    v3 eye = mk(c->eye[0], c->eye[1], c->eye[2]);
+    v3 viewDir = normalized(sub(mk(c->look_at[0], c->look_at[1], c->look_at[2]), eye), RS);
+    v3 up = normalized(mk(c->up[0], c->up[1], c->up[2]), RS);
+    v3 w = normalized(neg(viewDir), RS);
+    v3 u = normalized(cross(up, w), RS);
+    v3 v = cross(w, u);
+    float aspect = (float)W / (float)H;
+    const float DegToRad = 3.1415926f / 180.0f, Half = DegToRad / 2.0f;
+    float top = tanf(c->fov_deg * Half);
+    float right = aspect * top;
+    out.eye[0] = eye.x; out.eye[1] = eye.y; out.eye[2] = eye.z;
+    out.u[0] = u.x; out.u[1] = u.y; out.u[2] = u.z;
+    out.v[0] = v.x; out.v[1] = v.y; out.v[2] = v.z;
+    out.w[0] = w.x; out.w[1] = w.y; out.w[2] = w.z;
+    out.top = top; out.right = right; out.bottom = -top; out.left = -right;
+    out.W = W; out.H = H;
+    return MRT_OK;
+}
+
+static void fill_params(const Scene& s, RenderParams& P) {
+    const DeviceState& d = *s.dev;
+    P.nodes = d.nodes; P.leaves = d.leaves; P.prims = d.prims; P.verts = d.verts; P.normals = d.normals;
+    P.mats = d.mats; P.lights = d.lights; P.tables = d.tables; P.gamma = d.gamma;
+    P.gstack = d.gstack; P.gstride = d.gthreads; P.ctr = d.ctr;
+    P.bg[0] = s.bg[0]; P.bg[1] = s.bg[1]; P.bg[2] = s.bg[2];
+    P.n_lights = (int32_t)s.lights.size();
+    P.num_paths = s.num_paths;
+}
+
+static int ensure_slots(DeviceState& d, size_t slots) {
+    if (slots <= d.hit_slots) return MRT_OK;
+    if (d.hitbuf) (void)hipFree(d.hitbuf);
+    if (d.dirbuf) (void)hipFree(d.dirbuf);
+    d.hitbuf = nullptr; d.dirbuf = nullptr; d.hit_slots = 0;
+    HIP_OK(hipMalloc((void**)&d.hitbuf, slots * sizeof(float4)));
+    HIP_OK(hipMalloc((void**)&d.dirbuf, slots * sizeof(float4)));
+    d.hit_slots = slots;
+    return MRT_OK;
+}
+
+// Two launches on `stream`: primary rays -> hit records, then shading with
+// shadow rays.  Events bracket both (kernel_ms covers the whole frame).
+static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hipStream_t stream) {
+    DeviceState& d = *s.dev;
+    int rc = ensure_slots(d, slots);
+    if (rc) return rc;
+    P.hits = d.hitbuf;
+    P.dirs = d.dirbuf;
+    HIP_OK(hipMemsetAsync(d.ctr, 0, CTR_N * sizeof(unsigned long long), stream));
+    int g1 = std::max(1, std::min(d.grid_primary, (P.n_tiles + 3) / 4));
+    int g2 = std::max(1, std::min(d.grid_shade, (P.n_tiles + 3) / 4));
+    HIP_OK(hipEventRecord(d.ev0, stream));
+    if (count) hipLaunchKernelGGL(primary_kernel<true>, dim3(g1), dim3(kWG), 0, stream, P);
+    else hipLaunchKernelGGL(primary_kernel<false>, dim3(g1), dim3(kWG), 0, stream, P);
+    HIP_OK(hipEventRecord(d.evm, stream));
+    if (count) hipLaunchKernelGGL(shade_kernel<true>, dim3(g2), dim3(kWG), 0, stream, P);
+    else hipLaunchKernelGGL(shade_kernel<false>, dim3(g2), dim3(kWG), 0, stream, P);
+    d.last_was_render = true;
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(d.ev1, stream));
+    s.last = mrt_stats{};
+    return MRT_OK;
+}
+
+}  // namespace mrt
+
+using namespace mrt;
+
+// ================================================================== C ABI
+extern "C" {
+
+const char* mrt_last_error(void) { return g_err.c_str(); }
+int mrt_abi_version(void) { return MRT_ABI_VERSION; }
+int mrt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+mrt_scene* mrt_scene_create(void) { return new (std::nothrow) mrt_scene(); }
+void mrt_scene_destroy(mrt_scene* s) {
+    if (!s) return;
+    free_device(s->impl.dev);
+    delete s;
+}
+
+int mrt_scene_add_material(mrt_scene* s, const mrt_material* m) {
+    if (!s || !m || (m->type != MRT_LAMBERT && m->type != MRT_BLINN)) { set_error("bad material"); return MRT_ERR_INVALID; }
+    if (s->impl.materials.size() >= (size_t)kMaxMaterials) { set_error("too many materials"); return MRT_ERR_INVALID; }
+    DevMaterial d;
+    d.type = m->type;
+    memcpy(d.kd, m->kd, 12); memcpy(d.ka, m->ka, 12); memcpy(d.ks, m->ks, 12);
+    d.spec_exp = m->spec_exp; d.spec_amt = m->spec_amt;
+    s->impl.materials.push_back(d);
+    s->impl.dev_dirty = true;
+    return (int)s->impl.materials.size() - 1;
+}
+
+int mrt_scene_add_light(mrt_scene* s, const mrt_light* l) {
+    if (!s || !l || (l->type != MRT_POINT_LIGHT && l->type != MRT_RECT_LIGHT)) { set_error("bad light"); return MRT_ERR_INVALID; }
+    if (s->impl.lights.size() >= (size_t)kMaxLights) { set_error("too many lights"); return MRT_ERR_INVALID; }
+    DevLight d;
+    memset(&d, 0, sizeof d);
+    d.type = l->type;
+    memcpy(d.pos, l->pos, 12); memcpy(d.v1, l->v1, 12); memcpy(d.v2, l->v2, 12); memcpy(d.v3, l->v3, 12);
+    d.samples = l->samples < 1 ? 1 : l->samples;
+    d.noise = l->noise_threshold;
+    d.cast_shadows = l->cast_shadows;
+    d.power = l->power;
+    if (l->type == MRT_RECT_LIGHT) {
+        // RectangleLight::setPower (src/RectangleLight.cpp:14-40)
+        const uint16_t* RS = host_rsqrt_table();
+        v3 v1 = mk(l->v1[0], l->v1[1], l->v1[2]);
+        v3 e0 = sub(mk(l->v2[0], l->v2[1], l->v2[2]), v1), e1 = sub(mk(l->v3[0], l->v3[1], l->v3[2]), v1);
+        float recip = 1.0f, sq;
+        if (fabsf(dot(e0, e1)) < 0.001f) sq = dot(e0, e0) * dot(e1, e1);
+        else { v3 c = cross(e0, e1); sq = dot(c, c); }
+        if (sq > 0.001f) recip = rsqrt_nr(sq, RS);
+        d.power = l->power * recip;
+    }
+    s->impl.lights.push_back(d);
+    s->impl.dev_dirty = true;
+    return (int)s->impl.lights.size() - 1;
+}
+
+int mrt_scene_add_obj(mrt_scene* s, const char* path, const float* ctm16, int material) {
+    if (!s || !path) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    Mesh m;
+    std::string err;
+    int rc = load_obj(path, ctm16, m, err);
+    if (rc != MRT_OK) { set_error(err); return rc; }
+    m.material = material;
+    s->impl.meshes.push_back(std::move(m));
+    s->impl.built = false;
+    return (int)s->impl.meshes.size() - 1;
+}
+
+int mrt_scene_add_mesh(mrt_scene* s, const mrt_mesh* mesh, int material) {
+    if (!s || !mesh || mesh->nv < 0 || mesh->nn < 0 || mesh->nt < 0) { set_error("bad mesh"); return MRT_ERR_INVALID; }
+    Mesh m;
+    m.material = material;
+    for (int i = 0; i < mesh->nv; i++) m.verts.push_back(mk(mesh->verts[3 * i], mesh->verts[3 * i + 1], mesh->verts[3 * i + 2]));
+    for (int i = 0; i < mesh->nn; i++) m.normals.push_back(mk(mesh->normals[3 * i], mesh->normals[3 * i + 1], mesh->normals[3 * i + 2]));
+    m.vidx.assign(mesh->vidx, mesh->vidx + 3 * (size_t)mesh->nt);
+    m.nidx.assign(mesh->nidx, mesh->nidx + 3 * (size_t)mesh->nt);
+    for (size_t i = 0; i < m.vidx.size(); i++)
+        if (m.vidx[i] >= (uint32_t)mesh->nv || m.nidx[i] >= (uint32_t)mesh->nn) { set_error("mesh index out of range"); return MRT_ERR_INVALID; }
+    s->impl.meshes.push_back(std::move(m));
+    s->impl.built = false;
+    return (int)s->impl.meshes.size() - 1;
+}
+
+int mrt_scene_mesh_info(const mrt_scene* s, int mesh, int32_t* nv, int32_t* nn, int32_t* nt) {
+    if (!s || mesh < 0 || mesh >= (int)s->impl.meshes.size()) { set_error("bad mesh id"); return MRT_ERR_INVALID; }
+    const Mesh& m = s->impl.meshes[mesh];
+    *nv = (int32_t)m.verts.size(); *nn = (int32_t)m.normals.size(); *nt = m.nt();
+    return MRT_OK;
+}
+
+int mrt_scene_mesh_export(const mrt_scene* s, int mesh, float* verts, float* normals, uint32_t* vidx, uint32_t* nidx) {
+    if (!s || mesh < 0 || mesh >= (int)s->impl.meshes.size()) { set_error("bad mesh id"); return MRT_ERR_INVALID; }
+    const Mesh& m = s->impl.meshes[mesh];
+    for (size_t i = 0; i < m.verts.size(); i++) { verts[3*i] = m.verts[i].x; verts[3*i+1] = m.verts[i].y; verts[3*i+2] = m.verts[i].z; }
+    for (size_t i = 0; i < m.normals.size(); i++) { normals[3*i] = m.normals[i].x; normals[3*i+1] = m.normals[i].y; normals[3*i+2] = m.normals[i].z; }
+    memcpy(vidx, m.vidx.data(), m.vidx.size() * 4);
+    memcpy(nidx, m.nidx.data(), m.nidx.size() * 4);
+    return MRT_OK;
+}
+
+int mrt_scene_set_background(mrt_scene* s, const float rgb[3]) {
+    if (!s || !rgb) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    memcpy(s->impl.bg, rgb, 12);
+    return MRT_OK;
+}
+
+int mrt_scene_set_num_paths(mrt_scene* s, int num_paths) {
+    if (!s || num_paths < 1) { set_error("bad num_paths"); return MRT_ERR_INVALID; }
+    s->impl.num_paths = num_paths;
+    return MRT_OK;
+}
+
+int mrt_scene_build_bvh(mrt_scene* s) {
+    if (!s) { set_error("null scene"); return MRT_ERR_INVALID; }
+    for (auto& m : s->impl.meshes)
+        if (m.material < 0 || m.material >= (int)s->impl.materials.size()) { set_error("mesh references unknown material"); return MRT_ERR_INVALID; }
+    std::string err;
+    int rc = build_qbvh(s->impl, err);
+    if (rc != MRT_OK) set_error(err);
+    return rc;
+}
+
+int mrt_scene_bvh_info(const mrt_scene* s, mrt_bvh_info* info) {
+    if (!s || !info) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    if (!s->impl.built) { set_error("scene not built"); return MRT_ERR_NOT_BUILT; }
+    *info = s->impl.info;
+    return MRT_OK;
+}
+
+int mrt_scene_bvh_export(const mrt_scene* s, float* node_boxes, int32_t* node_child, float* leaf_tris, int32_t* leaf_prims) {
+    if (!s) { set_error("null scene"); return MRT_ERR_INVALID; }
+    if (!s->impl.built) { set_error("scene not built"); return MRT_ERR_NOT_BUILT; }
+    for (size_t i = 0; i < s->impl.nodes.size(); i++) {
+        memcpy(node_boxes + 24 * i, s->impl.nodes[i].box, 96);
+        memcpy(node_child + 4 * i, s->impl.nodes[i].child, 16);
+    }
+    for (size_t i = 0; i < s->impl.leaves.size(); i++) {
+        memcpy(leaf_tris + 36 * i, s->impl.leaves[i].t, 144);
+        memcpy(leaf_prims + 4 * i, s->impl.leaves[i].prim, 16);
+    }
+    return MRT_OK;
+}
+
+int mrt_scene_bvh_import(mrt_scene* s, int32_t nodes, int32_t leaves, const float* node_boxes, const int32_t* node_child,
+                         const float* leaf_tris, const int32_t* leaf_prims) {
+    if (!s || nodes < 1 || leaves < 0) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    Scene& S = s->impl;
+    if (!S.built) { set_error("build the scene first (prim ids come from it)"); return MRT_ERR_NOT_BUILT; }
+    std::vector<QNode> N((size_t)nodes);
+    std::vector<QLeaf> L((size_t)leaves);
+    for (int i = 0; i < nodes; i++) {
+        memset(&N[i], 0, sizeof(QNode));
+        memcpy(N[i].box, node_boxes + 24 * (size_t)i, 96);
+        memcpy(N[i].child, node_child + 4 * (size_t)i, 16);
+        for (int k = 0; k < 4; k++) {
+            int32_t c = N[i].child[k];
+            if (c == kEmptySlot) continue;
+            if ((c >= 0 && c >= nodes) || (c < 0 && ~c >= leaves)) { set_error("child index out of range"); return MRT_ERR_INVALID; }
+        }
+    }
+    for (int i = 0; i < leaves; i++) {
+        memcpy(L[i].t, leaf_tris + 36 * (size_t)i, 144);
+        memcpy(L[i].prim, leaf_prims + 4 * (size_t)i, 16);
+        for (int k = 0; k < 4; k++)
+            if (L[i].prim[k] >= S.info.prims) { set_error("prim id out of range"); return MRT_ERR_INVALID; }
+    }
+    S.nodes.swap(N);
+    S.leaves.swap(L);
+    S.info.nodes = nodes;
+    S.info.leaves = leaves;
+    S.dev_dirty = true;
+    return MRT_OK;
+}
+
+int mrt_scene_upload(mrt_scene* s, int device) {
+    if (!s) { set_error("null scene"); return MRT_ERR_INVALID; }
+    return ensure_device(s->impl, device);
+}
+
+int mrt_render_frame_async(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts, float* d_rgb,
+                           uint8_t* d_rgb8, void* stream) {
+    if (!s || !cam || !opts || !d_rgb) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    Scene& S = s->impl;
+    int rc = ensure_device(S, opts->device);
+    if (rc) return rc;
+    HIP_OK(hipSetDevice(opts->device));
+    RenderParams P{};
+    fill_params(S, P);
+    if ((rc = host_camera(cam, opts->width, opts->height, P.cam))) return rc;
+    P.seed = opts->seed ? opts->seed : 0x5EEDu;
+    P.mode = 0;
+    P.tiles_x = (opts->width + 7) / 8;
+    P.n_tiles = P.tiles_x * ((opts->height + 7) / 8);
+    P.out_rgb = d_rgb;
+    P.out_rgb8 = d_rgb8;
+    rc = launch_render(S, P, (size_t)opts->width * opts->height, opts->count_visits != 0, (hipStream_t)stream);
+    S.last.primary_rays = (uint64_t)opts->width * opts->height;
+    return rc;
+}
+
+int mrt_render_buckets_async(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts, const int32_t* d_buckets,
+                             int32_t n_buckets, float* d_tiles, void* stream) {
+    if (!s || !cam || !opts || !d_buckets || !d_tiles || n_buckets < 0) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    Scene& S = s->impl;
+    int rc = ensure_device(S, opts->device);
+    if (rc) return rc;
+    HIP_OK(hipSetDevice(opts->device));
+    RenderParams P{};
+    fill_params(S, P);
+    if ((rc = host_camera(cam, opts->width, opts->height, P.cam))) return rc;
+    P.seed = opts->seed ? opts->seed : 0x5EEDu;
+    P.mode = 1;
+    P.buckets = d_buckets;
+    P.buckets_x = (opts->width + 31) / 32;
+    P.n_tiles = n_buckets * 16;
+    P.out_rgb = d_tiles;
+    P.out_rgb8 = nullptr;
+    if (n_buckets == 0) return MRT_OK;
+    rc = launch_render(S, P, (size_t)n_buckets * 1024, opts->count_visits != 0, (hipStream_t)stream);
+    S.last.primary_rays = 0;
+    return rc;
+}
+
+int mrt_unpack_buckets_async(const int32_t* d_buckets, int32_t n_buckets, const float* d_tiles, int32_t width,
+                             int32_t height, float* d_frame, uint8_t* d_frame8, const mrt_scene* s_for_lut, void* stream) {
+    if (!d_buckets || !d_tiles || !d_frame || width <= 0 || height <= 0) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    if (d_frame8 && (!s_for_lut || !s_for_lut->impl.dev)) { set_error("rgb8 needs an uploaded scene for the LUT"); return MRT_ERR_INVALID; }
+    if (n_buckets == 0) return MRT_OK;
+    size_t n = (size_t)n_buckets * 1024;
+    const uint8_t* lut = d_frame8 ? s_for_lut->impl.dev->gamma : nullptr;
+    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_buckets,
+                       n_buckets, d_tiles, width, height, (width + 31) / 32, d_frame, d_frame8, lut);
+    HIP_OK(hipGetLastError());
+    return MRT_OK;
+}
+
+int mrt_render(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts, float* rgb, uint8_t* rgb8, mrt_hit* hits) {
+    if (!s || !cam || !opts || !rgb || opts->width <= 0 || opts->height <= 0) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    Scene& S = s->impl;
+    int rc = ensure_device(S, opts->device);
+    if (rc) return rc;
+    HIP_OK(hipSetDevice(opts->device));
+    DeviceState& d = *S.dev;
+    size_t px = (size_t)opts->width * opts->height;
+    if (px > d.frame_px) {
+        if (d.d_rgb) (void)hipFree(d.d_rgb);
+        if (d.d_rgb8) (void)hipFree(d.d_rgb8);
+        d.d_rgb = nullptr; d.d_rgb8 = nullptr; d.frame_px = 0;
+        HIP_OK(hipMalloc((void**)&d.d_rgb, px * 12));
+        HIP_OK(hipMalloc((void**)&d.d_rgb8, px * 3));
+        d.frame_px = px;
+    }
+    RenderParams P{};
+    fill_params(S, P);
+    if ((rc = host_camera(cam, opts->width, opts->height, P.cam))) return rc;
+    P.seed = opts->seed ? opts->seed : 0x5EEDu;
+    P.mode = 0;
+    P.tiles_x = (opts->width + 7) / 8;
+    P.n_tiles = P.tiles_x * ((opts->height + 7) / 8);
+    P.out_rgb = d.d_rgb;
+    P.out_rgb8 = d.d_rgb8;
+    if ((rc = launch_render(S, P, px, opts->count_visits != 0, nullptr))) return rc;
+    HIP_OK(hipMemcpy(rgb, d.d_rgb, px * 12, hipMemcpyDeviceToHost));
+    if (rgb8) HIP_OK(hipMemcpy(rgb8, d.d_rgb8, px * 3, hipMemcpyDeviceToHost));
+    if (hits) HIP_OK(hipMemcpy(hits, d.hitbuf, px * sizeof(mrt_hit), hipMemcpyDeviceToHost));
+    S.last.primary_rays = px;
+    mrt_stats tmp;
+    if ((rc = mrt_scene_last_stats(s, &tmp))) return rc;
+    return MRT_OK;
+}
+
+int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
+    if (!cs || !out) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    mrt_scene* s = const_cast<mrt_scene*>(cs);
+    Scene& S = s->impl;
+    if (!S.dev) { set_error("nothing rendered"); return MRT_ERR_INVALID; }
+    DeviceState& d = *S.dev;
+    HIP_OK(hipSetDevice(d.device));
+    HIP_OK(hipEventSynchronize(d.ev1));
+    unsigned long long c[CTR_N];
+    HIP_OK(hipMemcpy(c, d.ctr, sizeof c, hipMemcpyDeviceToHost));
+    float ms = 0.f, ms1 = 0.f, ms2 = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
+    if (d.last_was_render) {
+        HIP_OK(hipEventElapsedTime(&ms1, d.ev0, d.evm));
+        HIP_OK(hipEventElapsedTime(&ms2, d.evm, d.ev1));
+    }
+    S.last.primary_ms = ms1;
+    S.last.shade_ms = ms2;
+    S.last.primary_node_visits = c[CTR_NODES_P];
+    S.last.primary_leaf_visits = c[CTR_LEAVES_P];
+    S.last.shadow_rays = c[CTR_SHADOW];
+    S.last.primary_hits = c[CTR_HITS];
+    S.last.node_visits = c[CTR_NODES];
+    S.last.leaf_visits = c[CTR_LEAVES];
+    S.last.max_stack = (int32_t)c[CTR_MAXSP];
+    S.last.kernel_ms = ms;
+    *out = S.last;
+    if (c[CTR_OVERFLOW]) { set_error("traversal stack overflow"); return MRT_ERR_OVERFLOW; }
+    return MRT_OK;
+}
+
+int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const float* d_tmin, const float* d_tmax, size_t n,
+                    int any_hit, mrt_hit* d_out, void* stream) {
+    if (!s || (n && (!d_o || !d_d || !d_tmin || !d_tmax || !d_out))) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    Scene& S = s->impl;
+    int dev = S.dev ? S.dev->device : 0;
+    int rc = ensure_device(S, dev);
+    if (rc) return rc;
+    HIP_OK(hipSetDevice(dev));
+    DeviceState& d = *S.dev;
+    if (n == 0) return MRT_OK;
+    HIP_OK(hipMemsetAsync(d.ctr, 0, CTR_N * sizeof(unsigned long long), (hipStream_t)stream));
+    d.last_was_render = false;
+    int grid = (int)std::min<size_t>((size_t)d.grid, (n + kWG - 1) / kWG);
+    HIP_OK(hipEventRecord(d.ev0, (hipStream_t)stream));
+    if (any_hit)
+        hipLaunchKernelGGL(trace_kernel<true>, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables,
+                           d.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, d.ctr);
+    else
+        hipLaunchKernelGGL(trace_kernel<false>, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables,
+                           d.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, d.ctr);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(d.ev1, (hipStream_t)stream));
+    return MRT_OK;
+}
+
+int mrt_trace(mrt_scene* s, const float* o, const float* d, const float* tmin, const float* tmax, size_t n, int any_hit,
+              mrt_hit* out) {
+    if (!s || (n && (!o || !d || !tmin || !tmax || !out))) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    Scene& S = s->impl;
+    int dev = S.dev ? S.dev->device : 0;
+    int rc = ensure_device(S, dev);
+    if (rc) return rc;
+    if (n == 0) return MRT_OK;
+    HIP_OK(hipSetDevice(dev));
+    float *bo = nullptr, *bd = nullptr, *bmin = nullptr, *bmax = nullptr;
+    mrt_hit* bout = nullptr;
+    HIP_OK(hipMalloc((void**)&bo, n * 12));
+    HIP_OK(hipMalloc((void**)&bd, n * 12));
+    HIP_OK(hipMalloc((void**)&bmin, n * 4));
+    HIP_OK(hipMalloc((void**)&bmax, n * 4));
+    HIP_OK(hipMalloc((void**)&bout, n * sizeof(mrt_hit)));
+    HIP_OK(hipMemcpy(bo, o, n * 12, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(bd, d, n * 12, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(bmin, tmin, n * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(bmax, tmax, n * 4, hipMemcpyHostToDevice));
+    rc = mrt_trace_async(s, bo, bd, bmin, bmax, n, any_hit, bout, nullptr);
+    if (rc == MRT_OK) {
+        HIP_OK(hipMemcpy(out, bout, n * sizeof(mrt_hit), hipMemcpyDeviceToHost));
+        unsigned long long c[CTR_N];
+        HIP_OK(hipMemcpy(c, S.dev->ctr, sizeof c, hipMemcpyDeviceToHost));
+        if (c[CTR_OVERFLOW]) { set_error("traversal stack overflow"); rc = MRT_ERR_OVERFLOW; }
+    }
+    (void)hipFree(bo); (void)hipFree(bd); (void)hipFree(bmin); (void)hipFree(bmax); (void)hipFree(bout);
+    return rc;
+}
+
+float mrt_rcp_nr(float x) { return rcp_nr(x, host_rcp_table()); }
+float mrt_rsqrt_nr(float x) { return rsqrt_nr(x, host_rsqrt_table()); }
+
+}  // extern "C"

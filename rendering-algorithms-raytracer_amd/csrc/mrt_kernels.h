@@ -1,0 +1,185 @@
+// mrt_kernels.h -- device-side hot path (included by mrt_device.hip only).
+//
+// One lane = one pixel (or one query ray).  The traversal reproduces the
+// reference's QBVH stack order exactly (src/BVH.cpp:1128-1178): the node's
+// four boxes are tested once when it is popped (QBVH_Node::intersect,
+// src/BVH.cpp:391-414), leaf slots are intersected immediately in slot order
+// (intersect4, src/BVH.cpp:1298-1459), hit inner slots are pushed in slot order
+// so the highest slot is visited next.  The highest hit child is kept in a
+// register instead of a push+pop.  Stack: per-lane column in LDS (kLdsStack
+// entries, conflict-free [entry][lane] layout) spilling to a per-thread global
+// column beyond that.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/mrt.h"
+#include "mrt_math.h"
+#include "mrt_types.h"
+
+namespace mrt {
+
+static constexpr int kWG = 256;          // threads per workgroup (4 waves)
+static constexpr int kLdsStack = 24;     // stack entries per lane kept in LDS
+static constexpr int kGlobalStack = 72;  // spill entries per thread in HBM
+static constexpr int kTableWords = 4096; // rcp[2048] + rsqrt[2048] (u16)
+
+struct DRay {
+    float o[3], d[3], id[3];
+};
+
+// Ray(threadID, o, d, ...), src/Ray.h:71-101: id = 1/d, +-1e12 for d == 0.
+__device__ __forceinline__ DRay make_ray(v3 o, v3 d) {
+    DRay r;
+    r.o[0] = o.x; r.o[1] = o.y; r.o[2] = o.z;
+    r.d[0] = d.x; r.d[1] = d.y; r.d[2] = d.z;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        float v = 1.0f / r.d[k];
+        if (r.d[k] == 0.f) v = (v < -0.f) ? -1e12f : 1e12f;
+        r.id[k] = v;
+    }
+    return r;
+}
+
+struct DHit {
+    float t, a, b;
+    int32_t prim;
+};
+
+struct Trav {
+    const QNode* __restrict__ nodes;
+    const DLeaf* __restrict__ leaves;
+    const uint16_t* rcpT;     // LDS
+    int32_t* lds;             // this lane's LDS stack column (stride kWG)
+    int32_t* gstk;            // this thread's global spill column (stride gstride)
+    uint32_t gstride;
+};
+
+struct TravStats {
+    uint32_t nodes = 0, leaves = 0;
+    int max_sp = 0;
+    bool overflow = false;
+};
+
+__device__ __forceinline__ bool stk_push(const Trav& c, int& sp, int32_t v) {
+    if (sp < kLdsStack) c.lds[sp * kWG] = v;
+    else if (sp < kLdsStack + kGlobalStack) c.gstk[(size_t)(sp - kLdsStack) * c.gstride] = v;
+    else return false;
+    sp++;
+    return true;
+}
+__device__ __forceinline__ int32_t stk_pop(const Trav& c, int& sp) {
+    --sp;
+    return sp < kLdsStack ? c.lds[sp * kWG] : c.gstk[(size_t)(sp - kLdsStack) * c.gstride];
+}
+
+// intersect4 (src/BVH.cpp:1298-1459) for one 4-triangle packet, one triangle
+// at a time.  The reference tests all four lanes against result.t at packet
+// entry and keeps the lowest accepted t (first lane on ties).  Walking the lanes
+// in order and accepting only t < current best gives the same winner: a lane
+// that loses to an earlier one is never selected by the reference either.
+// Empty lanes (prim -1) are zero triangles, which the reference rejects via
+// det = 0 -> rcp_nr = NaN, so they are skipped.
+template <bool ANY>
+__device__ __forceinline__ bool intersect4(const DLeaf* __restrict__ L, const DRay& r, float tMin, DHit& h,
+                                           const uint16_t* rcpT) {
+    bool hit = false;
+    const int4 pr = *reinterpret_cast<const int4*>(L->prim);
+    const int32_t prim[4] = {pr.x, pr.y, pr.z, pr.w};
+#pragma unroll 1
+    for (int i = 0; i < 4; i++) {
+        int32_t pid = i == 0 ? prim[0] : i == 1 ? prim[1] : i == 2 ? prim[2] : prim[3];
+        if (pid < 0) break;
+        const float* T = L->tri[i];
+        float ax = T[0], ay = T[1], az = T[2], e0x = T[3], e0y = T[4], e0z = T[5], e1x = T[6], e1y = T[7], e1z = T[8];
+        float px = r.d[1] * e1z - r.d[2] * e1y;
+        float py = -1.0f * (r.d[0] * e1z - r.d[2] * e1x);
+        float pz = r.d[0] * e1y - r.d[1] * e1x;
+        float det = e0x * px + (e0y * py + e0z * pz);
+        float inv = rcp_nr(det, rcpT);
+        float tx = r.o[0] - ax, ty = r.o[1] - ay, tz = r.o[2] - az;
+        float a = inv * (tx * px + (ty * py + tz * pz));
+        float qx = ty * e0z - tz * e0y;
+        float qy = -1.0f * (tx * e0z - tz * e0x);
+        float qz = tx * e0y - ty * e0x;
+        float b = inv * (r.d[0] * qx + (r.d[1] * qy + r.d[2] * qz));
+        float t = inv * (e1x * qx + (e1y * qy + e1z * qz));
+        bool ok = (a >= 0.0f) & (a <= 1.0f) & (b >= 0.0f) & (b <= 1.0f) & ((a + b) <= 1.0f) & (t >= tMin) & (t < h.t);
+        if (ok) {
+            if (ANY) return true;
+            h.t = t; h.a = a; h.b = b; h.prim = pid;
+            hit = true;
+        }
+    }
+    return hit;
+}
+
+// QBVH_Node::intersect (src/BVH.cpp:391-414) -> 4-bit hit mask.
+__device__ __forceinline__ int box_test(const float4* bx, const DRay& r, float tMin, float tMax) {
+    float4 mnx = bx[0], mny = bx[1], mnz = bx[2], mxx = bx[3], mxy = bx[4], mxz = bx[5];
+    float lx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, ly[4] = {mny.x, mny.y, mny.z, mny.w}, lz[4] = {mnz.x, mnz.y, mnz.z, mnz.w};
+    float hx[4] = {mxx.x, mxx.y, mxx.z, mxx.w}, hy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, hz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        float t0x = (lx[i] - r.o[0]) * r.id[0], t1x = (hx[i] - r.o[0]) * r.id[0];
+        float t0y = (ly[i] - r.o[1]) * r.id[1], t1y = (hy[i] - r.o[1]) * r.id[1];
+        float t0z = (lz[i] - r.o[2]) * r.id[2], t1z = (hz[i] - r.o[2]) * r.id[2];
+        float t0 = sse_max(sse_min(t0x, t1x), sse_max(sse_min(t0y, t1y), sse_min(t0z, t1z)));
+        float t1 = sse_min(sse_max(t0x, t1x), sse_min(sse_max(t0y, t1y), sse_max(t0z, t1z)));
+        m |= (int)(sse_max(t0, tMin) <= sse_min(t1, tMax)) << i;
+    }
+    return m;
+}
+
+// BVH::intersect, QBVH branch (src/BVH.cpp:1128-1178).  Returns hit.  On a
+// stack overflow, st.overflow is set and the query is abandoned.
+template <bool ANY, bool COUNT>
+__device__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
+    int sp = 0;
+    int32_t cur = 0;
+    bool hit = false;
+    while (true) {
+        const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
+        int m = box_test(q, r, tMin, h.t);
+        int4 ch = reinterpret_cast<const int4*>(q)[6];
+        int32_t chv[4] = {ch.x, ch.y, ch.z, ch.w};
+        if (COUNT) st.nodes++;
+        int inner = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (!(m & (1 << i)) || chv[i] == kEmptySlot) continue;
+            if (chv[i] < 0) {
+                if (COUNT) st.leaves++;
+                if (intersect4<ANY>(c.leaves + ~chv[i], r, tMin, h, c.rcpT)) {
+                    hit = true;
+                    if (ANY) return true;
+                }
+            } else {
+                inner |= 1 << i;
+            }
+        }
+        if (inner) {
+            int top = 31 - __builtin_clz((unsigned)inner);
+            int rest = inner & ~(1 << top);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if (rest & (1 << i)) {
+                    if (!stk_push(c, sp, chv[i])) { st.overflow = true; return hit; }
+                }
+            }
+            if (COUNT && sp > st.max_sp) st.max_sp = sp;
+            int32_t nxt = chv[0];
+#pragma unroll
+            for (int i = 1; i < 4; i++)
+                if (top == i) nxt = chv[i];
+            cur = nxt;
+        } else {
+            if (sp == 0) break;
+            cur = stk_pop(c, sp);
+        }
+    }
+    return hit;
+}
+
+}  // namespace mrt

@@ -1,0 +1,111 @@
+// mrt_math.h -- the reference's numeric contract, shared by host and device.
+//
+// The reference computes in IEEE single precision with x86 SSE approximate
+// reciprocals: rcp_nr = 2r - x*r*r (r = RCPSS), rsqrt_nr = (0.5a)(3 - x*a*a)
+// (a = RSQRTSS) -- reference src/SSE.h:67-101; dot products use DPPS
+// (src/Vector3.h:279-288), SoA dots add as x + (y + z) (src/SSE.h:111-114).
+// RCPSS/RSQRTSS are reproduced bit-exactly from 2 x 2048-entry tables captured
+// on an Intel host (tools/gen_x86_tables.c, verified over all 2^32 inputs).
+// Every entry has exponent 126 and <= 12 significant mantissa bits, so the
+// device keeps them as 2 x 4 KB of u16 in LDS: bits = 0x3F000000 | (e << 11).
+//
+// Build with -ffp-contract=off: every expression below is a sequence of
+// individually rounded IEEE ops in the reference's order (no FMA contraction).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define MRT_HD __host__ __device__ __forceinline__
+#else
+#define MRT_HD static inline
+#endif
+
+namespace mrt {
+
+MRT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+MRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// 12-bit packed table entry -> float bits in [0.5, 1)
+MRT_HD uint32_t tbl_bits(uint16_t e) { return 0x3F000000u | ((uint32_t)e << 11); }
+
+// RCPSS emulation; T = 2048-entry packed rcp table.
+MRT_HD float x86_rcp(float x, const uint16_t* T) {
+    uint32_t u = f2u(x), s = u & 0x80000000u, e = (u >> 23) & 0xFFu, m = u & 0x7FFFFFu;
+    if (e == 0xFFu) return u2f(m ? (u | 0x00400000u) : s);
+    if (e == 0u) return u2f(s | 0x7F800000u);
+    uint32_t t = tbl_bits(T[m >> 12]);
+    int re = 126 - ((int)e - 127);
+    if (re <= 0) return u2f(s);
+    return u2f(s | ((uint32_t)re << 23) | (t & 0x7FFFFFu));
+}
+
+// RSQRTSS emulation; T = 2048-entry packed rsqrt table ([odd exponent][10 bits]).
+MRT_HD float x86_rsqrt(float x, const uint16_t* T) {
+    uint32_t u = f2u(x), s = u & 0x80000000u, e = (u >> 23) & 0xFFu, m = u & 0x7FFFFFu;
+    if (e == 0xFFu) return u2f(m ? (u | 0x00400000u) : (s ? 0xFFC00000u : 0u));
+    if (e == 0u) return u2f(s | 0x7F800000u);
+    if (s) return u2f(0xFFC00000u);
+    int E = (int)e - 127, odd = E & 1, k = (E - odd) / 2;
+    uint32_t t = tbl_bits(T[(odd << 10) | (m >> 13)]);
+    int re = 126 - k;
+    return u2f(((uint32_t)re << 23) | (t & 0x7FFFFFu));
+}
+
+// recipss / recipps (src/SSE.h:67-86)
+MRT_HD float rcp_nr(float x, const uint16_t* T) {
+    float r = x86_rcp(x, T);
+    return (2.0f * r) - (x * (r * r));
+}
+// fastrsqrtss / fastrsqrtps (src/SSE.h:88-101)
+MRT_HD float rsqrt_nr(float x, const uint16_t* T) {
+    float a = x86_rsqrt(x, T);
+    float muls = (x * a) * a;
+    return (0.5f * a) * (3.0f - muls);
+}
+
+MRT_HD float sse_min(float a, float b) { return a < b ? a : b; }  // MINPS
+MRT_HD float sse_max(float a, float b) { return a > b ? a : b; }  // MAXPS
+MRT_HD float std_min(float a, float b) { return b < a ? b : a; }  // std::min
+MRT_HD float std_max(float a, float b) { return a < b ? b : a; }  // std::max
+
+struct v3 { float x, y, z; };
+MRT_HD v3 mk(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+MRT_HD v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+MRT_HD v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+MRT_HD v3 mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+MRT_HD v3 scale(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+MRT_HD v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+// DPPS imm 0x71: (x*x' + y*y') + (z*z' + 0)
+MRT_HD float dot(v3 a, v3 b) {
+    float p0 = a.x * b.x, p1 = a.y * b.y, p2 = a.z * b.z;
+    return (p0 + p1) + (p2 + 0.0f);
+}
+MRT_HD v3 cross(v3 a, v3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+MRT_HD v3 normalized(v3 a, const uint16_t* T_rsqrt) { return scale(a, rsqrt_nr(dot(a, a), T_rsqrt)); }
+
+// 32768-entry gamma LUT lookup index (Image::Map, src/Image.cpp:71-76); negative /
+// NaN (UB in the reference's unsigned-short cast) -> 0.
+MRT_HD uint32_t map_index(float r) {
+    float rMap = 32768.0f * r;
+    if (rMap > 32768.0f) return 32768u;
+    if (!(rMap >= 0.0f)) return 0u;
+    return (uint32_t)(uint16_t)(int)rMap;
+}
+
+// Counter-based RNG standing in for Scene::getRand's global MT pool
+// (src/Scene.cpp:30-47); same float mapping ((float)u + 0.5) * 2^-32 in double.
+MRT_HD uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16; return x;
+}
+MRT_HD float rng(uint32_t pixel, uint32_t sample, uint32_t dim, uint32_t seed) {
+    uint32_t h = mix32(seed ^ 0x9E3779B9u);
+    h = mix32(h ^ pixel);
+    h = mix32(h ^ (sample * 0x85EBCA6Bu));
+    h = mix32(h ^ (dim * 0xC2B2AE35u));
+    return (float)(((double)(float)h + 0.5) * (1.0 / 4294967296.0));
+}
+
+}  // namespace mrt

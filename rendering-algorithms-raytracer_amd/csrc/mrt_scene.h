@@ -1,0 +1,58 @@
+// mrt_scene.h -- internal scene object behind the opaque mrt_scene handle.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mrt.h"
+#include "mrt_math.h"
+#include "mrt_types.h"
+
+namespace mrt {
+
+// Packed x86 approximation tables (host copies; uploaded to the device).
+const uint16_t* host_rcp_table();
+const uint16_t* host_rsqrt_table();
+const uint8_t* host_gamma_lut();  // 32769 entries, Image::generateGammaTables
+
+struct Mesh {
+    std::vector<v3> verts, normals;
+    std::vector<uint32_t> vidx, nidx;
+    int material = 0;
+    int32_t nt() const { return (int32_t)(vidx.size() / 3); }
+};
+
+struct DeviceState;  // defined in mrt_device.hip
+
+struct Scene {
+    std::vector<Mesh> meshes;
+    std::vector<DevMaterial> materials;
+    std::vector<DevLight> lights;
+    float bg[3] = {0.f, 0.f, 0.f};
+    int num_paths = 1;
+
+    // objects in scene order (makeMeshObjs): global prim id -> (mesh, tri)
+    std::vector<int32_t> obj_mesh, obj_tri;
+    // QBVH
+    std::vector<QNode> nodes;
+    std::vector<QLeaf> leaves;
+    mrt_bvh_info info{};
+    bool built = false;
+
+    DeviceState* dev = nullptr;
+    bool dev_dirty = true;
+    mrt_stats last{};
+};
+
+// host_build.cpp
+int load_obj(const char* path, const float* ctm16, Mesh& out, std::string& err);
+int build_qbvh(Scene& s, std::string& err);
+
+void set_error(const std::string& msg);
+
+}  // namespace mrt
+
+struct mrt_scene {
+    mrt::Scene impl;
+};

@@ -1,0 +1,71 @@
+// mrt_types.h -- scene data as it lives in HBM (shared host/device layout).
+#pragma once
+#include <stdint.h>
+
+namespace mrt {
+
+// 4-wide node, one 128-B line.  SoA boxes exactly as QBVH_Node
+// (reference src/BVH.h:83-109): minX[4] minY[4] minZ[4] maxX[4] maxY[4] maxZ[4].
+// child[i] >= 0: inner node index; child[i] == INT32_MIN: empty slot;
+// otherwise ~child[i] is a leaf-packet index.
+struct alignas(16) QNode {
+    float box[24];
+    int32_t child[4];
+    uint32_t pad[4];
+};
+static_assert(sizeof(QNode) == 128, "QNode must be one 128-B line");
+
+// 4-triangle packet, TriCache4 (src/BVH.h:37-50): A, e0 = B-A, e1 = C-A (SoA),
+// plus global prim ids (-1 = empty lane).  160 B.
+struct alignas(16) QLeaf {
+    float t[36];
+    int32_t prim[4];
+};
+static_assert(sizeof(QLeaf) == 160, "QLeaf must be 160 B");
+
+// Device copy of a packet: per-triangle AoS (Ax Ay Az e0x e0y e0z e1x e1y e1z)
+// so one lane walks its packet a triangle at a time; prim = -1 ends the packet.
+struct alignas(16) DLeaf {
+    float tri[4][9];
+    int32_t prim[4];
+};
+static_assert(sizeof(DLeaf) == 160, "DLeaf must be 160 B");
+
+static constexpr int32_t kEmptySlot = (int32_t)0x80000000u;
+
+// Per-triangle shading record: global vertex / normal indices + material.
+struct alignas(16) PrimShade {
+    uint32_t v[3];
+    uint32_t mat;
+    uint32_t n[3];
+    uint32_t pad;
+};
+static_assert(sizeof(PrimShade) == 32, "PrimShade is 32 B");
+
+struct DevMaterial {
+    int32_t type;
+    float kd[3], ka[3], ks[3];
+    float spec_exp, spec_amt;
+};
+
+struct DevLight {
+    int32_t type;
+    float pos[3], v1[3], v2[3], v3[3];
+    float power;        // point: m_power; rect: power * rsqrt_nr(area^2) (setPower)
+    int32_t samples;
+    float noise;
+    int32_t cast_shadows;
+};
+
+// Camera basis hoisted to the host (bit-identical to the per-ray recompute of
+// Camera::eyeRayAdaptive, src/Camera.cpp:116-137).
+struct CamParams {
+    float eye[3], u[3], v[3], w[3];
+    float left, right, bottom, top;
+    int32_t W, H;
+};
+
+static constexpr int kMaxLights = 8;
+static constexpr int kMaxMaterials = 64;
+
+}  // namespace mrt

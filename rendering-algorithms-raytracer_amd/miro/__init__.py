@@ -1,0 +1,375 @@
+"""miro -- host-side mirror of the reference's scene API over libmrt.so.
+
+Names, argument meaning and call order follow the reference scene scripts
+(reference src/assignment2.h, src/Scene.h, src/Camera.h, src/Light.h):
+
+    scene = Scene(); cam = Camera(); img = Image(); img.resize(512, 512)
+    scene.setBGColor(Vector3(0, 0, 0.2))
+    cam.setEye(Vector3(8, 1.5, 1)); cam.setLookAt(Vector3(0, 2.5, -1))
+    cam.setUp(Vector3(0, 1, 0)); cam.setFOV(55)
+    light = PointLight(); light.setPosition(Vector3(0, 10, 0)); light.setPower(200)
+    scene.addLight(light)
+    mesh = TriangleMesh(); mesh.load("sponza.obj"); makeMeshObjs(scene, mesh, Blinn(Vector3(1)))
+    scene.preCalc()                    # BVH::build
+    scene.raytraceImage(cam, img)      # 1 spp primary + shadow rays on the GPU
+
+Everything that computes runs in libmrt.so (HIP kernels for gfx950); this
+module only marshals data.  Missing library -> MRTError, no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import MRTError, check, f3
+
+__all__ = ["Vector3", "Matrix4x4", "TriangleMesh", "Lambert", "Blinn", "PointLight", "RectangleLight",
+           "Camera", "Image", "Scene", "Ray", "HitInfo", "makeMeshObjs", "MRTError", "lib", "device_count",
+           "rcp_nr", "rsqrt_nr"]
+
+lib = _lib.load
+
+
+def device_count() -> int:
+    return int(lib().mrt_device_count())
+
+
+def rcp_nr(x: float) -> float:
+    return float(lib().mrt_rcp_nr(float(x)))
+
+
+def rsqrt_nr(x: float) -> float:
+    return float(lib().mrt_rsqrt_nr(float(x)))
+
+
+class Vector3(tuple):
+    """Plain 3-tuple with the reference's constructors: Vector3(s) or Vector3(x, y, z)."""
+
+    def __new__(cls, *a):
+        if len(a) == 1 and np.ndim(a[0]) == 0:
+            a = (a[0], a[0], a[0])
+        elif len(a) == 1:
+            a = tuple(a[0])
+        if len(a) != 3:
+            raise ValueError("Vector3 needs 1 or 3 components")
+        return super().__new__(cls, (float(a[0]), float(a[1]), float(a[2])))
+
+    x = property(lambda s: s[0])
+    y = property(lambda s: s[1])
+    z = property(lambda s: s[2])
+
+
+class Matrix4x4:
+    """Row-major 4x4 (m11..m44), src/Matrix4x4.h.  Only used as a load-time ctm."""
+
+    def __init__(self, m=None):
+        self.m = np.eye(4, dtype=np.float32) if m is None else np.asarray(m, np.float32).reshape(4, 4).copy()
+
+    def setIdentity(self):
+        self.m = np.eye(4, dtype=np.float32)
+
+    def translate(self, x, y, z):  # setColumn4(Vector4(x,y,z,0) + column4), src/Matrix4x4.h:751-754
+        self.m[0, 3] = np.float32(x) + self.m[0, 3]
+        self.m[1, 3] = np.float32(y) + self.m[1, 3]
+        self.m[2, 3] = np.float32(z) + self.m[2, 3]
+
+    def scale(self, x, y, z):  # src/Matrix4x4.h:757-762
+        self.m[0, 0] *= np.float32(x)
+        self.m[1, 1] *= np.float32(y)
+        self.m[2, 2] *= np.float32(z)
+
+
+class TriangleMesh:
+    """TriangleMesh (src/TriangleMesh.h).  load() keeps the path; the OBJ is parsed
+    by libmrt's loader (src/TriangleMeshLoad.cpp semantics) at Scene.preCalc()."""
+
+    def __init__(self):
+        self.path: Optional[str] = None
+        self.ctm: Optional[np.ndarray] = None
+        self.verts = self.normals = self.vidx = self.nidx = None
+
+    def load(self, file, ctm: Optional[Matrix4x4] = None) -> bool:
+        self.path = str(file)
+        self.ctm = None if ctm is None else np.ascontiguousarray(ctm.m, np.float32)
+        return True
+
+    def createSingleTriangle(self):  # src/TriangleMesh.cpp:11-42
+        self.verts = np.zeros((3, 3), np.float32)
+        self.normals = np.zeros((3, 3), np.float32)
+        self.vidx = np.array([[0, 1, 2]], np.uint32)
+        self.nidx = np.array([[0, 1, 2]], np.uint32)
+
+    def setArrays(self, verts, normals, vidx, nidx):
+        self.verts = np.ascontiguousarray(verts, np.float32).reshape(-1, 3)
+        self.normals = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
+        self.vidx = np.ascontiguousarray(vidx, np.uint32).reshape(-1, 3)
+        self.nidx = np.ascontiguousarray(nidx, np.uint32).reshape(-1, 3)
+
+    def setV1(self, v): self.verts[0] = v
+    def setV2(self, v): self.verts[1] = v
+    def setV3(self, v): self.verts[2] = v
+    def setN1(self, n): self.normals[0] = n
+    def setN2(self, n): self.normals[1] = n
+    def setN3(self, n): self.normals[2] = n
+
+
+class Lambert:
+    """Lambert(kd = Vector3(1), ka = Vector3(0)), src/Lambert.h:11-13."""
+
+    def __init__(self, kd=Vector3(1), ka=Vector3(0)):
+        self.kd, self.ka = Vector3(kd), Vector3(ka)
+
+    def setKd(self, kd): self.kd = Vector3(kd)
+    def setKa(self, ka): self.ka = Vector3(ka)
+
+    def _c(self):
+        return _lib.mrt_material(0, f3(self.kd), f3(self.ka), f3((1, 1, 1)), 1.0, 0.0)
+
+
+class Blinn:
+    """Blinn(kd, ka, ks, kt, ior, specExp, specAmt, ...) defaults of src/Blinn.h:11-22.
+    Direct lighting only (reflect/refract/path tracing are SURVEY §8(f) rank 4)."""
+
+    def __init__(self, kd=Vector3(1), ka=Vector3(0), ks=Vector3(1), kt=Vector3(0), ior=1.5,
+                 specExp=1.0, specAmt=0.0, reflectAmt=0.0, refractAmt=0.0):
+        self.kd, self.ka, self.ks, self.kt = Vector3(kd), Vector3(ka), Vector3(ks), Vector3(kt)
+        self.ior, self.specExp, self.specAmt = float(ior), float(specExp), float(specAmt)
+        if reflectAmt or refractAmt:
+            raise NotImplementedError("Blinn reflection/refraction is not on the MI355X path yet")
+
+    def setKd(self, v): self.kd = Vector3(v)
+    def setKa(self, v): self.ka = Vector3(v)
+    def setKs(self, v): self.ks = Vector3(v)
+    def setSpecExp(self, e): self.specExp = float(e)
+    def setSpecAmt(self, a): self.specAmt = float(a)
+
+    def _c(self):
+        return _lib.mrt_material(1, f3(self.kd), f3(self.ka), f3(self.ks), self.specExp, self.specAmt)
+
+
+class _Light:
+    def __init__(self):  # Light::Light, src/Light.h:15-19
+        self.color = Vector3(0)
+        self.power = 0.0
+        self.samples = 1
+        self.castShadows = True
+        self.noiseThreshold = 0.001
+
+    def setColor(self, c): self.color = Vector3(c)
+    def setPower(self, p): self.power = float(p)
+    def setSamples(self, n): self.samples = int(n)
+    def setCastShadows(self, c): self.castShadows = bool(c)
+    def setNoiseThreshold(self, t): self.noiseThreshold = float(t)
+
+
+class PointLight(_Light):
+    def __init__(self):
+        super().__init__()
+        self.position = Vector3(0)
+
+    def setPosition(self, v): self.position = Vector3(v)
+
+    def _c(self):
+        return _lib.mrt_light(0, f3(self.position), f3((0, 0, 0)), f3((0, 0, 0)), f3((0, 0, 0)), self.power,
+                              self.samples, self.noiseThreshold, int(self.castShadows))
+
+
+class RectangleLight(_Light):
+    def __init__(self):
+        super().__init__()
+        self.v1 = self.v2 = self.v3 = Vector3(0)
+
+    def setVertices(self, v1, v2, v3):
+        self.v1, self.v2, self.v3 = Vector3(v1), Vector3(v2), Vector3(v3)
+
+    def _c(self):
+        return _lib.mrt_light(1, f3((0, 0, 0)), f3(self.v1), f3(self.v2), f3(self.v3), self.power,
+                              self.samples, self.noiseThreshold, int(self.castShadows))
+
+
+class Camera:
+    """Camera setters of src/Camera.h:26-45 (fov in degrees, like setFOV)."""
+
+    def __init__(self):
+        self.eye, self.lookAt, self.up, self.fov = Vector3(0), Vector3(0, 0, -1), Vector3(0, 1, 0), 45.0
+
+    def setEye(self, v): self.eye = Vector3(v)
+    def setLookAt(self, v): self.lookAt = Vector3(v)
+    def setUp(self, v): self.up = Vector3(v)
+    def setFOV(self, f): self.fov = float(f)
+
+    def _c(self):
+        return _lib.mrt_camera(f3(self.eye), f3(self.lookAt), f3(self.up), self.fov)
+
+
+class Image:
+    """Image (src/Image.h): 8-bit RGB, row 0 = bottom, plus the float RGB frame
+    before Image::Map (`rgb`) for parity checks."""
+
+    def __init__(self):
+        self.resize(1, 1)
+
+    def resize(self, w, h):
+        self.m_width, self.m_height = int(w), int(h)
+        self.rgb = np.zeros((self.m_height, self.m_width, 3), np.float32)
+        self.pixels = np.zeros((self.m_height, self.m_width, 3), np.uint8)
+
+    def width(self): return self.m_width
+    def height(self): return self.m_height
+
+    def writePPM(self, path):  # src/Image.cpp:137-154 (rows flipped)
+        with open(path, "wb") as f:
+            f.write(b"P6\n%d %d\n255\n" % (self.m_width, self.m_height))
+            f.write(np.ascontiguousarray(self.pixels[::-1]).tobytes())
+
+
+class Ray:
+    def __init__(self, o, d):
+        self.o, self.d = Vector3(o), Vector3(d)
+
+
+class HitInfo:
+    """HitInfo (src/Ray.h:185-200); obj is the global triangle id (-1 = none)."""
+
+    def __init__(self, t=1e12, a=0.0, b=0.0, obj=-1):
+        self.t, self.a, self.b, self.obj = float(t), float(a), float(b), int(obj)
+
+
+HIT_DTYPE = np.dtype([("t", "<f4"), ("a", "<f4"), ("b", "<f4"), ("prim", "<i4")])
+
+
+def makeMeshObjs(scene: "Scene", mesh: TriangleMesh, material):
+    """One Object per triangle, in mesh order (the reference's missing helper)."""
+    scene.addMesh(mesh, material)
+
+
+class Scene:
+    """Scene (src/Scene.h).  Objects are whole meshes here; object ids inside a
+    HitInfo are global triangle indices in insertion order."""
+
+    def __init__(self, device: int = 0):
+        self._meshes: List[tuple] = []
+        self._lights: List[_Light] = []
+        self.bg = Vector3(0)
+        self.m_numPaths = 1
+        self.device = int(device)
+        self._h = None
+        self.bvh_info = None
+
+    # -- construction (src/Scene.h:17-28)
+    def addMesh(self, mesh, material): self._meshes.append((mesh, material))
+    def addLight(self, light): self._lights.append(light)
+    def setBGColor(self, c): self.bg = Vector3(c)
+    def setNumPaths(self, p): self.m_numPaths = int(p)
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().mrt_scene_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise MRTError("call preCalc() first")
+        return self._h
+
+    def preCalc(self):
+        """Scene::preCalc -> BVH::build (host side of libmrt)."""
+        L = lib()
+        if self._h:
+            L.mrt_scene_destroy(self._h)
+        self._h = L.mrt_scene_create()
+        mats = {}
+        for mesh, mat in self._meshes:
+            if id(mat) not in mats:
+                m = mat._c()
+                mats[id(mat)] = check(L.mrt_scene_add_material(self._h, C.byref(m)), "add_material")
+            mid = mats[id(mat)]
+            if mesh.path is not None:
+                ctm = mesh.ctm.ctypes.data_as(C.POINTER(C.c_float)) if mesh.ctm is not None else None
+                check(L.mrt_scene_add_obj(self._h, mesh.path.encode(), ctm, mid), f"load {mesh.path}")
+            else:
+                v, n, vi, ni = mesh.verts, mesh.normals, mesh.vidx, mesh.nidx
+                mm = _lib.mrt_mesh(v.ctypes.data_as(C.POINTER(C.c_float)), n.ctypes.data_as(C.POINTER(C.c_float)),
+                                   vi.ctypes.data_as(C.POINTER(C.c_uint32)), ni.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                   len(v), len(n), len(vi))
+                check(L.mrt_scene_add_mesh(self._h, C.byref(mm), mid), "add_mesh")
+        for light in self._lights:
+            lc = light._c()
+            check(L.mrt_scene_add_light(self._h, C.byref(lc)), "add_light")
+        check(L.mrt_scene_set_background(self._h, f3(self.bg)), "bg")
+        check(L.mrt_scene_set_num_paths(self._h, self.m_numPaths), "num_paths")
+        check(L.mrt_scene_build_bvh(self._h), "BVH build")
+        info = _lib.mrt_bvh_info()
+        check(L.mrt_scene_bvh_info(self._h, C.byref(info)), "bvh_info")
+        self.bvh_info = {k: getattr(info, k) for k, _ in info._fields_}
+        return self.bvh_info
+
+    def mesh_arrays(self, mesh_id: int):
+        L = lib()
+        nv, nn, nt = C.c_int32(), C.c_int32(), C.c_int32()
+        check(L.mrt_scene_mesh_info(self.handle, mesh_id, C.byref(nv), C.byref(nn), C.byref(nt)), "mesh_info")
+        v = np.zeros((nv.value, 3), np.float32)
+        n = np.zeros((nn.value, 3), np.float32)
+        vi = np.zeros((nt.value, 3), np.uint32)
+        ni = np.zeros((nt.value, 3), np.uint32)
+        check(L.mrt_scene_mesh_export(self.handle, mesh_id, v.ctypes.data_as(C.POINTER(C.c_float)),
+                                      n.ctypes.data_as(C.POINTER(C.c_float)), vi.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                      ni.ctypes.data_as(C.POINTER(C.c_uint32))), "mesh_export")
+        return v, n, vi, ni
+
+    def bvh_export(self):
+        info = self.bvh_info
+        nb = np.zeros((info["nodes"], 24), np.float32)
+        nc = np.zeros((info["nodes"], 4), np.int32)
+        lt = np.zeros((info["leaves"], 36), np.float32)
+        lp = np.zeros((info["leaves"], 4), np.int32)
+        check(lib().mrt_scene_bvh_export(self.handle, nb.ctypes.data_as(C.POINTER(C.c_float)),
+                                         nc.ctypes.data_as(C.POINTER(C.c_int32)),
+                                         lt.ctypes.data_as(C.POINTER(C.c_float)),
+                                         lp.ctypes.data_as(C.POINTER(C.c_int32))), "bvh_export")
+        return nb, nc, lt, lp
+
+    # -- rendering (src/Scene.cpp:85-217)
+    def raytraceImage(self, cam: Camera, img: Image, count_visits=False, want_hits=False, seed=0):
+        W, H = img.width(), img.height()
+        opts = _lib.mrt_render_opts(W, H, self.device, int(count_visits), 1, int(want_hits), seed)
+        hits = np.zeros((H, W), HIT_DTYPE) if want_hits else None
+        c = cam._c()
+        check(lib().mrt_render(self.handle, C.byref(c), C.byref(opts), img.rgb.ctypes.data_as(C.POINTER(C.c_float)),
+                               img.pixels.ctypes.data_as(C.POINTER(C.c_uint8)),
+                               hits.ctypes.data if hits is not None else None), "raytraceImage")
+        self.last_stats = self.stats()
+        return hits
+
+    def stats(self):
+        st = _lib.mrt_stats()
+        check(lib().mrt_scene_last_stats(self.handle, C.byref(st)), "stats")
+        return {k: getattr(st, k) for k, _ in st._fields_}
+
+    # -- ray queries (src/Scene.cpp:295-298)
+    def traceBatch(self, o, d, tmin=0.001, tmax=1e12, any_hit=False):
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        n = len(o)
+        tmin = np.ascontiguousarray(np.broadcast_to(np.asarray(tmin, np.float32), (n,)))
+        tmax = np.ascontiguousarray(np.broadcast_to(np.asarray(tmax, np.float32), (n,)))
+        out = np.zeros(n, HIT_DTYPE)
+        fp = C.POINTER(C.c_float)
+        check(lib().mrt_trace(self.handle, o.ctypes.data_as(fp), d.ctypes.data_as(fp), tmin.ctypes.data_as(fp),
+                              tmax.ctypes.data_as(fp), n, int(any_hit), out.ctypes.data), "trace")
+        return out
+
+    def trace(self, hitInfo: HitInfo, ray: Ray, tMin=0.001) -> bool:
+        """Scene::trace(threadID, HitInfo&, const Ray&, tMin): hitInfo.t is tMax in, t out."""
+        r = self.traceBatch([ray.o], [ray.d], tMin, hitInfo.t)[0]
+        if r["prim"] < 0:
+            return False
+        hitInfo.t, hitInfo.a, hitInfo.b, hitInfo.obj = float(r["t"]), float(r["a"]), float(r["b"]), int(r["prim"])
+        return True

@@ -1,0 +1,134 @@
+"""ctypes binding of libmrt.so (include/mrt.h).  Loads the in-tree build only;
+raises if it is missing -- there is no fallback path."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("MRT_LIB", os.path.join(_PKG, "lib", "libmrt.so"))
+
+MRT_OK = 0
+ERRORS = {-1: "MRT_ERR_INVALID", -2: "MRT_ERR_IO", -3: "MRT_ERR_HIP", -4: "MRT_ERR_BUILD",
+          -5: "MRT_ERR_NOT_BUILT", -6: "MRT_ERR_OVERFLOW", -7: "MRT_ERR_NO_DEVICE"}
+
+# Every symbol include/mrt.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "mrt_last_error", "mrt_abi_version", "mrt_device_count", "mrt_scene_create", "mrt_scene_destroy",
+    "mrt_scene_add_material", "mrt_scene_add_light", "mrt_scene_add_obj", "mrt_scene_add_mesh",
+    "mrt_scene_mesh_info", "mrt_scene_mesh_export", "mrt_scene_set_background", "mrt_scene_set_num_paths",
+    "mrt_scene_build_bvh", "mrt_scene_bvh_info", "mrt_scene_bvh_export", "mrt_scene_bvh_import",
+    "mrt_scene_upload", "mrt_render", "mrt_render_buckets_async", "mrt_unpack_buckets_async",
+    "mrt_render_frame_async", "mrt_trace", "mrt_trace_async", "mrt_scene_last_stats", "mrt_rcp_nr",
+    "mrt_rsqrt_nr",
+]
+
+
+class mrt_material(C.Structure):
+    _fields_ = [("type", C.c_int32), ("kd", C.c_float * 3), ("ka", C.c_float * 3), ("ks", C.c_float * 3),
+                ("spec_exp", C.c_float), ("spec_amt", C.c_float)]
+
+
+class mrt_light(C.Structure):
+    _fields_ = [("type", C.c_int32), ("pos", C.c_float * 3), ("v1", C.c_float * 3), ("v2", C.c_float * 3),
+                ("v3", C.c_float * 3), ("power", C.c_float), ("samples", C.c_int32),
+                ("noise_threshold", C.c_float), ("cast_shadows", C.c_int32)]
+
+
+class mrt_camera(C.Structure):
+    _fields_ = [("eye", C.c_float * 3), ("look_at", C.c_float * 3), ("up", C.c_float * 3), ("fov_deg", C.c_float)]
+
+
+class mrt_mesh(C.Structure):
+    _fields_ = [("verts", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
+                ("vidx", C.POINTER(C.c_uint32)), ("nidx", C.POINTER(C.c_uint32)),
+                ("nv", C.c_int32), ("nn", C.c_int32), ("nt", C.c_int32)]
+
+
+class mrt_hit(C.Structure):
+    _fields_ = [("t", C.c_float), ("a", C.c_float), ("b", C.c_float), ("prim", C.c_int32)]
+
+
+class mrt_bvh_info(C.Structure):
+    _fields_ = [("nodes", C.c_int32), ("leaves", C.c_int32), ("prims", C.c_int32), ("bin_nodes", C.c_int32),
+                ("bin_leaves", C.c_int32), ("max_depth", C.c_int32), ("build_ms", C.c_double),
+                ("device_bytes", C.c_uint64)]
+
+
+class mrt_render_opts(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("device", C.c_int32), ("count_visits", C.c_int32),
+                ("want_rgb8", C.c_int32), ("want_hits", C.c_int32), ("seed", C.c_uint32)]
+
+
+class mrt_stats(C.Structure):
+    _fields_ = [("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("node_visits", C.c_uint64),
+                ("leaf_visits", C.c_uint64), ("primary_node_visits", C.c_uint64),
+                ("primary_leaf_visits", C.c_uint64), ("primary_hits", C.c_uint64), ("kernel_ms", C.c_float), ("primary_ms", C.c_float),
+                ("shade_ms", C.c_float), ("max_stack", C.c_int32)]
+
+
+_fp = C.POINTER(C.c_float)
+_ip = C.POINTER(C.c_int32)
+_up = C.POINTER(C.c_uint32)
+_bp = C.POINTER(C.c_uint8)
+_lib = None
+
+
+class MRTError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libmrt.so (fails loudly when the HIP build is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MRTError(f"libmrt.so not built at {LIB_PATH}; run __graft_entry__.build() "
+                       f"(make -C rendering-algorithms-raytracer_amd)")
+    L = C.CDLL(LIB_PATH)
+    L.mrt_last_error.restype = C.c_char_p
+    L.mrt_scene_create.restype = C.c_void_p
+    L.mrt_scene_destroy.argtypes = [C.c_void_p]
+    L.mrt_scene_add_material.argtypes = [C.c_void_p, C.POINTER(mrt_material)]
+    L.mrt_scene_add_light.argtypes = [C.c_void_p, C.POINTER(mrt_light)]
+    L.mrt_scene_add_obj.argtypes = [C.c_void_p, C.c_char_p, _fp, C.c_int]
+    L.mrt_scene_add_mesh.argtypes = [C.c_void_p, C.POINTER(mrt_mesh), C.c_int]
+    L.mrt_scene_mesh_info.argtypes = [C.c_void_p, C.c_int, _ip, _ip, _ip]
+    L.mrt_scene_mesh_export.argtypes = [C.c_void_p, C.c_int, _fp, _fp, _up, _up]
+    L.mrt_scene_set_background.argtypes = [C.c_void_p, _fp]
+    L.mrt_scene_set_num_paths.argtypes = [C.c_void_p, C.c_int]
+    L.mrt_scene_build_bvh.argtypes = [C.c_void_p]
+    L.mrt_scene_bvh_info.argtypes = [C.c_void_p, C.POINTER(mrt_bvh_info)]
+    L.mrt_scene_bvh_export.argtypes = [C.c_void_p, _fp, _ip, _fp, _ip]
+    L.mrt_scene_bvh_import.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _fp, _ip, _fp, _ip]
+    L.mrt_scene_upload.argtypes = [C.c_void_p, C.c_int]
+    L.mrt_render.argtypes = [C.c_void_p, C.POINTER(mrt_camera), C.POINTER(mrt_render_opts), _fp, _bp, C.c_void_p]
+    L.mrt_render_buckets_async.argtypes = [C.c_void_p, C.POINTER(mrt_camera), C.POINTER(mrt_render_opts),
+                                           C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+    L.mrt_unpack_buckets_async.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mrt_render_frame_async.argtypes = [C.c_void_p, C.POINTER(mrt_camera), C.POINTER(mrt_render_opts),
+                                         C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mrt_trace.argtypes = [C.c_void_p, _fp, _fp, _fp, _fp, C.c_size_t, C.c_int, C.c_void_p]
+    L.mrt_trace_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                  C.c_int, C.c_void_p, C.c_void_p]
+    L.mrt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(mrt_stats)]
+    L.mrt_rcp_nr.argtypes = [C.c_float]
+    L.mrt_rcp_nr.restype = C.c_float
+    L.mrt_rsqrt_nr.argtypes = [C.c_float]
+    L.mrt_rsqrt_nr.restype = C.c_float
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    """Raise MRTError for a negative status, return rc otherwise."""
+    if rc < 0:
+        msg = load().mrt_last_error().decode(errors="replace")
+        raise MRTError(f"{what}: {ERRORS.get(rc, rc)}: {msg}")
+    return rc
+
+
+def f3(v):
+    return (C.c_float * 3)(*[float(x) for x in v])

@@ -1,0 +1,291 @@
+"""Deterministic synthetic stand-ins for the BASELINE scenes whose assets are
+missing from the reference snapshot (.MISSING_LARGE_BLOBS: sponza.obj,
+bunny.obj, dragon_2.obj, buddha_smooth.obj), plus the config presets C1..C3
+(SURVEY.md §8(d)).  Camera and light parameters are the reference scripts':
+  C1 Cornell   : src/assignment2.h:457-460 (camera), PointLight (2.75, 5, -2.75)
+  C2 bunny     : src/assignment2.h:89-118  (eye (0,5,15), PointLight (10,20,10) 1000)
+  C3 Sponza    : src/assignment2.h:354-373 (eye (8,1.5,1) -> (0,2.5,-1), fov 55,
+                 PointLight (0,10,0) 200, Blinn kd = 1)
+Meshes are written as OBJ text (v / vn / f lines < 80 chars) and go through
+libmrt's OBJ loader like real assets would.  Every vertex carries a small
+seeded jitter so no >=128-triangle group shares a centroid coordinate (the
+reference's binning divides by the centroid extent, src/BVH.cpp:714).
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+
+import numpy as np
+
+SCENE_VERSION = 1
+
+
+def _cache_dir():
+    d = os.environ.get("MRT_SCENE_CACHE", os.path.join("/tmp", "mrt_scenes"))
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def write_obj(path, verts, faces, normals=None):
+    """faces: (n,3) 0-based.  With normals: one normal per vertex (f a//a ...)."""
+    verts = np.asarray(verts, np.float64)
+    faces = np.asarray(faces, np.int64) + 1
+    lines = ["# synthetic scene (rendering-algorithms-raytracer_amd/miro/scenes.py)"]
+    lines += ["v %.6f %.6f %.6f" % tuple(v) for v in verts]
+    if normals is not None:
+        lines += ["vn %.6f %.6f %.6f" % tuple(n) for n in np.asarray(normals, np.float64)]
+        lines += ["f %d//%d %d//%d %d//%d" % (a, a, b, b, c, c) for a, b, c in faces]
+    else:
+        lines += ["f %d %d %d" % tuple(f) for f in faces]
+    tmp = path + ".tmp%d" % os.getpid()
+    with open(tmp, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    os.replace(tmp, path)
+    return path
+
+
+class _Mesh:
+    def __init__(self):
+        self.v, self.f = [], []
+        self.nv = 0
+
+    def add(self, verts, faces):
+        verts = np.asarray(verts, np.float64).reshape(-1, 3)
+        self.v.append(verts)
+        self.f.append(np.asarray(faces, np.int64).reshape(-1, 3) + self.nv)
+        self.nv += len(verts)
+
+    def grid(self, origin, du, dv, nu, nv_):
+        """Quad grid spanning origin + s*du + t*dv, s,t in [0,1]; 2*nu*nv tris."""
+        s = np.linspace(0, 1, nu + 1)
+        t = np.linspace(0, 1, nv_ + 1)
+        S, T = np.meshgrid(s, t, indexing="ij")
+        P = np.asarray(origin) + S[..., None] * np.asarray(du) + T[..., None] * np.asarray(dv)
+        idx = np.arange((nu + 1) * (nv_ + 1)).reshape(nu + 1, nv_ + 1)
+        a, b, c, d = idx[:-1, :-1], idx[1:, :-1], idx[1:, 1:], idx[:-1, 1:]
+        f = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3), np.stack([a, c, d], -1).reshape(-1, 3)])
+        self.add(P.reshape(-1, 3), f)
+
+    def box(self, lo, hi, n=(1, 1, 1)):
+        lo, hi = np.asarray(lo, float), np.asarray(hi, float)
+        ex = hi - lo
+        X, Y, Z = np.eye(3) * ex
+        nx, ny, nz = n
+        self.grid(lo, X, Z, nx, nz)                 # bottom
+        self.grid(lo + Y, Z, X, nz, nx)             # top
+        self.grid(lo, Y, X, ny, nx)                 # front (z = lo)
+        self.grid(lo + Z, X, Y, nx, ny)             # back
+        self.grid(lo, Z, Y, nz, ny)                 # left
+        self.grid(lo + X, Y, Z, ny, nz)             # right
+
+    def cylinder(self, center, r, y0, y1, seg, rings):
+        th = np.linspace(0, 2 * np.pi, seg, endpoint=False)
+        ys = np.linspace(y0, y1, rings + 1)
+        P = np.stack([center[0] + r * np.cos(th)[None, :].repeat(rings + 1, 0),
+                      ys[:, None].repeat(seg, 1),
+                      center[1] + r * np.sin(th)[None, :].repeat(rings + 1, 0)], -1).reshape(-1, 3)
+        idx = np.arange((rings + 1) * seg).reshape(rings + 1, seg)
+        a, b = idx[:-1], np.roll(idx[:-1], -1, axis=1)
+        c, d = np.roll(idx[1:], -1, axis=1), idx[1:]
+        f = np.concatenate([np.stack([a, c, b], -1).reshape(-1, 3), np.stack([a, d, c], -1).reshape(-1, 3)])
+        self.add(P, f)
+
+    def arch(self, x0, x1, y_base, z0, z1, thick, seg):
+        """Semicircular arch band between x0 and x1 (extruded along z)."""
+        cx, R = 0.5 * (x0 + x1), 0.5 * (x1 - x0)
+        th = np.linspace(np.pi, 0, seg + 1)
+        ring = []
+        for rad in (R, R + thick):
+            for z in (z0, z1):
+                ring.append(np.stack([cx + rad * np.cos(th), y_base + rad * np.sin(th), np.full_like(th, z)], -1))
+        # ring order: inner-z0, inner-z1, outer-z0, outer-z1
+        base = self.nv
+        P = np.concatenate(ring)
+        n = seg + 1
+        f = []
+        for (p, q) in ((0, 1), (3, 2), (2, 0), (1, 3)):   # inner, outer, face z0, face z1
+            i = np.arange(seg)
+            a, b = p * n + i, p * n + i + 1
+            c, d = q * n + i + 1, q * n + i
+            f.append(np.stack([a, b, c], -1))
+            f.append(np.stack([a, c, d], -1))
+        self.v.append(P)
+        self.f.append(np.concatenate(f) + base)
+        self.nv += len(P)
+
+    def arrays(self):
+        return np.concatenate(self.v), np.concatenate(self.f)
+
+
+def _jitter(verts, seed, amp):
+    rng = np.random.default_rng(seed)
+    return verts + rng.uniform(-amp, amp, size=verts.shape)
+
+
+def sponza_standin(detail=1.0):
+    """Closed-wall atrium with two storeys of colonnades, arches, gallery slabs and
+    hanging banners (~66 k triangles at detail=1).  Units and extent follow the
+    Sponza camera of src/assignment2.h:357-368."""
+    m = _Mesh()
+    k = lambda n: max(1, int(round(n * detail)))
+    # floor and outer walls
+    m.grid((-15, 0, -7), (30, 0, 0), (0, 0, 14), k(118), k(56))
+    m.grid((-15, 0, -7), (0, 13, 0), (30, 0, 0), k(26), k(60))
+    m.grid((-15, 0, 7), (30, 0, 0), (0, 13, 0), k(60), k(26))
+    m.grid((-15, 0, -7), (0, 0, 14), (0, 13, 0), k(28), k(26))
+    m.grid((15, 0, -7), (0, 13, 0), (0, 0, 14), k(26), k(28))
+    for side in (-1, 1):
+        zc = 4.0 * side
+        # ground-floor colonnade + arches
+        xs = -12.5 + 2.5 * np.arange(11)
+        for x in xs:
+            m.cylinder((x, zc), 0.32, 0.35, 4.2, k(20), k(12))
+            m.box((x - 0.45, 0.0, zc - 0.45), (x + 0.45, 0.35, zc + 0.45))
+            m.box((x - 0.45, 4.2, zc - 0.45), (x + 0.45, 4.5, zc + 0.45))
+        for x0, x1 in zip(xs[:-1], xs[1:]):
+            m.arch(x0 + 0.3, x1 - 0.3, 4.5, zc - 0.3, zc + 0.3, 0.3, k(24))
+        # gallery slab over the aisle
+        zlo, zhi = (4.3, 7.0) if side > 0 else (-7.0, -4.3)
+        m.box((-15, 5.6, zlo), (15, 5.9, zhi), (k(60), 1, k(6)))
+        # upper colonnade + arches
+        xs2 = -13.0 + 2.0 * np.arange(14)
+        for x in xs2:
+            m.cylinder((x, zc), 0.22, 5.9, 9.2, k(16), k(12))
+        for x0, x1 in zip(xs2[:-1], xs2[1:]):
+            m.arch(x0 + 0.2, x1 - 0.2, 9.2, zc - 0.2, zc + 0.2, 0.25, k(20))
+        # banners hanging from the gallery edge (wavy sheets)
+        for j, x in enumerate((-9.0, -3.0, 3.0, 9.0)):
+            nu, nvv = k(20), k(40)
+            s = np.linspace(0, 1, nu + 1)
+            t = np.linspace(0, 1, nvv + 1)
+            S, T = np.meshgrid(s, t, indexing="ij")
+            X = x - 0.8 + 1.6 * S
+            Y = 9.0 - 6.5 * T
+            Z = zc - 0.5 * side + 0.25 * np.sin(6.0 * S + 3.0 * T + j) * T
+            P = np.stack([X, Y, Z], -1).reshape(-1, 3)
+            idx = np.arange((nu + 1) * (nvv + 1)).reshape(nu + 1, nvv + 1)
+            a, b, c, d = idx[:-1, :-1], idx[1:, :-1], idx[1:, 1:], idx[:-1, 1:]
+            f = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3), np.stack([a, c, d], -1).reshape(-1, 3)])
+            m.add(P, f)
+    v, f = m.arrays()
+    v = _jitter(v, 20110601, 1e-3)
+    return v, f
+
+
+def bunny_standin(nu=250, nv=140, radius=3.0):
+    """Seeded displaced sphere standing in for bunny.obj (~69.5 k tris, smooth normals)."""
+    th = np.linspace(0, np.pi, nv + 1)[1:-1]
+    ph = np.linspace(0, 2 * np.pi, nu, endpoint=False)
+    T, Ph = np.meshgrid(th, ph, indexing="ij")
+    dirs = np.stack([np.sin(T) * np.cos(Ph), np.cos(T), np.sin(T) * np.sin(Ph)], -1)
+    rng = np.random.default_rng(1994)
+    freq = rng.uniform(1.5, 5.0, (6, 3))
+    phase = rng.uniform(0, 2 * np.pi, 6)
+    disp = sum(0.035 * np.sin(dirs @ freq[i] * 2.0 + phase[i]) for i in range(6))
+    Rr = radius * (1.0 + disp)
+    P = dirs * Rr[..., None] + np.array([0.0, radius + 0.05, 0.0])
+    P = P.reshape(-1, 3)
+    top = np.array([[0.0, 2 * radius + 0.05, 0.0]])
+    bot = np.array([[0.0, 0.05, 0.0]])
+    V = np.concatenate([P, top, bot])
+    ring = lambda r: r * nu + np.arange(nu)
+    f = []
+    for r in range(nv - 2):
+        a, b = ring(r), ring(r) + 1 - nu * ((np.arange(nu) + 1) // nu)
+        c, d = ring(r + 1) + 1 - nu * ((np.arange(nu) + 1) // nu), ring(r + 1)
+        f.append(np.stack([a, b, c], -1))
+        f.append(np.stack([a, c, d], -1))
+    it, ib = len(P), len(P) + 1
+    r0 = ring(0)
+    f.append(np.stack([np.full(nu, it), r0 - nu * 0 + 0, np.roll(r0, -1)], -1)[:, [0, 2, 1]])
+    rl = ring(nv - 2)
+    f.append(np.stack([np.full(nu, ib), rl, np.roll(rl, -1)], -1))
+    F = np.concatenate(f)
+    # smooth normals: area-weighted vertex normals
+    e1 = V[F[:, 1]] - V[F[:, 0]]
+    e2 = V[F[:, 2]] - V[F[:, 0]]
+    fn = np.cross(e1, e2)
+    N = np.zeros_like(V)
+    for k in range(3):
+        np.add.at(N, F[:, k], fn)
+    N /= np.linalg.norm(N, axis=1, keepdims=True)
+    V = _jitter(V, 1994, 1e-4)
+    return V, F, N
+
+
+def _cached(name, builder):
+    key = hashlib.sha1(f"{name}-{SCENE_VERSION}".encode()).hexdigest()[:10]
+    path = os.path.join(_cache_dir(), f"{name}-{key}.obj")
+    if not os.path.exists(path):
+        out = builder()
+        if len(out) == 3:
+            write_obj(path, out[0], out[1], out[2])
+        else:
+            write_obj(path, out[0], out[1])
+    return path
+
+
+def sponza_obj():
+    return _cached("sponza_standin", sponza_standin)
+
+
+def bunny_obj():
+    return _cached("bunny_standin", bunny_standin)
+
+
+# ---------------------------------------------------------------- presets
+CONFIGS = {
+    # C1: cornell_box.obj 256x256, 1 spp, Lambert + 1 PointLight (plumbing)
+    "C1": dict(name="cornell_box.obj 256x256 Lambert+PointLight", W=256, H=256,
+               camera=dict(eye=(2.75, 2.75, 5.0), lookAt=(2.75, 2.75, 0.0), up=(0, 1, 0), fov=55.0),
+               lights=[dict(type="point", pos=(2.75, 5.0, -2.75), power=40.0)],
+               material=dict(kind="lambert", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="cornell"),
+    # C2: bunny stand-in 1024x1024, Blinn kd=1, PointLight (10,20,10) 1000, floor triangle
+    "C2": dict(name="bunny stand-in (69.5k tris) 1024x1024 Blinn+PointLight", W=1024, H=1024,
+               camera=dict(eye=(0.0, 5.0, 15.0), lookAt=(0.0, 0.0, 0.0), up=(0, 1, 0), fov=45.0),
+               lights=[dict(type="point", pos=(10.0, 20.0, 10.0), power=1000.0)],
+               material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="bunny"),
+    # C3: Sponza stand-in 1920x1080, Blinn kd=1, PointLight (0,10,0) 200
+    "C3": dict(name="sponza stand-in (~66k tris) 1920x1080 Blinn+PointLight", W=1920, H=1080,
+               camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
+               lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
+               material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza"),
+}
+
+
+def build_config(key, device=0):
+    """Product-side scene for a config preset -> (miro.Scene, miro.Camera, cfg).
+    C1 needs the Cornell mesh fixture path in MRT_CORNELL_NPZ (or tests/golden)."""
+    import miro
+
+    cfg = CONFIGS[key]
+    scene = miro.Scene(device=device)
+    mat = cfg["material"]
+    material = miro.Lambert(mat["kd"]) if mat["kind"] == "lambert" else miro.Blinn(mat["kd"])
+    mesh = miro.TriangleMesh()
+    if cfg["mesh"] == "cornell":
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        npz = os.environ.get("MRT_CORNELL_NPZ", os.path.join(root, "tests", "golden", "cornell_box_mesh.npz"))
+        f = np.load(npz)
+        mesh.setArrays(f["verts"], f["normals"], f["vidx"], f["nidx"])
+    else:
+        mesh.load(sponza_obj() if cfg["mesh"] == "sponza" else bunny_obj())
+    miro.makeMeshObjs(scene, mesh, material)
+    if cfg["mesh"] == "bunny":  # floor triangle, src/assignment2.h:110-124
+        fl = miro.TriangleMesh()
+        fl.createSingleTriangle()
+        fl.setV1((-100, 0, -100)); fl.setV2((0, 0, 100)); fl.setV3((100, 0, -100))
+        fl.setN1((0, 1, 0)); fl.setN2((0, 1, 0)); fl.setN3((0, 1, 0))
+        miro.makeMeshObjs(scene, fl, material)
+    for l in cfg["lights"]:
+        pl = miro.PointLight()
+        pl.setPosition(l["pos"])
+        pl.setPower(l["power"])
+        scene.addLight(pl)
+    scene.setBGColor(cfg["bg"])
+    scene.preCalc()
+    cam = miro.Camera()
+    c = cfg["camera"]
+    cam.setEye(c["eye"]); cam.setLookAt(c["lookAt"]); cam.setUp(c["up"]); cam.setFOV(c["fov"])
+    return scene, cam, cfg

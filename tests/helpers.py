@@ -1,0 +1,80 @@
+"""Shared scene builders for tests: the same scene description fed to the
+product (miro / libmrt.so) and to the CPU oracle."""
+import os
+
+import numpy as np
+
+import miro
+import oracle as O
+from miro import scenes
+
+from conftest import GOLDEN
+
+
+def fixture_mesh(name):
+    f = np.load(os.path.join(GOLDEN, f"{name}_mesh.npz"))
+    return f["verts"], f["normals"], f["vidx"], f["nidx"]
+
+
+def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1):
+    """Build (miro.Scene, OracleScene, camera dict) for a config dict."""
+    lights = cfg["lights"] if lights is None else lights
+    mat = cfg["material"]
+    P = miro.Scene()
+    pm = miro.Lambert(mat["kd"]) if mat["kind"] == "lambert" else miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0),
+                                                                           specAmt=mat.get("specAmt", 0.0))
+    O_ = O.OracleScene()
+    om = O_.add_material(mat["kind"], kd=mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0))
+    for arrs in (meshes or []):
+        tm = miro.TriangleMesh()
+        tm.setArrays(*arrs)
+        miro.makeMeshObjs(P, tm, pm)
+        O_.add_mesh(*arrs, om)
+    if obj is not None:
+        tm = miro.TriangleMesh()
+        tm.load(obj)
+        miro.makeMeshObjs(P, tm, pm)
+        O_.add_obj(obj, om)
+    if floor:
+        fl = miro.TriangleMesh()
+        fl.createSingleTriangle()
+        fl.setV1((-100, 0, -100)); fl.setV2((0, 0, 100)); fl.setV3((100, 0, -100))
+        fl.setN1((0, 1, 0)); fl.setN2((0, 1, 0)); fl.setN3((0, 1, 0))
+        miro.makeMeshObjs(P, fl, pm)
+        O_.add_mesh(fl.verts, fl.normals, fl.vidx, fl.nidx, om)
+    for l in lights:
+        if l["type"] == "point":
+            pl = miro.PointLight(); pl.setPosition(l["pos"]); pl.setPower(l["power"])
+            P.addLight(pl)
+            O_.add_point_light(l["pos"], l["power"])
+        else:
+            rl = miro.RectangleLight(); rl.setVertices(l["v1"], l["v2"], l["v3"]); rl.setPower(l["power"])
+            rl.setSamples(l.get("samples", 1)); rl.setNoiseThreshold(l.get("noise", 0.001))
+            P.addLight(rl)
+            O_.add_rect_light(l["v1"], l["v2"], l["v3"], l["power"], l.get("samples", 1), l.get("noise", 0.001))
+    P.setBGColor(cfg["bg"])
+    O_.set_bg(cfg["bg"])
+    P.setNumPaths(num_paths)
+    O_.set_num_paths(num_paths)
+    P.preCalc()
+    O_.build()
+    return P, O_, cfg["camera"]
+
+
+def camera(c):
+    cam = miro.Camera()
+    cam.setEye(c["eye"]); cam.setLookAt(c["lookAt"]); cam.setUp(c.get("up", (0, 1, 0))); cam.setFOV(c["fov"])
+    return cam
+
+
+def config_scene(key, **kw):
+    cfg = scenes.CONFIGS[key]
+    if cfg["mesh"] == "cornell":
+        return scene_pair(cfg, meshes=[fixture_mesh("cornell_box")], **kw)
+    if cfg["mesh"] == "bunny":
+        return scene_pair(cfg, obj=scenes.bunny_obj(), floor=True, **kw)
+    return scene_pair(cfg, obj=scenes.sponza_obj(), **kw)
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)

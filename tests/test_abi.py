@@ -1,0 +1,32 @@
+"""The C-ABI library loads and exports every symbol include/mrt.h declares
+(no compute calls: this runs on hosts without a GPU)."""
+import ctypes
+import os
+import re
+
+import miro
+from conftest import ROOT
+from miro import _lib
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "mrt.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mrt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = miro.lib()
+    missing = [s for s in declared_symbols() if not hasattr(L, s)]
+    assert not missing, missing
+    assert L.mrt_abi_version() == 1
+
+
+def test_errors_are_reported_not_raised():
+    L = miro.lib()
+    assert L.mrt_scene_build_bvh(None) == -1          # MRT_ERR_INVALID, no exception
+    assert b"null" in L.mrt_last_error()
