@@ -86,6 +86,13 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise MRTError(f"libmrt.so not built at {LIB_PATH}; run __graft_entry__.build() "
                        f"(make -C rendering-algorithms-raytracer_amd)")
+    # One HIP runtime per process: if PyTorch-ROCm is importable, load it first so
+    # libmrt's libamdhip64.so.7 resolves to the runtime torch already mapped
+    # (torch ships its own copy; two HIP/HSA runtimes cannot share the device).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     L = C.CDLL(LIB_PATH)
     L.mrt_last_error.restype = C.c_char_p
     L.mrt_scene_create.restype = C.c_void_p
