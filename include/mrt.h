@@ -105,6 +105,8 @@ typedef struct {
     uint64_t node_visits, leaf_visits;   /* all rays; valid when count_visits was set   */
     uint64_t primary_node_visits, primary_leaf_visits; /* primary-ray launch share     */
     uint64_t primary_hits;               /* primary rays that hit geometry               */
+    uint64_t primary_wave_steps;         /* count mode: sum over tiles of the max node
+                                            visits of a lane (x64 = issued lane-steps)   */
     float kernel_ms;                     /* device time of the last frame (all launches)*/
     float primary_ms, shade_ms;          /* per launch: primary rays / shade + shadows  */
     int32_t max_stack;                   /* deepest traversal stack seen (count mode)   */
@@ -184,6 +186,14 @@ int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const floa
 
 /* Counters of the last render on this scene (ray counts, visits, kernel time). */
 int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
+
+/* Performance A/B switches (no effect on results; defaults in brackets):
+ * "fast_box" 0/[1] (hardware min/max slab test when its finiteness precondition
+ * holds), "primary_waves" 0/[6] (occupancy target of the primary-ray kernel),
+ * "xcd_map" [0]/1 (XCD-banded tile schedule), "shade1" 0/[1] (specialised shading
+ * kernel for one point light and one path), "lds_pad_kb" [0]..128 (extra LDS per
+ * workgroup, lowers occupancy for sweeps).  Process-wide. */
+int mrt_set_tuning(const char* key, int value);
 
 /* Numerics probes (x86 RCPSS/RSQRTSS emulation + one Newton step, SSE.h:67-101). */
 float mrt_rcp_nr(float x);

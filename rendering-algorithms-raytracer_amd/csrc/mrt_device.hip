@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -34,7 +35,8 @@ void set_error(const std::string& m) { g_err = m; }
         }                                                                               \
     } while (0)
 
-enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLOW = 4, CTR_NODES_P = 5, CTR_LEAVES_P = 6, CTR_HITS = 7, CTR_N = 8 };
+enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLOW = 4, CTR_NODES_P = 5, CTR_LEAVES_P = 6, CTR_HITS = 7,
+       CTR_WAVE_STEPS_P = 8, CTR_N = 16 };
 
 struct RenderParams {
     const QNode* nodes;
@@ -53,6 +55,8 @@ struct RenderParams {
     float bg[3];
     int32_t n_lights, num_paths;
     uint32_t seed;
+    int32_t fast_box;            // node boxes finite && tuning allows the hardware min/max box test
+    int32_t xcd_map;             // 1: workgroups on one XCD take one contiguous band of tiles
     // work: 8x8 tiles
     int32_t tiles_x, n_tiles;    // frame mode: tiles_x = ceil(W/8)
     const int32_t* buckets;      // bucket mode: bucket ids (row-major bucket grid)
@@ -61,9 +65,9 @@ struct RenderParams {
     float* out_rgb;              // frame: W*H*3; buckets: n_buckets*1024*3
     uint8_t* out_rgb8;           // same slots as out_rgb (nullable)
     float4* hits;                // per slot: t, a, b, prim bits (kernel 1 -> kernel 2)
-    float4* dirs;                // per slot: primary direction
 };
 
+template <bool POINT_ONLY, bool FAST>
 struct Shader {
     const RenderParams& P;
     const Trav& T;
@@ -80,7 +84,7 @@ struct Shader {
         DRay r = make_ray(from, L);
         DHit h{tMax, 0.f, 0.f, -1};
         shadow_rays++;
-        return traverse<true, COUNT>(T, r, 0.001f, h, st);
+        return traverse<true, COUNT, FAST>(T, r, 0.001f, h, st);
     }
 
     // PointLight::sampleLight, src/PointLight.cpp:8-81
@@ -95,11 +99,15 @@ struct Shader {
         float distance = rcp_nr(distanceRecip, rcpT);
         L = scale(L, distanceRecip);
         nDotL *= distanceRecip;
+        // Everything the light returns except the shadow bit is formed before the
+        // shadow ray, so only three scalars stay live across its traversal.
+        const float A = (l.power * falloff) * (0.25f / 3.1415926f);
+        const float rdl = std_max(0.f, dot(rVec, L));
         float attenuate = 1.0f;
         if (l.cast_shadows && occluded<COUNT>(from, L, distance)) attenuate = 0.0f;
         attenuate *= nDotL;
-        outSpec = std_max(0.f, dot(rVec, L)) * attenuate;
-        return ((l.power * falloff) * (0.25f / 3.1415926f)) * attenuate;
+        outSpec = rdl * attenuate;
+        return A * attenuate;
     }
 
     // RectangleLight::sampleLight, src/RectangleLight.cpp:42-136 (fast shadows)
@@ -143,11 +151,12 @@ struct Shader {
     template <bool COUNT>
     __device__ v3 sample_light(int li, v3 from, v3 normal, v3 rVec, float& spec) {
         const DevLight& l = P.lights[li];
-        if (l.type == MRT_POINT_LIGHT) {
+        if (POINT_ONLY || l.type == MRT_POINT_LIGHT) {
             float e = point_light<COUNT>(l, from, normal, rVec, spec);
             return mk(e, e, e);
         }
-        return rect_light<COUNT>(l, from, normal, rVec, spec);
+        if constexpr (!POINT_ONLY) return rect_light<COUNT>(l, from, normal, rVec, spec);
+        return mk(0, 0, 0);
     }
 
     // HitInfo::getAllInfos (normals), src/Ray.cpp:5-49
@@ -213,6 +222,29 @@ struct Shader {
 
 __device__ __forceinline__ uint8_t map8(const uint8_t* lut, float v) { return lut[map_index(v)]; }
 
+// Tile schedule of a persistent workgroup.  xcd_map = 0: grid-stride over all
+// tiles.  xcd_map = 1 (grid a multiple of 8): workgroups b, b+8, ... -- observed
+// to share one XCD and its L2 (placement is a speed hint only, never needed for
+// correctness) -- walk one contiguous eighth of the tiles, so each XCD's L2
+// holds the part of the BVH its image band touches.
+struct TileIter {
+    int cur, step, end;
+    __device__ TileIter(const RenderParams& P, int wave) {
+        if (P.xcd_map && (gridDim.x & 7) == 0) {
+            int xcd = blockIdx.x & 7, local = blockIdx.x >> 3, per = gridDim.x >> 3;
+            int band = (P.n_tiles + 7) >> 3;
+            int beg = xcd * band;
+            end = min(P.n_tiles, beg + band);
+            cur = beg + local * 4 + wave;
+            step = per * 4;
+        } else {
+            cur = blockIdx.x * 4 + wave;
+            step = gridDim.x * 4;
+            end = P.n_tiles;
+        }
+    }
+};
+
 // work item (8x8 tile) + lane -> pixel (x, y) and output slot
 __device__ __forceinline__ bool item_pixel(const RenderParams& P, int item, int lane, int& x, int& y, size_t& slot) {
     if (P.mode == 0) {
@@ -264,45 +296,61 @@ __device__ __forceinline__ void flush_stats(const RenderParams& P, const TravSta
     if (st.overflow) atomicOr(&P.ctr[CTR_OVERFLOW], 1ull);
 }
 
+// Camera::eyeRayAdaptive(x, y, .5, .5, .5, .5) (src/Camera.cpp:116-157): two
+// jitter draws (dims 0, 1; the offsets are exactly 0.5) and the time draw (dim 2,
+// unused).  Deterministic, so kernel 2 recomputes it instead of storing it.
+__device__ __forceinline__ v3 camera_dir(const RenderParams& P, int x, int y, const uint16_t* rsqT) {
+    const CamParams& cam = P.cam;
+    const uint32_t pixel = (uint32_t)(y * cam.W + x);
+    float ur = rng(pixel, 0, 0, P.seed), vr = rng(pixel, 0, 1, P.seed);
+    float xo = (0.5f - 0.5f) * ur + 0.5f, yo = (0.5f - 0.5f) * vr + 0.5f;
+    float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
+    float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
+    v3 U = mk(cam.u[0], cam.u[1], cam.u[2]), Vv = mk(cam.v[0], cam.v[1], cam.v[2]), W = mk(cam.w[0], cam.w[1], cam.w[2]);
+    return normalized(sub(add(scale(U, Up), scale(Vv, Vp)), W), rsqT);
+}
+
 // Kernel 1: Camera::eyeRayAdaptive + closest-hit BVH::intersect per pixel.
 // Writes the HitInfo record (t, a, b, prim) to P.hits[slot].
-template <bool COUNT>
-__global__ void __launch_bounds__(kWG) primary_kernel(RenderParams P) {
+template <bool COUNT, int MINW, bool FAST>
+__global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[kTableWords];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     load_tables(P.tables, s_tab, kTableWords / 2);
     const uint16_t* rcpT = s_tab;
     const uint16_t* rsqT = s_tab + 2048;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    Trav T{P.nodes, P.fast_box != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
     uint32_t nhits = 0;
     const CamParams& cam = P.cam;
-    const v3 U = mk(cam.u[0], cam.u[1], cam.u[2]), Vv = mk(cam.v[0], cam.v[1], cam.v[2]),
-             W = mk(cam.w[0], cam.w[1], cam.w[2]), eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
-    for (int item = blockIdx.x * 4 + wave; item < P.n_tiles; item += gridDim.x * 4) {
+    const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
+    unsigned long long wave_steps = 0;  // count mode: sum over tiles of max lane node visits
+    TileIter it(P, wave);
+    for (int item = it.cur; item < it.end; item += it.step) {
         int x, y;
         size_t slot;
-        if (!item_pixel(P, item, lane, x, y, slot)) continue;
-        const uint32_t pixel = (uint32_t)(y * cam.W + x);
-        // eyeRayAdaptive(x, y, .5, .5, .5, .5): two jitter draws + one time draw (dims 0..2)
-        float ur = rng(pixel, 0, 0, P.seed), vr = rng(pixel, 0, 1, P.seed);
-        float xo = (0.5f - 0.5f) * ur + 0.5f, yo = (0.5f - 0.5f) * vr + 0.5f;
-        float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
-        float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
-        v3 dir = normalized(sub(add(scale(U, Up), scale(Vv, Vp)), W), rsqT);
-        DRay r = make_ray(eye, dir);
-        DHit h{1e12f, 0.f, 0.f, -1};
-        if (!traverse<false, COUNT>(T, r, 0.001f, h, st)) h.prim = -1;
-        else nhits++;
-        P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(h.prim));
-        P.dirs[slot] = make_float4(dir.x, dir.y, dir.z, 0.f);
+        const uint32_t n0 = st.nodes;
+        if (item_pixel(P, item, lane, x, y, slot)) {
+            DRay r = make_ray(eye, camera_dir(P, x, y, rsqT));
+            DHit h{1e12f, 0.f, 0.f, -1};
+            if (!traverse<false, COUNT, FAST>(T, r, 0.001f, h, st)) h.prim = -1;
+            item_pixel(P, item, lane, x, y, slot);  // recompute: keeps it out of the traversal's live set
+            P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(h.prim));
+            nhits += h.prim >= 0 ? 1u : 0u;  // wave-reduced in flush_stats
+        }
+        if (COUNT) {
+            uint32_t dmax = st.nodes - n0;
+            for (int off = 32; off > 0; off >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, off));
+            wave_steps += dmax;
+        }
     }
+    if (COUNT && lane == 0) atomicAdd(&P.ctr[CTR_WAVE_STEPS_P], wave_steps);
     flush_stats<COUNT, true>(P, st, nhits, lane);
 }
 
 // Kernel 2: Scene::sampleScene shading of the primary hit with shadow rays.
-template <bool COUNT>
+template <bool COUNT, bool POINT_ONLY, bool FAST>
 __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[kTableWords];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -310,12 +358,13 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     const uint16_t* rcpT = s_tab;
     const uint16_t* rsqT = s_tab + 2048;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    Trav T{P.nodes, P.fast_box != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
     uint32_t shadow_total = 0;
     const CamParams& cam = P.cam;
     const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
-    for (int item = blockIdx.x * 4 + wave; item < P.n_tiles; item += gridDim.x * 4) {
+    TileIter it(P, wave);
+    for (int item = it.cur; item < it.end; item += it.step) {
         int x, y;
         size_t slot;
         if (!item_pixel(P, item, lane, x, y, slot)) continue;
@@ -323,10 +372,9 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
         DHit h{hv.x, hv.y, hv.z, __float_as_int(hv.w)};
         v3 col;
         if (h.prim >= 0) {
-            float4 dv = P.dirs[slot];
-            DRay r = make_ray(eye, mk(dv.x, dv.y, dv.z));
-            Shader S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u};
-            col = S.shade<COUNT>(r, h);
+            DRay r = make_ray(eye, camera_dir(P, x, y, rsqT));
+            Shader<POINT_ONLY, FAST> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u};
+            col = S.template shade<COUNT>(r, h);
             shadow_total += S.shadow_rays;
         } else {
             col = mk(P.bg[0], P.bg[1], P.bg[2]);
@@ -341,24 +389,128 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     flush_stats<COUNT>(P, st, shadow_total, lane);
 }
 
+
+// Kernel 2, specialised for one point light and num_paths == 1 (the BASELINE
+// configs C1-C3): straight-line PointLight::sampleLight + Lambert/Blinn with only
+// the light's three pre-shadow scalars live across the any-hit traversal.
+// Same operations in the same order as Shader::shade.
+template <bool COUNT, bool FAST>
+__global__ void __launch_bounds__(kWG, 6) shade1_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[kTableWords];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    load_tables(P.tables, s_tab, kTableWords / 2);
+    const uint16_t* rcpT = s_tab;
+    const uint16_t* rsqT = s_tab + 2048;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    Trav T{P.nodes, P.fast_box != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    TravStats st;
+    uint32_t shadow_total = 0;
+    const v3 eye = mk(P.cam.eye[0], P.cam.eye[1], P.cam.eye[2]);
+    TileIter it(P, wave);
+    for (int item = it.cur; item < it.end; item += it.step) {
+        int x, y;
+        size_t slot;
+        if (!item_pixel(P, item, lane, x, y, slot)) continue;
+        const float4 hv = P.hits[slot];
+        const int prim = __float_as_int(hv.w);
+        v3 col = mk(P.bg[0], P.bg[1], P.bg[2]);
+        if (prim >= 0) {
+            // HitInfo::getAllInfos + Ray::getPoint
+            const v3 rayD = camera_dir(P, x, y, rsqT);
+            const DRay r = make_ray(eye, rayD);
+            const PrimShade ps = P.prims[prim];
+            const uint32_t mi = ps.mat;
+            const bool lambert = P.mats[mi].type == MRT_LAMBERT;
+            const float4 A = P.verts[ps.v[0]], B = P.verts[ps.v[1]], C = P.verts[ps.v[2]];
+            const v3 geoN = normalized(cross(mk(B.x - A.x, B.y - A.y, B.z - A.z), mk(C.x - A.x, C.y - A.y, C.z - A.z)), rsqT);
+            const float c = 1.0f - hv.y - hv.z;
+            const float4 n0 = P.normals[ps.n[0]], n1 = P.normals[ps.n[1]], n2 = P.normals[ps.n[2]];
+            const v3 N = normalized(add(add(scale(mk(n0.x, n0.y, n0.z), c), scale(mk(n1.x, n1.y, n1.z), hv.y)),
+                                        scale(mk(n2.x, n2.y, n2.z), hv.z)), rsqT);
+            const v3 from = mk(r.o[0] + hv.x * r.d[0], r.o[1] + hv.x * r.d[1], r.o[2] + hv.x * r.d[2]);
+            // Lambert::shade uses the shading normal and no reflection vector;
+            // Blinn::shade flips to the viewer's side (src/Blinn.cpp:150-170).
+            v3 n = N, rVec = mk(0, 0, 0);
+            if (!lambert) {
+                const v3 viewDir = neg(rayD);
+                float vDotN = dot(viewDir, N);
+                const float vDotGeoN = dot(viewDir, geoN);
+                const bool same = (vDotN * vDotGeoN) >= 0.0f;
+                n = same ? N : geoN;
+                vDotN = same ? vDotN : vDotGeoN;
+                if (vDotN < 0.0f) { vDotN = -vDotN; n = neg(n); }
+                rVec = add(rayD, scale(n, 2.0f * vDotN));
+            }
+            // PointLight::sampleLight (src/PointLight.cpp:8-81), as Shader::point_light
+            const DevLight& l = P.lights[0];
+            v3 L = sub(mk(l.pos[0], l.pos[1], l.pos[2]), from);
+            float nDotL = dot(n, L);
+            float e = 0.f, spec = 0.f;
+            if (nDotL > 0.0f) {
+                float falloff = dot(L, L);
+                const float distanceRecip = rsqrt_nr(falloff, rsqT);
+                falloff = rcp_nr(falloff, rcpT);
+                const float distance = rcp_nr(distanceRecip, rcpT);
+                L = scale(L, distanceRecip);
+                nDotL *= distanceRecip;
+                const float Aterm = (l.power * falloff) * (0.25f / 3.1415926f);
+                const float rdl = std_max(0.f, dot(rVec, L));
+                float attenuate = 1.0f;
+                if (l.cast_shadows) {
+                    const DRay sr = make_ray(from, L);
+                    DHit sh{distance, 0.f, 0.f, -1};
+                    shadow_total++;
+                    if (traverse<true, COUNT, FAST>(T, sr, 0.001f, sh, st)) attenuate = 0.0f;
+                }
+                attenuate *= nDotL;
+                spec = rdl * attenuate;
+                e = Aterm * attenuate;
+            }
+            const DevMaterial& M = P.mats[mi];
+            const v3 E = mk(e, e, e);
+            const v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+            v3 sh;
+            if (lambert) {
+                sh = add(add(mk(0, 0, 0), mul(E, kd)), ka);
+            } else {
+                const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
+                const float pw = (M.spec_exp == 1.0f) ? spec : powf(spec, M.spec_exp);
+                const v3 Ls = add(mk(0, 0, 0), scale(scale(mul(E, ks), M.spec_amt), pw));
+                const v3 Ld = add(add(mk(0, 0, 0), mul(E, kd)), ka);
+                const v3 z = mk(0, 0, 0);
+                sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), z);
+            }
+            col = scale(add(mk(0, 0, 0), sh), 1.0f / (float)P.num_paths);
+        }
+        item_pixel(P, item, lane, x, y, slot);
+        float* o = P.out_rgb + 3 * slot;
+        o[0] = col.x; o[1] = col.y; o[2] = col.z;
+        if (P.out_rgb8) {
+            uint8_t* o8 = P.out_rgb8 + 3 * slot;
+            o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
+        }
+    }
+    flush_stats<COUNT, false>(P, st, shadow_total, lane);
+}
+
 // Batched Scene::trace: one lane per query ray.
 template <bool ANY>
 __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DLeaf* leaves, const uint16_t* tables,
                                                     int32_t* gstack, uint32_t gstride, const float* o, const float* d,
                                                     const float* tmin, const float* tmax, size_t n, mrt_hit* out,
-                                                    unsigned long long* ctr) {
+                                                    unsigned long long* ctr, int fast_box) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     const int tid = threadIdx.x;
     for (int i = tid; i < 1024; i += kWG) reinterpret_cast<uint32_t*>(s_tab)[i] = reinterpret_cast<const uint32_t*>(tables)[i];
     __syncthreads();
     const uint32_t gtid = blockIdx.x * kWG + tid;
-    Trav T{nodes, leaves, s_tab, s_stack + tid, gstack + gtid, gstride};
+    Trav T{nodes, fast_box != 0, leaves, s_tab, s_stack + tid, gstack + gtid, gstride};
     TravStats st;
     for (size_t i = (size_t)blockIdx.x * kWG + tid; i < n; i += (size_t)gridDim.x * kWG) {
         DRay r = make_ray(mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]));
         DHit h{tmax[i], 0.f, 0.f, -1};
-        bool hit = traverse<ANY, false>(T, r, tmin[i], h, st);
+        bool hit = traverse<ANY, false, false>(T, r, tmin[i], h, st);
         mrt_hit res;
         res.t = h.t; res.a = h.a; res.b = h.b; res.prim = hit ? (ANY ? 0 : h.prim) : -1;
         if (ANY && hit) res.prim = 1;  // any-hit: occluded flag only
@@ -403,19 +555,30 @@ struct DeviceState {
     size_t frame_px = 0;
     // kernel 1 -> kernel 2 hand-off (per output slot)
     float4* hitbuf = nullptr;
-    float4* dirbuf = nullptr;
     size_t hit_slots = 0;
-    int grid_primary = 0, grid_shade = 0;
+    int grid_primary = 0, grid_shade = 0, grid_primary5 = 0, grid_shade1 = 0;
+    bool boxes_finite = false;
+    int cus = 0;
+    bool point_only = false;
     bool last_was_render = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
     size_t bytes = 0;
 };
 
+// Tuning knobs (mrt_set_tuning): A/B switches for performance work.
+static int g_fast_box = 1;        // hardware min/max box test when its precondition holds
+static int g_primary_waves = 6;   // 0: default launch bounds, 6: ask for 6 waves/SIMD (<= 80 VGPRs)
+static int g_lds_pad_kb = 0;      // extra dynamic LDS per workgroup (occupancy sweeps)
+static int g_xcd_map = 0;         // XCD-banded tile schedule (measured slower: static bands imbalance)
+static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
+
+static inline int fast_box(const DeviceState& d);
+
 static void free_device(DeviceState* d) {
     if (!d) return;
     if (d->device >= 0) (void)hipSetDevice(d->device);
     void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->tables,
-                    d->gamma, d->gstack, d->ctr, d->d_rgb, d->d_rgb8, d->hitbuf, d->dirbuf};
+                    d->gamma, d->gstack, d->ctr, d->d_rgb, d->d_rgb8, d->hitbuf};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (d->ev0) (void)hipEventDestroy(d->ev0);
@@ -489,12 +652,23 @@ static int ensure_device(Scene& s, int device) {
     // persistent grid: resident workgroups on every CU
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device));
-    int per_cu1 = 0, per_cu2 = 0;
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu1, primary_kernel<false>, kWG, 0));
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, shade_kernel<false>, kWG, 0));
+    int per_cu1 = 0, per_cu2 = 0, per_cu5 = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu1, (primary_kernel<false, 1, false>), kWG, 0));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu5, (primary_kernel<false, 6, false>), kWG, 0));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, (shade_kernel<false, false, false>), kWG, 0));
+    d.cus = prop.multiProcessorCount;
+    int per_cu3 = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu3, (shade1_kernel<false, false>), kWG, 0));
+    d.grid_shade1 = prop.multiProcessorCount * std::max(per_cu3, 1);
     d.grid_primary = prop.multiProcessorCount * std::max(per_cu1, 1);
+    d.grid_primary5 = prop.multiProcessorCount * std::max(per_cu5, 1);
     d.grid_shade = prop.multiProcessorCount * std::max(per_cu2, 1);
-    d.grid = std::max(d.grid_primary, d.grid_shade);
+    d.grid = std::max(std::max(std::max(d.grid_primary, d.grid_primary5), d.grid_shade), d.grid_shade1);
+    d.boxes_finite = true;
+    for (const QNode& q : s.nodes)
+        for (int k = 0; k < 24; k++) d.boxes_finite &= std::isfinite(q.box[k]);
+    d.point_only = true;
+    for (const DevLight& l : s.lights) d.point_only &= (l.type == MRT_POINT_LIGHT);
     d.gthreads = (uint32_t)d.grid * kWG;
     HIP_OK(hipMalloc((void**)&d.gstack, (size_t)kGlobalStack * d.gthreads * sizeof(int32_t)));
     HIP_OK(hipMalloc((void**)&d.ctr, CTR_N * sizeof(unsigned long long)));
@@ -539,13 +713,13 @@ static void fill_params(const Scene& s, RenderParams& P) {
     P.num_paths = s.num_paths;
 }
 
+static inline int fast_box(const DeviceState& d) { return (g_fast_box && d.boxes_finite) ? 1 : 0; }
+
 static int ensure_slots(DeviceState& d, size_t slots) {
     if (slots <= d.hit_slots) return MRT_OK;
     if (d.hitbuf) (void)hipFree(d.hitbuf);
-    if (d.dirbuf) (void)hipFree(d.dirbuf);
-    d.hitbuf = nullptr; d.dirbuf = nullptr; d.hit_slots = 0;
+    d.hitbuf = nullptr; d.hit_slots = 0;
     HIP_OK(hipMalloc((void**)&d.hitbuf, slots * sizeof(float4)));
-    HIP_OK(hipMalloc((void**)&d.dirbuf, slots * sizeof(float4)));
     d.hit_slots = slots;
     return MRT_OK;
 }
@@ -557,16 +731,48 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     int rc = ensure_slots(d, slots);
     if (rc) return rc;
     P.hits = d.hitbuf;
-    P.dirs = d.dirbuf;
+    P.fast_box = fast_box(d);
+    P.xcd_map = g_xcd_map;
     HIP_OK(hipMemsetAsync(d.ctr, 0, CTR_N * sizeof(unsigned long long), stream));
-    int g1 = std::max(1, std::min(d.grid_primary, (P.n_tiles + 3) / 4));
+    const bool w5 = g_primary_waves == 6;
+    const size_t pad = (size_t)g_lds_pad_kb * 1024;
+    int g1 = std::max(1, std::min(w5 ? d.grid_primary5 : d.grid_primary, (P.n_tiles + 3) / 4));
     int g2 = std::max(1, std::min(d.grid_shade, (P.n_tiles + 3) / 4));
+    if (pad) {
+        int pc1 = 0, pc2 = 0;
+        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc1, (primary_kernel<false, 6, false>), kWG, pad));
+        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc2, (shade_kernel<false, true, false>), kWG, pad));
+        g1 = std::max(1, std::min(g1, d.cus * std::max(pc1, 1)));
+        g2 = std::max(1, std::min(g2, d.cus * std::max(pc2, 1)));
+    }
     HIP_OK(hipEventRecord(d.ev0, stream));
-    if (count) hipLaunchKernelGGL(primary_kernel<true>, dim3(g1), dim3(kWG), 0, stream, P);
-    else hipLaunchKernelGGL(primary_kernel<false>, dim3(g1), dim3(kWG), 0, stream, P);
+    const bool fb = P.fast_box != 0;
+#define MRT_PRIMARY(C, W, F) hipLaunchKernelGGL((primary_kernel<C, W, F>), dim3(g1), dim3(kWG), pad, stream, P)
+#define MRT_SHADE(C, PO, F) hipLaunchKernelGGL((shade_kernel<C, PO, F>), dim3(g2), dim3(kWG), pad, stream, P)
+    if (count) {
+        if (w5) { if (fb) MRT_PRIMARY(true, 6, true); else MRT_PRIMARY(true, 6, false); }
+        else { if (fb) MRT_PRIMARY(true, 1, true); else MRT_PRIMARY(true, 1, false); }
+    } else {
+        if (w5) { if (fb) MRT_PRIMARY(false, 6, true); else MRT_PRIMARY(false, 6, false); }
+        else { if (fb) MRT_PRIMARY(false, 1, true); else MRT_PRIMARY(false, 1, false); }
+    }
     HIP_OK(hipEventRecord(d.evm, stream));
-    if (count) hipLaunchKernelGGL(shade_kernel<true>, dim3(g2), dim3(kWG), 0, stream, P);
-    else hipLaunchKernelGGL(shade_kernel<false>, dim3(g2), dim3(kWG), 0, stream, P);
+    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1;
+    if (one) {
+        const int g3 = std::max(1, std::min(d.grid_shade1, (P.n_tiles + 3) / 4));
+#define MRT_SHADE1(C, F) hipLaunchKernelGGL((shade1_kernel<C, F>), dim3(g3), dim3(kWG), pad, stream, P)
+        if (count) { if (fb) MRT_SHADE1(true, true); else MRT_SHADE1(true, false); }
+        else { if (fb) MRT_SHADE1(false, true); else MRT_SHADE1(false, false); }
+#undef MRT_SHADE1
+    } else if (d.point_only) {
+        if (count) { if (fb) MRT_SHADE(true, true, true); else MRT_SHADE(true, true, false); }
+        else { if (fb) MRT_SHADE(false, true, true); else MRT_SHADE(false, true, false); }
+    } else {
+        if (count) { if (fb) MRT_SHADE(true, false, true); else MRT_SHADE(true, false, false); }
+        else { if (fb) MRT_SHADE(false, false, true); else MRT_SHADE(false, false, false); }
+    }
+#undef MRT_PRIMARY
+#undef MRT_SHADE
     d.last_was_render = true;
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d.ev1, stream));
@@ -872,6 +1078,7 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     S.last.primary_leaf_visits = c[CTR_LEAVES_P];
     S.last.shadow_rays = c[CTR_SHADOW];
     S.last.primary_hits = c[CTR_HITS];
+    S.last.primary_wave_steps = c[CTR_WAVE_STEPS_P];
     S.last.node_visits = c[CTR_NODES];
     S.last.leaf_visits = c[CTR_LEAVES];
     S.last.max_stack = (int32_t)c[CTR_MAXSP];
@@ -897,10 +1104,10 @@ int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const floa
     HIP_OK(hipEventRecord(d.ev0, (hipStream_t)stream));
     if (any_hit)
         hipLaunchKernelGGL(trace_kernel<true>, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables,
-                           d.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, d.ctr);
+                           d.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, d.ctr, fast_box(d));
     else
         hipLaunchKernelGGL(trace_kernel<false>, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables,
-                           d.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, d.ctr);
+                           d.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, d.ctr, fast_box(d));
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d.ev1, (hipStream_t)stream));
     return MRT_OK;
@@ -935,6 +1142,24 @@ int mrt_trace(mrt_scene* s, const float* o, const float* d, const float* tmin, c
     }
     (void)hipFree(bo); (void)hipFree(bd); (void)hipFree(bmin); (void)hipFree(bmax); (void)hipFree(bout);
     return rc;
+}
+
+int mrt_set_tuning(const char* key, int value) {
+    if (!key) { set_error("null key"); return MRT_ERR_INVALID; }
+    std::string k(key);
+    if (k == "fast_box") g_fast_box = value ? 1 : 0;
+    else if (k == "primary_waves") {
+        if (value != 0 && value != 1 && value != 6) { set_error("primary_waves must be 0 or 6"); return MRT_ERR_INVALID; }
+        g_primary_waves = value;
+    } else if (k == "shade1") {
+        g_shade1 = value ? 1 : 0;
+    } else if (k == "xcd_map") {
+        g_xcd_map = value ? 1 : 0;
+    } else if (k == "lds_pad_kb") {
+        if (value < 0 || value > 128) { set_error("lds_pad_kb out of range"); return MRT_ERR_INVALID; }
+        g_lds_pad_kb = value;
+    } else { set_error("unknown tuning key " + k); return MRT_ERR_INVALID; }
+    return MRT_OK;
 }
 
 float mrt_rcp_nr(float x) { return rcp_nr(x, host_rcp_table()); }

@@ -19,12 +19,13 @@
 namespace mrt {
 
 static constexpr int kWG = 256;          // threads per workgroup (4 waves)
-static constexpr int kLdsStack = 24;     // stack entries per lane kept in LDS
-static constexpr int kGlobalStack = 72;  // spill entries per thread in HBM
+static constexpr int kLdsStack = 16;     // stack entries per lane kept in LDS (max seen: 11)
+static constexpr int kGlobalStack = 80;  // spill entries per thread in HBM
 static constexpr int kTableWords = 4096; // rcp[2048] + rsqrt[2048] (u16)
 
 struct DRay {
     float o[3], d[3], id[3];
+    bool finite;  // o and id finite: no box-test value can be NaN (see box_test_fast)
 };
 
 // Ray(threadID, o, d, ...), src/Ray.h:71-101: id = 1/d, +-1e12 for d == 0.
@@ -38,6 +39,8 @@ __device__ __forceinline__ DRay make_ray(v3 o, v3 d) {
         if (r.d[k] == 0.f) v = (v < -0.f) ? -1e12f : 1e12f;
         r.id[k] = v;
     }
+    r.finite = __builtin_isfinite(r.o[0]) & __builtin_isfinite(r.o[1]) & __builtin_isfinite(r.o[2]) &
+               __builtin_isfinite(r.id[0]) & __builtin_isfinite(r.id[1]) & __builtin_isfinite(r.id[2]);
     return r;
 }
 
@@ -48,6 +51,7 @@ struct DHit {
 
 struct Trav {
     const QNode* __restrict__ nodes;
+    bool fast_box;            // all node boxes finite and fast box test enabled
     const DLeaf* __restrict__ leaves;
     const uint16_t* rcpT;     // LDS
     int32_t* lds;             // this lane's LDS stack column (stride kWG)
@@ -132,16 +136,40 @@ __device__ __forceinline__ int box_test(const float4* bx, const DRay& r, float t
     return m;
 }
 
+// Same mask as box_test on the hardware min/max.  Precondition: ray origin,
+// 1/d and the node boxes are finite, so every slab value is finite or +-inf,
+// never NaN.  Then v_min/v_max (IEEE minnum/maxnum) return the same number as
+// the MINPS/MAXPS selects except possibly the sign of a zero, and the only
+// consumer of these values is `imin <= imax`, for which -0 == +0.
+__device__ __forceinline__ int box_test_fast(const float4* bx, const DRay& r, float tMin, float tMax) {
+    float4 mnx = bx[0], mny = bx[1], mnz = bx[2], mxx = bx[3], mxy = bx[4], mxz = bx[5];
+    float lx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, ly[4] = {mny.x, mny.y, mny.z, mny.w}, lz[4] = {mnz.x, mnz.y, mnz.z, mnz.w};
+    float hx[4] = {mxx.x, mxx.y, mxx.z, mxx.w}, hy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, hz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        float t0x = (lx[i] - r.o[0]) * r.id[0], t1x = (hx[i] - r.o[0]) * r.id[0];
+        float t0y = (ly[i] - r.o[1]) * r.id[1], t1y = (hy[i] - r.o[1]) * r.id[1];
+        float t0z = (lz[i] - r.o[2]) * r.id[2], t1z = (hz[i] - r.o[2]) * r.id[2];
+        float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
+                                   __builtin_fmaxf(__builtin_fminf(t0z, t1z), tMin));
+        float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
+                                   __builtin_fminf(__builtin_fmaxf(t0z, t1z), tMax));
+        m |= (int)(t0 <= t1) << i;
+    }
+    return m;
+}
+
 // BVH::intersect, QBVH branch (src/BVH.cpp:1128-1178).  Returns hit.  On a
 // stack overflow, st.overflow is set and the query is abandoned.
-template <bool ANY, bool COUNT>
-__device__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
+template <bool ANY, bool COUNT, bool FAST>
+__device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
     int sp = 0;
     int32_t cur = 0;
     bool hit = false;
     while (true) {
         const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
-        int m = box_test(q, r, tMin, h.t);
+        int m = FAST ? box_test_fast(q, r, tMin, h.t) : box_test(q, r, tMin, h.t);
         int4 ch = reinterpret_cast<const int4*>(q)[6];
         int32_t chv[4] = {ch.x, ch.y, ch.z, ch.w};
         if (COUNT) st.nodes++;
@@ -180,6 +208,14 @@ __device__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, Trav
         }
     }
     return hit;
+}
+
+// FAST (node boxes known finite) uses the hardware min/max slab test for rays
+// whose origin and 1/d are finite; any other ray takes the exact loop.
+template <bool ANY, bool COUNT, bool FAST = false>
+__device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
+    if (FAST && r.finite) return traverse_impl<ANY, COUNT, true>(c, r, tMin, h, st);
+    return traverse_impl<ANY, COUNT, false>(c, r, tMin, h, st);
 }
 
 }  // namespace mrt

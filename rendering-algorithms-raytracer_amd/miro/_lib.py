@@ -20,7 +20,7 @@ EXPORTS = [
     "mrt_scene_build_bvh", "mrt_scene_bvh_info", "mrt_scene_bvh_export", "mrt_scene_bvh_import",
     "mrt_scene_upload", "mrt_render", "mrt_render_buckets_async", "mrt_unpack_buckets_async",
     "mrt_render_frame_async", "mrt_trace", "mrt_trace_async", "mrt_scene_last_stats", "mrt_rcp_nr",
-    "mrt_rsqrt_nr",
+    "mrt_rsqrt_nr", "mrt_set_tuning",
 ]
 
 
@@ -63,7 +63,7 @@ class mrt_render_opts(C.Structure):
 class mrt_stats(C.Structure):
     _fields_ = [("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("node_visits", C.c_uint64),
                 ("leaf_visits", C.c_uint64), ("primary_node_visits", C.c_uint64),
-                ("primary_leaf_visits", C.c_uint64), ("primary_hits", C.c_uint64), ("kernel_ms", C.c_float), ("primary_ms", C.c_float),
+                ("primary_leaf_visits", C.c_uint64), ("primary_hits", C.c_uint64), ("primary_wave_steps", C.c_uint64), ("kernel_ms", C.c_float), ("primary_ms", C.c_float),
                 ("shade_ms", C.c_float), ("max_stack", C.c_int32)]
 
 
@@ -121,6 +121,7 @@ def load():
     L.mrt_trace_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                   C.c_int, C.c_void_p, C.c_void_p]
     L.mrt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(mrt_stats)]
+    L.mrt_set_tuning.argtypes = [C.c_char_p, C.c_int]
     L.mrt_rcp_nr.argtypes = [C.c_float]
     L.mrt_rcp_nr.restype = C.c_float
     L.mrt_rsqrt_nr.argtypes = [C.c_float]

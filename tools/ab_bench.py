@@ -1,0 +1,73 @@
+"""Interleaved A/B of tuning switches on config C3 (one process, one device).
+Usage: python tools/ab_bench.py key=v1,v2 [key2=...] [--rounds R]"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rendering-algorithms-raytracer_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import miro  # noqa: E402
+from miro import _lib, scenes  # noqa: E402
+
+
+def main():
+    args = [a for a in sys.argv[1:] if "=" in a]
+    rounds = 7
+    if "--rounds" in sys.argv:
+        rounds = int(sys.argv[sys.argv.index("--rounds") + 1])
+    cfgkey = os.environ.get("AB_CONFIG", "C3")
+    variants = [{}]
+    for a in args:
+        k, vs = a.split("=")
+        variants = [dict(v, **{k: int(x)}) for v in variants for x in vs.split(",")]
+    scene, cam, cfg = scenes.build_config(cfgkey)
+    W, H = cfg["W"], cfg["H"]
+    L = miro.lib()
+    frame = torch.empty(H * W * 3, dtype=torch.float32, device="cuda")
+    frame8 = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")
+    sh = torch.cuda.current_stream().cuda_stream
+    camc = cam._c()
+    ref = None
+
+    def run(v, count=False, reps=10):
+        for k, x in v.items():
+            _lib.check(L.mrt_set_tuning(k.encode(), x), k)
+        o = _lib.mrt_render_opts(W, H, 0, int(count), 1, 0, 0)
+        pm, sm = [], []
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc), C.byref(o), frame.data_ptr(),
+                                                frame8.data_ptr(), sh), "render")
+            st = scene.stats()
+            pm.append(st["primary_ms"]); sm.append(st["shade_ms"])
+        return pm, sm, st
+
+    res = {json.dumps(v): ([], []) for v in variants}
+    for v in variants:  # warm + correctness vs the first variant
+        run(v, reps=2)
+        out = frame.cpu().numpy().view(np.uint32).copy()
+        if ref is None:
+            ref = out
+        assert np.array_equal(ref, out), f"variant {v} changed the frame!"
+        _, _, st = run(v, count=True, reps=1)
+        print("variant", v, "counts", {k: st[k] for k in ("node_visits", "leaf_visits", "primary_node_visits",
+                                                          "max_stack", "shadow_rays", "primary_hits")},
+              "primary SIMD util %.3f" % (st["primary_node_visits"] / max(1, 64 * st["primary_wave_steps"])), flush=True)
+    for r in range(rounds):
+        for v in variants:
+            pm, sm, _ = run(v)
+            res[json.dumps(v)][0].extend(pm)
+            res[json.dumps(v)][1].extend(sm)
+    rays = W * H + st["shadow_rays"]
+    for k, (pm, sm) in res.items():
+        p, s = np.median(pm), np.median(sm)
+        print(f"{k:64s} primary {p:.4f} ms  shade {s:.4f} ms  "
+              f"frame {p + s:.4f} ms  -> {rays / (p + s) / 1e3:.0f} Mray/s (kernel time)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
