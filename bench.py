@@ -43,8 +43,9 @@ def kernel_bytes(st, px, hits):
     their sizes + per-pixel ray I/O + per-hit shading gathers."""
     pn, pl = st["primary_node_visits"], st["primary_leaf_visits"]
     sn, sl = st["node_visits"] - pn, st["leaf_visits"] - pl
-    primary = pn * NODE_B + pl * LEAF_B + px * 32                 # write hit + dir (2 x 16 B)
-    shade = sn * NODE_B + sl * LEAF_B + px * (32 + 12 + 3) + hits * (32 + 3 * 16 + 3 * 16)
+    primary = pn * NODE_B + pl * LEAF_B + px * 16                 # write the 16-B hit record
+    # read the hit record, write float RGB + RGB8; per hit: PrimShade + 3 vertices + 3 normals
+    shade = sn * NODE_B + sl * LEAF_B + px * (16 + 12 + 3) + hits * (32 + 3 * 16 + 3 * 16)
     return primary, shade
 
 
@@ -188,8 +189,10 @@ def main():
     hits_mine = hits_px
     b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine)
     pm, sm = float(np.median(prim_ms)), float(np.median(shade_ms))
+    one_light = len(cfg["lights"]) == 1 and cfg.get("num_paths", 1) == 1
+    shade_name = "shade1_kernel" if one_light else "shade_kernel"
     if sm >= pm:
-        dom, dom_ms, dom_b = "shade_kernel (shade + any-hit shadow rays)", sm, b_shade
+        dom, dom_ms, dom_b = shade_name + " (shade + any-hit shadow rays)", sm, b_shade
     else:
         dom, dom_ms, dom_b = "primary_kernel (camera rays, closest hit)", pm, b_prim
     achieved = dom_b / (dom_ms * 1e-3) / 1e9
@@ -197,7 +200,9 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("per_launch_bytes", {}).get(dom.split()[0])
+            prof = json.load(open(pmc))
+            if prof.get("config") == args.config:
+                traffic = prof.get("per_launch_hbm_bytes", {}).get(dom.split()[0])
         except Exception:
             traffic = None
     out = {

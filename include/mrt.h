@@ -190,7 +190,8 @@ int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
 /* Performance A/B switches (no effect on results; defaults in brackets):
  * "fast_box" 0/[1] (hardware min/max slab test when its finiteness precondition
  * holds), "primary_waves" 0/[6] (occupancy target of the primary-ray kernel),
- * "xcd_map" [0]/1 (XCD-banded tile schedule), "shade1" 0/[1] (specialised shading
+ * "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands, dynamic
+ * interleaved, dynamic banded; see TileSched), "shade1" 0/[1] (specialised shading
  * kernel for one point light and one path), "lds_pad_kb" [0]..128 (extra LDS per
  * workgroup, lowers occupancy for sweeps).  Process-wide. */
 int mrt_set_tuning(const char* key, int value);

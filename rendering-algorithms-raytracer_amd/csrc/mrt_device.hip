@@ -37,6 +37,8 @@ void set_error(const std::string& m) { g_err = m; }
 
 enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLOW = 4, CTR_NODES_P = 5, CTR_LEAVES_P = 6, CTR_HITS = 7,
        CTR_WAVE_STEPS_P = 8, CTR_N = 16 };
+// counter block: CTR_N u64 statistics, then two launches x 8 tile counters x 128 B
+static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 2 * 8 * 128;
 
 struct RenderParams {
     const QNode* nodes;
@@ -56,7 +58,8 @@ struct RenderParams {
     int32_t n_lights, num_paths;
     uint32_t seed;
     int32_t fast_box;            // node boxes finite && tuning allows the hardware min/max box test
-    int32_t xcd_map;             // 1: workgroups on one XCD take one contiguous band of tiles
+    int32_t sched;               // tile schedule (TileSched)
+    unsigned int* queue;         // 8 tile counters, 32 words apart (sched >= 2)
     // work: 8x8 tiles
     int32_t tiles_x, n_tiles;    // frame mode: tiles_x = ceil(W/8)
     const int32_t* buckets;      // bucket mode: bucket ids (row-major bucket grid)
@@ -222,26 +225,60 @@ struct Shader {
 
 __device__ __forceinline__ uint8_t map8(const uint8_t* lut, float v) { return lut[map_index(v)]; }
 
-// Tile schedule of a persistent workgroup.  xcd_map = 0: grid-stride over all
-// tiles.  xcd_map = 1 (grid a multiple of 8): workgroups b, b+8, ... -- observed
-// to share one XCD and its L2 (placement is a speed hint only, never needed for
-// correctness) -- walk one contiguous eighth of the tiles, so each XCD's L2
-// holds the part of the BVH its image band touches.
-struct TileIter {
-    int cur, step, end;
-    __device__ TileIter(const RenderParams& P, int wave) {
-        if (P.xcd_map && (gridDim.x & 7) == 0) {
-            int xcd = blockIdx.x & 7, local = blockIdx.x >> 3, per = gridDim.x >> 3;
-            int band = (P.n_tiles + 7) >> 3;
-            int beg = xcd * band;
+// Tile schedule of a persistent wave (one 8x8 tile = one wave step).
+//   sched 0: static grid-stride over all tiles.
+//   sched 1: static XCD bands -- workgroups b, b+8, ... (observed to share one XCD
+//            and its L2; placement is a speed hint only) walk one eighth.
+//   sched 2: dynamic -- 8 tile counters (one 128-B line each), counter c hands
+//            out tiles c, c+8, ...; a wave starts at counter blockIdx & 7 and moves
+//            to the next counter when one runs dry, so every wave stays busy until
+//            the frame is done.
+//   sched 3: dynamic, counter c hands out the contiguous band c (L2 locality per
+//            XCD) with the same stealing.
+// Counters are zeroed per launch; every wave sees -1 after at most 8 empty probes.
+struct TileSched {
+    const RenderParams& P;
+    int lane, mode, cur, step, end, home, probe, band;
+    __device__ TileSched(const RenderParams& P_, int wave, int lane_) : P(P_), lane(lane_) {
+        mode = P.sched;
+        home = blockIdx.x & 7;
+        probe = 0;
+        band = (P.n_tiles + 7) >> 3;
+        if (mode == 1 && (gridDim.x & 7) == 0) {
+            int local = blockIdx.x >> 3, per = gridDim.x >> 3;
+            int beg = home * band;
             end = min(P.n_tiles, beg + band);
             cur = beg + local * 4 + wave;
             step = per * 4;
         } else {
+            if (mode == 1) mode = 0;
             cur = blockIdx.x * 4 + wave;
             step = gridDim.x * 4;
             end = P.n_tiles;
         }
+    }
+    __device__ int dequeue() {
+        int item = -1;
+        if (lane == 0) {
+            while (probe < 8) {
+                const int c = (home + probe) & 7;
+                const unsigned v = atomicAdd(P.queue + c * 32, 1u);
+                const long idx = (mode == 3) ? (v < (unsigned)band ? (long)c * band + v : (long)P.n_tiles)
+                                             : (long)c + 8l * v;
+                if (idx < P.n_tiles) { item = (int)idx; break; }
+                probe++;
+            }
+        }
+        return __shfl(item, 0);
+    }
+    __device__ int first() {
+        if (mode >= 2) return dequeue();
+        return cur < end ? cur : -1;
+    }
+    __device__ int next(int item) {
+        if (mode >= 2) return dequeue();
+        item += step;
+        return item < end ? item : -1;
     }
 };
 
@@ -326,8 +363,8 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     const CamParams& cam = P.cam;
     const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
     unsigned long long wave_steps = 0;  // count mode: sum over tiles of max lane node visits
-    TileIter it(P, wave);
-    for (int item = it.cur; item < it.end; item += it.step) {
+    TileSched ts(P, wave, lane);
+    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
         int x, y;
         size_t slot;
         const uint32_t n0 = st.nodes;
@@ -363,8 +400,8 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     uint32_t shadow_total = 0;
     const CamParams& cam = P.cam;
     const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
-    TileIter it(P, wave);
-    for (int item = it.cur; item < it.end; item += it.step) {
+    TileSched ts(P, wave, lane);
+    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
         int x, y;
         size_t slot;
         if (!item_pixel(P, item, lane, x, y, slot)) continue;
@@ -406,8 +443,8 @@ __global__ void __launch_bounds__(kWG, 6) shade1_kernel(RenderParams P) {
     TravStats st;
     uint32_t shadow_total = 0;
     const v3 eye = mk(P.cam.eye[0], P.cam.eye[1], P.cam.eye[2]);
-    TileIter it(P, wave);
-    for (int item = it.cur; item < it.end; item += it.step) {
+    TileSched ts(P, wave, lane);
+    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
         int x, y;
         size_t slot;
         if (!item_pixel(P, item, lane, x, y, slot)) continue;
@@ -569,7 +606,7 @@ struct DeviceState {
 static int g_fast_box = 1;        // hardware min/max box test when its precondition holds
 static int g_primary_waves = 6;   // 0: default launch bounds, 6: ask for 6 waves/SIMD (<= 80 VGPRs)
 static int g_lds_pad_kb = 0;      // extra dynamic LDS per workgroup (occupancy sweeps)
-static int g_xcd_map = 0;         // XCD-banded tile schedule (measured slower: static bands imbalance)
+static int g_sched = 2;           // TileSched mode 0..3 (2 measured fastest)
 static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
 
 static inline int fast_box(const DeviceState& d);
@@ -671,7 +708,7 @@ static int ensure_device(Scene& s, int device) {
     for (const DevLight& l : s.lights) d.point_only &= (l.type == MRT_POINT_LIGHT);
     d.gthreads = (uint32_t)d.grid * kWG;
     HIP_OK(hipMalloc((void**)&d.gstack, (size_t)kGlobalStack * d.gthreads * sizeof(int32_t)));
-    HIP_OK(hipMalloc((void**)&d.ctr, CTR_N * sizeof(unsigned long long)));
+    HIP_OK(hipMalloc((void**)&d.ctr, kCtrBytes));
     HIP_OK(hipEventCreate(&d.ev0));
     HIP_OK(hipEventCreate(&d.ev1));
     HIP_OK(hipEventCreate(&d.evm));
@@ -732,8 +769,10 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     if (rc) return rc;
     P.hits = d.hitbuf;
     P.fast_box = fast_box(d);
-    P.xcd_map = g_xcd_map;
-    HIP_OK(hipMemsetAsync(d.ctr, 0, CTR_N * sizeof(unsigned long long), stream));
+    P.sched = g_sched;
+    HIP_OK(hipMemsetAsync(d.ctr, 0, kCtrBytes, stream));
+    unsigned int* qbase = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(d.ctr) + CTR_N * sizeof(unsigned long long));
+    P.queue = qbase;
     const bool w5 = g_primary_waves == 6;
     const size_t pad = (size_t)g_lds_pad_kb * 1024;
     int g1 = std::max(1, std::min(w5 ? d.grid_primary5 : d.grid_primary, (P.n_tiles + 3) / 4));
@@ -757,6 +796,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         else { if (fb) MRT_PRIMARY(false, 1, true); else MRT_PRIMARY(false, 1, false); }
     }
     HIP_OK(hipEventRecord(d.evm, stream));
+    P.queue = qbase + 8 * 32;
     const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1;
     if (one) {
         const int g3 = std::max(1, std::min(d.grid_shade1, (P.n_tiles + 3) / 4));
@@ -1153,8 +1193,9 @@ int mrt_set_tuning(const char* key, int value) {
         g_primary_waves = value;
     } else if (k == "shade1") {
         g_shade1 = value ? 1 : 0;
-    } else if (k == "xcd_map") {
-        g_xcd_map = value ? 1 : 0;
+    } else if (k == "sched") {
+        if (value < 0 || value > 3) { set_error("sched must be 0..3"); return MRT_ERR_INVALID; }
+        g_sched = value;
     } else if (k == "lds_pad_kb") {
         if (value < 0 || value > 128) { set_error("lds_pad_kb out of range"); return MRT_ERR_INVALID; }
         g_lds_pad_kb = value;

@@ -149,10 +149,11 @@ def test_edge_cases():
     assert np.array_equal(bits(got["t"]), bits(ref["t"]))
 
 
-@pytest.mark.parametrize("knobs", [dict(shade1=0, fast_box=0, xcd_map=0, primary_waves=0),
-                                   dict(shade1=1, fast_box=1, xcd_map=1, primary_waves=6),
-                                   dict(shade1=0, fast_box=1, xcd_map=1, primary_waves=0),
-                                   dict(shade1=1, fast_box=0, xcd_map=0, primary_waves=6)])
+@pytest.mark.parametrize("knobs", [dict(shade1=0, fast_box=0, sched=0, primary_waves=0),
+                                   dict(shade1=1, fast_box=1, sched=1, primary_waves=6),
+                                   dict(shade1=0, fast_box=1, sched=2, primary_waves=0),
+                                   dict(shade1=1, fast_box=0, sched=3, primary_waves=6),
+                                   dict(shade1=1, fast_box=1, sched=2, primary_waves=6)])
 def test_every_kernel_path_is_exact(knobs):
     """Performance switches must not change a single bit (fused vs split shading,
     hardware vs select box test, XCD schedule, occupancy build)."""
@@ -167,7 +168,7 @@ def test_every_kernel_path_is_exact(knobs):
         assert np.array_equal(hits["prim"], ref["hits"]["prim"])
         assert P.last_stats["shadow_rays"] == ref["shadow_rays"]
     finally:
-        for k, v in dict(shade1=1, fast_box=1, xcd_map=0, primary_waves=6).items():
+        for k, v in dict(shade1=1, fast_box=1, sched=2, primary_waves=6).items():
             L.mrt_set_tuning(k.encode(), v)
 
 
