@@ -669,7 +669,20 @@ static int ensure_device(Scene& s, int device) {
     memcpy(tab.data() + 2048, host_rsqrt_table(), 4096);
     size_t total = 0;
     int rc;
-    if ((rc = upload(d.nodes, s.nodes.data(), s.nodes.size() * sizeof(QNode), total))) return rc;
+    // device child words: leaf slots carry their packet's triangle count (leaf_child)
+    if (s.leaves.size() >= (size_t(1) << 29)) { set_error("too many leaf packets"); return MRT_ERR_OVERFLOW; }
+    std::vector<QNode> DN(s.nodes);
+    for (QNode& q : DN)
+        for (int k = 0; k < 4; k++) {
+            const int32_t c = q.child[k];
+            if (c >= 0 || c == kEmptySlot) continue;
+            const QLeaf& L = s.leaves[(size_t)~c];
+            int cnt = 0;
+            for (int j = 0; j < 4; j++)
+                if (L.prim[j] >= 0) cnt = j + 1;   // zero-filled lanes below cnt are rejected by det = 0
+            q.child[k] = leaf_child((uint32_t)~c, cnt < 1 ? 1 : cnt);
+        }
+    if ((rc = upload(d.nodes, DN.data(), DN.size() * sizeof(QNode), total))) return rc;
     std::vector<DLeaf> DL(s.leaves.size());
     for (size_t i = 0; i < DL.size(); i++) {
         for (int k = 0; k < 4; k++) {

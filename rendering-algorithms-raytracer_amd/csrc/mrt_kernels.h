@@ -77,45 +77,33 @@ __device__ __forceinline__ int32_t stk_pop(const Trav& c, int& sp) {
     return sp < kLdsStack ? c.lds[sp * kWG] : c.gstk[(size_t)(sp - kLdsStack) * c.gstride];
 }
 
-// intersect4 (src/BVH.cpp:1298-1459) for one 4-triangle packet, one triangle
-// at a time.  The reference tests all four lanes against result.t at packet
-// entry and keeps the lowest accepted t (first lane on ties).  Walking the lanes
-// in order and accepting only t < current best gives the same winner: a lane
-// that loses to an earlier one is never selected by the reference either.
-// Empty lanes (prim -1) are zero triangles, which the reference rejects via
-// det = 0 -> rcp_nr = NaN, so they are skipped.
-template <bool ANY>
-__device__ __forceinline__ bool intersect4(const DLeaf* __restrict__ L, const DRay& r, float tMin, DHit& h,
-                                           const uint16_t* rcpT) {
-    bool hit = false;
-    const int4 pr = *reinterpret_cast<const int4*>(L->prim);
-    const int32_t prim[4] = {pr.x, pr.y, pr.z, pr.w};
-#pragma unroll 1
-    for (int i = 0; i < 4; i++) {
-        int32_t pid = i == 0 ? prim[0] : i == 1 ? prim[1] : i == 2 ? prim[2] : prim[3];
-        if (pid < 0) break;
-        const float* T = L->tri[i];
-        float ax = T[0], ay = T[1], az = T[2], e0x = T[3], e0y = T[4], e0z = T[5], e1x = T[6], e1y = T[7], e1z = T[8];
-        float px = r.d[1] * e1z - r.d[2] * e1y;
-        float py = -1.0f * (r.d[0] * e1z - r.d[2] * e1x);
-        float pz = r.d[0] * e1y - r.d[1] * e1x;
-        float det = e0x * px + (e0y * py + e0z * pz);
-        float inv = rcp_nr(det, rcpT);
-        float tx = r.o[0] - ax, ty = r.o[1] - ay, tz = r.o[2] - az;
-        float a = inv * (tx * px + (ty * py + tz * pz));
-        float qx = ty * e0z - tz * e0y;
-        float qy = -1.0f * (tx * e0z - tz * e0x);
-        float qz = tx * e0y - ty * e0x;
-        float b = inv * (r.d[0] * qx + (r.d[1] * qy + r.d[2] * qz));
-        float t = inv * (e1x * qx + (e1y * qy + e1z * qz));
-        bool ok = (a >= 0.0f) & (a <= 1.0f) & (b >= 0.0f) & (b <= 1.0f) & ((a + b) <= 1.0f) & (t >= tMin) & (t < h.t);
-        if (ok) {
-            if (ANY) return true;
-            h.t = t; h.a = a; h.b = b; h.prim = pid;
-            hit = true;
-        }
-    }
-    return hit;
+__device__ __forceinline__ int32_t sel4(const int4& v, int i) {
+    return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+
+// One triangle of intersect4 (src/BVH.cpp:1298-1459), same operations and
+// rounding as the reference's SSE lane.  The reference tests all four lanes of
+// a packet against result.t at packet entry and keeps the lowest accepted t
+// (first lane on ties); walking the triangles in order and accepting only
+// t < current best selects the same winner.  Empty lanes are zero triangles:
+// det = 0 -> rcp_nr = NaN rejects them exactly as in the reference.
+__device__ __forceinline__ bool tri_test(const float* __restrict__ T, const DRay& r, float tMin, float tBest,
+                                         float& ot, float& oa, float& ob, const uint16_t* rcpT) {
+    const float ax = T[0], ay = T[1], az = T[2], e0x = T[3], e0y = T[4], e0z = T[5], e1x = T[6], e1y = T[7], e1z = T[8];
+    const float px = r.d[1] * e1z - r.d[2] * e1y;
+    const float py = -1.0f * (r.d[0] * e1z - r.d[2] * e1x);
+    const float pz = r.d[0] * e1y - r.d[1] * e1x;
+    const float det = e0x * px + (e0y * py + e0z * pz);
+    const float inv = rcp_nr(det, rcpT);
+    const float tx = r.o[0] - ax, ty = r.o[1] - ay, tz = r.o[2] - az;
+    const float a = inv * (tx * px + (ty * py + tz * pz));
+    const float qx = ty * e0z - tz * e0y;
+    const float qy = -1.0f * (tx * e0z - tz * e0x);
+    const float qz = tx * e0y - ty * e0x;
+    const float b = inv * (r.d[0] * qx + (r.d[1] * qy + r.d[2] * qz));
+    const float t = inv * (e1x * qx + (e1y * qy + e1z * qz));
+    ot = t; oa = a; ob = b;
+    return (a >= 0.0f) & (a <= 1.0f) & (b >= 0.0f) & (b <= 1.0f) & ((a + b) <= 1.0f) & (t >= tMin) & (t < tBest);
 }
 
 // QBVH_Node::intersect (src/BVH.cpp:391-414) -> 4-bit hit mask.
@@ -160,8 +148,24 @@ __device__ __forceinline__ int box_test_fast(const float4* bx, const DRay& r, fl
     return m;
 }
 
-// BVH::intersect, QBVH branch (src/BVH.cpp:1128-1178).  Returns hit.  On a
-// stack overflow, st.overflow is set and the query is abandoned.
+// Device child word of a QNode slot: >= 0 inner node; kEmptySlot; otherwise
+// ~(leaf << 2 | (count - 1)) with count = triangles in the packet (the host
+// re-encodes the canonical ~leaf on upload, see leaf_child()).
+__host__ __device__ __forceinline__ int32_t leaf_child(uint32_t leaf, int count) {
+    return ~(int32_t)((leaf << 2) | (uint32_t)(count - 1));
+}
+
+// BVH::intersect, QBVH branch (src/BVH.cpp:1128-1178).  Returns hit; h.prim is
+// then the packed triangle slot (leaf << 2 | k), resolved by traverse().  On a
+// stack overflow st.overflow is set and the query is abandoned.
+//
+// Per popped node: the 4-slot box mask (branch-free); hit inner slots other
+// than the highest are pushed in slot order (branch-free LDS writes, so the
+// highest is visited next and kept in a register); then the hit leaf slots
+// are intersected in slot order in ONE flattened per-lane loop, one triangle
+// per iteration, so a wave runs max-over-lanes(triangles) iterations instead
+// of one packet loop per slot.  Same visit order and same t at every box test
+// as the reference.
 template <bool ANY, bool COUNT, bool FAST>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
     int sp = 0;
@@ -169,38 +173,60 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
     bool hit = false;
     while (true) {
         const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
-        int m = FAST ? box_test_fast(q, r, tMin, h.t) : box_test(q, r, tMin, h.t);
-        int4 ch = reinterpret_cast<const int4*>(q)[6];
-        int32_t chv[4] = {ch.x, ch.y, ch.z, ch.w};
+        const int4 ch = reinterpret_cast<const int4*>(q)[6];
+        const int m = FAST ? box_test_fast(q, r, tMin, h.t) : box_test(q, r, tMin, h.t);
         if (COUNT) st.nodes++;
-        int inner = 0;
+        const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
+        const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
+                           (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
+        const int inner = m & isinner;
+        int lm = m & isleaf;
+        bool have_next = false;
+        int32_t nxt = 0;
+        if (inner) {
+            const int top = 31 - __builtin_clz((unsigned)inner);
+            const int rest = inner ^ (1 << top);
+            if (rest) {
+                if (sp + 4 <= kLdsStack) {
+                    c.lds[sp * kWG] = ch.x; sp += rest & 1;
+                    c.lds[sp * kWG] = ch.y; sp += (rest >> 1) & 1;
+                    c.lds[sp * kWG] = ch.z; sp += (rest >> 2) & 1;
+                    c.lds[sp * kWG] = ch.w; sp += (rest >> 3) & 1;
+                } else {
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            if (!(m & (1 << i)) || chv[i] == kEmptySlot) continue;
-            if (chv[i] < 0) {
-                if (COUNT) st.leaves++;
-                if (intersect4<ANY>(c.leaves + ~chv[i], r, tMin, h, c.rcpT)) {
-                    hit = true;
-                    if (ANY) return true;
+                    for (int i = 0; i < 4; i++)
+                        if ((rest >> i) & 1)
+                            if (!stk_push(c, sp, sel4(ch, i))) { st.overflow = true; return hit; }
                 }
-            } else {
-                inner |= 1 << i;
+                if (COUNT && sp > st.max_sp) st.max_sp = sp;
+            }
+            nxt = sel4(ch, top);
+            have_next = true;
+        }
+        if (lm) {
+            uint32_t leaf = 0;
+            int k = 0, cnt = 0;
+            while (true) {
+                if (k == cnt) {
+                    if (!lm) break;
+                    const int s = __builtin_ctz((unsigned)lm);
+                    lm &= lm - 1;
+                    const uint32_t v = ~(uint32_t)sel4(ch, s);
+                    leaf = v >> 2;
+                    cnt = (int)(v & 3u) + 1;
+                    k = 0;
+                    if (COUNT) st.leaves++;
+                }
+                float t, a, b;
+                if (tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT)) {
+                    if (ANY) return true;
+                    h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
+                    hit = true;
+                }
+                k++;
             }
         }
-        if (inner) {
-            int top = 31 - __builtin_clz((unsigned)inner);
-            int rest = inner & ~(1 << top);
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                if (rest & (1 << i)) {
-                    if (!stk_push(c, sp, chv[i])) { st.overflow = true; return hit; }
-                }
-            }
-            if (COUNT && sp > st.max_sp) st.max_sp = sp;
-            int32_t nxt = chv[0];
-#pragma unroll
-            for (int i = 1; i < 4; i++)
-                if (top == i) nxt = chv[i];
+        if (have_next) {
             cur = nxt;
         } else {
             if (sp == 0) break;
@@ -211,11 +237,14 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
 }
 
 // FAST (node boxes known finite) uses the hardware min/max slab test for rays
-// whose origin and 1/d are finite; any other ray takes the exact loop.
+// whose origin and 1/d are finite; any other ray takes the exact loop.  A
+// closest hit's packed slot is resolved to the global prim id here.
 template <bool ANY, bool COUNT, bool FAST = false>
 __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
-    if (FAST && r.finite) return traverse_impl<ANY, COUNT, true>(c, r, tMin, h, st);
-    return traverse_impl<ANY, COUNT, false>(c, r, tMin, h, st);
+    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true>(c, r, tMin, h, st)
+                                        : traverse_impl<ANY, COUNT, false>(c, r, tMin, h, st);
+    if (!ANY && hit) h.prim = c.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3];
+    return hit;
 }
 
 }  // namespace mrt
