@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -37,6 +38,7 @@ void set_error(const std::string& m) { g_err = m; }
 
 enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLOW = 4, CTR_NODES_P = 5, CTR_LEAVES_P = 6, CTR_HITS = 7,
        CTR_WAVE_STEPS_P = 8, CTR_N = 16 };
+static constexpr int kMaxBlocksPerCU = 8;  // 256-thread blocks: 8 waves per SIMD at most
 // counter block: CTR_N u64 statistics, then two launches x 8 tile counters x 128 B
 static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 2 * 8 * 128;
 
@@ -351,11 +353,11 @@ __device__ __forceinline__ v3 camera_dir(const RenderParams& P, int x, int y, co
 // Writes the HitInfo record (t, a, b, prim) to P.hits[slot].
 template <bool COUNT, int MINW, bool FAST>
 __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
-    __shared__ uint16_t s_tab[kTableWords];
+    __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
-    load_tables(P.tables, s_tab, kTableWords / 2);
-    const uint16_t* rcpT = s_tab;
-    const uint16_t* rsqT = s_tab + 2048;
+    load_tables(P.tables, s_tab, 1024);
+    const uint16_t* rcpT = s_tab;           // per triangle test: LDS
+    const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Trav T{P.nodes, P.fast_box != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
@@ -389,11 +391,11 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
 // Kernel 2: Scene::sampleScene shading of the primary hit with shadow rays.
 template <bool COUNT, bool POINT_ONLY, bool FAST>
 __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
-    __shared__ uint16_t s_tab[kTableWords];
+    __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
-    load_tables(P.tables, s_tab, kTableWords / 2);
-    const uint16_t* rcpT = s_tab;
-    const uint16_t* rsqT = s_tab + 2048;
+    load_tables(P.tables, s_tab, 1024);
+    const uint16_t* rcpT = s_tab;           // per triangle test: LDS
+    const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Trav T{P.nodes, P.fast_box != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
@@ -431,13 +433,13 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
 // configs C1-C3): straight-line PointLight::sampleLight + Lambert/Blinn with only
 // the light's three pre-shadow scalars live across the any-hit traversal.
 // Same operations in the same order as Shader::shade.
-template <bool COUNT, bool FAST>
-__global__ void __launch_bounds__(kWG, 6) shade1_kernel(RenderParams P) {
-    __shared__ uint16_t s_tab[kTableWords];
+template <bool COUNT, bool FAST, int MINW>
+__global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
-    load_tables(P.tables, s_tab, kTableWords / 2);
-    const uint16_t* rcpT = s_tab;
-    const uint16_t* rsqT = s_tab + 2048;
+    load_tables(P.tables, s_tab, 1024);
+    const uint16_t* rcpT = s_tab;           // per triangle test: LDS
+    const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Trav T{P.nodes, P.fast_box != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
@@ -584,7 +586,6 @@ struct DeviceState {
     uint8_t* gamma = nullptr;
     int32_t* gstack = nullptr;
     uint32_t gthreads = 0;
-    int grid = 0;
     unsigned long long* ctr = nullptr;
     // scratch for the synchronous API
     float* d_rgb = nullptr;
@@ -593,7 +594,7 @@ struct DeviceState {
     // kernel 1 -> kernel 2 hand-off (per output slot)
     float4* hitbuf = nullptr;
     size_t hit_slots = 0;
-    int grid_primary = 0, grid_shade = 0, grid_primary5 = 0, grid_shade1 = 0;
+    int grid = 0;                // upper bound of any launch (kMaxBlocksPerCU per CU)
     bool boxes_finite = false;
     int cus = 0;
     bool point_only = false;
@@ -604,7 +605,8 @@ struct DeviceState {
 
 // Tuning knobs (mrt_set_tuning): A/B switches for performance work.
 static int g_fast_box = 1;        // hardware min/max box test when its precondition holds
-static int g_primary_waves = 6;   // 0: default launch bounds, 6: ask for 6 waves/SIMD (<= 80 VGPRs)
+static int g_primary_waves = 7;   // launch-bounds occupancy target of the primary kernel: 0 (none), 6, 7, 8
+static int g_shade_waves = 6;     // same for shade1_kernel: 6, 7, 8
 static int g_lds_pad_kb = 0;      // extra dynamic LDS per workgroup (occupancy sweeps)
 static int g_sched = 2;           // TileSched mode 0..3 (2 measured fastest)
 static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
@@ -702,18 +704,8 @@ static int ensure_device(Scene& s, int device) {
     // persistent grid: resident workgroups on every CU
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device));
-    int per_cu1 = 0, per_cu2 = 0, per_cu5 = 0;
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu1, (primary_kernel<false, 1, false>), kWG, 0));
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu5, (primary_kernel<false, 6, false>), kWG, 0));
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, (shade_kernel<false, false, false>), kWG, 0));
     d.cus = prop.multiProcessorCount;
-    int per_cu3 = 0;
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu3, (shade1_kernel<false, false>), kWG, 0));
-    d.grid_shade1 = prop.multiProcessorCount * std::max(per_cu3, 1);
-    d.grid_primary = prop.multiProcessorCount * std::max(per_cu1, 1);
-    d.grid_primary5 = prop.multiProcessorCount * std::max(per_cu5, 1);
-    d.grid_shade = prop.multiProcessorCount * std::max(per_cu2, 1);
-    d.grid = std::max(std::max(std::max(d.grid_primary, d.grid_primary5), d.grid_shade), d.grid_shade1);
+    d.grid = d.cus * kMaxBlocksPerCU;
     d.boxes_finite = true;
     for (const QNode& q : s.nodes)
         for (int k = 0; k < 24; k++) d.boxes_finite &= std::isfinite(q.box[k]);
@@ -774,6 +766,58 @@ static int ensure_slots(DeviceState& d, size_t slots) {
     return MRT_OK;
 }
 
+
+using KernelFn = void (*)(RenderParams);
+
+// Resident workgroups per CU of one kernel instantiation (occupancy API, cached).
+// An over-estimate only queues blocks behind the resident ones: the tile
+// schedule (sched 2/3) keeps late blocks useful.
+static int blocks_per_cu(KernelFn f, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, size_t>, int> cache;
+    std::lock_guard<std::mutex> g(mu);
+    const auto key = std::make_pair(reinterpret_cast<const void*>(f), lds);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(f), kWG, lds) != hipSuccess) n = 1;
+    n = std::max(1, std::min(n, kMaxBlocksPerCU));
+    cache[key] = n;
+    return n;
+}
+
+template <int W>
+static KernelFn primary_fn(bool c, bool f) {
+    return c ? (f ? primary_kernel<true, W, true> : primary_kernel<true, W, false>)
+             : (f ? primary_kernel<false, W, true> : primary_kernel<false, W, false>);
+}
+static KernelFn pick_primary(int w, bool c, bool f) {
+    switch (w) {
+        case 6: return primary_fn<6>(c, f);
+        case 7: return primary_fn<7>(c, f);
+        case 8: return primary_fn<8>(c, f);
+        default: return primary_fn<1>(c, f);
+    }
+}
+template <int W>
+static KernelFn shade1_fn(bool c, bool f) {
+    return c ? (f ? shade1_kernel<true, true, W> : shade1_kernel<true, false, W>)
+             : (f ? shade1_kernel<false, true, W> : shade1_kernel<false, false, W>);
+}
+static KernelFn pick_shade1(int w, bool c, bool f) {
+    switch (w) {
+        case 7: return shade1_fn<7>(c, f);
+        case 8: return shade1_fn<8>(c, f);
+        default: return shade1_fn<6>(c, f);
+    }
+}
+static KernelFn pick_shade(bool c, bool po, bool f) {
+    if (po) return c ? (f ? shade_kernel<true, true, true> : shade_kernel<true, true, false>)
+                     : (f ? shade_kernel<false, true, true> : shade_kernel<false, true, false>);
+    return c ? (f ? shade_kernel<true, false, true> : shade_kernel<true, false, false>)
+             : (f ? shade_kernel<false, false, true> : shade_kernel<false, false, false>);
+}
+
 // Two launches on `stream`: primary rays -> hit records, then shading with
 // shadow rays.  Events bracket both (kernel_ms covers the whole frame).
 static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hipStream_t stream) {
@@ -786,46 +830,21 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     HIP_OK(hipMemsetAsync(d.ctr, 0, kCtrBytes, stream));
     unsigned int* qbase = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(d.ctr) + CTR_N * sizeof(unsigned long long));
     P.queue = qbase;
-    const bool w5 = g_primary_waves == 6;
     const size_t pad = (size_t)g_lds_pad_kb * 1024;
-    int g1 = std::max(1, std::min(w5 ? d.grid_primary5 : d.grid_primary, (P.n_tiles + 3) / 4));
-    int g2 = std::max(1, std::min(d.grid_shade, (P.n_tiles + 3) / 4));
-    if (pad) {
-        int pc1 = 0, pc2 = 0;
-        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc1, (primary_kernel<false, 6, false>), kWG, pad));
-        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc2, (shade_kernel<false, true, false>), kWG, pad));
-        g1 = std::max(1, std::min(g1, d.cus * std::max(pc1, 1)));
-        g2 = std::max(1, std::min(g2, d.cus * std::max(pc2, 1)));
-    }
+    const int items = (P.n_tiles + 3) / 4;
+    auto launch = [&](KernelFn f) -> int {
+        const int g = std::max(1, std::min(std::min(d.grid, d.cus * blocks_per_cu(f, pad)), items));
+        void* args[] = {&P};
+        HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(f), dim3(g), dim3(kWG), args, pad, stream));
+        return MRT_OK;
+    };
     HIP_OK(hipEventRecord(d.ev0, stream));
     const bool fb = P.fast_box != 0;
-#define MRT_PRIMARY(C, W, F) hipLaunchKernelGGL((primary_kernel<C, W, F>), dim3(g1), dim3(kWG), pad, stream, P)
-#define MRT_SHADE(C, PO, F) hipLaunchKernelGGL((shade_kernel<C, PO, F>), dim3(g2), dim3(kWG), pad, stream, P)
-    if (count) {
-        if (w5) { if (fb) MRT_PRIMARY(true, 6, true); else MRT_PRIMARY(true, 6, false); }
-        else { if (fb) MRT_PRIMARY(true, 1, true); else MRT_PRIMARY(true, 1, false); }
-    } else {
-        if (w5) { if (fb) MRT_PRIMARY(false, 6, true); else MRT_PRIMARY(false, 6, false); }
-        else { if (fb) MRT_PRIMARY(false, 1, true); else MRT_PRIMARY(false, 1, false); }
-    }
+    if ((rc = launch(pick_primary(g_primary_waves, count, fb)))) return rc;
     HIP_OK(hipEventRecord(d.evm, stream));
     P.queue = qbase + 8 * 32;
     const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1;
-    if (one) {
-        const int g3 = std::max(1, std::min(d.grid_shade1, (P.n_tiles + 3) / 4));
-#define MRT_SHADE1(C, F) hipLaunchKernelGGL((shade1_kernel<C, F>), dim3(g3), dim3(kWG), pad, stream, P)
-        if (count) { if (fb) MRT_SHADE1(true, true); else MRT_SHADE1(true, false); }
-        else { if (fb) MRT_SHADE1(false, true); else MRT_SHADE1(false, false); }
-#undef MRT_SHADE1
-    } else if (d.point_only) {
-        if (count) { if (fb) MRT_SHADE(true, true, true); else MRT_SHADE(true, true, false); }
-        else { if (fb) MRT_SHADE(false, true, true); else MRT_SHADE(false, true, false); }
-    } else {
-        if (count) { if (fb) MRT_SHADE(true, false, true); else MRT_SHADE(true, false, false); }
-        else { if (fb) MRT_SHADE(false, false, true); else MRT_SHADE(false, false, false); }
-    }
-#undef MRT_PRIMARY
-#undef MRT_SHADE
+    if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb)))) return rc;
     d.last_was_render = true;
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d.ev1, stream));
@@ -1202,8 +1221,11 @@ int mrt_set_tuning(const char* key, int value) {
     std::string k(key);
     if (k == "fast_box") g_fast_box = value ? 1 : 0;
     else if (k == "primary_waves") {
-        if (value != 0 && value != 1 && value != 6) { set_error("primary_waves must be 0 or 6"); return MRT_ERR_INVALID; }
+        if (value != 0 && value != 1 && (value < 6 || value > 8)) { set_error("primary_waves must be 0 or 6..8"); return MRT_ERR_INVALID; }
         g_primary_waves = value;
+    } else if (k == "shade_waves") {
+        if (value != 6 && value != 7 && value != 8) { set_error("shade_waves must be 6, 7 or 8"); return MRT_ERR_INVALID; }
+        g_shade_waves = value;
     } else if (k == "shade1") {
         g_shade1 = value ? 1 : 0;
     } else if (k == "sched") {

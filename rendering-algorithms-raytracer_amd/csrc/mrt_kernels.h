@@ -77,8 +77,10 @@ __device__ __forceinline__ int32_t stk_pop(const Trav& c, int& sp) {
     return sp < kLdsStack ? c.lds[sp * kWG] : c.gstk[(size_t)(sp - kLdsStack) * c.gstride];
 }
 
+// v[i] for a lane-varying i as three selects (no divergent branch tree).
 __device__ __forceinline__ int32_t sel4(const int4& v, int i) {
-    return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+    const int32_t lo = (i & 1) ? v.y : v.x, hi = (i & 1) ? v.w : v.z;
+    return (i & 2) ? hi : lo;
 }
 
 // One triangle of intersect4 (src/BVH.cpp:1298-1459), same operations and

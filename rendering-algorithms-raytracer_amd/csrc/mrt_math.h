@@ -26,30 +26,45 @@ namespace mrt {
 MRT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 MRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 
+// Device: an empty asm on a value keeps the load that produced it on the
+// straight-line path (otherwise the compiler sinks the table load into a
+// divergent branch around the rare NaN/inf inputs).
+#ifdef __HIP_DEVICE_COMPILE__
+#define MRT_OPAQUE(v) asm volatile("" : "+v"(v))
+#else
+#define MRT_OPAQUE(v) (void)0
+#endif
+
 // 12-bit packed table entry -> float bits in [0.5, 1)
 MRT_HD uint32_t tbl_bits(uint16_t e) { return 0x3F000000u | ((uint32_t)e << 11); }
 
-// RCPSS emulation; T = 2048-entry packed rcp table.
+// RCPSS emulation; T = 2048-entry packed rcp table.  Written as a select chain
+// (lowest priority first) so device code has no divergent branches; the table
+// index is in range for every input.
 MRT_HD float x86_rcp(float x, const uint16_t* T) {
-    uint32_t u = f2u(x), s = u & 0x80000000u, e = (u >> 23) & 0xFFu, m = u & 0x7FFFFFu;
-    if (e == 0xFFu) return u2f(m ? (u | 0x00400000u) : s);
-    if (e == 0u) return u2f(s | 0x7F800000u);
+    const uint32_t u = f2u(x), s = u & 0x80000000u, e = (u >> 23) & 0xFFu, m = u & 0x7FFFFFu;
     uint32_t t = tbl_bits(T[m >> 12]);
-    int re = 126 - ((int)e - 127);
-    if (re <= 0) return u2f(s);
-    return u2f(s | ((uint32_t)re << 23) | (t & 0x7FFFFFu));
+    MRT_OPAQUE(t);
+    const int re = 253 - (int)e;                                   // 126 - (e - 127)
+    uint32_t r = re <= 0 ? s : (s | ((uint32_t)re << 23) | (t & 0x7FFFFFu));
+    r = e == 0u ? (s | 0x7F800000u) : r;                          // zero / denormal -> inf
+    MRT_OPAQUE(r);
+    r = e == 0xFFu ? (m ? (u | 0x00400000u) : s) : r;              // NaN -> quiet, inf -> 0
+    return u2f(r);
 }
 
 // RSQRTSS emulation; T = 2048-entry packed rsqrt table ([odd exponent][10 bits]).
 MRT_HD float x86_rsqrt(float x, const uint16_t* T) {
-    uint32_t u = f2u(x), s = u & 0x80000000u, e = (u >> 23) & 0xFFu, m = u & 0x7FFFFFu;
-    if (e == 0xFFu) return u2f(m ? (u | 0x00400000u) : (s ? 0xFFC00000u : 0u));
-    if (e == 0u) return u2f(s | 0x7F800000u);
-    if (s) return u2f(0xFFC00000u);
-    int E = (int)e - 127, odd = E & 1, k = (E - odd) / 2;
+    const uint32_t u = f2u(x), s = u & 0x80000000u, e = (u >> 23) & 0xFFu, m = u & 0x7FFFFFu;
+    const int E = (int)e - 127, odd = E & 1, k = (E - odd) >> 1;    // E - odd is even: exact halving
     uint32_t t = tbl_bits(T[(odd << 10) | (m >> 13)]);
-    int re = 126 - k;
-    return u2f(((uint32_t)re << 23) | (t & 0x7FFFFFu));
+    MRT_OPAQUE(t);
+    uint32_t r = ((uint32_t)(126 - k) << 23) | (t & 0x7FFFFFu);
+    r = s ? 0xFFC00000u : r;                                       // negative -> NaN
+    r = e == 0u ? (s | 0x7F800000u) : r;                          // +-0 / denormal -> +-inf
+    MRT_OPAQUE(r);
+    r = e == 0xFFu ? (m ? (u | 0x00400000u) : (s ? 0xFFC00000u : 0u)) : r;
+    return u2f(r);
 }
 
 // recipss / recipps (src/SSE.h:67-86)

@@ -53,6 +53,24 @@ def test_product_matches_oracle_random():
         assert u(a) == u(b) or (np.isnan(a) and np.isnan(b))
 
 
+def test_product_matches_oracle_specials():
+    """Every exponent class of the select-chain emulation: zeros, denormals,
+    smallest/largest normals, results that flush, infinities, NaNs, negatives."""
+    pats = [0x00000000, 0x80000000, 0x00000001, 0x807FFFFF, 0x00400000, 0x00800000, 0x80800000,
+            0x01000000, 0x3F800000, 0xBF800000, 0x3F7FFFFF, 0x7E800000, 0x7E7FFFFF, 0x7EFFFFFF, 0x7F000000,
+            0x7F7FFFFF, 0xFF7FFFFF, 0x7F800000, 0xFF800000, 0x7FC00000, 0xFFC00001, 0x7F800001, 0x40490FDB]
+    for e in range(256):                      # every exponent, two mantissas, both signs
+        for m in (0, 0x5A5A5A):
+            pats += [(e << 23) | m, 0x80000000 | (e << 23) | m]
+    for p in pats:
+        x = struct.unpack("<f", struct.pack("<I", p))[0]
+        for fo, fp in ((O.rcp_nr, miro.rcp_nr), (O.rsqrt_nr, miro.rsqrt_nr), (O.x86_rcp, None)):
+            if fp is None:
+                continue
+            a, b = fo(x), fp(x)
+            assert u(a) == u(b) or (np.isnan(a) and np.isnan(b)), hex(p)
+
+
 @pytest.mark.skipif(not is_intel() or platform.machine() != "x86_64", reason="tables are Intel RCPSS/RSQRTSS")
 def test_tables_match_live_instructions(tmp_path):
     """Re-derive the tables from live RCPSS/RSQRTSS and compare with the committed
