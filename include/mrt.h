@@ -107,6 +107,8 @@ typedef struct {
     uint64_t primary_hits;               /* primary rays that hit geometry               */
     uint64_t primary_wave_steps;         /* count mode: sum over tiles of the max node
                                             visits of a lane (x64 = issued lane-steps)   */
+    uint64_t primary_uniform_visits;     /* count mode: primary node visits made in wave
+                                            steps where all active lanes were on one node */
     float kernel_ms;                     /* device time of the last frame (all launches)*/
     float primary_ms, shade_ms;          /* per launch: primary rays / shade + shadows  */
     int32_t max_stack;                   /* deepest traversal stack seen (count mode)   */

@@ -1132,11 +1132,11 @@ int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H, int x0, 
     if (y1 > H) y1 = H;
     oro_gamma_table(NULL);
     cam_basis b = camera_basis(cam, W, H);
-    uint64_t prim = 0, shadowr = 0, nodes = 0, leaves = 0;
+    uint64_t prim = 0, shadowr = 0, nodes = 0, leaves = 0, pnodes = 0, pleaves = 0;
     int err = 0;
 #ifdef _OPENMP
     if (n_threads < 1) n_threads = 1;
-#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads) reduction(+:prim,shadowr,nodes,leaves)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads) reduction(+:prim,shadowr,nodes,leaves,pnodes,pleaves)
 #endif
     for (int y = y0; y < y1; y++) {
         for (int x = x0; x < x1; x++) {
@@ -1154,8 +1154,12 @@ int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H, int x0, 
             if (hitout) { hitout[p].t = h.t; hitout[p].a = h.a; hitout[p].b = h.b; hitout[p].prim = h.prim; }
             if (shadow) shadow[p] = c.shadow_mask;
             prim++; shadowr += c.shadow_rays; nodes += nv + c.nodes; leaves += lv + c.leaves;
+            pnodes += nv; pleaves += lv;
         }
     }
-    if (counters) { counters[0] += prim; counters[1] += shadowr; counters[2] += nodes; counters[3] += leaves; }
+    if (counters) {
+        counters[0] += prim; counters[1] += shadowr; counters[2] += nodes; counters[3] += leaves;
+        counters[4] += pnodes; counters[5] += pleaves;
+    }
     return err;
 }

@@ -94,7 +94,8 @@ int oro_trace(const oro_scene* s, size_t n, const float* o /*3n*/, const float* 
  * 1 spp, Scene::adaptiveSampleScene with min=max subdivs=1 (src/Scene.cpp:252-293).
  * rgb: W*H*3 floats (before Image::Map), rgb8: W*H*3 (after Map), hit: W*H
  * primary hit records, shadow: W*H bitmask of occluded lights, may be NULL.
- * counters[4] (nullable) += {primary rays, shadow rays, node visits, leaf visits}.
+ * counters[6] (nullable) += {primary rays, shadow rays, node visits, leaf visits,
+ *                            primary-ray node visits, primary-ray leaf visits}.
  * n_threads > 1 uses OpenMP over rows (the oracle is deterministic per pixel). */
 int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H,
                int x0, int y0, int x1, int y1,

@@ -214,7 +214,7 @@ class OracleScene:
         rgb8 = np.zeros((H, W, 3), np.uint8)
         hits = np.zeros((H, W), HIT_DTYPE) if want_hits else None
         shadow = np.zeros((H, W), np.uint32)
-        counters = np.zeros(4, np.uint64)
+        counters = np.zeros(6, np.uint64)
         r = self.L.oro_render(self.h, C.byref(c), W, H, x0, y0, x1, y1, _p(rgb, _fp), _p(rgb8, _u8p),
                               hits.ctypes.data if hits is not None else None, _p(shadow, _u32p),
                               _p(counters, _u64p), int(threads))
@@ -222,7 +222,8 @@ class OracleScene:
             raise RuntimeError(f"oracle render failed ({r})")
         return {"rgb": rgb, "rgb8": rgb8, "hits": hits, "shadow": shadow,
                 "primary_rays": int(counters[0]), "shadow_rays": int(counters[1]),
-                "node_visits": int(counters[2]), "leaf_visits": int(counters[3])}
+                "node_visits": int(counters[2]), "leaf_visits": int(counters[3]),
+                "primary_node_visits": int(counters[4]), "primary_leaf_visits": int(counters[5])}
 
 
 def x86_rcp(x):

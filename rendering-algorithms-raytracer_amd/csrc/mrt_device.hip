@@ -37,7 +37,7 @@ void set_error(const std::string& m) { g_err = m; }
     } while (0)
 
 enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLOW = 4, CTR_NODES_P = 5, CTR_LEAVES_P = 6, CTR_HITS = 7,
-       CTR_WAVE_STEPS_P = 8, CTR_N = 16 };
+       CTR_WAVE_STEPS_P = 8, CTR_UNIFORM_P = 9, CTR_N = 16 };
 static constexpr int kMaxBlocksPerCU = 8;  // 256-thread blocks: 8 waves per SIMD at most
 // counter block: CTR_N u64 statistics, then two launches x 8 tile counters x 128 B
 static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 2 * 8 * 128;
@@ -61,6 +61,7 @@ struct RenderParams {
     uint32_t seed;
     int32_t fast_box;            // node boxes finite && tuning allows the hardware min/max box test
     int32_t sched;               // tile schedule (TileSched)
+    int32_t scalar_nodes;        // scalar fetch of wave-uniform nodes
     unsigned int* queue;         // 8 tile counters, 32 words apart (sched >= 2)
     // work: 8x8 tiles
     int32_t tiles_x, n_tiles;    // frame mode: tiles_x = ceil(W/8)
@@ -315,11 +316,12 @@ __device__ __forceinline__ void flush_stats(const RenderParams& P, const TravSta
     for (int off = 32; off > 0; off >>= 1) sh += __shfl_down(sh, off);
     if (lane == 0 && sh) atomicAdd(&P.ctr[PRIMARY ? CTR_HITS : CTR_SHADOW], sh);
     if (COUNT) {
-        unsigned long long nv = st.nodes, lv = st.leaves;
+        unsigned long long nv = st.nodes, lv = st.leaves, uv = st.uniform;
         int msp = st.max_sp;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             lv += __shfl_down(lv, off);
+            uv += __shfl_down(uv, off);
             msp = max(msp, __shfl_down(msp, off));
         }
         if (lane == 0) {
@@ -328,6 +330,7 @@ __device__ __forceinline__ void flush_stats(const RenderParams& P, const TravSta
             if (PRIMARY) {
                 atomicAdd(&P.ctr[CTR_NODES_P], nv);
                 atomicAdd(&P.ctr[CTR_LEAVES_P], lv);
+                atomicAdd(&P.ctr[CTR_UNIFORM_P], uv);
             }
             atomicMax(&P.ctr[CTR_MAXSP], (unsigned long long)msp);
         }
@@ -359,7 +362,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.fast_box != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
     uint32_t nhits = 0;
     const CamParams& cam = P.cam;
@@ -397,7 +400,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.fast_box != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
     uint32_t shadow_total = 0;
     const CamParams& cam = P.cam;
@@ -441,7 +444,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.fast_box != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
     uint32_t shadow_total = 0;
     const v3 eye = mk(P.cam.eye[0], P.cam.eye[1], P.cam.eye[2]);
@@ -544,7 +547,7 @@ __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DL
     for (int i = tid; i < 1024; i += kWG) reinterpret_cast<uint32_t*>(s_tab)[i] = reinterpret_cast<const uint32_t*>(tables)[i];
     __syncthreads();
     const uint32_t gtid = blockIdx.x * kWG + tid;
-    Trav T{nodes, fast_box != 0, leaves, s_tab, s_stack + tid, gstack + gtid, gstride};
+    Trav T{nodes, fast_box != 0, false, leaves, s_tab, s_stack + tid, gstack + gtid, gstride};
     TravStats st;
     for (size_t i = (size_t)blockIdx.x * kWG + tid; i < n; i += (size_t)gridDim.x * kWG) {
         DRay r = make_ray(mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]));
@@ -609,6 +612,7 @@ static int g_primary_waves = 7;   // launch-bounds occupancy target of the prima
 static int g_shade_waves = 6;     // same for shade1_kernel: 6, 7, 8
 static int g_lds_pad_kb = 0;      // extra dynamic LDS per workgroup (occupancy sweeps)
 static int g_sched = 2;           // TileSched mode 0..3 (2 measured fastest)
+static int g_scalar_nodes = 1;    // scalar-cache fetch of wave-uniform nodes
 static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
 
 static inline int fast_box(const DeviceState& d);
@@ -827,6 +831,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     P.hits = d.hitbuf;
     P.fast_box = fast_box(d);
     P.sched = g_sched;
+    P.scalar_nodes = g_scalar_nodes;
     HIP_OK(hipMemsetAsync(d.ctr, 0, kCtrBytes, stream));
     unsigned int* qbase = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(d.ctr) + CTR_N * sizeof(unsigned long long));
     P.queue = qbase;
@@ -1151,6 +1156,7 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     S.last.shadow_rays = c[CTR_SHADOW];
     S.last.primary_hits = c[CTR_HITS];
     S.last.primary_wave_steps = c[CTR_WAVE_STEPS_P];
+    S.last.primary_uniform_visits = c[CTR_UNIFORM_P];
     S.last.node_visits = c[CTR_NODES];
     S.last.leaf_visits = c[CTR_LEAVES];
     S.last.max_stack = (int32_t)c[CTR_MAXSP];
@@ -1226,6 +1232,8 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "shade_waves") {
         if (value != 6 && value != 7 && value != 8) { set_error("shade_waves must be 6, 7 or 8"); return MRT_ERR_INVALID; }
         g_shade_waves = value;
+    } else if (k == "scalar_nodes") {
+        g_scalar_nodes = value ? 1 : 0;
     } else if (k == "shade1") {
         g_shade1 = value ? 1 : 0;
     } else if (k == "sched") {

@@ -52,6 +52,7 @@ struct DHit {
 struct Trav {
     const QNode* __restrict__ nodes;
     bool fast_box;            // all node boxes finite and fast box test enabled
+    bool scalar_nodes;        // scalar fetch of wave-uniform nodes (tuning)
     const DLeaf* __restrict__ leaves;
     const uint16_t* rcpT;     // LDS
     int32_t* lds;             // this lane's LDS stack column (stride kWG)
@@ -60,7 +61,7 @@ struct Trav {
 };
 
 struct TravStats {
-    uint32_t nodes = 0, leaves = 0;
+    uint32_t nodes = 0, leaves = 0, uniform = 0;  // uniform: visits in wave-uniform node steps
     int max_sp = 0;
     bool overflow = false;
 };
@@ -174,10 +175,36 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
     int32_t cur = 0;
     bool hit = false;
     while (true) {
-        const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
-        const int4 ch = reinterpret_cast<const int4*>(q)[6];
-        const int m = FAST ? box_test_fast(q, r, tMin, h.t) : box_test(q, r, tMin, h.t);
-        if (COUNT) st.nodes++;
+        // stack top read at the start of the step: the LDS latency overlaps the
+        // node fetch and box test (used only if this step pops)
+        const int32_t peek = c.lds[(sp > 0 && sp <= kLdsStack ? sp - 1 : 0) * kWG];
+        int m;
+        int4 ch;
+        // Wave-uniform node (all active lanes on one node, ~70% of primary
+        // steps): fetch it once through the scalar cache into SGPRs instead of
+        // 64 copies through the vector memory path.
+        const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
+        if (FAST && c.scalar_nodes && __ballot(cur != c0) == 0) {
+            // constant address space + uniform address -> s_load_dwordx16 (node
+            // data is read-only for the whole launch)
+            typedef const __attribute__((address_space(4))) float cfloat;
+            typedef const __attribute__((address_space(4))) int32_t cint;
+            cfloat* q = (cfloat*)(const void*)(c.nodes + c0);
+            cint* qc = (cint*)(q + 24);
+            ch = make_int4(qc[0], qc[1], qc[2], qc[3]);
+            float4 bx[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
+            m = box_test_fast(bx, r, tMin, h.t);
+        } else {
+            const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
+            ch = reinterpret_cast<const int4*>(q)[6];
+            m = FAST ? box_test_fast(q, r, tMin, h.t) : box_test(q, r, tMin, h.t);
+        }
+        if (COUNT) {
+            st.nodes++;
+            if (__ballot(cur != c0) == 0) st.uniform++;  // all active lanes of the wave on one node
+        }
         const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
         const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
                            (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
@@ -232,8 +259,94 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
             cur = nxt;
         } else {
             if (sp == 0) break;
-            cur = stk_pop(c, sp);
+            if (sp <= kLdsStack) { cur = peek; sp--; }
+            else cur = stk_pop(c, sp);
         }
+    }
+    return hit;
+}
+
+struct NodeData {
+    float4 b[6];
+    int4 ch;
+};
+__device__ __forceinline__ NodeData load_node(const QNode* __restrict__ nodes, int32_t i) {
+    const float4* q = reinterpret_cast<const float4*>(nodes + i);
+    NodeData n;
+#pragma unroll
+    for (int k = 0; k < 6; k++) n.b[k] = q[k];
+    n.ch = reinterpret_cast<const int4*>(q)[6];
+    return n;
+}
+
+// traverse_impl<FAST = true> with the next node's fetch issued before the
+// current node's leaf triangles are tested.  The next node is fixed by the box
+// mask and the stack alone; only its box TEST needs the t the leaves may
+// lower, so the visit order (and every result) is unchanged while the node
+// fetch latency hides behind the triangle work.
+template <bool ANY, bool COUNT>
+__device__ bool traverse_pf(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
+    int sp = 0;
+    bool hit = false;
+    NodeData nd = load_node(c.nodes, 0);
+    while (true) {
+        const int32_t peek = c.lds[(sp > 0 && sp <= kLdsStack ? sp - 1 : 0) * kWG];
+        const int m = box_test_fast(nd.b, r, tMin, h.t);
+        const int4 ch = nd.ch;
+        if (COUNT) st.nodes++;
+        const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
+        const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
+                           (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
+        const int inner = m & isinner;
+        int lm = m & isleaf;
+        int32_t next = -1;
+        if (inner) {
+            const int top = 31 - __builtin_clz((unsigned)inner);
+            const int rest = inner ^ (1 << top);
+            if (rest) {
+                if (sp + 4 <= kLdsStack) {
+                    c.lds[sp * kWG] = ch.x; sp += rest & 1;
+                    c.lds[sp * kWG] = ch.y; sp += (rest >> 1) & 1;
+                    c.lds[sp * kWG] = ch.z; sp += (rest >> 2) & 1;
+                    c.lds[sp * kWG] = ch.w; sp += (rest >> 3) & 1;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if ((rest >> i) & 1)
+                            if (!stk_push(c, sp, sel4(ch, i))) { st.overflow = true; return hit; }
+                }
+                if (COUNT && sp > st.max_sp) st.max_sp = sp;
+            }
+            next = sel4(ch, top);
+        } else if (sp > 0) {
+            if (sp <= kLdsStack) { next = peek; sp--; }
+            else next = stk_pop(c, sp);
+        }
+        if (next >= 0) nd = load_node(c.nodes, next);
+        if (lm) {
+            uint32_t leaf = 0;
+            int k = 0, cnt = 0;
+            while (true) {
+                if (k == cnt) {
+                    if (!lm) break;
+                    const int s = __builtin_ctz((unsigned)lm);
+                    lm &= lm - 1;
+                    const uint32_t v = ~(uint32_t)sel4(ch, s);
+                    leaf = v >> 2;
+                    cnt = (int)(v & 3u) + 1;
+                    k = 0;
+                    if (COUNT) st.leaves++;
+                }
+                float t, a, b;
+                if (tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT)) {
+                    if (ANY) return true;
+                    h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
+                    hit = true;
+                }
+                k++;
+            }
+        }
+        if (next < 0) break;
     }
     return hit;
 }
@@ -243,8 +356,13 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
 // closest hit's packed slot is resolved to the global prim id here.
 template <bool ANY, bool COUNT, bool FAST = false>
 __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
+#ifdef MRT_PREFETCH  // build variant (make variant NAME=pf EXTRA=-DMRT_PREFETCH) for A/B runs
+    const bool hit = (FAST && r.finite) ? traverse_pf<ANY, COUNT>(c, r, tMin, h, st)
+                                        : traverse_impl<ANY, COUNT, false>(c, r, tMin, h, st);
+#else
     const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true>(c, r, tMin, h, st)
                                         : traverse_impl<ANY, COUNT, false>(c, r, tMin, h, st);
+#endif
     if (!ANY && hit) h.prim = c.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3];
     return hit;
 }

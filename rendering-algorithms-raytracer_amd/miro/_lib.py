@@ -63,7 +63,8 @@ class mrt_render_opts(C.Structure):
 class mrt_stats(C.Structure):
     _fields_ = [("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("node_visits", C.c_uint64),
                 ("leaf_visits", C.c_uint64), ("primary_node_visits", C.c_uint64),
-                ("primary_leaf_visits", C.c_uint64), ("primary_hits", C.c_uint64), ("primary_wave_steps", C.c_uint64), ("kernel_ms", C.c_float), ("primary_ms", C.c_float),
+                ("primary_leaf_visits", C.c_uint64), ("primary_hits", C.c_uint64), ("primary_wave_steps", C.c_uint64),
+                ("primary_uniform_visits", C.c_uint64), ("kernel_ms", C.c_float), ("primary_ms", C.c_float),
                 ("shade_ms", C.c_float), ("max_stack", C.c_int32)]
 
 

@@ -59,6 +59,10 @@ def test_configs_match_oracle(key, W, H):
          "a": ref["hits"]["a"], "b": ref["hits"]["b"]}
     assert_frame_equal(img, hits, r)
     assert P.last_stats["shadow_rays"] == ref["shadow_rays"]
+    # same traversal, node for node: primary-ray visit counts equal the oracle's
+    # (shadow rays are any-hit on the device, closest-hit in the oracle)
+    assert P.last_stats["primary_node_visits"] == ref["primary_node_visits"]
+    assert P.last_stats["primary_leaf_visits"] == ref["primary_leaf_visits"]
 
 
 def test_full_hd_sponza_rows_match_oracle():
@@ -153,7 +157,8 @@ def test_edge_cases():
                                    dict(shade1=1, fast_box=1, sched=1, primary_waves=6),
                                    dict(shade1=0, fast_box=1, sched=2, primary_waves=0),
                                    dict(shade1=1, fast_box=0, sched=3, primary_waves=6),
-                                   dict(shade1=1, fast_box=1, sched=2, primary_waves=6)])
+                                   dict(shade1=1, fast_box=1, sched=2, primary_waves=6, scalar_nodes=0),
+                                   dict(shade1=1, fast_box=1, sched=2, primary_waves=8, scalar_nodes=1)])
 def test_every_kernel_path_is_exact(knobs):
     """Performance switches must not change a single bit (fused vs split shading,
     hardware vs select box test, XCD schedule, occupancy build)."""
@@ -165,10 +170,13 @@ def test_every_kernel_path_is_exact(knobs):
         img, hits = render(P, cam, 160, 120)
         ref = Osc.render(cam, 160, 120, threads=8)
         assert np.array_equal(bits(img.rgb), bits(ref["rgb"]))
+        img_c, _ = render(P, cam, 160, 120, count_visits=True)
+        assert P.last_stats["primary_node_visits"] == ref["primary_node_visits"]
+        assert P.last_stats["primary_leaf_visits"] == ref["primary_leaf_visits"]
         assert np.array_equal(hits["prim"], ref["hits"]["prim"])
         assert P.last_stats["shadow_rays"] == ref["shadow_rays"]
     finally:
-        for k, v in dict(shade1=1, fast_box=1, sched=2, primary_waves=6).items():
+        for k, v in dict(shade1=1, fast_box=1, sched=2, primary_waves=7, scalar_nodes=1).items():
             L.mrt_set_tuning(k.encode(), v)
 
 

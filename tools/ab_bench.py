@@ -55,7 +55,7 @@ def main():
         assert np.array_equal(ref, out), f"variant {v} changed the frame!"
         _, _, st = run(v, count=True, reps=1)
         print("variant", v, "counts", {k: st[k] for k in ("node_visits", "leaf_visits", "primary_node_visits",
-                                                          "max_stack", "shadow_rays", "primary_hits")},
+                                                          "max_stack", "shadow_rays", "primary_hits", "primary_uniform_visits")},
               "primary SIMD util %.3f" % (st["primary_node_visits"] / max(1, 64 * st["primary_wave_steps"])), flush=True)
     for r in range(rounds):
         for v in variants:
