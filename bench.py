@@ -3,13 +3,18 @@
 (1920x1080, 1 spp, Blinn + PointLight; synthetic ~68k-triangle stand-in for the
 missing sponza.obj) -- BASELINE.json `metric` / configs[2].
 
-One "step" = one full frame: primary rays + shadow rays + shading + Image::Map.
-N = 1: the frame renders straight into HBM buffers.  N > 1 (torch.distributed,
-one process per GPU, backend nccl = RCCL): 32x32 buckets are dealt b mod N
-(reference bucket grid, src/Scene.cpp:90-95), every rank renders its buckets
-into a packed tile buffer, one RCCL gather brings them to rank 0, which
-scatters them into the frame.  value = rays of the whole frame / max-over-ranks
-wall time.  Rank 0 prints one JSON line.
+One "step" = one pass of the hot path over one batch: primary rays + shadow
+rays + shading + Image::Map.
+N = 1: one frame per step, rendered straight into HBM buffers (whole-frame
+launch pair).  N > 1 (torch.distributed, one process per GPU, backend nccl =
+RCCL): weak scaling -- a step renders a camera path of N frames (frame 0 is the
+config camera, then 2.5-degree pans), the 32x32 buckets of all N frames are
+dealt id mod N (reference bucket grid, src/Scene.cpp:90-95), every rank renders
+its share in one launch pair into packed 8-bit tiles, one RCCL gather per step
+brings them to rank 0, which scatters them into the N frames; the gather of
+step k overlaps the render of step k + 1 (miro/tiles.py BatchPipeline).
+value = rays of all frames of all steps / max-over-ranks wall time.  Rank 0
+prints one JSON line.
 """
 from __future__ import annotations
 
@@ -34,18 +39,34 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--frames", type=int, default=0, help="frames per step (default: 1 at N=1, N at N>1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-thread-seconds for the oracle sample")
     return ap.parse_args()
 
 
-def kernel_bytes(st, px, hits):
+def _camera(c):
+    import miro
+    cam = miro.Camera()
+    cam.setEye(c["eye"]); cam.setLookAt(c["lookAt"]); cam.setUp(c["up"]); cam.setFOV(c["fov"])
+    return cam
+
+
+def _pixels_in_frame(ids, bpf, bx, W, H):
+    n = 0
+    for i in ids:
+        b = i % bpf
+        n += min(32, W - (b % bx) * 32) * min(32, H - (b // bx) * 32)
+    return n
+
+
+def kernel_bytes(st, px, hits, float_out=True):
     """Algorithmic bytes per launch: node/leaf visits x
     their sizes + per-pixel ray I/O + per-hit shading gathers."""
     pn, pl = st["primary_node_visits"], st["primary_leaf_visits"]
     sn, sl = st["node_visits"] - pn, st["leaf_visits"] - pl
     primary = pn * NODE_B + pl * LEAF_B + px * 16                 # write the 16-B hit record
     # read the hit record, write float RGB + RGB8; per hit: PrimShade + 3 vertices + 3 normals
-    shade = sn * NODE_B + sl * LEAF_B + px * (16 + 12 + 3) + hits * (32 + 3 * 16 + 3 * 16)
+    shade = sn * NODE_B + sl * LEAF_B + px * (16 + (12 if float_out else 0) + 3) + hits * (32 + 3 * 16 + 3 * 16)
     return primary, shade
 
 
@@ -95,6 +116,7 @@ def main():
     import torch.distributed as dist
     import miro
     from miro import _lib, scenes
+    from miro import tiles as tiles_mod
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -111,35 +133,46 @@ def main():
     L = miro.lib()
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
-    camc = cam._c()
+    # frames per step: 1 at N = 1; N > 1 renders a camera path of N frames per
+    # step (weak scaling: one frame of work per GPU per step), every frame's
+    # buckets dealt over all ranks, 8-bit tiles gathered once per step
+    n_frames = args.frames or (1 if world == 1 else min(world, 16))
+    cams = [cam] if n_frames == 1 else [_camera(c) for c in scenes.camera_path(cfg["camera"], n_frames)]
     bx, by = (W + 31) // 32, (H + 31) // 32
-    nb = bx * by
-    frame = torch.empty(H * W * 3, dtype=torch.float32, device="cuda")
-    frame8 = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")
-    if world > 1:
-        mine = list(range(rank, nb, world))
-        per = (nb + world - 1) // world
-        ids = torch.tensor(mine + [mine[-1]] * (per - len(mine)), dtype=torch.int32, device="cuda")
-        tiles = torch.empty(per * 1024 * 3, dtype=torch.float32, device="cuda")
-        all_ids = [torch.tensor(list(range(r, nb, world)) + [list(range(r, nb, world))[-1]] * (per - len(range(r, nb, world))),
-                                dtype=torch.int32, device="cuda") for r in range(world)]
-        gathered = [torch.empty_like(tiles) for _ in range(world)] if rank == 0 else None
+    bpf = bx * by
+    use_frame_path = world == 1 and n_frames == 1
+    frame = torch.empty(H * W * 3, dtype=torch.float32, device="cuda") if use_frame_path else None
+    frames8 = torch.empty(n_frames * H * W * 3, dtype=torch.uint8, device="cuda")
+    camc = (_lib.mrt_camera * n_frames)(*[c._c() for c in cams])
     opts_count = _lib.mrt_render_opts(W, H, dev, 1, 1, 0, 0)
     opts = _lib.mrt_render_opts(W, H, dev, 0, 1, 0, 0)
+    if not use_frame_path:
+        mine = tiles_mod.batch_items(bpf, n_frames, world, rank)
+        items = torch.tensor(mine, dtype=torch.int32, device="cuda")
+        all_items = torch.tensor([i for r in range(world) for i in tiles_mod.batch_items(bpf, n_frames, world, r)],
+                                 dtype=torch.int32, device="cuda")
+        per = len(mine)
+
+        def render(ids, out, o=opts):
+            _lib.check(L.mrt_render_batch_async(scene.handle, camc, n_frames, C.byref(o), ids.data_ptr(), len(ids),
+                                                None, out.data_ptr(), sh), "render batch")
+
+        def unpack(ids, gathered):
+            _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(ids), None, gathered.data_ptr(), W, H, n_frames,
+                                                None, frames8.data_ptr(), scene.handle, sh), "unpack")
+
+        pipe = tiles_mod.BatchPipeline(world, rank, dist, items, all_items,
+                                       lambda k: torch.empty(k * per * 1024 * 3, dtype=torch.uint8, device="cuda"),
+                                       render, unpack)
 
     def step(o):
-        if world == 1:
-            _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc), C.byref(o), frame.data_ptr(),
-                                                frame8.data_ptr(), sh), "render")
+        if use_frame_path:
+            _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(o), frame.data_ptr(),
+                                                frames8.data_ptr(), sh), "render")
+        elif o is opts_count:
+            render(items, pipe.tiles[0], opts_count)     # instrumented launch only (no gather)
         else:
-            _lib.check(L.mrt_render_buckets_async(scene.handle, C.byref(camc), C.byref(o), ids.data_ptr(), len(ids),
-                                                  tiles.data_ptr(), sh), "render buckets")
-            dist.gather(tiles, gathered, dst=0)
-            if rank == 0:
-                for r in range(world):
-                    _lib.check(L.mrt_unpack_buckets_async(all_ids[r].data_ptr(), len(all_ids[r]), gathered[r].data_ptr(),
-                                                          W, H, frame.data_ptr(), frame8.data_ptr(), scene.handle, sh),
-                               "unpack")
+            pipe.step()
 
     # instrumented frame: node/leaf visits + per-launch times (not timed below)
     step(opts_count)
@@ -152,11 +185,13 @@ def main():
         shadow_total = int(t.item())
     else:
         shadow_total = shadow_mine
-    rays_per_frame = W * H + shadow_total
+    rays_per_step = n_frames * W * H + shadow_total      # all frames of the batch, all ranks
     hits_px = st["primary_hits"]
 
     for _ in range(args.warmup):
         step(opts)
+    if not use_frame_path:
+        pipe.flush()
     # per-launch durations of the uninstrumented kernels (HIP events on this stream)
     prim_ms, shade_ms = [], []
     torch.cuda.synchronize()
@@ -165,6 +200,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(opts)
+    if not use_frame_path:
+        pipe.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -174,9 +211,12 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    # separate short loop for per-launch event timing
+    # separate short loop for per-launch event timing (render launches only)
     for _ in range(5):
-        step(opts)
+        if use_frame_path:
+            step(opts)
+        else:
+            render(items, pipe.tiles[0])
         torch.cuda.synchronize()
         s2 = scene.stats()
         prim_ms.append(s2["primary_ms"])
@@ -184,10 +224,10 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
-    value = rays_per_frame * args.steps / elapsed / 1e6
-    px_mine = W * H if world == 1 else len(range(0, nb, world)) * 1024
+    value = rays_per_step * args.steps / elapsed / 1e6
+    px_mine = W * H if use_frame_path else _pixels_in_frame(sorted(set(mine)), bpf, bx, W, H)
     hits_mine = hits_px
-    b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine)
+    b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=use_frame_path)
     pm, sm = float(np.median(prim_ms)), float(np.median(shade_ms))
     one_light = len(cfg["lights"]) == 1 and cfg.get("num_paths", 1) == 1
     shade_name = "shade1_kernel" if one_light else "shade_kernel"
@@ -198,7 +238,7 @@ def main():
     achieved = dom_b / (dom_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    if use_frame_path and os.path.exists(pmc):   # PMC pass was taken on the N = 1 frame path
         try:
             prof = json.load(open(pmc))
             if prof.get("config") == args.config:
@@ -209,21 +249,22 @@ def main():
         "metric": "Mray/s (primary+shadow) on Sponza 1920x1080",
         "value": round(value, 2), "unit": "Mray/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "f32",
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (deterministic Sponza stand-in, %d tris; sponza.obj is not in the reference snapshot)"
                 % scene.bvh_info["prims"],
         "config": {"workload": cfg["name"], "config": args.config, "width": W, "height": H, "spp": 1,
-                   "rays_per_frame": rays_per_frame, "shadow_rays": shadow_total,
+                   "frames_per_step": n_frames, "rays_per_step": rays_per_step, "shadow_rays": shadow_total,
                    "qbvh_nodes": scene.bvh_info["nodes"], "qbvh_leaves": scene.bvh_info["leaves"],
-                   "parallelism": "replica" if world == 1 else f"bucket-tiles b mod {world} + RCCL gather"},
+                   "parallelism": "single GPU, whole frame" if use_frame_path else
+                   f"{n_frames}-frame camera path per step, 32x32 buckets dealt id mod {world}, "
+                   f"one RCCL gather of 8-bit tiles per step (double-buffered)"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(dom_b),
-                     "visits_per_ray": round((st["node_visits"]) / max(1, rays_per_frame if world == 1 else
-                                              px_mine + shadow_mine), 3)},
+                     "visits_per_ray": round(st["node_visits"] / max(1, px_mine + shadow_mine), 3)},
         "launch_ms": {"primary": round(pm, 4), "shade": round(sm, 4)},
     }
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         try:
             out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         except Exception as e:  # report, never hide

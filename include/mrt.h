@@ -173,6 +173,25 @@ int mrt_render_buckets_async(mrt_scene* s, const mrt_camera* cam, const mrt_rend
 int mrt_unpack_buckets_async(const int32_t* d_buckets, int32_t n_buckets, const float* d_tiles,
                              int32_t width, int32_t height, float* d_frame, uint8_t* d_frame8,
                              const mrt_scene* s_for_lut, void* stream);
+/* ---- batched bucket render: several frames (cameras) in one launch pair.
+ * Same bucket loop (src/Scene.cpp:90-174) over a batch of n_cams <= 16 frames of
+ * one size (e.g. a camera path, or one frame's buckets dealt across GPUs).
+ * d_items: device int32 ids, id = frame * buckets_per_frame + bucket, with
+ * buckets_per_frame = ceil(W/32) * ceil(H/32); an id whose frame is >= n_cams
+ * renders with the last camera.  Frame f uses RNG seed (opts->seed or the
+ * default) + f, so it equals an mrt_render of camera f with that seed.
+ * Outputs (either may be NULL, not both), slot-major like mrt_render_buckets_async:
+ * d_tiles n_items*1024*3 floats; d_tiles8 n_items*1024*3 bytes (Image::Map). */
+int mrt_render_batch_async(mrt_scene* s, const mrt_camera* cams, int32_t n_cams, const mrt_render_opts* opts,
+                           const int32_t* d_items, int32_t n_items, float* d_tiles, uint8_t* d_tiles8,
+                           void* stream);
+/* Scatter batch tiles into n_frames consecutive W*H frames (frame f at offset
+ * f*W*H*3).  d_frames needs d_tiles; d_frames8 copies d_tiles8 or, when it is
+ * NULL, maps d_tiles through the scene's gamma LUT.  Items of frames >= n_frames
+ * are skipped. */
+int mrt_unpack_batch_async(const int32_t* d_items, int32_t n_items, const float* d_tiles, const uint8_t* d_tiles8,
+                           int32_t width, int32_t height, int32_t n_frames, float* d_frames, uint8_t* d_frames8,
+                           const mrt_scene* s_for_lut, void* stream);
 /* Whole frame straight into device buffers (N = 1 fast path, no tiles). */
 int mrt_render_frame_async(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
                            float* d_rgb, uint8_t* d_rgb8, void* stream);

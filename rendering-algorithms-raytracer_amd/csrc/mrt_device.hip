@@ -55,7 +55,7 @@ struct RenderParams {
     int32_t* gstack;
     uint32_t gstride;        // total threads in the launch
     unsigned long long* ctr;
-    CamParams cam;
+    CamParams cam[kMaxBatch];    // frame mode: cam[0]; batch mode: one camera per frame
     float bg[3];
     int32_t n_lights, num_paths;
     uint32_t seed;
@@ -67,8 +67,10 @@ struct RenderParams {
     int32_t tiles_x, n_tiles;    // frame mode: tiles_x = ceil(W/8)
     const int32_t* buckets;      // bucket mode: bucket ids (row-major bucket grid)
     int32_t buckets_x;           // ceil(W/32)
+    int32_t buckets_per_frame;   // bucket mode: id = frame * buckets_per_frame + bucket
+    int32_t n_cams;              // bucket mode: frames (cameras) in the batch
     int32_t mode;                // 0 frame, 1 buckets
-    float* out_rgb;              // frame: W*H*3; buckets: n_buckets*1024*3
+    float* out_rgb;              // frame: W*H*3; buckets: n_buckets*1024*3 (nullable)
     uint8_t* out_rgb8;           // same slots as out_rgb (nullable)
     float4* hits;                // per slot: t, a, b, prim bits (kernel 1 -> kernel 2)
 };
@@ -82,8 +84,9 @@ struct Shader {
     TravStats& st;
     uint32_t pixel, dim;
     uint32_t shadow_rays;
+    uint32_t seed;
 
-    __device__ float next_rand() { return rng(pixel, 0, dim++, P.seed); }
+    __device__ float next_rand() { return rng(pixel, 0, dim++, seed); }
 
     template <bool COUNT>
     __device__ bool occluded(v3 from, v3 L, float tMax) {
@@ -274,34 +277,43 @@ struct TileSched {
         }
         return __shfl(item, 0);
     }
+    // items are wave-uniform: readfirstlane puts them (and the frame / camera
+    // lookups derived from them) in SGPRs
     __device__ int first() {
-        if (mode >= 2) return dequeue();
-        return cur < end ? cur : -1;
+        if (mode >= 2) return __builtin_amdgcn_readfirstlane(dequeue());
+        return __builtin_amdgcn_readfirstlane(cur < end ? cur : -1);
     }
     __device__ int next(int item) {
-        if (mode >= 2) return dequeue();
+        if (mode >= 2) return __builtin_amdgcn_readfirstlane(dequeue());
         item += step;
-        return item < end ? item : -1;
+        return __builtin_amdgcn_readfirstlane(item < end ? item : -1);
     }
 };
 
-// work item (8x8 tile) + lane -> pixel (x, y) and output slot
+// work item (8x8 tile, wave-uniform) -> frame of the item (frame mode: 0)
+__device__ __forceinline__ int item_frame(const RenderParams& P, int item) {
+    // clamped: an out-of-range id renders with the last camera instead of reading
+    // past the kernel argument block
+    return P.mode == 0 ? 0 : (int)min((uint32_t)P.buckets[item >> 4] / (uint32_t)P.buckets_per_frame, (uint32_t)(P.n_cams - 1));
+}
+
+// work item + lane -> pixel (x, y) and output slot
 __device__ __forceinline__ bool item_pixel(const RenderParams& P, int item, int lane, int& x, int& y, size_t& slot) {
     if (P.mode == 0) {
         int tx = item % P.tiles_x, ty = item / P.tiles_x;
         x = tx * 8 + (lane & 7);
         y = ty * 8 + (lane >> 3);
-        slot = (size_t)y * P.cam.W + x;
+        slot = (size_t)y * P.cam[0].W + x;
     } else {
         int bslot = item >> 4, sub = item & 15;
-        int b = P.buckets[bslot];
+        int b = (int)((uint32_t)P.buckets[bslot] % (uint32_t)P.buckets_per_frame);
         int bx = b % P.buckets_x, by = b / P.buckets_x;
         int lx = (sub & 3) * 8 + (lane & 7), ly = (sub >> 2) * 8 + (lane >> 3);
         x = bx * 32 + lx;
         y = by * 32 + ly;
         slot = (size_t)bslot * 1024 + ly * 32 + lx;
     }
-    return x < P.cam.W && y < P.cam.H;
+    return x < P.cam[0].W && y < P.cam[0].H;
 }
 
 __device__ __forceinline__ void load_tables(const uint16_t* g, uint16_t* s, int words32) {
@@ -341,10 +353,9 @@ __device__ __forceinline__ void flush_stats(const RenderParams& P, const TravSta
 // Camera::eyeRayAdaptive(x, y, .5, .5, .5, .5) (src/Camera.cpp:116-157): two
 // jitter draws (dims 0, 1; the offsets are exactly 0.5) and the time draw (dim 2,
 // unused).  Deterministic, so kernel 2 recomputes it instead of storing it.
-__device__ __forceinline__ v3 camera_dir(const RenderParams& P, int x, int y, const uint16_t* rsqT) {
-    const CamParams& cam = P.cam;
+__device__ __forceinline__ v3 camera_dir(const CamParams& cam, uint32_t seed, int x, int y, const uint16_t* rsqT) {
     const uint32_t pixel = (uint32_t)(y * cam.W + x);
-    float ur = rng(pixel, 0, 0, P.seed), vr = rng(pixel, 0, 1, P.seed);
+    float ur = rng(pixel, 0, 0, seed), vr = rng(pixel, 0, 1, seed);
     float xo = (0.5f - 0.5f) * ur + 0.5f, yo = (0.5f - 0.5f) * vr + 0.5f;
     float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
     float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
@@ -365,8 +376,6 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
     uint32_t nhits = 0;
-    const CamParams& cam = P.cam;
-    const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
     unsigned long long wave_steps = 0;  // count mode: sum over tiles of max lane node visits
     TileSched ts(P, wave, lane);
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
@@ -374,7 +383,9 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
         size_t slot;
         const uint32_t n0 = st.nodes;
         if (item_pixel(P, item, lane, x, y, slot)) {
-            DRay r = make_ray(eye, camera_dir(P, x, y, rsqT));
+            const int f = item_frame(P, item);
+            const CamParams& cam = P.cam[f];
+            DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, P.seed + (uint32_t)f, x, y, rsqT));
             DHit h{1e12f, 0.f, 0.f, -1};
             if (!traverse<false, COUNT, FAST>(T, r, 0.001f, h, st)) h.prim = -1;
             item_pixel(P, item, lane, x, y, slot);  // recompute: keeps it out of the traversal's live set
@@ -403,8 +414,6 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
     uint32_t shadow_total = 0;
-    const CamParams& cam = P.cam;
-    const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
     TileSched ts(P, wave, lane);
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
         int x, y;
@@ -414,15 +423,20 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
         DHit h{hv.x, hv.y, hv.z, __float_as_int(hv.w)};
         v3 col;
         if (h.prim >= 0) {
-            DRay r = make_ray(eye, camera_dir(P, x, y, rsqT));
-            Shader<POINT_ONLY, FAST> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u};
+            const int f = item_frame(P, item);
+            const CamParams& cam = P.cam[f];
+            const uint32_t seed = P.seed + (uint32_t)f;
+            DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, seed, x, y, rsqT));
+            Shader<POINT_ONLY, FAST> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u, seed};
             col = S.template shade<COUNT>(r, h);
             shadow_total += S.shadow_rays;
         } else {
             col = mk(P.bg[0], P.bg[1], P.bg[2]);
         }
-        float* o = P.out_rgb + 3 * slot;
-        o[0] = col.x; o[1] = col.y; o[2] = col.z;
+        if (P.out_rgb) {
+            float* o = P.out_rgb + 3 * slot;
+            o[0] = col.x; o[1] = col.y; o[2] = col.z;
+        }
         if (P.out_rgb8) {
             uint8_t* o8 = P.out_rgb8 + 3 * slot;
             o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
@@ -447,7 +461,6 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     TravStats st;
     uint32_t shadow_total = 0;
-    const v3 eye = mk(P.cam.eye[0], P.cam.eye[1], P.cam.eye[2]);
     TileSched ts(P, wave, lane);
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
         int x, y;
@@ -458,8 +471,10 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
         v3 col = mk(P.bg[0], P.bg[1], P.bg[2]);
         if (prim >= 0) {
             // HitInfo::getAllInfos + Ray::getPoint
-            const v3 rayD = camera_dir(P, x, y, rsqT);
-            const DRay r = make_ray(eye, rayD);
+            const int f = item_frame(P, item);
+            const CamParams& cam = P.cam[f];
+            const v3 rayD = camera_dir(cam, P.seed + (uint32_t)f, x, y, rsqT);
+            const DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), rayD);
             const PrimShade ps = P.prims[prim];
             const uint32_t mi = ps.mat;
             const bool lambert = P.mats[mi].type == MRT_LAMBERT;
@@ -525,8 +540,10 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
             col = scale(add(mk(0, 0, 0), sh), 1.0f / (float)P.num_paths);
         }
         item_pixel(P, item, lane, x, y, slot);
-        float* o = P.out_rgb + 3 * slot;
-        o[0] = col.x; o[1] = col.y; o[2] = col.z;
+        if (P.out_rgb) {
+            float* o = P.out_rgb + 3 * slot;
+            o[0] = col.x; o[1] = col.y; o[2] = col.z;
+        }
         if (P.out_rgb8) {
             uint8_t* o8 = P.out_rgb8 + 3 * slot;
             o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
@@ -561,18 +578,31 @@ __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DL
     if (st.overflow) atomicOr(&ctr[CTR_OVERFLOW], 1ull);
 }
 
-__global__ void unpack_kernel(const int32_t* buckets, int32_t n_buckets, const float* tiles, int32_t W, int32_t H,
-                              int32_t buckets_x, float* frame, uint8_t* frame8, const uint8_t* gamma) {
+// Bucket tiles -> frames.  Item id = frame * buckets_per_frame + bucket; frame f
+// of the output starts at f * W * H pixels.  Float tiles (nullable) go to
+// `frames`; 8-bit pixels come from tiles8 when given, else from the LUT.
+__global__ void unpack_kernel(const int32_t* items, int32_t n_items, const float* tiles, const uint8_t* tiles8,
+                              int32_t W, int32_t H, int32_t buckets_x, int32_t buckets_per_frame, int32_t n_frames,
+                              float* frames, uint8_t* frames8, const uint8_t* gamma) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)n_buckets * 1024) return;
+    if (i >= (size_t)n_items * 1024) return;
     int bslot = (int)(i >> 10), p = (int)(i & 1023);
-    int b = buckets[bslot];
-    int x = (b % buckets_x) * 32 + (p & 31), y = (b / buckets_x) * 32 + (p >> 5);
-    if (x >= W || y >= H) return;
-    size_t q = (size_t)y * W + x;
-    float r = tiles[3 * i], g = tiles[3 * i + 1], bl = tiles[3 * i + 2];
-    frame[3 * q] = r; frame[3 * q + 1] = g; frame[3 * q + 2] = bl;
-    if (frame8) { frame8[3 * q] = map8(gamma, r); frame8[3 * q + 1] = map8(gamma, g); frame8[3 * q + 2] = map8(gamma, bl); }
+    const uint32_t id = (uint32_t)items[bslot];
+    const uint32_t f = id / (uint32_t)buckets_per_frame, b = id % (uint32_t)buckets_per_frame;
+    int x = (int)(b % buckets_x) * 32 + (p & 31), y = (int)(b / buckets_x) * 32 + (p >> 5);
+    if (f >= (uint32_t)n_frames || x >= W || y >= H) return;  // ids outside the batch are ignored
+    size_t q = (size_t)f * W * H + (size_t)y * W + x;
+    if (tiles && frames) {
+        frames[3 * q] = tiles[3 * i]; frames[3 * q + 1] = tiles[3 * i + 1]; frames[3 * q + 2] = tiles[3 * i + 2];
+    }
+    if (frames8) {
+        if (tiles8) {
+            frames8[3 * q] = tiles8[3 * i]; frames8[3 * q + 1] = tiles8[3 * i + 1]; frames8[3 * q + 2] = tiles8[3 * i + 2];
+        } else {
+            frames8[3 * q] = map8(gamma, tiles[3 * i]); frames8[3 * q + 1] = map8(gamma, tiles[3 * i + 1]);
+            frames8[3 * q + 2] = map8(gamma, tiles[3 * i + 2]);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ device state
@@ -1050,7 +1080,7 @@ int mrt_render_frame_async(mrt_scene* s, const mrt_camera* cam, const mrt_render
     HIP_OK(hipSetDevice(opts->device));
     RenderParams P{};
     fill_params(S, P);
-    if ((rc = host_camera(cam, opts->width, opts->height, P.cam))) return rc;
+    if ((rc = host_camera(cam, opts->width, opts->height, P.cam[0]))) return rc;
     P.seed = opts->seed ? opts->seed : 0x5EEDu;
     P.mode = 0;
     P.tiles_x = (opts->width + 7) / 8;
@@ -1062,40 +1092,66 @@ int mrt_render_frame_async(mrt_scene* s, const mrt_camera* cam, const mrt_render
     return rc;
 }
 
-int mrt_render_buckets_async(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts, const int32_t* d_buckets,
-                             int32_t n_buckets, float* d_tiles, void* stream) {
-    if (!s || !cam || !opts || !d_buckets || !d_tiles || n_buckets < 0) { set_error("bad argument"); return MRT_ERR_INVALID; }
+int mrt_render_batch_async(mrt_scene* s, const mrt_camera* cams, int32_t n_cams, const mrt_render_opts* opts,
+                           const int32_t* d_items, int32_t n_items, float* d_tiles, uint8_t* d_tiles8, void* stream) {
+    if (!s || !cams || !opts || n_items < 0 || (n_items && !d_items) || (!d_tiles && !d_tiles8)) {
+        set_error("bad argument"); return MRT_ERR_INVALID;
+    }
+    if (n_cams < 1 || n_cams > kMaxBatch) { set_error("n_cams must be 1..16"); return MRT_ERR_INVALID; }
     Scene& S = s->impl;
     int rc = ensure_device(S, opts->device);
     if (rc) return rc;
     HIP_OK(hipSetDevice(opts->device));
     RenderParams P{};
     fill_params(S, P);
-    if ((rc = host_camera(cam, opts->width, opts->height, P.cam))) return rc;
+    for (int f = 0; f < n_cams; f++)
+        if ((rc = host_camera(cams + f, opts->width, opts->height, P.cam[f]))) return rc;
     P.seed = opts->seed ? opts->seed : 0x5EEDu;
     P.mode = 1;
-    P.buckets = d_buckets;
+    P.buckets = d_items;
     P.buckets_x = (opts->width + 31) / 32;
-    P.n_tiles = n_buckets * 16;
+    P.buckets_per_frame = P.buckets_x * ((opts->height + 31) / 32);
+    P.n_cams = n_cams;
+    P.n_tiles = n_items * 16;
     P.out_rgb = d_tiles;
-    P.out_rgb8 = nullptr;
-    if (n_buckets == 0) return MRT_OK;
-    rc = launch_render(S, P, (size_t)n_buckets * 1024, opts->count_visits != 0, (hipStream_t)stream);
+    P.out_rgb8 = d_tiles8;
+    if (n_items == 0) return MRT_OK;
+    rc = launch_render(S, P, (size_t)n_items * 1024, opts->count_visits != 0, (hipStream_t)stream);
     S.last.primary_rays = 0;
     return rc;
 }
 
-int mrt_unpack_buckets_async(const int32_t* d_buckets, int32_t n_buckets, const float* d_tiles, int32_t width,
-                             int32_t height, float* d_frame, uint8_t* d_frame8, const mrt_scene* s_for_lut, void* stream) {
-    if (!d_buckets || !d_tiles || !d_frame || width <= 0 || height <= 0) { set_error("bad argument"); return MRT_ERR_INVALID; }
-    if (d_frame8 && (!s_for_lut || !s_for_lut->impl.dev)) { set_error("rgb8 needs an uploaded scene for the LUT"); return MRT_ERR_INVALID; }
-    if (n_buckets == 0) return MRT_OK;
-    size_t n = (size_t)n_buckets * 1024;
-    const uint8_t* lut = d_frame8 ? s_for_lut->impl.dev->gamma : nullptr;
-    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_buckets,
-                       n_buckets, d_tiles, width, height, (width + 31) / 32, d_frame, d_frame8, lut);
+int mrt_render_buckets_async(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts, const int32_t* d_buckets,
+                             int32_t n_buckets, float* d_tiles, void* stream) {
+    if (!d_tiles) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    return mrt_render_batch_async(s, cam, 1, opts, d_buckets, n_buckets, d_tiles, nullptr, stream);
+}
+
+int mrt_unpack_batch_async(const int32_t* d_items, int32_t n_items, const float* d_tiles, const uint8_t* d_tiles8,
+                           int32_t width, int32_t height, int32_t n_frames, float* d_frames, uint8_t* d_frames8,
+                           const mrt_scene* s_for_lut, void* stream) {
+    if ((n_items && !d_items) || n_items < 0 || width <= 0 || height <= 0 || n_frames < 1 || (!d_frames && !d_frames8)) {
+        set_error("bad argument"); return MRT_ERR_INVALID;
+    }
+    if (d_frames && !d_tiles) { set_error("float frames need float tiles"); return MRT_ERR_INVALID; }
+    if (d_frames8 && !d_tiles8 && !d_tiles) { set_error("rgb8 frames need tiles"); return MRT_ERR_INVALID; }
+    const bool need_lut = d_frames8 && !d_tiles8;
+    if (need_lut && (!s_for_lut || !s_for_lut->impl.dev)) { set_error("rgb8 needs an uploaded scene for the LUT"); return MRT_ERR_INVALID; }
+    if (n_items == 0) return MRT_OK;
+    size_t n = (size_t)n_items * 1024;
+    const uint8_t* lut = need_lut ? s_for_lut->impl.dev->gamma : nullptr;
+    const int bx = (width + 31) / 32, bpf = bx * ((height + 31) / 32);
+    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_items,
+                       n_items, d_tiles, d_tiles8, width, height, bx, bpf, n_frames, d_frames, d_frames8, lut);
     HIP_OK(hipGetLastError());
     return MRT_OK;
+}
+
+int mrt_unpack_buckets_async(const int32_t* d_buckets, int32_t n_buckets, const float* d_tiles, int32_t width,
+                             int32_t height, float* d_frame, uint8_t* d_frame8, const mrt_scene* s_for_lut, void* stream) {
+    if (!d_tiles || !d_frame) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    return mrt_unpack_batch_async(d_buckets, n_buckets, d_tiles, nullptr, width, height, 1, d_frame, d_frame8,
+                                  s_for_lut, stream);
 }
 
 int mrt_render(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts, float* rgb, uint8_t* rgb8, mrt_hit* hits) {
@@ -1116,7 +1172,7 @@ int mrt_render(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
     }
     RenderParams P{};
     fill_params(S, P);
-    if ((rc = host_camera(cam, opts->width, opts->height, P.cam))) return rc;
+    if ((rc = host_camera(cam, opts->width, opts->height, P.cam[0]))) return rc;
     P.seed = opts->seed ? opts->seed : 0x5EEDu;
     P.mode = 0;
     P.tiles_x = (opts->width + 7) / 8;

@@ -66,6 +66,7 @@ struct CamParams {
 };
 
 static constexpr int kMaxLights = 8;
+static constexpr int kMaxBatch = 16;   // cameras (frames) per batched bucket launch (kernel argument)
 static constexpr int kMaxMaterials = 64;
 
 }  // namespace mrt

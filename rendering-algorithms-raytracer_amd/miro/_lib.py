@@ -20,7 +20,7 @@ EXPORTS = [
     "mrt_scene_build_bvh", "mrt_scene_bvh_info", "mrt_scene_bvh_export", "mrt_scene_bvh_import",
     "mrt_scene_upload", "mrt_render", "mrt_render_buckets_async", "mrt_unpack_buckets_async",
     "mrt_render_frame_async", "mrt_trace", "mrt_trace_async", "mrt_scene_last_stats", "mrt_rcp_nr",
-    "mrt_rsqrt_nr", "mrt_set_tuning",
+    "mrt_rsqrt_nr", "mrt_set_tuning", "mrt_render_batch_async", "mrt_unpack_batch_async",
 ]
 
 
@@ -116,6 +116,10 @@ def load():
                                            C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
     L.mrt_unpack_buckets_async.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mrt_render_batch_async.argtypes = [C.c_void_p, C.POINTER(mrt_camera), C.c_int32, C.POINTER(mrt_render_opts),
+                                         C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mrt_unpack_batch_async.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                         C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.mrt_render_frame_async.argtypes = [C.c_void_p, C.POINTER(mrt_camera), C.POINTER(mrt_render_opts),
                                          C.c_void_p, C.c_void_p, C.c_void_p]
     L.mrt_trace.argtypes = [C.c_void_p, _fp, _fp, _fp, _fp, C.c_size_t, C.c_int, C.c_void_p]

@@ -254,6 +254,22 @@ CONFIGS = {
 }
 
 
+def camera_path(cam, n, step_deg=2.5):
+    """n cameras panning from `cam` (a config camera dict): frame f turns the
+    view direction by f * step_deg degrees about the up (y) axis around the
+    fixed eye.  Frame 0 is `cam` itself.  Used for frame batches (bench.py at
+    N > 1 renders N frames per step)."""
+    eye = np.asarray(cam["eye"], np.float64)
+    d = np.asarray(cam["lookAt"], np.float64) - eye
+    out = []
+    for f in range(n):
+        a = np.deg2rad(step_deg * f)
+        c, s = np.cos(a), np.sin(a)
+        dd = np.array([c * d[0] + s * d[2], d[1], -s * d[0] + c * d[2]])
+        out.append(dict(cam, lookAt=tuple(float(x) for x in (eye + dd)) if f else tuple(cam["lookAt"])))
+    return out
+
+
 def build_config(key, device=0):
     """Product-side scene for a config preset -> (miro.Scene, miro.Camera, cfg).
     C1 needs the Cornell mesh fixture path in MRT_CORNELL_NPZ (or tests/golden)."""

@@ -1,5 +1,12 @@
 """Bucket tiling across ranks + the frame-end gather.
 
+Frame batches: a step may render several frames of one size (a camera path).
+Items are id = frame * buckets_per_frame + bucket, dealt id -> rank id mod N
+over the whole batch, rendered in ONE launch pair per rank
+(mrt_render_batch_async) and gathered once per step.  BatchPipeline
+double-buffers the tile buffers so the gather of step k overlaps the render of
+step k + 1.
+
 The reference renders 32x32 buckets (src/Miro.h:55) in a dynamic OpenMP loop
 (src/Scene.cpp:90-174).  Across GPUs the buckets are dealt statically,
 bucket b -> rank b mod N, which interleaves them over the image (load balance
@@ -58,3 +65,69 @@ def unpack_tiles_numpy(ids, tiles, W: int, H: int, frame=None):
         h, w = min(BUCKET, H - y0), min(BUCKET, W - x0)
         frame[y0:y0 + h, x0:x0 + w] = t[slot, :h, :w]
     return frame
+
+
+def batch_items(buckets_per_frame: int, n_frames: int, world: int, rank: int) -> List[int]:
+    """This rank's item ids (frame * buckets_per_frame + bucket) of a batch,
+    padded by repeating its last id to ceil(total / world) (equal gather sizes;
+    a repeated item rewrites the same pixels with the same values)."""
+    return padded_buckets(buckets_per_frame * n_frames, world, rank)
+
+
+class BatchPipeline:
+    """Per-step render -> gather(rank 0) -> unpack, double-buffered.
+
+    render(items, out_tiles) enqueues this rank's items into out_tiles;
+    unpack(all_items, gathered) assembles the batch on rank 0 from ONE buffer
+    holding every rank's tiles in rank order (all_items is the matching
+    concatenation of the ranks' item lists).  new_tiles(k) allocates k ranks'
+    worth of tiles.  Both callables are injected so the same pipeline drives
+    libmrt on the GPU (RCCL) and the CPU oracle in the gloo tests.
+
+    Step k writes buffer k % 2; before step k + 2 reuses it, the gather of step
+    k is waited on (work.wait() orders the compute stream after the collective
+    on nccl; it blocks on gloo).  Rank 0 unpacks step k after enqueuing the
+    render of step k + 1, so its next render is not queued behind the
+    collective."""
+
+    def __init__(self, world, rank, dist, items, all_items, new_tiles, render, unpack):
+        self.world, self.rank, self.dist = world, rank, dist
+        self.items, self.all_items = items, all_items
+        self.render, self.unpack = render, unpack
+        self.tiles = [new_tiles(1), new_tiles(1)]
+        self.recv = [new_tiles(world), new_tiles(world)] if (rank == 0 and world > 1) else None
+        self.work = [None, None]
+        self.pending = None      # (work, buffer) of the step rank 0 has not unpacked yet
+        self.k = 0
+
+    def step(self):
+        b = self.k & 1
+        if self.work[b] is not None:
+            self.work[b].wait()
+            self.work[b] = None
+        self.render(self.items, self.tiles[b])
+        if self.world == 1:
+            self.unpack(self.all_items, self.tiles[b])
+        else:
+            outs = list(self.recv[b].chunk(self.world)) if self.rank == 0 else None
+            w = self.dist.gather(self.tiles[b], outs, dst=0, async_op=True)
+            self.work[b] = w
+            self._drain()
+            if self.rank == 0:
+                self.pending = (w, b)
+        self.k += 1
+
+    def _drain(self):
+        if self.pending is not None:
+            w, pb = self.pending
+            w.wait()
+            self.unpack(self.all_items, self.recv[pb])
+            self.pending = None
+
+    def flush(self):
+        """Finish every outstanding gather / unpack (end of the timed region)."""
+        self._drain()
+        for i in range(2):
+            if self.work[i] is not None:
+                self.work[i].wait()
+                self.work[i] = None

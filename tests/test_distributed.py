@@ -87,3 +87,92 @@ def test_bucket_assignment_covers_frame_once():
         assert seen == list(range(nb))
         lens = {len(tiles.padded_buckets(nb, world, r)) for r in range(world)}
         assert lens == {(nb + world - 1) // world}
+
+
+def _batch_worker(rank, world, port, W, H, n_frames, steps, result_path):
+    """Each step renders a batch of n_frames cameras (shifted by the step index,
+    so a buffer mix-up between steps shows) through BatchPipeline."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, cam = _oracle_scene()
+        bx, by = tiles.bucket_grid(W, H)
+        bpf = bx * by
+        items = tiles.batch_items(bpf, n_frames, world, rank)
+        all_items = [i for r in range(world) for i in tiles.batch_items(bpf, n_frames, world, r)]
+        path = scenes.camera_path(cam, n_frames + steps, step_deg=4.0)
+        state = {"render": 0, "unpack": 0}
+        outs = []
+
+        def render(ids, out):
+            k = state["render"]
+            state["render"] += 1
+            t = out.view(-1, 32, 32, 3)
+            for slot, i in enumerate(ids):
+                f, b = divmod(i, bpf)
+                x0, y0 = (b % bx) * 32, (b // bx) * 32
+                r = s.render(path[k + f], W, H, rect=(x0, y0, x0 + 32, y0 + 32), want_hits=False)
+                h, w = min(32, H - y0), min(32, W - x0)
+                t[slot, :h, :w] = torch.from_numpy(r["rgb"][y0:y0 + h, x0:x0 + w])
+
+        def unpack(ids, gathered):
+            state["unpack"] += 1
+            frames = np.zeros((n_frames, H, W, 3), np.float32)
+            t = gathered.view(-1, 32, 32, 3).numpy()
+            for slot, i in enumerate(ids):
+                f, b = divmod(i, bpf)
+                x0, y0 = (b % bx) * 32, (b // bx) * 32
+                h, w = min(32, H - y0), min(32, W - x0)
+                frames[f, y0:y0 + h, x0:x0 + w] = t[slot, :h, :w]
+            outs.append(frames)
+
+        per = len(items)
+        pipe = tiles.BatchPipeline(world, rank, dist, items, all_items,
+                                   lambda k: torch.zeros(k * per * 1024 * 3, dtype=torch.float32), render, unpack)
+        for _ in range(steps):
+            pipe.step()
+        pipe.flush()
+        if rank == 0:
+            np.save(result_path, np.stack(outs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_batch_pipeline_frames_equal_single_rank(tmp_path, world):
+    W, H, n_frames, steps = 70, 40, 2, 3
+    path = str(tmp_path / "frames.npy")
+    mp.start_processes(_batch_worker, args=(world, _free_port(), W, H, n_frames, steps, path), nprocs=world,
+                       start_method="spawn")
+    got = np.load(path)
+    assert got.shape == (steps, n_frames, H, W, 3)
+    s, cam = _oracle_scene()
+    cams = scenes.camera_path(cam, n_frames + steps, step_deg=4.0)
+    for k in range(steps):
+        for f in range(n_frames):
+            ref = s.render(cams[k + f], W, H, want_hits=False)["rgb"]
+            assert np.array_equal(got[k, f].view(np.uint32), ref.view(np.uint32)), (k, f)
+
+
+def test_batch_items_cover_every_frame_once():
+    bpf = 60 * 34
+    for world in (1, 2, 4, 8):
+        for n_frames in (1, world):
+            got = sorted(i for r in range(world) for i in set(tiles.batch_items(bpf, n_frames, world, r)))
+            assert got == list(range(bpf * n_frames))
+            lens = {len(tiles.batch_items(bpf, n_frames, world, r)) for r in range(world)}
+            assert len(lens) == 1
+
+
+def test_camera_path_starts_at_config_camera():
+    cam = scenes.CONFIGS["C3"]["camera"]
+    path = scenes.camera_path(cam, 4)
+    assert path[0] == cam
+    eye = np.array(cam["eye"])
+    d0 = np.array(cam["lookAt"]) - eye
+    for f, c in enumerate(path):
+        assert c["eye"] == cam["eye"]
+        d = np.array(c["lookAt"]) - eye
+        assert abs(np.linalg.norm(d) - np.linalg.norm(d0)) < 1e-9
+        cosang = np.dot(d[[0, 2]], d0[[0, 2]]) / (np.linalg.norm(d[[0, 2]]) * np.linalg.norm(d0[[0, 2]]))
+        assert abs(np.degrees(np.arccos(min(1.0, cosang))) - 2.5 * f) < 1e-6
