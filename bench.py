@@ -6,7 +6,9 @@ missing sponza.obj) -- BASELINE.json `metric` / configs[2].
 One "step" = one pass of the hot path over one batch: primary rays + shadow
 rays + shading + Image::Map.
 N = 1: one frame per step, rendered straight into HBM buffers (whole-frame
-launch pair).  N > 1 (torch.distributed, one process per GPU, backend nccl =
+launch pair); consecutive steps alternate over --inflight (4) HIP streams, each
+with its own scratch in libmrt, so the tail of one frame's persistent launches
+overlaps the start of the next frame (4 streams = the HIP hardware queues per process).  N > 1 (torch.distributed, one process per GPU, backend nccl =
 RCCL): weak scaling -- a step renders a camera path of N frames (frame 0 is the
 config camera, then 2.5-degree pans), the 32x32 buckets of all N frames are
 dealt id mod N (reference bucket grid, src/Scene.cpp:90-95), every rank renders
@@ -40,6 +42,11 @@ def parse():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frames", type=int, default=0, help="frames per step (default: 1 at N=1, N at N>1)")
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="N = 1 frame path: frames in flight (consecutive steps alternate over this many HIP "
+                         "streams, so one frame's launch tail overlaps the next frame's start)")
+    ap.add_argument("--path", choices=["auto", "batch"], default="auto",
+                    help="batch: use the bucket-batch path even for one frame on one GPU (A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-thread-seconds for the oracle sample")
     return ap.parse_args()
 
@@ -140,9 +147,13 @@ def main():
     cams = [cam] if n_frames == 1 else [_camera(c) for c in scenes.camera_path(cfg["camera"], n_frames)]
     bx, by = (W + 31) // 32, (H + 31) // 32
     bpf = bx * by
-    use_frame_path = world == 1 and n_frames == 1
-    frame = torch.empty(H * W * 3, dtype=torch.float32, device="cuda") if use_frame_path else None
-    frames8 = torch.empty(n_frames * H * W * 3, dtype=torch.uint8, device="cuda")
+    use_frame_path = world == 1 and n_frames == 1 and args.path == "auto"
+    inflight = max(1, args.inflight) if use_frame_path else 1
+    streams = [stream] + [torch.cuda.Stream() for _ in range(inflight - 1)]
+    frame = [torch.empty(H * W * 3, dtype=torch.float32, device="cuda") for _ in range(inflight)] \
+        if use_frame_path else None
+    frame8 = [torch.empty(H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(inflight)]
+    frames8 = frame8[0] if use_frame_path else torch.empty(n_frames * H * W * 3, dtype=torch.uint8, device="cuda")
     camc = (_lib.mrt_camera * n_frames)(*[c._c() for c in cams])
     opts_count = _lib.mrt_render_opts(W, H, dev, 1, 1, 0, 0)
     opts = _lib.mrt_render_opts(W, H, dev, 0, 1, 0, 0)
@@ -165,17 +176,21 @@ def main():
                                        lambda k: torch.empty(k * per * 1024 * 3, dtype=torch.uint8, device="cuda"),
                                        render, unpack)
 
-    def step(o):
+    nstep = [0]
+
+    def step(o, serial=False):
         if use_frame_path:
-            _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(o), frame.data_ptr(),
-                                                frames8.data_ptr(), sh), "render")
+            i = 0 if serial else nstep[0] % inflight
+            nstep[0] += 1
+            _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(o), frame[i].data_ptr(),
+                                                frame8[i].data_ptr(), streams[i].cuda_stream), "render")
         elif o is opts_count:
             render(items, pipe.tiles[0], opts_count)     # instrumented launch only (no gather)
         else:
             pipe.step()
 
     # instrumented frame: node/leaf visits + per-launch times (not timed below)
-    step(opts_count)
+    step(opts_count, serial=True)
     torch.cuda.synchronize()
     st = scene.stats()
     shadow_mine = st["shadow_rays"]
@@ -214,7 +229,7 @@ def main():
     # separate short loop for per-launch event timing (render launches only)
     for _ in range(5):
         if use_frame_path:
-            step(opts)
+            step(opts, serial=True)
         else:
             render(items, pipe.tiles[0])
         torch.cuda.synchronize()
@@ -255,6 +270,7 @@ def main():
         "config": {"workload": cfg["name"], "config": args.config, "width": W, "height": H, "spp": 1,
                    "frames_per_step": n_frames, "rays_per_step": rays_per_step, "shadow_rays": shadow_total,
                    "qbvh_nodes": scene.bvh_info["nodes"], "qbvh_leaves": scene.bvh_info["leaves"],
+                   "frames_in_flight": inflight,
                    "parallelism": "single GPU, whole frame" if use_frame_path else
                    f"{n_frames}-frame camera path per step, 32x32 buckets dealt id mod {world}, "
                    f"one RCCL gather of 8-bit tiles per step (double-buffered)"},
@@ -263,6 +279,9 @@ def main():
                      "launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(dom_b),
                      "visits_per_ray": round(st["node_visits"] / max(1, px_mine + shadow_mine), 3)},
         "launch_ms": {"primary": round(pm, 4), "shade": round(sm, 4)},
+        # instrumented (count-mode) launch: wall-clock spread of the persistent waves
+        "wave_timing_us": {k: round(st[k], 1) for k in ("primary_span_us", "primary_ramp_us", "primary_tail_us",
+                                                       "shade_span_us", "shade_ramp_us", "shade_tail_us")},
     }
     if not args.no_cpu_baseline and world == 1:
         try:

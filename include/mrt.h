@@ -112,6 +112,11 @@ typedef struct {
     float kernel_ms;                     /* device time of the last frame (all launches)*/
     float primary_ms, shade_ms;          /* per launch: primary rays / shade + shadows  */
     int32_t max_stack;                   /* deepest traversal stack seen (count mode)   */
+    /* count mode, per launch of the persistent render kernels (device wall clock):
+     * span = first wave start -> last wave end, ramp = spread of wave starts,
+     * tail = spread of wave ends (time the launch runs below full occupancy)   */
+    float primary_span_us, primary_ramp_us, primary_tail_us;
+    float shade_span_us, shade_ramp_us, shade_tail_us;
 } mrt_stats;
 
 const char* mrt_last_error(void);
@@ -216,6 +221,16 @@ int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
  * kernel for one point light and one path), "lds_pad_kb" [0]..128 (extra LDS per
  * workgroup, lowers occupancy for sweeps).  Process-wide. */
 int mrt_set_tuning(const char* key, int value);
+
+/* Diagnostics: per-wave records of the last count-mode render (count_visits = 1)
+ * for launch 0 (primary rays) or 1 (shading + shadow rays): 60 x uint64 per wave
+ * {start, end (device wall clock ticks), tiles processed, node visits, then for the
+ * wave's first 28 tiles: tile id << 40 | low 40 bits of the tick it started, then
+ * for the same tiles the ticks their dequeue (tile-queue atomics) took}.
+ * Returns the number of waves copied (<= max_waves). */
+int mrt_debug_wave_log(const mrt_scene* s, int launch, uint64_t* out, int32_t max_waves);
+/* Device wall-clock rate (kHz) of the scene's device, for the ticks above. */
+int mrt_device_wall_clock_khz(const mrt_scene* s);
 
 /* Numerics probes (x86 RCPSS/RSQRTSS emulation + one Newton step, SSE.h:67-101). */
 float mrt_rcp_nr(float x);

@@ -37,8 +37,15 @@ void set_error(const std::string& m) { g_err = m; }
     } while (0)
 
 enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLOW = 4, CTR_NODES_P = 5, CTR_LEAVES_P = 6, CTR_HITS = 7,
-       CTR_WAVE_STEPS_P = 8, CTR_UNIFORM_P = 9, CTR_N = 16 };
-static constexpr int kMaxBlocksPerCU = 8;  // 256-thread blocks: 8 waves per SIMD at most
+       CTR_WAVE_STEPS_P = 8, CTR_UNIFORM_P = 9,
+       // count mode, per launch (primary at CTR_TP, shade at CTR_TS): wave start/end
+       // wall clocks as ~min start, max start, ~min end, max end (zero-initialised maxima)
+       CTR_TP = 10, CTR_TS = 14, CTR_N = 18 };
+static constexpr int kMaxBlocksPerCU = 8;
+// wave log record: start, end, tiles, node visits, then (tile id << 40 | start tick) of the first kLogTiles
+// tiles, then the wall-clock ticks each of those tiles' dequeue took
+static constexpr int kLogTiles = 28;
+static constexpr int kLogWords = 4 + 2 * kLogTiles;  // 256-thread blocks: 8 waves per SIMD at most
 // counter block: CTR_N u64 statistics, then two launches x 8 tile counters x 128 B
 static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 2 * 8 * 128;
 
@@ -55,12 +62,18 @@ struct RenderParams {
     int32_t* gstack;
     uint32_t gstride;        // total threads in the launch
     unsigned long long* ctr;
+    unsigned long long* wave_log;  // count mode: kLogWords per wave (this launch), see mrt_debug_wave_log
     CamParams cam[kMaxBatch];    // frame mode: cam[0]; batch mode: one camera per frame
     float bg[3];
     int32_t n_lights, num_paths;
     uint32_t seed;
     int32_t fast_box;            // node boxes finite && tuning allows the hardware min/max box test
     int32_t sched;               // tile schedule (TileSched)
+    int32_t order;               // frame mode: 0 tiles bottom-up, 1 top-down (dequeue order only)
+    int32_t prio;                // 1: waves on their final tiles raise their issue priority
+    int32_t n_waves;             // waves in this launch (prio heuristic)
+    int32_t decline;             // >0: a wave in CU slot s stops taking tiles when fewer than s * decline remain
+    int32_t cus;                 // compute units (slot of a persistent block = blockIdx / cus)
     int32_t scalar_nodes;        // scalar fetch of wave-uniform nodes
     unsigned int* queue;         // 8 tile counters, 32 words apart (sched >= 2)
     // work: 8x8 tiles
@@ -245,6 +258,7 @@ __device__ __forceinline__ uint8_t map8(const uint8_t* lut, float v) { return lu
 struct TileSched {
     const RenderParams& P;
     int lane, mode, cur, step, end, home, probe, band;
+    uint32_t deq_ticks = 0;  // count mode: wall-clock ticks of the last dequeue
     __device__ TileSched(const RenderParams& P_, int wave, int lane_) : P(P_), lane(lane_) {
         mode = P.sched;
         home = blockIdx.x & 7;
@@ -265,9 +279,19 @@ struct TileSched {
     }
     __device__ int dequeue() {
         int item = -1;
+        const uint64_t q0 = P.wave_log ? wall_clock64() : 0;
         if (lane == 0) {
+            // decline: later-dispatched blocks (issue priority goes to older waves)
+            // leave the last tiles to the older, faster waves
+            const int slot = blockIdx.x / P.cus;
+            const int keep = P.decline * slot;
             while (probe < 8) {
                 const int c = (home + probe) & 7;
+                if (keep > 0 && mode == 2) {
+                    const unsigned seen = __hip_atomic_load(P.queue + c * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const long left = ((long)P.n_tiles - c + 7) / 8 - (long)seen;   // tiles left on counter c
+                    if (left * 8 < keep) { probe = 8; break; }
+                }
                 const unsigned v = atomicAdd(P.queue + c * 32, 1u);
                 const long idx = (mode == 3) ? (v < (unsigned)band ? (long)c * band + v : (long)P.n_tiles)
                                              : (long)c + 8l * v;
@@ -275,16 +299,30 @@ struct TileSched {
                 probe++;
             }
         }
-        return __shfl(item, 0);
+        item = __shfl(item, 0);
+        if (P.wave_log) deq_ticks = (uint32_t)(wall_clock64() - q0);
+        return item;
     }
     // items are wave-uniform: readfirstlane puts them (and the frame / camera
     // lookups derived from them) in SGPRs
+    // prio 1: a wave whose tile is among the last n_waves handed out raises its
+    // issue priority (those tiles bound the launch); prio 2: also lowers it back
+    // to 0 before earlier tiles (reset)
+    __device__ void boost(int item) {
+        if (P.prio && item >= 0 && mode >= 2 && item_rank(item) >= P.n_tiles - P.n_waves) __builtin_amdgcn_s_setprio(3);
+        else if (P.prio == 2) __builtin_amdgcn_s_setprio(0);
+    }
+    // dequeue position of a tile under sched 2 / 3
+    __device__ int item_rank(int item) const {
+        if (mode == 3) return (item % band) * 8 + item / band;
+        return item;  // interleaved counters hand out tiles in index order overall
+    }
     __device__ int first() {
-        if (mode >= 2) return __builtin_amdgcn_readfirstlane(dequeue());
+        if (mode >= 2) { const int it = __builtin_amdgcn_readfirstlane(dequeue()); boost(it); return it; }
         return __builtin_amdgcn_readfirstlane(cur < end ? cur : -1);
     }
     __device__ int next(int item) {
-        if (mode >= 2) return __builtin_amdgcn_readfirstlane(dequeue());
+        if (mode >= 2) { const int it = __builtin_amdgcn_readfirstlane(dequeue()); boost(it); return it; }
         item += step;
         return __builtin_amdgcn_readfirstlane(item < end ? item : -1);
     }
@@ -300,7 +338,8 @@ __device__ __forceinline__ int item_frame(const RenderParams& P, int item) {
 // work item + lane -> pixel (x, y) and output slot
 __device__ __forceinline__ bool item_pixel(const RenderParams& P, int item, int lane, int& x, int& y, size_t& slot) {
     if (P.mode == 0) {
-        int tx = item % P.tiles_x, ty = item / P.tiles_x;
+        const int t = P.order ? P.n_tiles - 1 - item : item;
+        int tx = t % P.tiles_x, ty = t / P.tiles_x;
         x = tx * 8 + (lane & 7);
         y = ty * 8 + (lane >> 3);
         slot = (size_t)y * P.cam[0].W + x;
@@ -322,7 +361,20 @@ __device__ __forceinline__ void load_tables(const uint16_t* g, uint16_t* s, int 
 }
 
 template <bool COUNT, bool PRIMARY = false>
-__device__ __forceinline__ void flush_stats(const RenderParams& P, const TravStats& st, uint32_t shadow, int lane) {
+__device__ __forceinline__ void flush_stats(const RenderParams& P, const TravStats& st, uint32_t shadow, int lane,
+                                            uint64_t t0, uint32_t tiles) {
+    if ((COUNT || P.wave_log) && lane == 0) {   // ramp / tail of the persistent waves
+        const uint64_t t1 = wall_clock64();
+        if (P.wave_log) {
+            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6));
+            r[0] = t0; r[1] = t1; r[2] = tiles;
+        }
+        unsigned long long* c = P.ctr + (PRIMARY ? CTR_TP : CTR_TS);
+        atomicMax(c + 0, (unsigned long long)~t0);
+        atomicMax(c + 1, (unsigned long long)t0);
+        atomicMax(c + 2, (unsigned long long)~t1);
+        atomicMax(c + 3, (unsigned long long)t1);
+    }
     // shadow rays (shade kernel) or primary hits (primary kernel), always counted
     unsigned long long sh = shadow;
     for (int off = 32; off > 0; off >>= 1) sh += __shfl_down(sh, off);
@@ -337,6 +389,7 @@ __device__ __forceinline__ void flush_stats(const RenderParams& P, const TravSta
             msp = max(msp, __shfl_down(msp, off));
         }
         if (lane == 0) {
+            if (P.wave_log) P.wave_log[kLogWords * ((size_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6)) + 3] = nv;
             atomicAdd(&P.ctr[CTR_NODES], nv);
             atomicAdd(&P.ctr[CTR_LEAVES], lv);
             if (PRIMARY) {
@@ -370,6 +423,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     load_tables(P.tables, s_tab, 1024);
+    const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -378,7 +432,15 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     uint32_t nhits = 0;
     unsigned long long wave_steps = 0;  // count mode: sum over tiles of max lane node visits
     TileSched ts(P, wave, lane);
+    uint32_t ntiles = 0;
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
+        if (P.wave_log && lane == 0 && ntiles < kLogTiles)
+        {
+            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
+            r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
+            r[4 + kLogTiles + ntiles] = ts.deq_ticks;
+        }
+        ntiles++;
         int x, y;
         size_t slot;
         const uint32_t n0 = st.nodes;
@@ -399,7 +461,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
         }
     }
     if (COUNT && lane == 0) atomicAdd(&P.ctr[CTR_WAVE_STEPS_P], wave_steps);
-    flush_stats<COUNT, true>(P, st, nhits, lane);
+    flush_stats<COUNT, true>(P, st, nhits, lane, t0, ntiles);
 }
 
 // Kernel 2: Scene::sampleScene shading of the primary hit with shadow rays.
@@ -408,6 +470,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     load_tables(P.tables, s_tab, 1024);
+    const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -415,7 +478,15 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     TravStats st;
     uint32_t shadow_total = 0;
     TileSched ts(P, wave, lane);
+    uint32_t ntiles = 0;
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
+        if (P.wave_log && lane == 0 && ntiles < kLogTiles)
+        {
+            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
+            r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
+            r[4 + kLogTiles + ntiles] = ts.deq_ticks;
+        }
+        ntiles++;
         int x, y;
         size_t slot;
         if (!item_pixel(P, item, lane, x, y, slot)) continue;
@@ -442,7 +513,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
         }
     }
-    flush_stats<COUNT>(P, st, shadow_total, lane);
+    flush_stats<COUNT>(P, st, shadow_total, lane, t0, ntiles);
 }
 
 
@@ -455,6 +526,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     load_tables(P.tables, s_tab, 1024);
+    const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -462,7 +534,15 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     TravStats st;
     uint32_t shadow_total = 0;
     TileSched ts(P, wave, lane);
+    uint32_t ntiles = 0;
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
+        if (P.wave_log && lane == 0 && ntiles < kLogTiles)
+        {
+            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
+            r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
+            r[4 + kLogTiles + ntiles] = ts.deq_ticks;
+        }
+        ntiles++;
         int x, y;
         size_t slot;
         if (!item_pixel(P, item, lane, x, y, slot)) continue;
@@ -549,7 +629,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
             o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
         }
     }
-    flush_stats<COUNT, false>(P, st, shadow_total, lane);
+    flush_stats<COUNT, false>(P, st, shadow_total, lane, t0, ntiles);
 }
 
 // Batched Scene::trace: one lane per query ray.
@@ -606,6 +686,23 @@ __global__ void unpack_kernel(const int32_t* items, int32_t n_items, const float
 }
 
 // ------------------------------------------------------------------ device state
+// Launch scratch of one stream: everything a render / trace launch writes
+// besides the caller's outputs.  Two launches on different streams never share
+// one, so frames can overlap (the tail of one persistent launch with the start
+// of the next).
+struct StreamCtx {
+    hipStream_t stream = nullptr;
+    int32_t* gstack = nullptr;               // traversal-stack spill columns
+    unsigned long long* ctr = nullptr;       // statistics + tile counters
+    unsigned long long* wave_log = nullptr;  // 2 launches x grid x 4 waves x kLogWords u64 (diagnostics)
+    int log_waves[2] = {0, 0};               // waves of the last logged primary / shade launch
+    float4* hitbuf = nullptr;                // kernel 1 -> kernel 2 hand-off (per output slot)
+    size_t hit_slots = 0;
+    bool last_was_render = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
+};
+static constexpr int kMaxStreamCtx = 16;
+
 struct DeviceState {
     int device = -1;
     QNode* nodes = nullptr;
@@ -617,23 +714,21 @@ struct DeviceState {
     DevLight* lights = nullptr;
     uint16_t* tables = nullptr;
     uint8_t* gamma = nullptr;
-    int32_t* gstack = nullptr;
     uint32_t gthreads = 0;
-    unsigned long long* ctr = nullptr;
     // scratch for the synchronous API
     float* d_rgb = nullptr;
     uint8_t* d_rgb8 = nullptr;
     size_t frame_px = 0;
-    // kernel 1 -> kernel 2 hand-off (per output slot)
-    float4* hitbuf = nullptr;
-    size_t hit_slots = 0;
     int grid = 0;                // upper bound of any launch (kMaxBlocksPerCU per CU)
     bool boxes_finite = false;
     int cus = 0;
     bool point_only = false;
-    bool last_was_render = false;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
+    int wall_khz = 0;            // wall_clock64() rate
     size_t bytes = 0;
+    // per-stream launch scratch: frames on different streams are in flight at once
+    std::mutex mu;
+    std::vector<StreamCtx*> ctxs;
+    StreamCtx* last = nullptr;   // context of the most recent launch (stats, wave log)
 };
 
 // Tuning knobs (mrt_set_tuning): A/B switches for performance work.
@@ -642,22 +737,54 @@ static int g_primary_waves = 7;   // launch-bounds occupancy target of the prima
 static int g_shade_waves = 6;     // same for shade1_kernel: 6, 7, 8
 static int g_lds_pad_kb = 0;      // extra dynamic LDS per workgroup (occupancy sweeps)
 static int g_sched = 2;           // TileSched mode 0..3 (2 measured fastest)
+static int g_order = 0;           // frame-mode tile dequeue order (0 bottom-up, 1 top-down)
+static int g_prio = 0;            // wave priority heuristic for the final tiles
+static int g_decline = 0;         // tiles per CU slot (decline heuristic), 0 = off
+static int g_wave_log = 0;        // 1: timing-only wave log on uninstrumented launches (diagnostics)
 static int g_scalar_nodes = 1;    // scalar-cache fetch of wave-uniform nodes
 static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
 
 static inline int fast_box(const DeviceState& d);
 
+static void free_ctx(StreamCtx* c) {
+    void* ptrs[] = {c->gstack, c->ctr, c->wave_log, c->hitbuf};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->evm) (void)hipEventDestroy(c->evm);
+    delete c;
+}
+
 static void free_device(DeviceState* d) {
     if (!d) return;
     if (d->device >= 0) (void)hipSetDevice(d->device);
+    (void)hipDeviceSynchronize();   // no launch may still use the scratch below
+    for (StreamCtx* c : d->ctxs) free_ctx(c);
     void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->tables,
-                    d->gamma, d->gstack, d->ctr, d->d_rgb, d->d_rgb8, d->hitbuf};
+                    d->gamma, d->d_rgb, d->d_rgb8};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    if (d->ev0) (void)hipEventDestroy(d->ev0);
-    if (d->ev1) (void)hipEventDestroy(d->ev1);
-    if (d->evm) (void)hipEventDestroy(d->evm);
     delete d;
+}
+
+// Scratch context of `stream` (created on first use, at most kMaxStreamCtx).
+static int get_ctx(DeviceState& d, hipStream_t stream, StreamCtx*& out) {
+    std::lock_guard<std::mutex> g(d.mu);
+    for (StreamCtx* c : d.ctxs)
+        if (c->stream == stream) { out = c; return MRT_OK; }
+    if ((int)d.ctxs.size() >= kMaxStreamCtx) { set_error("too many streams on one scene (max 16)"); return MRT_ERR_INVALID; }
+    StreamCtx* c = new StreamCtx();
+    c->stream = stream;
+    d.ctxs.push_back(c);   // owned by d from here (freed with it even if an allocation below fails)
+    HIP_OK(hipMalloc((void**)&c->gstack, (size_t)kGlobalStack * d.gthreads * sizeof(int32_t)));
+    HIP_OK(hipMalloc((void**)&c->ctr, kCtrBytes));
+    HIP_OK(hipMalloc((void**)&c->wave_log, (size_t)2 * d.grid * (kWG / 64) * kLogWords * sizeof(unsigned long long)));
+    HIP_OK(hipEventCreate(&c->ev0));
+    HIP_OK(hipEventCreate(&c->ev1));
+    HIP_OK(hipEventCreate(&c->evm));
+    out = c;
+    return MRT_OK;
 }
 
 template <typename T>
@@ -739,6 +866,7 @@ static int ensure_device(Scene& s, int device) {
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, device));
     d.cus = prop.multiProcessorCount;
+    if (hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) d.wall_khz = 0;
     d.grid = d.cus * kMaxBlocksPerCU;
     d.boxes_finite = true;
     for (const QNode& q : s.nodes)
@@ -746,11 +874,6 @@ static int ensure_device(Scene& s, int device) {
     d.point_only = true;
     for (const DevLight& l : s.lights) d.point_only &= (l.type == MRT_POINT_LIGHT);
     d.gthreads = (uint32_t)d.grid * kWG;
-    HIP_OK(hipMalloc((void**)&d.gstack, (size_t)kGlobalStack * d.gthreads * sizeof(int32_t)));
-    HIP_OK(hipMalloc((void**)&d.ctr, kCtrBytes));
-    HIP_OK(hipEventCreate(&d.ev0));
-    HIP_OK(hipEventCreate(&d.ev1));
-    HIP_OK(hipEventCreate(&d.evm));
     s.info.device_bytes = total;
     s.dev_dirty = false;
     return MRT_OK;
@@ -783,7 +906,7 @@ static void fill_params(const Scene& s, RenderParams& P) {
     const DeviceState& d = *s.dev;
     P.nodes = d.nodes; P.leaves = d.leaves; P.prims = d.prims; P.verts = d.verts; P.normals = d.normals;
     P.mats = d.mats; P.lights = d.lights; P.tables = d.tables; P.gamma = d.gamma;
-    P.gstack = d.gstack; P.gstride = d.gthreads; P.ctr = d.ctr;
+    P.gstride = d.gthreads;
     P.bg[0] = s.bg[0]; P.bg[1] = s.bg[1]; P.bg[2] = s.bg[2];
     P.n_lights = (int32_t)s.lights.size();
     P.num_paths = s.num_paths;
@@ -791,12 +914,13 @@ static void fill_params(const Scene& s, RenderParams& P) {
 
 static inline int fast_box(const DeviceState& d) { return (g_fast_box && d.boxes_finite) ? 1 : 0; }
 
-static int ensure_slots(DeviceState& d, size_t slots) {
-    if (slots <= d.hit_slots) return MRT_OK;
-    if (d.hitbuf) (void)hipFree(d.hitbuf);
-    d.hitbuf = nullptr; d.hit_slots = 0;
-    HIP_OK(hipMalloc((void**)&d.hitbuf, slots * sizeof(float4)));
-    d.hit_slots = slots;
+static int ensure_slots(StreamCtx& c, size_t slots) {
+    if (slots <= c.hit_slots) return MRT_OK;
+    // the old buffer may still be read by this stream's previous launch
+    if (c.hitbuf) { HIP_OK(hipStreamSynchronize(c.stream)); (void)hipFree(c.hitbuf); }
+    c.hitbuf = nullptr; c.hit_slots = 0;
+    HIP_OK(hipMalloc((void**)&c.hitbuf, slots * sizeof(float4)));
+    c.hit_slots = slots;
     return MRT_OK;
 }
 
@@ -856,33 +980,51 @@ static KernelFn pick_shade(bool c, bool po, bool f) {
 // shadow rays.  Events bracket both (kernel_ms covers the whole frame).
 static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hipStream_t stream) {
     DeviceState& d = *s.dev;
-    int rc = ensure_slots(d, slots);
+    StreamCtx* cp = nullptr;
+    int rc = get_ctx(d, stream, cp);
     if (rc) return rc;
-    P.hits = d.hitbuf;
+    StreamCtx& c = *cp;
+    if ((rc = ensure_slots(c, slots))) return rc;
+    P.hits = c.hitbuf;
+    P.gstack = c.gstack;
+    P.ctr = c.ctr;
     P.fast_box = fast_box(d);
     P.sched = g_sched;
+    P.order = g_order;
+    P.prio = g_prio;
+    P.decline = g_decline;
+    P.cus = d.cus;
     P.scalar_nodes = g_scalar_nodes;
-    HIP_OK(hipMemsetAsync(d.ctr, 0, kCtrBytes, stream));
-    unsigned int* qbase = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(d.ctr) + CTR_N * sizeof(unsigned long long));
+    HIP_OK(hipMemsetAsync(c.ctr, 0, kCtrBytes, stream));
+    unsigned int* qbase = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(c.ctr) + CTR_N * sizeof(unsigned long long));
     P.queue = qbase;
     const size_t pad = (size_t)g_lds_pad_kb * 1024;
     const int items = (P.n_tiles + 3) / 4;
+    const size_t log_stride = (size_t)d.grid * (kWG / 64) * kLogWords;
+    const bool logw = count || g_wave_log;   // wave log: count mode, or timing-only on the timed kernels
+    if (logw) HIP_OK(hipMemsetAsync(c.wave_log, 0, 2 * log_stride * sizeof(unsigned long long), stream));
+    int which = 0;
     auto launch = [&](KernelFn f) -> int {
         const int g = std::max(1, std::min(std::min(d.grid, d.cus * blocks_per_cu(f, pad)), items));
+        P.wave_log = logw ? c.wave_log + which * log_stride : nullptr;
+        P.n_waves = g * (kWG / 64);
+        if (logw) c.log_waves[which] = g * (kWG / 64);
+        which++;
         void* args[] = {&P};
         HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(f), dim3(g), dim3(kWG), args, pad, stream));
         return MRT_OK;
     };
-    HIP_OK(hipEventRecord(d.ev0, stream));
+    HIP_OK(hipEventRecord(c.ev0, stream));
     const bool fb = P.fast_box != 0;
     if ((rc = launch(pick_primary(g_primary_waves, count, fb)))) return rc;
-    HIP_OK(hipEventRecord(d.evm, stream));
+    HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
     const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1;
     if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb)))) return rc;
-    d.last_was_render = true;
+    c.last_was_render = true;
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(d.ev1, stream));
+    HIP_OK(hipEventRecord(c.ev1, stream));
+    d.last = &c;
     s.last = mrt_stats{};
     return MRT_OK;
 }
@@ -1182,7 +1324,7 @@ int mrt_render(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
     if ((rc = launch_render(S, P, px, opts->count_visits != 0, nullptr))) return rc;
     HIP_OK(hipMemcpy(rgb, d.d_rgb, px * 12, hipMemcpyDeviceToHost));
     if (rgb8) HIP_OK(hipMemcpy(rgb8, d.d_rgb8, px * 3, hipMemcpyDeviceToHost));
-    if (hits) HIP_OK(hipMemcpy(hits, d.hitbuf, px * sizeof(mrt_hit), hipMemcpyDeviceToHost));
+    if (hits) HIP_OK(hipMemcpy(hits, d.last->hitbuf, px * sizeof(mrt_hit), hipMemcpyDeviceToHost));
     S.last.primary_rays = px;
     mrt_stats tmp;
     if ((rc = mrt_scene_last_stats(s, &tmp))) return rc;
@@ -1195,15 +1337,17 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     Scene& S = s->impl;
     if (!S.dev) { set_error("nothing rendered"); return MRT_ERR_INVALID; }
     DeviceState& d = *S.dev;
+    if (!d.last) { set_error("nothing rendered"); return MRT_ERR_INVALID; }
+    const StreamCtx& x = *d.last;
     HIP_OK(hipSetDevice(d.device));
-    HIP_OK(hipEventSynchronize(d.ev1));
+    HIP_OK(hipEventSynchronize(x.ev1));
     unsigned long long c[CTR_N];
-    HIP_OK(hipMemcpy(c, d.ctr, sizeof c, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(c, x.ctr, sizeof c, hipMemcpyDeviceToHost));
     float ms = 0.f, ms1 = 0.f, ms2 = 0.f;
-    HIP_OK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
-    if (d.last_was_render) {
-        HIP_OK(hipEventElapsedTime(&ms1, d.ev0, d.evm));
-        HIP_OK(hipEventElapsedTime(&ms2, d.evm, d.ev1));
+    HIP_OK(hipEventElapsedTime(&ms, x.ev0, x.ev1));
+    if (x.last_was_render) {
+        HIP_OK(hipEventElapsedTime(&ms1, x.ev0, x.evm));
+        HIP_OK(hipEventElapsedTime(&ms2, x.evm, x.ev1));
     }
     S.last.primary_ms = ms1;
     S.last.shade_ms = ms2;
@@ -1216,6 +1360,17 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     S.last.node_visits = c[CTR_NODES];
     S.last.leaf_visits = c[CTR_LEAVES];
     S.last.max_stack = (int32_t)c[CTR_MAXSP];
+    if (x.last_was_render && c[CTR_TP + 3]) {   // count mode: wave ramp / tail (wall clock)
+        const double us = d.wall_khz > 0 ? 1e3 / d.wall_khz : 0.0;
+        for (int k = 0; k < 2; k++) {
+            const unsigned long long* t = c + (k ? CTR_TS : CTR_TP);
+            const double s0 = (double)~t[0], s1 = (double)t[1], e0 = (double)~t[2], e1 = (double)t[3];
+            float* o = k ? &S.last.shade_span_us : &S.last.primary_span_us;
+            o[0] = (float)((e1 - s0) * us);   // first wave start -> last wave end
+            o[1] = (float)((s1 - s0) * us);   // ramp: first -> last wave start
+            o[2] = (float)((e1 - e0) * us);   // tail: first -> last wave end
+        }
+    }
     S.last.kernel_ms = ms;
     *out = S.last;
     if (c[CTR_OVERFLOW]) { set_error("traversal stack overflow"); return MRT_ERR_OVERFLOW; }
@@ -1232,18 +1387,22 @@ int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const floa
     HIP_OK(hipSetDevice(dev));
     DeviceState& d = *S.dev;
     if (n == 0) return MRT_OK;
-    HIP_OK(hipMemsetAsync(d.ctr, 0, CTR_N * sizeof(unsigned long long), (hipStream_t)stream));
-    d.last_was_render = false;
+    StreamCtx* cp = nullptr;
+    if ((rc = get_ctx(d, (hipStream_t)stream, cp))) return rc;
+    StreamCtx& c = *cp;
+    HIP_OK(hipMemsetAsync(c.ctr, 0, CTR_N * sizeof(unsigned long long), (hipStream_t)stream));
+    c.last_was_render = false;
     int grid = (int)std::min<size_t>((size_t)d.grid, (n + kWG - 1) / kWG);
-    HIP_OK(hipEventRecord(d.ev0, (hipStream_t)stream));
+    HIP_OK(hipEventRecord(c.ev0, (hipStream_t)stream));
     if (any_hit)
         hipLaunchKernelGGL(trace_kernel<true>, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables,
-                           d.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, d.ctr, fast_box(d));
+                           c.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, c.ctr, fast_box(d));
     else
         hipLaunchKernelGGL(trace_kernel<false>, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables,
-                           d.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, d.ctr, fast_box(d));
+                           c.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, c.ctr, fast_box(d));
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(d.ev1, (hipStream_t)stream));
+    HIP_OK(hipEventRecord(c.ev1, (hipStream_t)stream));
+    d.last = &c;
     return MRT_OK;
 }
 
@@ -1271,11 +1430,32 @@ int mrt_trace(mrt_scene* s, const float* o, const float* d, const float* tmin, c
     if (rc == MRT_OK) {
         HIP_OK(hipMemcpy(out, bout, n * sizeof(mrt_hit), hipMemcpyDeviceToHost));
         unsigned long long c[CTR_N];
-        HIP_OK(hipMemcpy(c, S.dev->ctr, sizeof c, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(c, S.dev->last->ctr, sizeof c, hipMemcpyDeviceToHost));
         if (c[CTR_OVERFLOW]) { set_error("traversal stack overflow"); rc = MRT_ERR_OVERFLOW; }
     }
     (void)hipFree(bo); (void)hipFree(bd); (void)hipFree(bmin); (void)hipFree(bmax); (void)hipFree(bout);
     return rc;
+}
+
+int mrt_debug_wave_log(const mrt_scene* cs, int launch, uint64_t* out, int32_t max_waves) {
+    if (!cs || !out || launch < 0 || launch > 1 || max_waves < 0) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    const Scene& S = cs->impl;
+    if (!S.dev) { set_error("nothing rendered"); return MRT_ERR_INVALID; }
+    const DeviceState& d = *S.dev;
+    HIP_OK(hipSetDevice(d.device));
+    if (!d.last) { set_error("nothing rendered"); return MRT_ERR_INVALID; }
+    HIP_OK(hipEventSynchronize(d.last->ev1));
+    const int n = std::min(max_waves, d.last->log_waves[launch]);
+    const size_t log_stride = (size_t)d.grid * (kWG / 64) * kLogWords;
+    if (n > 0)
+        HIP_OK(hipMemcpy(out, d.last->wave_log + launch * log_stride, (size_t)n * kLogWords * sizeof(uint64_t),
+                         hipMemcpyDeviceToHost));
+    return n;
+}
+
+int mrt_device_wall_clock_khz(const mrt_scene* cs) {
+    if (!cs || !cs->impl.dev) { set_error("scene not on a device"); return MRT_ERR_INVALID; }
+    return cs->impl.dev->wall_khz;
 }
 
 int mrt_set_tuning(const char* key, int value) {
@@ -1290,6 +1470,16 @@ int mrt_set_tuning(const char* key, int value) {
         g_shade_waves = value;
     } else if (k == "scalar_nodes") {
         g_scalar_nodes = value ? 1 : 0;
+    } else if (k == "decline") {
+        if (value < 0 || value > 1 << 20) { set_error("decline out of range"); return MRT_ERR_INVALID; }
+        g_decline = value;
+    } else if (k == "wave_log") {
+        g_wave_log = value ? 1 : 0;
+    } else if (k == "order") {
+        g_order = value ? 1 : 0;
+    } else if (k == "prio") {
+        if (value < 0 || value > 2) { set_error("prio must be 0..2"); return MRT_ERR_INVALID; }
+        g_prio = value;
     } else if (k == "shade1") {
         g_shade1 = value ? 1 : 0;
     } else if (k == "sched") {

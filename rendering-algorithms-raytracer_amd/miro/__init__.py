@@ -353,6 +353,17 @@ class Scene:
         check(lib().mrt_scene_last_stats(self.handle, C.byref(st)), "stats")
         return {k: getattr(st, k) for k, _ in st._fields_}
 
+    def wave_log(self, launch: int):
+        """Per-wave records of the last count-mode render (diagnostics):
+        array (waves, 60): start, end (device wall-clock ticks), tiles, node
+        visits, then per tile (first 28) tile id << 40 | start tick & (2^40 - 1),
+        then per tile its dequeue time in ticks;
+        for launch 0 (primary) or 1 (shade); plus the clock rate (kHz)."""
+        L = lib()
+        out = np.zeros((1 << 16, 60), np.uint64)
+        n = check(L.mrt_debug_wave_log(self.handle, int(launch), out.ctypes.data, len(out)), "wave_log")
+        return out[:n].copy(), int(L.mrt_device_wall_clock_khz(self.handle))
+
     # -- ray queries (src/Scene.cpp:295-298)
     def traceBatch(self, o, d, tmin=0.001, tmax=1e12, any_hit=False):
         o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)

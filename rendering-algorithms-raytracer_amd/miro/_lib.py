@@ -21,6 +21,7 @@ EXPORTS = [
     "mrt_scene_upload", "mrt_render", "mrt_render_buckets_async", "mrt_unpack_buckets_async",
     "mrt_render_frame_async", "mrt_trace", "mrt_trace_async", "mrt_scene_last_stats", "mrt_rcp_nr",
     "mrt_rsqrt_nr", "mrt_set_tuning", "mrt_render_batch_async", "mrt_unpack_batch_async",
+    "mrt_debug_wave_log", "mrt_device_wall_clock_khz",
 ]
 
 
@@ -65,7 +66,9 @@ class mrt_stats(C.Structure):
                 ("leaf_visits", C.c_uint64), ("primary_node_visits", C.c_uint64),
                 ("primary_leaf_visits", C.c_uint64), ("primary_hits", C.c_uint64), ("primary_wave_steps", C.c_uint64),
                 ("primary_uniform_visits", C.c_uint64), ("kernel_ms", C.c_float), ("primary_ms", C.c_float),
-                ("shade_ms", C.c_float), ("max_stack", C.c_int32)]
+                ("shade_ms", C.c_float), ("max_stack", C.c_int32),
+                ("primary_span_us", C.c_float), ("primary_ramp_us", C.c_float), ("primary_tail_us", C.c_float),
+                ("shade_span_us", C.c_float), ("shade_ramp_us", C.c_float), ("shade_tail_us", C.c_float)]
 
 
 _fp = C.POINTER(C.c_float)
@@ -127,6 +130,8 @@ def load():
                                   C.c_int, C.c_void_p, C.c_void_p]
     L.mrt_scene_last_stats.argtypes = [C.c_void_p, C.POINTER(mrt_stats)]
     L.mrt_set_tuning.argtypes = [C.c_char_p, C.c_int]
+    L.mrt_debug_wave_log.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int32]
+    L.mrt_device_wall_clock_khz.argtypes = [C.c_void_p]
     L.mrt_rcp_nr.argtypes = [C.c_float]
     L.mrt_rcp_nr.restype = C.c_float
     L.mrt_rsqrt_nr.argtypes = [C.c_float]
