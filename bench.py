@@ -153,7 +153,8 @@ def main():
     frame = [torch.empty(H * W * 3, dtype=torch.float32, device="cuda") for _ in range(inflight)] \
         if use_frame_path else None
     frame8 = [torch.empty(H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(inflight)]
-    frames8 = frame8[0] if use_frame_path else torch.empty(n_frames * H * W * 3, dtype=torch.uint8, device="cuda")
+    frames8 = [frame8[0]] if use_frame_path else \
+        [torch.empty(n_frames * H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(2)]
     camc = (_lib.mrt_camera * n_frames)(*[c._c() for c in cams])
     opts_count = _lib.mrt_render_opts(W, H, dev, 1, 1, 0, 0)
     opts = _lib.mrt_render_opts(W, H, dev, 0, 1, 0, 0)
@@ -166,15 +167,18 @@ def main():
 
         def render(ids, out, o=opts):
             _lib.check(L.mrt_render_batch_async(scene.handle, camc, n_frames, C.byref(o), ids.data_ptr(), len(ids),
-                                                None, out.data_ptr(), sh), "render batch")
+                                                None, out.data_ptr(), torch.cuda.current_stream().cuda_stream),
+                       "render batch")
 
-        def unpack(ids, gathered):
+        def unpack(ids, gathered, b):
             _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(ids), None, gathered.data_ptr(), W, H, n_frames,
-                                                None, frames8.data_ptr(), scene.handle, sh), "unpack")
+                                                None, frames8[b].data_ptr(), scene.handle,
+                                                torch.cuda.current_stream().cuda_stream), "unpack")
 
+        # two streams: consecutive steps' launch pairs overlap (libmrt keeps scratch per stream)
         pipe = tiles_mod.BatchPipeline(world, rank, dist, items, all_items,
                                        lambda k: torch.empty(k * per * 1024 * 3, dtype=torch.uint8, device="cuda"),
-                                       render, unpack)
+                                       render, unpack, streams=[torch.cuda.Stream(), torch.cuda.Stream()])
 
     nstep = [0]
 

@@ -18,6 +18,7 @@ the GPU box, gloo in the CPU tests), which scatters them into the frame.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import List
 
 import numpy as np
@@ -88,30 +89,42 @@ class BatchPipeline:
     k is waited on (work.wait() orders the compute stream after the collective
     on nccl; it blocks on gloo).  Rank 0 unpacks step k after enqueuing the
     render of step k + 1, so its next render is not queued behind the
-    collective."""
+    collective.  With `streams` (two torch.cuda.Stream), everything of buffer b
+    runs on streams[b]: consecutive steps' launches overlap on the device.
+    unpack(all_items, gathered, b) gets the buffer index, so rank 0 can keep
+    one output per buffer."""
 
-    def __init__(self, world, rank, dist, items, all_items, new_tiles, render, unpack):
+    def __init__(self, world, rank, dist, items, all_items, new_tiles, render, unpack, streams=None):
         self.world, self.rank, self.dist = world, rank, dist
         self.items, self.all_items = items, all_items
         self.render, self.unpack = render, unpack
+        self.streams = streams
         self.tiles = [new_tiles(1), new_tiles(1)]
         self.recv = [new_tiles(world), new_tiles(world)] if (rank == 0 and world > 1) else None
         self.work = [None, None]
         self.pending = None      # (work, buffer) of the step rank 0 has not unpacked yet
         self.k = 0
 
+    def _on(self, b):
+        if self.streams is None:
+            return contextlib.nullcontext()
+        import torch
+        return torch.cuda.stream(self.streams[b])
+
     def step(self):
         b = self.k & 1
-        if self.work[b] is not None:
-            self.work[b].wait()
-            self.work[b] = None
-        self.render(self.items, self.tiles[b])
-        if self.world == 1:
-            self.unpack(self.all_items, self.tiles[b])
-        else:
-            outs = list(self.recv[b].chunk(self.world)) if self.rank == 0 else None
-            w = self.dist.gather(self.tiles[b], outs, dst=0, async_op=True)
-            self.work[b] = w
+        with self._on(b):
+            if self.work[b] is not None:
+                self.work[b].wait()
+                self.work[b] = None
+            self.render(self.items, self.tiles[b])
+            if self.world == 1:
+                self.unpack(self.all_items, self.tiles[b], b)
+            else:
+                outs = list(self.recv[b].chunk(self.world)) if self.rank == 0 else None
+                w = self.dist.gather(self.tiles[b], outs, dst=0, async_op=True)
+                self.work[b] = w
+        if self.world > 1:
             self._drain()
             if self.rank == 0:
                 self.pending = (w, b)
@@ -120,8 +133,9 @@ class BatchPipeline:
     def _drain(self):
         if self.pending is not None:
             w, pb = self.pending
-            w.wait()
-            self.unpack(self.all_items, self.recv[pb])
+            with self._on(pb):
+                w.wait()
+                self.unpack(self.all_items, self.recv[pb], pb)
             self.pending = None
 
     def flush(self):
@@ -129,5 +143,6 @@ class BatchPipeline:
         self._drain()
         for i in range(2):
             if self.work[i] is not None:
-                self.work[i].wait()
+                with self._on(i):
+                    self.work[i].wait()
                 self.work[i] = None

@@ -115,7 +115,7 @@ def _batch_worker(rank, world, port, W, H, n_frames, steps, result_path):
                 h, w = min(32, H - y0), min(32, W - x0)
                 t[slot, :h, :w] = torch.from_numpy(r["rgb"][y0:y0 + h, x0:x0 + w])
 
-        def unpack(ids, gathered):
+        def unpack(ids, gathered, b):
             state["unpack"] += 1
             frames = np.zeros((n_frames, H, W, 3), np.float32)
             t = gathered.view(-1, 32, 32, 3).numpy()
