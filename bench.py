@@ -85,7 +85,8 @@ def cpu_baseline(cfg_key, seconds):
     cfg = scenes.CONFIGS[cfg_key]
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     s = O.OracleScene()
-    m = s.add_material(cfg["material"]["kind"], kd=cfg["material"]["kd"])
+    mat = cfg["material"]
+    m = s.add_material(mat["kind"], kd=mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0))
     if cfg["mesh"] == "sponza":
         s.add_obj(scenes.sponza_obj(), m)
     elif cfg["mesh"] == "bunny":
@@ -96,8 +97,12 @@ def cpu_baseline(cfg_key, seconds):
         f = np.load(os.path.join(ROOT, "tests", "golden", "cornell_box_mesh.npz"))
         s.add_mesh(f["verts"], f["normals"], f["vidx"], f["nidx"], m)
     for l in cfg["lights"]:
-        s.add_point_light(l["pos"], l["power"])
+        if l["type"] == "point":
+            s.add_point_light(l["pos"], l["power"])
+        else:
+            s.add_rect_light(l["v1"], l["v2"], l["v3"], l["power"], l.get("samples", 1), l.get("noise", 0.001))
     s.set_bg(cfg["bg"])
+    s.set_num_paths(cfg.get("num_paths", 1))
     s.build()
     W, H = cfg["W"], cfg["H"]
     rays, t_total, frames = 0, 0.0, 0
@@ -265,7 +270,7 @@ def main():
         except Exception:
             traffic = None
     out = {
-        "metric": "Mray/s (primary+shadow) on Sponza 1920x1080",
+        "metric": "Mray/s (primary+shadow) on Sponza 1920x1080" + ("" if args.config == "C3" else f" [{args.config}]"),
         "value": round(value, 2), "unit": "Mray/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",

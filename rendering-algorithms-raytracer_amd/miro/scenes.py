@@ -251,6 +251,16 @@ CONFIGS = {
                camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
                lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
                material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza"),
+    # C4: Sponza stand-in, RectangleLight (8,10,2)/(8,10,-2)/(-8,10,2) power 1.5 and
+    # Scene::m_numPaths = 16 (makeSponzaScenePathTrace, src/assignment2.h:663-708, direct
+    # lighting only): 16 shade() calls per hit, one area-light shadow ray each;
+    # Blinn with a specular lobe (specAmt > 0)
+    "C4": dict(name="sponza stand-in (~66k tris) 1920x1080 Blinn+RectangleLight, 16 paths", W=1920, H=1080,
+               camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
+               lights=[dict(type="rect", v1=(8.0, 10.0, 2.0), v2=(8.0, 10.0, -2.0), v3=(-8.0, 10.0, 2.0),
+                            power=1.5, samples=1, noise=0.001)],
+               material=dict(kind="blinn", kd=(1, 1, 1), specExp=8.0, specAmt=0.25), bg=(0.0, 0.0, 0.2),
+               mesh="sponza", num_paths=16),
 }
 
 
@@ -278,7 +288,8 @@ def build_config(key, device=0):
     cfg = CONFIGS[key]
     scene = miro.Scene(device=device)
     mat = cfg["material"]
-    material = miro.Lambert(mat["kd"]) if mat["kind"] == "lambert" else miro.Blinn(mat["kd"])
+    material = miro.Lambert(mat["kd"]) if mat["kind"] == "lambert" else \
+        miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0))
     mesh = miro.TriangleMesh()
     if cfg["mesh"] == "cornell":
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -295,11 +306,18 @@ def build_config(key, device=0):
         fl.setN1((0, 1, 0)); fl.setN2((0, 1, 0)); fl.setN3((0, 1, 0))
         miro.makeMeshObjs(scene, fl, material)
     for l in cfg["lights"]:
-        pl = miro.PointLight()
-        pl.setPosition(l["pos"])
+        if l["type"] == "point":
+            pl = miro.PointLight()
+            pl.setPosition(l["pos"])
+        else:
+            pl = miro.RectangleLight()
+            pl.setVertices(l["v1"], l["v2"], l["v3"])
+            pl.setSamples(l.get("samples", 1))
+            pl.setNoiseThreshold(l.get("noise", 0.001))
         pl.setPower(l["power"])
         scene.addLight(pl)
     scene.setBGColor(cfg["bg"])
+    scene.setNumPaths(cfg.get("num_paths", 1))
     scene.preCalc()
     cam = miro.Camera()
     c = cfg["camera"]

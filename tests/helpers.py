@@ -69,6 +69,7 @@ def camera(c):
 
 def config_scene(key, **kw):
     cfg = scenes.CONFIGS[key]
+    kw.setdefault("num_paths", cfg.get("num_paths", 1))
     if cfg["mesh"] == "cornell":
         return scene_pair(cfg, meshes=[fixture_mesh("cornell_box")], **kw)
     if cfg["mesh"] == "bunny":

@@ -259,3 +259,27 @@ def test_batch_render_equals_per_camera_frames():
     assert L.mrt_render_batch_async(P.handle, camc, 17, C.byref(opts), ids.data_ptr(), n, tiles.data_ptr(), None,
                                     stream) == -1
     assert L.mrt_render_batch_async(P.handle, camc, F, C.byref(opts), ids.data_ptr(), n, None, None, stream) == -1
+
+
+def assert_close_rgb(got, ref, rtol=1e-4):
+    """north_star tolerance for configs with a libm pow (Blinn specAmt > 0):
+    |got - ref| <= rtol * |ref| per channel (exact zeros must stay zero)."""
+    g, r = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    bad = np.abs(g - r) > rtol * np.abs(r)
+    assert not bad.any(), f"{bad.sum()} channels beyond {rtol} relative"
+    return float(np.mean(bits(got) == bits(ref)))
+
+
+@pytest.mark.parametrize("W,H", [(160, 90), (97, 61)])
+def test_c4_area_light_16_paths_matches_oracle(W, H):
+    """C4: RectangleLight, Scene::m_numPaths = 16, Blinn with a specular lobe.
+    Hits, shadow-ray counts bit-exact; float RGB within 1e-4 relative (pow)."""
+    P, Osc, cam = config_scene("C4")
+    img, hits = render(P, cam, W, H)
+    ref = Osc.render(cam, W, H, threads=8)
+    assert np.array_equal(hits["prim"], ref["hits"]["prim"])
+    assert P.last_stats["shadow_rays"] == ref["shadow_rays"]
+    exact = assert_close_rgb(img.rgb, ref["rgb"])
+    assert exact > 0.99, exact
+    same = np.all(bits(img.rgb) == bits(ref["rgb"]), axis=-1)
+    assert np.array_equal(img.pixels[same], ref["rgb8"][same])
