@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 1
+#define MRT_ABI_VERSION 2
 
 enum {
     MRT_OK = 0,
@@ -41,7 +41,7 @@ enum {
 };
 
 enum { MRT_LAMBERT = 0, MRT_BLINN = 1 };                 /* src/Lambert.h, src/Blinn.h */
-enum { MRT_POINT_LIGHT = 0, MRT_RECT_LIGHT = 1 };        /* src/Light.h:13 lightType_t  */
+enum { MRT_POINT_LIGHT = 0, MRT_RECT_LIGHT = 1, MRT_DOME_LIGHT = 2 }; /* src/Light.h:9 lightType_t */
 
 typedef struct mrt_scene mrt_scene;
 
@@ -54,13 +54,16 @@ typedef struct {
 
 /* Light as data (replaces virtual Light::sampleLight, src/Light.h:35). */
 typedef struct {
-    int32_t type;            /* MRT_POINT_LIGHT | MRT_RECT_LIGHT                       */
+    int32_t type;            /* MRT_POINT_LIGHT | MRT_RECT_LIGHT | MRT_DOME_LIGHT      */
     float pos[3];            /* PointLight::setPosition                                */
     float v1[3], v2[3], v3[3];/* RectangleLight::setVertices                           */
-    float power;             /* Light::setPower (area scaling applied internally)      */
+    float power;             /* Light::setPower (area scaling applied internally);
+                                DomeLight::setPower = m_Gain                           */
     int32_t samples;         /* Light::setSamples                                      */
     float noise_threshold;   /* Light::setNoiseThreshold (default 0.001)               */
-    int32_t cast_shadows;    /* Light::setCastShadows                                  */
+    int32_t cast_shadows;    /* Light::setCastShadows (a dome light always casts)      */
+    int32_t texture;         /* MRT_DOME_LIGHT: DomeLight::setTexture, a texture id of
+                                mrt_scene_add_texture (-1 for the other lights)        */
 } mrt_light;
 
 /* Camera (src/Camera.h:26-45): eye, lookAt, up, vertical FOV in degrees. */
@@ -143,6 +146,28 @@ int mrt_scene_mesh_export(const mrt_scene* s, int mesh, float* verts, float* nor
 int mrt_scene_set_background(mrt_scene* s, const float rgb[3]);
 /* Scene::m_numPaths (src/Scene.h:61): shade() calls per primary hit */
 int mrt_scene_set_num_paths(mrt_scene* s, int num_paths);
+/* ---- images and image-based lighting -------------------------------------
+ * HDRLoader::load (src/hdrloader.cpp:29-97, via RawImage::loadImage/loadHDR,
+ * src/RawImage.cpp:16-32): mrt_hdr_info reads the header, mrt_hdr_load decodes
+ * into caller memory, width*height*3 floats, row 0 = the top (first) scanline. */
+int mrt_hdr_info(const char* path, int32_t* width, int32_t* height);
+int mrt_hdr_load(const char* path, float* rgb, int32_t width, int32_t height);
+/* new RawImage(w, h, data, HDR) + new Texture(image) (src/RawImage.cpp:9-14,
+ * src/Texture.h:13): copies width*height*3 floats (row 0 = top).  Returns the
+ * texture id (<= 16 per scene). */
+int mrt_scene_add_texture(mrt_scene* s, const float* rgb, int32_t width, int32_t height);
+/* Scene::setEnvMap + Scene::setEnvExposure (src/Scene.h:23-24): primary rays
+ * that miss return the lat-long lookup x exposure instead of the background
+ * (src/Scene.cpp:236-239).  texture = -1 clears. */
+int mrt_scene_set_env_map(mrt_scene* s, int32_t texture, float exposure);
+/* Importance tables of dome light `light` (DomeLight::setTexture,
+ * src/DomeLight.cpp:8-78), for inspection: cdf_u[nu+1], func_u[nu],
+ * cdf_v[nu*(nv+1)], func_v[nu*nv], func_int[nu+1] (column integrals, then the u
+ * integral), cos_u/sin_u[nu+1], cos_v/sin_v[nv+1]. */
+int mrt_scene_dome_info(const mrt_scene* s, int32_t light, int32_t* nu, int32_t* nv);
+int mrt_scene_dome_export(const mrt_scene* s, int32_t light, float* cdf_u, float* func_u, float* cdf_v,
+                          float* func_v, float* func_int, float* cos_u, float* sin_u, float* cos_v, float* sin_v);
+
 /* Scene::preCalc -> BVH::build (src/Scene.cpp:62-79, src/BVH.cpp:457-575):
  * binned SAH, 4-wide collapse, host-side; then uploads to the device lazily. */
 int mrt_scene_build_bvh(mrt_scene* s);

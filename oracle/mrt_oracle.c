@@ -14,6 +14,7 @@
  * Compile with -ffp-contract=off and no fast-math (the Makefile does).
  */
 #include "mrt_oracle.h"
+#include "oro_ibl.h"
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -184,10 +185,15 @@ typedef struct {               /* BVH_Node::TriCache4 (src/BVH.h:37-50) */
     int32_t prim[4];
 } qleaf;
 
+#define ORO_MAX_TEX 16
+
 struct oro_scene {
     mesh_t* meshes; int n_meshes, cap_meshes;
     oro_material* mats; int n_mats;
     oro_light* lights; int n_lights;
+    ibl_dome* domes;                  /* per light; zeroed for non-dome lights */
+    ibl_image tex[ORO_MAX_TEX]; int n_tex;
+    int env_tex; float env_exposure;  /* Scene::m_envMap / m_envExposure */
     v3 bg;
     int num_paths;
     /* objects (Object*): one per triangle, scene order (makeMeshObjs) */
@@ -203,6 +209,8 @@ oro_scene* oro_scene_create(void) {
     oro_scene* s = (oro_scene*)calloc(1, sizeof(oro_scene));
     s->bg = V(0, 0, 0);
     s->num_paths = 1;
+    s->env_tex = -1;
+    s->env_exposure = 1.0f;
     return s;
 }
 static void free_build(oro_scene* s) {
@@ -216,7 +224,9 @@ void oro_scene_destroy(oro_scene* s) {
         free(s->meshes[i].verts); free(s->meshes[i].normals);
         free(s->meshes[i].vidx); free(s->meshes[i].nidx);
     }
-    free(s->meshes); free(s->mats); free(s->lights);
+    for (int i = 0; i < s->n_lights; i++) ibl_dome_free(&s->domes[i]);
+    for (int i = 0; i < s->n_tex; i++) free(s->tex[i].rgb);
+    free(s->meshes); free(s->mats); free(s->lights); free(s->domes);
     free_build(s);
     free(s);
 }
@@ -226,12 +236,72 @@ int oro_scene_add_material(oro_scene* s, const oro_material* m) {
     return s->n_mats++;
 }
 int oro_scene_add_light(oro_scene* s, const oro_light* l) {
+    ibl_dome dome;
+    memset(&dome, 0, sizeof dome);
+    if (l->type == ORO_DOME_LIGHT) {   /* DomeLight::setTexture, src/DomeLight.cpp:8-78 */
+        if (l->texture < 0 || l->texture >= s->n_tex) return -1;
+        if (ibl_dome_init(&dome, &s->tex[l->texture]) != 0) { ibl_dome_free(&dome); return -2; }
+    }
     s->lights = (oro_light*)realloc(s->lights, sizeof(oro_light) * (s->n_lights + 1));
+    s->domes = (ibl_dome*)realloc(s->domes, sizeof(ibl_dome) * (s->n_lights + 1));
     s->lights[s->n_lights] = *l;
+    s->domes[s->n_lights] = dome;
     return s->n_lights++;
 }
 void oro_scene_set_bg(oro_scene* s, float r, float g, float b) { s->bg = V(r, g, b); }
 void oro_scene_set_num_paths(oro_scene* s, int n) { s->num_paths = n < 1 ? 1 : n; }
+
+int oro_scene_add_texture(oro_scene* s, const float* rgb, int w, int h) {
+    if (s->n_tex >= ORO_MAX_TEX || !rgb || w <= 0 || h <= 0) return -1;
+    size_t n = (size_t)w * h * 3;
+    ibl_image* t = &s->tex[s->n_tex];
+    t->rgb = (float*)malloc(sizeof(float) * n);
+    memcpy(t->rgb, rgb, sizeof(float) * n);
+    t->W = w;
+    t->H = h;
+    return s->n_tex++;
+}
+int oro_scene_set_env_map(oro_scene* s, int texture, float exposure) {
+    if (texture < -1 || texture >= s->n_tex) return -1;
+    s->env_tex = texture;
+    s->env_exposure = exposure;
+    return 0;
+}
+int oro_hdr_info(const char* path, int* w, int* h) { return ibl_hdr_read(path, NULL, 0, 0, w, h); }
+int oro_hdr_load(const char* path, float* rgb, int w, int h) {
+    int ww = 0, hh = 0;
+    return ibl_hdr_read(path, rgb, w, h, &ww, &hh);
+}
+int oro_dome_info(const oro_scene* s, int light, int* nu, int* nv) {
+    if (light < 0 || light >= s->n_lights || s->lights[light].type != ORO_DOME_LIGHT) return -1;
+    *nu = s->domes[light].nu;
+    *nv = s->domes[light].nv;
+    return 0;
+}
+int oro_dome_export(const oro_scene* s, int light, float* cdf_u, float* func_u, float* cdf_v, float* func_v,
+                    float* func_int, float* cos_u, float* sin_u, float* cos_v, float* sin_v) {
+    int nu, nv;
+    if (oro_dome_info(s, light, &nu, &nv)) return -1;
+    const ibl_dome* d = &s->domes[light];
+    memcpy(cdf_u, d->u.cdf, sizeof(float) * (nu + 1));
+    memcpy(func_u, d->u.func, sizeof(float) * nu);
+    for (int u = 0; u < nu; u++) {
+        memcpy(cdf_v + (size_t)u * (nv + 1), d->v[u].cdf, sizeof(float) * (nv + 1));
+        memcpy(func_v + (size_t)u * nv, d->v[u].func, sizeof(float) * nv);
+        func_int[u] = d->v[u].funcInt;
+    }
+    func_int[nu] = d->u.funcInt;
+    memcpy(cos_u, d->cosU, sizeof(float) * (nu + 1));
+    memcpy(sin_u, d->sinU, sizeof(float) * (nu + 1));
+    memcpy(cos_v, d->cosV, sizeof(float) * (nv + 1));
+    memcpy(sin_v, d->sinV, sizeof(float) * (nv + 1));
+    return 0;
+}
+int oro_texture_lookup_dir(const oro_scene* s, int tex, int n, const float* dirs, float* out) {
+    if (tex < 0 || tex >= s->n_tex) return -1;
+    for (int i = 0; i < n; i++) ibl_lookup_dir(&s->tex[tex], dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2], out + 3 * i);
+    return 0;
+}
 
 static int push_mesh(oro_scene* s, mesh_t* m) {
     if (s->n_meshes == s->cap_meshes) {
@@ -974,9 +1044,55 @@ static v3 rect_light(shade_ctx* c, const oro_light* l, int li, v3 from, v3 norma
     return vscale(tmpResult, samplesDoneRecip);
 }
 
+/* DomeLight::sampleLight, src/DomeLight.cpp:80-160 (fast shadows, primary
+ * shading: m_numSamples draws).  A draw below the shading horizon is redrawn
+ * without counting it (`continue` at :106 skips samplesDone++).  Deviation: after
+ * DOME_MAX_REJECTS such redraws in one call the loop stops (the reference would
+ * not terminate when the whole map lies below the horizon). */
+#define DOME_MAX_REJECTS 256
+static const float TWO_PI2 = 2.f * (3.1415926f * 3.1415926f);   /* _2_PI2, src/Miro.h:61 */
+static v3 dome_light(shade_ctx* c, const oro_light* l, int li, v3 from, v3 normal, v3 rVec, float* outSpec) {
+    const ibl_dome* D = &c->s->domes[li];
+    const ibl_image* tex = &c->s->tex[l->texture];
+    v3 tmpResult = V(0, 0, 0);
+    float tmpSpec = 0, samplesDoneRecip = 1.0f;
+    int samplesDone = 0, cutOff = 0, rejects = 0;
+    do {
+        float e1 = next_rand(c);
+        float e2 = next_rand(c);
+        float pdf0, pdf1;
+        float fu = ibl_dist_sample(&D->u, e1, &pdf0);
+        int u = ((int)fu == D->u.count) ? (int)fu - 1 : (int)fu;
+        float fv = ibl_dist_sample(&D->v[u], e2, &pdf1);
+        float cosTheta = D->cosV[(int)fv], sinTheta = D->sinV[(int)fv];
+        float sinPhi = D->sinU[(int)fu], cosPhi = D->cosU[(int)fu];
+        v3 direction = V(-sinTheta * cosPhi, -cosTheta, -sinTheta * sinPhi);
+        if (vdot(normal, direction) < 0.0f) {
+            if (++rejects >= DOME_MAX_REJECTS) break;
+            continue;
+        }
+        float pdf = (pdf0 * pdf1) / (TWO_PI2 * sinTheta);
+        float img[3];
+        ibl_lookup_dir(tex, direction.x, direction.y, direction.z, img);
+        float attenuate = 1.0f;
+        if (trace_shadow(c, from, direction, 1e12f)) { attenuate = 0.0f; c->shadow_mask |= 1u << (li & 31); }
+        float inv = 1.0f / pdf;   /* E = m_Gain * imageSample / pdf (Vector3::operator/) */
+        v3 E = V((img[0] * l->power) * inv, (img[1] * l->power) * inv, (img[2] * l->power) * inv);
+        samplesDone++;
+        samplesDoneRecip = 1.0f / (float)samplesDone;
+        v3 Es = vscale(E, samplesDoneRecip);
+        cutOff = (((Es.x + Es.y) + Es.z) * 0.333333f) < l->noiseThreshold;
+        tmpResult = vadd(tmpResult, vscale(E, attenuate));
+        tmpSpec += vdot(rVec, direction) * attenuate;
+    } while (samplesDone < l->samples && !cutOff);
+    *outSpec = tmpSpec * samplesDoneRecip;
+    return vscale(tmpResult, samplesDoneRecip);
+}
+
 static v3 sample_light(shade_ctx* c, int li, v3 from, v3 normal, v3 rVec, float* outSpec) {
     const oro_light* l = &c->s->lights[li];
     if (l->type == ORO_POINT_LIGHT) { float e = point_light(c, l, li, from, normal, rVec, outSpec); return V(e, e, e); }
+    if (l->type == ORO_DOME_LIGHT) return dome_light(c, l, li, from, normal, rVec, outSpec);
     return rect_light(c, l, li, from, normal, rVec, outSpec);
 }
 
@@ -1035,7 +1151,8 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
     for (int i = 0; i < c->s->n_lights; i++) {
         float lightSpec = 0;
         v3 E = sample_light(c, i, P, theNormal, rVec, &lightSpec);
-        float pw = powf(lightSpec, mat->specExp);
+        /* libm pow of the reference, evaluated in double and rounded once */
+        float pw = (float)pow((double)lightSpec, (double)mat->specExp);
         Ls = vadd(Ls, vscale(vscale(vmul(E, ks), mat->specAmt), pw));
         Ld = vadd(Ld, vmul(E, kd));
     }
@@ -1120,6 +1237,11 @@ static v3 sample_scene(shade_ctx* c, const ray_t* r, hit_t* h, uint32_t* prim_nv
         return vscale(result, 1.0f / (float)s->num_paths);
     }
     h->prim = -1;
+    if (s->env_tex >= 0) {   /* environment map lookup, src/Scene.cpp:236-239 */
+        float e[3];
+        ibl_lookup_dir(&s->tex[s->env_tex], r->d[0], r->d[1], r->d[2], e);
+        return V(e[0] * s->env_exposure, e[1] * s->env_exposure, e[2] * s->env_exposure);
+    }
     return s->bg;
 }
 

@@ -31,7 +31,7 @@ extern "C" {
 typedef struct oro_scene oro_scene;
 
 enum { ORO_LAMBERT = 0, ORO_BLINN = 1 };
-enum { ORO_POINT_LIGHT = 0, ORO_RECT_LIGHT = 1 };
+enum { ORO_POINT_LIGHT = 0, ORO_RECT_LIGHT = 1, ORO_DOME_LIGHT = 2 };
 
 typedef struct {
     int type;               /* ORO_LAMBERT / ORO_BLINN                        */
@@ -47,6 +47,7 @@ typedef struct {
     int samples;            /* rect light samples (Light::m_numSamples)        */
     float noiseThreshold;   /* Light::m_noiseThreshold (default epsilon)       */
     int castShadows;
+    int texture;            /* dome light: texture id (oro_scene_add_texture)  */
 } oro_light;
 
 typedef struct {
@@ -101,6 +102,24 @@ int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H,
                int x0, int y0, int x1, int y1,
                float* rgb, uint8_t* rgb8, oro_hit* hit, uint32_t* shadow,
                uint64_t* counters, int n_threads);
+
+/* image-based lighting (src/hdrloader.cpp, src/Texture.cpp, src/DomeLight.*) -- */
+/* HDRLoader::load: header only (sizes), then W*H*3 floats, row 0 = top.
+ * 0 on success, negative on error (oro_ibl.c lists the rejected inputs). */
+int oro_hdr_info(const char* path, int* w, int* h);
+int oro_hdr_load(const char* path, float* rgb, int w, int h);
+/* RawImage + Texture: copies W*H*3 floats (row 0 = top); returns texture id. */
+int oro_scene_add_texture(oro_scene* s, const float* rgb, int w, int h);
+/* Scene::setEnvMap + setEnvExposure (src/Scene.h:23-24); texture -1 clears. */
+int oro_scene_set_env_map(oro_scene* s, int texture, float exposure);
+/* DomeLight::setTexture tables of light `light` (src/DomeLight.cpp:8-78):
+ * cdf_u[nu+1], func_u[nu], cdf_v[nu*(nv+1)], func_v[nu*nv], func_int[nu+1]
+ * (column integrals, then the u integral), cos_u/sin_u[nu+1], cos_v/sin_v[nv+1]. */
+int oro_dome_info(const oro_scene* s, int light, int* nu, int* nv);
+int oro_dome_export(const oro_scene* s, int light, float* cdf_u, float* func_u, float* cdf_v, float* func_v,
+                    float* func_int, float* cos_u, float* sin_u, float* cos_v, float* sin_v);
+/* Texture::getLookupXYZ3 of texture `tex` for n directions (3n floats in/out). */
+int oro_texture_lookup_dir(const oro_scene* s, int tex, int n, const float* dirs, float* out);
 
 /* numerics probes (for tests) */
 float oro_x86_rcp(float x);

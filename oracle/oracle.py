@@ -39,7 +39,7 @@ class Material(C.Structure):
 class Light(C.Structure):
     _fields_ = [("type", C.c_int), ("pos", C.c_float * 3), ("v1", C.c_float * 3), ("v2", C.c_float * 3),
                 ("v3", C.c_float * 3), ("power", C.c_float), ("samples", C.c_int),
-                ("noiseThreshold", C.c_float), ("castShadows", C.c_int)]
+                ("noiseThreshold", C.c_float), ("castShadows", C.c_int), ("texture", C.c_int)]
 
 
 class Camera(C.Structure):
@@ -82,6 +82,35 @@ def _declare(L):
     L.oro_gamma_table.argtypes = [_u8p]
     L.oro_rand.argtypes = [C.c_uint32] * 4
     L.oro_rand.restype = C.c_float
+    L.oro_hdr_info.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.oro_hdr_load.argtypes = [C.c_char_p, _fp, C.c_int, C.c_int]
+    L.oro_scene_add_texture.argtypes = [C.c_void_p, _fp, C.c_int, C.c_int]
+    L.oro_scene_set_env_map.argtypes = [C.c_void_p, C.c_int, C.c_float]
+    L.oro_dome_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.oro_dome_export.argtypes = [C.c_void_p, C.c_int] + [_fp] * 9
+    L.oro_texture_lookup_dir.argtypes = [C.c_void_p, C.c_int, C.c_int, _fp, _fp]
+
+
+DOME_KEYS = ("cdf_u", "func_u", "cdf_v", "func_v", "func_int", "cos_u", "sin_u", "cos_v", "sin_v")
+
+
+def dome_shapes(nu, nv):
+    return {"cdf_u": (nu + 1,), "func_u": (nu,), "cdf_v": (nu, nv + 1), "func_v": (nu, nv), "func_int": (nu + 1,),
+            "cos_u": (nu + 1,), "sin_u": (nu + 1,), "cos_v": (nv + 1,), "sin_v": (nv + 1,)}
+
+
+def hdr_load(path):
+    """HDRLoader::load restated: (H, W, 3) float32, row 0 = top.  Raises on error."""
+    L = lib()
+    w, h = C.c_int(), C.c_int()
+    r = L.oro_hdr_info(str(path).encode(), C.byref(w), C.byref(h))
+    if r != 0:
+        raise RuntimeError(f"oracle HDR header rejected ({r}): {path}")
+    rgb = np.zeros((h.value, w.value, 3), np.float32)
+    r = L.oro_hdr_load(str(path).encode(), _p(rgb, _fp), w.value, h.value)
+    if r != 0:
+        raise RuntimeError(f"oracle HDR load rejected ({r}): {path}")
+    return rgb
 
 
 def _p(a, t):
@@ -151,6 +180,7 @@ class OracleScene:
         l.samples = 1
         l.noiseThreshold = 0.001
         l.castShadows = int(cast_shadows)
+        l.texture = -1
         self.n_lights += 1
         return self.L.oro_scene_add_light(self.h, C.byref(l))
 
@@ -162,8 +192,50 @@ class OracleScene:
         l.samples = samples
         l.noiseThreshold = noise
         l.castShadows = int(cast_shadows)
+        l.texture = -1
         self.n_lights += 1
         return self.L.oro_scene_add_light(self.h, C.byref(l))
+
+    def add_texture(self, rgb):
+        a = np.ascontiguousarray(rgb, np.float32)
+        r = self.L.oro_scene_add_texture(self.h, _p(a, _fp), a.shape[1], a.shape[0])
+        if r < 0:
+            raise RuntimeError("oracle add_texture failed")
+        return r
+
+    def add_dome_light(self, texture, power, samples=1, noise=0.001):
+        """DomeLight: setTexture(texture) + setPower (m_Gain) + setSamples."""
+        l = Light()
+        l.type = 2
+        l.power = power
+        l.samples = samples
+        l.noiseThreshold = noise
+        l.castShadows = 1
+        l.texture = int(texture)
+        r = self.L.oro_scene_add_light(self.h, C.byref(l))
+        if r < 0:
+            raise RuntimeError(f"oracle dome light rejected ({r})")
+        self.n_lights += 1
+        return r
+
+    def set_env_map(self, texture, exposure=1.0):
+        if self.L.oro_scene_set_env_map(self.h, int(texture), float(exposure)) != 0:
+            raise RuntimeError("oracle set_env_map failed")
+
+    def dome_export(self, light):
+        nu, nv = C.c_int(), C.c_int()
+        if self.L.oro_dome_info(self.h, light, C.byref(nu), C.byref(nv)) != 0:
+            raise RuntimeError("not a dome light")
+        out = {k: np.zeros(s, np.float32) for k, s in dome_shapes(nu.value, nv.value).items()}
+        self.L.oro_dome_export(self.h, light, *[_p(out[k], _fp) for k in DOME_KEYS])
+        return out
+
+    def texture_lookup_dir(self, texture, dirs):
+        d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        out = np.zeros_like(d)
+        if self.L.oro_texture_lookup_dir(self.h, int(texture), len(d), _p(d, _fp), _p(out, _fp)) != 0:
+            raise RuntimeError("bad texture")
+        return out
 
     def set_bg(self, rgb):
         self.L.oro_scene_set_bg(self.h, *[float(x) for x in rgb])

@@ -21,6 +21,7 @@
 
 #include "mrt_kernels.h"
 #include "mrt_scene.h"
+#include "mrt_texture.h"
 
 namespace mrt {
 
@@ -57,6 +58,10 @@ struct RenderParams {
     const float4* normals;
     const DevMaterial* mats;
     const DevLight* lights;
+    const DevDome* domes;    // dome-light tables (DevLight::dome)
+    const float* env;        // environment map (nullable), env_w x env_h RGB, row 0 = top
+    int32_t env_w, env_h;
+    float env_exposure;
     const uint16_t* tables;  // rcp[2048] | rsqrt[2048]
     const uint8_t* gamma;
     int32_t* gstack;
@@ -177,6 +182,52 @@ struct Shader {
         return scale(acc, recip);
     }
 
+    // DomeLight::sampleLight, src/DomeLight.cpp:80-160 (fast shadows; primary
+    // shading, so m_numSamples draws).  A draw below the shading horizon is
+    // redrawn without counting it (`continue` at :106 skips samplesDone++); after
+    // kDomeMaxRejects such redraws in one call the loop stops (the reference would
+    // not terminate when the whole map lies below the horizon).
+    static constexpr int kDomeMaxRejects = 256;
+    template <bool COUNT>
+    __device__ v3 dome_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec) {
+        const DevDome& D = P.domes[l.dome];
+        v3 acc = mk(0, 0, 0);
+        float tmpSpec = 0.f, recip = 1.0f;
+        int done = 0, rejects = 0;
+        bool cut = false;
+        do {
+            const float e1 = next_rand();
+            const float e2 = next_rand();
+            float pdf0, pdf1;
+            const float fu = dist_sample(D.cdf_u, D.func_u, D.nu, D.inv_int_u, e1, pdf0);
+            const int iu = (int)fu;
+            const int u = iu == D.nu ? iu - 1 : iu;
+            const float fv = dist_sample(D.cdf_v + (size_t)u * (D.nv + 1), D.func_v + (size_t)u * D.nv, D.nv,
+                                         D.inv_int_v[u], e2, pdf1);
+            const int iv = (int)fv;
+            const float cosT = D.cos_v[iv], sinT = D.sin_v[iv], sinP = D.sin_u[iu], cosP = D.cos_u[iu];
+            const v3 dir = mk(-sinT * cosP, -cosT, -sinT * sinP);
+            if (dot(normal, dir) < 0.0f) {
+                if (++rejects >= kDomeMaxRejects) break;
+                continue;
+            }
+            const float pdf = (pdf0 * pdf1) / (kTwoPI2 * sinT);
+            const v3 img = tex_lookup_dir(D.tex, D.nu, D.nv, dir.x, dir.y, dir.z);
+            const float inv = 1.0f / pdf;  // E = m_Gain * imageSample / pdf (Vector3::operator/)
+            const v3 E = scale(scale(img, l.power), inv);
+            float att = 1.0f;
+            if (occluded<COUNT>(from, dir, 1e12f)) att = 0.0f;
+            done++;
+            recip = 1.0f / (float)done;
+            const v3 Es = scale(E, recip);
+            cut = (((Es.x + Es.y) + Es.z) * 0.333333f) < l.noise;
+            acc = add(acc, scale(E, att));
+            tmpSpec += dot(rVec, dir) * att;
+        } while (done < l.samples && !cut);
+        outSpec = tmpSpec * recip;
+        return scale(acc, recip);
+    }
+
     template <bool COUNT>
     __device__ v3 sample_light(int li, v3 from, v3 normal, v3 rVec, float& spec) {
         const DevLight& l = P.lights[li];
@@ -184,7 +235,10 @@ struct Shader {
             float e = point_light<COUNT>(l, from, normal, rVec, spec);
             return mk(e, e, e);
         }
-        if constexpr (!POINT_ONLY) return rect_light<COUNT>(l, from, normal, rVec, spec);
+        if constexpr (!POINT_ONLY) {
+            if (l.type == MRT_DOME_LIGHT) return dome_light<COUNT>(l, from, normal, rVec, spec);
+            return rect_light<COUNT>(l, from, normal, rVec, spec);
+        }
         return mk(0, 0, 0);
     }
 
@@ -508,6 +562,10 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             Shader<POINT_ONLY, FAST> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u, seed};
             col = S.template shade<COUNT>(r, h);
             shadow_total += S.shadow_rays;
+        } else if (P.env) {  // environment map lookup of the missed ray (src/Scene.cpp:236-239)
+            const int f = item_frame(P, item);
+            const v3 d = camera_dir(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
+            col = scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
         } else {
             col = mk(P.bg[0], P.bg[1], P.bg[2]);
         }
@@ -719,6 +777,9 @@ struct DeviceState {
     float4* normals = nullptr;
     DevMaterial* mats = nullptr;
     DevLight* lights = nullptr;
+    DevDome* domes = nullptr;
+    std::vector<void*> bufs;     // textures and dome tables (freed with the state)
+    const float* env = nullptr;  // environment texture (one of bufs)
     uint16_t* tables = nullptr;
     uint8_t* gamma = nullptr;
     uint32_t gthreads = 0;
@@ -768,9 +829,11 @@ static void free_device(DeviceState* d) {
     if (d->device >= 0) (void)hipSetDevice(d->device);
     (void)hipDeviceSynchronize();   // no launch may still use the scratch below
     for (StreamCtx* c : d->ctxs) free_ctx(c);
-    void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->tables,
+    void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->tables,
                     d->gamma, d->d_rgb, d->d_rgb8};
     for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (void* p : d->bufs)
         if (p) (void)hipFree(p);
     delete d;
 }
@@ -868,6 +931,34 @@ static int ensure_device(Scene& s, int device) {
     if ((rc = upload(d.lights, s.lights.data(), s.lights.size() * sizeof(DevLight), total))) return rc;
     if ((rc = upload(d.tables, tab.data(), tab.size() * sizeof(uint16_t), total))) return rc;
     if ((rc = upload(d.gamma, host_gamma_lut(), 32769, total))) return rc;
+    // textures, then each dome light's tables (DomeLight::setTexture products)
+    auto upload_floats = [&](const std::vector<float>& v, const float*& dst) -> int {
+        float* p = nullptr;
+        const int r = upload(p, v.data(), v.size() * sizeof(float), total);
+        d.bufs.push_back(p);
+        dst = p;
+        return r;
+    };
+    std::vector<const float*> dtex(s.textures.size(), nullptr);
+    for (size_t i = 0; i < s.textures.size(); i++)
+        if ((rc = upload_floats(s.textures[i].rgb, dtex[i]))) return rc;
+    std::vector<DevDome> DD(s.domes.size());
+    for (size_t i = 0; i < s.domes.size(); i++) {
+        const DomeTables& t = s.domes[i];
+        DevDome& g = DD[i];
+        if ((rc = upload_floats(t.cdf_u, g.cdf_u)) || (rc = upload_floats(t.func_u, g.func_u)) ||
+            (rc = upload_floats(t.cdf_v, g.cdf_v)) || (rc = upload_floats(t.func_v, g.func_v)) ||
+            (rc = upload_floats(t.inv_int_v, g.inv_int_v)) || (rc = upload_floats(t.cos_u, g.cos_u)) ||
+            (rc = upload_floats(t.sin_u, g.sin_u)) || (rc = upload_floats(t.cos_v, g.cos_v)) ||
+            (rc = upload_floats(t.sin_v, g.sin_v)))
+            return rc;
+        g.tex = dtex[t.tex];
+        g.inv_int_u = t.inv_int_u;
+        g.nu = t.nu;
+        g.nv = t.nv;
+    }
+    if ((rc = upload(d.domes, DD.data(), DD.size() * sizeof(DevDome), total))) return rc;
+    d.env = s.env_tex >= 0 ? dtex[s.env_tex] : nullptr;
     d.bytes = total;
     // persistent grid: resident workgroups on every CU
     hipDeviceProp_t prop;
@@ -913,6 +1004,11 @@ static void fill_params(const Scene& s, RenderParams& P) {
     const DeviceState& d = *s.dev;
     P.nodes = d.nodes; P.leaves = d.leaves; P.prims = d.prims; P.verts = d.verts; P.normals = d.normals;
     P.mats = d.mats; P.lights = d.lights; P.tables = d.tables; P.gamma = d.gamma;
+    P.domes = d.domes;
+    P.env = d.env;
+    P.env_w = d.env ? s.textures[s.env_tex].W : 0;
+    P.env_h = d.env ? s.textures[s.env_tex].H : 0;
+    P.env_exposure = s.env_exposure;
     P.gstride = d.gthreads;
     P.bg[0] = s.bg[0]; P.bg[1] = s.bg[1]; P.bg[2] = s.bg[2];
     P.n_lights = (int32_t)s.lights.size();
@@ -1026,7 +1122,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     if ((rc = launch(pick_primary(g_primary_waves, count, fb)))) return rc;
     HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
-    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1;
+    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env;
     if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb)))) return rc;
     c.last_was_render = true;
     HIP_OK(hipGetLastError());
@@ -1071,10 +1167,28 @@ int mrt_scene_add_material(mrt_scene* s, const mrt_material* m) {
 }
 
 int mrt_scene_add_light(mrt_scene* s, const mrt_light* l) {
-    if (!s || !l || (l->type != MRT_POINT_LIGHT && l->type != MRT_RECT_LIGHT)) { set_error("bad light"); return MRT_ERR_INVALID; }
+    if (!s || !l || (l->type != MRT_POINT_LIGHT && l->type != MRT_RECT_LIGHT && l->type != MRT_DOME_LIGHT)) {
+        set_error("bad light");
+        return MRT_ERR_INVALID;
+    }
     if (s->impl.lights.size() >= (size_t)kMaxLights) { set_error("too many lights"); return MRT_ERR_INVALID; }
     DevLight d;
     memset(&d, 0, sizeof d);
+    d.dome = -1;
+    if (l->type == MRT_DOME_LIGHT) {
+        // DomeLight::setTexture (src/DomeLight.cpp:8-78): tables built now, on the host
+        if (l->texture < 0 || l->texture >= (int32_t)s->impl.textures.size()) {
+            set_error("dome light needs a texture id from mrt_scene_add_texture");
+            return MRT_ERR_INVALID;
+        }
+        DomeTables t;
+        std::string err;
+        const int rc = build_dome(s->impl.textures[l->texture], t, err);
+        if (rc) { set_error(err); return rc; }
+        t.tex = l->texture;
+        d.dome = (int32_t)s->impl.domes.size();
+        s->impl.domes.push_back(std::move(t));
+    }
     d.type = l->type;
     memcpy(d.pos, l->pos, 12); memcpy(d.v1, l->v1, 12); memcpy(d.v2, l->v2, 12); memcpy(d.v3, l->v3, 12);
     d.samples = l->samples < 1 ? 1 : l->samples;
@@ -1095,6 +1209,80 @@ int mrt_scene_add_light(mrt_scene* s, const mrt_light* l) {
     s->impl.lights.push_back(d);
     s->impl.dev_dirty = true;
     return (int)s->impl.lights.size() - 1;
+}
+
+int mrt_hdr_info(const char* path, int32_t* width, int32_t* height) {
+    if (!path || !width || !height) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    int W = 0, H = 0;
+    std::string err;
+    const int rc = load_hdr(path, W, H, nullptr, err);
+    if (rc) { set_error(err); return rc; }
+    *width = W;
+    *height = H;
+    return MRT_OK;
+}
+
+int mrt_hdr_load(const char* path, float* rgb, int32_t width, int32_t height) {
+    if (!path || !rgb) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    int W = 0, H = 0;
+    std::string err;
+    std::vector<float> buf;
+    const int rc = load_hdr(path, W, H, &buf, err);
+    if (rc) { set_error(err); return rc; }
+    if (W != width || H != height) { set_error("HDR size differs from width x height (see mrt_hdr_info)"); return MRT_ERR_INVALID; }
+    memcpy(rgb, buf.data(), buf.size() * sizeof(float));
+    return MRT_OK;
+}
+
+int mrt_scene_add_texture(mrt_scene* s, const float* rgb, int32_t width, int32_t height) {
+    if (!s || !rgb || width <= 0 || height <= 0 || (int64_t)width * height > (int64_t(1) << 28)) {
+        set_error("bad texture");
+        return MRT_ERR_INVALID;
+    }
+    if (s->impl.textures.size() >= (size_t)kMaxTextures) { set_error("too many textures"); return MRT_ERR_INVALID; }
+    Texture t;
+    t.W = width;
+    t.H = height;
+    t.rgb.assign(rgb, rgb + (size_t)width * height * 3);
+    s->impl.textures.push_back(std::move(t));
+    s->impl.dev_dirty = true;
+    return (int)s->impl.textures.size() - 1;
+}
+
+int mrt_scene_set_env_map(mrt_scene* s, int32_t texture, float exposure) {
+    if (!s || texture < -1 || texture >= (int32_t)s->impl.textures.size()) { set_error("bad texture id"); return MRT_ERR_INVALID; }
+    s->impl.env_tex = texture;
+    s->impl.env_exposure = exposure;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
+static const DomeTables* dome_of(const mrt_scene* s, int32_t light) {
+    if (!s || light < 0 || light >= (int32_t)s->impl.lights.size() || s->impl.lights[light].dome < 0) return nullptr;
+    return &s->impl.domes[s->impl.lights[light].dome];
+}
+
+int mrt_scene_dome_info(const mrt_scene* s, int32_t light, int32_t* nu, int32_t* nv) {
+    const DomeTables* t = dome_of(s, light);
+    if (!t || !nu || !nv) { set_error("not a dome light"); return MRT_ERR_INVALID; }
+    *nu = t->nu;
+    *nv = t->nv;
+    return MRT_OK;
+}
+
+int mrt_scene_dome_export(const mrt_scene* s, int32_t light, float* cdf_u, float* func_u, float* cdf_v,
+                          float* func_v, float* func_int, float* cos_u, float* sin_u, float* cos_v, float* sin_v) {
+    const DomeTables* t = dome_of(s, light);
+    if (!t || !cdf_u || !func_u || !cdf_v || !func_v || !func_int || !cos_u || !sin_u || !cos_v || !sin_v) {
+        set_error("not a dome light / bad argument");
+        return MRT_ERR_INVALID;
+    }
+    auto put = [](const std::vector<float>& v, float* dst) { memcpy(dst, v.data(), v.size() * sizeof(float)); };
+    put(t->cdf_u, cdf_u); put(t->func_u, func_u); put(t->cdf_v, cdf_v); put(t->func_v, func_v);
+    put(t->int_v, func_int);
+    func_int[t->nu] = t->int_u;
+    put(t->cos_u, cos_u); put(t->sin_u, sin_u); put(t->cos_v, cos_v); put(t->sin_v, sin_v);
+    return MRT_OK;
 }
 
 int mrt_scene_add_obj(mrt_scene* s, const char* path, const float* ctm16, int material) {

@@ -23,12 +23,27 @@ struct Mesh {
     int32_t nt() const { return (int32_t)(vidx.size() / 3); }
 };
 
+struct Texture {                // RawImage (src/RawImage.h): W*H*3 floats, row 0 = top
+    std::vector<float> rgb;
+    int32_t W = 0, H = 0;
+};
+
+struct DomeTables {             // DomeLight::setTexture (src/DomeLight.cpp:8-78)
+    int32_t tex = -1, nu = 0, nv = 0;
+    std::vector<float> func_u, cdf_u, func_v, cdf_v, int_v, inv_int_v, cos_u, sin_u, cos_v, sin_v;
+    float int_u = 0.f, inv_int_u = 0.f;
+};
+
 struct DeviceState;  // defined in mrt_device.hip
 
 struct Scene {
     std::vector<Mesh> meshes;
     std::vector<DevMaterial> materials;
     std::vector<DevLight> lights;
+    std::vector<Texture> textures;
+    std::vector<DomeTables> domes;
+    int32_t env_tex = -1;           // Scene::m_envMap (-1: background colour)
+    float env_exposure = 1.f;       // Scene::m_envExposure
     float bg[3] = {0.f, 0.f, 0.f};
     int num_paths = 1;
 
@@ -48,6 +63,9 @@ struct Scene {
 // host_build.cpp
 int load_obj(const char* path, const float* ctm16, Mesh& out, std::string& err);
 int build_qbvh(Scene& s, std::string& err);
+// host_texture.cpp
+int load_hdr(const char* path, int& W, int& H, std::vector<float>* rgb, std::string& err);
+int build_dome(const Texture& t, DomeTables& d, std::string& err);
 
 void set_error(const std::string& msg);
 

@@ -51,10 +51,30 @@ struct DevMaterial {
 struct DevLight {
     int32_t type;
     float pos[3], v1[3], v2[3], v3[3];
-    float power;        // point: m_power; rect: power * rsqrt_nr(area^2) (setPower)
+    float power;        // point: m_power; rect: power * rsqrt_nr(area^2) (setPower); dome: m_Gain
     int32_t samples;
     float noise;
     int32_t cast_shadows;
+    int32_t dome;       // dome light: index of its DevDome tables (-1 otherwise)
+};
+
+// DomeLight::setTexture products in HBM (src/DomeLight.cpp:8-78): the lat-long
+// texture (nu x nv texels, row 0 = top), a Distribution1D over u of the column
+// integrals, one over v per column (nu x (nv+1) CDF, row-major by column), and
+// the sin / cos tables of the sampled angles.
+struct DevDome {
+    const float* tex;
+    const float* cdf_u;      // nu + 1
+    const float* func_u;     // nu
+    const float* cdf_v;      // nu * (nv + 1)
+    const float* func_v;     // nu * nv
+    const float* inv_int_v;  // nu
+    const float* cos_u;      // nu + 1
+    const float* sin_u;
+    const float* cos_v;      // nv + 1
+    const float* sin_v;
+    float inv_int_u;
+    int32_t nu, nv;
 };
 
 // Camera basis hoisted to the host (bit-identical to the per-ray recompute of
@@ -68,5 +88,6 @@ struct CamParams {
 static constexpr int kMaxLights = 8;
 static constexpr int kMaxBatch = 16;   // cameras (frames) per batched bucket launch (kernel argument)
 static constexpr int kMaxMaterials = 64;
+static constexpr int kMaxTextures = 16;
 
 }  // namespace mrt

@@ -27,6 +27,7 @@ from . import _lib
 from ._lib import MRTError, check, f3
 
 __all__ = ["Vector3", "Matrix4x4", "TriangleMesh", "Lambert", "Blinn", "PointLight", "RectangleLight",
+           "DomeLight", "RawImage", "Texture",
            "Camera", "Image", "Scene", "Ray", "HitInfo", "makeMeshObjs", "MRTError", "lib", "device_count",
            "rcp_nr", "rsqrt_nr"]
 
@@ -172,9 +173,9 @@ class PointLight(_Light):
 
     def setPosition(self, v): self.position = Vector3(v)
 
-    def _c(self):
+    def _c(self, texture=-1):
         return _lib.mrt_light(0, f3(self.position), f3((0, 0, 0)), f3((0, 0, 0)), f3((0, 0, 0)), self.power,
-                              self.samples, self.noiseThreshold, int(self.castShadows))
+                              self.samples, self.noiseThreshold, int(self.castShadows), -1)
 
 
 class RectangleLight(_Light):
@@ -185,9 +186,63 @@ class RectangleLight(_Light):
     def setVertices(self, v1, v2, v3):
         self.v1, self.v2, self.v3 = Vector3(v1), Vector3(v2), Vector3(v3)
 
-    def _c(self):
+    def _c(self, texture=-1):
         return _lib.mrt_light(1, f3((0, 0, 0)), f3(self.v1), f3(self.v2), f3(self.v3), self.power,
-                              self.samples, self.noiseThreshold, int(self.castShadows))
+                              self.samples, self.noiseThreshold, int(self.castShadows), -1)
+
+
+class RawImage:
+    """RawImage (src/RawImage.h:9-30): float RGB texels, row 0 = the top row,
+    as HDRLoader::load leaves them (m_rawData).  RawImage(w, h, data) wraps an
+    array; loadImage / loadHDR decode a Radiance .hdr file in libmrt."""
+
+    def __init__(self, w=0, h=0, data=None):
+        self.m_width, self.m_height = int(w), int(h)
+        self.m_rawData = None if data is None else np.ascontiguousarray(data, np.float32).reshape(self.m_height,
+                                                                                                   self.m_width, 3)
+
+    def loadImage(self, filename):  # src/RawImage.cpp:16-26
+        ext = str(filename).rsplit(".", 1)[-1]
+        if ext in ("hdr", "HDR"):
+            return self.loadHDR(filename)
+        raise MRTError(f".{ext} images are not on the MI355X path (Radiance .hdr only)")
+
+    def loadHDR(self, filename):  # src/RawImage.cpp:29-32 -> HDRLoader::load
+        L = lib()
+        w, h = C.c_int32(), C.c_int32()
+        check(L.mrt_hdr_info(str(filename).encode(), C.byref(w), C.byref(h)), f"HDR {filename}")
+        data = np.zeros((h.value, w.value, 3), np.float32)
+        check(L.mrt_hdr_load(str(filename).encode(), data.ctypes.data_as(C.POINTER(C.c_float)), w.value, h.value),
+              f"HDR {filename}")
+        self.m_width, self.m_height, self.m_rawData = w.value, h.value, data
+        return True
+
+
+class Texture:
+    """Texture(RawImage) (src/Texture.h:9-28): a lat-long map for DomeLight and
+    Scene.setEnvMap."""
+
+    def __init__(self, image: RawImage):
+        self.m_image = image
+
+    def getWidth(self): return self.m_image.m_width
+    def getHeight(self): return self.m_image.m_height
+
+
+class DomeLight(_Light):
+    """DomeLight (src/DomeLight.h:44-62): setTexture, setPower (= m_Gain, default
+    1), setSamples, setNoiseThreshold.  Importance-sampled from the texture."""
+
+    def __init__(self):
+        super().__init__()
+        self.power = 1.0
+        self.texture = None
+
+    def setTexture(self, t): self.texture = t
+
+    def _c(self, texture=-1):
+        return _lib.mrt_light(2, f3((0, 0, 0)), f3((0, 0, 0)), f3((0, 0, 0)), f3((0, 0, 0)), self.power,
+                              self.samples, self.noiseThreshold, int(self.castShadows), int(texture))
 
 
 class Camera:
@@ -255,6 +310,8 @@ class Scene:
         self._lights: List[_Light] = []
         self.bg = Vector3(0)
         self.m_numPaths = 1
+        self.m_envMap = None
+        self.m_envExposure = 1.0
         self.device = int(device)
         self._h = None
         self.bvh_info = None
@@ -264,6 +321,8 @@ class Scene:
     def addLight(self, light): self._lights.append(light)
     def setBGColor(self, c): self.bg = Vector3(c)
     def setNumPaths(self, p): self.m_numPaths = int(p)
+    def setEnvMap(self, t): self.m_envMap = t                    # src/Scene.h:23
+    def setEnvExposure(self, e): self.m_envExposure = float(e)   # src/Scene.h:24
 
     def __del__(self):
         try:
@@ -300,9 +359,25 @@ class Scene:
                                    vi.ctypes.data_as(C.POINTER(C.c_uint32)), ni.ctypes.data_as(C.POINTER(C.c_uint32)),
                                    len(v), len(n), len(vi))
                 check(L.mrt_scene_add_mesh(self._h, C.byref(mm), mid), "add_mesh")
+        tex_ids = {}
+
+        def tex_id(t):
+            if t is None:
+                return -1
+            if id(t) not in tex_ids:
+                img = t.m_image
+                if img.m_rawData is None:
+                    raise MRTError("texture image has no data (loadImage first)")
+                a = np.ascontiguousarray(img.m_rawData, np.float32)
+                tex_ids[id(t)] = check(L.mrt_scene_add_texture(self._h, a.ctypes.data_as(C.POINTER(C.c_float)),
+                                                               img.m_width, img.m_height), "add_texture")
+            return tex_ids[id(t)]
+
         for light in self._lights:
-            lc = light._c()
+            lc = light._c(tex_id(getattr(light, "texture", None)))
             check(L.mrt_scene_add_light(self._h, C.byref(lc)), "add_light")
+        if self.m_envMap is not None:
+            check(L.mrt_scene_set_env_map(self._h, tex_id(self.m_envMap), self.m_envExposure), "env map")
         check(L.mrt_scene_set_background(self._h, f3(self.bg)), "bg")
         check(L.mrt_scene_set_num_paths(self._h, self.m_numPaths), "num_paths")
         check(L.mrt_scene_build_bvh(self._h), "BVH build")
@@ -323,6 +398,20 @@ class Scene:
                                       n.ctypes.data_as(C.POINTER(C.c_float)), vi.ctypes.data_as(C.POINTER(C.c_uint32)),
                                       ni.ctypes.data_as(C.POINTER(C.c_uint32))), "mesh_export")
         return v, n, vi, ni
+
+    def dome_tables(self, light: int):
+        """DomeLight::setTexture tables of light `light` (host arrays of libmrt)."""
+        L = lib()
+        nu, nv = C.c_int32(), C.c_int32()
+        check(L.mrt_scene_dome_info(self.handle, int(light), C.byref(nu), C.byref(nv)), "dome_info")
+        nu, nv = nu.value, nv.value
+        shapes = {"cdf_u": (nu + 1,), "func_u": (nu,), "cdf_v": (nu, nv + 1), "func_v": (nu, nv),
+                  "func_int": (nu + 1,), "cos_u": (nu + 1,), "sin_u": (nu + 1,), "cos_v": (nv + 1,),
+                  "sin_v": (nv + 1,)}
+        out = {k: np.zeros(s, np.float32) for k, s in shapes.items()}
+        check(L.mrt_scene_dome_export(self.handle, int(light),
+                                      *[out[k].ctypes.data_as(C.POINTER(C.c_float)) for k in shapes]), "dome_export")
+        return out
 
     def bvh_export(self):
         info = self.bvh_info

@@ -21,7 +21,8 @@ EXPORTS = [
     "mrt_scene_upload", "mrt_render", "mrt_render_buckets_async", "mrt_unpack_buckets_async",
     "mrt_render_frame_async", "mrt_trace", "mrt_trace_async", "mrt_scene_last_stats", "mrt_rcp_nr",
     "mrt_rsqrt_nr", "mrt_set_tuning", "mrt_render_batch_async", "mrt_unpack_batch_async",
-    "mrt_debug_wave_log", "mrt_device_wall_clock_khz",
+    "mrt_debug_wave_log", "mrt_device_wall_clock_khz", "mrt_hdr_info", "mrt_hdr_load", "mrt_scene_add_texture",
+    "mrt_scene_set_env_map", "mrt_scene_dome_info", "mrt_scene_dome_export",
 ]
 
 
@@ -33,7 +34,7 @@ class mrt_material(C.Structure):
 class mrt_light(C.Structure):
     _fields_ = [("type", C.c_int32), ("pos", C.c_float * 3), ("v1", C.c_float * 3), ("v2", C.c_float * 3),
                 ("v3", C.c_float * 3), ("power", C.c_float), ("samples", C.c_int32),
-                ("noise_threshold", C.c_float), ("cast_shadows", C.c_int32)]
+                ("noise_threshold", C.c_float), ("cast_shadows", C.c_int32), ("texture", C.c_int32)]
 
 
 class mrt_camera(C.Structure):
@@ -132,6 +133,12 @@ def load():
     L.mrt_set_tuning.argtypes = [C.c_char_p, C.c_int]
     L.mrt_debug_wave_log.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int32]
     L.mrt_device_wall_clock_khz.argtypes = [C.c_void_p]
+    L.mrt_hdr_info.argtypes = [C.c_char_p, _ip, _ip]
+    L.mrt_hdr_load.argtypes = [C.c_char_p, _fp, C.c_int32, C.c_int32]
+    L.mrt_scene_add_texture.argtypes = [C.c_void_p, _fp, C.c_int32, C.c_int32]
+    L.mrt_scene_set_env_map.argtypes = [C.c_void_p, C.c_int32, C.c_float]
+    L.mrt_scene_dome_info.argtypes = [C.c_void_p, C.c_int32, _ip, _ip]
+    L.mrt_scene_dome_export.argtypes = [C.c_void_p, C.c_int32] + [_fp] * 9
     L.mrt_rcp_nr.argtypes = [C.c_float]
     L.mrt_rcp_nr.restype = C.c_float
     L.mrt_rsqrt_nr.argtypes = [C.c_float]

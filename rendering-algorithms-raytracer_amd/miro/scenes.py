@@ -234,6 +234,32 @@ def bunny_obj():
     return _cached("bunny_standin", bunny_standin)
 
 
+def sky_rgb(W=512, H=256):
+    """Deterministic lat-long sky for the dome-light / environment-map configs
+    (the reference's Images/*.hdr do not travel to the GPU box).  Same mapping
+    as Texture::getLookupXYZ3 (src/Texture.cpp:80-98): row 0 = +y (zenith),
+    column u = (atan2(z, x) + pi) / 2pi.  A blue sky brightening towards the
+    horizon, a warm sun disc with a glow, and a darker ground; float32 (H, W, 3)."""
+    v = (np.arange(H, dtype=np.float64) + 0.5) / H
+    u = (np.arange(W, dtype=np.float64) + 0.5) / W
+    phi = v * np.pi                                   # polar angle from +y
+    theta = u * 2.0 * np.pi - np.pi                   # atan2(z, x)
+    y = np.broadcast_to(np.cos(phi)[:, None], (H, W))
+    s = np.sin(phi)[:, None]
+    x = s * np.cos(theta)[None, :]
+    z = s * np.sin(theta)[None, :]
+    up = np.clip(y, 0.0, 1.0)[..., None]
+    sky = np.array([0.35, 0.55, 1.0]) * (0.35 + 0.65 * (1.0 - up)) + np.array([0.25, 0.3, 0.45]) * up
+    ground = np.broadcast_to(np.array([0.16, 0.14, 0.11]), (H, W, 3))
+    rgb = np.where((y >= 0.0)[..., None], sky, ground)
+    sun = np.array([0.45, 0.75, 0.48])
+    sun /= np.linalg.norm(sun)
+    c = x * sun[0] + y * sun[1] + z * sun[2]
+    glow = 40.0 * (c > np.cos(np.radians(2.5))) + 3.0 * np.clip(c, 0.0, 1.0) ** 64
+    rgb = rgb + glow[..., None] * np.array([1.0, 0.9, 0.72])
+    return np.ascontiguousarray(rgb, np.float32)
+
+
 # ---------------------------------------------------------------- presets
 CONFIGS = {
     # C1: cornell_box.obj 256x256, 1 spp, Lambert + 1 PointLight (plumbing)
@@ -261,6 +287,15 @@ CONFIGS = {
                             power=1.5, samples=1, noise=0.001)],
                material=dict(kind="blinn", kd=(1, 1, 1), specExp=8.0, specAmt=0.25), bg=(0.0, 0.0, 0.2),
                mesh="sponza", num_paths=16),
+    # D1: image-based lighting on the C2 bunny stand-in + floor: DomeLight (power
+    # 0.15, 6 samples, as src/main.cpp:157-165) over the synthetic sky, the same map
+    # as environment on missed primary rays; Blinn with a specular lobe
+    "D1": dict(name="bunny stand-in + floor 1024x1024 Blinn+DomeLight (6 samples) + env map", W=1024, H=1024,
+               camera=dict(eye=(0.0, 5.0, 15.0), lookAt=(0.0, 0.0, 0.0), up=(0, 1, 0), fov=45.0),
+               lights=[dict(type="dome", sky=(512, 256), power=0.15, samples=6, noise=0.001)],
+               env=dict(sky=(512, 256), exposure=1.0),
+               material=dict(kind="blinn", kd=(0.8, 0.8, 0.8), specExp=20.0, specAmt=0.3), bg=(0.0, 0.0, 0.2),
+               mesh="bunny"),
 }
 
 
@@ -305,10 +340,22 @@ def build_config(key, device=0):
         fl.setV1((-100, 0, -100)); fl.setV2((0, 0, 100)); fl.setV3((100, 0, -100))
         fl.setN1((0, 1, 0)); fl.setN2((0, 1, 0)); fl.setN3((0, 1, 0))
         miro.makeMeshObjs(scene, fl, material)
+    skies = {}
+
+    def sky_texture(size):
+        if size not in skies:
+            skies[size] = miro.Texture(miro.RawImage(size[0], size[1], sky_rgb(*size)))
+        return skies[size]
+
     for l in cfg["lights"]:
         if l["type"] == "point":
             pl = miro.PointLight()
             pl.setPosition(l["pos"])
+        elif l["type"] == "dome":
+            pl = miro.DomeLight()
+            pl.setTexture(sky_texture(tuple(l["sky"])))
+            pl.setSamples(l.get("samples", 1))
+            pl.setNoiseThreshold(l.get("noise", 0.001))
         else:
             pl = miro.RectangleLight()
             pl.setVertices(l["v1"], l["v2"], l["v3"])
@@ -317,6 +364,9 @@ def build_config(key, device=0):
         pl.setPower(l["power"])
         scene.addLight(pl)
     scene.setBGColor(cfg["bg"])
+    if cfg.get("env"):
+        scene.setEnvMap(sky_texture(tuple(cfg["env"]["sky"])))
+        scene.setEnvExposure(cfg["env"]["exposure"])
     scene.setNumPaths(cfg.get("num_paths", 1))
     scene.preCalc()
     cam = miro.Camera()

@@ -42,11 +42,30 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
         fl.setN1((0, 1, 0)); fl.setN2((0, 1, 0)); fl.setN3((0, 1, 0))
         miro.makeMeshObjs(P, fl, pm)
         O_.add_mesh(fl.verts, fl.normals, fl.vidx, fl.nidx, om)
+    textures = {}
+
+    def texture(rgb):  # one product Texture + one oracle texture per image
+        if id(rgb) not in textures:
+            tex = miro.Texture(miro.RawImage(rgb.shape[1], rgb.shape[0], rgb))
+            textures[id(rgb)] = (tex, O_.add_texture(rgb))
+        return textures[id(rgb)]
+
+    def sky(spec):
+        return spec if isinstance(spec, np.ndarray) else scenes.sky_rgb(*spec)
+
     for l in lights:
         if l["type"] == "point":
             pl = miro.PointLight(); pl.setPosition(l["pos"]); pl.setPower(l["power"])
             P.addLight(pl)
             O_.add_point_light(l["pos"], l["power"])
+        elif l["type"] == "dome":
+            rgb = sky(l["sky"])
+            l = dict(l, sky=rgb)
+            tex, otex = texture(rgb)
+            dl = miro.DomeLight(); dl.setTexture(tex); dl.setPower(l["power"])
+            dl.setSamples(l.get("samples", 1)); dl.setNoiseThreshold(l.get("noise", 0.001))
+            P.addLight(dl)
+            O_.add_dome_light(otex, l["power"], l.get("samples", 1), l.get("noise", 0.001))
         else:
             rl = miro.RectangleLight(); rl.setVertices(l["v1"], l["v2"], l["v3"]); rl.setPower(l["power"])
             rl.setSamples(l.get("samples", 1)); rl.setNoiseThreshold(l.get("noise", 0.001))
@@ -54,6 +73,11 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
             O_.add_rect_light(l["v1"], l["v2"], l["v3"], l["power"], l.get("samples", 1), l.get("noise", 0.001))
     P.setBGColor(cfg["bg"])
     O_.set_bg(cfg["bg"])
+    env = cfg.get("env")
+    if env:
+        tex, otex = texture(sky(env["sky"]))
+        P.setEnvMap(tex); P.setEnvExposure(env["exposure"])
+        O_.set_env_map(otex, env["exposure"])
     P.setNumPaths(num_paths)
     O_.set_num_paths(num_paths)
     P.preCalc()
