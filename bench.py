@@ -96,12 +96,23 @@ def cpu_baseline(cfg_key, seconds):
         import numpy as np
         f = np.load(os.path.join(ROOT, "tests", "golden", "cornell_box_mesh.npz"))
         s.add_mesh(f["verts"], f["normals"], f["vidx"], f["nidx"], m)
+    skies = {}
+
+    def sky(size):
+        if size not in skies:
+            skies[size] = s.add_texture(scenes.sky_rgb(*size))
+        return skies[size]
+
     for l in cfg["lights"]:
         if l["type"] == "point":
             s.add_point_light(l["pos"], l["power"])
+        elif l["type"] == "dome":
+            s.add_dome_light(sky(tuple(l["sky"])), l["power"], l.get("samples", 1), l.get("noise", 0.001))
         else:
             s.add_rect_light(l["v1"], l["v2"], l["v3"], l["power"], l.get("samples", 1), l.get("noise", 0.001))
     s.set_bg(cfg["bg"])
+    if cfg.get("env"):
+        s.set_env_map(sky(tuple(cfg["env"]["sky"])), cfg["env"]["exposure"])
     s.set_num_paths(cfg.get("num_paths", 1))
     s.build()
     W, H = cfg["W"], cfg["H"]
@@ -253,7 +264,9 @@ def main():
     hits_mine = hits_px
     b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=use_frame_path)
     pm, sm = float(np.median(prim_ms)), float(np.median(shade_ms))
-    one_light = len(cfg["lights"]) == 1 and cfg.get("num_paths", 1) == 1
+    # the specialised kernel runs for one point light, one path and no environment map
+    one_light = (len(cfg["lights"]) == 1 and cfg["lights"][0]["type"] == "point" and cfg.get("num_paths", 1) == 1
+                 and not cfg.get("env"))
     shade_name = "shade1_kernel" if one_light else "shade_kernel"
     if sm >= pm:
         dom, dom_ms, dom_b = shade_name + " (shade + any-hit shadow rays)", sm, b_shade
@@ -270,12 +283,14 @@ def main():
         except Exception:
             traffic = None
     out = {
-        "metric": "Mray/s (primary+shadow) on Sponza 1920x1080" + ("" if args.config == "C3" else f" [{args.config}]"),
+        "metric": ("Mray/s (primary+shadow) on Sponza 1920x1080" if args.config == "C3" else
+                   f"Mray/s (primary+shadow) [{args.config}: {cfg['name']}]"),
         "value": round(value, 2), "unit": "Mray/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (deterministic Sponza stand-in, %d tris; sponza.obj is not in the reference snapshot)"
-                % scene.bvh_info["prims"],
+        "data": ("synthetic (deterministic %s stand-in, %d tris; %s.obj is not in the reference snapshot%s)"
+                 % ({"sponza": "Sponza", "bunny": "bunny"}.get(cfg["mesh"], cfg["mesh"]), scene.bvh_info["prims"],
+                    cfg["mesh"], "; procedural lat-long sky for the dome / environment map" if cfg.get("env") else "")),
         "config": {"workload": cfg["name"], "config": args.config, "width": W, "height": H, "spp": 1,
                    "frames_per_step": n_frames, "rays_per_step": rays_per_step, "shadow_rays": shadow_total,
                    "qbvh_nodes": scene.bvh_info["nodes"], "qbvh_leaves": scene.bvh_info["leaves"],
