@@ -168,6 +168,23 @@ int mrt_scene_dome_info(const mrt_scene* s, int32_t light, int32_t* nu, int32_t*
 int mrt_scene_dome_export(const mrt_scene* s, int32_t light, float* cdf_u, float* func_u, float* cdf_v,
                           float* func_v, float* func_int, float* cos_u, float* sin_u, float* cos_v, float* sin_v);
 
+/* ---- instancing: ProxyObject (src/ProxyObject.cpp:5-95,131-167) -----------
+ * mrt_scene_make_blas builds a proxy BVH from meshes already added
+ * (ProxyObject::setupMultiProxy: the meshes in order, each mesh's triangles last
+ * to first, then BVH::build); those meshes leave the world object list.  Returns
+ * the BLAS id.  mrt_scene_add_instance adds one ProxyObject (row-major 4x4
+ * m_transform; ProxyMatrix derives the inverse and inverse transpose); it joins
+ * the world objects in call order with the world meshes.  Hit ids (mrt_hit.prim):
+ * world objects 0..n-1 (mrt_bvh_info.prims = n; a proxy's own slot never hits),
+ * then instance i's BLAS objects at n + (BLAS sizes of the instances before i) +
+ * BLAS object index.  blas_info/export give a BLAS's canonical QBVH arrays
+ * (same layout as mrt_scene_bvh_export). */
+int mrt_scene_make_blas(mrt_scene* s, const int32_t* meshes, int32_t n_meshes);
+int mrt_scene_add_instance(mrt_scene* s, int32_t blas, const float* m16);
+int mrt_scene_blas_info(const mrt_scene* s, int32_t blas, int32_t* nodes, int32_t* leaves, int32_t* prims);
+int mrt_scene_blas_export(const mrt_scene* s, int32_t blas, float* node_boxes, int32_t* node_child,
+                          float* leaf_tris, int32_t* leaf_prims);
+
 /* Scene::preCalc -> BVH::build (src/Scene.cpp:62-79, src/BVH.cpp:457-575):
  * binned SAH, 4-wide collapse, host-side; then uploads to the device lazily. */
 int mrt_scene_build_bvh(mrt_scene* s);

@@ -183,7 +183,15 @@ typedef struct {               /* QBVH_Node (src/BVH.h:83-109) */
 typedef struct {               /* BVH_Node::TriCache4 (src/BVH.h:37-50) */
     float t[36];               /* Ax[4] Ay[4] Az[4] e0x e0y e0z e1x e1y e1z */
     int32_t prim[4];
+    int32_t inst[4];           /* checkOut lanes: ProxyObject instance id, else -1 */
 } qleaf;
+
+typedef struct {               /* ProxyObject + ProxyMatrix (src/ProxyObject.cpp:5-12, src/ProxyMatrix.cpp:3-8) */
+    mat4 M, inv, invT;         /* m_transform, m_inverse, m_invTranspose */
+    int blas;                  /* the proxy's BVH */
+    int prim_base;             /* hit id of its BLAS object 0, counted after the world objects */
+    aabb box;                  /* ProxyObject::getAABB */
+} oro_inst;
 
 #define ORO_MAX_TEX 16
 
@@ -196,8 +204,12 @@ struct oro_scene {
     int env_tex; float env_exposure;  /* Scene::m_envMap / m_envExposure */
     v3 bg;
     int num_paths;
-    /* objects (Object*): one per triangle, scene order (makeMeshObjs) */
-    int n_obj; int* obj_mesh; int* obj_tri;
+    int* mesh_blas;                   /* per mesh: owning BLAS, -1 = world geometry */
+    int* groups; int n_groups;        /* world objects in add order: mesh m >= 0, instance ~i */
+    struct oro_scene** blas; int n_blas;   /* ProxyObject BVHs (sub-scenes sharing the meshes) */
+    oro_inst* inst; int n_inst;
+    /* objects (Object*): one per triangle (makeMeshObjs) or ProxyObject, scene order */
+    int n_obj; int* obj_mesh; int* obj_tri; int* obj_inst;
     /* build products */
     bnode* bn; int n_bn, cap_bn; int bin_leaves, bin_depth;
     qnode* qn; int n_qn, cap_qn;
@@ -214,8 +226,8 @@ oro_scene* oro_scene_create(void) {
     return s;
 }
 static void free_build(oro_scene* s) {
-    free(s->bn); free(s->qn); free(s->ql); free(s->obj_mesh); free(s->obj_tri);
-    s->bn = NULL; s->qn = NULL; s->ql = NULL; s->obj_mesh = NULL; s->obj_tri = NULL;
+    free(s->bn); free(s->qn); free(s->ql); free(s->obj_mesh); free(s->obj_tri); free(s->obj_inst);
+    s->bn = NULL; s->qn = NULL; s->ql = NULL; s->obj_mesh = NULL; s->obj_tri = NULL; s->obj_inst = NULL;
     s->n_bn = s->cap_bn = s->n_qn = s->cap_qn = s->n_ql = s->n_obj = 0; s->built = 0;
 }
 void oro_scene_destroy(oro_scene* s) {
@@ -226,6 +238,8 @@ void oro_scene_destroy(oro_scene* s) {
     }
     for (int i = 0; i < s->n_lights; i++) ibl_dome_free(&s->domes[i]);
     for (int i = 0; i < s->n_tex; i++) free(s->tex[i].rgb);
+    for (int i = 0; i < s->n_blas; i++) { free_build(s->blas[i]); free(s->blas[i]); }
+    free(s->blas); free(s->inst); free(s->groups); free(s->mesh_blas);
     free(s->meshes); free(s->mats); free(s->lights); free(s->domes);
     free_build(s);
     free(s);
@@ -307,8 +321,12 @@ static int push_mesh(oro_scene* s, mesh_t* m) {
     if (s->n_meshes == s->cap_meshes) {
         s->cap_meshes = s->cap_meshes ? 2 * s->cap_meshes : 8;
         s->meshes = (mesh_t*)realloc(s->meshes, sizeof(mesh_t) * s->cap_meshes);
+        s->mesh_blas = (int*)realloc(s->mesh_blas, sizeof(int) * s->cap_meshes);
     }
     s->meshes[s->n_meshes] = *m;
+    s->mesh_blas[s->n_meshes] = -1;
+    s->groups = (int*)realloc(s->groups, sizeof(int) * (s->n_groups + 1));
+    s->groups[s->n_groups++] = s->n_meshes;
     s->built = 0;
     return s->n_meshes++;
 }
@@ -445,6 +463,7 @@ static inline v3 overt(const oro_scene* s, int o, int k) {
 }
 /* TriangleMesh::getAABB, src/TriangleMesh.cpp:156-195 */
 static aabb obj_aabb(const oro_scene* s, int o) {
+    if (s->obj_inst && s->obj_inst[o] >= 0) return s->inst[s->obj_inst[o]].box;   /* ProxyObject::getAABB */
     v3 A = overt(s, o, 0), B = overt(s, o, 1), C = overt(s, o, 2);
     aabb b;
     b.mn[0] = std_min(A.x, std_min(B.x, C.x)); b.mn[1] = std_min(A.y, std_min(B.y, C.y)); b.mn[2] = std_min(A.z, std_min(B.z, C.z));
@@ -645,19 +664,21 @@ static void build_bin(build_ctx* c, int node, int* objs, aabb* pre, float* cen, 
     c->cur_depth--;
 }
 
-/* QBVH_Node::buildTriBundle, src/BVH.cpp:64-98 */
+/* QBVH_Node::buildTriBundle, src/BVH.cpp:64-98: a ProxyObject lane is a
+ * checkOut lane with a zero triangle (rejected by det = 0 -> NaN). */
 static int build_tri_bundle(oro_scene* s, const int* objs_all, int bnode_i, int* nodeNum) {
     qleaf* L = &s->ql[*nodeNum];
     memset(L, 0, sizeof(qleaf));
     const bnode* b = &s->bn[bnode_i];
-    for (int i = 0; i < 4; i++) L->prim[i] = -1;
+    for (int i = 0; i < 4; i++) { L->prim[i] = -1; L->inst[i] = -1; }
     for (int i = 0; i < b->count; i++) {
         int o = objs_all[b->start + i];
+        L->prim[i] = o;
+        if (s->obj_inst && s->obj_inst[o] >= 0) { L->inst[i] = s->obj_inst[o]; continue; }
         v3 A = overt(s, o, 0), B = overt(s, o, 1), C = overt(s, o, 2);
         L->t[0 + i] = A.x; L->t[4 + i] = A.y; L->t[8 + i] = A.z;
         L->t[12 + i] = B.x - A.x; L->t[16 + i] = B.y - A.y; L->t[20 + i] = B.z - A.z;
         L->t[24 + i] = C.x - A.x; L->t[28 + i] = C.y - A.y; L->t[32 + i] = C.z - A.z;
-        L->prim[i] = o;
     }
     return (*nodeNum)++;
 }
@@ -747,18 +768,10 @@ static void qbuild(oro_scene* s, const int* objs, int qi, int bi, int* nodeNum, 
 
 static int qbvh_max_depth = 0;
 
-/* BVH::build (USE_BINS + USE_QBVH), src/BVH.cpp:457-575 */
-int oro_scene_build(oro_scene* s) {
-    free_build(s);
-    int n = 0;
-    for (int m = 0; m < s->n_meshes; m++) n += s->meshes[m].nt;
-    if (n <= 0) return -1;
-    s->n_obj = n;
-    s->obj_mesh = (int*)malloc(sizeof(int) * n);
-    s->obj_tri = (int*)malloc(sizeof(int) * n);
-    int k = 0;
-    for (int m = 0; m < s->n_meshes; m++)
-        for (int t = 0; t < s->meshes[m].nt; t++) { s->obj_mesh[k] = m; s->obj_tri[k] = t; k++; }
+/* BVH::build (USE_BINS + USE_QBVH), src/BVH.cpp:457-575, over the object list
+ * already in s->obj_* (n = s->n_obj). */
+static int build_objects(oro_scene* s) {
+    int n = s->n_obj;
     build_ctx c; memset(&c, 0, sizeof c);
     c.s = s;
     c.objs = (int*)malloc(sizeof(int) * n);
@@ -797,6 +810,125 @@ int oro_scene_build(oro_scene* s) {
     return rc;
 }
 
+/* Scene::preCalc: the world objects in add order -- each world mesh's triangles
+ * (makeMeshObjs) and each ProxyObject -- then BVH::build. */
+int oro_scene_build(oro_scene* s) {
+    free_build(s);
+    int n = 0;
+    for (int g = 0; g < s->n_groups; g++) {
+        int id = s->groups[g];
+        if (id >= 0) { if (s->mesh_blas[id] < 0) n += s->meshes[id].nt; }
+        else n += 1;
+    }
+    if (n <= 0) return -1;
+    s->n_obj = n;
+    s->obj_mesh = (int*)malloc(sizeof(int) * n);
+    s->obj_tri = (int*)malloc(sizeof(int) * n);
+    s->obj_inst = (int*)malloc(sizeof(int) * n);
+    int k = 0;
+    for (int g = 0; g < s->n_groups; g++) {
+        int id = s->groups[g];
+        if (id >= 0) {
+            if (s->mesh_blas[id] >= 0) continue;
+            for (int t = 0; t < s->meshes[id].nt; t++) { s->obj_mesh[k] = id; s->obj_tri[k] = t; s->obj_inst[k] = -1; k++; }
+        } else {
+            s->obj_mesh[k] = -1; s->obj_tri[k] = -1; s->obj_inst[k] = ~id; k++;
+        }
+    }
+    int base = 0;   /* instance hit ids follow the world objects, instance by instance */
+    for (int i = 0; i < s->n_inst; i++) { s->inst[i].prim_base = base; base += s->blas[s->inst[i].blas]->n_obj; }
+    return build_objects(s);
+}
+
+/* QBVH_Node::getAABB (src/BVH.cpp:416-424) of a hierarchy's root: the union of
+ * all four slot boxes, unused slots included (zero boxes, src/BVH.cpp:107-112). */
+static aabb root_aabb(const oro_scene* b) {
+    aabb out = aabb_empty();
+    const qnode* q = &b->qn[0];
+    for (int i = 0; i < 4; i++) {
+        aabb x;
+        x.mn[0] = q->box[0 + i]; x.mn[1] = q->box[4 + i]; x.mn[2] = q->box[8 + i];
+        x.mx[0] = q->box[12 + i]; x.mx[1] = q->box[16 + i]; x.mx[2] = q->box[20 + i];
+        out = aabb_union(out, x);
+    }
+    return out;
+}
+
+/* ProxyObject::getAABB, src/ProxyObject.cpp:45-72: the BLAS box's corners
+ * A..F, bbMin, bbMax through multiplyAndDivideByW, grown in that order. */
+static aabb proxy_aabb(const oro_scene* b, const mat4* M) {
+    aabb t = root_aabb(b);
+    v3 P[8] = {V(t.mn[0], t.mn[1], t.mx[2]), V(t.mn[0], t.mx[1], t.mn[2]), V(t.mx[0], t.mn[1], t.mn[2]),
+               V(t.mn[0], t.mx[1], t.mx[2]), V(t.mx[0], t.mx[1], t.mn[2]), V(t.mx[0], t.mn[1], t.mx[2]),
+               V(t.mn[0], t.mn[1], t.mn[2]), V(t.mx[0], t.mx[1], t.mx[2])};
+    aabb nb = aabb_empty();
+    for (int k = 0; k < 8; k++) {
+        v3 q = mat_mul_div_w(M, P[k]);
+        float f[3] = {q.x, q.y, q.z};
+        aabb_grow(&nb, f);
+    }
+    return nb;
+}
+
+/* ProxyObject::setupMultiProxy (src/ProxyObject.cpp:149-167): the meshes in
+ * order, each mesh's triangles last to first, then BVH::build.  The meshes
+ * leave the world object list. */
+int oro_scene_make_blas(oro_scene* s, const int* meshes, int n_meshes) {
+    if (n_meshes <= 0 || !meshes) return -1;
+    int n = 0;
+    for (int j = 0; j < n_meshes; j++) {
+        int m = meshes[j];
+        if (m < 0 || m >= s->n_meshes || s->mesh_blas[m] >= 0) return -1;
+        for (int i = 0; i < j; i++) if (meshes[i] == m) return -1;
+        n += s->meshes[m].nt;
+    }
+    if (n <= 0) return -1;
+    oro_scene* b = (oro_scene*)calloc(1, sizeof(oro_scene));
+    b->meshes = s->meshes; b->n_meshes = s->n_meshes;     /* borrowed for the build only */
+    b->n_obj = n;
+    b->obj_mesh = (int*)malloc(sizeof(int) * n);
+    b->obj_tri = (int*)malloc(sizeof(int) * n);
+    int k = 0;
+    for (int j = 0; j < n_meshes; j++)
+        for (int t = s->meshes[meshes[j]].nt - 1; t >= 0; t--) { b->obj_mesh[k] = meshes[j]; b->obj_tri[k] = t; k++; }
+    int rc = build_objects(b);
+    b->meshes = NULL; b->n_meshes = 0;
+    if (rc) { free_build(b); free(b); return rc < 0 ? rc : -2; }
+    for (int j = 0; j < n_meshes; j++) s->mesh_blas[meshes[j]] = s->n_blas;
+    s->blas = (oro_scene**)realloc(s->blas, sizeof(oro_scene*) * (s->n_blas + 1));
+    s->blas[s->n_blas] = b;
+    s->built = 0;
+    return s->n_blas++;
+}
+
+int oro_scene_add_instance(oro_scene* s, int blas, const float* m16) {
+    if (blas < 0 || blas >= s->n_blas || !m16) return -1;
+    oro_inst I;
+    memset(&I, 0, sizeof I);
+    memcpy(I.M.m, m16, sizeof(float) * 16);
+    I.inv = mat_invert(I.M);                      /* ProxyMatrix(M), src/ProxyMatrix.cpp:3-8 */
+    I.invT = mat_transpose(mat_invert(I.M));
+    I.blas = blas;
+    I.box = proxy_aabb(s->blas[blas], &I.M);
+    s->inst = (oro_inst*)realloc(s->inst, sizeof(oro_inst) * (s->n_inst + 1));
+    s->inst[s->n_inst] = I;
+    s->groups = (int*)realloc(s->groups, sizeof(int) * (s->n_groups + 1));
+    s->groups[s->n_groups++] = ~s->n_inst;
+    s->built = 0;
+    return s->n_inst++;
+}
+
+int oro_blas_info(const oro_scene* s, int blas, int* n_nodes, int* n_leaves, int* n_prims) {
+    if (blas < 0 || blas >= s->n_blas) return -1;
+    *n_nodes = s->blas[blas]->n_qn; *n_leaves = s->blas[blas]->n_ql; *n_prims = s->blas[blas]->n_obj;
+    return 0;
+}
+int oro_blas_export(const oro_scene* s, int blas, float* node_boxes, int32_t* node_child, float* leaf_tris,
+                    int32_t* leaf_prims) {
+    if (blas < 0 || blas >= s->n_blas) return -1;
+    return oro_qbvh_export(s->blas[blas], node_boxes, node_child, leaf_tris, leaf_prims);
+}
+
 int oro_qbvh_info(const oro_scene* s, int* n_nodes, int* n_leaves, int* n_prims, int* bin_nodes, int* bin_leaves, int* max_depth) {
     if (!s->built) return -1;
     *n_nodes = s->n_qn; *n_leaves = s->n_ql; *n_prims = s->n_obj;
@@ -833,7 +965,12 @@ static ray_t make_ray(v3 o, v3 d) {
     return r;
 }
 
-typedef struct { float t, a, b; int prim; } hit_t;
+typedef struct { float t, a, b; int prim; int inst; } hit_t;   /* inst: ProxyObject of the hit, -1 */
+
+/* global hit id: world objects, then each instance's BLAS objects */
+static int hit_id(const oro_scene* s, const hit_t* h) {
+    return h->inst >= 0 ? s->n_obj + s->inst[h->inst].prim_base + h->prim : h->prim;
+}
 
 /* QBVH_Node::intersect, src/BVH.cpp:391-414 -> 4-bit boxHit */
 static int box_test(const qnode* q, const ray_t* r, float tMin, float tMax) {
@@ -853,8 +990,34 @@ static int box_test(const qnode* q, const ray_t* r, float tMin, float tMax) {
     return mask;
 }
 
-/* intersect4, src/BVH.cpp:1298-1459 (no proxy / MB / alpha in the hot path) */
-static int intersect4(const qleaf* L, const ray_t* r, float tMin, hit_t* h) {
+static int bvh_intersect(const oro_scene* s, const ray_t* r, float tMin, hit_t* h, uint32_t* nv, uint32_t* lv);
+
+/* ProxyObject::intersect, src/ProxyObject.cpp:76-95: the ray in object space
+ * (origin: multiplyAndDivideByW of (o, 1); direction: 4-wide dots with d.w = 0,
+ * src/Matrix4x4.h:706-748, o[3] = 1 and d[3] = 0 from src/Ray.h:140-141), the
+ * proxy's BVH with the current t as tMax. */
+static int proxy_intersect(const oro_scene* s, int inst, const ray_t* r, float tMin, hit_t* h, uint32_t* nv,
+                           uint32_t* lv) {
+    const oro_inst* I = &s->inst[inst];
+    float o4[4] = {r->o[0], r->o[1], r->o[2], 1.0f}, d4[4] = {r->d[0], r->d[1], r->d[2], 0.0f};
+    float w = rcp_nr(dp4(I->inv.m[3], o4));
+    v3 no = V(w * dp4(I->inv.m[0], o4), w * dp4(I->inv.m[1], o4), w * dp4(I->inv.m[2], o4));
+    v3 nd = V(dp4(I->inv.m[0], d4), dp4(I->inv.m[1], d4), dp4(I->inv.m[2], d4));
+    ray_t nr = make_ray(no, nd);
+    hit_t nh = {h->t, 0, 0, -1, -1};
+    int hit = bvh_intersect(s->blas[I->blas], &nr, tMin, &nh, nv, lv);
+    if (hit > 0) { h->a = nh.a; h->b = nh.b; h->t = nh.t; h->prim = nh.prim; h->inst = inst; return 1; }
+    return hit < 0 ? hit : 0;
+}
+
+/* intersect4, src/BVH.cpp:1298-1459: proxy (checkOut) lanes first, in lane
+ * order (:1305-1315), then the packet's triangles against the updated t.
+ * No motion blur / alpha maps on this path. */
+static int intersect4(const oro_scene* s, const qleaf* L, const ray_t* r, float tMin, hit_t* h, uint32_t* nv,
+                      uint32_t* lv) {
+    int proxyIntersect = 0;
+    for (int i = 0; i < 4; i++)
+        if (L->inst[i] >= 0 && proxy_intersect(s, L->inst[i], r, tMin, h, nv, lv)) proxyIntersect = 1;
     float newT[4], A[4], B[4];
     int tMask = 0;
     for (int i = 0; i < 4; i++) {
@@ -878,12 +1041,12 @@ static int intersect4(const qleaf* L, const ray_t* r, float tMin, hit_t* h) {
         tMask |= ok << i;
         newT[i] = t; A[i] = a; B[i] = b;
     }
-    if (!tMask) return 0;
+    if (!tMask) return proxyIntersect;
     for (int i = 0; i < 4; i++) newT[i] = (tMask & (1 << i)) ? newT[i] : 1e12f;
     float lowest = newT[0]; int li = 0;
     for (int i = 1; i < 4; i++) if (newT[i] < lowest) { lowest = newT[i]; li = i; }
     if (lowest < h->t) {
-        h->t = lowest; h->a = A[li]; h->b = B[li]; h->prim = L->prim[li];
+        h->t = lowest; h->a = A[li]; h->b = B[li]; h->prim = L->prim[li]; h->inst = -1;
     }
     return 1;
 }
@@ -906,7 +1069,7 @@ static int bvh_intersect(const oro_scene* s, const ray_t* r, float tMin, hit_t* 
             if (c == (int32_t)0x80000000u) continue;
             if (c < 0) {
                 if (lv) (*lv)++;
-                if (intersect4(&s->ql[~c], r, tMin, h)) hit = 1;
+                if (intersect4(s, &s->ql[~c], r, tMin, h, nv, lv)) hit = 1;
             } else tmp[ch++] = c;
         }
         if (sp + ch > 256) return -1;
@@ -921,11 +1084,11 @@ int oro_trace(const oro_scene* s, size_t n, const float* o, const float* d, cons
     if (!s->built) return -1;
     for (size_t i = 0; i < n; i++) {
         ray_t r = make_ray(V(o[3 * i], o[3 * i + 1], o[3 * i + 2]), V(d[3 * i], d[3 * i + 1], d[3 * i + 2]));
-        hit_t h = {tmax[i], 0, 0, -1};
+        hit_t h = {tmax[i], 0, 0, -1, -1};
         uint32_t nv = 0, lv = 0;
         int rc = bvh_intersect(s, &r, tmin[i], &h, &nv, &lv);
         if (rc < 0) return -2;
-        out[i].t = h.t; out[i].a = h.a; out[i].b = h.b; out[i].prim = rc ? h.prim : -1;
+        out[i].t = h.t; out[i].a = h.a; out[i].b = h.b; out[i].prim = rc ? hit_id(s, &h) : -1;
         if (node_visits) node_visits[i] = nv;
         if (leaf_visits) leaf_visits[i] = lv;
     }
@@ -961,7 +1124,7 @@ static float next_rand(shade_ctx* c) { return oro_rand(c->pixel, 0, c->dim++, 0x
 
 static int trace_shadow(shade_ctx* c, v3 from, v3 L, float tMax) {
     ray_t r = make_ray(from, L);
-    hit_t h = {tMax, 0, 0, -1};
+    hit_t h = {tMax, 0, 0, -1, -1};
     uint32_t nv = 0, lv = 0;
     int rc = bvh_intersect(c->s, &r, 0.001f, &h, &nv, &lv);
     c->shadow_rays++; c->nodes += nv; c->leaves += lv;
@@ -1096,16 +1259,29 @@ static v3 sample_light(shade_ctx* c, int li, v3 from, v3 normal, v3 rVec, float*
     return rect_light(c, l, li, from, normal, rVec, outSpec);
 }
 
-/* HitInfo::getAllInfos (normals only), src/Ray.cpp:5-49 */
+/* the mesh and triangle of a hit (an instance hit names its BLAS object) */
+static const mesh_t* hit_mesh(const oro_scene* s, const hit_t* h, int* tri) {
+    const oro_scene* os = h->inst >= 0 ? s->blas[s->inst[h->inst].blas] : s;
+    *tri = os->obj_tri[h->prim];
+    return &s->meshes[os->obj_mesh[h->prim]];
+}
+
+/* HitInfo::getAllInfos (normals only), src/Ray.cpp:5-49; an instance hit's
+ * normals go through m_invTranspose (Matrix4x4 * Vector3, src/Matrix4x4.h:693-704)
+ * and are renormalised (:27-31). */
 static void hit_normals(const oro_scene* s, const hit_t* h, v3* N, v3* geoN) {
-    int o = h->prim;
-    const mesh_t* m = omesh(s, o);
-    int t = s->obj_tri[o];
+    int t;
+    const mesh_t* m = hit_mesh(s, h, &t);
     v3 A = m->verts[m->vidx[3 * t]], B = m->verts[m->vidx[3 * t + 1]], C = m->verts[m->vidx[3 * t + 2]];
     *geoN = vnormalized(vcross(vsub(B, A), vsub(C, A)));
     float cc = 1.0f - h->a - h->b;
     v3 n0 = m->normals[m->nidx[3 * t]], n1 = m->normals[m->nidx[3 * t + 1]], n2 = m->normals[m->nidx[3 * t + 2]];
     *N = vnormalized(vadd(vadd(vscale(n0, cc), vscale(n1, h->a)), vscale(n2, h->b)));
+    if (h->inst >= 0) {
+        const oro_inst* I = &s->inst[h->inst];
+        *geoN = vnormalized(mat_mul_v3(&I->invT, *geoN));
+        *N = vnormalized(mat_mul_v3(&I->invT, *N));
+    }
 }
 
 /* Ray::getPoint, src/Ray.h:168-177 */
@@ -1225,11 +1401,12 @@ static uint8_t map_channel(float r) {
 /* Scene::sampleScene, src/Scene.cpp:219-243 */
 static v3 sample_scene(shade_ctx* c, const ray_t* r, hit_t* h, uint32_t* prim_nv, uint32_t* prim_lv) {
     const oro_scene* s = c->s;
-    h->t = 1e12f; h->a = h->b = 0; h->prim = -1;
+    h->t = 1e12f; h->a = h->b = 0; h->prim = -1; h->inst = -1;
     int rc = bvh_intersect(s, r, 0.001f, h, prim_nv, prim_lv);
     if (rc > 0) {
         v3 result = V(0, 0, 0);
-        const oro_material* mat = &s->mats[omesh(s, h->prim)->material];
+        int tri;
+        const oro_material* mat = &s->mats[hit_mesh(s, h, &tri)->material];
         for (int i = 0; i < s->num_paths; i++) {
             v3 sh = (mat->type == ORO_LAMBERT) ? shade_lambert(c, mat, r, h) : shade_blinn(c, mat, r, h);
             result = vadd(result, sh);
@@ -1273,7 +1450,7 @@ int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H, int x0, 
             size_t p = (size_t)y * W + x;
             if (rgb) { rgb[3 * p] = col.x; rgb[3 * p + 1] = col.y; rgb[3 * p + 2] = col.z; }
             if (rgb8) { rgb8[3 * p] = map_channel(col.x); rgb8[3 * p + 1] = map_channel(col.y); rgb8[3 * p + 2] = map_channel(col.z); }
-            if (hitout) { hitout[p].t = h.t; hitout[p].a = h.a; hitout[p].b = h.b; hitout[p].prim = h.prim; }
+            if (hitout) { hitout[p].t = h.t; hitout[p].a = h.a; hitout[p].b = h.b; hitout[p].prim = h.prim >= 0 ? hit_id(s, &h) : -1; }
             if (shadow) shadow[p] = c.shadow_mask;
             prim++; shadowr += c.shadow_rays; nodes += nv + c.nodes; leaves += lv + c.leaves;
             pnodes += nv; pleaves += lv;

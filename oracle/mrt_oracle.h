@@ -80,6 +80,19 @@ void oro_scene_set_bg(oro_scene* s, float r, float g, float b);
 void oro_scene_set_num_paths(oro_scene* s, int n);
 /* Scene::preCalc -> BVH::build (src/Scene.cpp:62-79, src/BVH.cpp:457-575). */
 int oro_scene_build(oro_scene* s);
+/* ProxyObject instancing (src/ProxyObject.cpp:5-95,131-167).  oro_scene_make_blas
+ * builds a proxy BVH from whole meshes (ProxyObject::setupMultiProxy: meshes in
+ * order, each one's triangles last to first); those meshes leave the world
+ * object list.  oro_scene_add_instance adds one ProxyObject (row-major 4x4) to
+ * the world objects, in add order with the world meshes.  Hit ids: world
+ * objects 0..n-1 (a proxy's own id never hits), then instance i's BLAS objects
+ * at n + (sum of the BLAS sizes of instances < i) + BLAS object index. */
+int oro_scene_make_blas(oro_scene* s, const int* meshes, int n_meshes);
+int oro_scene_add_instance(oro_scene* s, int blas, const float* m16);
+int oro_blas_info(const oro_scene* s, int blas, int* n_nodes, int* n_leaves, int* n_prims);
+int oro_blas_export(const oro_scene* s, int blas, float* node_boxes, int32_t* node_child, float* leaf_tris,
+                    int32_t* leaf_prims);
+
 /* Canonical QBVH export (preorder node numbering, leaf numbering = nodeNum). */
 int oro_qbvh_info(const oro_scene* s, int* n_nodes, int* n_leaves, int* n_prims,
                   int* bin_nodes, int* bin_leaves, int* max_depth);

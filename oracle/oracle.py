@@ -89,6 +89,10 @@ def _declare(L):
     L.oro_dome_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.oro_dome_export.argtypes = [C.c_void_p, C.c_int] + [_fp] * 9
     L.oro_texture_lookup_dir.argtypes = [C.c_void_p, C.c_int, C.c_int, _fp, _fp]
+    L.oro_scene_make_blas.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
+    L.oro_scene_add_instance.argtypes = [C.c_void_p, C.c_int, _fp]
+    L.oro_blas_info.argtypes = [C.c_void_p, C.c_int] + [C.POINTER(C.c_int)] * 3
+    L.oro_blas_export.argtypes = [C.c_void_p, C.c_int, _fp, _i32p, _fp, _i32p]
 
 
 DOME_KEYS = ("cdf_u", "func_u", "cdf_v", "func_v", "func_int", "cos_u", "sin_u", "cos_v", "sin_v")
@@ -217,6 +221,32 @@ class OracleScene:
             raise RuntimeError(f"oracle dome light rejected ({r})")
         self.n_lights += 1
         return r
+
+    def make_blas(self, meshes):
+        """ProxyObject::setupMultiProxy + BVH::build over mesh ids (they leave the world)."""
+        ids = (C.c_int * len(meshes))(*[int(m) for m in meshes])
+        r = self.L.oro_scene_make_blas(self.h, ids, len(meshes))
+        if r < 0:
+            raise RuntimeError(f"oracle BLAS build failed ({r})")
+        return r
+
+    def add_instance(self, blas, m):
+        m16 = np.ascontiguousarray(np.asarray(m, np.float32).reshape(16))
+        r = self.L.oro_scene_add_instance(self.h, int(blas), _p(m16, _fp))
+        if r < 0:
+            raise RuntimeError("oracle add_instance failed")
+        return r
+
+    def blas_export(self, blas):
+        n, l, p = C.c_int(), C.c_int(), C.c_int()
+        if self.L.oro_blas_info(self.h, int(blas), C.byref(n), C.byref(l), C.byref(p)) != 0:
+            raise RuntimeError("bad BLAS id")
+        nb = np.zeros((n.value, 24), np.float32)
+        nc = np.zeros((n.value, 4), np.int32)
+        lt = np.zeros((l.value, 36), np.float32)
+        lp = np.zeros((l.value, 4), np.int32)
+        self.L.oro_blas_export(self.h, int(blas), _p(nb, _fp), _p(nc, _i32p), _p(lt, _fp), _p(lp, _i32p))
+        return nb, nc, lt, lp
 
     def set_env_map(self, texture, exposure=1.0):
         if self.L.oro_scene_set_env_map(self.h, int(texture), float(exposure)) != 0:

@@ -270,10 +270,14 @@ struct BNode {
 
 class Builder {
    public:
-    Builder(Scene& s) : s_(s) {}
+    // objects (om_[o], ot_[o]) or, where (*oi_)[o] >= 0, ProxyObject (*oi_)[o];
+    // the hierarchy goes to nodes / leaves
+    Builder(const Scene& s, const std::vector<int32_t>& om, const std::vector<int32_t>& ot,
+            const std::vector<int32_t>* oi, std::vector<QNode>& nodes, std::vector<QLeaf>& leaves)
+        : s_(s), om_(om), ot_(ot), oi_(oi), nodes_(nodes), leaves_(leaves) {}
 
     int run(std::string& err) {
-        const int n = (int)s_.obj_mesh.size();
+        const int n = (int)om_.size();
         tri_box_.resize(n);
         cen_obj_.resize((size_t)3 * n);
         for (int i = 0; i < n; i++) {
@@ -303,9 +307,15 @@ class Builder {
     int bin_leaves = 0, bin_depth = 0, q_depth = 0;
 
    private:
-    Box tri_aabb(int o) const {  // TriangleMesh::getAABB, src/TriangleMesh.cpp:156-195
-        const Mesh& m = s_.meshes[s_.obj_mesh[o]];
-        const uint32_t* f = &m.vidx[3 * (size_t)s_.obj_tri[o]];
+    bool is_proxy(int o) const { return oi_ && (*oi_)[o] >= 0; }
+    // TriangleMesh::getAABB (src/TriangleMesh.cpp:156-195) / ProxyObject::getAABB
+    Box tri_aabb(int o) const {
+        if (is_proxy(o)) {
+            const float* b = s_.instances[(*oi_)[o]].box;
+            return Box{{b[0], b[1], b[2]}, {b[3], b[4], b[5]}};
+        }
+        const Mesh& m = s_.meshes[om_[o]];
+        const uint32_t* f = &m.vidx[3 * (size_t)ot_[o]];
         v3 A = m.verts[f[0]], B = m.verts[f[1]], C = m.verts[f[2]];
         return Box{{std_min(A.x, std_min(B.x, C.x)), std_min(A.y, std_min(B.y, C.y)), std_min(A.z, std_min(B.z, C.z))},
                    {std_max(A.x, std_max(B.x, C.x)), std_max(A.y, std_max(B.y, C.y)), std_max(A.z, std_max(B.z, C.z))}};
@@ -436,39 +446,43 @@ class Builder {
     int32_t new_node() {
         QNode q{};
         for (int k = 0; k < 4; k++) q.child[k] = kEmptySlot;
-        s_.nodes.push_back(q);
-        return (int32_t)s_.nodes.size() - 1;
+        nodes_.push_back(q);
+        return (int32_t)nodes_.size() - 1;
     }
     void set_box(int32_t qi, int slot, int32_t b) {
         const Box& x = bn_[b].box;
-        float* box = s_.nodes[qi].box;
+        float* box = nodes_[qi].box;
         box[0 + slot] = x.mn[0]; box[4 + slot] = x.mn[1]; box[8 + slot] = x.mn[2];
         box[12 + slot] = x.mx[0]; box[16 + slot] = x.mx[1]; box[20 + slot] = x.mx[2];
     }
-    int32_t make_leaf(int32_t b) {  // buildTriBundle, src/BVH.cpp:64-98
+    // buildTriBundle, src/BVH.cpp:64-98: a ProxyObject lane keeps a zero
+    // triangle (checkOut lane, rejected by det = 0)
+    int32_t make_leaf(int32_t b) {
         QLeaf L{};
         for (int i = 0; i < 4; i++) L.prim[i] = -1;
         for (int i = 0; i < bn_[b].count; i++) {
             int o = objs_[bn_[b].start + i];
-            const Mesh& m = s_.meshes[s_.obj_mesh[o]];
-            const uint32_t* f = &m.vidx[3 * (size_t)s_.obj_tri[o]];
+            L.prim[i] = o;
+            if (is_proxy(o)) continue;
+            const Mesh& m = s_.meshes[om_[o]];
+            const uint32_t* f = &m.vidx[3 * (size_t)ot_[o]];
             v3 A = m.verts[f[0]], B = m.verts[f[1]], C = m.verts[f[2]];
             L.t[0 + i] = A.x; L.t[4 + i] = A.y; L.t[8 + i] = A.z;
             L.t[12 + i] = B.x - A.x; L.t[16 + i] = B.y - A.y; L.t[20 + i] = B.z - A.z;
             L.t[24 + i] = C.x - A.x; L.t[28 + i] = C.y - A.y; L.t[32 + i] = C.z - A.z;
             L.prim[i] = o;
         }
-        s_.leaves.push_back(L);
-        return ~(int32_t)(s_.leaves.size() - 1);
+        leaves_.push_back(L);
+        return ~(int32_t)(leaves_.size() - 1);
     }
     // slot <- binary node b: leaf packet now, or a new 4-wide node built recursively
     void fill(int32_t qi, int slot, int32_t b, int depth) {
         if (bn_[b].leaf) {
             int32_t c = make_leaf(b);
-            s_.nodes[qi].child[slot] = c;
+            nodes_[qi].child[slot] = c;
         } else {
             int32_t c = new_node();
-            s_.nodes[qi].child[slot] = c;
+            nodes_[qi].child[slot] = c;
             qbuild(c, b, depth + 1);
         }
     }
@@ -506,10 +520,10 @@ class Builder {
         }
     }
     void collapse() {
-        s_.nodes.clear();
-        s_.leaves.clear();
-        s_.nodes.reserve(bn_.size() / 4 + 4);
-        s_.leaves.reserve((size_t)bin_leaves);
+        nodes_.clear();
+        leaves_.clear();
+        nodes_.reserve(bn_.size() / 4 + 4);
+        leaves_.reserve((size_t)bin_leaves);
         int32_t root = new_node();
         qbuild(root, 0, 1);
     }
@@ -519,7 +533,12 @@ class Builder {
         fail_ = true;
     }
 
-    Scene& s_;
+    const Scene& s_;
+    const std::vector<int32_t>& om_;
+    const std::vector<int32_t>& ot_;
+    const std::vector<int32_t>* oi_;
+    std::vector<QNode>& nodes_;
+    std::vector<QLeaf>& leaves_;
     std::vector<Box> tri_box_, pre_;
     std::vector<float> cen_obj_, cen_;
     std::vector<int> objs_, bin_ids_;
@@ -539,16 +558,32 @@ int build_qbvh(Scene& s, std::string& err) {
     auto t0 = std::chrono::steady_clock::now();
     s.obj_mesh.clear();
     s.obj_tri.clear();
-    for (size_t m = 0; m < s.meshes.size(); m++)
-        for (int32_t t = 0; t < s.meshes[m].nt(); t++) {
-            s.obj_mesh.push_back((int32_t)m);
-            s.obj_tri.push_back(t);
+    s.obj_inst.clear();
+    // world objects in add order: a world mesh's triangles (makeMeshObjs), a ProxyObject
+    for (int32_t g : s.groups) {
+        if (g >= 0) {
+            if (s.mesh_blas[g] >= 0) continue;
+            for (int32_t t = 0; t < s.meshes[g].nt(); t++) {
+                s.obj_mesh.push_back(g);
+                s.obj_tri.push_back(t);
+                s.obj_inst.push_back(-1);
+            }
+        } else {
+            s.obj_mesh.push_back(-1);
+            s.obj_tri.push_back(-1);
+            s.obj_inst.push_back(~g);
         }
+    }
     if (s.obj_mesh.empty()) {
         err = "scene has no triangles";
         return MRT_ERR_BUILD;
     }
-    Builder b(s);
+    int32_t base = (int32_t)s.obj_mesh.size();  // instance hit ids follow the world objects
+    for (Instance& I : s.instances) {
+        I.hit_base = base;
+        base += (int32_t)s.blas[I.blas].obj_mesh.size();
+    }
+    Builder b(s, s.obj_mesh, s.obj_tri, &s.obj_inst, s.nodes, s.leaves);
     int rc = b.run(err);
     if (rc != MRT_OK) return rc;
     auto t1 = std::chrono::steady_clock::now();
@@ -562,6 +597,72 @@ int build_qbvh(Scene& s, std::string& err) {
     s.built = true;
     s.dev_dirty = true;
     return MRT_OK;
+}
+
+// ProxyObject::setupMultiProxy (src/ProxyObject.cpp:149-167) + BVH::build
+int make_blas(Scene& s, const int32_t* meshes, int n_meshes, std::string& err) {
+    if (!meshes || n_meshes <= 0) { err = "no meshes"; return MRT_ERR_INVALID; }
+    Blas B;
+    for (int j = 0; j < n_meshes; j++) {
+        const int32_t m = meshes[j];
+        if (m < 0 || m >= (int32_t)s.meshes.size() || s.mesh_blas[m] >= 0 || std::count(meshes, meshes + j, m)) {
+            err = "bad mesh id, or the mesh already belongs to a BLAS";
+            return MRT_ERR_INVALID;
+        }
+        B.meshes.push_back(m);
+        for (int32_t t = s.meshes[m].nt() - 1; t >= 0; t--) {
+            B.obj_mesh.push_back(m);
+            B.obj_tri.push_back(t);
+        }
+    }
+    if (B.obj_mesh.empty()) { err = "BLAS has no triangles"; return MRT_ERR_BUILD; }
+    Builder b(s, B.obj_mesh, B.obj_tri, nullptr, B.nodes, B.leaves);
+    const int rc = b.run(err);
+    if (rc != MRT_OK) return rc;
+    const int32_t id = (int32_t)s.blas.size();
+    for (int32_t m : B.meshes) s.mesh_blas[m] = id;
+    s.blas.push_back(std::move(B));
+    s.built = false;
+    s.dev_dirty = true;
+    return id;
+}
+
+// new ProxyObject(objects, bvh, M) with its ProxyMatrix (src/ProxyObject.cpp:5-12,
+// src/ProxyMatrix.cpp:3-8) and ProxyObject::getAABB (src/ProxyObject.cpp:45-72):
+// the BLAS root box (QBVH_Node::getAABB: the union of all four slots, unused ones
+// included as zero boxes, src/BVH.cpp:107-112,416-424), corners A..F, bbMin,
+// bbMax through multiplyAndDivideByW, grown in that order.
+int add_instance(Scene& s, int32_t blas, const float* m16, std::string& err) {
+    if (!m16 || blas < 0 || blas >= (int32_t)s.blas.size()) { err = "bad BLAS id or matrix"; return MRT_ERR_INVALID; }
+    Instance I{};
+    Mat4 M;
+    memcpy(M.m, m16, sizeof M.m);
+    const Mat4 inv = inverse(M), inv_t = transpose(inverse(M));
+    memcpy(I.m, M.m, sizeof I.m);
+    memcpy(I.inv, inv.m, sizeof I.inv);
+    memcpy(I.inv_t, inv_t.m, sizeof I.inv_t);
+    I.blas = blas;
+    const QNode& r = s.blas[blas].nodes[0];
+    Box t = empty_box();
+    for (int k = 0; k < 4; k++)
+        t = merge(t, Box{{r.box[0 + k], r.box[4 + k], r.box[8 + k]}, {r.box[12 + k], r.box[16 + k], r.box[20 + k]}});
+    const v3 P[8] = {mk(t.mn[0], t.mn[1], t.mx[2]), mk(t.mn[0], t.mx[1], t.mn[2]), mk(t.mx[0], t.mn[1], t.mn[2]),
+                     mk(t.mn[0], t.mx[1], t.mx[2]), mk(t.mx[0], t.mx[1], t.mn[2]), mk(t.mx[0], t.mn[1], t.mx[2]),
+                     mk(t.mn[0], t.mn[1], t.mn[2]), mk(t.mx[0], t.mx[1], t.mx[2])};
+    Box nb = empty_box();
+    for (const v3& p : P) {
+        const v3 q = xform_point(M, p);
+        nb = merge(nb, Box{{q.x, q.y, q.z}, {q.x, q.y, q.z}});
+    }
+    for (int k = 0; k < 3; k++) {
+        I.box[k] = nb.mn[k];
+        I.box[3 + k] = nb.mx[k];
+    }
+    s.instances.push_back(I);
+    s.groups.push_back(~(int32_t)(s.instances.size() - 1));
+    s.built = false;
+    s.dev_dirty = true;
+    return (int)s.instances.size() - 1;
 }
 
 }  // namespace mrt

@@ -59,6 +59,8 @@ struct RenderParams {
     const DevMaterial* mats;
     const DevLight* lights;
     const DevDome* domes;    // dome-light tables (DevLight::dome)
+    const DevInstance* insts;  // ProxyObjects (instanced scenes)
+    int32_t n_insts, n_world;  // instances; world objects (instance hit ids start here)
     const float* env;        // environment map (nullable), env_w x env_h RGB, row 0 = top
     int32_t env_w, env_h;
     float env_exposure;
@@ -100,7 +102,13 @@ struct RenderParams {
 // against the oracle to 1e-4 relative (north_star), everything else bit-exact.
 __device__ __forceinline__ float spec_pow(float x, float e) { return (float)pow((double)x, (double)e); }
 
-template <bool POINT_ONLY, bool FAST>
+// operator*(Matrix4x4, Vector3) (src/Matrix4x4.h:693-704) on rows 0-2 of T (stride 4)
+__device__ __forceinline__ v3 xform_dir3(const float* T, v3 u) {
+    return mk(T[0] * u.x + T[1] * u.y + T[2] * u.z, T[4] * u.x + T[5] * u.y + T[6] * u.z,
+              T[8] * u.x + T[9] * u.y + T[10] * u.z);
+}
+
+template <bool POINT_ONLY, bool FAST, bool INST = false>
 struct Shader {
     const RenderParams& P;
     const Trav& T;
@@ -118,7 +126,7 @@ struct Shader {
         DRay r = make_ray(from, L);
         DHit h{tMax, 0.f, 0.f, -1};
         shadow_rays++;
-        return traverse<true, COUNT, FAST>(T, r, 0.001f, h, st);
+        return traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st);
     }
 
     // PointLight::sampleLight, src/PointLight.cpp:8-81
@@ -243,14 +251,31 @@ struct Shader {
     }
 
     // HitInfo::getAllInfos (normals), src/Ray.cpp:5-49
+    // an instance hit (id >= n_world) names instance i's BLAS object id - hit_base
     __device__ void normals(const DHit& h, v3& N, v3& geoN, uint32_t& mat) {
-        PrimShade ps = P.prims[h.prim];
+        int32_t ps_i = h.prim, inst = -1;
+        if (INST && h.prim >= P.n_world) {
+            int lo = 0, hi = P.n_insts - 1;  // the last instance with hit_base <= id
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (P.insts[mid].hit_base <= h.prim) lo = mid;
+                else hi = mid - 1;
+            }
+            inst = lo;
+            ps_i = P.insts[lo].shade_base + (h.prim - P.insts[lo].hit_base);
+        }
+        PrimShade ps = P.prims[ps_i];
         float4 A = P.verts[ps.v[0]], B = P.verts[ps.v[1]], C = P.verts[ps.v[2]];
         geoN = normalized(cross(mk(B.x - A.x, B.y - A.y, B.z - A.z), mk(C.x - A.x, C.y - A.y, C.z - A.z)), rsqT);
         float c = 1.0f - h.a - h.b;
         float4 n0 = P.normals[ps.n[0]], n1 = P.normals[ps.n[1]], n2 = P.normals[ps.n[2]];
         v3 s = add(add(scale(mk(n0.x, n0.y, n0.z), c), scale(mk(n1.x, n1.y, n1.z), h.a)), scale(mk(n2.x, n2.y, n2.z), h.b));
         N = normalized(s, rsqT);
+        if (INST && inst >= 0) {  // HitInfo::getAllInfos with m_proxy (src/Ray.cpp:27-31)
+            const float* T = P.insts[inst].inv_t;
+            geoN = normalized(xform_dir3(T, geoN), rsqT);
+            N = normalized(xform_dir3(T, N), rsqT);
+        }
         mat = ps.mat;
     }
 
@@ -479,7 +504,7 @@ __device__ __forceinline__ v3 camera_dir(const CamParams& cam, uint32_t seed, in
 
 // Kernel 1: Camera::eyeRayAdaptive + closest-hit BVH::intersect per pixel.
 // Writes the HitInfo record (t, a, b, prim) to P.hits[slot].
-template <bool COUNT, int MINW, bool FAST>
+template <bool COUNT, int MINW, bool FAST, bool INST = false>
 __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -489,6 +514,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
     TravStats st;
     uint32_t nhits = 0;
     unsigned long long wave_steps = 0;  // count mode: sum over tiles of max lane node visits
@@ -510,7 +536,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
             const CamParams& cam = P.cam[f];
             DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, P.seed + (uint32_t)f, x, y, rsqT));
             DHit h{1e12f, 0.f, 0.f, -1};
-            if (!traverse<false, COUNT, FAST>(T, r, 0.001f, h, st)) h.prim = -1;
+            if (!traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st)) h.prim = -1;
             item_pixel(P, item, lane, x, y, slot);  // recompute: keeps it out of the traversal's live set
             P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(h.prim));
             nhits += h.prim >= 0 ? 1u : 0u;  // wave-reduced in flush_stats
@@ -526,7 +552,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
 }
 
 // Kernel 2: Scene::sampleScene shading of the primary hit with shadow rays.
-template <bool COUNT, bool POINT_ONLY, bool FAST>
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST = false>
 __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -536,6 +562,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
     TravStats st;
     uint32_t shadow_total = 0;
     TileSched ts(P, wave, lane);
@@ -559,7 +586,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             const CamParams& cam = P.cam[f];
             const uint32_t seed = P.seed + (uint32_t)f;
             DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, seed, x, y, rsqT));
-            Shader<POINT_ONLY, FAST> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u, seed};
+            Shader<POINT_ONLY, FAST, INST> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u, seed};
             col = S.template shade<COUNT>(r, h);
             shadow_total += S.shadow_rays;
         } else if (P.env) {  // environment map lookup of the missed ray (src/Scene.cpp:236-239)
@@ -596,6 +623,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
     TravStats st;
     uint32_t shadow_total = 0;
     TileSched ts(P, wave, lane);
@@ -698,11 +726,12 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
 }
 
 // Batched Scene::trace: one lane per query ray.
-template <bool ANY>
+template <bool ANY, bool INST = false>
 __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DLeaf* leaves, const uint16_t* tables,
                                                     int32_t* gstack, uint32_t gstride, const float* o, const float* d,
                                                     const float* tmin, const float* tmax, size_t n, mrt_hit* out,
-                                                    unsigned long long* ctr, int fast_box) {
+                                                    unsigned long long* ctr, int fast_box,
+                                                    const DevInstance* insts) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     const int tid = threadIdx.x;
@@ -710,11 +739,12 @@ __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DL
     __syncthreads();
     const uint32_t gtid = blockIdx.x * kWG + tid;
     Trav T{nodes, fast_box != 0, false, leaves, s_tab, s_stack + tid, gstack + gtid, gstride};
+    T.inst = insts;
     TravStats st;
     for (size_t i = (size_t)blockIdx.x * kWG + tid; i < n; i += (size_t)gridDim.x * kWG) {
         DRay r = make_ray(mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]));
         DHit h{tmax[i], 0.f, 0.f, -1};
-        bool hit = traverse<ANY, false, false>(T, r, tmin[i], h, st);
+        bool hit = traverse<ANY, false, false, INST>(T, r, tmin[i], h, st);
         mrt_hit res;
         res.t = h.t; res.a = h.a; res.b = h.b; res.prim = hit ? (ANY ? 0 : h.prim) : -1;
         if (ANY && hit) res.prim = 1;  // any-hit: occluded flag only
@@ -778,6 +808,8 @@ struct DeviceState {
     DevMaterial* mats = nullptr;
     DevLight* lights = nullptr;
     DevDome* domes = nullptr;
+    DevInstance* insts = nullptr;
+    int n_insts = 0, n_world = 0;
     std::vector<void*> bufs;     // textures and dome tables (freed with the state)
     const float* env = nullptr;  // environment texture (one of bufs)
     uint16_t* tables = nullptr;
@@ -829,7 +861,7 @@ static void free_device(DeviceState* d) {
     if (d->device >= 0) (void)hipSetDevice(d->device);
     (void)hipDeviceSynchronize();   // no launch may still use the scratch below
     for (StreamCtx* c : d->ctxs) free_ctx(c);
-    void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->tables,
+    void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts, d->tables,
                     d->gamma, d->d_rgb, d->d_rgb8};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -886,43 +918,88 @@ static int ensure_device(Scene& s, int device) {
         for (auto& p : s.meshes[m].verts) V.push_back(make_float4(p.x, p.y, p.z, 1.f));
         for (auto& p : s.meshes[m].normals) N.push_back(make_float4(p.x, p.y, p.z, 0.f));
     }
-    std::vector<PrimShade> PS(s.obj_mesh.size());
-    for (size_t i = 0; i < PS.size(); i++) {
-        const Mesh& m = s.meshes[s.obj_mesh[i]];
-        size_t t = (size_t)s.obj_tri[i];
+    // PrimShade: the world objects (a ProxyObject's own slot stays zero), then each BLAS's objects
+    auto shade_rec = [&](int32_t mesh, int32_t tri) {
+        PrimShade p{};
+        if (mesh < 0) return p;
+        const Mesh& m = s.meshes[mesh];
+        const size_t t = (size_t)tri;
         for (int k = 0; k < 3; k++) {
-            PS[i].v[k] = vbase[s.obj_mesh[i]] + m.vidx[3 * t + k];
-            PS[i].n[k] = nbase[s.obj_mesh[i]] + m.nidx[3 * t + k];
+            p.v[k] = vbase[mesh] + m.vidx[3 * t + k];
+            p.n[k] = nbase[mesh] + m.nidx[3 * t + k];
         }
-        PS[i].mat = (uint32_t)m.material;
-        PS[i].pad = 0;
+        p.mat = (uint32_t)m.material;
+        return p;
+    };
+    std::vector<PrimShade> PS;
+    for (size_t i = 0; i < s.obj_mesh.size(); i++) PS.push_back(shade_rec(s.obj_mesh[i], s.obj_tri[i]));
+    std::vector<int32_t> shade_base(s.blas.size());
+    for (size_t b = 0; b < s.blas.size(); b++) {
+        shade_base[b] = (int32_t)PS.size();
+        for (size_t i = 0; i < s.blas[b].obj_mesh.size(); i++) PS.push_back(shade_rec(s.blas[b].obj_mesh[i], s.blas[b].obj_tri[i]));
     }
     std::vector<uint16_t> tab(4096);
     memcpy(tab.data(), host_rcp_table(), 4096);
     memcpy(tab.data() + 2048, host_rsqrt_table(), 4096);
     size_t total = 0;
     int rc;
-    // device child words: leaf slots carry their packet's triangle count (leaf_child)
-    if (s.leaves.size() >= (size_t(1) << 29)) { set_error("too many leaf packets"); return MRT_ERR_OVERFLOW; }
-    std::vector<QNode> DN(s.nodes);
-    for (QNode& q : DN)
-        for (int k = 0; k < 4; k++) {
-            const int32_t c = q.child[k];
-            if (c >= 0 || c == kEmptySlot) continue;
-            const QLeaf& L = s.leaves[(size_t)~c];
-            int cnt = 0;
-            for (int j = 0; j < 4; j++)
-                if (L.prim[j] >= 0) cnt = j + 1;   // zero-filled lanes below cnt are rejected by det = 0
-            q.child[k] = leaf_child((uint32_t)~c, cnt < 1 ? 1 : cnt);
+    // device node / leaf arrays: the world hierarchy, then each BLAS (indices
+    // offset).  Leaf slots carry their packet's object count and a ProxyObject
+    // bit (leaf_child); a ProxyObject lane's prim is -2 - instance.
+    size_t n_leaves = s.leaves.size();
+    for (const Blas& B : s.blas) n_leaves += B.leaves.size();
+    if (n_leaves >= (size_t(1) << 28)) { set_error("too many leaf packets"); return MRT_ERR_OVERFLOW; }
+    std::vector<QNode> DN;
+    std::vector<DLeaf> DL;
+    auto append = [&](const std::vector<QNode>& nodes, const std::vector<QLeaf>& leaves,
+                      const std::vector<int32_t>* oi) -> int32_t {
+        const int32_t nb = (int32_t)DN.size(), lb = (int32_t)DL.size();
+        auto proxy_of = [&](int32_t p) { return (oi && p >= 0 && (size_t)p < oi->size()) ? (*oi)[p] : -1; };
+        for (QNode q : nodes) {
+            for (int k = 0; k < 4; k++) {
+                const int32_t c = q.child[k];
+                if (c == kEmptySlot) continue;
+                if (c >= 0) { q.child[k] = c + nb; continue; }
+                const QLeaf& L = leaves[(size_t)~c];
+                int cnt = 0;
+                bool proxy = false;
+                for (int j = 0; j < 4; j++)
+                    if (L.prim[j] >= 0) {  // zero-filled lanes below cnt are rejected by det = 0
+                        cnt = j + 1;
+                        proxy |= proxy_of(L.prim[j]) >= 0;
+                    }
+                q.child[k] = leaf_child((uint32_t)(~c + lb), cnt < 1 ? 1 : cnt, proxy);
+            }
+            DN.push_back(q);
         }
+        for (const QLeaf& L : leaves) {
+            DLeaf D{};
+            for (int k = 0; k < 4; k++) {
+                for (int c = 0; c < 9; c++) D.tri[k][c] = L.t[4 * c + k];
+                const int32_t pi = proxy_of(L.prim[k]);
+                D.prim[k] = pi >= 0 ? -2 - pi : L.prim[k];
+            }
+            DL.push_back(D);
+        }
+        return nb;
+    };
+    append(s.nodes, s.leaves, &s.obj_inst);
+    std::vector<int32_t> blas_root(s.blas.size());
+    for (size_t b = 0; b < s.blas.size(); b++) blas_root[b] = append(s.blas[b].nodes, s.blas[b].leaves, nullptr);
     if ((rc = upload(d.nodes, DN.data(), DN.size() * sizeof(QNode), total))) return rc;
-    std::vector<DLeaf> DL(s.leaves.size());
-    for (size_t i = 0; i < DL.size(); i++) {
-        for (int k = 0; k < 4; k++) {
-            for (int c = 0; c < 9; c++) DL[i].tri[k][c] = s.leaves[i].t[4 * c + k];
-            DL[i].prim[k] = s.leaves[i].prim[k];
-        }
+    std::vector<DevInstance> DI(s.instances.size());
+    for (size_t i = 0; i < DI.size(); i++) {
+        const Instance& I = s.instances[i];
+        memcpy(DI[i].inv, I.inv, sizeof DI[i].inv);
+        memcpy(DI[i].inv_t, I.inv_t, sizeof DI[i].inv_t);  // rows 0-2
+        DI[i].root = blas_root[I.blas];
+        DI[i].hit_base = I.hit_base;
+        DI[i].shade_base = shade_base[I.blas];
+        DI[i].pad = 0;
     }
+    if ((rc = upload(d.insts, DI.data(), DI.size() * sizeof(DevInstance), total))) return rc;
+    d.n_insts = (int)DI.size();
+    d.n_world = (int)s.obj_mesh.size();
     if ((rc = upload(d.leaves, DL.data(), DL.size() * sizeof(DLeaf), total))) return rc;
     if ((rc = upload(d.prims, PS.data(), PS.size() * sizeof(PrimShade), total))) return rc;
     if ((rc = upload(d.verts, V.data(), V.size() * sizeof(float4), total))) return rc;
@@ -967,7 +1044,7 @@ static int ensure_device(Scene& s, int device) {
     if (hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) d.wall_khz = 0;
     d.grid = d.cus * kMaxBlocksPerCU;
     d.boxes_finite = true;
-    for (const QNode& q : s.nodes)
+    for (const QNode& q : DN)
         for (int k = 0; k < 24; k++) d.boxes_finite &= std::isfinite(q.box[k]);
     d.point_only = true;
     for (const DevLight& l : s.lights) d.point_only &= (l.type == MRT_POINT_LIGHT);
@@ -1005,6 +1082,9 @@ static void fill_params(const Scene& s, RenderParams& P) {
     P.nodes = d.nodes; P.leaves = d.leaves; P.prims = d.prims; P.verts = d.verts; P.normals = d.normals;
     P.mats = d.mats; P.lights = d.lights; P.tables = d.tables; P.gamma = d.gamma;
     P.domes = d.domes;
+    P.insts = d.insts;
+    P.n_insts = d.n_insts;
+    P.n_world = d.n_world;
     P.env = d.env;
     P.env_w = d.env ? s.textures[s.env_tex].W : 0;
     P.env_h = d.env ? s.textures[s.env_tex].H : 0;
@@ -1047,12 +1127,13 @@ static int blocks_per_cu(KernelFn f, size_t lds) {
     return n;
 }
 
-template <int W>
+template <int W, bool I = false>
 static KernelFn primary_fn(bool c, bool f) {
-    return c ? (f ? primary_kernel<true, W, true> : primary_kernel<true, W, false>)
-             : (f ? primary_kernel<false, W, true> : primary_kernel<false, W, false>);
+    return c ? (f ? primary_kernel<true, W, true, I> : primary_kernel<true, W, false, I>)
+             : (f ? primary_kernel<false, W, true, I> : primary_kernel<false, W, false, I>);
 }
-static KernelFn pick_primary(int w, bool c, bool f) {
+static KernelFn pick_primary(int w, bool c, bool f, bool inst) {
+    if (inst) return primary_fn<1, true>(c, f);  // instanced scenes: no occupancy bound
     switch (w) {
         case 6: return primary_fn<6>(c, f);
         case 7: return primary_fn<7>(c, f);
@@ -1072,7 +1153,9 @@ static KernelFn pick_shade1(int w, bool c, bool f) {
         default: return shade1_fn<6>(c, f);
     }
 }
-static KernelFn pick_shade(bool c, bool po, bool f) {
+static KernelFn pick_shade(bool c, bool po, bool f, bool inst) {
+    if (inst) return c ? (f ? shade_kernel<true, false, true, true> : shade_kernel<true, false, false, true>)
+                       : (f ? shade_kernel<false, false, true, true> : shade_kernel<false, false, false, true>);
     if (po) return c ? (f ? shade_kernel<true, true, true> : shade_kernel<true, true, false>)
                      : (f ? shade_kernel<false, true, true> : shade_kernel<false, true, false>);
     return c ? (f ? shade_kernel<true, false, true> : shade_kernel<true, false, false>)
@@ -1119,11 +1202,12 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     };
     HIP_OK(hipEventRecord(c.ev0, stream));
     const bool fb = P.fast_box != 0;
-    if ((rc = launch(pick_primary(g_primary_waves, count, fb)))) return rc;
+    const bool inst = d.n_insts > 0;
+    if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst)))) return rc;
     HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
-    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env;
-    if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb)))) return rc;
+    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst;
+    if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb, inst)))) return rc;
     c.last_was_render = true;
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(c.ev1, stream));
@@ -1211,6 +1295,53 @@ int mrt_scene_add_light(mrt_scene* s, const mrt_light* l) {
     return (int)s->impl.lights.size() - 1;
 }
 
+int mrt_scene_make_blas(mrt_scene* s, const int32_t* meshes, int32_t n_meshes) {
+    if (!s) { set_error("null scene"); return MRT_ERR_INVALID; }
+    std::string err;
+    const int rc = make_blas(s->impl, meshes, n_meshes, err);
+    if (rc < 0) set_error(err);
+    return rc;
+}
+
+int mrt_scene_add_instance(mrt_scene* s, int32_t blas, const float* m16) {
+    if (!s) { set_error("null scene"); return MRT_ERR_INVALID; }
+    std::string err;
+    const int rc = add_instance(s->impl, blas, m16, err);
+    if (rc < 0) set_error(err);
+    return rc;
+}
+
+int mrt_scene_blas_info(const mrt_scene* s, int32_t blas, int32_t* nodes, int32_t* leaves, int32_t* prims) {
+    if (!s || !nodes || !leaves || !prims || blas < 0 || blas >= (int32_t)s->impl.blas.size()) {
+        set_error("bad BLAS id / argument");
+        return MRT_ERR_INVALID;
+    }
+    const Blas& B = s->impl.blas[blas];
+    *nodes = (int32_t)B.nodes.size();
+    *leaves = (int32_t)B.leaves.size();
+    *prims = (int32_t)B.obj_mesh.size();
+    return MRT_OK;
+}
+
+int mrt_scene_blas_export(const mrt_scene* s, int32_t blas, float* node_boxes, int32_t* node_child, float* leaf_tris,
+                          int32_t* leaf_prims) {
+    if (!s || !node_boxes || !node_child || !leaf_tris || !leaf_prims || blas < 0 ||
+        blas >= (int32_t)s->impl.blas.size()) {
+        set_error("bad BLAS id / argument");
+        return MRT_ERR_INVALID;
+    }
+    const Blas& B = s->impl.blas[blas];
+    for (size_t i = 0; i < B.nodes.size(); i++) {
+        memcpy(node_boxes + 24 * i, B.nodes[i].box, 24 * sizeof(float));
+        memcpy(node_child + 4 * i, B.nodes[i].child, 4 * sizeof(int32_t));
+    }
+    for (size_t i = 0; i < B.leaves.size(); i++) {
+        memcpy(leaf_tris + 36 * i, B.leaves[i].t, 36 * sizeof(float));
+        memcpy(leaf_prims + 4 * i, B.leaves[i].prim, 4 * sizeof(int32_t));
+    }
+    return MRT_OK;
+}
+
 int mrt_hdr_info(const char* path, int32_t* width, int32_t* height) {
     if (!path || !width || !height) { set_error("bad argument"); return MRT_ERR_INVALID; }
     int W = 0, H = 0;
@@ -1292,7 +1423,7 @@ int mrt_scene_add_obj(mrt_scene* s, const char* path, const float* ctm16, int ma
     int rc = load_obj(path, ctm16, m, err);
     if (rc != MRT_OK) { set_error(err); return rc; }
     m.material = material;
-    s->impl.meshes.push_back(std::move(m));
+    s->impl.push_mesh(std::move(m));
     s->impl.built = false;
     return (int)s->impl.meshes.size() - 1;
 }
@@ -1307,7 +1438,7 @@ int mrt_scene_add_mesh(mrt_scene* s, const mrt_mesh* mesh, int material) {
     m.nidx.assign(mesh->nidx, mesh->nidx + 3 * (size_t)mesh->nt);
     for (size_t i = 0; i < m.vidx.size(); i++)
         if (m.vidx[i] >= (uint32_t)mesh->nv || m.nidx[i] >= (uint32_t)mesh->nn) { set_error("mesh index out of range"); return MRT_ERR_INVALID; }
-    s->impl.meshes.push_back(std::move(m));
+    s->impl.push_mesh(std::move(m));
     s->impl.built = false;
     return (int)s->impl.meshes.size() - 1;
 }
@@ -1589,12 +1720,10 @@ int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const floa
     c.last_was_render = false;
     int grid = (int)std::min<size_t>((size_t)d.grid, (n + kWG - 1) / kWG);
     HIP_OK(hipEventRecord(c.ev0, (hipStream_t)stream));
-    if (any_hit)
-        hipLaunchKernelGGL(trace_kernel<true>, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables,
-                           c.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, c.ctr, fast_box(d));
-    else
-        hipLaunchKernelGGL(trace_kernel<false>, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables,
-                           c.gstack, d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, c.ctr, fast_box(d));
+    auto kern = any_hit ? (d.n_insts ? trace_kernel<true, true> : trace_kernel<true, false>)
+                        : (d.n_insts ? trace_kernel<false, true> : trace_kernel<false, false>);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables, c.gstack,
+                       d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, c.ctr, fast_box(d), d.insts);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(c.ev1, (hipStream_t)stream));
     d.last = &c;

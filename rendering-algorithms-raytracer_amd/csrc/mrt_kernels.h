@@ -47,6 +47,7 @@ __device__ __forceinline__ DRay make_ray(v3 o, v3 d) {
 struct DHit {
     float t, a, b;
     int32_t prim;
+    int32_t inst = -1;  // ProxyObject of the hit (-1: world triangle)
 };
 
 struct Trav {
@@ -58,6 +59,7 @@ struct Trav {
     int32_t* lds;             // this lane's LDS stack column (stride kWG)
     int32_t* gstk;            // this thread's global spill column (stride gstride)
     uint32_t gstride;
+    const DevInstance* inst = nullptr;  // ProxyObjects (instanced scenes)
 };
 
 struct TravStats {
@@ -152,10 +154,43 @@ __device__ __forceinline__ int box_test_fast(const float4* bx, const DRay& r, fl
 }
 
 // Device child word of a QNode slot: >= 0 inner node; kEmptySlot; otherwise
-// ~(leaf << 2 | (count - 1)) with count = triangles in the packet (the host
-// re-encodes the canonical ~leaf on upload, see leaf_child()).
-__host__ __device__ __forceinline__ int32_t leaf_child(uint32_t leaf, int count) {
-    return ~(int32_t)((leaf << 2) | (uint32_t)(count - 1));
+// ~(leaf << 3 | proxy << 2 | (count - 1)) with count = objects in the packet and
+// proxy = the packet has ProxyObject (checkOut) lanes (the host re-encodes the
+// canonical ~leaf on upload).
+__host__ __device__ __forceinline__ int32_t leaf_child(uint32_t leaf, int count, bool proxy = false) {
+    return ~(int32_t)((leaf << 3) | (proxy ? 4u : 0u) | (uint32_t)(count - 1));
+}
+
+__device__ __forceinline__ float dp4(const float* row, float x, float y, float z, float w) {
+    const float p0 = row[0] * x, p1 = row[1] * y, p2 = row[2] * z, p3 = row[3] * w;
+    return (p0 + p1) + (p2 + p3);  // DPPS 0xFF
+}
+
+// ProxyObject::intersect (src/ProxyObject.cpp:78-82): the origin through
+// multiplyAndDivideByW (DPPS 0xFF dots, RCPSS w; o.w = 1), the direction through
+// the 4-wide dots with d.w = 0 (src/Matrix4x4.h:706-748, src/Ray.h:140-141).
+__device__ __forceinline__ DRay object_ray(const DevInstance& I, const DRay& r, const uint16_t* rcpT) {
+    const float ox = r.o[0], oy = r.o[1], oz = r.o[2], dx = r.d[0], dy = r.d[1], dz = r.d[2];
+    const float w = rcp_nr(dp4(I.inv + 12, ox, oy, oz, 1.0f), rcpT);
+    const v3 o = mk(w * dp4(I.inv, ox, oy, oz, 1.0f), w * dp4(I.inv + 4, ox, oy, oz, 1.0f),
+                    w * dp4(I.inv + 8, ox, oy, oz, 1.0f));
+    const v3 d = mk(dp4(I.inv, dx, dy, dz, 0.0f), dp4(I.inv + 4, dx, dy, dz, 0.0f), dp4(I.inv + 8, dx, dy, dz, 0.0f));
+    return make_ray(o, d);
+}
+
+template <bool ANY, bool COUNT, bool FAST, bool INST = false>
+__device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root = 0,
+                              int sp0 = 0);
+
+// One ProxyObject lane: its BLAS traversed with the object-space ray, the
+// current t as tMax, on the same stack above the caller's entries.
+template <bool ANY, bool COUNT, bool FAST>
+__device__ __forceinline__ bool proxy_hit(const Trav& c, int inst, const DRay& r, float tMin, DHit& h,
+                                          TravStats& st, int sp) {
+    const DevInstance& I = c.inst[inst];
+    const DRay ro = object_ray(I, r, c.rcpT);
+    if (FAST && ro.finite) return traverse_impl<ANY, COUNT, true, false>(c, ro, tMin, h, st, I.root, sp);
+    return traverse_impl<ANY, COUNT, false, false>(c, ro, tMin, h, st, I.root, sp);
 }
 
 // BVH::intersect, QBVH branch (src/BVH.cpp:1128-1178).  Returns hit; h.prim is
@@ -169,10 +204,15 @@ __host__ __device__ __forceinline__ int32_t leaf_child(uint32_t leaf, int count)
 // per iteration, so a wave runs max-over-lanes(triangles) iterations instead
 // of one packet loop per slot.  Same visit order and same t at every box test
 // as the reference.
-template <bool ANY, bool COUNT, bool FAST>
-__device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
-    int sp = 0;
-    int32_t cur = 0;
+//
+// INST: leaf packets with ProxyObject lanes (child-word bit 2) intersect those
+// lanes first, in lane order (intersect4, src/BVH.cpp:1305-1315), each through
+// a nested BLAS traversal (proxy_hit); root / sp0 start such a nested walk.
+template <bool ANY, bool COUNT, bool FAST, bool INST>
+__device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root,
+                              int sp0) {
+    int sp = sp0;
+    int32_t cur = root;
     bool hit = false;
     while (true) {
         // stack top read at the start of the step: the LDS latency overlaps the
@@ -241,15 +281,30 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                     const int s = __builtin_ctz((unsigned)lm);
                     lm &= lm - 1;
                     const uint32_t v = ~(uint32_t)sel4(ch, s);
-                    leaf = v >> 2;
+                    leaf = v >> 3;
                     cnt = (int)(v & 3u) + 1;
                     k = 0;
                     if (COUNT) st.leaves++;
+                    if (INST && (v & 4u)) {
+                        for (int j = 0; j < cnt; j++) {
+                            const int32_t pm = c.leaves[leaf].prim[j];
+                            if (pm > -2) continue;  // a triangle lane
+                            DHit hi{h.t, 0.f, 0.f, -1};
+                            const bool ph = proxy_hit<ANY, COUNT, FAST>(c, -2 - pm, r, tMin, hi, st, sp);
+                            if (st.overflow) return hit;
+                            if (ph) {
+                                if (ANY) return true;
+                                h.t = hi.t; h.a = hi.a; h.b = hi.b; h.prim = hi.prim; h.inst = -2 - pm;
+                                hit = true;
+                            }
+                        }
+                    }
                 }
                 float t, a, b;
                 if (tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT)) {
                     if (ANY) return true;
                     h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
+                    if (INST) h.inst = -1;
                     hit = true;
                 }
                 k++;
@@ -258,7 +313,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         if (have_next) {
             cur = nxt;
         } else {
-            if (sp == 0) break;
+            if (sp == sp0) break;
             if (sp <= kLdsStack) { cur = peek; sp--; }
             else cur = stk_pop(c, sp);
         }
@@ -332,7 +387,7 @@ __device__ bool traverse_pf(const Trav& c, const DRay& r, float tMin, DHit& h, T
                     const int s = __builtin_ctz((unsigned)lm);
                     lm &= lm - 1;
                     const uint32_t v = ~(uint32_t)sel4(ch, s);
-                    leaf = v >> 2;
+                    leaf = v >> 3;
                     cnt = (int)(v & 3u) + 1;
                     k = 0;
                     if (COUNT) st.leaves++;
@@ -354,16 +409,20 @@ __device__ bool traverse_pf(const Trav& c, const DRay& r, float tMin, DHit& h, T
 // FAST (node boxes known finite) uses the hardware min/max slab test for rays
 // whose origin and 1/d are finite; any other ray takes the exact loop.  A
 // closest hit's packed slot is resolved to the global prim id here.
-template <bool ANY, bool COUNT, bool FAST = false>
+// An instance hit's id is the instance's hit_base + its BLAS object index.
+template <bool ANY, bool COUNT, bool FAST = false, bool INST = false>
 __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
 #ifdef MRT_PREFETCH  // build variant (make variant NAME=pf EXTRA=-DMRT_PREFETCH) for A/B runs
-    const bool hit = (FAST && r.finite) ? traverse_pf<ANY, COUNT>(c, r, tMin, h, st)
-                                        : traverse_impl<ANY, COUNT, false>(c, r, tMin, h, st);
+    const bool hit = (FAST && r.finite && !INST) ? traverse_pf<ANY, COUNT>(c, r, tMin, h, st)
+                                                 : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
 #else
-    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true>(c, r, tMin, h, st)
-                                        : traverse_impl<ANY, COUNT, false>(c, r, tMin, h, st);
+    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
+                                        : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
 #endif
-    if (!ANY && hit) h.prim = c.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3];
+    if (!ANY && hit) {
+        h.prim = c.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3];
+        if (INST && h.inst >= 0) h.prim += c.inst[h.inst].hit_base;
+    }
     return hit;
 }
 

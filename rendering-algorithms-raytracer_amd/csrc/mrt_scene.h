@@ -34,6 +34,23 @@ struct DomeTables {             // DomeLight::setTexture (src/DomeLight.cpp:8-78
     float int_u = 0.f, inv_int_u = 0.f;
 };
 
+// A ProxyObject's BVH (ProxyObject::setupMultiProxy, src/ProxyObject.cpp:149-167):
+// objects are the meshes in order, each mesh's triangles last to first.
+struct Blas {
+    std::vector<int32_t> meshes;
+    std::vector<int32_t> obj_mesh, obj_tri;
+    std::vector<QNode> nodes;
+    std::vector<QLeaf> leaves;
+};
+
+// ProxyObject + ProxyMatrix (src/ProxyObject.cpp:5-12, src/ProxyMatrix.cpp:3-8)
+struct Instance {
+    float m[16], inv[16], inv_t[16];  // m_transform, m_inverse, m_invTranspose (row-major)
+    float box[6];                     // ProxyObject::getAABB: min xyz, max xyz
+    int32_t blas;
+    int32_t hit_base;                 // hit id of its BLAS object 0 (set by build_qbvh)
+};
+
 struct DeviceState;  // defined in mrt_device.hip
 
 struct Scene {
@@ -46,9 +63,23 @@ struct Scene {
     float env_exposure = 1.f;       // Scene::m_envExposure
     float bg[3] = {0.f, 0.f, 0.f};
     int num_paths = 1;
+    // world object groups in add order: mesh id (>= 0) or ~instance id
+    std::vector<int32_t> groups;
+    std::vector<int32_t> mesh_blas;   // per mesh: owning BLAS, -1 = world geometry
+    std::vector<Blas> blas;
+    std::vector<Instance> instances;
+
+    int32_t push_mesh(Mesh&& m) {
+        meshes.push_back(std::move(m));
+        mesh_blas.push_back(-1);
+        groups.push_back((int32_t)meshes.size() - 1);
+        built = false;
+        dev_dirty = true;
+        return (int32_t)meshes.size() - 1;
+    }
 
     // objects in scene order (makeMeshObjs): global prim id -> (mesh, tri)
-    std::vector<int32_t> obj_mesh, obj_tri;
+    std::vector<int32_t> obj_mesh, obj_tri, obj_inst;  // obj_inst >= 0: a ProxyObject
     // QBVH
     std::vector<QNode> nodes;
     std::vector<QLeaf> leaves;
@@ -63,6 +94,8 @@ struct Scene {
 // host_build.cpp
 int load_obj(const char* path, const float* ctm16, Mesh& out, std::string& err);
 int build_qbvh(Scene& s, std::string& err);
+int make_blas(Scene& s, const int32_t* meshes, int n_meshes, std::string& err);
+int add_instance(Scene& s, int32_t blas, const float* m16, std::string& err);
 // host_texture.cpp
 int load_hdr(const char* path, int& W, int& H, std::vector<float>* rgb, std::string& err);
 int build_dome(const Texture& t, DomeTables& d, std::string& err);

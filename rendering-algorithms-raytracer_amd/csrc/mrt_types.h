@@ -33,6 +33,17 @@ static_assert(sizeof(DLeaf) == 160, "DLeaf must be 160 B");
 
 static constexpr int32_t kEmptySlot = (int32_t)0x80000000u;
 
+// A ProxyObject on the device (src/ProxyObject.cpp:76-95, src/Ray.cpp:27-31).
+struct alignas(16) DevInstance {
+    float inv[16];       // ProxyMatrix::m_inverse, row-major: rays into object space
+    float inv_t[12];     // m_invTranspose rows 0-2 (4 floats each): normals back to world space
+    int32_t root;        // the BLAS root in the scene's node array
+    int32_t hit_base;    // hit id of BLAS object 0
+    int32_t shade_base;  // PrimShade index of BLAS object 0
+    int32_t pad;
+};
+static_assert(sizeof(DevInstance) == 128, "DevInstance is 128 B");
+
 // Per-triangle shading record: global vertex / normal indices + material.
 struct alignas(16) PrimShade {
     uint32_t v[3];

@@ -27,7 +27,7 @@ from . import _lib
 from ._lib import MRTError, check, f3
 
 __all__ = ["Vector3", "Matrix4x4", "TriangleMesh", "Lambert", "Blinn", "PointLight", "RectangleLight",
-           "DomeLight", "RawImage", "Texture",
+           "DomeLight", "RawImage", "Texture", "Objects", "BVH", "ProxyObject",
            "Camera", "Image", "Scene", "Ray", "HitInfo", "makeMeshObjs", "MRTError", "lib", "device_count",
            "rcp_nr", "rsqrt_nr"]
 
@@ -301,6 +301,39 @@ def makeMeshObjs(scene: "Scene", mesh: TriangleMesh, material):
     scene.addMesh(mesh, material)
 
 
+class Objects(list):
+    """Objects (std::vector<Object*>) of a proxy: (mesh, material) pairs here."""
+
+
+class BVH:
+    """A ProxyObject's BVH (src/BVH.h:113-154); built in libmrt at Scene.preCalc()."""
+
+    def __init__(self):
+        self.objects = None
+
+
+class ProxyObject:
+    """ProxyObject(objects, bvh, Matrix4x4) (src/ProxyObject.h, src/ProxyObject.cpp:5-12):
+    one instance of a shared BVH under a transform.  setupProxy / setupMultiProxy
+    fill the Objects and BVH as the reference's static helpers do
+    (src/ProxyObject.cpp:131-167); Scene.addObject adds the instance."""
+
+    def __init__(self, objects, bvh, t=None):
+        self.objects, self.bvh = objects, bvh
+        self.matrix = (t if t is not None else Matrix4x4()).m.copy()
+
+    @staticmethod
+    def setupProxy(mesh, mat, objects, bvh):
+        objects.append((mesh, mat))
+        bvh.objects = objects
+
+    @staticmethod
+    def setupMultiProxy(meshes, numObjs, mats, objects, bvh):
+        for j in range(numObjs):
+            objects.append((meshes[j], mats[j]))
+        bvh.objects = objects
+
+
 class Scene:
     """Scene (src/Scene.h).  Objects are whole meshes here; object ids inside a
     HitInfo are global triangle indices in insertion order."""
@@ -318,6 +351,7 @@ class Scene:
 
     # -- construction (src/Scene.h:17-28)
     def addMesh(self, mesh, material): self._meshes.append((mesh, material))
+    def addObject(self, proxy): self._meshes.append((proxy, None))   # Scene::addObject (a ProxyObject)
     def addLight(self, light): self._lights.append(light)
     def setBGColor(self, c): self.bg = Vector3(c)
     def setNumPaths(self, p): self.m_numPaths = int(p)
@@ -345,20 +379,33 @@ class Scene:
             L.mrt_scene_destroy(self._h)
         self._h = L.mrt_scene_create()
         mats = {}
-        for mesh, mat in self._meshes:
+
+        def add_mesh(mesh, mat):
             if id(mat) not in mats:
                 m = mat._c()
                 mats[id(mat)] = check(L.mrt_scene_add_material(self._h, C.byref(m)), "add_material")
             mid = mats[id(mat)]
             if mesh.path is not None:
                 ctm = mesh.ctm.ctypes.data_as(C.POINTER(C.c_float)) if mesh.ctm is not None else None
-                check(L.mrt_scene_add_obj(self._h, mesh.path.encode(), ctm, mid), f"load {mesh.path}")
-            else:
-                v, n, vi, ni = mesh.verts, mesh.normals, mesh.vidx, mesh.nidx
-                mm = _lib.mrt_mesh(v.ctypes.data_as(C.POINTER(C.c_float)), n.ctypes.data_as(C.POINTER(C.c_float)),
-                                   vi.ctypes.data_as(C.POINTER(C.c_uint32)), ni.ctypes.data_as(C.POINTER(C.c_uint32)),
-                                   len(v), len(n), len(vi))
-                check(L.mrt_scene_add_mesh(self._h, C.byref(mm), mid), "add_mesh")
+                return check(L.mrt_scene_add_obj(self._h, mesh.path.encode(), ctm, mid), f"load {mesh.path}")
+            v, n, vi, ni = mesh.verts, mesh.normals, mesh.vidx, mesh.nidx
+            mm = _lib.mrt_mesh(v.ctypes.data_as(C.POINTER(C.c_float)), n.ctypes.data_as(C.POINTER(C.c_float)),
+                               vi.ctypes.data_as(C.POINTER(C.c_uint32)), ni.ctypes.data_as(C.POINTER(C.c_uint32)),
+                               len(v), len(n), len(vi))
+            return check(L.mrt_scene_add_mesh(self._h, C.byref(mm), mid), "add_mesh")
+
+        blas = {}   # BVH object -> BLAS id (built once, shared by its instances)
+        self.blas_ids = blas
+        for item, mat in self._meshes:
+            if not isinstance(item, ProxyObject):
+                add_mesh(item, mat)
+                continue
+            key = id(item.bvh)
+            if key not in blas:
+                ids = (C.c_int32 * len(item.bvh.objects))(*[add_mesh(m, mt) for m, mt in item.bvh.objects])
+                blas[key] = check(L.mrt_scene_make_blas(self._h, ids, len(ids)), "BLAS build")
+            m16 = np.ascontiguousarray(item.matrix, np.float32).reshape(16)
+            check(L.mrt_scene_add_instance(self._h, blas[key], m16.ctypes.data_as(C.POINTER(C.c_float))), "instance")
         tex_ids = {}
 
         def tex_id(t):
@@ -412,6 +459,19 @@ class Scene:
         check(L.mrt_scene_dome_export(self.handle, int(light),
                                       *[out[k].ctypes.data_as(C.POINTER(C.c_float)) for k in shapes]), "dome_export")
         return out
+
+    def blas_export(self, blas: int):
+        L = lib()
+        n, l, p = C.c_int32(), C.c_int32(), C.c_int32()
+        check(L.mrt_scene_blas_info(self.handle, int(blas), C.byref(n), C.byref(l), C.byref(p)), "blas_info")
+        nb = np.zeros((n.value, 24), np.float32)
+        nc = np.zeros((n.value, 4), np.int32)
+        lt = np.zeros((l.value, 36), np.float32)
+        lp = np.zeros((l.value, 4), np.int32)
+        check(L.mrt_scene_blas_export(self.handle, int(blas), nb.ctypes.data_as(C.POINTER(C.c_float)),
+                                      nc.ctypes.data_as(C.POINTER(C.c_int32)), lt.ctypes.data_as(C.POINTER(C.c_float)),
+                                      lp.ctypes.data_as(C.POINTER(C.c_int32))), "blas_export")
+        return nb, nc, lt, lp
 
     def bvh_export(self):
         info = self.bvh_info

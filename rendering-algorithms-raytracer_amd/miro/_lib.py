@@ -22,7 +22,8 @@ EXPORTS = [
     "mrt_render_frame_async", "mrt_trace", "mrt_trace_async", "mrt_scene_last_stats", "mrt_rcp_nr",
     "mrt_rsqrt_nr", "mrt_set_tuning", "mrt_render_batch_async", "mrt_unpack_batch_async",
     "mrt_debug_wave_log", "mrt_device_wall_clock_khz", "mrt_hdr_info", "mrt_hdr_load", "mrt_scene_add_texture",
-    "mrt_scene_set_env_map", "mrt_scene_dome_info", "mrt_scene_dome_export",
+    "mrt_scene_set_env_map", "mrt_scene_dome_info", "mrt_scene_dome_export", "mrt_scene_make_blas",
+    "mrt_scene_add_instance", "mrt_scene_blas_info", "mrt_scene_blas_export",
 ]
 
 
@@ -139,6 +140,10 @@ def load():
     L.mrt_scene_set_env_map.argtypes = [C.c_void_p, C.c_int32, C.c_float]
     L.mrt_scene_dome_info.argtypes = [C.c_void_p, C.c_int32, _ip, _ip]
     L.mrt_scene_dome_export.argtypes = [C.c_void_p, C.c_int32] + [_fp] * 9
+    L.mrt_scene_make_blas.argtypes = [C.c_void_p, _ip, C.c_int32]
+    L.mrt_scene_add_instance.argtypes = [C.c_void_p, C.c_int32, _fp]
+    L.mrt_scene_blas_info.argtypes = [C.c_void_p, C.c_int32, _ip, _ip, _ip]
+    L.mrt_scene_blas_export.argtypes = [C.c_void_p, C.c_int32, _fp, _ip, _fp, _ip]
     L.mrt_rcp_nr.argtypes = [C.c_float]
     L.mrt_rcp_nr.restype = C.c_float
     L.mrt_rsqrt_nr.argtypes = [C.c_float]
