@@ -89,8 +89,13 @@ def cpu_baseline(cfg_key, seconds):
     m = s.add_material(mat["kind"], kd=mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0))
     if cfg["mesh"] == "sponza":
         s.add_obj(scenes.sponza_obj(), m)
-    elif cfg["mesh"] == "bunny":
-        s.add_obj(scenes.bunny_obj(), m)
+    elif cfg["mesh"] in ("bunny", "instances"):
+        if cfg["mesh"] == "bunny":
+            s.add_obj(scenes.bunny_obj(), m)
+        else:   # two ProxyObject BVHs, instances alternating (as scenes.build_config)
+            blas = [s.make_blas([s.add_obj(p, m)]) for p in (scenes.dragon_obj(), scenes.buddha_obj())]
+            for i, M in enumerate(scenes.instance_transforms(**cfg["instances"])):
+                s.add_instance(blas[i % 2], M)
         s.add_mesh([(-100, 0, -100), (0, 0, 100), (100, 0, -100)], [(0, 1, 0)] * 3, [(0, 1, 2)], [(0, 1, 2)], m)
     else:
         import numpy as np
@@ -289,8 +294,10 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": ("synthetic (deterministic %s stand-in, %d tris; %s.obj is not in the reference snapshot%s)"
-                 % ({"sponza": "Sponza", "bunny": "bunny"}.get(cfg["mesh"], cfg["mesh"]), scene.bvh_info["prims"],
-                    cfg["mesh"], "; procedural lat-long sky for the dome / environment map" if cfg.get("env") else "")),
+                 % ({"sponza": "Sponza", "bunny": "bunny", "instances": "dragon_2 / buddha_smooth"}.get(
+                     cfg["mesh"], cfg["mesh"]), scene.bvh_info["prims"],
+                    {"instances": "dragon_2.obj / buddha_smooth"}.get(cfg["mesh"], cfg["mesh"]),
+                    "; procedural lat-long sky for the dome / environment map" if cfg.get("env") else "")),
         "config": {"workload": cfg["name"], "config": args.config, "width": W, "height": H, "spp": 1,
                    "frames_per_step": n_frames, "rays_per_step": rays_per_step, "shadow_rays": shadow_total,
                    "qbvh_nodes": scene.bvh_info["nodes"], "qbvh_leaves": scene.bvh_info["leaves"],

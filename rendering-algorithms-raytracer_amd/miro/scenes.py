@@ -214,6 +214,81 @@ def bunny_standin(nu=250, nv=140, radius=3.0):
     return V, F, N
 
 
+def _smooth_normals(V, F):
+    e1 = V[F[:, 1]] - V[F[:, 0]]
+    e2 = V[F[:, 2]] - V[F[:, 0]]
+    fn = np.cross(e1, e2)
+    N = np.zeros_like(V)
+    for k in range(3):
+        np.add.at(N, F[:, k], fn)
+    return N / np.linalg.norm(N, axis=1, keepdims=True)
+
+
+def _tube(center, radius, n_ring):
+    """Closed tube around a closed polyline `center` (n, 3) with per-sample radius."""
+    n = len(center)
+    t = np.roll(center, -1, 0) - np.roll(center, 1, 0)
+    t /= np.linalg.norm(t, axis=1, keepdims=True)
+    a = np.cross(t, np.array([0.0, 1.0, 0.3]))
+    a /= np.linalg.norm(a, axis=1, keepdims=True)
+    b = np.cross(t, a)
+    ang = np.linspace(0, 2 * np.pi, n_ring, endpoint=False)
+    V = (center[:, None, :] + radius[..., None] * (np.cos(ang)[None, :, None] * a[:, None, :] +
+                                                   np.sin(ang)[None, :, None] * b[:, None, :])).reshape(-1, 3)
+    i = np.arange(n)[:, None]
+    j = np.arange(n_ring)[None, :]
+    v00, v01 = i * n_ring + j, i * n_ring + (j + 1) % n_ring
+    v10, v11 = ((i + 1) % n) * n_ring + j, ((i + 1) % n) * n_ring + (j + 1) % n_ring
+    F = np.concatenate([np.stack([v00, v10, v11], -1).reshape(-1, 3), np.stack([v00, v11, v01], -1).reshape(-1, 3)])
+    return V, F
+
+
+def dragon_standin(n_len=800, n_ring=64):
+    """Seeded (2,3) torus-knot tube with a bumpy, tapering radius standing in for
+    dragon_2.obj (~102 k tris, smooth normals), about 2 units across, resting on y = 0."""
+    u = np.linspace(0, 2 * np.pi, n_len, endpoint=False)
+    r = 0.6 + 0.25 * np.cos(3 * u)
+    c = np.stack([r * np.cos(2 * u), 0.25 * np.sin(3 * u), r * np.sin(2 * u)], -1) * 1.2
+    rng = np.random.default_rng(2002)
+    k = rng.uniform(3, 9, 4)
+    ph = rng.uniform(0, 2 * np.pi, 4)
+    rad = 0.16 + 0.05 * np.sin(u * 2 + 0.5) + sum(0.012 * np.sin(k[i] * u * 3 + ph[i]) for i in range(4))
+    rad = np.broadcast_to(rad[:, None], (n_len, n_ring))
+    V, F = _tube(c, rad, n_ring)
+    V[:, 1] -= V[:, 1].min() - 0.01
+    N = _smooth_normals(V, F)
+    return _jitter(V, 2002, 1e-4), F, N
+
+
+def buddha_standin(nu=500, nv=250):
+    """Seeded seated-figure stand-in for buddha_smooth.obj: a displaced,
+    vertically stretched sphere with a narrower upper half (~248 k tris,
+    smooth normals), about 1.6 units wide and 2.4 tall, resting on y = 0."""
+    V, F, _ = bunny_standin(nu, nv, radius=1.0)
+    y = V[:, 1] / V[:, 1].max()
+    squeeze = 0.8 - 0.25 * np.clip(y - 0.45, 0.0, 1.0) + 0.1 * np.exp(-((y - 0.85) / 0.08) ** 2)
+    V = V * np.stack([squeeze, np.full_like(y, 1.2), squeeze], -1)
+    V[:, 1] -= V[:, 1].min() - 0.01
+    N = _smooth_normals(V, F)
+    return _jitter(V, 1993, 1e-4), F, N
+
+
+def instance_transforms(n=64, grid=8, spacing=3.2, seed=64):
+    """Row-major 4x4 ProxyObject transforms of config C5: an n = grid x grid
+    layout, seeded rotation about y, uniform scale 0.8-1.2 and jitter."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        gx, gz = i % grid, i // grid
+        a = rng.uniform(0, 2 * np.pi)
+        s = rng.uniform(0.8, 1.2)
+        tx = (gx - (grid - 1) / 2) * spacing + rng.uniform(-0.4, 0.4)
+        tz = -(gz - (grid - 1) / 2) * spacing + rng.uniform(-0.4, 0.4)
+        c, sn = np.cos(a), np.sin(a)
+        out.append(np.array([[c * s, 0, sn * s, tx], [0, s, 0, 0], [-sn * s, 0, c * s, tz], [0, 0, 0, 1]], np.float32))
+    return out
+
+
 def _cached(name, builder):
     key = hashlib.sha1(f"{name}-{SCENE_VERSION}".encode()).hexdigest()[:10]
     path = os.path.join(_cache_dir(), f"{name}-{key}.obj")
@@ -232,6 +307,14 @@ def sponza_obj():
 
 def bunny_obj():
     return _cached("bunny_standin", bunny_standin)
+
+
+def dragon_obj():
+    return _cached("dragon_standin", dragon_standin)
+
+
+def buddha_obj():
+    return _cached("buddha_standin", buddha_standin)
 
 
 def sky_rgb(W=512, H=256):
@@ -287,6 +370,16 @@ CONFIGS = {
                             power=1.5, samples=1, noise=0.001)],
                material=dict(kind="blinn", kd=(1, 1, 1), specExp=8.0, specAmt=0.25), bg=(0.0, 0.0, 0.2),
                mesh="sponza", num_paths=16),
+    # C5: dragon + buddha stand-ins instanced 64x via ProxyObject (two BLASes,
+    # alternating, seeded transforms) on a floor triangle, 3840x2160, DomeLight (power
+    # 0.15, 6 samples, src/main.cpp:157-165) over the procedural sky, the same map
+    # as environment on missed rays; Blinn with a specular lobe
+    "C5": dict(name="dragon + buddha stand-ins instanced 64x (ProxyObject) 3840x2160, DomeLight 6 samples + env map",
+               W=3840, H=2160, camera=dict(eye=(0.0, 10.0, 27.0), lookAt=(0.0, 0.5, 0.0), up=(0, 1, 0), fov=45.0),
+               lights=[dict(type="dome", sky=(512, 256), power=0.15, samples=6, noise=0.001)],
+               env=dict(sky=(512, 256), exposure=1.0),
+               material=dict(kind="blinn", kd=(0.8, 0.8, 0.8), specExp=20.0, specAmt=0.3), bg=(0.0, 0.0, 0.2),
+               mesh="instances", instances=dict(n=64, grid=8, spacing=3.2, seed=64)),
     # D1: image-based lighting on the C2 bunny stand-in + floor: DomeLight (power
     # 0.15, 6 samples, as src/main.cpp:157-165) over the synthetic sky, the same map
     # as environment on missed primary rays; Blinn with a specular lobe
@@ -331,10 +424,22 @@ def build_config(key, device=0):
         npz = os.environ.get("MRT_CORNELL_NPZ", os.path.join(root, "tests", "golden", "cornell_box_mesh.npz"))
         f = np.load(npz)
         mesh.setArrays(f["verts"], f["normals"], f["vidx"], f["nidx"])
-    else:
+    elif cfg["mesh"] in ("sponza", "bunny"):
         mesh.load(sponza_obj() if cfg["mesh"] == "sponza" else bunny_obj())
-    miro.makeMeshObjs(scene, mesh, material)
-    if cfg["mesh"] == "bunny":  # floor triangle, src/assignment2.h:110-124
+    if cfg["mesh"] != "instances":
+        miro.makeMeshObjs(scene, mesh, material)
+    else:  # two ProxyObject BVHs, 64 instances alternating (src/main.cpp proxy scenes)
+        protos = []
+        for path in (dragon_obj(), buddha_obj()):
+            tm = miro.TriangleMesh()
+            tm.load(path)
+            objs, bvh = miro.Objects(), miro.BVH()
+            miro.ProxyObject.setupProxy(tm, material, objs, bvh)
+            protos.append((objs, bvh))
+        for i, M in enumerate(instance_transforms(**cfg["instances"])):
+            objs, bvh = protos[i % 2]
+            scene.addObject(miro.ProxyObject(objs, bvh, miro.Matrix4x4(M)))
+    if cfg["mesh"] in ("bunny", "instances"):  # floor triangle, src/assignment2.h:110-124
         fl = miro.TriangleMesh()
         fl.createSingleTriangle()
         fl.setV1((-100, 0, -100)); fl.setV2((0, 0, 100)); fl.setV3((100, 0, -100))

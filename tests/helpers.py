@@ -16,7 +16,7 @@ def fixture_mesh(name):
     return f["verts"], f["normals"], f["vidx"], f["nidx"]
 
 
-def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1):
+def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1, instances=None):
     """Build (miro.Scene, OracleScene, camera dict) for a config dict."""
     lights = cfg["lights"] if lights is None else lights
     mat = cfg["material"]
@@ -35,6 +35,19 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
         tm.load(obj)
         miro.makeMeshObjs(P, tm, pm)
         O_.add_obj(obj, om)
+    if instances:  # ((obj path, ...) per BLAS, [(blas index, 4x4), ...]) -- ProxyObjects
+        paths, placed = instances
+        protos, oblas = [], []
+        for path in paths:
+            tm = miro.TriangleMesh()
+            tm.load(path)
+            objs, bvh = miro.Objects(), miro.BVH()
+            miro.ProxyObject.setupProxy(tm, pm, objs, bvh)
+            protos.append((objs, bvh))
+            oblas.append(O_.make_blas([O_.add_obj(path, om)]))
+        for b, M in placed:
+            P.addObject(miro.ProxyObject(*protos[b], miro.Matrix4x4(M)))
+            O_.add_instance(oblas[b], M)
     if floor:
         fl = miro.TriangleMesh()
         fl.createSingleTriangle()
@@ -98,6 +111,9 @@ def config_scene(key, **kw):
         return scene_pair(cfg, meshes=[fixture_mesh("cornell_box")], **kw)
     if cfg["mesh"] == "bunny":
         return scene_pair(cfg, obj=scenes.bunny_obj(), floor=True, **kw)
+    if cfg["mesh"] == "instances":
+        placed = [(i % 2, M) for i, M in enumerate(scenes.instance_transforms(**cfg["instances"]))]
+        return scene_pair(cfg, floor=True, instances=((scenes.dragon_obj(), scenes.buddha_obj()), placed), **kw)
     return scene_pair(cfg, obj=scenes.sponza_obj(), **kw)
 
 

@@ -343,3 +343,17 @@ def test_dome_light_batch_equals_frame():
                                     P.handle, stream) == 0
     torch.cuda.synchronize()
     assert np.array_equal(bits(frame.cpu().numpy().reshape(64, 64, 3)), bits(img.rgb))
+
+
+def test_c5_instanced_dome_matches_oracle():
+    """C5 (64 ProxyObjects of two BLASes + floor, DomeLight 6 samples, env map) at a
+    small size: hit ids (instance encoding) and shadow-ray counts exact, float RGB
+    within 1e-4 relative (double atan2 / acos / pow)."""
+    P, Osc, cam = config_scene("C5")
+    img, hits = render(P, cam, 96, 54)
+    ref = Osc.render(cam, 96, 54, threads=8)
+    assert np.array_equal(hits["prim"], ref["hits"]["prim"])
+    assert (ref["hits"]["prim"] >= P.bvh_info["prims"]).sum() > 500   # instance hits
+    assert P.last_stats["shadow_rays"] == ref["shadow_rays"] > 0
+    exact = assert_close_rgb(img.rgb, ref["rgb"])
+    assert exact > 0.99, exact
