@@ -66,14 +66,21 @@ def _pixels_in_frame(ids, bpf, bx, W, H):
     return n
 
 
-def kernel_bytes(st, px, hits, float_out=True):
+def kernel_bytes(st, px, hits, float_out=True, wavefront=False):
     """Algorithmic bytes per launch: node/leaf visits x
-    their sizes + per-pixel ray I/O + per-hit shading gathers."""
+    their sizes + per-pixel ray I/O + per-hit shading gathers.  With the
+    wavefront shadow pass each shadow ray is also written (32 B), read back
+    (32 B) and answered (1 B write + 1 B read), the hit record and the shading
+    gathers are read twice (kernels 2a and 2c) and each pixel's ray count once."""
     pn, pl = st["primary_node_visits"], st["primary_leaf_visits"]
     sn, sl = st["node_visits"] - pn, st["leaf_visits"] - pl
     primary = pn * NODE_B + pl * LEAF_B + px * 16                 # write the 16-B hit record
     # read the hit record, write float RGB + RGB8; per hit: PrimShade + 3 vertices + 3 normals
-    shade = sn * NODE_B + sl * LEAF_B + px * (16 + (12 if float_out else 0) + 3) + hits * (32 + 3 * 16 + 3 * 16)
+    gathers = 2 if wavefront else 1
+    shade = (sn * NODE_B + sl * LEAF_B + px * (16 * gathers + (12 if float_out else 0) + 3)
+             + hits * (32 + 3 * 16 + 3 * 16) * gathers)
+    if wavefront:
+        shade += st["shadow_rays"] * (32 + 32 + 1 + 1) + px * 2
     return primary, shade
 
 
@@ -267,14 +274,15 @@ def main():
     value = rays_per_step * args.steps / elapsed / 1e6
     px_mine = W * H if use_frame_path else _pixels_in_frame(sorted(set(mine)), bpf, bx, W, H)
     hits_mine = hits_px
-    b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=use_frame_path)
-    pm, sm = float(np.median(prim_ms)), float(np.median(shade_ms))
     # the specialised kernel runs for one point light, one path and no environment map
     one_light = (len(cfg["lights"]) == 1 and cfg["lights"][0]["type"] == "point" and cfg.get("num_paths", 1) == 1
                  and not cfg.get("env"))
-    shade_name = "shade1_kernel" if one_light else "shade_kernel"
+    b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=use_frame_path, wavefront=not one_light)
+    pm, sm = float(np.median(prim_ms)), float(np.median(shade_ms))
+    shade_name = ("shade1_kernel (shade + any-hit shadow rays)" if one_light else
+                  "shade pass (shade_kernel<gen> + shadow_kernel any-hit + shade_kernel<resolve>)")
     if sm >= pm:
-        dom, dom_ms, dom_b = shade_name + " (shade + any-hit shadow rays)", sm, b_shade
+        dom, dom_ms, dom_b = shade_name, sm, b_shade
     else:
         dom, dom_ms, dom_b = "primary_kernel (camera rays, closest hit)", pm, b_prim
     achieved = dom_b / (dom_ms * 1e-3) / 1e9

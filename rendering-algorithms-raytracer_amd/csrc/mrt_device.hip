@@ -48,7 +48,15 @@ static constexpr int kMaxBlocksPerCU = 8;
 static constexpr int kLogTiles = 28;
 static constexpr int kLogWords = 4 + 2 * kLogTiles;  // 256-thread blocks: 8 waves per SIMD at most
 // counter block: CTR_N u64 statistics, then two launches x 8 tile counters x 128 B
-static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 2 * 8 * 128;
+static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 3 * 8 * 128;
+// Shadow rays of the general shading path, wavefront style (ShadowMode): kernel
+// 2a runs the shading code and writes every shadow ray to its slot, kernel 2b
+// traces all of them any-hit (few registers, full occupancy), kernel 2c runs the
+// same shading code again with the occlusion bits.  Same rays, same order, same
+// arithmetic as the fused kernel, which keeps the whole shading state live
+// across each traversal.
+enum ShadowMode { kFused = 0, kGen = 1, kResolve = 2 };
+static constexpr int kMaxWaveShadow = 64;  // rays per pixel beyond this use the fused kernel
 
 struct RenderParams {
     const QNode* nodes;
@@ -62,6 +70,11 @@ struct RenderParams {
     const DevInstance* insts;  // ProxyObjects (instanced scenes)
     int32_t n_insts, n_world;  // instances; world objects (instance hit ids start here)
     const float* env;        // environment map (nullable), env_w x env_h RGB, row 0 = top
+    float4* ray_o;           // wavefront shadow rays: slot * max_shadow + j -> origin, tMax
+    float4* ray_d;           //   direction
+    uint8_t* occl;           //   1 = occluded (kernel 2b)
+    uint8_t* nrays;          //   rays of each output slot (kernel 2a)
+    int32_t max_shadow;      //   rays per pixel at most (num_paths x light samples)
     int32_t env_w, env_h;
     float env_exposure;
     const uint16_t* tables;  // rcp[2048] | rsqrt[2048]
@@ -108,7 +121,7 @@ __device__ __forceinline__ v3 xform_dir3(const float* T, v3 u) {
               T[8] * u.x + T[9] * u.y + T[10] * u.z);
 }
 
-template <bool POINT_ONLY, bool FAST, bool INST = false>
+template <bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused>
 struct Shader {
     const RenderParams& P;
     const Trav& T;
@@ -118,15 +131,26 @@ struct Shader {
     uint32_t pixel, dim;
     uint32_t shadow_rays;
     uint32_t seed;
+    size_t slot0;            // wavefront modes: this pixel's first ray slot
+    uint32_t nslot;          //   rays so far
 
     __device__ float next_rand() { return rng(pixel, 0, dim++, seed); }
 
     template <bool COUNT>
     __device__ bool occluded(v3 from, v3 L, float tMax) {
-        DRay r = make_ray(from, L);
-        DHit h{tMax, 0.f, 0.f, -1};
         shadow_rays++;
-        return traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st);
+        if constexpr (MODE == kGen) {  // no shading result depends on the answer but the final sums
+            const size_t s = slot0 + nslot++;
+            P.ray_o[s] = make_float4(from.x, from.y, from.z, tMax);
+            P.ray_d[s] = make_float4(L.x, L.y, L.z, 0.f);
+            return false;
+        } else if constexpr (MODE == kResolve) {
+            return P.occl[slot0 + nslot++] != 0;
+        } else {
+            DRay r = make_ray(from, L);
+            DHit h{tMax, 0.f, 0.f, -1};
+            return traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st);
+        }
     }
 
     // PointLight::sampleLight, src/PointLight.cpp:8-81
@@ -552,7 +576,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
 }
 
 // Kernel 2: Scene::sampleScene shading of the primary hit with shadow rays.
-template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST = false>
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused>
 __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -577,7 +601,10 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
         ntiles++;
         int x, y;
         size_t slot;
-        if (!item_pixel(P, item, lane, x, y, slot)) continue;
+        if (!item_pixel(P, item, lane, x, y, slot)) {
+            if (MODE == kGen && P.mode != 0) P.nrays[slot] = 0;  // bucket slot outside the frame
+            continue;
+        }
         float4 hv = P.hits[slot];
         DHit h{hv.x, hv.y, hv.z, __float_as_int(hv.w)};
         v3 col;
@@ -586,9 +613,14 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             const CamParams& cam = P.cam[f];
             const uint32_t seed = P.seed + (uint32_t)f;
             DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, seed, x, y, rsqT));
-            Shader<POINT_ONLY, FAST, INST> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u, seed};
+            Shader<POINT_ONLY, FAST, INST, MODE> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u, seed,
+                                                   slot * (size_t)P.max_shadow, 0u};
             col = S.template shade<COUNT>(r, h);
             shadow_total += S.shadow_rays;
+            if (MODE == kGen) P.nrays[slot] = (uint8_t)S.nslot;
+        } else if (MODE == kGen) {
+            P.nrays[slot] = 0;
+            continue;
         } else if (P.env) {  // environment map lookup of the missed ray (src/Scene.cpp:236-239)
             const int f = item_frame(P, item);
             const v3 d = camera_dir(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
@@ -596,6 +628,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
         } else {
             col = mk(P.bg[0], P.bg[1], P.bg[2]);
         }
+        if (MODE == kGen) continue;
         if (P.out_rgb) {
             float* o = P.out_rgb + 3 * slot;
             o[0] = col.x; o[1] = col.y; o[2] = col.z;
@@ -605,7 +638,43 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
         }
     }
-    flush_stats<COUNT>(P, st, shadow_total, lane, t0, ntiles);
+    flush_stats<COUNT>(P, st, MODE == kResolve ? 0u : shadow_total, lane, t0, ntiles);
+}
+
+// Kernel 2b: every wavefront shadow ray of the frame, one lane each, any-hit
+// (the occlusion answer of Shader::occluded).  Slots past a pixel's ray count
+// are skipped.
+template <bool COUNT, bool FAST, bool INST>
+__global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_rays) {
+    __shared__ uint16_t s_tab[2048];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    load_tables(P.tables, s_tab, 1024);
+    const int tid = threadIdx.x, lane = tid & 63;
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, s_tab, s_stack + tid,
+           P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
+    TravStats st;
+    const size_t m = (size_t)P.max_shadow;
+    for (size_t e = (size_t)blockIdx.x * kWG + tid; e < n_rays; e += (size_t)gridDim.x * kWG) {
+        const size_t pslot = e / m;
+        if (e - pslot * m >= (size_t)P.nrays[pslot]) continue;
+        const float4 o = P.ray_o[e], d = P.ray_d[e];
+        const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
+        DHit h{o.w, 0.f, 0.f, -1};
+        P.occl[e] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
+    }
+    if (COUNT) {
+        unsigned long long nv = st.nodes, lv = st.leaves;
+        for (int off = 32; off > 0; off >>= 1) {
+            nv += __shfl_down(nv, off);
+            lv += __shfl_down(lv, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&P.ctr[CTR_NODES], nv);
+            atomicAdd(&P.ctr[CTR_LEAVES], lv);
+        }
+    }
+    if (st.overflow) atomicOr(&P.ctr[CTR_OVERFLOW], 1ull);
 }
 
 
@@ -793,6 +862,10 @@ struct StreamCtx {
     int log_waves[2] = {0, 0};               // waves of the last logged primary / shade launch
     float4* hitbuf = nullptr;                // kernel 1 -> kernel 2 hand-off (per output slot)
     size_t hit_slots = 0;
+    float4* rays = nullptr;                  // wavefront shadow rays: origin+tMax | direction
+    uint8_t* occl = nullptr;                 // per ray: occluded
+    uint8_t* nrays = nullptr;                // per output slot: rays written
+    size_t ray_cap = 0, nrays_cap = 0;
     bool last_was_render = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
 };
@@ -843,11 +916,12 @@ static int g_decline = 0;         // tiles per CU slot (decline heuristic), 0 = 
 static int g_wave_log = 0;        // 1: timing-only wave log on uninstrumented launches (diagnostics)
 static int g_scalar_nodes = 1;    // scalar-cache fetch of wave-uniform nodes
 static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
+static int g_wavefront = 1;       // general shading: gen / trace / resolve kernels instead of one fused kernel
 
 static inline int fast_box(const DeviceState& d);
 
 static void free_ctx(StreamCtx* c) {
-    void* ptrs[] = {c->gstack, c->ctr, c->wave_log, c->hitbuf};
+    void* ptrs[] = {c->gstack, c->ctr, c->wave_log, c->hitbuf, c->rays, c->occl, c->nrays};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1097,6 +1171,23 @@ static void fill_params(const Scene& s, RenderParams& P) {
 
 static inline int fast_box(const DeviceState& d) { return (g_fast_box && d.boxes_finite) ? 1 : 0; }
 
+// wavefront shadow-ray buffers of a stream context (grown, never shrunk)
+static int ensure_rays(StreamCtx& c, size_t slots, size_t per_slot) {
+    const size_t n = slots * per_slot;
+    if (n <= c.ray_cap && slots <= c.nrays_cap) return MRT_OK;
+    HIP_OK(hipStreamSynchronize(c.stream));  // the previous launch may still read them
+    void* ptrs[] = {c.rays, c.occl, c.nrays};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    c.rays = nullptr; c.occl = nullptr; c.nrays = nullptr; c.ray_cap = c.nrays_cap = 0;
+    HIP_OK(hipMalloc((void**)&c.rays, 2 * n * sizeof(float4)));
+    HIP_OK(hipMalloc((void**)&c.occl, n));
+    HIP_OK(hipMalloc((void**)&c.nrays, slots));
+    c.ray_cap = n;
+    c.nrays_cap = slots;
+    return MRT_OK;
+}
+
 static int ensure_slots(StreamCtx& c, size_t slots) {
     if (slots <= c.hit_slots) return MRT_OK;
     // the old buffer may still be read by this stream's previous launch
@@ -1153,6 +1244,26 @@ static KernelFn pick_shade1(int w, bool c, bool f) {
         default: return shade1_fn<6>(c, f);
     }
 }
+template <int MODE>
+static KernelFn shade_mode_fn(bool c, bool po, bool inst) {   // kGen / kResolve: no traversal, FAST unused
+    if (inst) return c ? shade_kernel<true, false, false, true, MODE> : shade_kernel<false, false, false, true, MODE>;
+    if (po) return c ? shade_kernel<true, true, false, false, MODE> : shade_kernel<false, true, false, false, MODE>;
+    return c ? shade_kernel<true, false, false, false, MODE> : shade_kernel<false, false, false, false, MODE>;
+}
+using ShadowFn = void (*)(RenderParams, size_t);
+static ShadowFn pick_shadow(bool c, bool f, bool inst) {
+    if (inst) return c ? (f ? shadow_kernel<true, true, true> : shadow_kernel<true, false, true>)
+                       : (f ? shadow_kernel<false, true, true> : shadow_kernel<false, false, true>);
+    return c ? (f ? shadow_kernel<true, true, false> : shadow_kernel<true, false, false>)
+             : (f ? shadow_kernel<false, true, false> : shadow_kernel<false, false, false>);
+}
+// shadow rays per pixel at most: num_paths x (1 per point light, m_numSamples per area / dome light)
+static int max_shadow_rays(const Scene& s) {
+    int per_path = 0;
+    for (const DevLight& l : s.lights) per_path += l.type == MRT_POINT_LIGHT ? 1 : std::max(1, l.samples);
+    return s.num_paths * per_path;
+}
+
 static KernelFn pick_shade(bool c, bool po, bool f, bool inst) {
     if (inst) return c ? (f ? shade_kernel<true, false, true, true> : shade_kernel<true, false, false, true>)
                        : (f ? shade_kernel<false, false, true, true> : shade_kernel<false, false, false, true>);
@@ -1192,9 +1303,9 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     int which = 0;
     auto launch = [&](KernelFn f) -> int {
         const int g = std::max(1, std::min(std::min(d.grid, d.cus * blocks_per_cu(f, pad)), items));
-        P.wave_log = logw ? c.wave_log + which * log_stride : nullptr;
+        P.wave_log = logw && which < 2 ? c.wave_log + which * log_stride : nullptr;  // primary + first shade
         P.n_waves = g * (kWG / 64);
-        if (logw) c.log_waves[which] = g * (kWG / 64);
+        if (logw && which < 2) c.log_waves[which] = g * (kWG / 64);
         which++;
         void* args[] = {&P};
         HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(f), dim3(g), dim3(kWG), args, pad, stream));
@@ -1207,7 +1318,27 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
     const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst;
-    if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb, inst)))) return rc;
+    const int max_sh = max_shadow_rays(s);
+    const bool wave = !one && g_wavefront && max_sh > 0 && max_sh <= kMaxWaveShadow;
+    if (one || !wave) {
+        if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb, inst)))) return rc;
+    } else {
+        if ((rc = ensure_rays(c, slots, (size_t)max_sh))) return rc;
+        P.ray_o = c.rays;
+        P.ray_d = c.rays + slots * (size_t)max_sh;
+        P.occl = c.occl;
+        P.nrays = c.nrays;
+        P.max_shadow = max_sh;
+        if ((rc = launch(shade_mode_fn<kGen>(count, d.point_only, inst)))) return rc;
+        const ShadowFn sf = pick_shadow(count, fb, inst);
+        const int g = std::max(1, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(sf), 0)));
+        size_t n_rays = slots * (size_t)max_sh;
+        void* args[] = {&P, &n_rays};
+        P.wave_log = nullptr;
+        HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(sf), dim3(g), dim3(kWG), args, 0, stream));
+        P.queue = qbase + 16 * 32;
+        if ((rc = launch(shade_mode_fn<kResolve>(count, d.point_only, inst)))) return rc;
+    }
     c.last_was_render = true;
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(c.ev1, stream));
@@ -1806,6 +1937,8 @@ int mrt_set_tuning(const char* key, int value) {
         g_prio = value;
     } else if (k == "shade1") {
         g_shade1 = value ? 1 : 0;
+    } else if (k == "wavefront") {
+        g_wavefront = value ? 1 : 0;
     } else if (k == "sched") {
         if (value < 0 || value > 3) { set_error("sched must be 0..3"); return MRT_ERR_INVALID; }
         g_sched = value;

@@ -158,7 +158,8 @@ def test_edge_cases():
                                    dict(shade1=0, fast_box=1, sched=2, primary_waves=0),
                                    dict(shade1=1, fast_box=0, sched=3, primary_waves=6),
                                    dict(shade1=1, fast_box=1, sched=2, primary_waves=6, scalar_nodes=0),
-                                   dict(shade1=1, fast_box=1, sched=2, primary_waves=8, scalar_nodes=1)])
+                                   dict(shade1=1, fast_box=1, sched=2, primary_waves=8, scalar_nodes=1),
+                                   dict(shade1=0, wavefront=0), dict(shade1=0, wavefront=1, fast_box=0)])
 def test_every_kernel_path_is_exact(knobs):
     """Performance switches must not change a single bit (fused vs split shading,
     hardware vs select box test, XCD schedule, occupancy build)."""
@@ -176,7 +177,7 @@ def test_every_kernel_path_is_exact(knobs):
         assert np.array_equal(hits["prim"], ref["hits"]["prim"])
         assert P.last_stats["shadow_rays"] == ref["shadow_rays"]
     finally:
-        for k, v in dict(shade1=1, fast_box=1, sched=2, primary_waves=7, scalar_nodes=1).items():
+        for k, v in dict(shade1=1, fast_box=1, sched=2, primary_waves=7, scalar_nodes=1, wavefront=1).items():
             L.mrt_set_tuning(k.encode(), v)
 
 
@@ -357,3 +358,25 @@ def test_c5_instanced_dome_matches_oracle():
     assert P.last_stats["shadow_rays"] == ref["shadow_rays"] > 0
     exact = assert_close_rgb(img.rgb, ref["rgb"])
     assert exact > 0.99, exact
+
+
+@pytest.mark.parametrize("key,W,H", [("C4", 120, 68), ("D1", 96, 96), ("C5", 96, 54)])
+def test_wavefront_shadow_pass_equals_fused_kernel(key, W, H):
+    """Kernel 2a/2b/2c (shadow rays written, traced any-hit in a separate launch,
+    shading resolved) against the fused shading kernel: every bit of RGB, hits and
+    the shadow-ray count, in frame mode and through the batched bucket path."""
+    L = miro.lib()
+    P, _, cam = config_scene(key)
+    try:
+        assert L.mrt_set_tuning(b"wavefront", 0) == 0
+        img0, hits0 = render(P, cam, W, H)
+        st0 = P.last_stats
+        assert L.mrt_set_tuning(b"wavefront", 1) == 0
+        img1, hits1 = render(P, cam, W, H)
+        st1 = P.last_stats
+    finally:
+        L.mrt_set_tuning(b"wavefront", 1)
+    assert np.array_equal(hits0["prim"], hits1["prim"])
+    assert np.array_equal(bits(img0.rgb), bits(img1.rgb))
+    assert np.array_equal(img0.pixels, img1.pixels)
+    assert st0["shadow_rays"] == st1["shadow_rays"] > 0
