@@ -126,6 +126,8 @@ def cpu_baseline(cfg_key, seconds):
     if cfg.get("env"):
         s.set_env_map(sky(tuple(cfg["env"]["sky"])), cfg["env"]["exposure"])
     s.set_num_paths(cfg.get("num_paths", 1))
+    if cfg.get("subdivs"):
+        s.set_subdivs(*cfg["subdivs"])
     s.build()
     W, H = cfg["W"], cfg["H"]
     rays, t_total, frames = 0, 0.0, 0
@@ -226,13 +228,17 @@ def main():
     torch.cuda.synchronize()
     st = scene.stats()
     shadow_mine = st["shadow_rays"]
+    # adaptive supersampling (subdivs > 1): eye rays per pixel vary, counted by the kernel
+    adaptive = bool(cfg.get("subdivs")) and max(cfg["subdivs"][:2]) > 1
+    eye_mine = st["primary_rays"] if adaptive else 0
     if world > 1:
-        t = torch.tensor([shadow_mine], dtype=torch.float64, device="cuda")
+        t = torch.tensor([shadow_mine, eye_mine], dtype=torch.float64, device="cuda")
         dist.all_reduce(t)
-        shadow_total = int(t.item())
+        shadow_total, eye_total = int(t[0].item()), int(t[1].item())
     else:
-        shadow_total = shadow_mine
-    rays_per_step = n_frames * W * H + shadow_total      # all frames of the batch, all ranks
+        shadow_total, eye_total = shadow_mine, eye_mine
+    primary_total = eye_total if adaptive else n_frames * W * H
+    rays_per_step = primary_total + shadow_total      # all frames of the batch, all ranks
     hits_px = st["primary_hits"]
 
     for _ in range(args.warmup):
@@ -281,7 +287,11 @@ def main():
     pm, sm = float(np.median(prim_ms)), float(np.median(shade_ms))
     shade_name = ("shade1_kernel (shade + any-hit shadow rays)" if one_light else
                   "shade pass (shade_kernel<gen> + shadow_kernel any-hit + shade_kernel<resolve>)")
-    if sm >= pm:
+    if adaptive:   # one fused launch: eye rays, shading, inline shadow rays (its time is shade_ms)
+        dom, dom_ms = "adaptive_kernel (eye rays + shading + any-hit shadow rays)", sm
+        dom_b = (st["node_visits"] * NODE_B + st["leaf_visits"] * LEAF_B
+                 + px_mine * (16 + (12 if use_frame_path else 0) + 3) + hits_px * (32 + 3 * 16 + 3 * 16))
+    elif sm >= pm:
         dom, dom_ms, dom_b = shade_name, sm, b_shade
     else:
         dom, dom_ms, dom_b = "primary_kernel (camera rays, closest hit)", pm, b_prim
@@ -306,7 +316,8 @@ def main():
                      cfg["mesh"], cfg["mesh"]), scene.bvh_info["prims"],
                     {"instances": "dragon_2.obj / buddha_smooth"}.get(cfg["mesh"], cfg["mesh"]),
                     "; procedural lat-long sky for the dome / environment map" if cfg.get("env") else "")),
-        "config": {"workload": cfg["name"], "config": args.config, "width": W, "height": H, "spp": 1,
+        "config": {"workload": cfg["name"], "config": args.config, "width": W, "height": H, "spp": 1 if not adaptive else f"adaptive {cfg['subdivs'][0]}..{cfg['subdivs'][1]} subdivs, "
+                   f"{primary_total / (n_frames * W * H):.2f} eye rays/px",
                    "frames_per_step": n_frames, "rays_per_step": rays_per_step, "shadow_rays": shadow_total,
                    "qbvh_nodes": scene.bvh_info["nodes"], "qbvh_leaves": scene.bvh_info["leaves"],
                    "frames_in_flight": inflight,
@@ -316,7 +327,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(dom_b),
-                     "visits_per_ray": round(st["node_visits"] / max(1, px_mine + shadow_mine), 3)},
+                     "visits_per_ray": round(st["node_visits"] / max(1, (eye_mine if adaptive else px_mine) + shadow_mine), 3)},
         "launch_ms": {"primary": round(pm, 4), "shade": round(sm, 4)},
         # instrumented (count-mode) launch: wall-clock spread of the persistent waves
         "wave_timing_us": {k: round(st[k], 1) for k in ("primary_span_us", "primary_ramp_us", "primary_tail_us",

@@ -146,6 +146,13 @@ int mrt_scene_mesh_export(const mrt_scene* s, int mesh, float* verts, float* nor
 int mrt_scene_set_background(mrt_scene* s, const float rgb[3]);
 /* Scene::m_numPaths (src/Scene.h:61): shade() calls per primary hit */
 int mrt_scene_set_num_paths(mrt_scene* s, int num_paths);
+/* Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55; defaults
+ * 1, 1, 0.01 at src/Scene.cpp:20-22): adaptive supersampling of
+ * Scene::adaptiveSampleScene (src/Scene.cpp:252-293).  With both counts 1 a
+ * frame is one ray per pixel; otherwise levels 2.. of n x n jittered sub-samples
+ * run until the gamma-space change is below noise (at least up to min_subdivs,
+ * at most max_subdivs).  1 <= min_subdivs <= max_subdivs <= 16. */
+int mrt_scene_set_subdivs(mrt_scene* s, int min_subdivs, int max_subdivs, float noise_threshold);
 /* ---- images and image-based lighting -------------------------------------
  * HDRLoader::load (src/hdrloader.cpp:29-97, via RawImage::loadImage/loadHDR,
  * src/RawImage.cpp:16-32): mrt_hdr_info reads the header, mrt_hdr_load decodes

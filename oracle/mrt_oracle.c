@@ -204,7 +204,9 @@ struct oro_scene {
     int env_tex; float env_exposure;  /* Scene::m_envMap / m_envExposure */
     v3 bg;
     int num_paths;
-    int* mesh_blas;                   /* per mesh: owning BLAS, -1 = world geometry */
+    int min_subdivs, max_subdivs;     /* Scene::m_minSubdivs / m_maxSubdivs (src/Scene.cpp:21-22) */
+    float noise;                      /* Scene::m_noiseThreshold (src/Scene.cpp:20) */
+    int* mesh_blas;                  /* per mesh: owning BLAS, -1 = world geometry */
     int* groups; int n_groups;        /* world objects in add order: mesh m >= 0, instance ~i */
     struct oro_scene** blas; int n_blas;   /* ProxyObject BVHs (sub-scenes sharing the meshes) */
     oro_inst* inst; int n_inst;
@@ -221,6 +223,8 @@ oro_scene* oro_scene_create(void) {
     oro_scene* s = (oro_scene*)calloc(1, sizeof(oro_scene));
     s->bg = V(0, 0, 0);
     s->num_paths = 1;
+    s->min_subdivs = s->max_subdivs = 1;
+    s->noise = 0.01f;
     s->env_tex = -1;
     s->env_exposure = 1.0f;
     return s;
@@ -264,6 +268,12 @@ int oro_scene_add_light(oro_scene* s, const oro_light* l) {
 }
 void oro_scene_set_bg(oro_scene* s, float r, float g, float b) { s->bg = V(r, g, b); }
 void oro_scene_set_num_paths(oro_scene* s, int n) { s->num_paths = n < 1 ? 1 : n; }
+/* Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55) */
+int oro_scene_set_subdivs(oro_scene* s, int min_subdivs, int max_subdivs, float noise) {
+    if (min_subdivs < 1 || max_subdivs < min_subdivs || max_subdivs > 16 || !(noise >= 0.f)) return -1;
+    s->min_subdivs = min_subdivs; s->max_subdivs = max_subdivs; s->noise = noise;
+    return 0;
+}
 
 int oro_scene_add_texture(oro_scene* s, const float* rgb, int w, int h) {
     if (s->n_tex >= ORO_MAX_TEX || !rgb || w <= 0 || h <= 0) return -1;
@@ -1116,11 +1126,12 @@ static const float PI_F = 3.1415926f;                  /* src/Miro.h:57 */
 typedef struct {
     const oro_scene* s;
     uint32_t pixel; uint32_t dim;   /* RNG stream position */
+    uint32_t sample;                /* eye ray of the pixel (adaptive supersampling) */
     uint64_t shadow_rays, nodes, leaves;
     uint32_t shadow_mask;
 } shade_ctx;
 
-static float next_rand(shade_ctx* c) { return oro_rand(c->pixel, 0, c->dim++, 0x5EEDu); }
+static float next_rand(shade_ctx* c) { return oro_rand(c->pixel, c->sample, c->dim++, 0x5EEDu); }
 
 static int trace_shadow(shade_ctx* c, v3 from, v3 L, float tMax) {
     ray_t r = make_ray(from, L);
@@ -1362,6 +1373,15 @@ static cam_basis camera_basis(const oro_camera* cam, int W, int H) {
     return b;
 }
 /* eyeRayAdaptive (aperture 0), src/Camera.cpp:138-157; offsets (0.5, 0.5). */
+static ray_t camera_ray_adaptive(const cam_basis* b, int x, int y, float minX, float maxX, float minY, float maxY,
+                                 float urand, float vrand) {
+    float xOffset = (maxX - minX) * urand + minX;   /* src/Camera.cpp:146-147 */
+    float yOffset = (maxY - minY) * vrand + minY;
+    float U = b->left + (b->right - b->left) * (((float)x + xOffset) / (float)b->W);
+    float Vp = b->bottom + (b->top - b->bottom) * (((float)y + yOffset) / (float)b->H);
+    v3 dir = vnormalized(vsub(vadd(vscale(b->u, U), vscale(b->v, Vp)), b->w));
+    return make_ray(b->eye, dir);
+}
 static ray_t camera_ray(const cam_basis* b, int x, int y, float urand, float vrand) {
     float xOffset = (0.5f - 0.5f) * urand + 0.5f;
     float yOffset = (0.5f - 0.5f) * vrand + 0.5f;
@@ -1373,6 +1393,7 @@ static ray_t camera_ray(const cam_basis* b, int x, int y, float urand, float vra
 
 /* ---------------------------------------------------------------- image */
 static uint8_t g_lut[32769];
+static float g_lutF[32769];     /* Image::linear_to_gammaF */
 static int g_lut_ready = 0;
 /* Image::generateGammaTables, src/Image.cpp:19-35 */
 void oro_gamma_table(uint8_t* out) {
@@ -1380,6 +1401,7 @@ void oro_gamma_table(uint8_t* out) {
         const float GAMMA = 2.2f;
         for (int i = 0; i < 32769; i++) {
             float r2 = (float)((double)powf(i / 32768.0f, 1 / GAMMA) * 255.0 + 0.5);
+            g_lutF[i] = r2;
             g_lut[i] = (uint8_t)(int)r2;
         }
         g_lut_ready = 1;
@@ -1422,6 +1444,53 @@ static v3 sample_scene(shade_ctx* c, const ray_t* r, hit_t* h, uint32_t* prim_nv
     return s->bg;
 }
 
+/* getSum, src/Scene.cpp:245-248 */
+static int get_sum(const int n) { return (int)(n * (n + 1) * (2 * n + 1) * 0.16666667f); }
+/* Image::linear_to_gammaF[int(min(v, 1) * 32767)], src/Scene.cpp:278-283.
+ * Deviation: negative / NaN (an out-of-bounds read there) -> entry 0. */
+static float gamma_f(float v) {
+    float f = ((v > 1.f) ? 1.f : v) * 32767.f;
+    return g_lutF[f >= 0.f ? (int)f : 0];
+}
+/* Scene::adaptiveSampleScene levels 2.. (src/Scene.cpp:257-290), after the
+ * centre sample's result.  Eye ray k of a pixel draws from RNG stream
+ * (pixel, k), dims 0-2 for eyeRayAdaptive, then the shading draws. */
+static v3 adaptive_levels(shade_ctx* c, const cam_basis* b, int x, int y, v3 shadeResult, uint64_t* eye,
+                          uint32_t* nv, uint32_t* lv) {
+    const oro_scene* s = c->s;
+    int curLevel = 2, cutOff = 0;
+    while ((curLevel <= s->max_subdivs && !cutOff) || curLevel <= s->min_subdivs) {
+        v3 curResult = V(0, 0, 0);
+        for (int i = 0; i < curLevel; i++) {
+            for (int j = 0; j < curLevel; j++) {
+                float offset = 1.0f / (float)curLevel;
+                c->sample++;
+                c->dim = 0;
+                float urand = next_rand(c), vrand = next_rand(c);
+                (void)next_rand(c);      /* getTimeSample */
+                ray_t r = camera_ray_adaptive(b, x, y, i * offset, (i + 1) * offset, j * offset, (j + 1) * offset,
+                                              urand, vrand);
+                hit_t h;
+                curResult = vadd(curResult, sample_scene(c, &r, &h, nv, lv));
+                (*eye)++;
+            }
+        }
+        float numSamplesPre = (float)get_sum(curLevel - 1);
+        float numSamplesNow = (float)(curLevel * curLevel);
+        v3 newResult = vscale(vadd(vscale(shadeResult, numSamplesPre), curResult),
+                              1.0f / (numSamplesPre + numSamplesNow));
+        float tx = gamma_f(shadeResult.x) - gamma_f(newResult.x);
+        float ty = gamma_f(shadeResult.y) - gamma_f(newResult.y);
+        float tz = gamma_f(shadeResult.z) - gamma_f(newResult.z);
+        float myz = fabsf(ty) > fabsf(tz) ? fabsf(ty) : fabsf(tz);
+        float m = fabsf(tx) > myz ? fabsf(tx) : myz;
+        cutOff = m < s->noise;
+        shadeResult = newResult;
+        curLevel++;
+    }
+    return shadeResult;
+}
+
 int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H, int x0, int y0, int x1, int y1,
                float* rgb, uint8_t* rgb8, oro_hit* hitout, uint32_t* shadow, uint64_t* counters, int n_threads) {
     if (!s->built || W <= 0 || H <= 0) return -1;
@@ -1447,12 +1516,14 @@ int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H, int x0, 
             hit_t h;
             uint32_t nv = 0, lv = 0;
             v3 col = sample_scene(&c, &r, &h, &nv, &lv);
+            uint64_t eye = 1;
+            if (s->min_subdivs > 1 || s->max_subdivs > 1) col = adaptive_levels(&c, &b, x, y, col, &eye, &nv, &lv);
             size_t p = (size_t)y * W + x;
             if (rgb) { rgb[3 * p] = col.x; rgb[3 * p + 1] = col.y; rgb[3 * p + 2] = col.z; }
             if (rgb8) { rgb8[3 * p] = map_channel(col.x); rgb8[3 * p + 1] = map_channel(col.y); rgb8[3 * p + 2] = map_channel(col.z); }
             if (hitout) { hitout[p].t = h.t; hitout[p].a = h.a; hitout[p].b = h.b; hitout[p].prim = h.prim >= 0 ? hit_id(s, &h) : -1; }
             if (shadow) shadow[p] = c.shadow_mask;
-            prim++; shadowr += c.shadow_rays; nodes += nv + c.nodes; leaves += lv + c.leaves;
+            prim += eye; shadowr += c.shadow_rays; nodes += nv + c.nodes; leaves += lv + c.leaves;
             pnodes += nv; pleaves += lv;
         }
     }

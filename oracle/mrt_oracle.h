@@ -78,6 +78,8 @@ int oro_scene_add_material(oro_scene* s, const oro_material* m);
 int oro_scene_add_light(oro_scene* s, const oro_light* l);
 void oro_scene_set_bg(oro_scene* s, float r, float g, float b);
 void oro_scene_set_num_paths(oro_scene* s, int n);
+/* Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55); 0 = OK */
+int oro_scene_set_subdivs(oro_scene* s, int min_subdivs, int max_subdivs, float noise);
 /* Scene::preCalc -> BVH::build (src/Scene.cpp:62-79, src/BVH.cpp:457-575). */
 int oro_scene_build(oro_scene* s);
 /* ProxyObject instancing (src/ProxyObject.cpp:5-95,131-167).  oro_scene_make_blas

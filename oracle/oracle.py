@@ -70,6 +70,7 @@ def _declare(L):
     L.oro_scene_add_light.argtypes = [C.c_void_p, C.POINTER(Light)]
     L.oro_scene_set_bg.argtypes = [C.c_void_p, C.c_float, C.c_float, C.c_float]
     L.oro_scene_set_num_paths.argtypes = [C.c_void_p, C.c_int]
+    L.oro_scene_set_subdivs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float]
     L.oro_scene_build.argtypes = [C.c_void_p]
     L.oro_qbvh_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 6
     L.oro_qbvh_export.argtypes = [C.c_void_p, _fp, _i32p, _fp, _i32p]
@@ -272,6 +273,11 @@ class OracleScene:
 
     def set_num_paths(self, n):
         self.L.oro_scene_set_num_paths(self.h, int(n))
+
+    def set_subdivs(self, min_subdivs, max_subdivs, noise=0.01):
+        """Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55)."""
+        if self.L.oro_scene_set_subdivs(self.h, int(min_subdivs), int(max_subdivs), float(noise)) != 0:
+            raise ValueError("need 1 <= min_subdivs <= max_subdivs <= 16 and noise >= 0")
 
     def build(self):
         r = self.L.oro_scene_build(self.h)

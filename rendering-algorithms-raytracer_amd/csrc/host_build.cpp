@@ -33,6 +33,7 @@ namespace {
 struct Tables {
     uint16_t rcp[2048], rsq[2048];
     uint8_t gamma[32769];
+    float gammaF[32769];
     Tables() {
         for (int i = 0; i < 2048; i++) {
             rcp[i] = (uint16_t)((MRT_RCP_TABLE[i] >> 11) & 0xFFFu);
@@ -42,6 +43,7 @@ struct Tables {
         const float GAMMA = 2.2f;
         for (int i = 0; i < 32769; i++) {
             float r2 = (float)((double)powf(i / 32768.0f, 1 / GAMMA) * 255.0 + 0.5);
+            gammaF[i] = r2;
             gamma[i] = (uint8_t)(int)r2;
         }
     }
@@ -55,6 +57,7 @@ const Tables& tables() {
 const uint16_t* host_rcp_table() { return tables().rcp; }
 const uint16_t* host_rsqrt_table() { return tables().rsq; }
 const uint8_t* host_gamma_lut() { return tables().gamma; }
+const float* host_gamma_float_lut() { return tables().gammaF; }
 
 // ------------------------------------------------------------------ Matrix4x4
 namespace {

@@ -41,7 +41,9 @@ enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLO
        CTR_WAVE_STEPS_P = 8, CTR_UNIFORM_P = 9,
        // count mode, per launch (primary at CTR_TP, shade at CTR_TS): wave start/end
        // wall clocks as ~min start, max start, ~min end, max end (zero-initialised maxima)
-       CTR_TP = 10, CTR_TS = 14, CTR_N = 18 };
+       CTR_TP = 10, CTR_TS = 14,
+       CTR_RAYS_P = 18,  // eye rays traced (adaptive supersampling; otherwise one per pixel)
+       CTR_N = 19 };
 static constexpr int kMaxBlocksPerCU = 8;
 // wave log record: start, end, tiles, node visits, then (tile id << 40 | start tick) of the first kLogTiles
 // tiles, then the wall-clock ticks each of those tiles' dequeue took
@@ -79,6 +81,9 @@ struct RenderParams {
     float env_exposure;
     const uint16_t* tables;  // rcp[2048] | rsqrt[2048]
     const uint8_t* gamma;
+    const float* gammaF;     // Image::linear_to_gammaF (adaptive supersampling stop test)
+    int32_t min_subdivs, max_subdivs;
+    float noise;             // Scene::m_noiseThreshold
     int32_t* gstack;
     uint32_t gstride;        // total threads in the launch
     unsigned long long* ctr;
@@ -133,8 +138,9 @@ struct Shader {
     uint32_t seed;
     size_t slot0;            // wavefront modes: this pixel's first ray slot
     uint32_t nslot;          //   rays so far
+    uint32_t sample = 0;     // eye-ray sample of the pixel (adaptive supersampling)
 
-    __device__ float next_rand() { return rng(pixel, 0, dim++, seed); }
+    __device__ float next_rand() { return rng(pixel, sample, dim++, seed); }
 
     template <bool COUNT>
     __device__ bool occluded(v3 from, v3 L, float tMax) {
@@ -641,6 +647,127 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     flush_stats<COUNT>(P, st, MODE == kResolve ? 0u : shadow_total, lane, t0, ntiles);
 }
 
+// getSum (src/Scene.cpp:245-248): 1^2 + ... + n^2 through the float 1/6
+__device__ __forceinline__ int sum_squares(int n) { return (int)((float)(n * (n + 1) * (2 * n + 1)) * 0.16666667f); }
+
+// Image::linear_to_gammaF[int(min(v, 1) * 32767)] (src/Scene.cpp:278-283).
+// Deviation: a negative / NaN channel (an out-of-bounds read there) uses entry 0.
+__device__ __forceinline__ float gamma_f(const float* lut, float v) {
+    const float c = (v > 1.f) ? 1.f : v;
+    const float f = c * 32767.f;
+    return lut[(f >= 0.f) ? (int)f : 0];
+}
+
+// Kernel 3: Scene::adaptiveSampleScene (src/Scene.cpp:252-293), fused.  One
+// persistent launch; a lane loops over its pixel's eye rays -- the centre
+// sample, then levels 2.. of n x n jittered sub-samples (eyeRayAdaptive with
+// offsets [i/n, (i+1)/n] x [j/n, (j+1)/n], src/Camera.cpp:144-150) -- each
+// through Scene::sampleScene (closest hit, shading with inline shadow rays,
+// environment / background on a miss), with the reference's running mean and
+// gamma-space stop test after every level.  Eye ray k of a pixel draws from
+// RNG stream (pixel, k): ray 0 is the 1-spp frame path's ray.  Lanes of a wave
+// stop independently; the wave runs until its last lane is done.
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST>
+__global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[2048];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    load_tables(P.tables, s_tab, 1024);
+    const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
+    const uint16_t* rcpT = s_tab;
+    const uint16_t* rsqT = P.tables + 2048;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
+    TravStats st;
+    uint32_t shadow_total = 0, eye_rays = 0, eye_hits = 0;
+    TileSched ts(P, wave, lane);
+    uint32_t ntiles = 0;
+    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
+        ntiles++;
+        int x, y;
+        size_t slot;
+        if (!item_pixel(P, item, lane, x, y, slot)) continue;
+        const int f = item_frame(P, item);
+        const CamParams& cam = P.cam[f];
+        const uint32_t seed = P.seed + (uint32_t)f;
+        const uint32_t pixel = (uint32_t)(y * cam.W + x);
+        const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
+        const v3 U = mk(cam.u[0], cam.u[1], cam.u[2]), Vv = mk(cam.v[0], cam.v[1], cam.v[2]),
+                 W = mk(cam.w[0], cam.w[1], cam.w[2]);
+        v3 result = mk(0, 0, 0), cur = mk(0, 0, 0);
+        int level = 1, i = 0, j = 0;
+        bool cut = false;
+        for (uint32_t sample = 0;; sample++) {
+            float x0 = 0.5f, x1 = 0.5f, y0 = 0.5f, y1 = 0.5f;
+            if (level > 1) {
+                const float off = 1.0f / (float)level;
+                x0 = (float)i * off; x1 = (float)(i + 1) * off;
+                y0 = (float)j * off; y1 = (float)(j + 1) * off;
+            }
+            const float ur = rng(pixel, sample, 0, seed), vr = rng(pixel, sample, 1, seed);
+            const float xo = (x1 - x0) * ur + x0, yo = (y1 - y0) * vr + y0;
+            const float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
+            const float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
+            const v3 d = normalized(sub(add(scale(U, Up), scale(Vv, Vp)), W), rsqT);
+            const DRay r = make_ray(eye, d);
+            DHit h{1e12f, 0.f, 0.f, -1};
+            v3 col;
+            eye_rays++;
+            const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
+            if (sample == 0) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
+            if (hit) {
+                eye_hits++;
+                Shader<POINT_ONLY, FAST, INST, kFused> S{P, T, rcpT, rsqT, st, pixel, 3u, 0u, seed, 0, 0u};
+                S.sample = sample;
+                col = S.template shade<COUNT>(r, h);
+                shadow_total += S.shadow_rays;
+            } else if (P.env) {
+                col = scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
+            } else {
+                col = mk(P.bg[0], P.bg[1], P.bg[2]);
+            }
+            if (level == 1) {
+                result = col;
+                level = 2;
+            } else {
+                cur = add(cur, col);
+                if (++j < level) continue;
+                j = 0;
+                if (++i < level) continue;
+                i = 0;
+                const float pre = (float)sum_squares(level - 1), now = (float)(level * level);
+                const v3 nr = scale(add(scale(result, pre), cur), 1.0f / (pre + now));
+                const float tx = gamma_f(P.gammaF, result.x) - gamma_f(P.gammaF, nr.x);
+                const float ty = gamma_f(P.gammaF, result.y) - gamma_f(P.gammaF, nr.y);
+                const float tz = gamma_f(P.gammaF, result.z) - gamma_f(P.gammaF, nr.z);
+                cut = fmaxf(fabsf(tx), fmaxf(fabsf(ty), fabsf(tz))) < P.noise;
+                result = nr;
+                cur = mk(0, 0, 0);
+                level++;
+            }
+            if (!((level <= P.max_subdivs && !cut) || level <= P.min_subdivs)) break;
+        }
+        if (P.out_rgb) {
+            float* o = P.out_rgb + 3 * slot;
+            o[0] = result.x; o[1] = result.y; o[2] = result.z;
+        }
+        if (P.out_rgb8) {
+            uint8_t* o8 = P.out_rgb8 + 3 * slot;
+            o8[0] = map8(P.gamma, result.x); o8[1] = map8(P.gamma, result.y); o8[2] = map8(P.gamma, result.z);
+        }
+    }
+    unsigned long long er = eye_rays, eh = eye_hits;
+    for (int off = 32; off > 0; off >>= 1) {
+        er += __shfl_down(er, off);
+        eh += __shfl_down(eh, off);
+    }
+    if (lane == 0) {
+        atomicAdd(&P.ctr[CTR_RAYS_P], er);
+        atomicAdd(&P.ctr[CTR_HITS], eh);
+    }
+    flush_stats<COUNT, false>(P, st, shadow_total, lane, t0, ntiles);
+}
+
 // Kernel 2b: every wavefront shadow ray of the frame, one lane each, any-hit
 // (the occlusion answer of Shader::occluded).  Slots past a pixel's ray count
 // are skipped.
@@ -887,6 +1014,7 @@ struct DeviceState {
     const float* env = nullptr;  // environment texture (one of bufs)
     uint16_t* tables = nullptr;
     uint8_t* gamma = nullptr;
+    float* gammaF = nullptr;
     uint32_t gthreads = 0;
     // scratch for the synchronous API
     float* d_rgb = nullptr;
@@ -936,7 +1064,7 @@ static void free_device(DeviceState* d) {
     (void)hipDeviceSynchronize();   // no launch may still use the scratch below
     for (StreamCtx* c : d->ctxs) free_ctx(c);
     void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts, d->tables,
-                    d->gamma, d->d_rgb, d->d_rgb8};
+                    d->gamma, d->gammaF, d->d_rgb, d->d_rgb8};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (void* p : d->bufs)
@@ -1082,6 +1210,7 @@ static int ensure_device(Scene& s, int device) {
     if ((rc = upload(d.lights, s.lights.data(), s.lights.size() * sizeof(DevLight), total))) return rc;
     if ((rc = upload(d.tables, tab.data(), tab.size() * sizeof(uint16_t), total))) return rc;
     if ((rc = upload(d.gamma, host_gamma_lut(), 32769, total))) return rc;
+    if ((rc = upload(d.gammaF, host_gamma_float_lut(), 32769 * sizeof(float), total))) return rc;
     // textures, then each dome light's tables (DomeLight::setTexture products)
     auto upload_floats = [&](const std::vector<float>& v, const float*& dst) -> int {
         float* p = nullptr;
@@ -1155,6 +1284,10 @@ static void fill_params(const Scene& s, RenderParams& P) {
     const DeviceState& d = *s.dev;
     P.nodes = d.nodes; P.leaves = d.leaves; P.prims = d.prims; P.verts = d.verts; P.normals = d.normals;
     P.mats = d.mats; P.lights = d.lights; P.tables = d.tables; P.gamma = d.gamma;
+    P.gammaF = d.gammaF;
+    P.min_subdivs = s.min_subdivs;
+    P.max_subdivs = s.max_subdivs;
+    P.noise = s.noise_threshold;
     P.domes = d.domes;
     P.insts = d.insts;
     P.n_insts = d.n_insts;
@@ -1273,8 +1406,18 @@ static KernelFn pick_shade(bool c, bool po, bool f, bool inst) {
              : (f ? shade_kernel<false, false, true> : shade_kernel<false, false, false>);
 }
 
+static KernelFn pick_adaptive(bool c, bool po, bool f, bool inst) {
+    if (inst) return c ? (f ? adaptive_kernel<true, false, true, true> : adaptive_kernel<true, false, false, true>)
+                       : (f ? adaptive_kernel<false, false, true, true> : adaptive_kernel<false, false, false, true>);
+    if (po) return c ? (f ? adaptive_kernel<true, true, true, false> : adaptive_kernel<true, true, false, false>)
+                     : (f ? adaptive_kernel<false, true, true, false> : adaptive_kernel<false, true, false, false>);
+    return c ? (f ? adaptive_kernel<true, false, true, false> : adaptive_kernel<true, false, false, false>)
+             : (f ? adaptive_kernel<false, false, true, false> : adaptive_kernel<false, false, false, false>);
+}
+
 // Two launches on `stream`: primary rays -> hit records, then shading with
-// shadow rays.  Events bracket both (kernel_ms covers the whole frame).
+// shadow rays.  Events bracket both (kernel_ms covers the whole frame).  With
+// adaptive supersampling (subdivs > 1) one fused launch (kernel 3) instead.
 static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hipStream_t stream) {
     DeviceState& d = *s.dev;
     StreamCtx* cp = nullptr;
@@ -1314,6 +1457,16 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     HIP_OK(hipEventRecord(c.ev0, stream));
     const bool fb = P.fast_box != 0;
     const bool inst = d.n_insts > 0;
+    if (P.min_subdivs > 1 || P.max_subdivs > 1) {
+        HIP_OK(hipEventRecord(c.evm, stream));   // primary_ms = 0: one launch
+        if ((rc = launch(pick_adaptive(count, d.point_only, fb, inst)))) return rc;
+        c.last_was_render = true;
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipEventRecord(c.ev1, stream));
+        d.last = &c;
+        s.last = mrt_stats{};
+        return MRT_OK;
+    }
     if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst)))) return rc;
     HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
@@ -1603,6 +1756,17 @@ int mrt_scene_set_num_paths(mrt_scene* s, int num_paths) {
     return MRT_OK;
 }
 
+int mrt_scene_set_subdivs(mrt_scene* s, int min_subdivs, int max_subdivs, float noise_threshold) {
+    if (!s || min_subdivs < 1 || max_subdivs < min_subdivs || max_subdivs > 16 || !(noise_threshold >= 0.f)) {
+        set_error("bad subdivs: need 1 <= min <= max <= 16 and noise >= 0");
+        return MRT_ERR_INVALID;
+    }
+    s->impl.min_subdivs = min_subdivs;
+    s->impl.max_subdivs = max_subdivs;
+    s->impl.noise_threshold = noise_threshold;
+    return MRT_OK;
+}
+
 int mrt_scene_build_bvh(mrt_scene* s) {
     if (!s) { set_error("null scene"); return MRT_ERR_INVALID; }
     for (auto& m : s->impl.meshes)
@@ -1812,6 +1976,7 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     S.last.primary_leaf_visits = c[CTR_LEAVES_P];
     S.last.shadow_rays = c[CTR_SHADOW];
     S.last.primary_hits = c[CTR_HITS];
+    if (c[CTR_RAYS_P]) S.last.primary_rays = c[CTR_RAYS_P];   // adaptive supersampling: eye rays traced
     S.last.primary_wave_steps = c[CTR_WAVE_STEPS_P];
     S.last.primary_uniform_visits = c[CTR_UNIFORM_P];
     S.last.node_visits = c[CTR_NODES];

@@ -15,6 +15,7 @@ namespace mrt {
 const uint16_t* host_rcp_table();
 const uint16_t* host_rsqrt_table();
 const uint8_t* host_gamma_lut();  // 32769 entries, Image::generateGammaTables
+const float* host_gamma_float_lut();  // Image::linear_to_gammaF, 32769 entries
 
 struct Mesh {
     std::vector<v3> verts, normals;
@@ -63,6 +64,9 @@ struct Scene {
     float env_exposure = 1.f;       // Scene::m_envExposure
     float bg[3] = {0.f, 0.f, 0.f};
     int num_paths = 1;
+    // Scene::m_minSubdivs / m_maxSubdivs / m_noiseThreshold (src/Scene.cpp:20-22)
+    int min_subdivs = 1, max_subdivs = 1;
+    float noise_threshold = 0.01f;
     // world object groups in add order: mesh id (>= 0) or ~instance id
     std::vector<int32_t> groups;
     std::vector<int32_t> mesh_blas;   // per mesh: owning BLAS, -1 = world geometry

@@ -343,6 +343,9 @@ class Scene:
         self._lights: List[_Light] = []
         self.bg = Vector3(0)
         self.m_numPaths = 1
+        self.m_minSubdivs = 1            # src/Scene.cpp:20-22
+        self.m_maxSubdivs = 1
+        self.m_noiseThreshold = 0.01
         self.m_envMap = None
         self.m_envExposure = 1.0
         self.device = int(device)
@@ -355,6 +358,13 @@ class Scene:
     def addLight(self, light): self._lights.append(light)
     def setBGColor(self, c): self.bg = Vector3(c)
     def setNumPaths(self, p): self.m_numPaths = int(p)
+    # adaptive supersampling, Scene::adaptiveSampleScene (src/Scene.h:42-55, src/Scene.cpp:252-293)
+    def setMinSubdivs(self, r): self.m_minSubdivs = int(r)
+    def minSubdivs(self): return self.m_minSubdivs
+    def setMaxSubdivs(self, r): self.m_maxSubdivs = int(r)
+    def maxSubdivs(self): return self.m_maxSubdivs
+    def setNoise(self, n): self.m_noiseThreshold = float(n)
+    def noise(self): return self.m_noiseThreshold
     def setEnvMap(self, t): self.m_envMap = t                    # src/Scene.h:23
     def setEnvExposure(self, e): self.m_envExposure = float(e)   # src/Scene.h:24
 
@@ -427,6 +437,7 @@ class Scene:
             check(L.mrt_scene_set_env_map(self._h, tex_id(self.m_envMap), self.m_envExposure), "env map")
         check(L.mrt_scene_set_background(self._h, f3(self.bg)), "bg")
         check(L.mrt_scene_set_num_paths(self._h, self.m_numPaths), "num_paths")
+        check(L.mrt_scene_set_subdivs(self._h, self.m_minSubdivs, self.m_maxSubdivs, self.m_noiseThreshold), "subdivs")
         check(L.mrt_scene_build_bvh(self._h), "BVH build")
         info = _lib.mrt_bvh_info()
         check(L.mrt_scene_bvh_info(self._h, C.byref(info)), "bvh_info")

@@ -360,6 +360,15 @@ CONFIGS = {
                camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
                lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
                material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza"),
+    # A3: C3 with adaptive supersampling as the Assignment 3 scenes set it
+    # (m_minSubdivs = 1, m_maxSubdivs = 4, src/Assignment3.h:31-32; noise 0.01,
+    # src/Scene.cpp:20): Scene::adaptiveSampleScene, 5 to 30 eye rays per pixel
+    "A3": dict(name="sponza stand-in (~66k tris) 1920x1080 Blinn+PointLight, adaptive supersampling 1..4 subdivs",
+               W=1920, H=1080,
+               camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
+               lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
+               material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza",
+               subdivs=(1, 4, 0.01)),
     # C4: Sponza stand-in, RectangleLight (8,10,2)/(8,10,-2)/(-8,10,2) power 1.5 and
     # Scene::m_numPaths = 16 (makeSponzaScenePathTrace, src/assignment2.h:663-708, direct
     # lighting only): 16 shade() calls per hit, one area-light shadow ray each;
@@ -473,6 +482,9 @@ def build_config(key, device=0):
         scene.setEnvMap(sky_texture(tuple(cfg["env"]["sky"])))
         scene.setEnvExposure(cfg["env"]["exposure"])
     scene.setNumPaths(cfg.get("num_paths", 1))
+    if cfg.get("subdivs"):
+        lo, hi, noise = cfg["subdivs"]
+        scene.setMinSubdivs(lo); scene.setMaxSubdivs(hi); scene.setNoise(noise)
     scene.preCalc()
     cam = miro.Camera()
     c = cfg["camera"]

@@ -16,7 +16,7 @@ def fixture_mesh(name):
     return f["verts"], f["normals"], f["vidx"], f["nidx"]
 
 
-def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1, instances=None):
+def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1, instances=None, subdivs=None):
     """Build (miro.Scene, OracleScene, camera dict) for a config dict."""
     lights = cfg["lights"] if lights is None else lights
     mat = cfg["material"]
@@ -93,6 +93,9 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
         O_.set_env_map(otex, env["exposure"])
     P.setNumPaths(num_paths)
     O_.set_num_paths(num_paths)
+    if subdivs is not None:  # (min, max, noise): Scene::adaptiveSampleScene
+        P.setMinSubdivs(subdivs[0]); P.setMaxSubdivs(subdivs[1]); P.setNoise(subdivs[2])
+        O_.set_subdivs(*subdivs)
     P.preCalc()
     O_.build()
     return P, O_, cfg["camera"]
@@ -107,6 +110,7 @@ def camera(c):
 def config_scene(key, **kw):
     cfg = scenes.CONFIGS[key]
     kw.setdefault("num_paths", cfg.get("num_paths", 1))
+    kw.setdefault("subdivs", cfg.get("subdivs"))
     if cfg["mesh"] == "cornell":
         return scene_pair(cfg, meshes=[fixture_mesh("cornell_box")], **kw)
     if cfg["mesh"] == "bunny":
