@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 2
+#define MRT_ABI_VERSION 3
 
 enum {
     MRT_OK = 0,
@@ -120,6 +120,7 @@ typedef struct {
      * tail = spread of wave ends (time the launch runs below full occupancy)   */
     float primary_span_us, primary_ramp_us, primary_tail_us;
     float shade_span_us, shade_ramp_us, shade_tail_us;
+    uint64_t secondary_rays;             /* Blinn reflection / refraction rays traced   */
 } mrt_stats;
 
 const char* mrt_last_error(void);
@@ -146,6 +147,11 @@ int mrt_scene_mesh_export(const mrt_scene* s, int mesh, float* verts, float* nor
 int mrt_scene_set_background(mrt_scene* s, const float rgb[3]);
 /* Scene::m_numPaths (src/Scene.h:61): shade() calls per primary hit */
 int mrt_scene_set_num_paths(mrt_scene* s, int num_paths);
+/* Blinn::setReflectAmt / Material::setRefractAmt / Blinn::setIor (src/Blinn.h:38-41,
+ * src/Material.h:32; Blinn ctor defaults 0, 0, 1.5, src/Blinn.h:11-22): reflection and refraction rays of Blinn::shade (src/Blinn.cpp:238-330),
+ * Fresnel-weighted Russian roulette, at most 5 bounces, IOR history per ray.
+ * No effect on Lambert materials. */
+int mrt_scene_set_material_optics(mrt_scene* s, int material, float reflect_amt, float refract_amt, float ior);
 /* Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55; defaults
  * 1, 1, 0.01 at src/Scene.cpp:20-22): adaptive supersampling of
  * Scene::adaptiveSampleScene (src/Scene.cpp:252-293).  With both counts 1 a

@@ -1128,6 +1128,7 @@ typedef struct {
     uint32_t pixel; uint32_t dim;   /* RNG stream position */
     uint32_t sample;                /* eye ray of the pixel (adaptive supersampling) */
     uint64_t shadow_rays, nodes, leaves;
+    uint64_t secondary_rays;        /* reflection / refraction rays */
     uint32_t shadow_mask;
 } shade_ctx;
 
@@ -1315,10 +1316,39 @@ static v3 shade_lambert(shade_ctx* c, const oro_material* mat, const ray_t* r, c
     return vadd(L, V(mat->ka[0], mat->ka[1], mat->ka[2]));
 }
 
-/* Blinn::shade direct-lighting branch, src/Blinn.cpp:91-237,335 (reflect =
- * refract = 0, no maps, no path tracing, specGloss = 1, no translucency). */
-static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h) {
-    v3 Ld = V(0, 0, 0), Ls = V(0, 0, 0);
+/* Ray::IORList, src/Ray.h:43-50: [0] = 1, the camera ray pushes 1.001 (:99) */
+typedef struct { float v[12]; unsigned idx; } ior_list;
+
+static v3 shade_hit(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior, int bounces);
+
+/* Material::fresnel (full form, src/Material.h:47-55); sin/acos of the
+ * reference's libm evaluated in double and rounded once. */
+static float fresnel(float n1, float n2, float cosThetaI) {
+    const float n1CosTh = n1 * cosThetaI;
+    const float th = (float)acos((double)cosThetaI);
+    const float n1_n2SinTh = (n1 * (float)sin((double)th)) / n2;
+    const float n2CosTh = n2 * std_max(0.0f, sqrtf(1.0f - n1_n2SinTh * n1_n2SinTh));
+    const float Rs = (n1CosTh - n2CosTh) / (n1CosTh + n2CosTh);
+    return Rs * Rs;
+}
+
+/* Material::getEnvironmentColor, src/Material.cpp:44-62 (scene map or background) */
+static v3 env_color(const oro_scene* s, v3 d) {
+    if (s->env_tex >= 0) {
+        float e[3];
+        ibl_lookup_dir(&s->tex[s->env_tex], d.x, d.y, d.z, e);
+        return V(e[0] * s->env_exposure, e[1] * s->env_exposure, e[2] * s->env_exposure);
+    }
+    return s->bg;
+}
+
+/* Blinn::shade, src/Blinn.cpp:91-335: Fresnel-weighted Russian roulette between
+ * direct lighting and one reflection or refraction ray (bounces < 5), with the
+ * ray's IOR history (no maps, no path tracing, specGloss = 1, no translucency,
+ * no dispersion). */
+static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h, ior_list* ior,
+                      int bounces) {
+    v3 Ld = V(0, 0, 0), Ls = V(0, 0, 0), Lr = V(0, 0, 0), Lt = V(0, 0, 0);
     v3 rayD = V(r->d[0], r->d[1], r->d[2]);
     v3 viewDir = vneg(rayD);
     v3 N, geoN;
@@ -1329,25 +1359,87 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
     int nEqGeoN = ((double)(vDotN * vDotGeoN) >= 0.0);
     v3 theNormal = nEqGeoN ? N : geoN;
     vDotN = nEqGeoN ? vDotN : vDotGeoN;
-    if ((double)vDotN < 0.0) { vDotN = -vDotN; theNormal = vneg(theNormal); }
+    int flip = 0;
+    if ((double)vDotN < 0.0) { flip = 1; vDotN = -vDotN; theNormal = vneg(theNormal); }
     v3 rVec = vadd(rayD, vscale(theNormal, 2.0f * vDotN));
-    float rrFloat = next_rand(c);        /* Russian roulette draw, src/Blinn.cpp:195 */
-    (void)rrFloat;                        /* rrWeight == 1 -> always the direct branch */
+    float outIOR;
+    const float inIOR = ior->v[ior->idx];
+    if (flip) {             /* leaving the material: pop the ray's history */
+        if (ior->idx > 0) ior->idx--;
+        outIOR = ior->v[ior->idx];
+    } else {
+        outIOR = mat->ior;
+    }
+    float Rs = 0, Ts = 0;
+    if ((double)mat->reflect > 0.0 || (double)mat->refract > 0.0) {
+        Rs = fresnel(inIOR, outIOR, vDotN);
+        Ts = 1.0f - Rs;
+    }
+    float rrFloat = next_rand(c);        /* src/Blinn.cpp:195 */
+    float rrWeight = (1.0f - Rs * mat->reflect) - Ts * mat->refract;
+    float rrWeightRecip = (rrWeight > 0.f) ? 1.f / rrWeight : 1.f;
+    float rrWeightRecipSpec = (1.f - rrWeight > 0.f) ? 1.f / (1.f - rrWeight) : 1.f;
     v3 ks = V(mat->ks[0], mat->ks[1], mat->ks[2]);
     v3 kd = V(mat->kd[0], mat->kd[1], mat->kd[2]);
-    for (int i = 0; i < c->s->n_lights; i++) {
-        float lightSpec = 0;
-        v3 E = sample_light(c, i, P, theNormal, rVec, &lightSpec);
-        /* libm pow of the reference, evaluated in double and rounded once */
-        float pw = (float)pow((double)lightSpec, (double)mat->specExp);
-        Ls = vadd(Ls, vscale(vscale(vmul(E, ks), mat->specAmt), pw));
-        Ld = vadd(Ld, vmul(E, kd));
+    v3 zero = V(0, 0, 0);
+    if (rrFloat <= rrWeight) {
+        for (int i = 0; i < c->s->n_lights; i++) {
+            float lightSpec = 0;
+            v3 E = sample_light(c, i, P, theNormal, rVec, &lightSpec);
+            /* libm pow of the reference, evaluated in double and rounded once */
+            float pw = (float)pow((double)lightSpec, (double)mat->specExp);
+            Ls = vadd(Ls, vscale(vscale(vmul(E, ks), mat->specAmt), pw));
+            Ld = vadd(Ld, vmul(E, kd));
+        }
+    } else {
+        int doEnv = 1;
+        rrFloat = next_rand(c);
+        if (rrFloat < mat->reflect * Rs) {
+            if (mat->reflect * Rs > 0.0f && bounces < 5) {
+                ior_list child = *ior;
+                ray_t rr = make_ray(P, rVec);
+                hit_t nh = {1e12f, 0, 0, -1, -1};
+                uint32_t nv = 0, lv = 0;
+                c->secondary_rays++;
+                int hit = bvh_intersect(c->s, &rr, 0.001f, &nh, &nv, &lv) > 0;
+                c->nodes += nv; c->leaves += lv;
+                if (hit) {
+                    Lr = vadd(Lr, vmul(ks, shade_hit(c, &rr, &nh, &child, bounces + 1)));
+                    doEnv = 0;
+                }
+            }
+            if (mat->reflect * Rs > 0.0f && doEnv) Lr = vadd(Lr, vmul(ks, env_color(c->s, rVec)));
+        } else if (mat->refract * Ts > 0.0f) {
+            float snellsQ = inIOR / outIOR;
+            float sqrtPart = std_max(0.0f, sqrtf(1.0f - (snellsQ * snellsQ) * (1.0f - vDotN * vDotN)));
+            v3 tVec = vnormalized(vadd(vscale(rayD, snellsQ), vscale(theNormal, snellsQ * vDotN - sqrtPart)));
+            if (bounces < 5) {
+                ior_list child = *ior;     /* push, trace with the copy, pop */
+                child.v[++child.idx] = outIOR;
+                ray_t tr = make_ray(P, tVec);
+                hit_t nh = {1e12f, 0, 0, -1, -1};
+                uint32_t nv = 0, lv = 0;
+                c->secondary_rays++;
+                int hit = bvh_intersect(c->s, &tr, 0.001f, &nh, &nv, &lv) > 0;
+                c->nodes += nv; c->leaves += lv;
+                if (hit) {
+                    Lt = vadd(Lt, vmul(ks, shade_hit(c, &tr, &nh, &child, bounces + 1)));
+                    doEnv = 0;
+                }
+            }
+            if (doEnv) Lt = vadd(Lt, vmul(ks, env_color(c->s, tVec)));
+        }
     }
     Ld = vadd(Ld, V(mat->ka[0], mat->ka[1], mat->ka[2]));
-    v3 zero = V(0, 0, 0);
     /* (Ld + Ls + translucency)*rrWeightRecip + (Lr + Lt)*rrWeightRecipSpec + m_Le */
-    v3 res = vadd(vadd(vscale(vadd(vadd(Ld, Ls), zero), 1.0f), vscale(vadd(zero, zero), 1.0f)), zero);
-    return res;
+    return vadd(vadd(vscale(vadd(vadd(Ld, Ls), zero), rrWeightRecip), vscale(vadd(Lr, Lt), rrWeightRecipSpec)), zero);
+}
+
+/* Material::shade dispatch of a hit */
+static v3 shade_hit(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior, int bounces) {
+    int tri;
+    const oro_material* mat = &c->s->mats[hit_mesh(c->s, h, &tri)->material];
+    return mat->type == ORO_LAMBERT ? shade_lambert(c, mat, r, h) : shade_blinn(c, mat, r, h, ior, bounces);
 }
 
 /* ---------------------------------------------------------------- camera */
@@ -1430,7 +1522,9 @@ static v3 sample_scene(shade_ctx* c, const ray_t* r, hit_t* h, uint32_t* prim_nv
         int tri;
         const oro_material* mat = &s->mats[hit_mesh(s, h, &tri)->material];
         for (int i = 0; i < s->num_paths; i++) {
-            v3 sh = (mat->type == ORO_LAMBERT) ? shade_lambert(c, mat, r, h) : shade_blinn(c, mat, r, h);
+            ior_list ior;           /* the camera ray's history: 1, then 1.001 */
+            ior.v[0] = 1.0f; ior.v[1] = 1.001f; ior.idx = 1;
+            v3 sh = (mat->type == ORO_LAMBERT) ? shade_lambert(c, mat, r, h) : shade_blinn(c, mat, r, h, &ior, 0);
             result = vadd(result, sh);
         }
         return vscale(result, 1.0f / (float)s->num_paths);
@@ -1500,11 +1594,11 @@ int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H, int x0, 
     if (y1 > H) y1 = H;
     oro_gamma_table(NULL);
     cam_basis b = camera_basis(cam, W, H);
-    uint64_t prim = 0, shadowr = 0, nodes = 0, leaves = 0, pnodes = 0, pleaves = 0;
+    uint64_t prim = 0, shadowr = 0, nodes = 0, leaves = 0, pnodes = 0, pleaves = 0, second = 0;
     int err = 0;
 #ifdef _OPENMP
     if (n_threads < 1) n_threads = 1;
-#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads) reduction(+:prim,shadowr,nodes,leaves,pnodes,pleaves)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads) reduction(+:prim,shadowr,nodes,leaves,pnodes,pleaves,second)
 #endif
     for (int y = y0; y < y1; y++) {
         for (int x = x0; x < x1; x++) {
@@ -1523,13 +1617,13 @@ int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H, int x0, 
             if (rgb8) { rgb8[3 * p] = map_channel(col.x); rgb8[3 * p + 1] = map_channel(col.y); rgb8[3 * p + 2] = map_channel(col.z); }
             if (hitout) { hitout[p].t = h.t; hitout[p].a = h.a; hitout[p].b = h.b; hitout[p].prim = h.prim >= 0 ? hit_id(s, &h) : -1; }
             if (shadow) shadow[p] = c.shadow_mask;
-            prim += eye; shadowr += c.shadow_rays; nodes += nv + c.nodes; leaves += lv + c.leaves;
+            prim += eye; shadowr += c.shadow_rays; second += c.secondary_rays; nodes += nv + c.nodes; leaves += lv + c.leaves;
             pnodes += nv; pleaves += lv;
         }
     }
     if (counters) {
         counters[0] += prim; counters[1] += shadowr; counters[2] += nodes; counters[3] += leaves;
-        counters[4] += pnodes; counters[5] += pleaves;
+        counters[4] += pnodes; counters[5] += pleaves; counters[6] += second;
     }
     return err;
 }

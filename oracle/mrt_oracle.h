@@ -37,6 +37,8 @@ typedef struct {
     int type;               /* ORO_LAMBERT / ORO_BLINN                        */
     float kd[3], ka[3], ks[3];
     float specExp, specAmt; /* Blinn only (reference src/Blinn.h:11-22)       */
+    float reflect, refract; /* Blinn m_reflectAmt / m_refractAmt               */
+    float ior;              /* Blinn m_ior (src/Blinn.cpp:25-27)                */
 } oro_material;
 
 typedef struct {
@@ -107,11 +109,14 @@ int oro_trace(const oro_scene* s, size_t n, const float* o /*3n*/, const float* 
               uint32_t* node_visits, uint32_t* leaf_visits);
 
 /* Render rows [y0,y1) x columns [x0,x1) of a W x H frame (row 0 = bottom),
- * 1 spp, Scene::adaptiveSampleScene with min=max subdivs=1 (src/Scene.cpp:252-293).
+ * Scene::adaptiveSampleScene (src/Scene.cpp:252-293; 1 spp unless
+ * oro_scene_set_subdivs raised the subdivisions), Blinn reflection /
+ * refraction rays (src/Blinn.cpp:238-330) for materials with reflect / refract.
  * rgb: W*H*3 floats (before Image::Map), rgb8: W*H*3 (after Map), hit: W*H
  * primary hit records, shadow: W*H bitmask of occluded lights, may be NULL.
- * counters[6] (nullable) += {primary rays, shadow rays, node visits, leaf visits,
- *                            primary-ray node visits, primary-ray leaf visits}.
+ * counters[7] (nullable) += {primary rays, shadow rays, node visits, leaf visits,
+ *                            primary-ray node visits, primary-ray leaf visits,
+ *                            reflection + refraction rays}.
  * n_threads > 1 uses OpenMP over rows (the oracle is deterministic per pixel). */
 int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H,
                int x0, int y0, int x1, int y1,

@@ -33,7 +33,8 @@ def lib():
 
 class Material(C.Structure):
     _fields_ = [("type", C.c_int), ("kd", C.c_float * 3), ("ka", C.c_float * 3), ("ks", C.c_float * 3),
-                ("specExp", C.c_float), ("specAmt", C.c_float)]
+                ("specExp", C.c_float), ("specAmt", C.c_float),
+                ("reflect", C.c_float), ("refract", C.c_float), ("ior", C.c_float)]
 
 
 class Light(C.Structure):
@@ -142,8 +143,11 @@ class OracleScene:
         except Exception:
             pass
 
-    def add_material(self, kind="lambert", kd=(1, 1, 1), ka=(0, 0, 0), ks=(1, 1, 1), specExp=1.0, specAmt=0.0):
-        m = Material(0 if kind == "lambert" else 1, _v3(kd), _v3(ka), _v3(ks), specExp, specAmt)
+    def add_material(self, kind="lambert", kd=(1, 1, 1), ka=(0, 0, 0), ks=(1, 1, 1), specExp=1.0, specAmt=0.0,
+                     reflectAmt=0.0, refractAmt=0.0, ior=1.5):
+        """Lambert / Blinn (src/Blinn.h:11-22 defaults: ior 1.5, no reflection / refraction)."""
+        m = Material(0 if kind == "lambert" else 1, _v3(kd), _v3(ka), _v3(ks), specExp, specAmt,
+                     reflectAmt, refractAmt, ior)
         return self.L.oro_scene_add_material(self.h, C.byref(m))
 
     def add_obj(self, path, material, ctm=None):
@@ -322,7 +326,7 @@ class OracleScene:
         rgb8 = np.zeros((H, W, 3), np.uint8)
         hits = np.zeros((H, W), HIT_DTYPE) if want_hits else None
         shadow = np.zeros((H, W), np.uint32)
-        counters = np.zeros(6, np.uint64)
+        counters = np.zeros(7, np.uint64)
         r = self.L.oro_render(self.h, C.byref(c), W, H, x0, y0, x1, y1, _p(rgb, _fp), _p(rgb8, _u8p),
                               hits.ctypes.data if hits is not None else None, _p(shadow, _u32p),
                               _p(counters, _u64p), int(threads))
@@ -331,7 +335,8 @@ class OracleScene:
         return {"rgb": rgb, "rgb8": rgb8, "hits": hits, "shadow": shadow,
                 "primary_rays": int(counters[0]), "shadow_rays": int(counters[1]),
                 "node_visits": int(counters[2]), "leaf_visits": int(counters[3]),
-                "primary_node_visits": int(counters[4]), "primary_leaf_visits": int(counters[5])}
+                "primary_node_visits": int(counters[4]), "primary_leaf_visits": int(counters[5]),
+                "secondary_rays": int(counters[6])}
 
 
 def x86_rcp(x):

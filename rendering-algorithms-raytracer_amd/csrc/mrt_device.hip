@@ -43,7 +43,8 @@ enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLO
        // wall clocks as ~min start, max start, ~min end, max end (zero-initialised maxima)
        CTR_TP = 10, CTR_TS = 14,
        CTR_RAYS_P = 18,  // eye rays traced (adaptive supersampling; otherwise one per pixel)
-       CTR_N = 19 };
+       CTR_SECONDARY = 19,  // Blinn reflection / refraction rays
+       CTR_N = 20 };
 static constexpr int kMaxBlocksPerCU = 8;
 // wave log record: start, end, tiles, node visits, then (tile id << 40 | start tick) of the first kLogTiles
 // tiles, then the wall-clock ticks each of those tiles' dequeue took
@@ -91,6 +92,7 @@ struct RenderParams {
     CamParams cam[kMaxBatch];    // frame mode: cam[0]; batch mode: one camera per frame
     float bg[3];
     int32_t n_lights, num_paths;
+    int32_t recursive;           // a material reflects or refracts: Shader::shade_path
     uint32_t seed;
     int32_t fast_box;            // node boxes finite && tuning allows the hardware min/max box test
     int32_t sched;               // tile schedule (TileSched)
@@ -321,6 +323,12 @@ struct Shader {
         v3 result = mk(0, 0, 0);
         for (int path = 0; path < P.num_paths; path++) {
             v3 sh;
+            if constexpr (MODE == kFused) {
+                if (P.recursive) {   // reflective / refractive materials in the scene
+                    result = add(result, shade_path<COUNT>(r, h));
+                    continue;
+                }
+            }
             if (M.type == MRT_LAMBERT) {  // Lambert::shade
                 v3 L = mk(0, 0, 0);
                 for (int i = 0; i < P.n_lights; i++) {
@@ -355,6 +363,139 @@ struct Shader {
             result = add(result, sh);
         }
         return scale(result, 1.0f / (float)P.num_paths);
+    }
+
+    // Material::fresnel, full form (src/Material.h:47-55); the reference's libm
+    // acos / sin evaluated in double and rounded once (as in the oracle)
+    __device__ static float fresnel(float n1, float n2, float c) {
+        const float n1CosTh = n1 * c;
+        const float th = (float)acos((double)c);
+        const float n1_n2SinTh = (n1 * (float)sin((double)th)) / n2;
+        const float n2CosTh = n2 * std_max(0.0f, sqrtf(1.0f - n1_n2SinTh * n1_n2SinTh));
+        const float Rs = (n1CosTh - n2CosTh) / (n1CosTh + n2CosTh);
+        return Rs * Rs;
+    }
+
+    // Material::getEnvironmentColor (src/Material.cpp:44-62): scene map or background
+    __device__ v3 env_color(v3 d) {
+        if (P.env) return scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
+        return mk(P.bg[0], P.bg[1], P.bg[2]);
+    }
+
+    // Material::shade of one hit with Blinn's secondary rays (src/Blinn.cpp:91-335):
+    // Fresnel-weighted Russian roulette between direct lighting and one reflection
+    // or refraction ray (bounces < 5), with the ray's IOR history (Ray::IORList,
+    // src/Ray.h:43-50).  The recursion is a path (one child per level), so it runs
+    // as a loop: each level that spawns a ray which hits keeps its own terms
+    // (direct part x rrWeightRecip, ks, rrWeightRecipSpec, reflect / refract) and
+    // the levels are combined deepest first, in the reference's operation order.
+    static constexpr int kMaxBounce = 5;
+    uint32_t secondary = 0;
+    template <bool COUNT>
+    __device__ v3 shade_path(DRay r, DHit h) {
+        const v3 z = mk(0, 0, 0);
+        v3 lvA[kMaxBounce], lvKs[kMaxBounce];
+        float lvW[kMaxBounce];
+        bool lvRefr[kMaxBounce];
+        float ior[kMaxBounce + 3];   // [0] = 1, the camera ray pushes 1.001, one push per refraction level
+        ior[0] = 1.0f; ior[1] = 1.001f;
+        int idx = 1, depth = 0;
+        v3 val;
+        for (;;) {
+            v3 N, geoN;
+            uint32_t mi;
+            normals(h, N, geoN, mi);
+            const DevMaterial& M = P.mats[mi];
+            const v3 Pt = mk(r.o[0] + h.t * r.d[0], r.o[1] + h.t * r.d[1], r.o[2] + h.t * r.d[2]);
+            const v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+            if (M.type == MRT_LAMBERT) {   // Lambert::shade: no secondary rays
+                v3 L = z;
+                for (int i = 0; i < P.n_lights; i++) {
+                    float discard;
+                    L = add(L, mul(sample_light<COUNT>(i, Pt, N, z, discard), kd));
+                }
+                val = add(L, ka);
+                break;
+            }
+            const v3 rayD = mk(r.d[0], r.d[1], r.d[2]);
+            const v3 viewDir = neg(rayD);
+            float vDotN = dot(viewDir, N);
+            const float vDotGeoN = dot(viewDir, geoN);
+            const bool same = (vDotN * vDotGeoN) >= 0.0f;
+            v3 n = same ? N : geoN;
+            vDotN = same ? vDotN : vDotGeoN;
+            bool flip = false;
+            if (vDotN < 0.0f) { flip = true; vDotN = -vDotN; n = neg(n); }
+            const v3 rVec = add(rayD, scale(n, 2.0f * vDotN));
+            const float inIOR = ior[idx];
+            float outIOR = M.ior;
+            if (flip) {   // leaving the material: pop the history
+                if (idx > 0) idx--;
+                outIOR = ior[idx];
+            }
+            float Rs = 0.f, Ts = 0.f;
+            if (M.reflect > 0.0f || M.refract > 0.0f) {
+                Rs = fresnel(inIOR, outIOR, vDotN);
+                Ts = 1.0f - Rs;
+            }
+            float rr = next_rand();
+            const float rrW = (1.0f - Rs * M.reflect) - Ts * M.refract;
+            const float rrRecip = (rrW > 0.f) ? 1.f / rrW : 1.f;
+            const float rrSpec = (1.f - rrW > 0.f) ? 1.f / (1.f - rrW) : 1.f;
+            const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
+            if (rr <= rrW) {   // direct lighting
+                v3 Ld = z, Ls = z;
+                for (int i = 0; i < P.n_lights; i++) {
+                    float spec = 0.f;
+                    v3 E = sample_light<COUNT>(i, Pt, n, rVec, spec);
+                    float pw = (M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
+                    Ls = add(Ls, scale(scale(mul(E, ks), M.spec_amt), pw));
+                    Ld = add(Ld, mul(E, kd));
+                }
+                Ld = add(Ld, ka);
+                val = add(add(scale(add(add(Ld, Ls), z), rrRecip), scale(add(z, z), rrSpec)), z);
+                break;
+            }
+            const v3 base = scale(add(add(add(z, ka), z), z), rrRecip);   // (Ld + Ls + translucency) * rrWeightRecip
+            rr = next_rand();
+            bool refr, spawn;
+            v3 dir;
+            if (rr < M.reflect * Rs) {
+                refr = false;
+                dir = rVec;
+                spawn = M.reflect * Rs > 0.0f && depth < kMaxBounce;
+            } else if (M.refract * Ts > 0.0f) {
+                refr = true;
+                const float q = inIOR / outIOR;
+                const float sq = std_max(0.0f, sqrtf(1.0f - (q * q) * (1.0f - vDotN * vDotN)));
+                dir = normalized(add(scale(rayD, q), scale(n, q * vDotN - sq)), rsqT);
+                spawn = depth < kMaxBounce;
+            } else {   // refraction branch with nothing to refract: Lr = Lt = 0
+                val = add(add(base, scale(add(z, z), rrSpec)), z);
+                break;
+            }
+            if (spawn) {
+                const DRay r2 = make_ray(Pt, dir);
+                DHit h2{1e12f, 0.f, 0.f, -1};
+                secondary++;
+                if (traverse<false, COUNT, FAST, INST>(T, r2, 0.001f, h2, st)) {
+                    lvA[depth] = base; lvKs[depth] = ks; lvW[depth] = rrSpec; lvRefr[depth] = refr;
+                    depth++;
+                    if (refr) ior[++idx] = outIOR;   // the child's history: push (the parent pops after)
+                    r = r2;
+                    h = h2;
+                    continue;
+                }
+            }
+            const v3 L = add(z, mul(ks, env_color(dir)));   // Lr / Lt += m_ks * environment
+            val = add(add(base, scale(refr ? add(z, L) : add(L, z), rrSpec)), z);
+            break;
+        }
+        for (int k = depth - 1; k >= 0; k--) {   // Lr / Lt += m_ks * shade(child)
+            const v3 L = add(z, mul(lvKs[k], val));
+            val = add(add(lvA[k], scale(lvRefr[k] ? add(z, L) : add(L, z), lvW[k])), z);
+        }
+        return val;
     }
 };
 
@@ -519,6 +660,13 @@ __device__ __forceinline__ void flush_stats(const RenderParams& P, const TravSta
     if (st.overflow) atomicOr(&P.ctr[CTR_OVERFLOW], 1ull);
 }
 
+// reflection / refraction rays of a wave (Shader::shade_path), always counted
+__device__ __forceinline__ void flush_secondary(const RenderParams& P, uint32_t n, int lane) {
+    unsigned long long v = n;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+    if (lane == 0 && v) atomicAdd(&P.ctr[CTR_SECONDARY], v);
+}
+
 // Camera::eyeRayAdaptive(x, y, .5, .5, .5, .5) (src/Camera.cpp:116-157): two
 // jitter draws (dims 0, 1; the offsets are exactly 0.5) and the time draw (dim 2,
 // unused).  Deterministic, so kernel 2 recomputes it instead of storing it.
@@ -594,7 +742,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     TravStats st;
-    uint32_t shadow_total = 0;
+    uint32_t shadow_total = 0, secondary_total = 0;
     TileSched ts(P, wave, lane);
     uint32_t ntiles = 0;
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
@@ -623,6 +771,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
                                                    slot * (size_t)P.max_shadow, 0u};
             col = S.template shade<COUNT>(r, h);
             shadow_total += S.shadow_rays;
+            secondary_total += S.secondary;
             if (MODE == kGen) P.nrays[slot] = (uint8_t)S.nslot;
         } else if (MODE == kGen) {
             P.nrays[slot] = 0;
@@ -644,6 +793,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
         }
     }
+    flush_secondary(P, secondary_total, lane);
     flush_stats<COUNT>(P, st, MODE == kResolve ? 0u : shadow_total, lane, t0, ntiles);
 }
 
@@ -679,7 +829,7 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     TravStats st;
-    uint32_t shadow_total = 0, eye_rays = 0, eye_hits = 0;
+    uint32_t shadow_total = 0, eye_rays = 0, eye_hits = 0, secondary_total = 0;
     TileSched ts(P, wave, lane);
     uint32_t ntiles = 0;
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
@@ -721,6 +871,7 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
                 S.sample = sample;
                 col = S.template shade<COUNT>(r, h);
                 shadow_total += S.shadow_rays;
+                secondary_total += S.secondary;
             } else if (P.env) {
                 col = scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
             } else {
@@ -765,6 +916,7 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
         atomicAdd(&P.ctr[CTR_RAYS_P], er);
         atomicAdd(&P.ctr[CTR_HITS], eh);
     }
+    flush_secondary(P, secondary_total, lane);
     flush_stats<COUNT, false>(P, st, shadow_total, lane, t0, ntiles);
 }
 
@@ -1024,6 +1176,7 @@ struct DeviceState {
     bool boxes_finite = false;
     int cus = 0;
     bool point_only = false;
+    bool recursive = false;      // a material reflects or refracts (fused shading with shade_path)
     int wall_khz = 0;            // wall_clock64() rate
     size_t bytes = 0;
     // per-stream launch scratch: frames on different streams are in flight at once
@@ -1251,6 +1404,8 @@ static int ensure_device(Scene& s, int device) {
         for (int k = 0; k < 24; k++) d.boxes_finite &= std::isfinite(q.box[k]);
     d.point_only = true;
     for (const DevLight& l : s.lights) d.point_only &= (l.type == MRT_POINT_LIGHT);
+    d.recursive = false;
+    for (const DevMaterial& m : s.materials) d.recursive |= m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f);
     d.gthreads = (uint32_t)d.grid * kWG;
     s.info.device_bytes = total;
     s.dev_dirty = false;
@@ -1300,6 +1455,7 @@ static void fill_params(const Scene& s, RenderParams& P) {
     P.bg[0] = s.bg[0]; P.bg[1] = s.bg[1]; P.bg[2] = s.bg[2];
     P.n_lights = (int32_t)s.lights.size();
     P.num_paths = s.num_paths;
+    P.recursive = d.recursive ? 1 : 0;
 }
 
 static inline int fast_box(const DeviceState& d) { return (g_fast_box && d.boxes_finite) ? 1 : 0; }
@@ -1470,9 +1626,10 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst)))) return rc;
     HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
-    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst;
+    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst && !d.recursive;
     const int max_sh = max_shadow_rays(s);
-    const bool wave = !one && g_wavefront && max_sh > 0 && max_sh <= kMaxWaveShadow;
+    // secondary rays and their shadow rays depend on hits along the path: fused kernel
+    const bool wave = !one && g_wavefront && max_sh > 0 && max_sh <= kMaxWaveShadow && !d.recursive;
     if (one || !wave) {
         if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb, inst)))) return rc;
     } else {
@@ -1529,6 +1686,7 @@ int mrt_scene_add_material(mrt_scene* s, const mrt_material* m) {
     d.type = m->type;
     memcpy(d.kd, m->kd, 12); memcpy(d.ka, m->ka, 12); memcpy(d.ks, m->ks, 12);
     d.spec_exp = m->spec_exp; d.spec_amt = m->spec_amt;
+    d.reflect = 0.f; d.refract = 0.f; d.ior = 1.5f;   // Blinn defaults (src/Blinn.h:11-22)
     s->impl.materials.push_back(d);
     s->impl.dev_dirty = true;
     return (int)s->impl.materials.size() - 1;
@@ -1756,6 +1914,20 @@ int mrt_scene_set_num_paths(mrt_scene* s, int num_paths) {
     return MRT_OK;
 }
 
+int mrt_scene_set_material_optics(mrt_scene* s, int material, float reflect_amt, float refract_amt, float ior) {
+    if (!s || material < 0 || material >= (int)s->impl.materials.size() || !(reflect_amt >= 0.f) ||
+        !(refract_amt >= 0.f) || !(ior > 0.f)) {
+        set_error("bad material optics: need a valid material, reflect / refract >= 0 and ior > 0");
+        return MRT_ERR_INVALID;
+    }
+    DevMaterial& m = s->impl.materials[(size_t)material];
+    m.reflect = reflect_amt;
+    m.refract = refract_amt;
+    m.ior = ior;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
 int mrt_scene_set_subdivs(mrt_scene* s, int min_subdivs, int max_subdivs, float noise_threshold) {
     if (!s || min_subdivs < 1 || max_subdivs < min_subdivs || max_subdivs > 16 || !(noise_threshold >= 0.f)) {
         set_error("bad subdivs: need 1 <= min <= max <= 16 and noise >= 0");
@@ -1976,7 +2148,8 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     S.last.primary_leaf_visits = c[CTR_LEAVES_P];
     S.last.shadow_rays = c[CTR_SHADOW];
     S.last.primary_hits = c[CTR_HITS];
-    if (c[CTR_RAYS_P]) S.last.primary_rays = c[CTR_RAYS_P];   // adaptive supersampling: eye rays traced
+    if (c[CTR_RAYS_P]) S.last.primary_rays = c[CTR_RAYS_P];
+    S.last.secondary_rays = c[CTR_SECONDARY];   // adaptive supersampling: eye rays traced
     S.last.primary_wave_steps = c[CTR_WAVE_STEPS_P];
     S.last.primary_uniform_visits = c[CTR_UNIFORM_P];
     S.last.node_visits = c[CTR_NODES];

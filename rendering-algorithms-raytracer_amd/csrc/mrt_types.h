@@ -57,6 +57,8 @@ struct DevMaterial {
     int32_t type;
     float kd[3], ka[3], ks[3];
     float spec_exp, spec_amt;
+    float reflect, refract;  // Blinn m_reflectAmt / m_refractAmt (src/Blinn.h:62, src/Material.h:73)
+    float ior;               // Blinn m_ior (src/Blinn.cpp:25-27)
 };
 
 struct DevLight {

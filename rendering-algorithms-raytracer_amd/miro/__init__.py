@@ -131,15 +131,21 @@ class Lambert:
 
 
 class Blinn:
-    """Blinn(kd, ka, ks, kt, ior, specExp, specAmt, ...) defaults of src/Blinn.h:11-22.
-    Direct lighting only (reflect/refract/path tracing are SURVEY §8(f) rank 4)."""
+    """Blinn(kd, ka, ks, kt, ior, specExp, specAmt, reflectAmt, refractAmt) defaults of
+    src/Blinn.h:11-22: direct lighting plus Fresnel-weighted reflection / refraction
+    rays (src/Blinn.cpp:91-335).  Path tracing, gloss < 1, translucency, dispersion
+    and texture maps are not on the MI355X path."""
 
     def __init__(self, kd=Vector3(1), ka=Vector3(0), ks=Vector3(1), kt=Vector3(0), ior=1.5,
                  specExp=1.0, specAmt=0.0, reflectAmt=0.0, refractAmt=0.0):
         self.kd, self.ka, self.ks, self.kt = Vector3(kd), Vector3(ka), Vector3(ks), Vector3(kt)
         self.ior, self.specExp, self.specAmt = float(ior), float(specExp), float(specAmt)
-        if reflectAmt or refractAmt:
-            raise NotImplementedError("Blinn reflection/refraction is not on the MI355X path yet")
+        self.reflectAmt, self.refractAmt = float(reflectAmt), float(refractAmt)
+
+    def setReflectAmt(self, a): self.reflectAmt = float(a)     # src/Blinn.h:41
+    def setRefractAmt(self, a): self.refractAmt = float(a)     # src/Material.h:32
+    def setIor(self, ior, i=0):                                # src/Blinn.h:38 (m_ior[1] is used)
+        self.ior = float(ior)
 
     def setKd(self, v): self.kd = Vector3(v)
     def setKa(self, v): self.ka = Vector3(v)
@@ -394,6 +400,9 @@ class Scene:
             if id(mat) not in mats:
                 m = mat._c()
                 mats[id(mat)] = check(L.mrt_scene_add_material(self._h, C.byref(m)), "add_material")
+                if isinstance(mat, Blinn):
+                    check(L.mrt_scene_set_material_optics(self._h, mats[id(mat)], mat.reflectAmt, mat.refractAmt,
+                                                          mat.ior), "material optics")
             mid = mats[id(mat)]
             if mesh.path is not None:
                 ctm = mesh.ctm.ctypes.data_as(C.POINTER(C.c_float)) if mesh.ctm is not None else None
