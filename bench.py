@@ -93,7 +93,9 @@ def cpu_baseline(cfg_key, seconds):
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     s = O.OracleScene()
     mat = cfg["material"]
-    m = s.add_material(mat["kind"], kd=mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0))
+    m = s.add_material(mat["kind"], kd=mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0),
+                       reflectAmt=mat.get("reflectAmt", 0.0), refractAmt=mat.get("refractAmt", 0.0),
+                       ior=mat.get("ior", 1.5))
     if cfg["mesh"] == "sponza":
         s.add_obj(scenes.sponza_obj(), m)
     elif cfg["mesh"] in ("bunny", "instances"):
@@ -138,7 +140,7 @@ def cpu_baseline(cfg_key, seconds):
         t0 = time.perf_counter()
         r = s.render(cfg["camera"], W, H, rect=(0, y0, W, min(H, y0 + band)), threads=threads, want_hits=False)
         t_total += time.perf_counter() - t0
-        rays += r["primary_rays"] + r["shadow_rays"]
+        rays += r["primary_rays"] + r["shadow_rays"] + r["secondary_rays"]
         y += band
         frames += 1
     return {"value": round(rays / t_total / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
@@ -231,14 +233,15 @@ def main():
     # adaptive supersampling (subdivs > 1): eye rays per pixel vary, counted by the kernel
     adaptive = bool(cfg.get("subdivs")) and max(cfg["subdivs"][:2]) > 1
     eye_mine = st["primary_rays"] if adaptive else 0
+    second_mine = st["secondary_rays"]   # Blinn reflection / refraction rays
     if world > 1:
-        t = torch.tensor([shadow_mine, eye_mine], dtype=torch.float64, device="cuda")
+        t = torch.tensor([shadow_mine, eye_mine, second_mine], dtype=torch.float64, device="cuda")
         dist.all_reduce(t)
-        shadow_total, eye_total = int(t[0].item()), int(t[1].item())
+        shadow_total, eye_total, second_total = int(t[0].item()), int(t[1].item()), int(t[2].item())
     else:
-        shadow_total, eye_total = shadow_mine, eye_mine
+        shadow_total, eye_total, second_total = shadow_mine, eye_mine, second_mine
     primary_total = eye_total if adaptive else n_frames * W * H
-    rays_per_step = primary_total + shadow_total      # all frames of the batch, all ranks
+    rays_per_step = primary_total + shadow_total + second_total      # all frames of the batch, all ranks
     hits_px = st["primary_hits"]
 
     for _ in range(args.warmup):
@@ -281,11 +284,17 @@ def main():
     px_mine = W * H if use_frame_path else _pixels_in_frame(sorted(set(mine)), bpf, bx, W, H)
     hits_mine = hits_px
     # the specialised kernel runs for one point light, one path and no environment map
+    mat = cfg["material"]
+    recursive = mat["kind"] == "blinn" and (mat.get("reflectAmt", 0) > 0 or mat.get("refractAmt", 0) > 0)
     one_light = (len(cfg["lights"]) == 1 and cfg["lights"][0]["type"] == "point" and cfg.get("num_paths", 1) == 1
-                 and not cfg.get("env"))
-    b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=use_frame_path, wavefront=not one_light)
+                 and not cfg.get("env") and not recursive)
+    b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=use_frame_path,
+                                   wavefront=not one_light and not recursive)
+    if recursive:   # each secondary hit gathers its PrimShade + 3 vertices + 3 normals
+        b_shade += second_mine * (16 + 32 + 3 * 16 + 3 * 16)
     pm, sm = float(np.median(prim_ms)), float(np.median(shade_ms))
     shade_name = ("shade1_kernel (shade + any-hit shadow rays)" if one_light else
+                  "shade_kernel (fused: shade + reflection/refraction rays + any-hit shadow rays)" if recursive else
                   "shade pass (shade_kernel<gen> + shadow_kernel any-hit + shade_kernel<resolve>)")
     if adaptive:   # one fused launch: eye rays, shading, inline shadow rays (its time is shade_ms)
         dom, dom_ms = "adaptive_kernel (eye rays + shading + any-hit shadow rays)", sm
@@ -307,7 +316,7 @@ def main():
             traffic = None
     out = {
         "metric": ("Mray/s (primary+shadow) on Sponza 1920x1080" if args.config == "C3" else
-                   f"Mray/s (primary+shadow) [{args.config}: {cfg['name']}]"),
+                   f"Mray/s (primary+shadow{'+secondary' if second_total else ''}) [{args.config}: {cfg['name']}]"),
         "value": round(value, 2), "unit": "Mray/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
@@ -319,6 +328,7 @@ def main():
         "config": {"workload": cfg["name"], "config": args.config, "width": W, "height": H, "spp": 1 if not adaptive else f"adaptive {cfg['subdivs'][0]}..{cfg['subdivs'][1]} subdivs, "
                    f"{primary_total / (n_frames * W * H):.2f} eye rays/px",
                    "frames_per_step": n_frames, "rays_per_step": rays_per_step, "shadow_rays": shadow_total,
+                   "secondary_rays": second_total,
                    "qbvh_nodes": scene.bvh_info["nodes"], "qbvh_leaves": scene.bvh_info["leaves"],
                    "frames_in_flight": inflight,
                    "parallelism": "single GPU, whole frame" if use_frame_path else
@@ -327,7 +337,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(dom_b),
-                     "visits_per_ray": round(st["node_visits"] / max(1, (eye_mine if adaptive else px_mine) + shadow_mine), 3)},
+                     "visits_per_ray": round(st["node_visits"] / max(1, (eye_mine if adaptive else px_mine) + shadow_mine + second_mine), 3)},
         "launch_ms": {"primary": round(pm, 4), "shade": round(sm, 4)},
         # instrumented (count-mode) launch: wall-clock spread of the persistent waves
         "wave_timing_us": {k: round(st[k], 1) for k in ("primary_span_us", "primary_ramp_us", "primary_tail_us",

@@ -92,7 +92,6 @@ struct RenderParams {
     CamParams cam[kMaxBatch];    // frame mode: cam[0]; batch mode: one camera per frame
     float bg[3];
     int32_t n_lights, num_paths;
-    int32_t recursive;           // a material reflects or refracts: Shader::shade_path
     uint32_t seed;
     int32_t fast_box;            // node boxes finite && tuning allows the hardware min/max box test
     int32_t sched;               // tile schedule (TileSched)
@@ -128,7 +127,10 @@ __device__ __forceinline__ v3 xform_dir3(const float* T, v3 u) {
               T[8] * u.x + T[9] * u.y + T[10] * u.z);
 }
 
-template <bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused>
+// REC: the scene has reflective / refractive materials (Blinn secondary rays,
+// shade_path); compiled only into the kernels that run such scenes, so the
+// direct-lighting kernels keep their register budget.
+template <bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused, bool REC = false>
 struct Shader {
     const RenderParams& P;
     const Trav& T;
@@ -323,11 +325,9 @@ struct Shader {
         v3 result = mk(0, 0, 0);
         for (int path = 0; path < P.num_paths; path++) {
             v3 sh;
-            if constexpr (MODE == kFused) {
-                if (P.recursive) {   // reflective / refractive materials in the scene
-                    result = add(result, shade_path<COUNT>(r, h));
-                    continue;
-                }
+            if constexpr (MODE == kFused && REC) {   // reflective / refractive materials in the scene
+                result = add(result, shade_path<COUNT>(r, h));
+                continue;
             }
             if (M.type == MRT_LAMBERT) {  // Lambert::shade
                 v3 L = mk(0, 0, 0);
@@ -730,7 +730,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
 }
 
 // Kernel 2: Scene::sampleScene shading of the primary hit with shadow rays.
-template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused>
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused, bool REC = false>
 __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -767,7 +767,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             const CamParams& cam = P.cam[f];
             const uint32_t seed = P.seed + (uint32_t)f;
             DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, seed, x, y, rsqT));
-            Shader<POINT_ONLY, FAST, INST, MODE> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u, seed,
+            Shader<POINT_ONLY, FAST, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u, seed,
                                                    slot * (size_t)P.max_shadow, 0u};
             col = S.template shade<COUNT>(r, h);
             shadow_total += S.shadow_rays;
@@ -817,7 +817,7 @@ __device__ __forceinline__ float gamma_f(const float* lut, float v) {
 // gamma-space stop test after every level.  Eye ray k of a pixel draws from
 // RNG stream (pixel, k): ray 0 is the 1-spp frame path's ray.  Lanes of a wave
 // stop independently; the wave runs until its last lane is done.
-template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST>
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST, bool REC = false>
 __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -867,7 +867,7 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
             if (sample == 0) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
             if (hit) {
                 eye_hits++;
-                Shader<POINT_ONLY, FAST, INST, kFused> S{P, T, rcpT, rsqT, st, pixel, 3u, 0u, seed, 0, 0u};
+                Shader<POINT_ONLY, FAST, INST, kFused, REC> S{P, T, rcpT, rsqT, st, pixel, 3u, 0u, seed, 0, 0u};
                 S.sample = sample;
                 col = S.template shade<COUNT>(r, h);
                 shadow_total += S.shadow_rays;
@@ -1455,7 +1455,6 @@ static void fill_params(const Scene& s, RenderParams& P) {
     P.bg[0] = s.bg[0]; P.bg[1] = s.bg[1]; P.bg[2] = s.bg[2];
     P.n_lights = (int32_t)s.lights.size();
     P.num_paths = s.num_paths;
-    P.recursive = d.recursive ? 1 : 0;
 }
 
 static inline int fast_box(const DeviceState& d) { return (g_fast_box && d.boxes_finite) ? 1 : 0; }
@@ -1553,7 +1552,15 @@ static int max_shadow_rays(const Scene& s) {
     return s.num_paths * per_path;
 }
 
-static KernelFn pick_shade(bool c, bool po, bool f, bool inst) {
+static KernelFn pick_shade(bool c, bool po, bool f, bool inst, bool rec) {
+    if (rec) {   // secondary rays, fused shadow rays (instanced: general light loop)
+        if (inst) return c ? (f ? shade_kernel<true, false, true, true, kFused, true> : shade_kernel<true, false, false, true, kFused, true>)
+                           : (f ? shade_kernel<false, false, true, true, kFused, true> : shade_kernel<false, false, false, true, kFused, true>);
+        if (po) return c ? (f ? shade_kernel<true, true, true, false, kFused, true> : shade_kernel<true, true, false, false, kFused, true>)
+                         : (f ? shade_kernel<false, true, true, false, kFused, true> : shade_kernel<false, true, false, false, kFused, true>);
+        return c ? (f ? shade_kernel<true, false, true, false, kFused, true> : shade_kernel<true, false, false, false, kFused, true>)
+                 : (f ? shade_kernel<false, false, true, false, kFused, true> : shade_kernel<false, false, false, false, kFused, true>);
+    }
     if (inst) return c ? (f ? shade_kernel<true, false, true, true> : shade_kernel<true, false, false, true>)
                        : (f ? shade_kernel<false, false, true, true> : shade_kernel<false, false, false, true>);
     if (po) return c ? (f ? shade_kernel<true, true, true> : shade_kernel<true, true, false>)
@@ -1562,7 +1569,15 @@ static KernelFn pick_shade(bool c, bool po, bool f, bool inst) {
              : (f ? shade_kernel<false, false, true> : shade_kernel<false, false, false>);
 }
 
-static KernelFn pick_adaptive(bool c, bool po, bool f, bool inst) {
+static KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, bool rec) {
+    if (rec) {   // secondary rays (instanced: general light loop)
+        if (inst) return c ? (f ? adaptive_kernel<true, false, true, true, true> : adaptive_kernel<true, false, false, true, true>)
+                           : (f ? adaptive_kernel<false, false, true, true, true> : adaptive_kernel<false, false, false, true, true>);
+        if (po) return c ? (f ? adaptive_kernel<true, true, true, false, true> : adaptive_kernel<true, true, false, false, true>)
+                         : (f ? adaptive_kernel<false, true, true, false, true> : adaptive_kernel<false, true, false, false, true>);
+        return c ? (f ? adaptive_kernel<true, false, true, false, true> : adaptive_kernel<true, false, false, false, true>)
+                 : (f ? adaptive_kernel<false, false, true, false, true> : adaptive_kernel<false, false, false, false, true>);
+    }
     if (inst) return c ? (f ? adaptive_kernel<true, false, true, true> : adaptive_kernel<true, false, false, true>)
                        : (f ? adaptive_kernel<false, false, true, true> : adaptive_kernel<false, false, false, true>);
     if (po) return c ? (f ? adaptive_kernel<true, true, true, false> : adaptive_kernel<true, true, false, false>)
@@ -1615,7 +1630,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     const bool inst = d.n_insts > 0;
     if (P.min_subdivs > 1 || P.max_subdivs > 1) {
         HIP_OK(hipEventRecord(c.evm, stream));   // primary_ms = 0: one launch
-        if ((rc = launch(pick_adaptive(count, d.point_only, fb, inst)))) return rc;
+        if ((rc = launch(pick_adaptive(count, d.point_only, fb, inst, d.recursive)))) return rc;
         c.last_was_render = true;
         HIP_OK(hipGetLastError());
         HIP_OK(hipEventRecord(c.ev1, stream));
@@ -1631,7 +1646,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     // secondary rays and their shadow rays depend on hits along the path: fused kernel
     const bool wave = !one && g_wavefront && max_sh > 0 && max_sh <= kMaxWaveShadow && !d.recursive;
     if (one || !wave) {
-        if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb, inst)))) return rc;
+        if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb, inst, d.recursive)))) return rc;
     } else {
         if ((rc = ensure_rays(c, slots, (size_t)max_sh))) return rc;
         P.ray_o = c.rays;

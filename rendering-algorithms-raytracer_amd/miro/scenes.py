@@ -369,6 +369,16 @@ CONFIGS = {
                lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
                material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza",
                subdivs=(1, 4, 0.01)),
+    # R3: C3 with Whitted-style secondary rays: a Blinn material that reflects
+    # (reflectAmt 0.5) and refracts (refractAmt 0.5, ior 1.5), Blinn::shade's
+    # Fresnel-weighted roulette between direct light and one secondary ray per
+    # level, up to 5 bounces (src/Blinn.cpp:180-330)
+    "R3": dict(name="sponza stand-in (~66k tris) 1920x1080 Blinn reflect+refract (Fresnel roulette, 5 bounces)+PointLight",
+               W=1920, H=1080,
+               camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
+               lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
+               material=dict(kind="blinn", kd=(1, 1, 1), reflectAmt=0.5, refractAmt=0.5, ior=1.5),
+               bg=(0.0, 0.0, 0.2), mesh="sponza"),
     # C4: Sponza stand-in, RectangleLight (8,10,2)/(8,10,-2)/(-8,10,2) power 1.5 and
     # Scene::m_numPaths = 16 (makeSponzaScenePathTrace, src/assignment2.h:663-708, direct
     # lighting only): 16 shade() calls per hit, one area-light shadow ray each;
@@ -426,7 +436,8 @@ def build_config(key, device=0):
     scene = miro.Scene(device=device)
     mat = cfg["material"]
     material = miro.Lambert(mat["kd"]) if mat["kind"] == "lambert" else \
-        miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0))
+        miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0),
+                   reflectAmt=mat.get("reflectAmt", 0.0), refractAmt=mat.get("refractAmt", 0.0), ior=mat.get("ior", 1.5))
     mesh = miro.TriangleMesh()
     if cfg["mesh"] == "cornell":
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
