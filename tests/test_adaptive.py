@@ -148,3 +148,30 @@ def test_adaptive_count_mode_is_exact():
     assert np.array_equal(bits(img.rgb), bits(ref["rgb"]))
     assert ref["primary_node_visits"] < P.last_stats["node_visits"] <= ref["node_visits"]
     assert P.last_stats["primary_rays"] == ref["primary_rays"]
+
+
+@pytest.mark.gpu
+def test_adaptive_bucket_batch_equals_frame():
+    """The multi-GPU path (32x32 buckets dealt to ranks, mrt_render_batch_async)
+    renders adaptive frames bit-identically to the whole-frame launch."""
+    torch = pytest.importorskip("torch")
+    import ctypes as C
+    from miro import _lib
+    P, _, cam = oracle_c1((1, 3, 0.01), kind="blinn")
+    W, H = 70, 45
+    img, _ = gpu_render(P, cam, W, H)
+    bpf = ((W + 31) // 32) * ((H + 31) // 32)
+    order = np.random.default_rng(3).permutation(bpf).tolist()
+    ids = torch.tensor(order, dtype=torch.int32, device="cuda")
+    tiles = torch.zeros(bpf * 1024 * 3, dtype=torch.float32, device="cuda")
+    frame = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+    camc = (_lib.mrt_camera * 1)(camera(cam)._c())
+    opts = _lib.mrt_render_opts(W, H, 0, 0, 0, 0, 0)
+    L = miro.lib()
+    stream = torch.cuda.current_stream().cuda_stream
+    _lib.check(L.mrt_render_batch_async(P.handle, camc, 1, C.byref(opts), ids.data_ptr(), bpf, tiles.data_ptr(),
+                                        None, stream), "batch")
+    _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), bpf, tiles.data_ptr(), None, W, H, 1, frame.data_ptr(),
+                                        None, P.handle, stream), "unpack")
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(frame.cpu().numpy().reshape(H, W, 3)), bits(img.rgb))
