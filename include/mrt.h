@@ -152,6 +152,10 @@ int mrt_scene_set_num_paths(mrt_scene* s, int num_paths);
  * Fresnel-weighted Russian roulette, at most 5 bounces, IOR history per ray.
  * No effect on Lambert materials. */
 int mrt_scene_set_material_optics(mrt_scene* s, int material, float reflect_amt, float refract_amt, float ior);
+/* Blinn::setReflectGloss (src/Blinn.h:42; default 1): below 1 the reflection
+ * vector is blended with a cosine-distributed sample
+ * (Material::getCosineDistributedSamples, src/Material.cpp:14-41; src/Blinn.cpp:166-171). */
+int mrt_scene_set_material_gloss(mrt_scene* s, int material, float gloss);
 /* Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55; defaults
  * 1, 1, 0.01 at src/Scene.cpp:20-22): adaptive supersampling of
  * Scene::adaptiveSampleScene (src/Scene.cpp:252-293).  With both counts 1 a

@@ -1332,6 +1332,21 @@ static float fresnel(float n1, float n2, float cosThetaI) {
     return Rs * Rs;
 }
 
+/* Material::getCosineDistributedSamples, src/Material.cpp:14-41 (SSE path);
+ * libm cos / sin evaluated in double and rounded once. */
+static v3 cosine_sample(shade_ctx* c, v3 N) {
+    const float e1 = next_rand(c);
+    float e2 = next_rand(c);
+    e2 = ((double)e2 > 0.99) ? (float)0.99 : e2;
+    v3 u = vnormalized(vcross(((double)fabsf(N.x) > 0.1) ? V(0, 1, 0) : V(1, 0, 0), N));
+    v3 v = vcross(N, u);
+    float _2_PI_e1 = 2 * PI_F * e1;
+    float sqrte2 = rcp_nr(rsqrt_nr(e2));
+    float sqrt1_e2 = rcp_nr(rsqrt_nr(fabsf(1.0f - e2)));
+    float cs = (float)cos((double)_2_PI_e1), sn = (float)sin((double)_2_PI_e1);
+    return vnormalized(vadd(vadd(vscale(u, cs * sqrte2), vscale(v, sn * sqrte2)), vscale(N, sqrt1_e2)));
+}
+
 /* Material::getEnvironmentColor, src/Material.cpp:44-62 (scene map or background) */
 static v3 env_color(const oro_scene* s, v3 d) {
     if (s->env_tex >= 0) {
@@ -1344,7 +1359,7 @@ static v3 env_color(const oro_scene* s, v3 d) {
 
 /* Blinn::shade, src/Blinn.cpp:91-335: Fresnel-weighted Russian roulette between
  * direct lighting and one reflection or refraction ray (bounces < 5), with the
- * ray's IOR history (no maps, no path tracing, specGloss = 1, no translucency,
+ * ray's IOR history, glossy reflection vector (no maps, no path tracing, no translucency,
  * no dispersion). */
 static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h, ior_list* ior,
                       int bounces) {
@@ -1362,6 +1377,10 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
     int flip = 0;
     if ((double)vDotN < 0.0) { flip = 1; vDotN = -vDotN; theNormal = vneg(theNormal); }
     v3 rVec = vadd(rayD, vscale(theNormal, 2.0f * vDotN));
+    if ((double)mat->gloss < 1.0) {     /* src/Blinn.cpp:166-171 */
+        v3 randD = cosine_sample(c, theNormal);
+        rVec = vnormalized(vadd(vscale(rVec, mat->gloss), vscale(randD, 1 - mat->gloss)));
+    }
     float outIOR;
     const float inIOR = ior->v[ior->idx];
     if (flip) {             /* leaving the material: pop the ray's history */

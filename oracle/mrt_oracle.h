@@ -39,6 +39,7 @@ typedef struct {
     float specExp, specAmt; /* Blinn only (reference src/Blinn.h:11-22)       */
     float reflect, refract; /* Blinn m_reflectAmt / m_refractAmt               */
     float ior;              /* Blinn m_ior (src/Blinn.cpp:25-27)                */
+    float gloss;            /* Blinn m_specGloss (src/Blinn.h:42,65)           */
 } oro_material;
 
 typedef struct {

@@ -376,6 +376,22 @@ struct Shader {
         return Rs * Rs;
     }
 
+    // Material::getCosineDistributedSamples (src/Material.cpp:14-41): two draws,
+    // RSQRTSS/RCPSS square roots, libm cos / sin in double rounded once
+    __device__ v3 cosine_sample(v3 N) {
+        const float e1 = next_rand();
+        float e2 = next_rand();
+        e2 = ((double)e2 > 0.99) ? (float)0.99 : e2;
+        const v3 a = ((double)fabsf(N.x) > 0.1) ? mk(0, 1, 0) : mk(1, 0, 0);
+        const v3 u = normalized(cross(a, N), rsqT);
+        const v3 v = cross(N, u);
+        const float t = (2.0f * 3.1415926f) * e1;
+        const float sqrte2 = rcp_nr(rsqrt_nr(e2, rsqT), rcpT);
+        const float sqrt1_e2 = rcp_nr(rsqrt_nr(fabsf(1.0f - e2), rsqT), rcpT);
+        const float c = (float)cos((double)t), s = (float)sin((double)t);
+        return normalized(add(add(scale(u, c * sqrte2), scale(v, s * sqrte2)), scale(N, sqrt1_e2)), rsqT);
+    }
+
     // Material::getEnvironmentColor (src/Material.cpp:44-62): scene map or background
     __device__ v3 env_color(v3 d) {
         if (P.env) return scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
@@ -426,7 +442,11 @@ struct Shader {
             vDotN = same ? vDotN : vDotGeoN;
             bool flip = false;
             if (vDotN < 0.0f) { flip = true; vDotN = -vDotN; n = neg(n); }
-            const v3 rVec = add(rayD, scale(n, 2.0f * vDotN));
+            v3 rVec = add(rayD, scale(n, 2.0f * vDotN));
+            if (M.gloss < 1.0f) {   // glossy reflection vector (src/Blinn.cpp:166-171)
+                const v3 rd = cosine_sample(n);
+                rVec = normalized(add(scale(rVec, M.gloss), scale(rd, 1.0f - M.gloss)), rsqT);
+            }
             const float inIOR = ior[idx];
             float outIOR = M.ior;
             if (flip) {   // leaving the material: pop the history
@@ -1405,7 +1425,8 @@ static int ensure_device(Scene& s, int device) {
     d.point_only = true;
     for (const DevLight& l : s.lights) d.point_only &= (l.type == MRT_POINT_LIGHT);
     d.recursive = false;
-    for (const DevMaterial& m : s.materials) d.recursive |= m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f);
+    for (const DevMaterial& m : s.materials)
+        d.recursive |= m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f || m.gloss < 1.f);
     d.gthreads = (uint32_t)d.grid * kWG;
     s.info.device_bytes = total;
     s.dev_dirty = false;
@@ -1701,7 +1722,7 @@ int mrt_scene_add_material(mrt_scene* s, const mrt_material* m) {
     d.type = m->type;
     memcpy(d.kd, m->kd, 12); memcpy(d.ka, m->ka, 12); memcpy(d.ks, m->ks, 12);
     d.spec_exp = m->spec_exp; d.spec_amt = m->spec_amt;
-    d.reflect = 0.f; d.refract = 0.f; d.ior = 1.5f;   // Blinn defaults (src/Blinn.h:11-22)
+    d.reflect = 0.f; d.refract = 0.f; d.ior = 1.5f; d.gloss = 1.f;   // Blinn defaults (src/Blinn.h:11-22)
     s->impl.materials.push_back(d);
     s->impl.dev_dirty = true;
     return (int)s->impl.materials.size() - 1;
@@ -1939,6 +1960,16 @@ int mrt_scene_set_material_optics(mrt_scene* s, int material, float reflect_amt,
     m.reflect = reflect_amt;
     m.refract = refract_amt;
     m.ior = ior;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
+int mrt_scene_set_material_gloss(mrt_scene* s, int material, float gloss) {
+    if (!s || material < 0 || material >= (int)s->impl.materials.size() || !(gloss >= 0.f && gloss <= 1.f)) {
+        set_error("bad gloss: need a valid material and 0 <= gloss <= 1");
+        return MRT_ERR_INVALID;
+    }
+    s->impl.materials[(size_t)material].gloss = gloss;
     s->impl.dev_dirty = true;
     return MRT_OK;
 }

@@ -59,6 +59,7 @@ struct DevMaterial {
     float spec_exp, spec_amt;
     float reflect, refract;  // Blinn m_reflectAmt / m_refractAmt (src/Blinn.h:62, src/Material.h:73)
     float ior;               // Blinn m_ior (src/Blinn.cpp:25-27)
+    float gloss;             // Blinn m_specGloss (src/Blinn.h:42,65): < 1 jitters the reflection vector
 };
 
 struct DevLight {

@@ -133,14 +133,17 @@ class Lambert:
 class Blinn:
     """Blinn(kd, ka, ks, kt, ior, specExp, specAmt, reflectAmt, refractAmt) defaults of
     src/Blinn.h:11-22: direct lighting plus Fresnel-weighted reflection / refraction
-    rays (src/Blinn.cpp:91-335).  Path tracing, gloss < 1, translucency, dispersion
+    rays (src/Blinn.cpp:91-335), glossy reflection vectors.  Path tracing, translucency, dispersion
     and texture maps are not on the MI355X path."""
 
     def __init__(self, kd=Vector3(1), ka=Vector3(0), ks=Vector3(1), kt=Vector3(0), ior=1.5,
-                 specExp=1.0, specAmt=0.0, reflectAmt=0.0, refractAmt=0.0):
+                 specExp=1.0, specAmt=0.0, reflectAmt=0.0, refractAmt=0.0, specGloss=1.0):
         self.kd, self.ka, self.ks, self.kt = Vector3(kd), Vector3(ka), Vector3(ks), Vector3(kt)
         self.ior, self.specExp, self.specAmt = float(ior), float(specExp), float(specAmt)
         self.reflectAmt, self.refractAmt = float(reflectAmt), float(refractAmt)
+        self.specGloss = float(specGloss)
+
+    def setReflectGloss(self, g): self.specGloss = float(g)    # src/Blinn.h:42
 
     def setReflectAmt(self, a): self.reflectAmt = float(a)     # src/Blinn.h:41
     def setRefractAmt(self, a): self.refractAmt = float(a)     # src/Material.h:32
@@ -403,6 +406,7 @@ class Scene:
                 if isinstance(mat, Blinn):
                     check(L.mrt_scene_set_material_optics(self._h, mats[id(mat)], mat.reflectAmt, mat.refractAmt,
                                                           mat.ior), "material optics")
+                    check(L.mrt_scene_set_material_gloss(self._h, mats[id(mat)], mat.specGloss), "material gloss")
             mid = mats[id(mat)]
             if mesh.path is not None:
                 ctm = mesh.ctm.ctypes.data_as(C.POINTER(C.c_float)) if mesh.ctm is not None else None

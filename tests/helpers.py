@@ -21,7 +21,8 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
     lights = cfg["lights"] if lights is None else lights
     mat = cfg["material"]
     P = miro.Scene()
-    optics = dict(reflectAmt=mat.get("reflectAmt", 0.0), refractAmt=mat.get("refractAmt", 0.0), ior=mat.get("ior", 1.5))
+    optics = dict(reflectAmt=mat.get("reflectAmt", 0.0), refractAmt=mat.get("refractAmt", 0.0), ior=mat.get("ior", 1.5),
+                  specGloss=mat.get("specGloss", 1.0))
     pm = miro.Lambert(mat["kd"]) if mat["kind"] == "lambert" else miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0),
                                                                            specAmt=mat.get("specAmt", 0.0), **optics)
     O_ = O.OracleScene()

@@ -25,6 +25,8 @@ def cornell(material, lights=None, subdivs=None):
 
 MIRROR = dict(kind="blinn", kd=(0.6, 0.5, 0.4), reflectAmt=1.0, ior=1.5)
 GLASS = dict(kind="blinn", kd=(0.6, 0.5, 0.4), refractAmt=1.0, ior=1.5)
+GLOSSY = dict(kind="blinn", kd=(0.6, 0.5, 0.4), reflectAmt=0.8, ior=1.5, specGloss=0.6, specExp=8.0, specAmt=0.3)
+SHINY = dict(kind="blinn", kd=(0.6, 0.5, 0.4), specGloss=0.5, specExp=10.0, specAmt=0.5)   # gloss, no secondary rays
 MIXED = dict(kind="blinn", kd=(0.6, 0.5, 0.4), ks=(0.9, 0.8, 0.7), reflectAmt=0.6, refractAmt=0.7, ior=1.33,
              specExp=12.0, specAmt=0.2)
 
@@ -55,6 +57,17 @@ def test_oracle_black_mirror_frame_is_finite_and_non_negative():
     assert (ref["rgb"] >= 0).all() and np.isfinite(ref["rgb"]).all()
 
 
+def test_oracle_gloss_jitters_the_reflection_vector():
+    """specGloss < 1 draws a cosine sample per shade (src/Blinn.cpp:166-171):
+    the specular highlight moves, the frame stays deterministic."""
+    _, O1, cam = cornell(dict(SHINY, specGloss=1.0))
+    _, O2, _ = cornell(SHINY)
+    a, b = O1.render(cam, 32, 24, threads=4), O2.render(cam, 32, 24, threads=4)
+    assert not np.array_equal(bits(a["rgb"]), bits(b["rgb"]))
+    assert np.array_equal(bits(b["rgb"]), bits(O2.render(cam, 32, 24, threads=1)["rgb"]))
+    assert b["secondary_rays"] == 0
+
+
 def test_material_optics_are_validated():
     L = miro.lib()
     h = L.mrt_scene_create()
@@ -64,6 +77,9 @@ def test_material_optics_are_validated():
         m = _lib.mrt_material(1, (C.c_float * 3)(1, 1, 1), (C.c_float * 3)(0, 0, 0), (C.c_float * 3)(1, 1, 1), 1.0, 0.0)
         mid = L.mrt_scene_add_material(h, C.byref(m))
         assert L.mrt_scene_set_material_optics(h, mid, 0.5, 0.5, 1.5) == 0
+        assert L.mrt_scene_set_material_gloss(h, mid, 0.5) == 0
+        for bad in [(mid + 1, 0.5), (mid, -0.1), (mid, 1.5)]:
+            assert L.mrt_scene_set_material_gloss(h, *bad) < 0
         for bad in [(mid + 1, 0.5, 0.5, 1.5), (mid, -1.0, 0.0, 1.5), (mid, 0.0, -1.0, 1.5), (mid, 0.0, 0.0, 0.0)]:
             assert L.mrt_scene_set_material_optics(h, *bad) < 0
     finally:
@@ -90,11 +106,18 @@ def assert_same(P, O_, cam, W, H):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mat", [MIRROR, GLASS, MIXED], ids=["mirror", "glass", "mixed"])
+@pytest.mark.parametrize("mat", [MIRROR, GLASS, MIXED, GLOSSY], ids=["mirror", "glass", "mixed", "glossy"])
 def test_secondary_rays_match_oracle(mat):
     P, O_, cam = cornell(mat)
     ref = assert_same(P, O_, cam, 72, 56)
     assert ref["secondary_rays"] > 0
+
+
+@pytest.mark.gpu
+def test_gloss_without_secondary_rays_matches_oracle():
+    P, O_, cam = cornell(SHINY)
+    ref = assert_same(P, O_, cam, 64, 48)
+    assert ref["secondary_rays"] == 0
 
 
 @pytest.mark.gpu
