@@ -156,6 +156,11 @@ int mrt_scene_set_material_optics(mrt_scene* s, int material, float reflect_amt,
  * vector is blended with a cosine-distributed sample
  * (Material::getCosineDistributedSamples, src/Material.cpp:14-41; src/Blinn.cpp:166-171). */
 int mrt_scene_set_material_gloss(mrt_scene* s, int material, float gloss);
+/* Material::setTranslucency (src/Material.h:30; default 0): above 0.01 a Blinn
+ * material also samples every light from the back side (-normal) and adds
+ * translucency * light * kd (src/Blinn.cpp:224-236), as the reference's leaf
+ * materials do (src/main.cpp:253, src/Assignment3.h:70). */
+int mrt_scene_set_material_translucency(mrt_scene* s, int material, float translucency);
 /* Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55; defaults
  * 1, 1, 0.01 at src/Scene.cpp:20-22): adaptive supersampling of
  * Scene::adaptiveSampleScene (src/Scene.cpp:252-293).  With both counts 1 a

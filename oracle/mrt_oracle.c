@@ -1359,11 +1359,11 @@ static v3 env_color(const oro_scene* s, v3 d) {
 
 /* Blinn::shade, src/Blinn.cpp:91-335: Fresnel-weighted Russian roulette between
  * direct lighting and one reflection or refraction ray (bounces < 5), with the
- * ray's IOR history, glossy reflection vector (no maps, no path tracing, no translucency,
+ * ray's IOR history, glossy reflection vector, translucency (no maps, no path tracing,
  * no dispersion). */
 static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h, ior_list* ior,
                       int bounces) {
-    v3 Ld = V(0, 0, 0), Ls = V(0, 0, 0), Lr = V(0, 0, 0), Lt = V(0, 0, 0);
+    v3 Ld = V(0, 0, 0), Ls = V(0, 0, 0), Lr = V(0, 0, 0), Lt = V(0, 0, 0), translucency = V(0, 0, 0);
     v3 rayD = V(r->d[0], r->d[1], r->d[2]);
     v3 viewDir = vneg(rayD);
     v3 N, geoN;
@@ -1410,6 +1410,14 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
             Ls = vadd(Ls, vscale(vscale(vmul(E, ks), mat->specAmt), pw));
             Ld = vadd(Ld, vmul(E, kd));
         }
+        if (mat->translucency > 0.01f) {   /* src/Blinn.cpp:224-236 */
+            v3 lightTotal = V(0, 0, 0);
+            for (int i = 0; i < c->s->n_lights; i++) {
+                float lightSpec = 0;
+                lightTotal = vadd(lightTotal, sample_light(c, i, P, vneg(theNormal), rVec, &lightSpec));
+            }
+            translucency = vadd(translucency, vmul(vscale(lightTotal, mat->translucency), kd));
+        }
     } else {
         int doEnv = 1;
         rrFloat = next_rand(c);
@@ -1451,7 +1459,7 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
     }
     Ld = vadd(Ld, V(mat->ka[0], mat->ka[1], mat->ka[2]));
     /* (Ld + Ls + translucency)*rrWeightRecip + (Lr + Lt)*rrWeightRecipSpec + m_Le */
-    return vadd(vadd(vscale(vadd(vadd(Ld, Ls), zero), rrWeightRecip), vscale(vadd(Lr, Lt), rrWeightRecipSpec)), zero);
+    return vadd(vadd(vscale(vadd(vadd(Ld, Ls), translucency), rrWeightRecip), vscale(vadd(Lr, Lt), rrWeightRecipSpec)), zero);
 }
 
 /* Material::shade dispatch of a hit */

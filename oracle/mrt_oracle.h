@@ -40,6 +40,7 @@ typedef struct {
     float reflect, refract; /* Blinn m_reflectAmt / m_refractAmt               */
     float ior;              /* Blinn m_ior (src/Blinn.cpp:25-27)                */
     float gloss;            /* Blinn m_specGloss (src/Blinn.h:42,65)           */
+    float translucency;     /* Material::m_translucency (src/Material.h:30,44) */
 } oro_material;
 
 typedef struct {

@@ -34,7 +34,8 @@ def lib():
 class Material(C.Structure):
     _fields_ = [("type", C.c_int), ("kd", C.c_float * 3), ("ka", C.c_float * 3), ("ks", C.c_float * 3),
                 ("specExp", C.c_float), ("specAmt", C.c_float),
-                ("reflect", C.c_float), ("refract", C.c_float), ("ior", C.c_float), ("gloss", C.c_float)]
+                ("reflect", C.c_float), ("refract", C.c_float), ("ior", C.c_float), ("gloss", C.c_float),
+                ("translucency", C.c_float)]
 
 
 class Light(C.Structure):
@@ -144,10 +145,10 @@ class OracleScene:
             pass
 
     def add_material(self, kind="lambert", kd=(1, 1, 1), ka=(0, 0, 0), ks=(1, 1, 1), specExp=1.0, specAmt=0.0,
-                     reflectAmt=0.0, refractAmt=0.0, ior=1.5, specGloss=1.0):
+                     reflectAmt=0.0, refractAmt=0.0, ior=1.5, specGloss=1.0, translucency=0.0):
         """Lambert / Blinn (src/Blinn.h:11-22 defaults: ior 1.5, no reflection / refraction)."""
         m = Material(0 if kind == "lambert" else 1, _v3(kd), _v3(ka), _v3(ks), specExp, specAmt,
-                     reflectAmt, refractAmt, ior, specGloss)
+                     reflectAmt, refractAmt, ior, specGloss, translucency)
         return self.L.oro_scene_add_material(self.h, C.byref(m))
 
     def add_obj(self, path, material, ctm=None):

@@ -472,8 +472,17 @@ struct Shader {
                     Ls = add(Ls, scale(scale(mul(E, ks), M.spec_amt), pw));
                     Ld = add(Ld, mul(E, kd));
                 }
+                v3 tr = z;
+                if (M.translucency > 0.01f) {   // lights seen through the surface (src/Blinn.cpp:224-236)
+                    v3 total = z;
+                    for (int i = 0; i < P.n_lights; i++) {
+                        float spec = 0.f;
+                        total = add(total, sample_light<COUNT>(i, Pt, neg(n), rVec, spec));
+                    }
+                    tr = add(z, mul(scale(total, M.translucency), kd));
+                }
                 Ld = add(Ld, ka);
-                val = add(add(scale(add(add(Ld, Ls), z), rrRecip), scale(add(z, z), rrSpec)), z);
+                val = add(add(scale(add(add(Ld, Ls), tr), rrRecip), scale(add(z, z), rrSpec)), z);
                 break;
             }
             const v3 base = scale(add(add(add(z, ka), z), z), rrRecip);   // (Ld + Ls + translucency) * rrWeightRecip
@@ -1426,7 +1435,7 @@ static int ensure_device(Scene& s, int device) {
     for (const DevLight& l : s.lights) d.point_only &= (l.type == MRT_POINT_LIGHT);
     d.recursive = false;
     for (const DevMaterial& m : s.materials)
-        d.recursive |= m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f || m.gloss < 1.f);
+        d.recursive |= m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f || m.gloss < 1.f || m.translucency > 0.01f);
     d.gthreads = (uint32_t)d.grid * kWG;
     s.info.device_bytes = total;
     s.dev_dirty = false;
@@ -1723,6 +1732,7 @@ int mrt_scene_add_material(mrt_scene* s, const mrt_material* m) {
     memcpy(d.kd, m->kd, 12); memcpy(d.ka, m->ka, 12); memcpy(d.ks, m->ks, 12);
     d.spec_exp = m->spec_exp; d.spec_amt = m->spec_amt;
     d.reflect = 0.f; d.refract = 0.f; d.ior = 1.5f; d.gloss = 1.f;   // Blinn defaults (src/Blinn.h:11-22)
+    d.translucency = 0.f;
     s->impl.materials.push_back(d);
     s->impl.dev_dirty = true;
     return (int)s->impl.materials.size() - 1;
@@ -1960,6 +1970,16 @@ int mrt_scene_set_material_optics(mrt_scene* s, int material, float reflect_amt,
     m.reflect = reflect_amt;
     m.refract = refract_amt;
     m.ior = ior;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
+int mrt_scene_set_material_translucency(mrt_scene* s, int material, float translucency) {
+    if (!s || material < 0 || material >= (int)s->impl.materials.size() || !(translucency >= 0.f)) {
+        set_error("bad translucency: need a valid material and translucency >= 0");
+        return MRT_ERR_INVALID;
+    }
+    s->impl.materials[(size_t)material].translucency = translucency;
     s->impl.dev_dirty = true;
     return MRT_OK;
 }

@@ -60,6 +60,7 @@ struct DevMaterial {
     float reflect, refract;  // Blinn m_reflectAmt / m_refractAmt (src/Blinn.h:62, src/Material.h:73)
     float ior;               // Blinn m_ior (src/Blinn.cpp:25-27)
     float gloss;             // Blinn m_specGloss (src/Blinn.h:42,65): < 1 jitters the reflection vector
+    float translucency;      // Material::m_translucency (src/Material.h:30,44): > 0.01 lights the back side
 };
 
 struct DevLight {

@@ -133,7 +133,7 @@ class Lambert:
 class Blinn:
     """Blinn(kd, ka, ks, kt, ior, specExp, specAmt, reflectAmt, refractAmt) defaults of
     src/Blinn.h:11-22: direct lighting plus Fresnel-weighted reflection / refraction
-    rays (src/Blinn.cpp:91-335), glossy reflection vectors.  Path tracing, translucency, dispersion
+    rays (src/Blinn.cpp:91-335), glossy reflection vectors, translucency.  Path tracing, dispersion
     and texture maps are not on the MI355X path."""
 
     def __init__(self, kd=Vector3(1), ka=Vector3(0), ks=Vector3(1), kt=Vector3(0), ior=1.5,
@@ -142,6 +142,9 @@ class Blinn:
         self.ior, self.specExp, self.specAmt = float(ior), float(specExp), float(specAmt)
         self.reflectAmt, self.refractAmt = float(reflectAmt), float(refractAmt)
         self.specGloss = float(specGloss)
+        self.translucency = 0.0
+
+    def setTranslucency(self, t): self.translucency = float(t)   # src/Material.h:30
 
     def setReflectGloss(self, g): self.specGloss = float(g)    # src/Blinn.h:42
 
@@ -407,6 +410,8 @@ class Scene:
                     check(L.mrt_scene_set_material_optics(self._h, mats[id(mat)], mat.reflectAmt, mat.refractAmt,
                                                           mat.ior), "material optics")
                     check(L.mrt_scene_set_material_gloss(self._h, mats[id(mat)], mat.specGloss), "material gloss")
+                    check(L.mrt_scene_set_material_translucency(self._h, mats[id(mat)], mat.translucency),
+                          "material translucency")
             mid = mats[id(mat)]
             if mesh.path is not None:
                 ctm = mesh.ctm.ctypes.data_as(C.POINTER(C.c_float)) if mesh.ctm is not None else None

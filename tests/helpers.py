@@ -23,11 +23,14 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
     P = miro.Scene()
     optics = dict(reflectAmt=mat.get("reflectAmt", 0.0), refractAmt=mat.get("refractAmt", 0.0), ior=mat.get("ior", 1.5),
                   specGloss=mat.get("specGloss", 1.0))
+    translucency = mat.get("translucency", 0.0)
     pm = miro.Lambert(mat["kd"]) if mat["kind"] == "lambert" else miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0),
                                                                            specAmt=mat.get("specAmt", 0.0), **optics)
+    if translucency and mat["kind"] == "blinn":
+        pm.setTranslucency(translucency)
     O_ = O.OracleScene()
     om = O_.add_material(mat["kind"], kd=mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0),
-                         **optics)
+                         translucency=translucency if mat["kind"] == "blinn" else 0.0, **optics)
     for arrs in (meshes or []):
         tm = miro.TriangleMesh()
         tm.setArrays(*arrs)

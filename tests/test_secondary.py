@@ -27,6 +27,7 @@ MIRROR = dict(kind="blinn", kd=(0.6, 0.5, 0.4), reflectAmt=1.0, ior=1.5)
 GLASS = dict(kind="blinn", kd=(0.6, 0.5, 0.4), refractAmt=1.0, ior=1.5)
 GLOSSY = dict(kind="blinn", kd=(0.6, 0.5, 0.4), reflectAmt=0.8, ior=1.5, specGloss=0.6, specExp=8.0, specAmt=0.3)
 SHINY = dict(kind="blinn", kd=(0.6, 0.5, 0.4), specGloss=0.5, specExp=10.0, specAmt=0.5)   # gloss, no secondary rays
+LEAF = dict(kind="blinn", kd=(0.3, 0.7, 0.2), translucency=0.6, specExp=6.0, specAmt=0.2)   # main.cpp:253
 MIXED = dict(kind="blinn", kd=(0.6, 0.5, 0.4), ks=(0.9, 0.8, 0.7), reflectAmt=0.6, refractAmt=0.7, ior=1.33,
              specExp=12.0, specAmt=0.2)
 
@@ -66,6 +67,27 @@ def test_oracle_gloss_jitters_the_reflection_vector():
     assert not np.array_equal(bits(a["rgb"]), bits(b["rgb"]))
     assert np.array_equal(bits(b["rgb"]), bits(O2.render(cam, 32, 24, threads=1)["rgb"]))
     assert b["secondary_rays"] == 0
+
+
+def leaf_floor(translucency):
+    """Bunny stand-in + floor, one light above and one below the floor: the
+    floor's back side (-normal) sees the lower light."""
+    cfg = dict(scenes.CONFIGS["D1"])
+    cfg.pop("env")
+    cfg["material"] = dict(LEAF, translucency=translucency)
+    lights = [dict(type="point", pos=(10.0, 20.0, 10.0), power=1000.0),
+              dict(type="point", pos=(0.0, -5.0, 3.0), power=300.0)]
+    return scene_pair(cfg, obj=scenes.bunny_obj(), floor=True, lights=lights)
+
+
+def test_oracle_translucency_samples_the_back_side():
+    """translucency > 0.01 adds one more sampleLight per light with -normal
+    (src/Blinn.cpp:224-236): more shadow rays, a brighter floor."""
+    _, O0, cam = leaf_floor(0.0)
+    _, O1, _ = leaf_floor(0.6)
+    a, b = O0.render(cam, 32, 24, threads=4), O1.render(cam, 32, 24, threads=4)
+    assert b["shadow_rays"] > a["shadow_rays"]
+    assert (b["rgb"] >= a["rgb"]).all() and (b["rgb"] > a["rgb"]).any()
 
 
 def test_material_optics_are_validated():
@@ -111,6 +133,17 @@ def test_secondary_rays_match_oracle(mat):
     P, O_, cam = cornell(mat)
     ref = assert_same(P, O_, cam, 72, 56)
     assert ref["secondary_rays"] > 0
+
+
+@pytest.mark.gpu
+def test_translucency_matches_oracle():
+    lights = [dict(type="rect", v1=(3.0, 5.4, -2.5), v2=(3.0, 5.4, -3.0), v3=(2.5, 5.4, -2.5), power=15.0,
+                   samples=3, noise=0.001),
+              dict(type="point", pos=(2.75, 2.0, -2.75), power=20.0)]
+    P, O_, cam = cornell(LEAF, lights=lights)
+    assert_same(P, O_, cam, 64, 48)
+    P, O_, cam = leaf_floor(0.6)
+    assert_same(P, O_, cam, 48, 40)
 
 
 @pytest.mark.gpu
