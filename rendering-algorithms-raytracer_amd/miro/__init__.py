@@ -19,6 +19,7 @@ module only marshals data.  Missing library -> MRTError, no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import time
 from typing import List, Optional
 
 import numpy as np
@@ -456,7 +457,9 @@ class Scene:
         check(L.mrt_scene_set_background(self._h, f3(self.bg)), "bg")
         check(L.mrt_scene_set_num_paths(self._h, self.m_numPaths), "num_paths")
         check(L.mrt_scene_set_subdivs(self._h, self.m_minSubdivs, self.m_maxSubdivs, self.m_noiseThreshold), "subdivs")
+        t0 = time.perf_counter()
         check(L.mrt_scene_build_bvh(self._h), "BVH build")
+        self.bvh_build_ms = (time.perf_counter() - t0) * 1e3   # host BVH::build wall time
         info = _lib.mrt_bvh_info()
         check(L.mrt_scene_bvh_info(self._h, C.byref(info)), "bvh_info")
         self.bvh_info = {k: getattr(info, k) for k, _ in info._fields_}
