@@ -81,6 +81,8 @@ def test_bvh_from_fixture_arrays(name):
 def test_explosion01_counts_product():
     p = product_scene(arrays=fixture_mesh("explosion01"))
     assert p.bvh_info["nodes"] == 11647 and p.bvh_info["leaves"] == 23365
+    # bench.py's scene_setup line reads the host build time recorded by preCalc
+    assert p.bvh_build_ms > 0
 
 
 @pytest.mark.parametrize("which", ["sponza", "bunny"])
