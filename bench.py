@@ -153,7 +153,9 @@ def _scene_setup(scene):
     ms = getattr(scene, "bvh_build_ms", None)
     prims = scene.bvh_info["prims"]
     return {"bvh_build_ms": None if ms is None else round(ms, 2), "prims": prims, "threads": 1,
-            "build_mprims_per_s": None if not ms else round(prims / ms / 1e3, 3)}
+            "build_mprims_per_s": None if not ms else round(prims / ms / 1e3, 3),
+            # instanced scenes: the BLAS builds (mrt_scene_make_blas) happen before the world QBVH
+            "blas_build_ms": round(getattr(scene, "blas_build_ms", 0.0), 2)}
 
 
 def main():

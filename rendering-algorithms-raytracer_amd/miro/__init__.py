@@ -424,6 +424,7 @@ class Scene:
             return check(L.mrt_scene_add_mesh(self._h, C.byref(mm), mid), "add_mesh")
 
         blas = {}   # BVH object -> BLAS id (built once, shared by its instances)
+        self.blas_build_ms = 0.0
         self.blas_ids = blas
         for item, mat in self._meshes:
             if not isinstance(item, ProxyObject):
@@ -432,7 +433,9 @@ class Scene:
             key = id(item.bvh)
             if key not in blas:
                 ids = (C.c_int32 * len(item.bvh.objects))(*[add_mesh(m, mt) for m, mt in item.bvh.objects])
+                t0 = time.perf_counter()
                 blas[key] = check(L.mrt_scene_make_blas(self._h, ids, len(ids)), "BLAS build")
+                self.blas_build_ms += (time.perf_counter() - t0) * 1e3
             m16 = np.ascontiguousarray(item.matrix, np.float32).reshape(16)
             check(L.mrt_scene_add_instance(self._h, blas[key], m16.ctypes.data_as(C.POINTER(C.c_float))), "instance")
         tex_ids = {}
