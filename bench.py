@@ -354,6 +354,7 @@ def main():
         # instrumented (count-mode) launch: wall-clock spread of the persistent waves
         "wave_timing_us": {k: round(st[k], 1) for k in ("primary_span_us", "primary_ramp_us", "primary_tail_us",
                                                        "shade_span_us", "shade_ramp_us", "shade_tail_us")},
+        "lane_util": round(st["primary_node_visits"] / max(1, 64 * st["primary_wave_steps"]), 4),
     }
     if not args.no_cpu_baseline and world == 1:
         try:

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 3
+#define MRT_ABI_VERSION 4
 
 enum {
     MRT_OK = 0,
@@ -50,6 +50,13 @@ typedef struct {
     int32_t type;            /* MRT_LAMBERT | MRT_BLINN                               */
     float kd[3], ka[3], ks[3];
     float spec_exp, spec_amt;/* Blinn m_specExp / m_specAmt (src/Blinn.h:59-61)       */
+    float le[3];             /* Blinn m_Le, setLightEmittedColor (src/Blinn.h:45,64):
+                                added to every Blinn shade() result (src/Blinn.cpp:335) */
+    float emitted;           /* Blinn m_lightEmitted, setLightEmittedIntensity
+                                (src/Blinn.h:44,63): with path tracing, a GI ray that
+                                reaches this surface returns emitted * le
+                                (src/Blinn.cpp:46-51).  Both 0 = not an emitter
+                                (the Blinn ctor forces 0, src/Blinn.cpp:28-29)     */
 } mrt_material;
 
 /* Light as data (replaces virtual Light::sampleLight, src/Light.h:35). */
@@ -72,18 +79,26 @@ typedef struct {
     float fov_deg;
 } mrt_camera;
 
-/* Raw triangle mesh (TriangleMesh arrays, src/TriangleMesh.h:36-47). */
+/* Raw triangle mesh (TriangleMesh arrays, src/TriangleMesh.h:36-47).  The
+ * reference keeps vertices and normals as 16-byte Vector3 (src/Vector3.h:19,
+ * x y z + pad): pass vert_stride = normal_stride = 4 to hand those arrays over
+ * without repacking; 0 (or 3) = packed x y z. */
 typedef struct {
-    const float* verts;      /* nv*3                                                    */
-    const float* normals;    /* nn*3                                                    */
-    const uint32_t* vidx;    /* nt*3 vertex indices                                     */
-    const uint32_t* nidx;    /* nt*3 normal indices                                     */
+    const float* verts;      /* nv*vert_stride floats                                   */
+    const float* normals;    /* nn*normal_stride floats                                 */
+    const uint32_t* vidx;    /* nt*3 vertex indices (TupleI3 m_vertexIndices)           */
+    const uint32_t* nidx;    /* nt*3 normal indices (TupleI3 m_normalIndices)           */
     int32_t nv, nn, nt;
+    int32_t vert_stride, normal_stride;  /* floats per vertex / normal: 0 or 3 packed, 4 Vector3 */
 } mrt_mesh;
 
-typedef struct {             /* HitInfo (src/Ray.h:185-200); obj -> prim id           */
+typedef struct {             /* HitInfo (src/Ray.h:185-200)                            */
     float t, a, b;
-    int32_t prim;            /* global triangle id in scene order, -1 = miss           */
+    int32_t prim;            /* global object id in scene order, -1 = miss (or, for an
+                                any-hit query, 1 = occluded); mrt_scene_prim_object
+                                maps it to (mesh, triangle, instance) = HitInfo::obj  */
+    int32_t inst;            /* HitInfo::m_proxy: ProxyObject instance of the hit,
+                                -1 = a world triangle (or a miss)                      */
 } mrt_hit;
 
 typedef struct {
@@ -101,6 +116,13 @@ typedef struct {
     int32_t want_rgb8;       /* 1: also write tone-mapped 8-bit RGB (Image::Map)        */
     int32_t want_hits;       /* 1: also write primary mrt_hit per pixel (debug/parity)  */
     uint32_t seed;           /* stochastic configs only (counter RNG stream)            */
+    /* mrt_render only: render on several HIP devices of this process.  The 32x32
+     * buckets of src/Scene.cpp:90-95 are dealt bucket b -> devices[b mod n] (a
+     * device may appear more than once), each device renders its share from its
+     * own scene replica, and the tiles are gathered into the caller's frame.  The
+     * result is bit-identical to a one-device render.  NULL / 0 = `device` only. */
+    const int32_t* devices;
+    int32_t n_devices;
 } mrt_render_opts;
 
 typedef struct {
@@ -161,6 +183,20 @@ int mrt_scene_set_material_gloss(mrt_scene* s, int material, float gloss);
  * translucency * light * kd (src/Blinn.cpp:224-236), as the reference's leaf
  * materials do (src/main.cpp:253, src/Assignment3.h:70). */
 int mrt_scene_set_material_translucency(mrt_scene* s, int material, float translucency);
+/* Blinn::setLightEmittedIntensity / setLightEmittedColor after the material was
+ * added (same fields as mrt_material.emitted / le). */
+int mrt_scene_set_material_emission(mrt_scene* s, int material, float emitted, const float le[3]);
+/* Material::setSampleEnv (src/Material.h:27; default true): a path-tracing GI ray
+ * that misses takes the environment colour only when both this flag and the
+ * scene's (mrt_scene_set_path_trace) are set (src/Blinn.cpp:70-73). */
+int mrt_scene_set_material_sample_env(mrt_scene* s, int material, int sample_env);
+/* Scene::m_pathTrace / m_maxBounces / setSampleEnv (src/Scene.h:40,48,57-64;
+ * defaults false, 10; the reference never initialises m_sampleLightFromEnv, read
+ * here as false): Blinn::calculatePathTracing (src/Blinn.cpp:39-89) adds one
+ * cosine-distributed GI ray per direct-lighting shade() while the ray's GI bounce
+ * count is below max_bounces - 1, and samples the lights directly at the last
+ * bounce.  1 <= max_bounces <= 64. */
+int mrt_scene_set_path_trace(mrt_scene* s, int enable, int max_bounces, int sample_env);
 /* Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55; defaults
  * 1, 1, 0.01 at src/Scene.cpp:20-22): adaptive supersampling of
  * Scene::adaptiveSampleScene (src/Scene.cpp:252-293).  With both counts 1 a
@@ -211,6 +247,10 @@ int mrt_scene_blas_export(const mrt_scene* s, int32_t blas, float* node_boxes, i
  * binned SAH, 4-wide collapse, host-side; then uploads to the device lazily. */
 int mrt_scene_build_bvh(mrt_scene* s);
 int mrt_scene_bvh_info(const mrt_scene* s, mrt_bvh_info* info);
+/* HitInfo::obj / m_proxy of a hit id (mrt_hit.prim): the Object's mesh id and
+ * triangle index (Object::m_mesh / m_index, src/Object.h:49-77) and the
+ * ProxyObject instance (-1 = a world triangle).  Valid after mrt_scene_build_bvh. */
+int mrt_scene_prim_object(const mrt_scene* s, int32_t prim, int32_t* mesh, int32_t* tri, int32_t* inst);
 /* Canonical QBVH arrays: node_boxes[24*nodes] (minX4 minY4 minZ4 maxX4 maxY4 maxZ4),
  * node_child[4*nodes] (>=0 inner node, ~leaf for a leaf slot, INT32_MIN empty),
  * leaf_tris[36*leaves] (Ax4 Ay4 Az4 e0x4 e0y4 e0z4 e1x4 e1y4 e1z4),

@@ -204,6 +204,7 @@ struct oro_scene {
     int env_tex; float env_exposure;  /* Scene::m_envMap / m_envExposure */
     v3 bg;
     int num_paths;
+    int path_trace, max_bounces, sample_env;  /* Scene::m_pathTrace / m_maxBounces / sampleEnv */
     int min_subdivs, max_subdivs;     /* Scene::m_minSubdivs / m_maxSubdivs (src/Scene.cpp:21-22) */
     float noise;                      /* Scene::m_noiseThreshold (src/Scene.cpp:20) */
     int* mesh_blas;                  /* per mesh: owning BLAS, -1 = world geometry */
@@ -223,6 +224,7 @@ oro_scene* oro_scene_create(void) {
     oro_scene* s = (oro_scene*)calloc(1, sizeof(oro_scene));
     s->bg = V(0, 0, 0);
     s->num_paths = 1;
+    s->max_bounces = 10;              /* src/Scene.cpp:19 */
     s->min_subdivs = s->max_subdivs = 1;
     s->noise = 0.01f;
     s->env_tex = -1;
@@ -267,7 +269,12 @@ int oro_scene_add_light(oro_scene* s, const oro_light* l) {
     return s->n_lights++;
 }
 void oro_scene_set_bg(oro_scene* s, float r, float g, float b) { s->bg = V(r, g, b); }
-void oro_scene_set_num_paths(oro_scene* s, int n) { s->num_paths = n < 1 ? 1 : n; }
+void oro_scene_set_num_paths(oro_scene* s, int n) { s->num_paths = n < 1 ? 1 : (n > 1024 ? 1024 : n); }
+int oro_scene_set_path_trace(oro_scene* s, int enable, int max_bounces, int sample_env) {
+    if (max_bounces < 1 || max_bounces > 64) return -1;
+    s->path_trace = enable != 0; s->max_bounces = max_bounces; s->sample_env = sample_env != 0;
+    return 0;
+}
 /* Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55) */
 int oro_scene_set_subdivs(oro_scene* s, int min_subdivs, int max_subdivs, float noise) {
     if (min_subdivs < 1 || max_subdivs < min_subdivs || max_subdivs > 16 || !(noise >= 0.f)) return -1;
@@ -1125,14 +1132,23 @@ static const float PI_F = 3.1415926f;                  /* src/Miro.h:57 */
 
 typedef struct {
     const oro_scene* s;
-    uint32_t pixel; uint32_t dim;   /* RNG stream position */
+    uint32_t pixel;
     uint32_t sample;                /* eye ray of the pixel (adaptive supersampling) */
+    uint32_t skey;                  /* RNG sub-stream: sample * 1024 + path */
+    uint32_t dim;                   /* RNG draw key: (level + 1) << 24 | k (camera: 0-2) */
     uint64_t shadow_rays, nodes, leaves;
-    uint64_t secondary_rays;        /* reflection / refraction rays */
+    uint64_t secondary_rays;        /* reflection / refraction / path-tracing GI rays */
     uint32_t shadow_mask;
 } shade_ctx;
 
-static float next_rand(shade_ctx* c) { return oro_rand(c->pixel, c->sample, c->dim++, 0x5EEDu); }
+/* Counter RNG keys: every shade() call (one chain level of one path) draws from
+ * its own sub-stream, so paths and levels are independent of each other's draw
+ * counts -- the order-free form the device's wavefront passes need.  The
+ * reference draws one global sequence (src/Scene.cpp:39-47); both are
+ * independent uniforms per draw. */
+static float next_rand(shade_ctx* c) { return oro_rand(c->pixel, c->skey, c->dim++, 0x5EEDu); }
+static void begin_level(shade_ctx* c, int level) { c->dim = (uint32_t)(level + 1) << 24; }
+static void begin_camera(shade_ctx* c) { c->skey = c->sample * 1024u; c->dim = 0; }
 
 static int trace_shadow(shade_ctx* c, v3 from, v3 L, float tMax) {
     ray_t r = make_ray(from, L);
@@ -1219,16 +1235,18 @@ static v3 rect_light(shade_ctx* c, const oro_light* l, int li, v3 from, v3 norma
     return vscale(tmpResult, samplesDoneRecip);
 }
 
-/* DomeLight::sampleLight, src/DomeLight.cpp:80-160 (fast shadows, primary
- * shading: m_numSamples draws).  A draw below the shading horizon is redrawn
- * without counting it (`continue` at :106 skips samplesDone++).  Deviation: after
- * DOME_MAX_REJECTS such redraws in one call the loop stops (the reference would
- * not terminate when the whole map lies below the horizon). */
+/* DomeLight::sampleLight, src/DomeLight.cpp:80-160 (fast shadows; m_numSamples
+ * draws, one for secondary shading, :89).  A draw below the shading horizon is
+ * redrawn without counting it (`continue` at :106 skips samplesDone++).
+ * Deviation: after DOME_MAX_REJECTS such redraws in one call the loop stops (the
+ * reference would not terminate when the whole map lies below the horizon). */
 #define DOME_MAX_REJECTS 256
 static const float TWO_PI2 = 2.f * (3.1415926f * 3.1415926f);   /* _2_PI2, src/Miro.h:61 */
-static v3 dome_light(shade_ctx* c, const oro_light* l, int li, v3 from, v3 normal, v3 rVec, float* outSpec) {
+static v3 dome_light(shade_ctx* c, const oro_light* l, int li, v3 from, v3 normal, v3 rVec, float* outSpec,
+                     int secondary) {
     const ibl_dome* D = &c->s->domes[li];
     const ibl_image* tex = &c->s->tex[l->texture];
+    const int numSamples = secondary ? 1 : l->samples;
     v3 tmpResult = V(0, 0, 0);
     float tmpSpec = 0, samplesDoneRecip = 1.0f;
     int samplesDone = 0, cutOff = 0, rejects = 0;
@@ -1259,15 +1277,16 @@ static v3 dome_light(shade_ctx* c, const oro_light* l, int li, v3 from, v3 norma
         cutOff = (((Es.x + Es.y) + Es.z) * 0.333333f) < l->noiseThreshold;
         tmpResult = vadd(tmpResult, vscale(E, attenuate));
         tmpSpec += vdot(rVec, direction) * attenuate;
-    } while (samplesDone < l->samples && !cutOff);
+    } while (samplesDone < numSamples && !cutOff);
     *outSpec = tmpSpec * samplesDoneRecip;
     return vscale(tmpResult, samplesDoneRecip);
 }
 
-static v3 sample_light(shade_ctx* c, int li, v3 from, v3 normal, v3 rVec, float* outSpec) {
+/* Light::sampleLight dispatch; `secondary` = the isSecondary argument */
+static v3 sample_light(shade_ctx* c, int li, v3 from, v3 normal, v3 rVec, float* outSpec, int secondary) {
     const oro_light* l = &c->s->lights[li];
     if (l->type == ORO_POINT_LIGHT) { float e = point_light(c, l, li, from, normal, rVec, outSpec); return V(e, e, e); }
-    if (l->type == ORO_DOME_LIGHT) return dome_light(c, l, li, from, normal, rVec, outSpec);
+    if (l->type == ORO_DOME_LIGHT) return dome_light(c, l, li, from, normal, rVec, outSpec, secondary);
     return rect_light(c, l, li, from, normal, rVec, outSpec);
 }
 
@@ -1301,8 +1320,9 @@ static v3 ray_point(const ray_t* r, float t) {
     return V(r->o[0] + t * r->d[0], r->o[1] + t * r->d[1], r->o[2] + t * r->d[2]);
 }
 
-/* Lambert::shade, src/Lambert.cpp:19-53 */
-static v3 shade_lambert(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h) {
+/* Lambert::shade, src/Lambert.cpp:19-53 (sampleLight without isSecondary) */
+static v3 shade_lambert(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h, int level) {
+    begin_level(c, level);
     v3 L = V(0, 0, 0);
     v3 P = ray_point(r, h->t);
     v3 N, geoN;
@@ -1310,7 +1330,7 @@ static v3 shade_lambert(shade_ctx* c, const oro_material* mat, const ray_t* r, c
     v3 kd = V(mat->kd[0], mat->kd[1], mat->kd[2]);
     for (int i = 0; i < c->s->n_lights; i++) {
         float discard;
-        v3 E = sample_light(c, i, P, N, V(0, 0, 0), &discard);
+        v3 E = sample_light(c, i, P, N, V(0, 0, 0), &discard, 0);
         L = vadd(L, vmul(E, kd));
     }
     return vadd(L, V(mat->ka[0], mat->ka[1], mat->ka[2]));
@@ -1319,7 +1339,11 @@ static v3 shade_lambert(shade_ctx* c, const oro_material* mat, const ray_t* r, c
 /* Ray::IORList, src/Ray.h:43-50: [0] = 1, the camera ray pushes 1.001 (:99) */
 typedef struct { float v[12]; unsigned idx; } ior_list;
 
-static v3 shade_hit(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior, int bounces);
+/* chain position of a shade() call: Ray bounces / giBounces (src/Ray.h:24-25,97),
+ * isSecondary, and the chain level (bounces + giBounces) that keys its draws */
+typedef struct { int bounces, gi, secondary, level; } chain_t;
+
+static v3 shade_hit(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior, chain_t ch);
 
 /* Material::fresnel (full form, src/Material.h:47-55); sin/acos of the
  * reference's libm evaluated in double and rounded once. */
@@ -1357,12 +1381,62 @@ static v3 env_color(const oro_scene* s, v3 d) {
     return s->bg;
 }
 
+/* closest hit of a secondary (reflection / refraction / GI) ray, counted */
+static int trace_secondary(shade_ctx* c, const ray_t* r, hit_t* nh) {
+    nh->t = 1e12f; nh->a = nh->b = 0; nh->prim = -1; nh->inst = -1;
+    uint32_t nv = 0, lv = 0;
+    c->secondary_rays++;
+    int hit = bvh_intersect(c->s, r, 0.001f, nh, &nv, &lv) > 0;
+    c->nodes += nv; c->leaves += lv;
+    return hit;
+}
+/* shade() of a child ray's hit; the caller's own draws continue after it */
+static v3 shade_child(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior, chain_t ch) {
+    const uint32_t saved = c->dim;
+    v3 v = shade_hit(c, r, h, ior, ch);
+    c->dim = saved;
+    return v;
+}
+
+/* Blinn::calculatePathTracing, src/Blinn.cpp:39-89: an emitter returns its
+ * light; below the last bounce one cosine-distributed GI ray (IOR history
+ * [1, current], giBounces + 1, shaded with isSecondary) weighted by kd, or the
+ * environment on a miss when both sampleEnv flags are set; at the last bounce
+ * the lights sampled directly (isSecondary, rVec = 0). */
+static v3 path_trace(shade_ctx* c, const oro_material* mat, v3 P, v3 theNormal, v3 kd, float curIOR, chain_t ch) {
+    const oro_scene* s = c->s;
+    v3 out = V(0, 0, 0);
+    v3 le = V(mat->le[0], mat->le[1], mat->le[2]);
+    if (mat->emitted > 0.0f || (le.x + le.y) + le.z > 0.0f) return vadd(out, vscale(le, mat->emitted));
+    if (ch.gi < s->max_bounces - 1) {
+        v3 randD = cosine_sample(c, theNormal);
+        ray_t gr = make_ray(P, randD);
+        hit_t nh;
+        if (trace_secondary(c, &gr, &nh)) {
+            ior_list child;
+            child.v[0] = 1.0f; child.v[1] = curIOR; child.idx = 1;   /* Ray(threadID) + set(.., r_IOR(), ..) */
+            chain_t cc = {ch.bounces, ch.gi + 1, 1, ch.level + 1};
+            out = vadd(out, vmul(kd, shade_child(c, &gr, &nh, &child, cc)));
+        } else if (mat->sample_env && s->sample_env) {
+            out = vadd(out, vmul(kd, env_color(s, randD)));
+        }
+    } else {
+        for (int i = 0; i < s->n_lights; i++) {
+            float lightSpec = 0;
+            v3 E = sample_light(c, i, P, theNormal, V(0, 0, 0), &lightSpec, 1);
+            out = vadd(out, vmul(E, kd));
+        }
+    }
+    return out;
+}
+
 /* Blinn::shade, src/Blinn.cpp:91-335: Fresnel-weighted Russian roulette between
- * direct lighting and one reflection or refraction ray (bounces < 5), with the
- * ray's IOR history, glossy reflection vector, translucency (no maps, no path tracing,
- * no dispersion). */
+ * direct lighting (+ path tracing) and one reflection or refraction ray (bounces
+ * < 5), with the ray's IOR history, glossy reflection vector, translucency and
+ * m_Le (no texture maps, no dispersion). */
 static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h, ior_list* ior,
-                      int bounces) {
+                      chain_t ch) {
+    begin_level(c, ch.level);
     v3 Ld = V(0, 0, 0), Ls = V(0, 0, 0), Lr = V(0, 0, 0), Lt = V(0, 0, 0), translucency = V(0, 0, 0);
     v3 rayD = V(r->d[0], r->d[1], r->d[2]);
     v3 viewDir = vneg(rayD);
@@ -1383,7 +1457,7 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
     }
     float outIOR;
     const float inIOR = ior->v[ior->idx];
-    if (flip) {             /* leaving the material: pop the ray's history */
+    if (flip) {             /* leaving the material: pop the ray's (mutable) history */
         if (ior->idx > 0) ior->idx--;
         outIOR = ior->v[ior->idx];
     } else {
@@ -1400,11 +1474,11 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
     float rrWeightRecipSpec = (1.f - rrWeight > 0.f) ? 1.f / (1.f - rrWeight) : 1.f;
     v3 ks = V(mat->ks[0], mat->ks[1], mat->ks[2]);
     v3 kd = V(mat->kd[0], mat->kd[1], mat->kd[2]);
-    v3 zero = V(0, 0, 0);
     if (rrFloat <= rrWeight) {
+        if (c->s->path_trace) Ld = vadd(Ld, path_trace(c, mat, P, theNormal, kd, ior->v[ior->idx], ch));
         for (int i = 0; i < c->s->n_lights; i++) {
             float lightSpec = 0;
-            v3 E = sample_light(c, i, P, theNormal, rVec, &lightSpec);
+            v3 E = sample_light(c, i, P, theNormal, rVec, &lightSpec, ch.secondary);
             /* libm pow of the reference, evaluated in double and rounded once */
             float pw = (float)pow((double)lightSpec, (double)mat->specExp);
             Ls = vadd(Ls, vscale(vscale(vmul(E, ks), mat->specAmt), pw));
@@ -1414,24 +1488,21 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
             v3 lightTotal = V(0, 0, 0);
             for (int i = 0; i < c->s->n_lights; i++) {
                 float lightSpec = 0;
-                lightTotal = vadd(lightTotal, sample_light(c, i, P, vneg(theNormal), rVec, &lightSpec));
+                lightTotal = vadd(lightTotal, sample_light(c, i, P, vneg(theNormal), rVec, &lightSpec, ch.secondary));
             }
             translucency = vadd(translucency, vmul(vscale(lightTotal, mat->translucency), kd));
         }
     } else {
         int doEnv = 1;
         rrFloat = next_rand(c);
+        chain_t cc = {ch.bounces + 1, ch.gi, 0, ch.level + 1};   /* shade(..) default isSecondary = false */
         if (rrFloat < mat->reflect * Rs) {
-            if (mat->reflect * Rs > 0.0f && bounces < 5) {
+            if (mat->reflect * Rs > 0.0f && ch.bounces < 5) {
                 ior_list child = *ior;
                 ray_t rr = make_ray(P, rVec);
-                hit_t nh = {1e12f, 0, 0, -1, -1};
-                uint32_t nv = 0, lv = 0;
-                c->secondary_rays++;
-                int hit = bvh_intersect(c->s, &rr, 0.001f, &nh, &nv, &lv) > 0;
-                c->nodes += nv; c->leaves += lv;
-                if (hit) {
-                    Lr = vadd(Lr, vmul(ks, shade_hit(c, &rr, &nh, &child, bounces + 1)));
+                hit_t nh;
+                if (trace_secondary(c, &rr, &nh)) {
+                    Lr = vadd(Lr, vmul(ks, shade_child(c, &rr, &nh, &child, cc)));
                     doEnv = 0;
                 }
             }
@@ -1440,17 +1511,15 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
             float snellsQ = inIOR / outIOR;
             float sqrtPart = std_max(0.0f, sqrtf(1.0f - (snellsQ * snellsQ) * (1.0f - vDotN * vDotN)));
             v3 tVec = vnormalized(vadd(vscale(rayD, snellsQ), vscale(theNormal, snellsQ * vDotN - sqrtPart)));
-            if (bounces < 5) {
-                ior_list child = *ior;     /* push, trace with the copy, pop */
-                child.v[++child.idx] = outIOR;
+            if (ch.bounces < 5) {
+                /* ray.r_IOR.push(outIOR) on the mutable history, the child copies it, then pop */
+                ior->v[ior->idx + 1] = outIOR;
+                ior_list child = *ior;
+                child.idx = ior->idx + 1;
                 ray_t tr = make_ray(P, tVec);
-                hit_t nh = {1e12f, 0, 0, -1, -1};
-                uint32_t nv = 0, lv = 0;
-                c->secondary_rays++;
-                int hit = bvh_intersect(c->s, &tr, 0.001f, &nh, &nv, &lv) > 0;
-                c->nodes += nv; c->leaves += lv;
-                if (hit) {
-                    Lt = vadd(Lt, vmul(ks, shade_hit(c, &tr, &nh, &child, bounces + 1)));
+                hit_t nh;
+                if (trace_secondary(c, &tr, &nh)) {
+                    Lt = vadd(Lt, vmul(ks, shade_child(c, &tr, &nh, &child, cc)));
                     doEnv = 0;
                 }
             }
@@ -1459,14 +1528,15 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
     }
     Ld = vadd(Ld, V(mat->ka[0], mat->ka[1], mat->ka[2]));
     /* (Ld + Ls + translucency)*rrWeightRecip + (Lr + Lt)*rrWeightRecipSpec + m_Le */
-    return vadd(vadd(vscale(vadd(vadd(Ld, Ls), translucency), rrWeightRecip), vscale(vadd(Lr, Lt), rrWeightRecipSpec)), zero);
+    return vadd(vadd(vscale(vadd(vadd(Ld, Ls), translucency), rrWeightRecip), vscale(vadd(Lr, Lt), rrWeightRecipSpec)),
+                V(mat->le[0], mat->le[1], mat->le[2]));
 }
 
 /* Material::shade dispatch of a hit */
-static v3 shade_hit(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior, int bounces) {
+static v3 shade_hit(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior, chain_t ch) {
     int tri;
     const oro_material* mat = &c->s->mats[hit_mesh(c->s, h, &tri)->material];
-    return mat->type == ORO_LAMBERT ? shade_lambert(c, mat, r, h) : shade_blinn(c, mat, r, h, ior, bounces);
+    return mat->type == ORO_LAMBERT ? shade_lambert(c, mat, r, h, ch.level) : shade_blinn(c, mat, r, h, ior, ch);
 }
 
 /* ---------------------------------------------------------------- camera */
@@ -1539,20 +1609,21 @@ static uint8_t map_channel(float r) {
 }
 
 /* ---------------------------------------------------------------- render */
-/* Scene::sampleScene, src/Scene.cpp:219-243 */
+/* Scene::sampleScene, src/Scene.cpp:219-243.  The m_numPaths shade() calls share
+ * the camera ray and so its IOR history, which Blinn::shade pops on a back-face
+ * hit (src/Blinn.cpp:176-179): the pops persist from one path to the next. */
 static v3 sample_scene(shade_ctx* c, const ray_t* r, hit_t* h, uint32_t* prim_nv, uint32_t* prim_lv) {
     const oro_scene* s = c->s;
     h->t = 1e12f; h->a = h->b = 0; h->prim = -1; h->inst = -1;
     int rc = bvh_intersect(s, r, 0.001f, h, prim_nv, prim_lv);
     if (rc > 0) {
         v3 result = V(0, 0, 0);
-        int tri;
-        const oro_material* mat = &s->mats[hit_mesh(s, h, &tri)->material];
+        ior_list ior;           /* the camera ray's history: 1, then 1.001 */
+        ior.v[0] = 1.0f; ior.v[1] = 1.001f; ior.idx = 1;
         for (int i = 0; i < s->num_paths; i++) {
-            ior_list ior;           /* the camera ray's history: 1, then 1.001 */
-            ior.v[0] = 1.0f; ior.v[1] = 1.001f; ior.idx = 1;
-            v3 sh = (mat->type == ORO_LAMBERT) ? shade_lambert(c, mat, r, h) : shade_blinn(c, mat, r, h, &ior, 0);
-            result = vadd(result, sh);
+            c->skey = c->sample * 1024u + (uint32_t)i;
+            chain_t ch = {0, 0, 0, 0};
+            result = vadd(result, shade_hit(c, r, h, &ior, ch));
         }
         return vscale(result, 1.0f / (float)s->num_paths);
     }
@@ -1586,7 +1657,7 @@ static v3 adaptive_levels(shade_ctx* c, const cam_basis* b, int x, int y, v3 sha
             for (int j = 0; j < curLevel; j++) {
                 float offset = 1.0f / (float)curLevel;
                 c->sample++;
-                c->dim = 0;
+                begin_camera(c);
                 float urand = next_rand(c), vrand = next_rand(c);
                 (void)next_rand(c);      /* getTimeSample */
                 ray_t r = camera_ray_adaptive(b, x, y, i * offset, (i + 1) * offset, j * offset, (j + 1) * offset,
@@ -1631,6 +1702,7 @@ int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H, int x0, 
         for (int x = x0; x < x1; x++) {
             shade_ctx c; memset(&c, 0, sizeof c);
             c.s = s; c.pixel = (uint32_t)(y * W + x);
+            begin_camera(&c);
             float urand = next_rand(&c), vrand = next_rand(&c);
             (void)next_rand(&c);            /* getTimeSample draw, src/Camera.cpp:154 */
             ray_t r = camera_ray(&b, x, y, urand, vrand);

@@ -41,6 +41,9 @@ typedef struct {
     float ior;              /* Blinn m_ior (src/Blinn.cpp:25-27)                */
     float gloss;            /* Blinn m_specGloss (src/Blinn.h:42,65)           */
     float translucency;     /* Material::m_translucency (src/Material.h:30,44) */
+    float le[3];            /* Blinn m_Le (src/Blinn.h:64), added to shade()   */
+    float emitted;          /* Blinn m_lightEmitted (src/Blinn.h:63)           */
+    int sample_env;         /* Material::m_sampleEnv (src/Material.h:43)       */
 } oro_material;
 
 typedef struct {
@@ -82,6 +85,8 @@ int oro_scene_add_material(oro_scene* s, const oro_material* m);
 int oro_scene_add_light(oro_scene* s, const oro_light* l);
 void oro_scene_set_bg(oro_scene* s, float r, float g, float b);
 void oro_scene_set_num_paths(oro_scene* s, int n);
+/* Scene::m_pathTrace / m_maxBounces / m_sampleLightFromEnv (src/Scene.h:40-64) */
+int oro_scene_set_path_trace(oro_scene* s, int enable, int max_bounces, int sample_env);
 /* Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55); 0 = OK */
 int oro_scene_set_subdivs(oro_scene* s, int min_subdivs, int max_subdivs, float noise);
 /* Scene::preCalc -> BVH::build (src/Scene.cpp:62-79, src/BVH.cpp:457-575). */
@@ -149,7 +154,9 @@ float oro_x86_rsqrt(float x);
 float oro_rcp_nr(float x);
 float oro_rsqrt_nr(float x);
 void oro_gamma_table(uint8_t* lut32769);
-/* counter-based RNG used in place of the reference's global MT pool */
+/* counter-based RNG used in place of the reference's global MT pool.  Keys:
+ * skey = eye-ray sample * 1024 + path, dim = (chain level + 1) << 24 | k for the
+ * k-th draw of one shade() call (the camera ray's draws are dims 0-2). */
 float oro_rand(uint32_t pixel, uint32_t sample, uint32_t dim, uint32_t seed);
 
 #ifdef __cplusplus

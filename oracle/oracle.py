@@ -35,7 +35,7 @@ class Material(C.Structure):
     _fields_ = [("type", C.c_int), ("kd", C.c_float * 3), ("ka", C.c_float * 3), ("ks", C.c_float * 3),
                 ("specExp", C.c_float), ("specAmt", C.c_float),
                 ("reflect", C.c_float), ("refract", C.c_float), ("ior", C.c_float), ("gloss", C.c_float),
-                ("translucency", C.c_float)]
+                ("translucency", C.c_float), ("le", C.c_float * 3), ("emitted", C.c_float), ("sample_env", C.c_int)]
 
 
 class Light(C.Structure):
@@ -72,6 +72,7 @@ def _declare(L):
     L.oro_scene_add_light.argtypes = [C.c_void_p, C.POINTER(Light)]
     L.oro_scene_set_bg.argtypes = [C.c_void_p, C.c_float, C.c_float, C.c_float]
     L.oro_scene_set_num_paths.argtypes = [C.c_void_p, C.c_int]
+    L.oro_scene_set_path_trace.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
     L.oro_scene_set_subdivs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float]
     L.oro_scene_build.argtypes = [C.c_void_p]
     L.oro_qbvh_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 6
@@ -145,10 +146,12 @@ class OracleScene:
             pass
 
     def add_material(self, kind="lambert", kd=(1, 1, 1), ka=(0, 0, 0), ks=(1, 1, 1), specExp=1.0, specAmt=0.0,
-                     reflectAmt=0.0, refractAmt=0.0, ior=1.5, specGloss=1.0, translucency=0.0):
-        """Lambert / Blinn (src/Blinn.h:11-22 defaults: ior 1.5, no reflection / refraction)."""
+                     reflectAmt=0.0, refractAmt=0.0, ior=1.5, specGloss=1.0, translucency=0.0, le=(0, 0, 0),
+                     emitted=0.0, sampleEnv=True):
+        """Lambert / Blinn (src/Blinn.h:11-22 defaults: ior 1.5, no reflection / refraction;
+        setLightEmittedColor / setLightEmittedIntensity -> le / emitted; Material::setSampleEnv)."""
         m = Material(0 if kind == "lambert" else 1, _v3(kd), _v3(ka), _v3(ks), specExp, specAmt,
-                     reflectAmt, refractAmt, ior, specGloss, translucency)
+                     reflectAmt, refractAmt, ior, specGloss, translucency, _v3(le), emitted, int(bool(sampleEnv)))
         return self.L.oro_scene_add_material(self.h, C.byref(m))
 
     def add_obj(self, path, material, ctm=None):
@@ -278,6 +281,11 @@ class OracleScene:
 
     def set_num_paths(self, n):
         self.L.oro_scene_set_num_paths(self.h, int(n))
+
+    def set_path_trace(self, enable=True, max_bounces=10, sample_env=False):
+        """Scene::m_pathTrace / m_maxBounces / setSampleEnv (src/Scene.h:40-64)."""
+        if self.L.oro_scene_set_path_trace(self.h, int(bool(enable)), int(max_bounces), int(bool(sample_env))) != 0:
+            raise ValueError("need 1 <= max_bounces <= 64")
 
     def set_subdivs(self, min_subdivs, max_subdivs, noise=0.01):
         """Scene::setMinSubdivs / setMaxSubdivs / setNoise (src/Scene.h:42-55)."""

@@ -20,7 +20,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cmath>
+#include <string>
 
 #include "mrt_scene.h"
 
@@ -581,10 +583,18 @@ int build_qbvh(Scene& s, std::string& err) {
         err = "scene has no triangles";
         return MRT_ERR_BUILD;
     }
-    int32_t base = (int32_t)s.obj_mesh.size();  // instance hit ids follow the world objects
+    // instance hit ids follow the world objects; every id must fit mrt_hit.prim
+    // (int32) -- the reference's 201 x 201 proxy grid (src/main.cpp:37-51) of a
+    // >53k-triangle BLAS would not
+    int64_t base = (int64_t)s.obj_mesh.size();
     for (Instance& I : s.instances) {
-        I.hit_base = base;
-        base += (int32_t)s.blas[I.blas].obj_mesh.size();
+        if (base > (int64_t)INT32_MAX) break;
+        I.hit_base = (int32_t)base;
+        base += (int64_t)s.blas[I.blas].obj_mesh.size();
+    }
+    if (base - 1 > (int64_t)INT32_MAX) {
+        err = "world objects + instances x BLAS objects exceed 2^31 hit ids (" + std::to_string(base) + ")";
+        return MRT_ERR_INVALID;
     }
     Builder b(s, s.obj_mesh, s.obj_tri, &s.obj_inst, s.nodes, s.leaves);
     int rc = b.run(err);

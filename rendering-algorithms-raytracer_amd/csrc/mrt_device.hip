@@ -92,6 +92,9 @@ struct RenderParams {
     CamParams cam[kMaxBatch];    // frame mode: cam[0]; batch mode: one camera per frame
     float bg[3];
     int32_t n_lights, num_paths;
+    int32_t path_trace, max_bounces, sample_env;  // Scene::m_pathTrace / m_maxBounces / sampleEnv
+    float* lvl;                  // REC kernels: chain level records, (level * lvl_words + w) * gstride + thread
+    int32_t lvl_words;           //   words per level record
     uint32_t seed;
     int32_t fast_box;            // node boxes finite && tuning allows the hardware min/max box test
     int32_t sched;               // tile schedule (TileSched)
@@ -130,21 +133,34 @@ __device__ __forceinline__ v3 xform_dir3(const float* T, v3 u) {
 // REC: the scene has reflective / refractive materials (Blinn secondary rays,
 // shade_path); compiled only into the kernels that run such scenes, so the
 // direct-lighting kernels keep their register budget.
-template <bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused, bool REC = false>
+// RNG keys of the counter RNG (mrt_math.h): sub-stream skey = eye-ray sample *
+// 1024 + path, draw key dim = (chain level + 1) << 24 | k (camera: dims 0-2).
+__device__ __forceinline__ uint32_t level_key(int level) { return (uint32_t)(level + 1) << 24; }
+
+// Working IOR history of the rays below the camera ray (Ray::IORList,
+// src/Ray.h:43-50): a per-lane LDS column in the REC kernels.
+static constexpr int kIorCap = 8;
+
+// REC: 0 direct lighting only; 1 Blinn reflection / refraction chains; 2 also
+// path tracing (GI rays).  Compiled into the kernels that run such scenes only.
+template <bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused, int REC = 0>
 struct Shader {
     const RenderParams& P;
     const Trav& T;
     const uint16_t* rcpT;
     const uint16_t* rsqT;
     TravStats& st;
-    uint32_t pixel, dim;
+    uint32_t pixel;
     uint32_t shadow_rays;
     uint32_t seed;
     size_t slot0;            // wavefront modes: this pixel's first ray slot
     uint32_t nslot;          //   rays so far
     uint32_t sample = 0;     // eye-ray sample of the pixel (adaptive supersampling)
+    uint32_t skey = 0, dim = 0;  // RNG sub-stream / draw key
+    float* iorS = nullptr;   // REC: LDS IOR column (stride kWG)
+    float* lvl = nullptr;    // REC: this thread's level records (stride P.gstride)
 
-    __device__ float next_rand() { return rng(pixel, sample, dim++, seed); }
+    __device__ float next_rand() { return rng(pixel, skey, dim++, seed); }
 
     template <bool COUNT>
     __device__ bool occluded(v3 from, v3 L, float tMax) {
@@ -224,15 +240,16 @@ struct Shader {
         return scale(acc, recip);
     }
 
-    // DomeLight::sampleLight, src/DomeLight.cpp:80-160 (fast shadows; primary
-    // shading, so m_numSamples draws).  A draw below the shading horizon is
+    // DomeLight::sampleLight, src/DomeLight.cpp:80-160 (fast shadows; m_numSamples
+    // draws, one for secondary shading, :89).  A draw below the shading horizon is
     // redrawn without counting it (`continue` at :106 skips samplesDone++); after
     // kDomeMaxRejects such redraws in one call the loop stops (the reference would
     // not terminate when the whole map lies below the horizon).
     static constexpr int kDomeMaxRejects = 256;
     template <bool COUNT>
-    __device__ v3 dome_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec) {
+    __device__ v3 dome_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec, bool secondary) {
         const DevDome& D = P.domes[l.dome];
+        const int numSamples = secondary ? 1 : l.samples;
         v3 acc = mk(0, 0, 0);
         float tmpSpec = 0.f, recip = 1.0f;
         int done = 0, rejects = 0;
@@ -265,20 +282,21 @@ struct Shader {
             cut = (((Es.x + Es.y) + Es.z) * 0.333333f) < l.noise;
             acc = add(acc, scale(E, att));
             tmpSpec += dot(rVec, dir) * att;
-        } while (done < l.samples && !cut);
+        } while (done < numSamples && !cut);
         outSpec = tmpSpec * recip;
         return scale(acc, recip);
     }
 
+    // Light::sampleLight dispatch; `secondary` = the isSecondary argument
     template <bool COUNT>
-    __device__ v3 sample_light(int li, v3 from, v3 normal, v3 rVec, float& spec) {
+    __device__ v3 sample_light(int li, v3 from, v3 normal, v3 rVec, float& spec, bool secondary = false) {
         const DevLight& l = P.lights[li];
         if (POINT_ONLY || l.type == MRT_POINT_LIGHT) {
             float e = point_light<COUNT>(l, from, normal, rVec, spec);
             return mk(e, e, e);
         }
         if constexpr (!POINT_ONLY) {
-            if (l.type == MRT_DOME_LIGHT) return dome_light<COUNT>(l, from, normal, rVec, spec);
+            if (l.type == MRT_DOME_LIGHT) return dome_light<COUNT>(l, from, normal, rVec, spec, secondary);
             return rect_light<COUNT>(l, from, normal, rVec, spec);
         }
         return mk(0, 0, 0);
@@ -313,7 +331,8 @@ struct Shader {
         mat = ps.mat;
     }
 
-    // Scene::sampleScene hit branch (src/Scene.cpp:224-233)
+    // Scene::sampleScene hit branch (src/Scene.cpp:224-233): m_numPaths shade()
+    // calls on the camera ray, each path its own RNG sub-stream.
     template <bool COUNT>
     __device__ v3 shade(const DRay& r, const DHit& h) {
         v3 N, geoN;
@@ -323,10 +342,15 @@ struct Shader {
         v3 P_ = mk(r.o[0] + h.t * r.d[0], r.o[1] + h.t * r.d[1], r.o[2] + h.t * r.d[2]);  // Ray::getPoint
         v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
         v3 result = mk(0, 0, 0);
+        // the camera ray's IOR history [1, 1.001]: Blinn::shade pops it on a
+        // back-face hit and the pop persists into the next path (src/Blinn.cpp:176-179)
+        IorCam cam;
         for (int path = 0; path < P.num_paths; path++) {
+            skey = sample * 1024u + (uint32_t)path;
+            dim = level_key(0);
             v3 sh;
-            if constexpr (MODE == kFused && REC) {   // reflective / refractive materials in the scene
-                result = add(result, shade_path<COUNT>(r, h));
+            if constexpr (MODE == kFused && REC) {   // secondary rays / path tracing in the scene
+                result = add(result, shade_path<COUNT>(r, h, cam));
                 continue;
             }
             if (M.type == MRT_LAMBERT) {  // Lambert::shade
@@ -358,7 +382,7 @@ struct Shader {
                 }
                 Ld = add(Ld, ka);
                 v3 z = mk(0, 0, 0);
-                sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), z);
+                sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), mk(M.le[0], M.le[1], M.le[2]));
             }
             result = add(result, sh);
         }
@@ -398,33 +422,44 @@ struct Shader {
         return mk(P.bg[0], P.bg[1], P.bg[2]);
     }
 
-    // Material::shade of one hit with Blinn's secondary rays (src/Blinn.cpp:91-335):
-    // Fresnel-weighted Russian roulette between direct lighting and one reflection
-    // or refraction ray (bounces < 5), with the ray's IOR history (Ray::IORList,
-    // src/Ray.h:43-50).  The recursion is a path (one child per level), so it runs
-    // as a loop: each level that spawns a ray which hits keeps its own terms
-    // (direct part x rrWeightRecip, ks, rrWeightRecipSpec, reflect / refract) and
-    // the levels are combined deepest first, in the reference's operation order.
+    // the camera ray's history: [1, 1.001, (a level-0 refraction push)] and its index
+    struct IorCam {
+        float v1 = 1.001f, v2 = 0.f;
+        int idx = 1;
+        __device__ float at(int i) const { return i == 0 ? 1.0f : (i == 1 ? v1 : v2); }
+    };
+    __device__ float& ior_at(int i) { return iorS[i * kWG]; }
+    // level record word w of chain level k (global memory, one column per thread)
+    __device__ float& rec(int k, int w) { return lvl[((size_t)k * P.lvl_words + w) * P.gstride]; }
+
+    // Material::shade of one hit with Blinn's secondary rays and path tracing
+    // (src/Blinn.cpp:39-335): Fresnel-weighted Russian roulette between direct
+    // lighting (+ Blinn::calculatePathTracing's GI ray) and one reflection or
+    // refraction ray (bounces < 5), with each ray's IOR history (Ray::IORList,
+    // src/Ray.h:43-50).  Every level spawns at most one child, so the recursion
+    // runs as a loop down the chain: a level whose child ray hits writes its
+    // terms to a global level record -- reflect / refract: rrWeightRecip,
+    // rrWeightRecipSpec; GI: also Ls, the translucency and each light's E * kd,
+    // sampled before descending (each level draws from its own RNG key) -- and the
+    // levels are combined deepest first in the reference's operation order.
     static constexpr int kMaxBounce = 5;
     uint32_t secondary = 0;
+    enum { kRefl = 1, kRefr = 2, kGI = 3 };
     template <bool COUNT>
-    __device__ v3 shade_path(DRay r, DHit h) {
+    __device__ v3 shade_path(DRay r, DHit h, IorCam& cam) {
         const v3 z = mk(0, 0, 0);
-        v3 lvA[kMaxBounce], lvKs[kMaxBounce];
-        float lvW[kMaxBounce];
-        bool lvRefr[kMaxBounce];
-        float ior[kMaxBounce + 3];   // [0] = 1, the camera ray pushes 1.001, one push per refraction level
-        ior[0] = 1.0f; ior[1] = 1.001f;
-        int idx = 1, depth = 0;
+        int idx = 0, depth = 0, gi = 0, bounces = 0;
+        bool isSecondary = false;
         v3 val;
         for (;;) {
+            dim = level_key(depth);
             v3 N, geoN;
             uint32_t mi;
             normals(h, N, geoN, mi);
             const DevMaterial& M = P.mats[mi];
             const v3 Pt = mk(r.o[0] + h.t * r.d[0], r.o[1] + h.t * r.d[1], r.o[2] + h.t * r.d[2]);
             const v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
-            if (M.type == MRT_LAMBERT) {   // Lambert::shade: no secondary rays
+            if (M.type == MRT_LAMBERT) {   // Lambert::shade: no secondary rays (isSecondary not passed on)
                 v3 L = z;
                 for (int i = 0; i < P.n_lights; i++) {
                     float discard;
@@ -433,6 +468,7 @@ struct Shader {
                 val = add(L, ka);
                 break;
             }
+            const v3 le = mk(M.le[0], M.le[1], M.le[2]);
             const v3 rayD = mk(r.d[0], r.d[1], r.d[2]);
             const v3 viewDir = neg(rayD);
             float vDotN = dot(viewDir, N);
@@ -447,12 +483,16 @@ struct Shader {
                 const v3 rd = cosine_sample(n);
                 rVec = normalized(add(scale(rVec, M.gloss), scale(rd, 1.0f - M.gloss)), rsqT);
             }
-            const float inIOR = ior[idx];
-            float outIOR = M.ior;
-            if (flip) {   // leaving the material: pop the history
-                if (idx > 0) idx--;
-                outIOR = ior[idx];
+            // inIOR, then a back-face hit pops the (mutable) history (src/Blinn.cpp:167-185)
+            float inIOR, outIOR = M.ior;
+            if (depth == 0) {
+                inIOR = cam.at(cam.idx);
+                if (flip) { if (cam.idx > 0) cam.idx--; outIOR = cam.at(cam.idx); }
+            } else {
+                inIOR = ior_at(idx);
+                if (flip) { if (idx > 0) idx--; outIOR = ior_at(idx); }
             }
+            const float curIOR = depth == 0 ? cam.at(cam.idx) : ior_at(idx);   // r_IOR() after the pop
             float Rs = 0.f, Ts = 0.f;
             if (M.reflect > 0.0f || M.refract > 0.0f) {
                 Rs = fresnel(inIOR, outIOR, vDotN);
@@ -464,25 +504,60 @@ struct Shader {
             const float rrSpec = (1.f - rrW > 0.f) ? 1.f / (1.f - rrW) : 1.f;
             const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
             if (rr <= rrW) {   // direct lighting
-                v3 Ld = z, Ls = z;
+                bool child = false;
+                DRay r2;
+                DHit h2{1e12f, 0.f, 0.f, -1};
+                v3 Ld = z;
+                if constexpr (REC == 2) {   // Blinn::calculatePathTracing (src/Blinn.cpp:39-89)
+                    v3 pt = z;
+                    if (M.emitter) {
+                        pt = add(z, scale(le, M.emitted));
+                    } else if (gi < P.max_bounces - 1) {
+                        const v3 randD = cosine_sample(n);
+                        r2 = make_ray(Pt, randD);
+                        secondary++;
+                        if (traverse<false, COUNT, FAST, INST>(T, r2, 0.001f, h2, st)) child = true;
+                        else if (M.sample_env && P.sample_env) pt = add(z, mul(kd, env_color(randD)));
+                    } else {   // last bounce: the lights directly, isSecondary, rVec = 0
+                        for (int i = 0; i < P.n_lights; i++) {
+                            float spec = 0.f;
+                            pt = add(pt, mul(sample_light<COUNT>(i, Pt, n, z, spec, true), kd));
+                        }
+                    }
+                    if (!child) Ld = add(Ld, pt);
+                }
+                v3 Ls = z;
                 for (int i = 0; i < P.n_lights; i++) {
                     float spec = 0.f;
-                    v3 E = sample_light<COUNT>(i, Pt, n, rVec, spec);
+                    v3 E = sample_light<COUNT>(i, Pt, n, rVec, spec, isSecondary);
                     float pw = (M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
                     Ls = add(Ls, scale(scale(mul(E, ks), M.spec_amt), pw));
-                    Ld = add(Ld, mul(E, kd));
+                    const v3 term = mul(E, kd);
+                    if (child) { rec(depth, 9 + 3 * i) = term.x; rec(depth, 10 + 3 * i) = term.y; rec(depth, 11 + 3 * i) = term.z; }
+                    else Ld = add(Ld, term);
                 }
                 v3 tr = z;
                 if (M.translucency > 0.01f) {   // lights seen through the surface (src/Blinn.cpp:224-236)
                     v3 total = z;
                     for (int i = 0; i < P.n_lights; i++) {
                         float spec = 0.f;
-                        total = add(total, sample_light<COUNT>(i, Pt, neg(n), rVec, spec));
+                        total = add(total, sample_light<COUNT>(i, Pt, neg(n), rVec, spec, isSecondary));
                     }
                     tr = add(z, mul(scale(total, M.translucency), kd));
                 }
+                if (child) {   // descend into the GI ray: IOR history [1, current]
+                    rec(depth, 0) = __int_as_float((int)mi | (kGI << 16));
+                    rec(depth, 1) = rrRecip; rec(depth, 2) = rrSpec;
+                    rec(depth, 3) = Ls.x; rec(depth, 4) = Ls.y; rec(depth, 5) = Ls.z;
+                    rec(depth, 6) = tr.x; rec(depth, 7) = tr.y; rec(depth, 8) = tr.z;
+                    ior_at(0) = 1.0f; ior_at(1) = curIOR; idx = 1;
+                    depth++; gi++;
+                    isSecondary = true;
+                    r = r2; h = h2;
+                    continue;
+                }
                 Ld = add(Ld, ka);
-                val = add(add(scale(add(add(Ld, Ls), tr), rrRecip), scale(add(z, z), rrSpec)), z);
+                val = add(add(scale(add(add(Ld, Ls), tr), rrRecip), scale(add(z, z), rrSpec)), le);
                 break;
             }
             const v3 base = scale(add(add(add(z, ka), z), z), rrRecip);   // (Ld + Ls + translucency) * rrWeightRecip
@@ -492,15 +567,26 @@ struct Shader {
             if (rr < M.reflect * Rs) {
                 refr = false;
                 dir = rVec;
-                spawn = M.reflect * Rs > 0.0f && depth < kMaxBounce;
+                spawn = M.reflect * Rs > 0.0f && bounces < kMaxBounce;
+                if (spawn && depth == 0) {   // the child copies the camera ray's history
+                    ior_at(0) = 1.0f; ior_at(1) = cam.v1; ior_at(2) = cam.v2; idx = cam.idx;
+                }
             } else if (M.refract * Ts > 0.0f) {
                 refr = true;
                 const float q = inIOR / outIOR;
                 const float sq = std_max(0.0f, sqrtf(1.0f - (q * q) * (1.0f - vDotN * vDotN)));
                 dir = normalized(add(scale(rayD, q), scale(n, q * vDotN - sq)), rsqT);
-                spawn = depth < kMaxBounce;
+                spawn = bounces < kMaxBounce;
+                if (spawn) {   // r_IOR.push(outIOR) on the mutable history, the child copies it
+                    if (depth == 0) {
+                        if (cam.idx == 0) cam.v1 = outIOR; else cam.v2 = outIOR;
+                        ior_at(0) = 1.0f; ior_at(1) = cam.v1; ior_at(2) = cam.v2; idx = cam.idx + 1;
+                    } else {
+                        ior_at(idx + 1) = outIOR; idx++;
+                    }
+                }
             } else {   // refraction branch with nothing to refract: Lr = Lt = 0
-                val = add(add(base, scale(add(z, z), rrSpec)), z);
+                val = add(add(base, scale(add(z, z), rrSpec)), le);
                 break;
             }
             if (spawn) {
@@ -508,21 +594,35 @@ struct Shader {
                 DHit h2{1e12f, 0.f, 0.f, -1};
                 secondary++;
                 if (traverse<false, COUNT, FAST, INST>(T, r2, 0.001f, h2, st)) {
-                    lvA[depth] = base; lvKs[depth] = ks; lvW[depth] = rrSpec; lvRefr[depth] = refr;
-                    depth++;
-                    if (refr) ior[++idx] = outIOR;   // the child's history: push (the parent pops after)
-                    r = r2;
-                    h = h2;
+                    rec(depth, 0) = __int_as_float((int)mi | ((refr ? kRefr : kRefl) << 16));
+                    rec(depth, 1) = rrRecip; rec(depth, 2) = rrSpec;
+                    depth++; bounces++;
+                    isSecondary = false;   // shade(..) with the default isSecondary
+                    r = r2; h = h2;
                     continue;
                 }
             }
             const v3 L = add(z, mul(ks, env_color(dir)));   // Lr / Lt += m_ks * environment
-            val = add(add(base, scale(refr ? add(z, L) : add(L, z), rrSpec)), z);
+            val = add(add(base, scale(refr ? add(z, L) : add(L, z), rrSpec)), le);
             break;
         }
-        for (int k = depth - 1; k >= 0; k--) {   // Lr / Lt += m_ks * shade(child)
-            const v3 L = add(z, mul(lvKs[k], val));
-            val = add(add(lvA[k], scale(lvRefr[k] ? add(z, L) : add(L, z), lvW[k])), z);
+        for (int k = depth - 1; k >= 0; k--) {   // combine deepest first
+            const int info = __float_as_int(rec(k, 0));
+            const DevMaterial& M = P.mats[info & 0xFFFF];
+            const int kind = info >> 16;
+            const float rrRecip = rec(k, 1), rrSpec = rec(k, 2);
+            const v3 le = mk(M.le[0], M.le[1], M.le[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+            if (kind == kGI) {   // Ld = 0 + (0 + kd * child) + each light's E * kd + ka
+                v3 Ld = add(z, add(z, mul(mk(M.kd[0], M.kd[1], M.kd[2]), val)));
+                for (int i = 0; i < P.n_lights; i++) Ld = add(Ld, mk(rec(k, 9 + 3 * i), rec(k, 10 + 3 * i), rec(k, 11 + 3 * i)));
+                Ld = add(Ld, ka);
+                const v3 Ls = mk(rec(k, 3), rec(k, 4), rec(k, 5)), tr = mk(rec(k, 6), rec(k, 7), rec(k, 8));
+                val = add(add(scale(add(add(Ld, Ls), tr), rrRecip), scale(add(z, z), rrSpec)), le);
+            } else {   // Lr / Lt += m_ks * shade(child)
+                const v3 L = add(z, mul(mk(M.ks[0], M.ks[1], M.ks[2]), val));
+                const v3 base = scale(add(add(add(z, ka), z), z), rrRecip);
+                val = add(add(base, scale(kind == kRefr ? add(z, L) : add(L, z), rrSpec)), le);
+            }
         }
         return val;
     }
@@ -759,10 +859,11 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
 }
 
 // Kernel 2: Scene::sampleScene shading of the primary hit with shadow rays.
-template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused, bool REC = false>
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused, int REC = 0>
 __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
+    __shared__ float s_ior[REC ? kIorCap * kWG : 1];
     load_tables(P.tables, s_tab, 1024);
     const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
@@ -796,8 +897,9 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             const CamParams& cam = P.cam[f];
             const uint32_t seed = P.seed + (uint32_t)f;
             DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, seed, x, y, rsqT));
-            Shader<POINT_ONLY, FAST, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 3u, 0u, seed,
+            Shader<POINT_ONLY, FAST, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 0u, seed,
                                                    slot * (size_t)P.max_shadow, 0u};
+            if constexpr (REC) { S.iorS = s_ior + tid; S.lvl = P.lvl + (blockIdx.x * kWG + tid); }
             col = S.template shade<COUNT>(r, h);
             shadow_total += S.shadow_rays;
             secondary_total += S.secondary;
@@ -846,10 +948,11 @@ __device__ __forceinline__ float gamma_f(const float* lut, float v) {
 // gamma-space stop test after every level.  Eye ray k of a pixel draws from
 // RNG stream (pixel, k): ray 0 is the 1-spp frame path's ray.  Lanes of a wave
 // stop independently; the wave runs until its last lane is done.
-template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST, bool REC = false>
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST, int REC = 0>
 __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
+    __shared__ float s_ior[REC ? kIorCap * kWG : 1];
     load_tables(P.tables, s_tab, 1024);
     const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
     const uint16_t* rcpT = s_tab;
@@ -883,7 +986,7 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
                 x0 = (float)i * off; x1 = (float)(i + 1) * off;
                 y0 = (float)j * off; y1 = (float)(j + 1) * off;
             }
-            const float ur = rng(pixel, sample, 0, seed), vr = rng(pixel, sample, 1, seed);
+            const float ur = rng(pixel, sample * 1024u, 0, seed), vr = rng(pixel, sample * 1024u, 1, seed);
             const float xo = (x1 - x0) * ur + x0, yo = (y1 - y0) * vr + y0;
             const float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
             const float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
@@ -896,8 +999,9 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
             if (sample == 0) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
             if (hit) {
                 eye_hits++;
-                Shader<POINT_ONLY, FAST, INST, kFused, REC> S{P, T, rcpT, rsqT, st, pixel, 3u, 0u, seed, 0, 0u};
+                Shader<POINT_ONLY, FAST, INST, kFused, REC> S{P, T, rcpT, rsqT, st, pixel, 0u, seed, 0, 0u};
                 S.sample = sample;
+                if constexpr (REC) { S.iorS = s_ior + tid; S.lvl = P.lvl + (blockIdx.x * kWG + tid); }
                 col = S.template shade<COUNT>(r, h);
                 shadow_total += S.shadow_rays;
                 secondary_total += S.secondary;
@@ -1085,7 +1189,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
                 const v3 Ls = add(mk(0, 0, 0), scale(scale(mul(E, ks), M.spec_amt), pw));
                 const v3 Ld = add(add(mk(0, 0, 0), mul(E, kd)), ka);
                 const v3 z = mk(0, 0, 0);
-                sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), z);
+                sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), mk(M.le[0], M.le[1], M.le[2]));
             }
             col = scale(add(mk(0, 0, 0), sh), 1.0f / (float)P.num_paths);
         }
@@ -1124,6 +1228,7 @@ __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DL
         bool hit = traverse<ANY, false, false, INST>(T, r, tmin[i], h, st);
         mrt_hit res;
         res.t = h.t; res.a = h.a; res.b = h.b; res.prim = hit ? (ANY ? 0 : h.prim) : -1;
+        res.inst = (hit && !ANY) ? h.inst : -1;
         if (ANY && hit) res.prim = 1;  // any-hit: occluded flag only
         out[i] = res;
     }
@@ -1174,6 +1279,8 @@ struct StreamCtx {
     uint8_t* occl = nullptr;                 // per ray: occluded
     uint8_t* nrays = nullptr;                // per output slot: rays written
     size_t ray_cap = 0, nrays_cap = 0;
+    float* lvl = nullptr;                    // REC kernels: chain level records (RenderParams::lvl)
+    size_t lvl_cap = 0;                      //   floats
     bool last_was_render = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
 };
@@ -1205,13 +1312,14 @@ struct DeviceState {
     bool boxes_finite = false;
     int cus = 0;
     bool point_only = false;
-    bool recursive = false;      // a material reflects or refracts (fused shading with shade_path)
+    int recursive = 0;           // chain shading (Shader REC): 1 reflection / refraction, 2 + path tracing
     int wall_khz = 0;            // wall_clock64() rate
     size_t bytes = 0;
     // per-stream launch scratch: frames on different streams are in flight at once
     std::mutex mu;
     std::vector<StreamCtx*> ctxs;
     StreamCtx* last = nullptr;   // context of the most recent launch (stats, wave log)
+    std::vector<hipStream_t> share_streams;  // mrt_render over several devices: one stream per bucket share
 };
 
 // Tuning knobs (mrt_set_tuning): A/B switches for performance work.
@@ -1231,7 +1339,7 @@ static int g_wavefront = 1;       // general shading: gen / trace / resolve kern
 static inline int fast_box(const DeviceState& d);
 
 static void free_ctx(StreamCtx* c) {
-    void* ptrs[] = {c->gstack, c->ctr, c->wave_log, c->hitbuf, c->rays, c->occl, c->nrays};
+    void* ptrs[] = {c->gstack, c->ctr, c->wave_log, c->hitbuf, c->rays, c->occl, c->nrays, c->lvl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1245,6 +1353,7 @@ static void free_device(DeviceState* d) {
     if (d->device >= 0) (void)hipSetDevice(d->device);
     (void)hipDeviceSynchronize();   // no launch may still use the scratch below
     for (StreamCtx* c : d->ctxs) free_ctx(c);
+    for (hipStream_t st : d->share_streams) (void)hipStreamDestroy(st);
     void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts, d->tables,
                     d->gamma, d->gammaF, d->d_rgb, d->d_rgb8};
     for (void* p : ptrs)
@@ -1281,16 +1390,34 @@ static int upload(T*& dst, const void* src, size_t bytes, size_t& total) {
     return MRT_OK;
 }
 
+static int upload_scene(Scene& s, DeviceState& d, int device);
+
+static void free_replicas(Scene& s) {
+    for (DeviceState* d : s.devs) free_device(d);
+    s.devs.clear();
+    s.dev = nullptr;
+}
+
+// The scene's replica on `device` (uploaded on first use; all replicas are
+// dropped when the host scene changed) becomes s.dev.
 static int ensure_device(Scene& s, int device) {
     if (!s.built) { set_error("scene not built"); return MRT_ERR_NOT_BUILT; }
-    if (s.dev && !s.dev_dirty && s.dev->device == device) return MRT_OK;
+    if (s.dev_dirty) { free_replicas(s); s.dev_dirty = false; }
+    for (DeviceState* d : s.devs)
+        if (d->device == device) { s.dev = d; return MRT_OK; }
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) { set_error("no HIP device"); return MRT_ERR_NO_DEVICE; }
     if (device < 0 || device >= n) { set_error("bad device ordinal"); return MRT_ERR_INVALID; }
     if (s.lights.size() > (size_t)kMaxLights) { set_error("too many lights"); return MRT_ERR_INVALID; }
-    free_device(s.dev);
-    s.dev = new DeviceState();
-    DeviceState& d = *s.dev;
+    DeviceState* d = new DeviceState();
+    const int rc = upload_scene(s, *d, device);
+    if (rc) { free_device(d); return rc; }
+    s.devs.push_back(d);
+    s.dev = d;
+    return MRT_OK;
+}
+
+static int upload_scene(Scene& s, DeviceState& d, int device) {
     d.device = device;
     HIP_OK(hipSetDevice(device));
     // shading arrays: concatenate meshes
@@ -1433,12 +1560,12 @@ static int ensure_device(Scene& s, int device) {
         for (int k = 0; k < 24; k++) d.boxes_finite &= std::isfinite(q.box[k]);
     d.point_only = true;
     for (const DevLight& l : s.lights) d.point_only &= (l.type == MRT_POINT_LIGHT);
-    d.recursive = false;
+    d.recursive = 0;
     for (const DevMaterial& m : s.materials)
-        d.recursive |= m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f || m.gloss < 1.f || m.translucency > 0.01f);
+        if (m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f || m.gloss < 1.f || m.translucency > 0.01f)) d.recursive = 1;
+    if (s.path_trace) d.recursive = 2;
     d.gthreads = (uint32_t)d.grid * kWG;
     s.info.device_bytes = total;
-    s.dev_dirty = false;
     return MRT_OK;
 }
 
@@ -1485,6 +1612,23 @@ static void fill_params(const Scene& s, RenderParams& P) {
     P.bg[0] = s.bg[0]; P.bg[1] = s.bg[1]; P.bg[2] = s.bg[2];
     P.n_lights = (int32_t)s.lights.size();
     P.num_paths = s.num_paths;
+    P.path_trace = s.path_trace ? 1 : 0;
+    P.max_bounces = s.max_bounces;
+    P.sample_env = s.sample_env ? 1 : 0;
+}
+
+// chain levels of the REC kernels: reflection / refraction bounces (< 5) plus
+// the GI bounces (giBounces < m_maxBounces - 1)
+static int chain_levels(const Scene& s) { return 6 + (s.path_trace ? s.max_bounces : 0); }
+static int level_words(const Scene& s) { return s.path_trace ? 9 + 3 * (int)s.lights.size() : 3; }
+
+static int ensure_levels(StreamCtx& c, size_t floats) {
+    if (floats <= c.lvl_cap) return MRT_OK;
+    if (c.lvl) { HIP_OK(hipStreamSynchronize(c.stream)); (void)hipFree(c.lvl); }
+    c.lvl = nullptr; c.lvl_cap = 0;
+    HIP_OK(hipMalloc((void**)&c.lvl, floats * sizeof(float)));
+    c.lvl_cap = floats;
+    return MRT_OK;
 }
 
 static inline int fast_box(const DeviceState& d) { return (g_fast_box && d.boxes_finite) ? 1 : 0; }
@@ -1582,38 +1726,30 @@ static int max_shadow_rays(const Scene& s) {
     return s.num_paths * per_path;
 }
 
-static KernelFn pick_shade(bool c, bool po, bool f, bool inst, bool rec) {
-    if (rec) {   // secondary rays, fused shadow rays (instanced: general light loop)
-        if (inst) return c ? (f ? shade_kernel<true, false, true, true, kFused, true> : shade_kernel<true, false, false, true, kFused, true>)
-                           : (f ? shade_kernel<false, false, true, true, kFused, true> : shade_kernel<false, false, false, true, kFused, true>);
-        if (po) return c ? (f ? shade_kernel<true, true, true, false, kFused, true> : shade_kernel<true, true, false, false, kFused, true>)
-                         : (f ? shade_kernel<false, true, true, false, kFused, true> : shade_kernel<false, true, false, false, kFused, true>);
-        return c ? (f ? shade_kernel<true, false, true, false, kFused, true> : shade_kernel<true, false, false, false, kFused, true>)
-                 : (f ? shade_kernel<false, false, true, false, kFused, true> : shade_kernel<false, false, false, false, kFused, true>);
-    }
-    if (inst) return c ? (f ? shade_kernel<true, false, true, true> : shade_kernel<true, false, false, true>)
-                       : (f ? shade_kernel<false, false, true, true> : shade_kernel<false, false, false, true>);
-    if (po) return c ? (f ? shade_kernel<true, true, true> : shade_kernel<true, true, false>)
-                     : (f ? shade_kernel<false, true, true> : shade_kernel<false, true, false>);
-    return c ? (f ? shade_kernel<true, false, true> : shade_kernel<true, false, false>)
-             : (f ? shade_kernel<false, false, true> : shade_kernel<false, false, false>);
+template <template <bool, bool, bool, bool, int> class K, int REC>
+static KernelFn pick4(bool c, bool po, bool f, bool inst) {
+    if (inst) return c ? (f ? K<true, false, true, true, REC>::fn : K<true, false, false, true, REC>::fn)
+                       : (f ? K<false, false, true, true, REC>::fn : K<false, false, false, true, REC>::fn);
+    if (po) return c ? (f ? K<true, true, true, false, REC>::fn : K<true, true, false, false, REC>::fn)
+                     : (f ? K<false, true, true, false, REC>::fn : K<false, true, false, false, REC>::fn);
+    return c ? (f ? K<true, false, true, false, REC>::fn : K<true, false, false, false, REC>::fn)
+             : (f ? K<false, false, true, false, REC>::fn : K<false, false, false, false, REC>::fn);
 }
+template <bool C, bool PO, bool F, bool I, int REC>
+struct ShadeK { static constexpr KernelFn fn = shade_kernel<C, PO, F, I, kFused, REC>; };
+template <bool C, bool PO, bool F, bool I, int REC>
+struct AdaptK { static constexpr KernelFn fn = adaptive_kernel<C, PO, F, I, REC>; };
 
-static KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, bool rec) {
-    if (rec) {   // secondary rays (instanced: general light loop)
-        if (inst) return c ? (f ? adaptive_kernel<true, false, true, true, true> : adaptive_kernel<true, false, false, true, true>)
-                           : (f ? adaptive_kernel<false, false, true, true, true> : adaptive_kernel<false, false, false, true, true>);
-        if (po) return c ? (f ? adaptive_kernel<true, true, true, false, true> : adaptive_kernel<true, true, false, false, true>)
-                         : (f ? adaptive_kernel<false, true, true, false, true> : adaptive_kernel<false, true, false, false, true>);
-        return c ? (f ? adaptive_kernel<true, false, true, false, true> : adaptive_kernel<true, false, false, false, true>)
-                 : (f ? adaptive_kernel<false, false, true, false, true> : adaptive_kernel<false, false, false, false, true>);
-    }
-    if (inst) return c ? (f ? adaptive_kernel<true, false, true, true> : adaptive_kernel<true, false, false, true>)
-                       : (f ? adaptive_kernel<false, false, true, true> : adaptive_kernel<false, false, false, true>);
-    if (po) return c ? (f ? adaptive_kernel<true, true, true, false> : adaptive_kernel<true, true, false, false>)
-                     : (f ? adaptive_kernel<false, true, true, false> : adaptive_kernel<false, true, false, false>);
-    return c ? (f ? adaptive_kernel<true, false, true, false> : adaptive_kernel<true, false, false, false>)
-             : (f ? adaptive_kernel<false, false, true, false> : adaptive_kernel<false, false, false, false>);
+// rec: Shader REC (0 direct, 1 reflection / refraction chains, 2 + path tracing)
+static KernelFn pick_shade(bool c, bool po, bool f, bool inst, int rec) {
+    if (rec == 2) return pick4<ShadeK, 2>(c, po, f, inst);
+    if (rec == 1) return pick4<ShadeK, 1>(c, po, f, inst);
+    return pick4<ShadeK, 0>(c, po, f, inst);
+}
+static KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec) {
+    if (rec == 2) return pick4<AdaptK, 2>(c, po, f, inst);
+    if (rec == 1) return pick4<AdaptK, 1>(c, po, f, inst);
+    return pick4<AdaptK, 0>(c, po, f, inst);
 }
 
 // Two launches on `stream`: primary rays -> hit records, then shading with
@@ -1625,7 +1761,13 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     int rc = get_ctx(d, stream, cp);
     if (rc) return rc;
     StreamCtx& c = *cp;
+    s.stats_final = false;
     if ((rc = ensure_slots(c, slots))) return rc;
+    if (d.recursive) {
+        P.lvl_words = level_words(s);
+        if ((rc = ensure_levels(c, (size_t)d.gthreads * chain_levels(s) * P.lvl_words))) return rc;
+        P.lvl = c.lvl;
+    }
     P.hits = c.hitbuf;
     P.gstack = c.gstack;
     P.ctr = c.ctr;
@@ -1720,7 +1862,7 @@ int mrt_device_count(void) {
 mrt_scene* mrt_scene_create(void) { return new (std::nothrow) mrt_scene(); }
 void mrt_scene_destroy(mrt_scene* s) {
     if (!s) return;
-    free_device(s->impl.dev);
+    free_replicas(s->impl);
     delete s;
 }
 
@@ -1733,6 +1875,11 @@ int mrt_scene_add_material(mrt_scene* s, const mrt_material* m) {
     d.spec_exp = m->spec_exp; d.spec_amt = m->spec_amt;
     d.reflect = 0.f; d.refract = 0.f; d.ior = 1.5f; d.gloss = 1.f;   // Blinn defaults (src/Blinn.h:11-22)
     d.translucency = 0.f;
+    memcpy(d.le, m->le, 12);
+    d.emitted = m->emitted;
+    d.sample_env = 1;                                                 // Material::Material, src/Material.cpp:6
+    d.emitter = (d.emitted > 0.0f || (d.le[0] + d.le[1]) + d.le[2] > 0.0f) ? 1 : 0;   // src/Blinn.cpp:47
+    if (m->type != MRT_BLINN) { d.le[0] = d.le[1] = d.le[2] = 0.f; d.emitted = 0.f; d.emitter = 0; }
     s->impl.materials.push_back(d);
     s->impl.dev_dirty = true;
     return (int)s->impl.materials.size() - 1;
@@ -1918,10 +2065,21 @@ int mrt_scene_add_obj(mrt_scene* s, const char* path, const float* ctm16, int ma
 
 int mrt_scene_add_mesh(mrt_scene* s, const mrt_mesh* mesh, int material) {
     if (!s || !mesh || mesh->nv < 0 || mesh->nn < 0 || mesh->nt < 0) { set_error("bad mesh"); return MRT_ERR_INVALID; }
+    const int vs = mesh->vert_stride ? mesh->vert_stride : 3, ns = mesh->normal_stride ? mesh->normal_stride : 3;
+    if (vs < 3 || ns < 3 || (mesh->nv && !mesh->verts) || (mesh->nn && !mesh->normals) ||
+        (mesh->nt && (!mesh->vidx || !mesh->nidx))) {
+        set_error("bad mesh: null array or stride < 3"); return MRT_ERR_INVALID;
+    }
     Mesh m;
     m.material = material;
-    for (int i = 0; i < mesh->nv; i++) m.verts.push_back(mk(mesh->verts[3 * i], mesh->verts[3 * i + 1], mesh->verts[3 * i + 2]));
-    for (int i = 0; i < mesh->nn; i++) m.normals.push_back(mk(mesh->normals[3 * i], mesh->normals[3 * i + 1], mesh->normals[3 * i + 2]));
+    for (int i = 0; i < mesh->nv; i++) {
+        const float* v = mesh->verts + (size_t)vs * i;
+        m.verts.push_back(mk(v[0], v[1], v[2]));
+    }
+    for (int i = 0; i < mesh->nn; i++) {
+        const float* v = mesh->normals + (size_t)ns * i;
+        m.normals.push_back(mk(v[0], v[1], v[2]));
+    }
     m.vidx.assign(mesh->vidx, mesh->vidx + 3 * (size_t)mesh->nt);
     m.nidx.assign(mesh->nidx, mesh->nidx + 3 * (size_t)mesh->nt);
     for (size_t i = 0; i < m.vidx.size(); i++)
@@ -1955,8 +2113,59 @@ int mrt_scene_set_background(mrt_scene* s, const float rgb[3]) {
 }
 
 int mrt_scene_set_num_paths(mrt_scene* s, int num_paths) {
-    if (!s || num_paths < 1) { set_error("bad num_paths"); return MRT_ERR_INVALID; }
+    if (!s || num_paths < 1 || num_paths > 1024) { set_error("bad num_paths (1..1024)"); return MRT_ERR_INVALID; }
     s->impl.num_paths = num_paths;
+    return MRT_OK;
+}
+
+int mrt_scene_set_material_emission(mrt_scene* s, int material, float emitted, const float le[3]) {
+    if (!s || !le || material < 0 || material >= (int)s->impl.materials.size()) {
+        set_error("bad material / emission"); return MRT_ERR_INVALID;
+    }
+    DevMaterial& m = s->impl.materials[(size_t)material];
+    if (m.type != MRT_BLINN) { set_error("only Blinn materials emit (src/Blinn.h:44-45)"); return MRT_ERR_INVALID; }
+    memcpy(m.le, le, 12);
+    m.emitted = emitted;
+    m.emitter = (m.emitted > 0.0f || (m.le[0] + m.le[1]) + m.le[2] > 0.0f) ? 1 : 0;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
+int mrt_scene_set_material_sample_env(mrt_scene* s, int material, int sample_env) {
+    if (!s || material < 0 || material >= (int)s->impl.materials.size()) { set_error("bad material"); return MRT_ERR_INVALID; }
+    s->impl.materials[(size_t)material].sample_env = sample_env ? 1 : 0;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
+int mrt_scene_set_path_trace(mrt_scene* s, int enable, int max_bounces, int sample_env) {
+    if (!s || max_bounces < 1 || max_bounces > 64) { set_error("bad path trace settings (1 <= max_bounces <= 64)"); return MRT_ERR_INVALID; }
+    s->impl.path_trace = enable != 0;
+    s->impl.max_bounces = max_bounces;
+    s->impl.sample_env = sample_env != 0;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
+int mrt_scene_prim_object(const mrt_scene* s, int32_t prim, int32_t* mesh, int32_t* tri, int32_t* inst) {
+    if (!s || !mesh || !tri || !inst) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    const Scene& S = s->impl;
+    if (!S.built) { set_error("scene not built"); return MRT_ERR_NOT_BUILT; }
+    if (prim < 0) { set_error("prim id out of range"); return MRT_ERR_INVALID; }
+    if ((size_t)prim < S.obj_mesh.size()) {   // a world object (a ProxyObject's own slot never hits)
+        *mesh = S.obj_mesh[prim]; *tri = S.obj_tri[prim]; *inst = S.obj_inst[prim];
+        return MRT_OK;
+    }
+    int lo = 0, hi = (int)S.instances.size() - 1;   // the last instance with hit_base <= prim
+    if (hi < 0) { set_error("prim id out of range"); return MRT_ERR_INVALID; }
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (S.instances[mid].hit_base <= prim) lo = mid; else hi = mid - 1;
+    }
+    const Blas& B = S.blas[S.instances[lo].blas];
+    const int64_t k = (int64_t)prim - S.instances[lo].hit_base;
+    if (k < 0 || k >= (int64_t)B.obj_mesh.size()) { set_error("prim id out of range"); return MRT_ERR_INVALID; }
+    *mesh = B.obj_mesh[k]; *tri = B.obj_tri[k]; *inst = lo;
     return MRT_OK;
 }
 
@@ -2155,8 +2364,145 @@ int mrt_unpack_buckets_async(const int32_t* d_buckets, int32_t n_buckets, const 
                                   s_for_lut, stream);
 }
 
+// HitInfo of a device hit record (t, a, b, prim bits): m_proxy from the id
+static mrt_hit to_hit(const Scene& S, const float4& v) {
+    mrt_hit h;
+    h.t = v.x; h.a = v.y; h.b = v.z;
+    h.prim = __builtin_bit_cast(int32_t, v.w);
+    h.inst = -1;
+    if (h.prim >= (int32_t)S.obj_mesh.size() && !S.instances.empty()) {
+        int lo = 0, hi = (int)S.instances.size() - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (S.instances[mid].hit_base <= h.prim) lo = mid; else hi = mid - 1;
+        }
+        h.inst = lo;
+    }
+    return h;
+}
+
+// mrt_render over several devices: bucket b of the frame's 32x32 grid
+// (src/Scene.cpp:90-95) -> share b mod n, share k rendered on devices[k] from
+// that device's scene replica (own stream), tiles copied back and scattered into
+// the caller's frame.  Each pixel is a pure function of (scene, camera, pixel,
+// seed), so the frame is bit-identical to a one-device render.
+static int render_shared(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts, float* rgb, uint8_t* rgb8,
+                         mrt_hit* hits) {
+    Scene& S = s->impl;
+    const int n = opts->n_devices, W = opts->width, H = opts->height;
+    const int bx = (W + 31) / 32, bpf = bx * ((H + 31) / 32);
+    struct Share {
+        int device = -1;
+        DeviceState* d = nullptr;
+        hipStream_t stream = nullptr;
+        std::vector<int32_t> items;
+        int32_t* d_items = nullptr;
+        float* d_tiles = nullptr;
+        std::vector<float> tiles;
+        std::vector<float4> hitrec;
+    };
+    std::vector<Share> sh((size_t)n);
+    std::vector<int> used(n, 0);   // share index within its device (stream per share)
+    int rc = MRT_OK;
+    for (int k = 0; k < n && rc == MRT_OK; k++) {
+        Share& q = sh[k];
+        q.device = opts->devices[k];
+        for (int b = k; b < bpf; b += n) q.items.push_back(b);
+        if ((rc = ensure_device(S, q.device))) break;
+        q.d = S.dev;
+        int slot = 0;
+        for (int j = 0; j < k; j++) slot += sh[j].device == q.device;
+        if (hipSetDevice(q.device) != hipSuccess) { set_error("hipSetDevice"); rc = MRT_ERR_HIP; break; }
+        while ((int)q.d->share_streams.size() <= slot) {
+            hipStream_t st;
+            if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { set_error("stream"); rc = MRT_ERR_HIP; break; }
+            q.d->share_streams.push_back(st);
+        }
+        if (rc) break;
+        q.stream = q.d->share_streams[slot];
+        if (q.items.empty()) continue;
+        const size_t ni = q.items.size();
+        if (hipMalloc((void**)&q.d_items, ni * sizeof(int32_t)) != hipSuccess ||
+            hipMalloc((void**)&q.d_tiles, ni * 1024 * 3 * sizeof(float)) != hipSuccess) {
+            set_error("out of device memory (bucket shares)"); rc = MRT_ERR_HIP; break;
+        }
+        if (hipMemcpyAsync(q.d_items, q.items.data(), ni * sizeof(int32_t), hipMemcpyHostToDevice, q.stream) != hipSuccess) {
+            set_error("hipMemcpyAsync"); rc = MRT_ERR_HIP; break;
+        }
+        mrt_render_opts o = *opts;
+        o.device = q.device; o.devices = nullptr; o.n_devices = 0;
+        rc = mrt_render_batch_async(s, cam, 1, &o, q.d_items, (int32_t)ni, q.d_tiles, nullptr, q.stream);
+    }
+    mrt_stats total{};
+    for (int k = 0; k < n && rc == MRT_OK; k++) {
+        Share& q = sh[k];
+        if (q.items.empty()) continue;
+        const size_t ni = q.items.size();
+        if (hipSetDevice(q.device) != hipSuccess) { set_error("hipSetDevice"); rc = MRT_ERR_HIP; break; }
+        q.tiles.resize(ni * 1024 * 3);
+        if (hipMemcpyAsync(q.tiles.data(), q.d_tiles, q.tiles.size() * sizeof(float), hipMemcpyDeviceToHost, q.stream) != hipSuccess) {
+            set_error("hipMemcpyAsync"); rc = MRT_ERR_HIP; break;
+        }
+        StreamCtx* c = nullptr;
+        if ((rc = get_ctx(*q.d, q.stream, c))) break;
+        if (hits) {
+            q.hitrec.resize(ni * 1024);
+            if (hipMemcpyAsync(q.hitrec.data(), c->hitbuf, ni * 1024 * sizeof(float4), hipMemcpyDeviceToHost, q.stream) != hipSuccess) {
+                set_error("hipMemcpyAsync"); rc = MRT_ERR_HIP; break;
+            }
+        }
+        if (hipStreamSynchronize(q.stream) != hipSuccess) { set_error("hipStreamSynchronize"); rc = MRT_ERR_HIP; break; }
+        // this share's counters (the share's own stream context)
+        q.d->last = c;
+        S.dev = q.d;
+        mrt_stats st{};
+        const int src = mrt_scene_last_stats(s, &st);
+        if (src && src != MRT_ERR_OVERFLOW) { rc = src; break; }
+        total.shadow_rays += st.shadow_rays; total.secondary_rays += st.secondary_rays;
+        total.node_visits += st.node_visits; total.leaf_visits += st.leaf_visits;
+        total.primary_node_visits += st.primary_node_visits; total.primary_leaf_visits += st.primary_leaf_visits;
+        total.primary_hits += st.primary_hits; total.primary_wave_steps += st.primary_wave_steps;
+        total.primary_uniform_visits += st.primary_uniform_visits;
+        total.kernel_ms = std::max(total.kernel_ms, st.kernel_ms);
+        total.max_stack = std::max(total.max_stack, st.max_stack);
+        if (src == MRT_ERR_OVERFLOW) rc = src;
+        // scatter the share's buckets into the frame (row 0 = bottom)
+        const uint8_t* lut = host_gamma_lut();
+        for (size_t i = 0; i < ni; i++) {
+            const int b = q.items[i], x0 = (b % bx) * 32, y0 = (b / bx) * 32;
+            for (int ly = 0; ly < 32 && y0 + ly < H; ly++)
+                for (int lx = 0; lx < 32 && x0 + lx < W; lx++) {
+                    const size_t px = (size_t)(y0 + ly) * W + x0 + lx, t = i * 1024 + ly * 32 + lx;
+                    for (int ch = 0; ch < 3; ch++) {
+                        rgb[3 * px + ch] = q.tiles[3 * t + ch];
+                        if (rgb8) rgb8[3 * px + ch] = lut[map_index(q.tiles[3 * t + ch])];
+                    }
+                    if (hits) hits[px] = to_hit(S, q.hitrec[t]);
+                }
+        }
+    }
+    for (Share& q : sh) {
+        if (q.device >= 0) (void)hipSetDevice(q.device);
+        if (q.stream) (void)hipStreamSynchronize(q.stream);
+        if (q.d_items) (void)hipFree(q.d_items);
+        if (q.d_tiles) (void)hipFree(q.d_tiles);
+    }
+    if (rc && rc != MRT_ERR_OVERFLOW) return rc;
+    total.primary_rays = (uint64_t)W * H;
+    S.last = total;
+    S.stats_final = true;
+    S.last_rc = rc;
+    if (rc) set_error("traversal stack overflow");
+    return rc;
+}
+
 int mrt_render(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts, float* rgb, uint8_t* rgb8, mrt_hit* hits) {
     if (!s || !cam || !opts || !rgb || opts->width <= 0 || opts->height <= 0) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    if (opts->n_devices < 0 || (opts->n_devices > 0 && !opts->devices)) { set_error("bad device list"); return MRT_ERR_INVALID; }
+    if (opts->n_devices > 1 || (opts->n_devices == 1 && opts->devices[0] != opts->device)) {
+        if (opts->n_devices > 64) { set_error("at most 64 bucket shares"); return MRT_ERR_INVALID; }
+        return render_shared(s, cam, opts, rgb, rgb8, hits);
+    }
     Scene& S = s->impl;
     int rc = ensure_device(S, opts->device);
     if (rc) return rc;
@@ -2183,7 +2529,11 @@ int mrt_render(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
     if ((rc = launch_render(S, P, px, opts->count_visits != 0, nullptr))) return rc;
     HIP_OK(hipMemcpy(rgb, d.d_rgb, px * 12, hipMemcpyDeviceToHost));
     if (rgb8) HIP_OK(hipMemcpy(rgb8, d.d_rgb8, px * 3, hipMemcpyDeviceToHost));
-    if (hits) HIP_OK(hipMemcpy(hits, d.last->hitbuf, px * sizeof(mrt_hit), hipMemcpyDeviceToHost));
+    if (hits) {
+        std::vector<float4> rec(px);
+        HIP_OK(hipMemcpy(rec.data(), d.last->hitbuf, px * sizeof(float4), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < px; i++) hits[i] = to_hit(S, rec[i]);
+    }
     S.last.primary_rays = px;
     mrt_stats tmp;
     if ((rc = mrt_scene_last_stats(s, &tmp))) return rc;
@@ -2194,6 +2544,11 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     if (!cs || !out) { set_error("bad argument"); return MRT_ERR_INVALID; }
     mrt_scene* s = const_cast<mrt_scene*>(cs);
     Scene& S = s->impl;
+    if (S.stats_final) {   // multi-device mrt_render: the shares' counters, summed
+        *out = S.last;
+        if (S.last_rc) set_error("traversal stack overflow");
+        return S.last_rc;
+    }
     if (!S.dev) { set_error("nothing rendered"); return MRT_ERR_INVALID; }
     DeviceState& d = *S.dev;
     if (!d.last) { set_error("nothing rendered"); return MRT_ERR_INVALID; }
@@ -2251,6 +2606,7 @@ int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const floa
     StreamCtx* cp = nullptr;
     if ((rc = get_ctx(d, (hipStream_t)stream, cp))) return rc;
     StreamCtx& c = *cp;
+    S.stats_final = false;
     HIP_OK(hipMemsetAsync(c.ctr, 0, CTR_N * sizeof(unsigned long long), (hipStream_t)stream));
     c.last_was_render = false;
     int grid = (int)std::min<size_t>((size_t)d.grid, (n + kWG - 1) / kWG);

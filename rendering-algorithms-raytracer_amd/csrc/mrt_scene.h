@@ -64,6 +64,10 @@ struct Scene {
     float env_exposure = 1.f;       // Scene::m_envExposure
     float bg[3] = {0.f, 0.f, 0.f};
     int num_paths = 1;
+    // Scene::m_pathTrace / m_maxBounces / m_sampleLightFromEnv (src/Scene.cpp:17-19)
+    bool path_trace = false;
+    int max_bounces = 10;
+    bool sample_env = false;
     // Scene::m_minSubdivs / m_maxSubdivs / m_noiseThreshold (src/Scene.cpp:20-22)
     int min_subdivs = 1, max_subdivs = 1;
     float noise_threshold = 0.01f;
@@ -90,9 +94,17 @@ struct Scene {
     mrt_bvh_info info{};
     bool built = false;
 
+    // device replicas (one per HIP device used, mrt_render_opts.devices); `dev` is
+    // the one the last call used.  dev_dirty: the host scene changed, every
+    // replica is re-uploaded on its next use.
+    std::vector<DeviceState*> devs;
     DeviceState* dev = nullptr;
     bool dev_dirty = true;
     mrt_stats last{};
+    // the last call was a multi-device mrt_render: `last` already holds the summed
+    // counters of its shares (last_rc: MRT_ERR_OVERFLOW if a share overflowed)
+    bool stats_final = false;
+    int last_rc = 0;
 };
 
 // host_build.cpp

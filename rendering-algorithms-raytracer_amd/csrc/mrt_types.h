@@ -61,6 +61,10 @@ struct DevMaterial {
     float ior;               // Blinn m_ior (src/Blinn.cpp:25-27)
     float gloss;             // Blinn m_specGloss (src/Blinn.h:42,65): < 1 jitters the reflection vector
     float translucency;      // Material::m_translucency (src/Material.h:30,44): > 0.01 lights the back side
+    float le[3];             // Blinn m_Le (src/Blinn.h:64): added to every shade() result (src/Blinn.cpp:335)
+    float emitted;           // Blinn m_lightEmitted (src/Blinn.h:63): path-tracing emitter intensity
+    int32_t sample_env;      // Material::m_sampleEnv (src/Material.h:43; default true)
+    int32_t emitter;         // host-derived: emitted > 0 || le.x + le.y + le.z > 0 (src/Blinn.cpp:47)
 };
 
 struct DevLight {

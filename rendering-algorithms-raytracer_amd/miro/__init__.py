@@ -127,15 +127,20 @@ class Lambert:
     def setKd(self, kd): self.kd = Vector3(kd)
     def setKa(self, ka): self.ka = Vector3(ka)
 
+    def setSampleEnv(self, b): self.sampleEnv = bool(b)          # Material::setSampleEnv (src/Material.h:27)
+
+    sampleEnv = True
+
     def _c(self):
-        return _lib.mrt_material(0, f3(self.kd), f3(self.ka), f3((1, 1, 1)), 1.0, 0.0)
+        return _lib.mrt_material(0, f3(self.kd), f3(self.ka), f3((1, 1, 1)), 1.0, 0.0, f3((0, 0, 0)), 0.0)
 
 
 class Blinn:
     """Blinn(kd, ka, ks, kt, ior, specExp, specAmt, reflectAmt, refractAmt) defaults of
     src/Blinn.h:11-22: direct lighting plus Fresnel-weighted reflection / refraction
-    rays (src/Blinn.cpp:91-335), glossy reflection vectors, translucency.  Path tracing, dispersion
-    and texture maps are not on the MI355X path."""
+    rays (src/Blinn.cpp:91-335), glossy reflection vectors, translucency, emission
+    (setLightEmittedIntensity / setLightEmittedColor) and path tracing (Scene.setPathTrace).
+    Dispersion and texture maps are not on the MI355X path."""
 
     def __init__(self, kd=Vector3(1), ka=Vector3(0), ks=Vector3(1), kt=Vector3(0), ior=1.5,
                  specExp=1.0, specAmt=0.0, reflectAmt=0.0, refractAmt=0.0, specGloss=1.0):
@@ -144,6 +149,13 @@ class Blinn:
         self.reflectAmt, self.refractAmt = float(reflectAmt), float(refractAmt)
         self.specGloss = float(specGloss)
         self.translucency = 0.0
+        self.lightEmitted = 0.0          # the Blinn ctor forces 0 (src/Blinn.cpp:28-29)
+        self.Le = Vector3(0)
+        self.sampleEnv = True            # Material::m_sampleEnv (src/Material.cpp:6)
+
+    def setLightEmittedIntensity(self, le): self.lightEmitted = float(le)   # src/Blinn.h:44
+    def setLightEmittedColor(self, c): self.Le = Vector3(c)                 # src/Blinn.h:45
+    def setSampleEnv(self, b): self.sampleEnv = bool(b)                     # src/Material.h:27
 
     def setTranslucency(self, t): self.translucency = float(t)   # src/Material.h:30
 
@@ -161,7 +173,8 @@ class Blinn:
     def setSpecAmt(self, a): self.specAmt = float(a)
 
     def _c(self):
-        return _lib.mrt_material(1, f3(self.kd), f3(self.ka), f3(self.ks), self.specExp, self.specAmt)
+        return _lib.mrt_material(1, f3(self.kd), f3(self.ka), f3(self.ks), self.specExp, self.specAmt, f3(self.Le),
+                                 self.lightEmitted)
 
 
 class _Light:
@@ -306,7 +319,7 @@ class HitInfo:
         self.t, self.a, self.b, self.obj = float(t), float(a), float(b), int(obj)
 
 
-HIT_DTYPE = np.dtype([("t", "<f4"), ("a", "<f4"), ("b", "<f4"), ("prim", "<i4")])
+HIT_DTYPE = np.dtype([("t", "<f4"), ("a", "<f4"), ("b", "<f4"), ("prim", "<i4"), ("inst", "<i4")])
 
 
 def makeMeshObjs(scene: "Scene", mesh: TriangleMesh, material):
@@ -356,6 +369,9 @@ class Scene:
         self._lights: List[_Light] = []
         self.bg = Vector3(0)
         self.m_numPaths = 1
+        self.m_pathTrace = False         # src/Scene.cpp:17-19
+        self.m_maxBounces = 10
+        self.m_sampleLightFromEnv = False   # never initialised by the reference's Scene ctor
         self.m_minSubdivs = 1            # src/Scene.cpp:20-22
         self.m_maxSubdivs = 1
         self.m_noiseThreshold = 0.01
@@ -371,6 +387,10 @@ class Scene:
     def addLight(self, light): self._lights.append(light)
     def setBGColor(self, c): self.bg = Vector3(c)
     def setNumPaths(self, p): self.m_numPaths = int(p)
+    def setPathTrace(self, pt): self.m_pathTrace = bool(pt)        # src/Scene.h:40
+    def setMaxBounces(self, mb): self.m_maxBounces = int(mb)       # src/Scene.h:48
+    def maxBounces(self): return self.m_maxBounces
+    def setSampleEnv(self, b): self.m_sampleLightFromEnv = bool(b)  # src/Scene.h:57
     # adaptive supersampling, Scene::adaptiveSampleScene (src/Scene.h:42-55, src/Scene.cpp:252-293)
     def setMinSubdivs(self, r): self.m_minSubdivs = int(r)
     def minSubdivs(self): return self.m_minSubdivs
@@ -413,6 +433,7 @@ class Scene:
                     check(L.mrt_scene_set_material_gloss(self._h, mats[id(mat)], mat.specGloss), "material gloss")
                     check(L.mrt_scene_set_material_translucency(self._h, mats[id(mat)], mat.translucency),
                           "material translucency")
+                check(L.mrt_scene_set_material_sample_env(self._h, mats[id(mat)], int(mat.sampleEnv)), "sampleEnv")
             mid = mats[id(mat)]
             if mesh.path is not None:
                 ctm = mesh.ctm.ctypes.data_as(C.POINTER(C.c_float)) if mesh.ctm is not None else None
@@ -420,7 +441,7 @@ class Scene:
             v, n, vi, ni = mesh.verts, mesh.normals, mesh.vidx, mesh.nidx
             mm = _lib.mrt_mesh(v.ctypes.data_as(C.POINTER(C.c_float)), n.ctypes.data_as(C.POINTER(C.c_float)),
                                vi.ctypes.data_as(C.POINTER(C.c_uint32)), ni.ctypes.data_as(C.POINTER(C.c_uint32)),
-                               len(v), len(n), len(vi))
+                               len(v), len(n), len(vi), v.shape[1] if v.ndim == 2 else 3, n.shape[1] if n.ndim == 2 else 3)
             return check(L.mrt_scene_add_mesh(self._h, C.byref(mm), mid), "add_mesh")
 
         blas = {}   # BVH object -> BLAS id (built once, shared by its instances)
@@ -459,6 +480,8 @@ class Scene:
             check(L.mrt_scene_set_env_map(self._h, tex_id(self.m_envMap), self.m_envExposure), "env map")
         check(L.mrt_scene_set_background(self._h, f3(self.bg)), "bg")
         check(L.mrt_scene_set_num_paths(self._h, self.m_numPaths), "num_paths")
+        check(L.mrt_scene_set_path_trace(self._h, int(self.m_pathTrace), self.m_maxBounces,
+                                         int(self.m_sampleLightFromEnv)), "path trace")
         check(L.mrt_scene_set_subdivs(self._h, self.m_minSubdivs, self.m_maxSubdivs, self.m_noiseThreshold), "subdivs")
         t0 = time.perf_counter()
         check(L.mrt_scene_build_bvh(self._h), "BVH build")
@@ -521,9 +544,14 @@ class Scene:
         return nb, nc, lt, lp
 
     # -- rendering (src/Scene.cpp:85-217)
-    def raytraceImage(self, cam: Camera, img: Image, count_visits=False, want_hits=False, seed=0):
+    def raytraceImage(self, cam: Camera, img: Image, count_visits=False, want_hits=False, seed=0, devices=None):
+        """devices: HIP device ordinals to deal the 32x32 buckets over (bucket b ->
+        devices[b % n], mrt_render_opts.devices; one device may repeat)."""
         W, H = img.width(), img.height()
         opts = _lib.mrt_render_opts(W, H, self.device, int(count_visits), 1, int(want_hits), seed)
+        if devices:
+            dev_arr = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+            opts.devices, opts.n_devices = dev_arr, len(devices)
         hits = np.zeros((H, W), HIT_DTYPE) if want_hits else None
         c = cam._c()
         check(lib().mrt_render(self.handle, C.byref(c), C.byref(opts), img.rgb.ctypes.data_as(C.POINTER(C.c_float)),
@@ -560,6 +588,12 @@ class Scene:
         check(lib().mrt_trace(self.handle, o.ctypes.data_as(fp), d.ctypes.data_as(fp), tmin.ctypes.data_as(fp),
                               tmax.ctypes.data_as(fp), n, int(any_hit), out.ctypes.data), "trace")
         return out
+
+    def primObject(self, prim: int):
+        """HitInfo::obj / m_proxy of a hit id: (mesh id, triangle index, instance or -1)."""
+        m, t, i = C.c_int32(), C.c_int32(), C.c_int32()
+        check(lib().mrt_scene_prim_object(self.handle, int(prim), C.byref(m), C.byref(t), C.byref(i)), "prim_object")
+        return m.value, t.value, i.value
 
     def trace(self, hitInfo: HitInfo, ray: Ray, tMin=0.001) -> bool:
         """Scene::trace(threadID, HitInfo&, const Ray&, tMin): hitInfo.t is tMax in, t out."""

@@ -23,13 +23,14 @@ EXPORTS = [
     "mrt_rsqrt_nr", "mrt_set_tuning", "mrt_render_batch_async", "mrt_unpack_batch_async",
     "mrt_debug_wave_log", "mrt_device_wall_clock_khz", "mrt_hdr_info", "mrt_hdr_load", "mrt_scene_add_texture",
     "mrt_scene_set_env_map", "mrt_scene_dome_info", "mrt_scene_dome_export", "mrt_scene_make_blas",
-    "mrt_scene_add_instance", "mrt_scene_blas_info", "mrt_scene_blas_export",
+    "mrt_scene_add_instance", "mrt_scene_blas_info", "mrt_scene_blas_export", "mrt_scene_set_material_emission",
+    "mrt_scene_set_material_sample_env", "mrt_scene_set_path_trace", "mrt_scene_prim_object",
 ]
 
 
 class mrt_material(C.Structure):
     _fields_ = [("type", C.c_int32), ("kd", C.c_float * 3), ("ka", C.c_float * 3), ("ks", C.c_float * 3),
-                ("spec_exp", C.c_float), ("spec_amt", C.c_float)]
+                ("spec_exp", C.c_float), ("spec_amt", C.c_float), ("le", C.c_float * 3), ("emitted", C.c_float)]
 
 
 class mrt_light(C.Structure):
@@ -45,11 +46,12 @@ class mrt_camera(C.Structure):
 class mrt_mesh(C.Structure):
     _fields_ = [("verts", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
                 ("vidx", C.POINTER(C.c_uint32)), ("nidx", C.POINTER(C.c_uint32)),
-                ("nv", C.c_int32), ("nn", C.c_int32), ("nt", C.c_int32)]
+                ("nv", C.c_int32), ("nn", C.c_int32), ("nt", C.c_int32),
+                ("vert_stride", C.c_int32), ("normal_stride", C.c_int32)]
 
 
 class mrt_hit(C.Structure):
-    _fields_ = [("t", C.c_float), ("a", C.c_float), ("b", C.c_float), ("prim", C.c_int32)]
+    _fields_ = [("t", C.c_float), ("a", C.c_float), ("b", C.c_float), ("prim", C.c_int32), ("inst", C.c_int32)]
 
 
 class mrt_bvh_info(C.Structure):
@@ -60,7 +62,8 @@ class mrt_bvh_info(C.Structure):
 
 class mrt_render_opts(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("device", C.c_int32), ("count_visits", C.c_int32),
-                ("want_rgb8", C.c_int32), ("want_hits", C.c_int32), ("seed", C.c_uint32)]
+                ("want_rgb8", C.c_int32), ("want_hits", C.c_int32), ("seed", C.c_uint32),
+                ("devices", C.POINTER(C.c_int32)), ("n_devices", C.c_int32)]
 
 
 class mrt_stats(C.Structure):
@@ -116,6 +119,10 @@ def load():
     L.mrt_scene_set_material_optics.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float]
     L.mrt_scene_set_material_gloss.argtypes = [C.c_void_p, C.c_int, C.c_float]
     L.mrt_scene_set_material_translucency.argtypes = [C.c_void_p, C.c_int, C.c_float]
+    L.mrt_scene_set_material_emission.argtypes = [C.c_void_p, C.c_int, C.c_float, _fp]
+    L.mrt_scene_set_material_sample_env.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    L.mrt_scene_set_path_trace.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+    L.mrt_scene_prim_object.argtypes = [C.c_void_p, C.c_int32, _ip, _ip, _ip]
     L.mrt_scene_build_bvh.argtypes = [C.c_void_p]
     L.mrt_scene_bvh_info.argtypes = [C.c_void_p, C.POINTER(mrt_bvh_info)]
     L.mrt_scene_bvh_export.argtypes = [C.c_void_p, _fp, _ip, _fp, _ip]

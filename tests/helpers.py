@@ -16,21 +16,34 @@ def fixture_mesh(name):
     return f["verts"], f["normals"], f["vidx"], f["nidx"]
 
 
-def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1, instances=None, subdivs=None):
-    """Build (miro.Scene, OracleScene, camera dict) for a config dict."""
+def materials_pair(P, O_, mat):
+    """One material description -> (product material, oracle material id)."""
+    optics = dict(reflectAmt=mat.get("reflectAmt", 0.0), refractAmt=mat.get("refractAmt", 0.0), ior=mat.get("ior", 1.5),
+                  specGloss=mat.get("specGloss", 1.0))
+    if mat["kind"] == "lambert":
+        pm = miro.Lambert(mat["kd"])
+        return pm, O_.add_material("lambert", kd=mat["kd"])
+    pm = miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0), **optics)
+    pm.setTranslucency(mat.get("translucency", 0.0))
+    pm.setLightEmittedIntensity(mat.get("emitted", 0.0))
+    pm.setLightEmittedColor(mat.get("le", (0, 0, 0)))
+    pm.setSampleEnv(mat.get("sampleEnv", True))
+    om = O_.add_material("blinn", kd=mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0),
+                         translucency=mat.get("translucency", 0.0), le=mat.get("le", (0, 0, 0)),
+                         emitted=mat.get("emitted", 0.0), sampleEnv=mat.get("sampleEnv", True), **optics)
+    return pm, om
+
+
+def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1, instances=None, subdivs=None,
+               extra=None, path_trace=None):
+    """Build (miro.Scene, OracleScene, camera dict) for a config dict.
+    extra: [(mesh arrays, material dict), ...] added after the main geometry;
+    path_trace: (max_bounces, sample_env) turns Scene::m_pathTrace on."""
     lights = cfg["lights"] if lights is None else lights
     mat = cfg["material"]
     P = miro.Scene()
-    optics = dict(reflectAmt=mat.get("reflectAmt", 0.0), refractAmt=mat.get("refractAmt", 0.0), ior=mat.get("ior", 1.5),
-                  specGloss=mat.get("specGloss", 1.0))
-    translucency = mat.get("translucency", 0.0)
-    pm = miro.Lambert(mat["kd"]) if mat["kind"] == "lambert" else miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0),
-                                                                           specAmt=mat.get("specAmt", 0.0), **optics)
-    if translucency and mat["kind"] == "blinn":
-        pm.setTranslucency(translucency)
     O_ = O.OracleScene()
-    om = O_.add_material(mat["kind"], kd=mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0),
-                         translucency=translucency if mat["kind"] == "blinn" else 0.0, **optics)
+    pm, om = materials_pair(P, O_, mat)
     for arrs in (meshes or []):
         tm = miro.TriangleMesh()
         tm.setArrays(*arrs)
@@ -54,6 +67,12 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
         for b, M in placed:
             P.addObject(miro.ProxyObject(*protos[b], miro.Matrix4x4(M)))
             O_.add_instance(oblas[b], M)
+    for arrs, emat in (extra or []):
+        xm, oxm = materials_pair(P, O_, emat)
+        tm = miro.TriangleMesh()
+        tm.setArrays(*arrs)
+        miro.makeMeshObjs(P, tm, xm)
+        O_.add_mesh(*arrs, oxm)
     if floor:
         fl = miro.TriangleMesh()
         fl.createSingleTriangle()
@@ -99,6 +118,9 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
         O_.set_env_map(otex, env["exposure"])
     P.setNumPaths(num_paths)
     O_.set_num_paths(num_paths)
+    if path_trace is not None:
+        P.setPathTrace(True); P.setMaxBounces(path_trace[0]); P.setSampleEnv(path_trace[1])
+        O_.set_path_trace(True, path_trace[0], path_trace[1])
     if subdivs is not None:  # (min, max, noise): Scene::adaptiveSampleScene
         P.setMinSubdivs(subdivs[0]); P.setMaxSubdivs(subdivs[1]); P.setNoise(subdivs[2])
         O_.set_subdivs(*subdivs)
