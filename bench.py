@@ -1,20 +1,29 @@
 #!/usr/bin/env python3
 """Headline benchmark: Mray/s (primary + shadow) on the Sponza config C3
 (1920x1080, 1 spp, Blinn + PointLight; synthetic ~68k-triangle stand-in for the
-missing sponza.obj) -- BASELINE.json `metric` / configs[2].
+missing sponza.obj) -- BASELINE.json `metric` / configs[2].  --config picks the
+other presets of miro/scenes.py (C2, C4, C5, D1, A3, R3, P4).
 
 One "step" = one pass of the hot path over one batch: primary rays + shadow
-rays + shading + Image::Map.
+rays (+ secondary / GI rays) + shading + Image::Map, inputs resident in HBM.
+
 N = 1: one frame per step, rendered straight into HBM buffers (whole-frame
 launch pair); consecutive steps alternate over --inflight (4) HIP streams, each
 with its own scratch in libmrt, so the tail of one frame's persistent launches
-overlaps the start of the next frame (4 streams = the HIP hardware queues per process).  N > 1 (torch.distributed, one process per GPU, backend nccl =
-RCCL): weak scaling -- a step renders a camera path of N frames (frame 0 is the
-config camera, then 2.5-degree pans), the 32x32 buckets of all N frames are
-dealt id mod N (reference bucket grid, src/Scene.cpp:90-95), every rank renders
-its share in one launch pair into packed 8-bit tiles, one RCCL gather per step
-brings them to rank 0, which scatters them into the N frames; the gather of
-step k overlaps the render of step k + 1 (miro/tiles.py BatchPipeline).
+overlaps the start of the next frame.
+
+N > 1: one process per GPU (torch.distributed, backend nccl = RCCL).  `python
+bench.py --gpus N` spawns the N ranks itself when WORLD_SIZE is not set (the
+parent never touches torch or HIP); under torch.distributed.run WORLD_SIZE must
+equal --gpus.  The headline `value` is weak scaling: a step renders a camera
+path of N frames (frame 0 is the config camera, then 2.5-degree pans), the
+32x32 buckets of all N frames are dealt id mod N (reference bucket grid,
+src/Scene.cpp:90-95), every rank renders its share in one launch pair into
+packed 8-bit tiles, one RCCL gather per step brings them to rank 0, which
+scatters them into the N frames; the gather of step k overlaps the render of
+step k + 1 (miro/tiles.py BatchPipeline).  `strong` times the north-star split
+of ONE frame: its buckets dealt id mod N, float tiles gathered to rank 0.
+
 value = rays of all frames of all steps / max-over-ranks wall time.  Rank 0
 prints one JSON line.
 """
@@ -24,6 +33,8 @@ import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,7 +42,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "rendering-algorithms-raytracer_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 ~34.5 TB/s aggregate
 NODE_B, LEAF_B = 128, 160      # QNode / DLeaf bytes (csrc/mrt_types.h)
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+CPU_CAL_FILE = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
 
 
 def parse():
@@ -47,10 +61,32 @@ def parse():
                          "streams, so one frame's launch tail overlaps the next frame's start)")
     ap.add_argument("--path", choices=["auto", "batch"], default="auto",
                     help="batch: use the bucket-batch path even for one frame on one GPU (A/B)")
+    ap.add_argument("--strong-steps", type=int, default=0, help="N > 1: single-frame steps timed (default --steps)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-thread-seconds for the oracle sample")
     return ap.parse_args()
 
 
+# ------------------------------------------------------------------ launcher
+def spawn(args):
+    """--gpus N without WORLD_SIZE: start N fresh rank processes (one per GPU)
+    before anything in this process touches torch / HIP; return rank 0's code."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+# ------------------------------------------------------------------ helpers
 def _camera(c):
     import miro
     cam = miro.Camera()
@@ -61,6 +97,8 @@ def _camera(c):
 def _pixels_in_frame(ids, bpf, bx, W, H):
     n = 0
     for i in ids:
+        if i < 0:
+            continue
         b = i % bpf
         n += min(32, W - (b % bx) * 32) * min(32, H - (b // bx) * 32)
     return n
@@ -84,18 +122,44 @@ def kernel_bytes(st, px, hits, float_out=True, wavefront=False):
     return primary, shade
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    """The host cores this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS when the environment sets it (the GPU box's CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(cfg_key, seconds):
     """The CPU oracle (C restatement, OpenMP) on this host's cores, bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from miro import scenes
     cfg = scenes.CONFIGS[cfg_key]
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = cpu_threads()
     s = O.OracleScene()
-    mat = cfg["material"]
-    m = s.add_material(mat["kind"], kd=mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0),
-                       reflectAmt=mat.get("reflectAmt", 0.0), refractAmt=mat.get("refractAmt", 0.0),
-                       ior=mat.get("ior", 1.5))
+
+    def material(mat):
+        return s.add_material(mat["kind"], kd=mat["kd"], specExp=mat.get("specExp", 1.0),
+                              specAmt=mat.get("specAmt", 0.0), reflectAmt=mat.get("reflectAmt", 0.0),
+                              refractAmt=mat.get("refractAmt", 0.0), ior=mat.get("ior", 1.5),
+                              specGloss=mat.get("specGloss", 1.0), translucency=mat.get("translucency", 0.0),
+                              le=mat.get("le", (0, 0, 0)), emitted=mat.get("emitted", 0.0),
+                              sampleEnv=mat.get("sampleEnv", True))
+
+    m = material(cfg["material"])
     if cfg["mesh"] == "sponza":
         s.add_obj(scenes.sponza_obj(), m)
     elif cfg["mesh"] in ("bunny", "instances"):
@@ -105,35 +169,41 @@ def cpu_baseline(cfg_key, seconds):
             blas = [s.make_blas([s.add_obj(p, m)]) for p in (scenes.dragon_obj(), scenes.buddha_obj())]
             for i, M in enumerate(scenes.instance_transforms(**cfg["instances"])):
                 s.add_instance(blas[i % 2], M)
-        s.add_mesh([(-100, 0, -100), (0, 0, 100), (100, 0, -100)], [(0, 1, 0)] * 3, [(0, 1, 2)], [(0, 1, 2)], m)
     else:
         import numpy as np
         f = np.load(os.path.join(ROOT, "tests", "golden", "cornell_box_mesh.npz"))
         s.add_mesh(f["verts"], f["normals"], f["vidx"], f["nidx"], m)
+    for name, emat in cfg.get("extra", ()):
+        s.add_obj(scenes.EXTRA_OBJS[name], material(emat))
+    if cfg["mesh"] in ("bunny", "instances"):
+        s.add_mesh([(-100, 0, -100), (0, 0, 100), (100, 0, -100)], [(0, 1, 0)] * 3, [(0, 1, 2)], [(0, 1, 2)], m)
     skies = {}
 
-    def sky(size):
-        if size not in skies:
-            skies[size] = s.add_texture(scenes.sky_rgb(*size))
-        return skies[size]
+    def sky(spec):
+        k = scenes.sky_key(spec)
+        if k not in skies:
+            skies[k] = s.add_texture(scenes.env_image(spec, hdr_loader=O.hdr_load))
+        return skies[k]
 
     for l in cfg["lights"]:
         if l["type"] == "point":
             s.add_point_light(l["pos"], l["power"])
         elif l["type"] == "dome":
-            s.add_dome_light(sky(tuple(l["sky"])), l["power"], l.get("samples", 1), l.get("noise", 0.001))
+            s.add_dome_light(sky(l["sky"]), l["power"], l.get("samples", 1), l.get("noise", 0.001))
         else:
             s.add_rect_light(l["v1"], l["v2"], l["v3"], l["power"], l.get("samples", 1), l.get("noise", 0.001))
     s.set_bg(cfg["bg"])
     if cfg.get("env"):
-        s.set_env_map(sky(tuple(cfg["env"]["sky"])), cfg["env"]["exposure"])
+        s.set_env_map(sky(cfg["env"]["sky"]), cfg["env"]["exposure"])
     s.set_num_paths(cfg.get("num_paths", 1))
+    if cfg.get("path_trace"):
+        s.set_path_trace(True, *cfg["path_trace"])
     if cfg.get("subdivs"):
         s.set_subdivs(*cfg["subdivs"])
     s.build()
     W, H = cfg["W"], cfg["H"]
     rays, t_total, frames = 0, 0.0, 0
-    band = 64
+    band = 64 if not cfg.get("path_trace") else 8
     y = 0
     while t_total * threads < seconds and t_total < 60.0:
         y0 = y % H
@@ -143,23 +213,50 @@ def cpu_baseline(cfg_key, seconds):
         rays += r["primary_rays"] + r["shadow_rays"] + r["secondary_rays"]
         y += band
         frames += 1
-    return {"value": round(rays / t_total / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
-            "sample": f"{cfg_key} {W}x{H}: {frames} bands of {band} rows ({rays} rays, {t_total:.1f} s wall, "
-                      f"{threads} OpenMP threads, oracle/mrt_oracle.c -O2)"}
+    value = rays / t_total / 1e6
+    out = {"value": round(value, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+           "cpu": cpu_model(), "affinity_cpus": len(os.sched_getaffinity(0)),
+           "sample": f"{cfg_key} {W}x{H}: {frames} bands of {band} rows ({rays} rays, {t_total:.1f} s wall, "
+                     f"{threads} OpenMP threads, oracle/mrt_oracle.c -O2)"}
+    if os.path.exists(CPU_CAL_FILE):   # oracle vs the reference's own 1-thread rate, same Xeon
+        cal = json.load(open(CPU_CAL_FILE))
+        out["reference_equivalent"] = round(value * cal["ratio_reference_over_oracle"], 3)
+        out["calibration"] = (f"x{cal['ratio_reference_over_oracle']}: the reference renders explosion01 1920x1080 "
+                              f"at {cal['reference_mray_s'][0]}-{cal['reference_mray_s'][1]} Mray/s on 1 thread, the "
+                              f"oracle at {cal['oracle_mray_s']} on the same {cal['cpu']} "
+                              f"(profiles/r02_cpu_calibration.json)")
+    return out
 
 
 def _scene_setup(scene):
     """One-time host BVH::build (src/BVH.cpp:457-575), outside the timed region."""
     ms = getattr(scene, "bvh_build_ms", None)
     prims = scene.bvh_info["prims"]
-    return {"bvh_build_ms": None if ms is None else round(ms, 2), "prims": prims, "threads": 1,
+    return {"bvh_build_ms": None if ms is None else round(ms, 2), "prims": prims,
             "build_mprims_per_s": None if not ms else round(prims / ms / 1e3, 3),
             # instanced scenes: the BLAS builds (mrt_scene_make_blas) happen before the world QBVH
-            "blas_build_ms": round(getattr(scene, "blas_build_ms", 0.0), 2)}
+            "blas_build_ms": round(getattr(scene, "blas_build_ms", 0.0), 2),
+            "blas_prims": getattr(scene, "blas_prims", 0)}
 
 
+def pmc_traffic(config):
+    """HBM bytes per launch of each pass, from the committed rocprofv3 --pmc
+    passes of this config (tools/pmc.sh + tools/pmc_summary.py)."""
+    if not os.path.exists(PMC_FILE):
+        return None, None
+    prof = json.load(open(PMC_FILE))
+    entry = prof.get("configs", {}).get(config)
+    return (entry or {}).get("per_launch_hbm_bytes"), prof.get("source", {}).get(config)
+
+
+# ------------------------------------------------------------------ worker
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn(args))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}")
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -181,7 +278,6 @@ def main():
     W, H = cfg["W"], cfg["H"]
     L = miro.lib()
     stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
     # frames per step: 1 at N = 1; N > 1 renders a camera path of N frames per
     # step (weak scaling: one frame of work per GPU per step), every frame's
     # buckets dealt over all ranks, 8-bit tiles gathered once per step
@@ -192,25 +288,29 @@ def main():
     use_frame_path = world == 1 and n_frames == 1 and args.path == "auto"
     inflight = max(1, args.inflight) if use_frame_path else 1
     streams = [stream] + [torch.cuda.Stream() for _ in range(inflight - 1)]
-    frame = [torch.empty(H * W * 3, dtype=torch.float32, device="cuda") for _ in range(inflight)] \
-        if use_frame_path else None
+    frame = [torch.empty(H * W * 3, dtype=torch.float32, device="cuda") for _ in range(inflight)]
     frame8 = [torch.empty(H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(inflight)]
     frames8 = [frame8[0]] if use_frame_path else \
         [torch.empty(n_frames * H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(2)]
     camc = (_lib.mrt_camera * n_frames)(*[c._c() for c in cams])
     opts_count = _lib.mrt_render_opts(W, H, dev, 1, 1, 0, 0)
     opts = _lib.mrt_render_opts(W, H, dev, 0, 1, 0, 0)
+
+    def render_items(ids, n, cams_, n_cams, tiles_f, tiles_8, o=opts):
+        _lib.check(L.mrt_render_batch_async(scene.handle, cams_, n_cams, C.byref(o), ids.data_ptr(), n,
+                                            tiles_f, tiles_8, torch.cuda.current_stream().cuda_stream), "render batch")
+
     if not use_frame_path:
-        mine = tiles_mod.batch_items(bpf, n_frames, world, rank)
+        # this rank's items, unpadded; the gather needs equal sizes, so every rank's
+        # buffer holds `per` slots and the unused ones are unpacked as id -1 (skipped)
+        mine = tiles_mod.rank_buckets(bpf * n_frames, world, rank)
+        per = -(-bpf * n_frames // world)
         items = torch.tensor(mine, dtype=torch.int32, device="cuda")
-        all_items = torch.tensor([i for r in range(world) for i in tiles_mod.batch_items(bpf, n_frames, world, r)],
+        all_items = torch.tensor([i for r in range(world) for i in tiles_mod.padded_items(bpf * n_frames, world, r)],
                                  dtype=torch.int32, device="cuda")
-        per = len(mine)
 
         def render(ids, out, o=opts):
-            _lib.check(L.mrt_render_batch_async(scene.handle, camc, n_frames, C.byref(o), ids.data_ptr(), len(ids),
-                                                None, out.data_ptr(), torch.cuda.current_stream().cuda_stream),
-                       "render batch")
+            render_items(ids, len(mine), camc, n_frames, None, out.data_ptr(), o)
 
         def unpack(ids, gathered, b):
             _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(ids), None, gathered.data_ptr(), W, H, n_frames,
@@ -224,12 +324,15 @@ def main():
 
     nstep = [0]
 
+    def frame_step(o, serial=False):
+        i = 0 if serial else nstep[0] % inflight
+        nstep[0] += 1
+        _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(o), frame[i].data_ptr(),
+                                            frame8[i].data_ptr(), streams[i].cuda_stream), "render")
+
     def step(o, serial=False):
         if use_frame_path:
-            i = 0 if serial else nstep[0] % inflight
-            nstep[0] += 1
-            _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(o), frame[i].data_ptr(),
-                                                frame8[i].data_ptr(), streams[i].cuda_stream), "render")
+            frame_step(o, serial)
         elif o is opts_count:
             render(items, pipe.tiles[0], opts_count)     # instrumented launch only (no gather)
         else:
@@ -243,7 +346,7 @@ def main():
     # adaptive supersampling (subdivs > 1): eye rays per pixel vary, counted by the kernel
     adaptive = bool(cfg.get("subdivs")) and max(cfg["subdivs"][:2]) > 1
     eye_mine = st["primary_rays"] if adaptive else 0
-    second_mine = st["secondary_rays"]   # Blinn reflection / refraction rays
+    second_mine = st["secondary_rays"]   # Blinn reflection / refraction / GI rays
     if world > 1:
         t = torch.tensor([shadow_mine, eye_mine, second_mine], dtype=torch.float64, device="cuda")
         dist.all_reduce(t)
@@ -258,8 +361,6 @@ def main():
         step(opts)
     if not use_frame_path:
         pipe.flush()
-    # per-launch durations of the uninstrumented kernels (HIP events on this stream)
-    prim_ms, shade_ms = [], []
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -272,18 +373,69 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    st_last = scene.stats()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    # separate short loop for per-launch event timing (render launches only)
+
+    # strong scaling: ONE frame per step, its buckets dealt id mod N, float tiles
+    # gathered to rank 0 and scattered into the frame (the north-star split)
+    strong = None
+    if world > 1:
+        sb = tiles_mod.rank_buckets(bpf, world, rank)
+        sper = -(-bpf // world)
+        s_items = torch.tensor(sb, dtype=torch.int32, device="cuda")
+        s_all = torch.tensor([i for r in range(world) for i in tiles_mod.padded_items(bpf, world, r)],
+                             dtype=torch.int32, device="cuda")
+        s_tiles = torch.empty(sper * 1024 * 3, dtype=torch.float32, device="cuda")
+        s_recv = torch.empty(world * sper * 1024 * 3, dtype=torch.float32, device="cuda") if rank == 0 else None
+        cam1 = (_lib.mrt_camera * 1)(cams[0]._c())
+
+        def strong_step():
+            render_items(s_items, len(sb), cam1, 1, s_tiles.data_ptr(), None)
+            dist.gather(s_tiles, list(s_recv.chunk(world)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                _lib.check(L.mrt_unpack_batch_async(s_all.data_ptr(), len(s_all), s_recv.data_ptr(), None, W, H, 1,
+                                                    frame[0].data_ptr(), frame8[0].data_ptr(), scene.handle,
+                                                    torch.cuda.current_stream().cuda_stream), "unpack strong")
+
+        render_items(s_items, len(sb), cam1, 1, s_tiles.data_ptr(), None, opts_count)
+        torch.cuda.synchronize()
+        sst = scene.stats()
+        t = torch.tensor([sst["shadow_rays"], sst["secondary_rays"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        s_rays = W * H + int(t[0].item()) + int(t[1].item())
+        for _ in range(max(1, args.warmup)):
+            strong_step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        k_strong = args.strong_steps or args.steps
+        t0 = time.perf_counter()
+        for _ in range(k_strong):
+            strong_step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        se = time.perf_counter() - t0
+        t = torch.tensor([se], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        se = t.item()
+        strong = {"value": round(s_rays * k_strong / se / 1e6, 2), "unit": "Mray/s", "frames_per_step": 1,
+                  "steps": k_strong, "ms_per_frame": round(se / k_strong * 1e3, 4), "rays_per_frame": s_rays,
+                  "split": f"one {W}x{H} frame, 32x32 buckets dealt id mod {world}, float32 tiles gathered to rank 0 "
+                           f"(RCCL) and unpacked there, serial steps"}
+
+    # per-launch durations of the uninstrumented kernels (HIP events on the
+    # launch's stream), and the latency of one frame with nothing else in flight
+    prim_ms, shade_ms, lat_ms = [], [], []
     for _ in range(5):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         if use_frame_path:
             step(opts, serial=True)
         else:
             render(items, pipe.tiles[0])
         torch.cuda.synchronize()
+        lat_ms.append((time.perf_counter() - t1) * 1e3)
         s2 = scene.stats()
         prim_ms.append(s2["primary_ms"])
         shade_ms.append(s2["shade_ms"])
@@ -294,36 +446,34 @@ def main():
     px_mine = W * H if use_frame_path else _pixels_in_frame(sorted(set(mine)), bpf, bx, W, H)
     hits_mine = hits_px
     # the specialised kernel runs for one point light, one path and no environment map
-    mat = cfg["material"]
-    recursive = mat["kind"] == "blinn" and (mat.get("reflectAmt", 0) > 0 or mat.get("refractAmt", 0) > 0)
+    chain = scenes.chain_level(cfg)
     one_light = (len(cfg["lights"]) == 1 and cfg["lights"][0]["type"] == "point" and cfg.get("num_paths", 1) == 1
-                 and not cfg.get("env") and not recursive)
+                 and not cfg.get("env") and chain == 0 and not cfg.get("extra"))
     b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=use_frame_path,
-                                   wavefront=not one_light and not recursive)
-    if recursive:   # each secondary hit gathers its PrimShade + 3 vertices + 3 normals
-        b_shade += second_mine * (16 + 32 + 3 * 16 + 3 * 16)
+                                   wavefront=not one_light and chain == 0)
+    if chain:   # each secondary / GI hit gathers its PrimShade + 3 vertices + 3 normals (+ its level record)
+        b_shade += second_mine * (16 + 32 + 3 * 16 + 3 * 16 + 12)
     pm, sm = float(np.median(prim_ms)), float(np.median(shade_ms))
     shade_name = ("shade1_kernel (shade + any-hit shadow rays)" if one_light else
-                  "shade_kernel (fused: shade + reflection/refraction rays + any-hit shadow rays)" if recursive else
+                  "shade_kernel (fused chains: shade + reflection/refraction/GI rays + any-hit shadow rays)" if chain else
                   "shade pass (shade_kernel<gen> + shadow_kernel any-hit + shade_kernel<resolve>)")
     if adaptive:   # one fused launch: eye rays, shading, inline shadow rays (its time is shade_ms)
-        dom, dom_ms = "adaptive_kernel (eye rays + shading + any-hit shadow rays)", sm
+        dom, dom_key, dom_ms = "adaptive_kernel (eye rays + shading + any-hit shadow rays)", "shade", sm
         dom_b = (st["node_visits"] * NODE_B + st["leaf_visits"] * LEAF_B
                  + px_mine * (16 + (12 if use_frame_path else 0) + 3) + hits_px * (32 + 3 * 16 + 3 * 16))
     elif sm >= pm:
-        dom, dom_ms, dom_b = shade_name, sm, b_shade
+        dom, dom_key, dom_ms, dom_b = shade_name, "shade", sm, b_shade
     else:
-        dom, dom_ms, dom_b = "primary_kernel (camera rays, closest hit)", pm, b_prim
+        dom, dom_key, dom_ms, dom_b = "primary_kernel (camera rays, closest hit)", "primary", pm, b_prim
     achieved = dom_b / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if use_frame_path and os.path.exists(pmc):   # PMC pass was taken on the N = 1 frame path
-        try:
-            prof = json.load(open(pmc))
-            if prof.get("config") == args.config:
-                traffic = prof.get("per_launch_hbm_bytes", {}).get(dom.split()[0])
-        except Exception:
-            traffic = None
+    traffic, pmc_src = pmc_traffic(args.config) if use_frame_path else (None, None)
+    dom_traffic = (traffic or {}).get(dom_key)
+    hbm = None
+    if dom_traffic:
+        hbm_gbs = dom_traffic / (dom_ms * 1e-3) / 1e9
+        hbm = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": int(dom_traffic), "source": pmc_src}
+    lane_util = round(st["primary_node_visits"] / max(1, 64 * st["primary_wave_steps"]), 4)
     out = {
         "metric": ("Mray/s (primary+shadow) on Sponza 1920x1080" if args.config == "C3" else
                    f"Mray/s (primary+shadow{'+secondary' if second_total else ''}) [{args.config}: {cfg['name']}]"),
@@ -334,8 +484,9 @@ def main():
                  % ({"sponza": "Sponza", "bunny": "bunny", "instances": "dragon_2 / buddha_smooth"}.get(
                      cfg["mesh"], cfg["mesh"]), scene.bvh_info["prims"],
                     {"instances": "dragon_2.obj / buddha_smooth"}.get(cfg["mesh"], cfg["mesh"]),
-                    "; procedural lat-long sky for the dome / environment map" if cfg.get("env") else "")),
-        "config": {"workload": cfg["name"], "config": args.config, "width": W, "height": H, "spp": 1 if not adaptive else f"adaptive {cfg['subdivs'][0]}..{cfg['subdivs'][1]} subdivs, "
+                    "; Images/Arches_E_PineTree.hdr dome / environment map" if cfg.get("env") else "")),
+        "config": {"workload": cfg["name"], "config": args.config, "width": W, "height": H,
+                   "spp": 1 if not adaptive else f"adaptive {cfg['subdivs'][0]}..{cfg['subdivs'][1]} subdivs, "
                    f"{primary_total / (n_frames * W * H):.2f} eye rays/px",
                    "frames_per_step": n_frames, "rays_per_step": rays_per_step, "shadow_rays": shadow_total,
                    "secondary_rays": second_total,
@@ -344,18 +495,27 @@ def main():
                    "parallelism": "single GPU, whole frame" if use_frame_path else
                    f"{n_frames}-frame camera path per step, 32x32 buckets dealt id mod {world}, "
                    f"one RCCL gather of 8-bit tiles per step (double-buffered)"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+        # The traversal is bound by latency along each wave's dependent chain
+        # (~35% VALU busy, 41% memory wait); its algorithmic bytes
+        # are served by L1/L2, so the ceiling they are priced against is the L2
+        # bandwidth; `hbm` prices the counter-measured DRAM-side bytes.
+        "roofline": {"bound": "l2", "kernel": dom, "achieved": round(achieved, 1), "peak": L2_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / L2_PEAK_GBS, 4),
+                     "traffic": None if dom_traffic is None else int(dom_traffic),
+                     "hbm": hbm, "lane_util": lane_util,
                      "launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(dom_b),
-                     "visits_per_ray": round(st["node_visits"] / max(1, (eye_mine if adaptive else px_mine) + shadow_mine + second_mine), 3)},
+                     "visits_per_ray": round(st["node_visits"] / max(1, (eye_mine if adaptive else px_mine)
+                                                                    + shadow_mine + second_mine), 3)},
         "launch_ms": {"primary": round(pm, 4), "shade": round(sm, 4)},
+        "frame_latency_ms": round(float(np.median(lat_ms)), 4),
         # one-time host side (outside the timed region): BVH::build over the scene's triangles
         "scene_setup": _scene_setup(scene),
         # instrumented (count-mode) launch: wall-clock spread of the persistent waves
         "wave_timing_us": {k: round(st[k], 1) for k in ("primary_span_us", "primary_ramp_us", "primary_tail_us",
                                                        "shade_span_us", "shade_ramp_us", "shade_tail_us")},
-        "lane_util": round(st["primary_node_visits"] / max(1, 64 * st["primary_wave_steps"]), 4),
     }
+    if strong is not None:
+        out["strong"] = strong
     if not args.no_cpu_baseline and world == 1:
         try:
             out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)

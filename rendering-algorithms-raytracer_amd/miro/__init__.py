@@ -446,6 +446,7 @@ class Scene:
 
         blas = {}   # BVH object -> BLAS id (built once, shared by its instances)
         self.blas_build_ms = 0.0
+        self.blas_prims = 0
         self.blas_ids = blas
         for item, mat in self._meshes:
             if not isinstance(item, ProxyObject):
@@ -457,6 +458,9 @@ class Scene:
                 t0 = time.perf_counter()
                 blas[key] = check(L.mrt_scene_make_blas(self._h, ids, len(ids)), "BLAS build")
                 self.blas_build_ms += (time.perf_counter() - t0) * 1e3
+                n, lv, p = C.c_int32(), C.c_int32(), C.c_int32()
+                check(L.mrt_scene_blas_info(self._h, blas[key], C.byref(n), C.byref(lv), C.byref(p)), "blas_info")
+                self.blas_prims += p.value
             m16 = np.ascontiguousarray(item.matrix, np.float32).reshape(16)
             check(L.mrt_scene_add_instance(self._h, blas[key], m16.ctypes.data_as(C.POINTER(C.c_float))), "instance")
         tex_ids = {}

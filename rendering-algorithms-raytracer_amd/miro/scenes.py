@@ -20,6 +20,14 @@ import numpy as np
 
 SCENE_VERSION = 1
 
+# Reference data files the configs use as they are (copied from the reference's
+# Images/ and Models/; data, not code): the dome / environment map of config 5
+# and the Sponza path-tracing light panel of makeSponzaScenePathTrace.
+ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "assets")
+ARCHES_HDR = os.path.join(ASSETS, "Arches_E_PineTree.hdr")      # Images/Arches_E_PineTree.hdr, 1000 x 500
+SPONZA_LIGHT_OBJ = os.path.join(ASSETS, "sponza-light.obj")      # Models/sponza-light.obj
+SKIES = {"arches": ARCHES_HDR}
+
 
 def _cache_dir():
     d = os.environ.get("MRT_SCENE_CACHE", os.path.join("/tmp", "mrt_scenes"))
@@ -343,6 +351,21 @@ def sky_rgb(W=512, H=256):
     return np.ascontiguousarray(rgb, np.float32)
 
 
+def env_image(spec, hdr_loader=None):
+    """(H, W, 3) float32 lat-long image of a config's sky spec: a name in SKIES
+    (a Radiance .hdr decoded by `hdr_loader(path)`, default libmrt's
+    HDRLoader::load restatement) or a (W, H) tuple (the procedural sky_rgb)."""
+    if isinstance(spec, str):
+        path = SKIES[spec]
+        if hdr_loader is None:
+            import miro
+            img = miro.RawImage()
+            img.loadHDR(path)
+            return img.m_rawData
+        return hdr_loader(path)
+    return sky_rgb(*spec)
+
+
 # ---------------------------------------------------------------- presets
 CONFIGS = {
     # C1: cornell_box.obj 256x256, 1 spp, Lambert + 1 PointLight (plumbing)
@@ -391,23 +414,37 @@ CONFIGS = {
                mesh="sponza", num_paths=16),
     # C5: dragon + buddha stand-ins instanced 64x via ProxyObject (two BLASes,
     # alternating, seeded transforms) on a floor triangle, 3840x2160, DomeLight (power
-    # 0.15, 6 samples, src/main.cpp:157-165) over the procedural sky, the same map
-    # as environment on missed rays; Blinn with a specular lobe
-    "C5": dict(name="dragon + buddha stand-ins instanced 64x (ProxyObject) 3840x2160, DomeLight 6 samples + env map",
+    # 0.15, 6 samples, src/main.cpp:157-165) over Images/Arches_E_PineTree.hdr, the same
+    # map as environment on missed rays; Blinn with a specular lobe
+    "C5": dict(name="dragon + buddha stand-ins instanced 64x (ProxyObject) 3840x2160, DomeLight "
+                    "(Arches_E_PineTree.hdr) 6 samples + env map",
                W=3840, H=2160, camera=dict(eye=(0.0, 10.0, 27.0), lookAt=(0.0, 0.5, 0.0), up=(0, 1, 0), fov=45.0),
-               lights=[dict(type="dome", sky=(512, 256), power=0.15, samples=6, noise=0.001)],
-               env=dict(sky=(512, 256), exposure=1.0),
+               lights=[dict(type="dome", sky="arches", power=0.15, samples=6, noise=0.001)],
+               env=dict(sky="arches", exposure=1.0),
                material=dict(kind="blinn", kd=(0.8, 0.8, 0.8), specExp=20.0, specAmt=0.3), bg=(0.0, 0.0, 0.2),
                mesh="instances", instances=dict(n=64, grid=8, spacing=3.2, seed=64)),
     # D1: image-based lighting on the C2 bunny stand-in + floor: DomeLight (power
-    # 0.15, 6 samples, as src/main.cpp:157-165) over the synthetic sky, the same map
-    # as environment on missed primary rays; Blinn with a specular lobe
-    "D1": dict(name="bunny stand-in + floor 1024x1024 Blinn+DomeLight (6 samples) + env map", W=1024, H=1024,
+    # 0.15, 6 samples, as src/main.cpp:157-165) over Images/Arches_E_PineTree.hdr, the
+    # same map as environment on missed primary rays; Blinn with a specular lobe
+    "D1": dict(name="bunny stand-in + floor 1024x1024 Blinn+DomeLight (Arches_E_PineTree.hdr, 6 samples) + env map",
+               W=1024, H=1024,
                camera=dict(eye=(0.0, 5.0, 15.0), lookAt=(0.0, 0.0, 0.0), up=(0, 1, 0), fov=45.0),
-               lights=[dict(type="dome", sky=(512, 256), power=0.15, samples=6, noise=0.001)],
-               env=dict(sky=(512, 256), exposure=1.0),
+               lights=[dict(type="dome", sky="arches", power=0.15, samples=6, noise=0.001)],
+               env=dict(sky="arches", exposure=1.0),
                material=dict(kind="blinn", kd=(0.8, 0.8, 0.8), specExp=20.0, specAmt=0.3), bg=(0.0, 0.0, 0.2),
                mesh="bunny"),
+    # P4: makeSponzaScenePathTrace (src/assignment2.h:663-710) as written: 512x512,
+    # Scene::m_pathTrace with m_numPaths = 16 and m_maxBounces = 10, RectangleLight
+    # (8,10,2)/(8,10,-2)/(-8,10,2) power 1.5, Models/sponza-light.obj as an emissive
+    # Blinn (setLightEmittedIntensity 1.5, colour 1), Blinn kd = 1 on the Sponza stand-in
+    "P4": dict(name="sponza stand-in (~66k tris) 512x512 path tracing (16 paths, 10 bounces) + RectangleLight "
+                    "+ emissive sponza-light.obj", W=512, H=512,
+               camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
+               lights=[dict(type="rect", v1=(8.0, 10.0, 2.0), v2=(8.0, 10.0, -2.0), v3=(-8.0, 10.0, 2.0),
+                            power=1.5, samples=1, noise=0.001)],
+               extra=[("sponza_light", dict(kind="blinn", kd=(1, 1, 1), emitted=1.5, le=(1, 1, 1)))],
+               material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza", num_paths=16,
+               path_trace=(10, False)),
 }
 
 
@@ -427,6 +464,40 @@ def camera_path(cam, n, step_deg=2.5):
     return out
 
 
+EXTRA_OBJS = {"sponza_light": SPONZA_LIGHT_OBJ}
+
+
+def sky_key(spec):
+    return spec if isinstance(spec, str) else tuple(spec)
+
+
+def make_material(mat):
+    """miro material of a config's material dict (all of its Blinn settings)."""
+    import miro
+    if mat["kind"] == "lambert":
+        return miro.Lambert(mat["kd"])
+    m = miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0),
+                   reflectAmt=mat.get("reflectAmt", 0.0), refractAmt=mat.get("refractAmt", 0.0), ior=mat.get("ior", 1.5),
+                   specGloss=mat.get("specGloss", 1.0))
+    m.setTranslucency(mat.get("translucency", 0.0))
+    m.setLightEmittedIntensity(mat.get("emitted", 0.0))
+    m.setLightEmittedColor(mat.get("le", (0, 0, 0)))
+    m.setSampleEnv(mat.get("sampleEnv", True))
+    return m
+
+
+def chain_level(cfg):
+    """Which shading path libmrt takes for a config (Shader REC): 2 path tracing,
+    1 reflection / refraction / gloss / translucency chains, 0 direct lighting."""
+    if cfg.get("path_trace"):
+        return 2
+    for m in [cfg["material"]] + [e[1] for e in cfg.get("extra", ())]:
+        if m["kind"] == "blinn" and (m.get("reflectAmt", 0) > 0 or m.get("refractAmt", 0) > 0
+                                     or m.get("specGloss", 1.0) < 1.0 or m.get("translucency", 0) > 0.01):
+            return 1
+    return 0
+
+
 def build_config(key, device=0):
     """Product-side scene for a config preset -> (miro.Scene, miro.Camera, cfg).
     C1 needs the Cornell mesh fixture path in MRT_CORNELL_NPZ (or tests/golden)."""
@@ -434,10 +505,7 @@ def build_config(key, device=0):
 
     cfg = CONFIGS[key]
     scene = miro.Scene(device=device)
-    mat = cfg["material"]
-    material = miro.Lambert(mat["kd"]) if mat["kind"] == "lambert" else \
-        miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0),
-                   reflectAmt=mat.get("reflectAmt", 0.0), refractAmt=mat.get("refractAmt", 0.0), ior=mat.get("ior", 1.5))
+    material = make_material(cfg["material"])
     mesh = miro.TriangleMesh()
     if cfg["mesh"] == "cornell":
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -459,6 +527,10 @@ def build_config(key, device=0):
         for i, M in enumerate(instance_transforms(**cfg["instances"])):
             objs, bvh = protos[i % 2]
             scene.addObject(miro.ProxyObject(objs, bvh, miro.Matrix4x4(M)))
+    for name, emat in cfg.get("extra", ()):   # e.g. the emissive light panel of P4
+        tm = miro.TriangleMesh()
+        tm.load(EXTRA_OBJS[name])
+        miro.makeMeshObjs(scene, tm, make_material(emat))
     if cfg["mesh"] in ("bunny", "instances"):  # floor triangle, src/assignment2.h:110-124
         fl = miro.TriangleMesh()
         fl.createSingleTriangle()
@@ -467,10 +539,11 @@ def build_config(key, device=0):
         miro.makeMeshObjs(scene, fl, material)
     skies = {}
 
-    def sky_texture(size):
-        if size not in skies:
-            skies[size] = miro.Texture(miro.RawImage(size[0], size[1], sky_rgb(*size)))
-        return skies[size]
+    def sky_texture(spec):
+        if spec not in skies:
+            rgb = env_image(spec)
+            skies[spec] = miro.Texture(miro.RawImage(rgb.shape[1], rgb.shape[0], rgb))
+        return skies[spec]
 
     for l in cfg["lights"]:
         if l["type"] == "point":
@@ -478,7 +551,7 @@ def build_config(key, device=0):
             pl.setPosition(l["pos"])
         elif l["type"] == "dome":
             pl = miro.DomeLight()
-            pl.setTexture(sky_texture(tuple(l["sky"])))
+            pl.setTexture(sky_texture(sky_key(l["sky"])))
             pl.setSamples(l.get("samples", 1))
             pl.setNoiseThreshold(l.get("noise", 0.001))
         else:
@@ -490,9 +563,13 @@ def build_config(key, device=0):
         scene.addLight(pl)
     scene.setBGColor(cfg["bg"])
     if cfg.get("env"):
-        scene.setEnvMap(sky_texture(tuple(cfg["env"]["sky"])))
+        scene.setEnvMap(sky_texture(sky_key(cfg["env"]["sky"])))
         scene.setEnvExposure(cfg["env"]["exposure"])
     scene.setNumPaths(cfg.get("num_paths", 1))
+    if cfg.get("path_trace"):
+        scene.setPathTrace(True)
+        scene.setMaxBounces(cfg["path_trace"][0])
+        scene.setSampleEnv(cfg["path_trace"][1])
     if cfg.get("subdivs"):
         lo, hi, noise = cfg["subdivs"]
         scene.setMinSubdivs(lo); scene.setMaxSubdivs(hi); scene.setNoise(noise)

@@ -68,6 +68,15 @@ def unpack_tiles_numpy(ids, tiles, W: int, H: int, frame=None):
     return frame
 
 
+def padded_items(n: int, world: int, rank: int) -> List[int]:
+    """This rank's item ids (i mod world == rank) padded with -1 to the common
+    length ceil(n / world): the gather buffers have equal sizes, the renders skip
+    the padding (they see only the unpadded list) and the unpack ignores id -1
+    (its frame index is past the batch), so no work is done or counted twice."""
+    mine = rank_buckets(n, world, rank)
+    return mine + [-1] * (-(-n // world) - len(mine))
+
+
 def batch_items(buckets_per_frame: int, n_frames: int, world: int, rank: int) -> List[int]:
     """This rank's item ids (frame * buckets_per_frame + bucket) of a batch,
     padded by repeating its last id to ceil(total / world) (equal gather sizes;

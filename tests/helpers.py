@@ -67,12 +67,16 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
         for b, M in placed:
             P.addObject(miro.ProxyObject(*protos[b], miro.Matrix4x4(M)))
             O_.add_instance(oblas[b], M)
-    for arrs, emat in (extra or []):
+    for arrs, emat in (extra or []):   # mesh arrays, or an OBJ path
         xm, oxm = materials_pair(P, O_, emat)
         tm = miro.TriangleMesh()
-        tm.setArrays(*arrs)
+        if isinstance(arrs, str):
+            tm.load(arrs)
+            O_.add_obj(arrs, oxm)
+        else:
+            tm.setArrays(*arrs)
+            O_.add_mesh(*arrs, oxm)
         miro.makeMeshObjs(P, tm, xm)
-        O_.add_mesh(*arrs, oxm)
     if floor:
         fl = miro.TriangleMesh()
         fl.createSingleTriangle()
@@ -88,8 +92,15 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
             textures[id(rgb)] = (tex, O_.add_texture(rgb))
         return textures[id(rgb)]
 
-    def sky(spec):
-        return spec if isinstance(spec, np.ndarray) else scenes.sky_rgb(*spec)
+    skies = {}
+
+    def sky(spec):   # a config sky spec -> one image per spec (HDR files: the oracle's decoder)
+        if isinstance(spec, np.ndarray):
+            return spec
+        key = scenes.sky_key(spec)
+        if key not in skies:
+            skies[key] = scenes.env_image(spec, hdr_loader=O.hdr_load)
+        return skies[key]
 
     for l in lights:
         if l["type"] == "point":
@@ -139,6 +150,8 @@ def config_scene(key, **kw):
     cfg = scenes.CONFIGS[key]
     kw.setdefault("num_paths", cfg.get("num_paths", 1))
     kw.setdefault("subdivs", cfg.get("subdivs"))
+    kw.setdefault("path_trace", cfg.get("path_trace"))
+    kw.setdefault("extra", [(scenes.EXTRA_OBJS[n], m) for n, m in cfg.get("extra", ())])
     if cfg["mesh"] == "cornell":
         return scene_pair(cfg, meshes=[fixture_mesh("cornell_box")], **kw)
     if cfg["mesh"] == "bunny":

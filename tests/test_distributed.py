@@ -176,3 +176,91 @@ def test_camera_path_starts_at_config_camera():
         assert abs(np.linalg.norm(d) - np.linalg.norm(d0)) < 1e-9
         cosang = np.dot(d[[0, 2]], d0[[0, 2]]) / (np.linalg.norm(d[[0, 2]]) * np.linalg.norm(d0[[0, 2]]))
         assert abs(np.degrees(np.arccos(min(1.0, cosang))) - 2.5 * f) < 1e-6
+
+
+def test_padded_items_cover_once_with_minus_one_padding():
+    for n in (1, 7, 60 * 34, 2 * 60 * 34 + 5):
+        for world in (1, 2, 3, 8):
+            if world > n:
+                continue
+            lists = [tiles.padded_items(n, world, r) for r in range(world)]
+            assert {len(x) for x in lists} == {-(-n // world)}
+            real = sorted(i for x in lists for i in x if i >= 0)
+            assert real == list(range(n))
+            for r, x in enumerate(lists):   # padding only at the end, -1 only
+                k = len(tiles.rank_buckets(n, world, r))
+                assert all(i == -1 for i in x[k:]) and all(i >= 0 for i in x[:k])
+
+
+def test_bench_refuses_a_world_size_that_differs_from_gpus():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=3 but --gpus 2" in r.stderr
+
+
+def _libmrt_worker(rank, world, port, key, W, H, result_path):
+    """One rank of a multi-process render on one GPU: this rank's 32x32 buckets
+    (id mod world) through libmrt's batch path, host copies gathered over gloo,
+    rank 0 scatters them with libmrt's unpack kernel."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import ctypes as C
+        import sys
+        here = os.path.dirname(os.path.abspath(__file__))
+        sys.path.insert(0, here)
+        import conftest  # noqa: F401  (paths)
+        import miro
+        from miro import _lib
+        from helpers import config_scene, camera
+        torch.cuda.set_device(0)
+        P, _, cam = config_scene(key)
+        L = miro.lib()
+        bx, by = tiles.bucket_grid(W, H)
+        bpf = bx * by
+        mine = tiles.rank_buckets(bpf, world, rank)
+        per = -(-bpf // world)
+        d_items = torch.tensor(mine, dtype=torch.int32, device="cuda")
+        d_tiles = torch.zeros(per * 1024 * 3, dtype=torch.float32, device="cuda")
+        opts = _lib.mrt_render_opts(W, H, 0, 0, 1, 0, 0)
+        camc = (_lib.mrt_camera * 1)(camera(cam)._c())
+        s = torch.cuda.current_stream().cuda_stream
+        _lib.check(L.mrt_render_batch_async(P.handle, camc, 1, C.byref(opts), d_items.data_ptr(), len(mine),
+                                            d_tiles.data_ptr(), None, s), "render batch")
+        host = d_tiles.cpu()
+        got = [torch.zeros_like(host) for _ in range(world)] if rank == 0 else None
+        dist.gather(host, got, dst=0)
+        if rank == 0:
+            allt = torch.cat(got).cuda()
+            ids = torch.tensor([i for r in range(world) for i in tiles.padded_items(bpf, world, r)], dtype=torch.int32,
+                               device="cuda")
+            frame = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+            _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(ids), allt.data_ptr(), None, W, H, 1,
+                                                frame.data_ptr(), None, P.handle, s), "unpack")
+            np.save(result_path, frame.cpu().numpy().reshape(H, W, 3))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key,world,W,H", [("C3", 2, 200, 120), ("C4", 3, 130, 70), ("C5", 2, 160, 90)])
+def test_libmrt_multi_process_frame_equals_single_process(tmp_path, key, world, W, H):
+    """the N > 1 path on libmrt end to end under a process group --
+    several processes share cuda:0, each renders its buckets through
+    mrt_render_batch_async, gloo gathers, the frame equals one mrt_render."""
+    import miro
+    from helpers import config_scene, camera
+    if miro.device_count() < 1:
+        pytest.skip("no HIP device")
+    path = str(tmp_path / "frame.npy")
+    mp.start_processes(_libmrt_worker, args=(world, _free_port(), key, W, H, path), nprocs=world,
+                       start_method="spawn")
+    frame = np.load(path)
+    P, _, cam = config_scene(key)
+    img = miro.Image(); img.resize(W, H)
+    P.raytraceImage(camera(cam), img)
+    assert np.array_equal(frame.view(np.uint32), img.rgb.view(np.uint32))

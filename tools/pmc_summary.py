@@ -1,16 +1,16 @@
-"""Summarise tools/pmc.sh output (rocprofv3 --pmc CSV passes) per kernel.
-
-Writes a text table (mean counter value per dispatch) and, with --json, the
-per-launch HBM traffic that bench.py reports as roofline.traffic:
+"""Summarise tools/pmc.sh output per config: kernel-trace stats and the HBM
+bytes per launch of each bench pass, for bench.py's roofline.
 
     hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
 
-FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KiB.  On gfx950
+FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KiB; on gfx950
 FETCH_SIZE counts 128-B read requests at 64 B, i.e. half the bytes
-(MI355X_MICROARCH.md, HBM section), hence the factor 2; WRITE_SIZE is exact
-for 16-B-per-lane stores.  Both count L2 -> fabric traffic, so Infinity-Cache
-hits are included: an upper bound on HBM bytes.
-"""
+(MI355X_MICROARCH.md, HBM section), hence the factor 2.  Both count L2 ->
+fabric requests, so Infinity-Cache hits are included: an upper bound on DRAM
+bytes.  Only the timed (uninstrumented, COUNT = false) kernel instantiations
+are used.  Pass mapping: primary = primary_kernel; shade = shade1_kernel, or
+shade_kernel (gen + resolve, or fused chains) + shadow_kernel, or
+adaptive_kernel (one fused launch)."""
 from __future__ import annotations
 
 import argparse
@@ -21,64 +21,87 @@ import os
 import re
 from collections import defaultdict
 
-
-def short(name: str) -> str:
-    name = re.sub(r"\(.*\)$", "", name.strip())
-    name = name.replace("void ", "").replace("mrt::", "")
-    return name
+PASS = {"primary_kernel": "primary", "shade1_kernel": "shade", "shade_kernel": "shade", "shadow_kernel": "shade",
+        "adaptive_kernel": "shade"}
 
 
-def load(root):
-    per = defaultdict(lambda: defaultdict(list))      # kernel -> counter -> [values per dispatch]
+def parse_name(name):
+    """'void mrt::shade_kernel<false, true, ...>(mrt::RenderParams)' -> ('shade_kernel', 'false, true, ...')"""
+    m = re.search(r"mrt::(\w+)<([^>]*)>", name)
+    if not m:
+        m2 = re.search(r"mrt::(\w+)", name)
+        return (m2.group(1) if m2 else name.strip()), ""
+    return m.group(1), m.group(2)
+
+
+def counters(root):
+    per = defaultdict(lambda: defaultdict(list))      # full kernel -> counter -> values per dispatch
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(f, newline="") as fh:
             for row in csv.DictReader(fh):
-                k = short(row.get("Kernel_Name", "?"))
-                per[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                per[row.get("Kernel_Name", "?")][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return per
+
+
+def stats(root):
+    rows = []
+    for f in glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True):
+        with open(f, newline="") as fh:
+            rows += list(csv.DictReader(fh))
+    return rows
+
+
+def summarise(cfg, root):
+    lines = [f"## {cfg}"]
+    tr = stats(os.path.join(root, "trace"))
+    if tr:
+        lines.append("kernel-trace --stats (rocprofv3):")
+        for r in sorted(tr, key=lambda r: -float(r.get("TotalDurationNs", 0))):
+            base, targs = parse_name(r["Name"])
+            lines.append("    %-34s calls %5s  avg %12.1f ns  total %14.1f ns  [%s]" % (
+                base, r.get("Calls"), float(r.get("AverageNs", 0)), float(r.get("TotalDurationNs", 0)), targs))
+    per = counters(root)
+    passes = defaultdict(float)
+    lines.append("PMC (mean per dispatch):")
+    for k in sorted(per):
+        base, targs = parse_name(k)
+        cs = per[k]
+        f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) if cs.get("FETCH_SIZE") else None
+        w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) if cs.get("WRITE_SIZE") else None
+        lines.append("    %-34s FETCH_SIZE %s KiB  WRITE_SIZE %s KiB  [%s]" % (
+            base, "-" if f is None else "%.1f" % f, "-" if w is None else "%.1f" % w, targs))
+        timed = targs.split(",")[0].strip() == "false"
+        if timed and base in PASS and f is not None and w is not None:
+            passes[PASS[base]] += 2 * f * 1024 + w * 1024
+    for p, b in sorted(passes.items()):
+        lines.append("    pass %-8s hbm_bytes_per_launch %16.0f   (2*FETCH_SIZE + WRITE_SIZE)" % (p, b))
+    return lines, {p: int(b) for p, b in passes.items()}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root", nargs="?", default="gpurun_out/pmc")
-    ap.add_argument("--out", default=None)
-    ap.add_argument("--json", default=None)
-    ap.add_argument("--config", default="C3")
+    ap.add_argument("--round", default="r02")
+    ap.add_argument("--json", default="profiles/r02_pmc_traffic.json")
     a = ap.parse_args()
-    per = load(a.root)
-    lines = ["# rocprofv3 --pmc (one counter set per pass), mean value per dispatch",
-             "# workload: python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline (config %s)" % a.config]
-    traffic = {}
-    for k in sorted(per):
-        cs = per[k]
-        lines.append(k)
-        for c in sorted(cs):
-            v = cs[c]
-            lines.append("    %-32s %16.1f   (n=%d)" % (c, sum(v) / len(v), len(v)))
-        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
-            fetch = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
-            write = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
-            hbm = 2 * fetch * 1024 + write * 1024
-            lines.append("    %-32s %16.0f   (2*FETCH_SIZE + WRITE_SIZE, bytes)" % ("hbm_bytes_per_launch", hbm))
-            if "<false" in k:      # uninstrumented (timed) instantiation
-                base = k.split("<")[0]
-                traffic[base] = int(hbm)
-        if "TCC_HIT_sum" in cs and "TCC_MISS_sum" in cs:
-            h = sum(cs["TCC_HIT_sum"]); m = sum(cs["TCC_MISS_sum"])
-            lines.append("    %-32s %16.4f" % ("L2 hit rate", h / max(1.0, h + m)))
-        if "SQ_WAVE_CYCLES" in cs:
-            wc = sum(cs["SQ_WAVE_CYCLES"])
-            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
-                if c in cs:
-                    lines.append("    %-32s %16.4f" % (c + " / WAVE_CYCLES", sum(cs[c]) / max(1.0, wc)))
-    txt = "\n".join(lines) + "\n"
-    print(txt)
-    if a.out:
-        open(a.out, "w").write(txt)
-    if a.json:
-        json.dump({"config": a.config, "per_launch_hbm_bytes": traffic,
-                   "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)",
-                   "source": a.out}, open(a.json, "w"), indent=1)
+    out = json.load(open(a.json)) if os.path.exists(a.json) else {}
+    out.setdefault("configs", {})
+    out.setdefault("source", {})
+    out["formula"] = "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per dispatch (gfx950 FETCH_SIZE half-count correction)"
+    for d in sorted(glob.glob(os.path.join(a.root, "*"))):
+        if not os.path.isdir(d):
+            continue
+        cfg = os.path.basename(d)
+        lines, passes = summarise(cfg, d)
+        txt = "\n".join(lines) + "\n"
+        print(txt)
+        path = f"profiles/{a.round}_{cfg.lower()}_rocprof.txt"
+        open(path, "w").write(f"# rocprofv3 summaries: python3 bench.py --config {cfg} --steps 5 --warmup 1 "
+                              f"--no-cpu-baseline (tools/pmc.sh)\n" + txt)
+        if passes:
+            out["configs"][cfg] = {"per_launch_hbm_bytes": passes}
+            out["source"][cfg] = path
+    json.dump(out, open(a.json, "w"), indent=1)
 
 
 if __name__ == "__main__":
