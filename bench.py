@@ -338,6 +338,17 @@ def main():
         else:
             pipe.step()
 
+    # setup: every in-flight stream renders once, so libmrt's per-stream scratch
+    # (hit records, stacks, counters) is allocated before the warmup / timed steps
+    if use_frame_path:
+        for i in range(inflight):
+            _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(opts), frame[i].data_ptr(),
+                                                frame8[i].data_ptr(), streams[i].cuda_stream), "render")
+    else:
+        for b in range(2):
+            with torch.cuda.stream(pipe.streams[b]):
+                render(items, pipe.tiles[b])
+    torch.cuda.synchronize()
     # instrumented frame: node/leaf visits + per-launch times (not timed below)
     step(opts_count, serial=True)
     torch.cuda.synchronize()
@@ -473,7 +484,8 @@ def main():
         hbm_gbs = dom_traffic / (dom_ms * 1e-3) / 1e9
         hbm = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": int(dom_traffic), "source": pmc_src}
-    lane_util = round(st["primary_node_visits"] / max(1, 64 * st["primary_wave_steps"]), 4)
+    # primary-kernel lanes doing node work per issued wave step (adaptive: no primary launch)
+    lane_util = round(st["primary_node_visits"] / (64 * st["primary_wave_steps"]), 4) if st["primary_wave_steps"] else None
     out = {
         "metric": ("Mray/s (primary+shadow) on Sponza 1920x1080" if args.config == "C3" else
                    f"Mray/s (primary+shadow{'+secondary' if second_total else ''}) [{args.config}: {cfg['name']}]"),
