@@ -142,7 +142,10 @@ typedef struct {
      * tail = spread of wave ends (time the launch runs below full occupancy)   */
     float primary_span_us, primary_ramp_us, primary_tail_us;
     float shade_span_us, shade_ramp_us, shade_tail_us;
-    uint64_t secondary_rays;             /* Blinn reflection / refraction rays traced   */
+    uint64_t secondary_rays;             /* Blinn reflection / refraction / GI rays traced */
+    /* count mode, wavefront shadow_kernel: wave loop steps and node visits (lane
+     * utilisation = shadow_node_visits / (64 * shadow_wave_steps)) */
+    uint64_t shadow_wave_steps, shadow_node_visits;
 } mrt_stats;
 
 const char* mrt_last_error(void);
@@ -318,6 +321,8 @@ int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const floa
 int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
 
 /* Performance A/B switches (no effect on results; defaults in brackets):
+ * "shadow_sched" [-1]..2 (wavefront shadow rays: auto, grid-stride, XCD bands,
+ * bands + lane refill), "refill_min" 1..64 [40] (idle lanes that trigger a refill),
  * "fast_box" 0/[1] (hardware min/max slab test when its finiteness precondition
  * holds), "primary_waves" 0/[6] (occupancy target of the primary-ray kernel),
  * "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands, dynamic

@@ -44,14 +44,16 @@ enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLO
        CTR_TP = 10, CTR_TS = 14,
        CTR_RAYS_P = 18,  // eye rays traced (adaptive supersampling; otherwise one per pixel)
        CTR_SECONDARY = 19,  // Blinn reflection / refraction rays
-       CTR_N = 20 };
+       CTR_WAVE_STEPS_S = 20, CTR_NODES_S = 21,  // count mode, shadow_kernel: wave loop steps, node visits
+       CTR_N = 22 };
 static constexpr int kMaxBlocksPerCU = 8;
 // wave log record: start, end, tiles, node visits, then (tile id << 40 | start tick) of the first kLogTiles
 // tiles, then the wall-clock ticks each of those tiles' dequeue took
 static constexpr int kLogTiles = 28;
 static constexpr int kLogWords = 4 + 2 * kLogTiles;  // 256-thread blocks: 8 waves per SIMD at most
-// counter block: CTR_N u64 statistics, then two launches x 8 tile counters x 128 B
-static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 3 * 8 * 128;
+// counter block: CTR_N u64 statistics, then four launches x 8 work counters x 128 B
+// (primary, shade / gen, resolve, shadow_kernel's per-XCD ray queues)
+static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 4 * 8 * 128;
 // Shadow rays of the general shading path, wavefront style (ShadowMode): kernel
 // 2a runs the shading code and writes every shadow ray to its slot, kernel 2b
 // traces all of them any-hit (few registers, full occupancy), kernel 2c runs the
@@ -1053,11 +1055,25 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
     flush_stats<COUNT, false>(P, st, shadow_total, lane, t0, ntiles);
 }
 
-// Kernel 2b: every wavefront shadow ray of the frame, one lane each, any-hit
-// (the occlusion answer of Shader::occluded).  Slots past a pixel's ray count
-// are skipped.
+// Kernel 2b: every wavefront shadow ray of the frame, any-hit (the occlusion
+// answer of Shader::occluded).  Slots past a pixel's ray count are skipped.
+//   sched 0: grid-stride, one ray per lane per iteration.
+//   sched 1: XCD bands -- the ray slots are cut into 8 contiguous bands (slot
+//            order is pixel order, so a band is a band of the image) and
+//            workgroup b, which runs on XCD b mod 8, takes 64-slot chunks of band
+//            b mod 8 from that band's counter, then steals from the others: the
+//            rays one XCD traces touch the geometry of one image band, so its
+//            4 MB L2 holds that band's share of the hierarchy.
+//   sched 2: sched 1 + lane refill (non-instanced scenes): a lane whose ray is
+//            done (an any-hit ray ends at its first accepted triangle) or whose
+//            slot is empty takes a new slot as soon as `refill_min` lanes of its
+//            wave are idle; traversal runs one node visit per wave step
+//            (anyhit_step), so the wave no longer waits for its longest ray.
+// Every ray is traced with the same visit order and tests as traverse(), so
+// the answers are identical under every schedule.
+static constexpr int kShadowChunk = 64;
 template <bool COUNT, bool FAST, bool INST>
-__global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_rays) {
+__global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_rays, int sched, int refill_min) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     load_tables(P.tables, s_tab, 1024);
@@ -1066,14 +1082,111 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
            P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     TravStats st;
-    const size_t m = (size_t)P.max_shadow;
-    for (size_t e = (size_t)blockIdx.x * kWG + tid; e < n_rays; e += (size_t)gridDim.x * kWG) {
-        const size_t pslot = e / m;
-        if (e - pslot * m >= (size_t)P.nrays[pslot]) continue;
+    unsigned long long wave_steps = 0;
+    // slot e = pixel slot * max_shadow + j (n_rays < 2^32, checked on the host: 32-bit division)
+    const uint32_t m = (uint32_t)P.max_shadow, nr32 = (uint32_t)n_rays;
+    auto valid = [&](size_t e64) {
+        const uint32_t e = (uint32_t)e64, px = e / m;
+        return e64 < n_rays && e < nr32 && e - px * m < (uint32_t)P.nrays[px];
+    };
+    auto trace_one = [&](size_t e) {
         const float4 o = P.ray_o[e], d = P.ray_d[e];
         const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
         DHit h{o.w, 0.f, 0.f, -1};
+        const uint32_t n0 = st.nodes;
         P.occl[e] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
+        return st.nodes - n0;
+    };
+    if (sched == 0) {
+        for (size_t e0 = (size_t)blockIdx.x * kWG + (tid & ~63); e0 < n_rays; e0 += (size_t)gridDim.x * kWG) {
+            const size_t e = e0 + lane;
+            uint32_t v = valid(e) ? trace_one(e) : 0u;
+            if (COUNT) {
+                for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off));
+                wave_steps += v;
+            }
+        }
+    } else {
+        // per-XCD band of ray slots and its chunk counter (own 128-B line)
+        const int home = blockIdx.x & 7;
+        auto band_lo = [&](int k) { return n_rays * (size_t)k / 8; };
+        int band = home, probes = 0;
+        bool exhausted = false;   // wave-uniform
+        // wave-level dequeue of `want` consecutive slots of the current band (or
+        // the next band with slots left); returns the first slot (lane 0's atomic,
+        // broadcast) and the end of its band, or exhausted
+        auto dequeue = [&](uint32_t want, size_t& first, size_t& end) {
+            unsigned long long got = ~0ull, hi = 0;
+            if (lane == 0) {
+                while (probes < 8) {
+                    const size_t lo = band_lo(band), bend = band_lo(band + 1);
+                    const unsigned long long v = atomicAdd(reinterpret_cast<unsigned long long*>(P.queue + band * 32),
+                                                           (unsigned long long)want);
+                    if (lo + v < bend) { got = lo + v; hi = bend; break; }
+                    band = (band + 1) & 7;
+                    probes++;
+                }
+            }
+            got = __shfl(got, 0);
+            hi = __shfl(hi, 0);
+            first = (size_t)got;
+            end = (size_t)hi;
+            return got != ~0ull;
+        };
+        if (INST || sched == 1) {   // wave-uniform chunks, one ray per lane
+            size_t first, end;
+            while (dequeue(kShadowChunk, first, end)) {
+                const size_t e = first + lane;
+                uint32_t v = (e < end && valid(e)) ? trace_one(e) : 0u;
+                if (COUNT) {
+                    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off));
+                    wave_steps += v;
+                }
+            }
+        } else if constexpr (!INST) {   // lane refill
+            bool active = false;
+            size_t e = 0;
+            DRay r{};
+            float tmax = 0.f;
+            int32_t cur = 0;
+            int sp = 0;
+            for (;;) {
+                const unsigned long long idle = __ballot(!active);
+                const int nidle = __popcll(idle);
+                if (!exhausted && (nidle >= refill_min || nidle == 64)) {
+                    size_t first, end;
+                    if (!dequeue((uint32_t)nidle, first, end)) {
+                        exhausted = true;
+                    } else if (!active) {
+                        const size_t c = first + (size_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                        if (c < end && valid(c)) {
+                            e = c;
+                            const float4 o = P.ray_o[e], d = P.ray_d[e];
+                            r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
+                            tmax = o.w;
+                            cur = 0;
+                            sp = 0;
+                            active = true;
+                        }
+                    }
+                }
+                if (__ballot(active) == 0) {
+                    if (exhausted) break;
+                    continue;
+                }
+                if (COUNT) wave_steps++;
+                if (active) {
+                    bool hit = false;
+                    const bool done = (FAST && r.finite) ? anyhit_step<COUNT, true>(T, r, 0.001f, tmax, cur, sp, hit, st)
+                                                         : anyhit_step<COUNT, false>(T, r, 0.001f, tmax, cur, sp, hit, st);
+                    if (done) {
+                        P.occl[e] = hit ? 1 : 0;
+                        active = false;
+                    }
+                }
+            }
+        }
     }
     if (COUNT) {
         unsigned long long nv = st.nodes, lv = st.leaves;
@@ -1084,6 +1197,8 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
         if (lane == 0) {
             atomicAdd(&P.ctr[CTR_NODES], nv);
             atomicAdd(&P.ctr[CTR_LEAVES], lv);
+            atomicAdd(&P.ctr[CTR_NODES_S], nv);
+            atomicAdd(&P.ctr[CTR_WAVE_STEPS_S], wave_steps);
         }
     }
     if (st.overflow) atomicOr(&P.ctr[CTR_OVERFLOW], 1ull);
@@ -1335,6 +1450,9 @@ static int g_wave_log = 0;        // 1: timing-only wave log on uninstrumented l
 static int g_scalar_nodes = 1;    // scalar-cache fetch of wave-uniform nodes
 static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
 static int g_wavefront = 1;       // general shading: gen / trace / resolve kernels instead of one fused kernel
+static int g_shadow_sched = -1;   // shadow_kernel schedule: 0 grid-stride, 1 XCD bands, 2 bands + lane refill,
+                                  // -1 auto: refill for dome-light (incoherent) rays of uninstanced scenes, else bands
+static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
 
 static inline int fast_box(const DeviceState& d);
 
@@ -1712,7 +1830,7 @@ static KernelFn shade_mode_fn(bool c, bool po, bool inst) {   // kGen / kResolve
     if (po) return c ? shade_kernel<true, true, false, false, MODE> : shade_kernel<false, true, false, false, MODE>;
     return c ? shade_kernel<true, false, false, false, MODE> : shade_kernel<false, false, false, false, MODE>;
 }
-using ShadowFn = void (*)(RenderParams, size_t);
+using ShadowFn = void (*)(RenderParams, size_t, int, int);
 static ShadowFn pick_shadow(bool c, bool f, bool inst) {
     if (inst) return c ? (f ? shadow_kernel<true, true, true> : shadow_kernel<true, false, true>)
                        : (f ? shadow_kernel<false, true, true> : shadow_kernel<false, false, true>);
@@ -1828,10 +1946,17 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         P.max_shadow = max_sh;
         if ((rc = launch(shade_mode_fn<kGen>(count, d.point_only, inst)))) return rc;
         const ShadowFn sf = pick_shadow(count, fb, inst);
-        const int g = std::max(1, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(sf), 0)));
+        int g = std::max(1, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(sf), 0)));
+        bool dome = false;
+        for (const DevLight& l : s.lights) dome |= l.type == MRT_DOME_LIGHT;
+        int sched = g_shadow_sched >= 0 ? g_shadow_sched : (dome && !inst ? 2 : 1), refill = g_refill_min;
+        if (sched && (g & 7)) g &= ~7;          // XCD bands need a whole number of workgroups per XCD
+        if (g < 8) sched = 0;
         size_t n_rays = slots * (size_t)max_sh;
-        void* args[] = {&P, &n_rays};
+        if (n_rays >= (size_t(1) << 32)) { set_error("too many wavefront shadow-ray slots (2^32)"); return MRT_ERR_INVALID; }
+        void* args[] = {&P, &n_rays, &sched, &refill};
         P.wave_log = nullptr;
+        P.queue = qbase + 24 * 32;
         HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(sf), dim3(g), dim3(kWG), args, 0, stream));
         P.queue = qbase + 16 * 32;
         if ((rc = launch(shade_mode_fn<kResolve>(count, d.point_only, inst)))) return rc;
@@ -2576,6 +2701,8 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     S.last.node_visits = c[CTR_NODES];
     S.last.leaf_visits = c[CTR_LEAVES];
     S.last.max_stack = (int32_t)c[CTR_MAXSP];
+    S.last.shadow_wave_steps = c[CTR_WAVE_STEPS_S];
+    S.last.shadow_node_visits = c[CTR_NODES_S];
     if (x.last_was_render && c[CTR_TP + 3]) {   // count mode: wave ramp / tail (wall clock)
         const double us = d.wall_khz > 0 ? 1e3 / d.wall_khz : 0.0;
         for (int k = 0; k < 2; k++) {
@@ -2699,6 +2826,12 @@ int mrt_set_tuning(const char* key, int value) {
         g_shade1 = value ? 1 : 0;
     } else if (k == "wavefront") {
         g_wavefront = value ? 1 : 0;
+    } else if (k == "shadow_sched") {
+        if (value < -1 || value > 2) { set_error("shadow_sched must be -1..2"); return MRT_ERR_INVALID; }
+        g_shadow_sched = value;
+    } else if (k == "refill_min") {
+        if (value < 1 || value > 64) { set_error("refill_min must be 1..64"); return MRT_ERR_INVALID; }
+        g_refill_min = value;
     } else if (k == "sched") {
         if (value < 0 || value > 3) { set_error("sched must be 0..3"); return MRT_ERR_INVALID; }
         g_sched = value;

@@ -406,6 +406,86 @@ __device__ bool traverse_pf(const Trav& c, const DRay& r, float tMin, DHit& h, T
     return hit;
 }
 
+// One node visit of an any-hit traversal, resumable (traverse_impl's loop body
+// for ANY, no instancing): the caller keeps cur / sp between calls, so a lane
+// can drop a finished ray and start another while its wave keeps going (lane
+// refill in shadow_kernel).  The visit order and every test are traverse_impl's.
+// Returns true when the ray is done: `hit` = a triangle was accepted; otherwise
+// the stack ran empty (miss) or overflowed (st.overflow).
+template <bool COUNT, bool FAST>
+__device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float tMin, float tMax, int32_t& cur,
+                                            int& sp, bool& hit, TravStats& st) {
+    int m;
+    int4 ch;
+    const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
+    if (FAST && c.scalar_nodes && __ballot(cur != c0) == 0) {   // wave-uniform node: scalar fetch
+        typedef const __attribute__((address_space(4))) float cfloat;
+        typedef const __attribute__((address_space(4))) int32_t cint;
+        cfloat* q = (cfloat*)(const void*)(c.nodes + c0);
+        cint* qc = (cint*)(q + 24);
+        ch = make_int4(qc[0], qc[1], qc[2], qc[3]);
+        float4 bx[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
+        m = box_test_fast(bx, r, tMin, tMax);
+    } else {
+        const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
+        ch = reinterpret_cast<const int4*>(q)[6];
+        m = FAST ? box_test_fast(q, r, tMin, tMax) : box_test(q, r, tMin, tMax);
+    }
+    if (COUNT) st.nodes++;
+    const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
+    const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
+                       (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
+    const int inner = m & isinner;
+    int lm = m & isleaf;
+    bool have_next = false;
+    int32_t nxt = 0;
+    if (inner) {
+        const int top = 31 - __builtin_clz((unsigned)inner);
+        const int rest = inner ^ (1 << top);
+        if (rest) {
+            if (sp + 4 <= kLdsStack) {
+                c.lds[sp * kWG] = ch.x; sp += rest & 1;
+                c.lds[sp * kWG] = ch.y; sp += (rest >> 1) & 1;
+                c.lds[sp * kWG] = ch.z; sp += (rest >> 2) & 1;
+                c.lds[sp * kWG] = ch.w; sp += (rest >> 3) & 1;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if ((rest >> i) & 1)
+                        if (!stk_push(c, sp, sel4(ch, i))) { st.overflow = true; return true; }
+            }
+            if (COUNT && sp > st.max_sp) st.max_sp = sp;
+        }
+        nxt = sel4(ch, top);
+        have_next = true;
+    }
+    if (lm) {
+        uint32_t leaf = 0;
+        int k = 0, cnt = 0;
+        while (true) {
+            if (k == cnt) {
+                if (!lm) break;
+                const int s = __builtin_ctz((unsigned)lm);
+                lm &= lm - 1;
+                const uint32_t v = ~(uint32_t)sel4(ch, s);
+                leaf = v >> 3;
+                cnt = (int)(v & 3u) + 1;
+                k = 0;
+                if (COUNT) st.leaves++;
+            }
+            float t, a, b;
+            if (tri_test(c.leaves[leaf].tri[k], r, tMin, tMax, t, a, b, c.rcpT)) { hit = true; return true; }
+            k++;
+        }
+    }
+    if (have_next) { cur = nxt; return false; }
+    if (sp == 0) return true;
+    cur = stk_pop(c, sp);
+    return false;
+}
+
 // FAST (node boxes known finite) uses the hardware min/max slab test for rays
 // whose origin and 1/d are finite; any other ray takes the exact loop.  A
 // closest hit's packed slot is resolved to the global prim id here.

@@ -56,7 +56,8 @@ def main():
         _, _, st = run(v, count=True, reps=1)
         print("variant", v, "counts", {k: st[k] for k in ("node_visits", "leaf_visits", "primary_node_visits",
                                                           "max_stack", "shadow_rays", "primary_hits", "primary_uniform_visits")},
-              "primary SIMD util %.3f" % (st["primary_node_visits"] / max(1, 64 * st["primary_wave_steps"])), flush=True)
+              "primary SIMD util %.3f" % (st["primary_node_visits"] / max(1, 64 * st["primary_wave_steps"])),
+              "shadow SIMD util %.3f" % (st["shadow_node_visits"] / max(1, 64 * st["shadow_wave_steps"])), flush=True)
     for r in range(rounds):
         for v in variants:
             pm, sm, _ = run(v)
