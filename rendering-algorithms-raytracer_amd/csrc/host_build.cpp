@@ -20,7 +20,16 @@
 
 #include <algorithm>
 #include <chrono>
+#include <sched.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
 #include <climits>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <string>
 
@@ -273,45 +282,178 @@ struct BNode {
     bool leaf = false;
 };
 
+// Worker threads for the host build: MRT_BUILD_THREADS, else the affinity
+// mask capped by OMP_NUM_THREADS (the GPU box's CPU share), at most 64.
+int build_threads() {
+    if (const char* e = getenv("MRT_BUILD_THREADS")) {
+        const int v = atoi(e);
+        if (v >= 1) return std::min(v, 64);
+    }
+    int n = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (const char* e = getenv("OMP_NUM_THREADS")) {
+        const int v = atoi(e);
+        if (v >= 1) n = std::min(n, v);
+    }
+    return std::max(1, std::min(n, 64));
+}
+
+// Fork-join pool of the host build: run() queues a task under a ticket,
+// wait() runs queued tasks until that ticket is done (so nested fork-join never
+// blocks a thread).  Workers take the oldest (largest) tasks, a waiting thread
+// the newest.
+class Pool {
+   public:
+    struct Ticket {
+        std::atomic<bool> done{false};
+    };
+    explicit Pool(int n) {
+        for (int i = 1; i < n; i++) workers_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& w : workers_) w.join();
+    }
+    int size() const { return (int)workers_.size() + 1; }
+    void run(Ticket* t, std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(Item{t, std::move(f)});
+        }
+        cv_.notify_one();
+    }
+    void wait(Ticket* t) {
+        while (!t->done.load(std::memory_order_acquire)) {
+            Item it;
+            bool got = false;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (!q_.empty()) { it = std::move(q_.back()); q_.pop_back(); got = true; }
+            }
+            if (got) exec(it);
+            else std::this_thread::yield();
+        }
+    }
+
+   private:
+    struct Item {
+        Ticket* t = nullptr;
+        std::function<void()> f;
+    };
+    static void exec(Item& it) {
+        it.f();
+        it.t->done.store(true, std::memory_order_release);
+    }
+    void loop() {
+        for (;;) {
+            Item it;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;
+                it = std::move(q_.front());
+                q_.pop_front();
+            }
+            exec(it);
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::deque<Item> q_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool stop_ = false;
+};
+
+// The binned-SAH build, task-parallel with results independent of the thread
+// count: a node's two subtrees only read and write their own object ranges, so
+// they are built as concurrent tasks (binary-node slots come from an atomic
+// arena; the 4-wide collapse numbers nodes and leaves by its own preorder walk,
+// so arena order does not matter); the per-node passes over many objects
+// (bounds, centroid bounds, bin boxes and counts, bin ids) are split across
+// threads with exact reductions (min / max / integer sums); the loose in-place
+// partition stays sequential, as its quirk depends on the visit order.
 class Builder {
    public:
     // objects (om_[o], ot_[o]) or, where (*oi_)[o] >= 0, ProxyObject (*oi_)[o];
     // the hierarchy goes to nodes / leaves
     Builder(const Scene& s, const std::vector<int32_t>& om, const std::vector<int32_t>& ot,
-            const std::vector<int32_t>* oi, std::vector<QNode>& nodes, std::vector<QLeaf>& leaves)
-        : s_(s), om_(om), ot_(ot), oi_(oi), nodes_(nodes), leaves_(leaves) {}
+            const std::vector<int32_t>* oi, std::vector<QNode>& nodes, std::vector<QLeaf>& leaves, int threads)
+        : s_(s), om_(om), ot_(ot), oi_(oi), nodes_(nodes), leaves_(leaves), threads_(std::max(1, threads)) {}
 
     int run(std::string& err) {
         const int n = (int)om_.size();
+        std::unique_ptr<Pool> pool;
+        if (threads_ > 1 && n >= kTaskMin) pool.reset(new Pool(threads_));
+        pool_ = pool.get();
         tri_box_.resize(n);
         cen_obj_.resize((size_t)3 * n);
-        for (int i = 0; i < n; i++) {
-            tri_box_[i] = tri_aabb(i);
-            for (int k = 0; k < 3; k++) cen_obj_[3 * i + k] = (tri_box_[i].mn[k] + tri_box_[i].mx[k]) * 0.5f;
-        }
         objs_.resize(n);
         pre_.resize(n);
         cen_.resize((size_t)3 * n);
         bin_ids_.resize(n);
-        for (int i = 0; i < n; i++) {
-            objs_[i] = i;
-            pre_[i] = tri_box_[i];
-            for (int k = 0; k < 3; k++) cen_[3 * i + k] = cen_obj_[3 * i + k];
-        }
-        bn_.reserve((size_t)2 * n + 2);
-        bn_.emplace_back();
-        build_bin(0, 0, n);
+        par_for(n, [&](int lo, int hi, int) {
+            for (int i = lo; i < hi; i++) {
+                tri_box_[i] = tri_aabb(i);
+                for (int k = 0; k < 3; k++) cen_obj_[3 * i + k] = (tri_box_[i].mn[k] + tri_box_[i].mx[k]) * 0.5f;
+                objs_[i] = i;
+                pre_[i] = tri_box_[i];
+                for (int k = 0; k < 3; k++) cen_[3 * i + k] = cen_obj_[3 * i + k];
+            }
+        }, true);
+        const auto t0 = std::chrono::steady_clock::now();
+        bn_.resize((size_t)2 * n + 2);
+        bn_next_ = 1;
+        build_bin(0, 0, n, 0);
         if (fail_) {
             err = fail_msg_;
             return MRT_ERR_BUILD;
         }
+        const auto t1 = std::chrono::steady_clock::now();
+        bn_.resize((size_t)bn_next_.load());
+        bin_leaves = bin_leaves_.load();
+        bin_depth = bin_depth_.load();
         collapse();
+        if (getenv("MRT_BUILD_TRACE")) {
+            const auto t2 = std::chrono::steady_clock::now();
+            fprintf(stderr, "[mrt build] %d objects, %d threads: binary %.1f ms, collapse %.1f ms\n", n, threads_,
+                    std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                    std::chrono::duration<double, std::milli>(t2 - t1).count());
+        }
         return MRT_OK;
     }
 
     int bin_leaves = 0, bin_depth = 0, q_depth = 0;
 
    private:
+    // objects in a node before its passes are split across threads (the
+    // reference's loose partition makes very uneven splits -- 1.09 M -> 2 k + 1.09 M
+    // at the buddha root -- so a long chain of large nodes is the critical path)
+    static constexpr int kParMin = 1 << 14;
+    static constexpr int kTaskMin = 1 << 11;   // objects in a subtree before it becomes its own task
+
+    // fn(lo, hi, chunk) over [0, n) in contiguous chunks, in parallel when n is
+    // large and threads are free; chunk c covers [c*n/T, (c+1)*n/T)
+    template <typename F>
+    int par_for(int n, F fn, bool force = false) {
+        int T = 1;
+        if (pool_ && (n >= kParMin || (force && n >= 4096))) T = std::min(std::min(threads_, 64), std::max(1, n / 2048));
+        if (T <= 1) {
+            fn(0, n, 0);
+            return 1;
+        }
+        std::vector<Pool::Ticket> tk(T);
+        for (int c = 1; c < T; c++)
+            pool_->run(&tk[c], [&, c] { fn((int)((int64_t)n * c / T), (int)((int64_t)n * (c + 1) / T), c); });
+        fn(0, (int)((int64_t)n / T), 0);
+        for (int c = 1; c < T; c++) pool_->wait(&tk[c]);
+        return T;
+    }
+
     bool is_proxy(int o) const { return oi_ && (*oi_)[o] >= 0; }
     // TriangleMesh::getAABB (src/TriangleMesh.cpp:156-195) / ProxyObject::getAABB
     Box tri_aabb(int o) const {
@@ -335,20 +477,28 @@ class Builder {
     }
 
     // BVH_Node::buildBin, src/BVH.cpp:625-689
-    void build_bin(int node, int start, int n) {
+    void build_bin(int node, int start, int n, int depth) {
         if (fail_) return;
         Box b = empty_box();
-        for (int i = 0; i < n; i++) b = merge(b, tri_box_[objs_[start + i]]);
+        {   // the node box: std::min / std::max merges are exact, so chunked partial boxes merge to the same box
+            Box part[64];
+            const int T = par_for(n, [&](int lo, int hi, int c) {
+                Box q = empty_box();
+                for (int i = lo; i < hi; i++) q = merge(q, tri_box_[objs_[start + i]]);
+                part[c] = q;
+            });
+            for (int c = 0; c < T; c++) b = merge(b, part[c]);
+        }
         bn_[node].box = b;
         if (n <= 4) {
             bn_[node].leaf = true;
             bn_[node].start = start;
             bn_[node].count = n;
-            bin_leaves++;
+            bin_leaves_++;
             return;
         }
-        depth_++;
-        bin_depth = std::max(bin_depth, depth_);
+        int d = bin_depth_.load();
+        while (depth + 1 > d && !bin_depth_.compare_exchange_weak(d, depth + 1)) {}
         unsigned part = 0;
         partition(start, n, part);
         if (fail_) return;
@@ -357,13 +507,18 @@ class Builder {
             fail("BVH partition produced an empty side (reference would recurse forever)");
             return;
         }
-        int32_t l = (int32_t)bn_.size();
-        bn_.emplace_back();
-        bn_.emplace_back();
+        const int32_t l = bn_next_.fetch_add(2);
         bn_[node].left = l;
-        build_bin(l, start, (int)ln);
-        build_bin(l + 1, start + (int)ln, (int)rn);
-        depth_--;
+        // the left subtree as a task of its own while a thread is free
+        if (pool_ && (int)ln >= kTaskMin) {
+            Pool::Ticket t;
+            pool_->run(&t, [=] { build_bin(l, start, (int)ln, depth + 1); });
+            build_bin(l + 1, start + (int)ln, (int)rn, depth + 1);
+            pool_->wait(&t);
+        } else {
+            build_bin(l, start, (int)ln, depth + 1);
+            build_bin(l + 1, start + (int)ln, (int)rn, depth + 1);
+        }
     }
 
     // BVH_Node::partitionSweepBin, src/BVH.cpp:691-901
@@ -376,11 +531,23 @@ class Builder {
         float* cen = cen_.data() + 3 * (size_t)start;
         if (n >= 128) {
             Box bb = empty_box();
-            for (int i = 0; i < n; i++)
-                for (int k = 0; k < 3; k++) {
-                    bb.mn[k] = std_min(bb.mn[k], cen[3 * i + k]);
-                    bb.mx[k] = std_max(bb.mx[k], cen[3 * i + k]);
-                }
+            {
+                Box part[64];
+                const int T = par_for(n, [&](int lo, int hi, int c) {
+                    Box q = empty_box();
+                    for (int i = lo; i < hi; i++)
+                        for (int k = 0; k < 3; k++) {
+                            q.mn[k] = std_min(q.mn[k], cen[3 * i + k]);
+                            q.mx[k] = std_max(q.mx[k], cen[3 * i + k]);
+                        }
+                    part[c] = q;
+                });
+                for (int c = 0; c < T; c++)
+                    for (int k = 0; k < 3; k++) {
+                        bb.mn[k] = std_min(bb.mn[k], part[c].mn[k]);
+                        bb.mx[k] = std_max(bb.mx[k], part[c].mx[k]);
+                    }
+            }
             float len[3] = {bb.mx[0] - bb.mn[0], bb.mx[1] - bb.mn[1], bb.mx[2] - bb.mn[2]};
             bool any = false;
             for (int axis = 0; axis < 3; axis++) {
@@ -391,11 +558,25 @@ class Builder {
                 Box bins[8];
                 int cnt[8] = {0};
                 for (int i = 0; i < 8; i++) bins[i] = empty_box();
-                for (int i = 0; i < n; i++) {
-                    int id = trunc_x86(kl * (cen[3 * i + axis] - ko));
-                    if (id < 0 || id > 7) { fail("bin id out of range"); return; }
-                    bins[id] = merge(bins[id], pre[i]);
-                    cnt[id]++;
+                {
+                    Box pb[64][8];
+                    int pc[64][8];
+                    std::atomic<bool> bad{false};
+                    const int T = par_for(n, [&](int lo, int hi, int c) {
+                        Box lb[8];   // this chunk's bins, local: published once (no shared lines in the loop)
+                        int lc[8] = {0};
+                        for (int j = 0; j < 8; j++) lb[j] = empty_box();
+                        for (int i = lo; i < hi; i++) {
+                            int id = trunc_x86(kl * (cen[3 * i + axis] - ko));
+                            if (id < 0 || id > 7) { bad = true; return; }
+                            lb[id] = merge(lb[id], pre[i]);
+                            lc[id]++;
+                        }
+                        for (int j = 0; j < 8; j++) { pb[c][j] = lb[j]; pc[c][j] = lc[j]; }
+                    });
+                    if (bad) { fail("bin id out of range"); return; }
+                    for (int c = 0; c < T; c++)
+                        for (int j = 0; j < 8; j++) { bins[j] = merge(bins[j], pb[c][j]); cnt[j] += pc[c][j]; }
                 }
                 float la[8], ra[8];
                 Box acc = empty_box();
@@ -412,9 +593,12 @@ class Builder {
             }
             if (!any) { partPt = (unsigned)(n / 2 - 1); return; }
             float kl = (float)8 * (1.0f - 0.001f) / len[bestAxis], ko = bb.mn[bestAxis];
-            int* ids = bin_ids_.data();
-            for (int i = 0; i < n; i++) ids[i] = trunc_x86(kl * (cen[3 * i + bestAxis] - ko));
+            int* ids = bin_ids_.data() + start;   // this node's own range of the scratch
+            par_for(n, [&](int lo, int hi, int) {
+                for (int i = lo; i < hi; i++) ids[i] = trunc_x86(kl * (cen[3 * i + bestAxis] - ko));
+            });
             // Loose in-place partition, src/BVH.cpp:769-792 (ids are NOT swapped).
+            if (pool_ && n >= kParMin) { loose_partition_par(start, n, ids, binPart, partPt); return; }
             int rev = n - 1;
             for (int i = 0; i < n; i++) {
                 if (ids[i] < binPart) continue;
@@ -446,13 +630,71 @@ class Builder {
         if (bestAxis < 2) sort_by_axis(start, n, (int)bestAxis);
     }
 
+    // The loose partition in parallel.  The ids are never swapped, so the
+    // reference's sweep is fixed by the static id array: the k-th position with
+    // id >= binPart from the left (B_k) swaps objects with the k-th position
+    // with id < binPart from the right (S_k) while S_k > B_k; the sweep stops
+    // at the first B_K without such a partner (S_K <= B_K, or none left) with
+    // partPt = B_K - 1, and leaves partPt as it was when no B_K is left.  The
+    // pairs are disjoint, so the swaps run in parallel.
+    void loose_partition_par(int start, int n, const int* ids, int binPart, unsigned& partPt) {
+        int* objs = objs_.data() + start;
+        Box* pre = pre_.data() + start;
+        float* cen = cen_.data() + 3 * (size_t)start;
+        const int T = std::min(threads_, 64);
+        std::vector<int> nb(T + 1, 0), ns(T + 1, 0);
+        auto lo_of = [&](int c) { return (int)((int64_t)n * c / T); };
+        std::vector<Pool::Ticket> tk(T);
+        auto each = [&](auto fn) {
+            for (int c = 1; c < T; c++) pool_->run(&tk[c], [&, c] { fn(c); });
+            fn(0);
+            for (int c = 1; c < T; c++) { pool_->wait(&tk[c]); tk[c].done = false; }
+        };
+        each([&](int c) {
+            int b = 0;
+            for (int i = lo_of(c); i < lo_of(c + 1); i++) b += ids[i] >= binPart;
+            nb[c + 1] = b;
+            ns[c + 1] = (lo_of(c + 1) - lo_of(c)) - b;
+        });
+        for (int c = 0; c < T; c++) { nb[c + 1] += nb[c]; ns[c + 1] += ns[c]; }
+        const int NB = nb[T], NS = ns[T];
+        std::vector<int> B(NB), S(NS);   // B ascending; S descending (k-th small from the right)
+        each([&](int c) {
+            int b = nb[c], sm = NS - 1 - ns[c];
+            for (int i = lo_of(c); i < lo_of(c + 1); i++) {
+                if (ids[i] >= binPart) B[b++] = i;
+                else S[sm--] = i;
+            }
+        });
+        int lo = 0, hi = std::min(NB, NS);   // K = first k with S_k <= B_k (monotone in k)
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (S[mid] <= B[mid]) hi = mid; else lo = mid + 1;
+        }
+        const int K = lo;
+        each([&](int c) {
+            const int k0 = (int)((int64_t)K * c / T), k1 = (int)((int64_t)K * (c + 1) / T);
+            for (int k = k0; k < k1; k++) {
+                const int i = B[k], r = S[k];
+                std::swap(pre[i], pre[r]);
+                for (int a = 0; a < 3; a++) std::swap(cen[3 * i + a], cen[3 * r + a]);
+                std::swap(objs[i], objs[r]);
+            }
+        });
+        if (K < NB) partPt = (unsigned)(B[K] - 1);
+    }
+
     // QBVH_Node::build, src/BVH.cpp:100-389 -- preorder node numbering, leaf
-    // packets numbered in creation order (nodeNum).
-    int32_t new_node() {
+    // packets numbered in creation order (nodeNum).  Two passes so subtrees can
+    // be built in parallel into their own index ranges: count() gives every
+    // binary node that roots a 4-wide node the size of its 4-wide subtree, then
+    // qbuild() fills node qi from binary node b with the children in the
+    // reference's slot order, handing each child subtree the index ranges a
+    // sequential preorder walk would give it.
+    void init_node(int32_t qi) {
         QNode q{};
         for (int k = 0; k < 4; k++) q.child[k] = kEmptySlot;
-        nodes_.push_back(q);
-        return (int32_t)nodes_.size() - 1;
+        nodes_[qi] = q;
     }
     void set_box(int32_t qi, int slot, int32_t b) {
         const Box& x = bn_[b].box;
@@ -462,7 +704,7 @@ class Builder {
     }
     // buildTriBundle, src/BVH.cpp:64-98: a ProxyObject lane keeps a zero
     // triangle (checkOut lane, rejected by det = 0)
-    int32_t make_leaf(int32_t b) {
+    void make_leaf(int32_t li, int32_t b) {
         QLeaf L{};
         for (int i = 0; i < 4; i++) L.prim[i] = -1;
         for (int i = 0; i < bn_[b].count; i++) {
@@ -475,65 +717,91 @@ class Builder {
             L.t[0 + i] = A.x; L.t[4 + i] = A.y; L.t[8 + i] = A.z;
             L.t[12 + i] = B.x - A.x; L.t[16 + i] = B.y - A.y; L.t[20 + i] = B.z - A.z;
             L.t[24 + i] = C.x - A.x; L.t[28 + i] = C.y - A.y; L.t[32 + i] = C.z - A.z;
-            L.prim[i] = o;
         }
-        leaves_.push_back(L);
-        return ~(int32_t)(leaves_.size() - 1);
+        leaves_[li] = L;
     }
-    // slot <- binary node b: leaf packet now, or a new 4-wide node built recursively
-    void fill(int32_t qi, int slot, int32_t b, int depth) {
-        if (bn_[b].leaf) {
-            int32_t c = make_leaf(b);
-            nodes_[qi].child[slot] = c;
-        } else {
-            int32_t c = new_node();
-            nodes_[qi].child[slot] = c;
-            qbuild(c, b, depth + 1);
-        }
-    }
-    void qbuild(int32_t qi, int32_t b, int depth) {
-        q_depth = std::max(q_depth, depth);
+    // slot assignment of a 4-wide node built from binary node b: (slot, binary
+    // node) in the order the reference fills them; returns the count
+    int slots(int32_t b, int32_t (&sl)[4], int32_t (&bb)[4]) const {
         const BNode& n = bn_[b];
-        if (n.leaf) {  // only the root can be a leaf
-            set_box(qi, 0, b);
-            fill(qi, 0, b, depth);
-            return;
-        }
+        if (n.leaf) { sl[0] = 0; bb[0] = b; return 1; }   // only the root can be a leaf
         const int32_t c0 = n.left, c1 = n.left + 1;
         const bool l0 = bn_[c0].leaf, l1 = bn_[c1].leaf;
-        if (l0 && l1) {
-            set_box(qi, 0, c0);
-            set_box(qi, 1, c1);
-            fill(qi, 0, c0, depth);
-            fill(qi, 1, c1, depth);
-        } else if (l0) {  // leaf, then child 1's two children in slots 1, 2
-            const int32_t g0 = bn_[c1].left, g1 = g0 + 1;
-            set_box(qi, 0, c0); set_box(qi, 1, g0); set_box(qi, 2, g1);
-            fill(qi, 0, c0, depth);
-            fill(qi, 1, g0, depth);
-            fill(qi, 2, g1, depth);
-        } else if (l1) {  // child 0's two children in slots 0, 1, leaf in slot 2 (leaf first)
-            const int32_t g0 = bn_[c0].left, g1 = g0 + 1;
-            set_box(qi, 0, g0); set_box(qi, 1, g1); set_box(qi, 2, c1);
-            fill(qi, 2, c1, depth);
-            fill(qi, 0, g0, depth);
-            fill(qi, 1, g1, depth);
-        } else {
-            const int32_t g[4] = {bn_[c0].left, bn_[c0].left + 1, bn_[c1].left, bn_[c1].left + 1};
-            for (int k = 0; k < 4; k++) set_box(qi, k, g[k]);
-            for (int k = 0; k < 4; k++) fill(qi, k, g[k], depth);
+        if (l0 && l1) { sl[0] = 0; bb[0] = c0; sl[1] = 1; bb[1] = c1; return 2; }
+        if (l0) {   // leaf, then child 1's two children in slots 1, 2
+            const int32_t g0 = bn_[c1].left;
+            sl[0] = 0; bb[0] = c0; sl[1] = 1; bb[1] = g0; sl[2] = 2; bb[2] = g0 + 1;
+            return 3;
         }
+        if (l1) {   // child 0's two children in slots 0, 1, leaf in slot 2 -- the leaf is filled first
+            const int32_t g0 = bn_[c0].left;
+            sl[0] = 2; bb[0] = c1; sl[1] = 0; bb[1] = g0; sl[2] = 1; bb[2] = g0 + 1;
+            return 3;
+        }
+        const int32_t g[4] = {bn_[c0].left, bn_[c0].left + 1, bn_[c1].left, bn_[c1].left + 1};
+        for (int k = 0; k < 4; k++) { sl[k] = k; bb[k] = g[k]; }
+        return 4;
+    }
+    // pass 1: 4-wide nodes / leaf packets of the subtree of binary node b (b roots a 4-wide node)
+    void count(int32_t b, int depth) {
+        int32_t sl[4], bb[4];
+        const int k = slots(b, sl, bb);
+        Pool::Ticket tk[4];
+        bool spawned[4] = {false, false, false, false};
+        for (int i = 0; i < k; i++) {
+            if (bn_[bb[i]].leaf) continue;
+            if (pool_ && depth < 5) { spawned[i] = true; pool_->run(&tk[i], [=] { count(bb[i], depth + 1); }); }
+            else count(bb[i], depth + 1);
+        }
+        int32_t nn = 1, nl = 0;
+        for (int i = 0; i < k; i++) {
+            if (bn_[bb[i]].leaf) { nl++; continue; }
+            if (spawned[i]) pool_->wait(&tk[i]);
+            nn += qn_[bb[i]];
+            nl += ql_[bb[i]];
+        }
+        qn_[b] = nn;
+        ql_[b] = nl;
+    }
+    // pass 2: node qi from binary node b; its child nodes start at index nb, leaves at lb
+    void qbuild(int32_t qi, int32_t b, int depth, int32_t nb, int32_t lb) {
+        int d = q_depth_.load();
+        while (depth > d && !q_depth_.compare_exchange_weak(d, depth)) {}
+        init_node(qi);
+        int32_t sl[4], bb[4];
+        const int k = slots(b, sl, bb);
+        for (int i = 0; i < k; i++) set_box(qi, sl[i], bb[i]);
+        Pool::Ticket tk[4];
+        bool spawned[4] = {false, false, false, false};
+        for (int i = 0; i < k; i++) {
+            const int32_t g = bb[i];
+            if (bn_[g].leaf) {
+                nodes_[qi].child[sl[i]] = ~lb;
+                make_leaf(lb++, g);
+                continue;
+            }
+            const int32_t c = nb, cn = nb + 1, cl = lb;
+            nodes_[qi].child[sl[i]] = c;
+            nb += qn_[g];
+            lb += ql_[g];
+            if (pool_ && depth < 6) { spawned[i] = true; pool_->run(&tk[i], [=] { qbuild(c, g, depth + 1, cn, cl); }); }
+            else qbuild(c, g, depth + 1, cn, cl);
+        }
+        for (int i = 0; i < k; i++)
+            if (spawned[i]) pool_->wait(&tk[i]);
     }
     void collapse() {
-        nodes_.clear();
-        leaves_.clear();
-        nodes_.reserve(bn_.size() / 4 + 4);
-        leaves_.reserve((size_t)bin_leaves);
-        int32_t root = new_node();
-        qbuild(root, 0, 1);
+        qn_.assign(bn_.size(), 0);
+        ql_.assign(bn_.size(), 0);
+        count(0, 0);
+        nodes_.resize((size_t)qn_[0]);
+        leaves_.resize((size_t)ql_[0]);
+        qbuild(0, 0, 1, 1, 0);
+        q_depth = q_depth_.load();
     }
 
     void fail(const char* m) {
+        std::lock_guard<std::mutex> g(fail_mu_);
         if (!fail_) fail_msg_ = m;
         fail_ = true;
     }
@@ -544,12 +812,17 @@ class Builder {
     const std::vector<int32_t>* oi_;
     std::vector<QNode>& nodes_;
     std::vector<QLeaf>& leaves_;
+    const int threads_;
     std::vector<Box> tri_box_, pre_;
     std::vector<float> cen_obj_, cen_;
     std::vector<int> objs_, bin_ids_;
     std::vector<BNode> bn_;
-    int depth_ = 0;
-    bool fail_ = false;
+    std::atomic<int32_t> bn_next_{1};
+    std::atomic<int> bin_leaves_{0}, bin_depth_{0}, q_depth_{0};
+    Pool* pool_ = nullptr;
+    std::vector<int32_t> qn_, ql_;   // collapse: QBVH nodes / leaf packets of the 4-wide subtree rooted at a binary node
+    std::atomic<bool> fail_{false};
+    std::mutex fail_mu_;
     std::string fail_msg_;
 
    public:
@@ -596,7 +869,7 @@ int build_qbvh(Scene& s, std::string& err) {
         err = "world objects + instances x BLAS objects exceed 2^31 hit ids (" + std::to_string(base) + ")";
         return MRT_ERR_INVALID;
     }
-    Builder b(s, s.obj_mesh, s.obj_tri, &s.obj_inst, s.nodes, s.leaves);
+    Builder b(s, s.obj_mesh, s.obj_tri, &s.obj_inst, s.nodes, s.leaves, build_threads());
     int rc = b.run(err);
     if (rc != MRT_OK) return rc;
     auto t1 = std::chrono::steady_clock::now();
@@ -629,7 +902,7 @@ int make_blas(Scene& s, const int32_t* meshes, int n_meshes, std::string& err) {
         }
     }
     if (B.obj_mesh.empty()) { err = "BLAS has no triangles"; return MRT_ERR_BUILD; }
-    Builder b(s, B.obj_mesh, B.obj_tri, nullptr, B.nodes, B.leaves);
+    Builder b(s, B.obj_mesh, B.obj_tri, nullptr, B.nodes, B.leaves, build_threads());
     const int rc = b.run(err);
     if (rc != MRT_OK) return rc;
     const int32_t id = (int32_t)s.blas.size();

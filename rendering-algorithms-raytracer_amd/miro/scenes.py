@@ -281,6 +281,12 @@ def buddha_standin(nu=500, nv=250):
     return _jitter(V, 1993, 1e-4), F, N
 
 
+def buddha_full_standin():
+    """buddha_standin at the size of buddha_smooth.obj (1,087,716 tris): 1,090,980
+    triangles -- the host-build throughput case."""
+    return buddha_standin(nu=1045, nv=523)
+
+
 def instance_transforms(n=64, grid=8, spacing=3.2, seed=64):
     """Row-major 4x4 ProxyObject transforms of config C5: an n = grid x grid
     layout, seeded rotation about y, uniform scale 0.8-1.2 and jitter."""
@@ -323,6 +329,10 @@ def dragon_obj():
 
 def buddha_obj():
     return _cached("buddha_standin", buddha_standin)
+
+
+def buddha_full_obj():
+    return _cached("buddha_full_standin", buddha_full_standin)
 
 
 def sky_rgb(W=512, H=256):
