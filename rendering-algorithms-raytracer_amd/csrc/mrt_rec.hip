@@ -1,0 +1,23 @@
+// mrt_rec.hip -- instantiations of the fused chain kernels (Shader REC 1 / 2:
+// Blinn reflection / refraction chains and path tracing traced inline) and of
+// the adaptive supersampling kernels.  A translation unit of its own so the
+// library's kernels compile in parallel (the shading code is mrt_shader.h).
+#include "mrt_shader.h"
+
+namespace mrt {
+
+template <bool C, bool PO, bool F, bool I, int REC>
+struct AdaptK { static constexpr KernelFn fn = adaptive_kernel<C, PO, F, I, REC>; };
+
+KernelFn pick_shade_rec(bool c, bool po, bool f, bool inst, int rec) {
+    if (rec == 2) return pick4<ShadeK, 2>(c, po, f, inst);
+    return pick4<ShadeK, 1>(c, po, f, inst);
+}
+
+KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec) {
+    if (rec == 2) return pick4<AdaptK, 2>(c, po, f, inst);
+    if (rec == 1) return pick4<AdaptK, 1>(c, po, f, inst);
+    return pick4<AdaptK, 0>(c, po, f, inst);
+}
+
+}  // namespace mrt

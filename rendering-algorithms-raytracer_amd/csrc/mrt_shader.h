@@ -1,0 +1,1125 @@
+// mrt_shader.h -- device shading code shared by the kernel translation units
+// (mrt_device.hip: frame kernels + host; mrt_rec.hip: the fused chain and
+// adaptive kernels; mrt_chain.hip: the wavefront chain kernels).  Included
+// after mrt_kernels.h / mrt_scene.h / mrt_texture.h inside namespace mrt.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "mrt_kernels.h"
+#include "mrt_scene.h"
+#include "mrt_texture.h"
+
+namespace mrt {
+
+enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLOW = 4, CTR_NODES_P = 5, CTR_LEAVES_P = 6, CTR_HITS = 7,
+       CTR_WAVE_STEPS_P = 8, CTR_UNIFORM_P = 9,
+       // count mode, per launch (primary at CTR_TP, shade at CTR_TS): wave start/end
+       // wall clocks as ~min start, max start, ~min end, max end (zero-initialised maxima)
+       CTR_TP = 10, CTR_TS = 14,
+       CTR_RAYS_P = 18,  // eye rays traced (adaptive supersampling; otherwise one per pixel)
+       CTR_SECONDARY = 19,  // Blinn reflection / refraction rays
+       CTR_WAVE_STEPS_S = 20, CTR_NODES_S = 21,  // count mode, shadow_kernel: wave loop steps, node visits
+       CTR_N = 22 };
+static constexpr int kMaxBlocksPerCU = 8;
+// wave log record: start, end, tiles, node visits, then (tile id << 40 | start tick) of the first kLogTiles
+// tiles, then the wall-clock ticks each of those tiles' dequeue took
+static constexpr int kLogTiles = 28;
+static constexpr int kLogWords = 4 + 2 * kLogTiles;  // 256-thread blocks: 8 waves per SIMD at most
+// counter block: CTR_N u64 statistics, then four launches x 8 work counters x 128 B
+// (primary, shade / gen, resolve, shadow_kernel's per-XCD ray queues)
+static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 4 * 8 * 128;
+// Shadow rays of the general shading path, wavefront style (ShadowMode): kernel
+// 2a runs the shading code and writes every shadow ray to its slot, kernel 2b
+// traces all of them any-hit (few registers, full occupancy), kernel 2c runs the
+// same shading code again with the occlusion bits.  Same rays, same order, same
+// arithmetic as the fused kernel, which keeps the whole shading state live
+// across each traversal.
+enum ShadowMode { kFused = 0, kGen = 1, kResolve = 2 };
+static constexpr int kMaxWaveShadow = 64;  // rays per pixel beyond this use the fused kernel
+
+struct RenderParams {
+    const QNode* nodes;
+    const DLeaf* leaves;
+    const PrimShade* prims;
+    const float4* verts;
+    const float4* normals;
+    const DevMaterial* mats;
+    const DevLight* lights;
+    const DevDome* domes;    // dome-light tables (DevLight::dome)
+    const DevInstance* insts;  // ProxyObjects (instanced scenes)
+    int32_t n_insts, n_world;  // instances; world objects (instance hit ids start here)
+    const float* env;        // environment map (nullable), env_w x env_h RGB, row 0 = top
+    float4* ray_o;           // wavefront shadow rays: slot * max_shadow + j -> origin, tMax
+    float4* ray_d;           //   direction
+    uint8_t* occl;           //   1 = occluded (kernel 2b)
+    uint8_t* nrays;          //   rays of each output slot (kernel 2a)
+    int32_t max_shadow;      //   rays per pixel at most (num_paths x light samples)
+    int32_t env_w, env_h;
+    float env_exposure;
+    const uint16_t* tables;  // rcp[2048] | rsqrt[2048]
+    const uint8_t* gamma;
+    const float* gammaF;     // Image::linear_to_gammaF (adaptive supersampling stop test)
+    int32_t min_subdivs, max_subdivs;
+    float noise;             // Scene::m_noiseThreshold
+    int32_t* gstack;
+    uint32_t gstride;        // total threads in the launch
+    unsigned long long* ctr;
+    unsigned long long* wave_log;  // count mode: kLogWords per wave (this launch), see mrt_debug_wave_log
+    CamParams cam[kMaxBatch];    // frame mode: cam[0]; batch mode: one camera per frame
+    float bg[3];
+    int32_t n_lights, num_paths;
+    int32_t path_trace, max_bounces, sample_env;  // Scene::m_pathTrace / m_maxBounces / sampleEnv
+    float* lvl;                  // REC kernels: chain level records, (level * lvl_words + w) * gstride + thread
+    int32_t lvl_words;           //   words per level record
+    uint32_t seed;
+    int32_t fast_box;            // node boxes finite && tuning allows the hardware min/max box test
+    int32_t sched;               // tile schedule (TileSched)
+    int32_t order;               // frame mode: 0 tiles bottom-up, 1 top-down (dequeue order only)
+    int32_t prio;                // 1: waves on their final tiles raise their issue priority
+    int32_t n_waves;             // waves in this launch (prio heuristic)
+    int32_t decline;             // >0: a wave in CU slot s stops taking tiles when fewer than s * decline remain
+    int32_t cus;                 // compute units (slot of a persistent block = blockIdx / cus)
+    int32_t scalar_nodes;        // scalar fetch of wave-uniform nodes
+    unsigned int* queue;         // 8 tile counters, 32 words apart (sched >= 2)
+    // work: 8x8 tiles
+    int32_t tiles_x, n_tiles;    // frame mode: tiles_x = ceil(W/8)
+    const int32_t* buckets;      // bucket mode: bucket ids (row-major bucket grid)
+    int32_t buckets_x;           // ceil(W/32)
+    int32_t buckets_per_frame;   // bucket mode: id = frame * buckets_per_frame + bucket
+    int32_t n_cams;              // bucket mode: frames (cameras) in the batch
+    int32_t mode;                // 0 frame, 1 buckets
+    float* out_rgb;              // frame: W*H*3; buckets: n_buckets*1024*3 (nullable)
+    uint8_t* out_rgb8;           // same slots as out_rgb (nullable)
+    float4* hits;                // per slot: t, a, b, prim bits (kernel 1 -> kernel 2)
+    // wavefront chain engine (mrt_chain.hip; REC scenes on the frame / bucket
+    // path): level k's entries live in arrays of ch_cap slots each
+    float4* ch_ray;              // [level][2][cap]: origin | path id bits, direction | state bits
+    float4* ch_ior;              // [level][2][cap]: IOR history 1..7 | parent entry bits
+    float4* ch_hit;              // [level][cap]: closest hit (t, a, b, prim bits)
+    float* ch_rec;               // [level][lvl_words][cap]: level records of spawning entries
+    float4* ch_sp;               // [4][cap]: the current level's spawned children, at the parent's index
+    uint8_t* ch_flag;            // [cap]: spawned (ch_sp slot valid)
+    float4* ch_tv;               // [paths]: final value of the path's deepest level | (level | none << 8) bits
+    uint32_t* ch_te;             // [paths]: entry of that level
+    uint32_t* ch_cnt;            // [level]: entries (level 0: unused, the chunk's paths)
+    uint32_t ch_cap;             // slots per level array (= paths of a chunk)
+    int32_t ch_level;            // the level a chain launch works on
+    int32_t ch_levels;           // levels allocated
+    int32_t item_base;           // chain launches: first work item of the chunk
+    const uint32_t* sh_count;    // shadow_kernel: pixel / entry count on the device (nullable)
+};
+
+// pow(spec, specExp) of Blinn::shade (src/Blinn.cpp:219-220; libm powf in the
+// reference).  Evaluated in double and rounded once: the correctly rounded
+// result in all but a vanishing fraction of inputs, where libm powf (<= 1 ulp)
+// may differ by one ulp -- the configs with specAmt > 0 are therefore checked
+// against the oracle to 1e-4 relative (north_star), everything else bit-exact.
+__device__ __forceinline__ float spec_pow(float x, float e) { return (float)pow((double)x, (double)e); }
+
+// operator*(Matrix4x4, Vector3) (src/Matrix4x4.h:693-704) on rows 0-2 of T (stride 4)
+__device__ __forceinline__ v3 xform_dir3(const float* T, v3 u) {
+    return mk(T[0] * u.x + T[1] * u.y + T[2] * u.z, T[4] * u.x + T[5] * u.y + T[6] * u.z,
+              T[8] * u.x + T[9] * u.y + T[10] * u.z);
+}
+
+// REC: the scene has reflective / refractive materials (Blinn secondary rays,
+// shade_path); compiled only into the kernels that run such scenes, so the
+// direct-lighting kernels keep their register budget.
+// RNG keys of the counter RNG (mrt_math.h): sub-stream skey = eye-ray sample *
+// 1024 + path, draw key dim = (chain level + 1) << 24 | k (camera: dims 0-2).
+__device__ __forceinline__ uint32_t level_key(int level) { return (uint32_t)(level + 1) << 24; }
+
+// Working IOR history of the rays below the camera ray (Ray::IORList,
+// src/Ray.h:43-50): a per-lane LDS column in the REC kernels.
+static constexpr int kIorCap = 8;
+
+// Chain state of one path at its current level (Shader::level).
+enum { kRefl = 1, kRefr = 2, kGI = 3 };
+struct ChainState {
+    int idx = 0, depth = 0, gi = 0, bounces = 0;  // IOR history index, level, GI / reflect-refract levels so far
+    bool secondary = false;                       // isSecondary of this level's shade()
+};
+// A chain level's record (the terms of the level that spawned a child): word w at p[w * stride]
+struct ChainRec {
+    float* p;
+    size_t stride;
+    __device__ float& operator()(int w) const { return p[(size_t)w * stride]; }
+};
+struct LevelOut {
+    DRay r2;         // the spawned child ray
+    v3 val, dir;     // the level's final value / the child's direction
+    bool spawn;      // a child ray was spawned (its terms are in the level record)
+    bool env_miss;   // a missed child takes the environment colour (false: GI with no environment sampling)
+};
+
+// Material::getEnvironmentColor (src/Material.cpp:44-62): scene map or background
+__device__ __forceinline__ v3 env_or_bg(const RenderParams& P, v3 d) {
+    if (P.env) return scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
+    return mk(P.bg[0], P.bg[1], P.bg[2]);
+}
+
+// Fold a child's value into its parent level (Blinn::shade, src/Blinn.cpp:
+// 238-335, and calculatePathTracing's Ld, :39-89), with the reference's adds.
+// `none`: the child was a GI ray that missed with no environment sampling
+// (calculatePathTracing adds nothing).
+__device__ __forceinline__ v3 chain_combine(const RenderParams& P, const ChainRec& rec, v3 val, bool none) {
+    const v3 z = mk(0, 0, 0);
+    const int info = __float_as_int(rec(0));
+    const DevMaterial& M = P.mats[info & 0xFFFF];
+    const int kind = info >> 16;
+    const float rrRecip = rec(1), rrSpec = rec(2);
+    const v3 le = mk(M.le[0], M.le[1], M.le[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+    if (kind == kGI) {   // Ld = 0 + (0 + kd * child) + each light's E * kd + ka
+        v3 Ld = add(z, none ? z : add(z, mul(mk(M.kd[0], M.kd[1], M.kd[2]), val)));
+        for (int i = 0; i < P.n_lights; i++) Ld = add(Ld, mk(rec(9 + 3 * i), rec(10 + 3 * i), rec(11 + 3 * i)));
+        Ld = add(Ld, ka);
+        const v3 Ls = mk(rec(3), rec(4), rec(5)), tr = mk(rec(6), rec(7), rec(8));
+        return add(add(scale(add(add(Ld, Ls), tr), rrRecip), scale(add(z, z), rrSpec)), le);
+    }
+    // Lr / Lt += m_ks * shade(child) (or * the environment when the child missed)
+    const v3 L = add(z, mul(mk(M.ks[0], M.ks[1], M.ks[2]), val));
+    const v3 base = scale(add(add(add(z, ka), z), z), rrRecip);
+    return add(add(base, scale(kind == kRefr ? add(z, L) : add(L, z), rrSpec)), le);
+}
+
+// REC: 0 direct lighting only; 1 Blinn reflection / refraction chains; 2 also
+// path tracing (GI rays).  Compiled into the kernels that run such scenes only.
+template <bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused, int REC = 0>
+struct Shader {
+    const RenderParams& P;
+    const Trav& T;
+    const uint16_t* rcpT;
+    const uint16_t* rsqT;
+    TravStats& st;
+    uint32_t pixel;
+    uint32_t shadow_rays;
+    uint32_t seed;
+    size_t slot0;            // wavefront modes: this pixel's first ray slot
+    uint32_t nslot;          //   rays so far
+    uint32_t sample = 0;     // eye-ray sample of the pixel (adaptive supersampling)
+    uint32_t skey = 0, dim = 0;  // RNG sub-stream / draw key
+    float* iorS = nullptr;   // REC: LDS IOR column (stride kWG)
+    float* lvl = nullptr;    // REC: this thread's level records (stride P.gstride)
+
+    __device__ float next_rand() { return rng(pixel, skey, dim++, seed); }
+
+    template <bool COUNT>
+    __device__ bool occluded(v3 from, v3 L, float tMax) {
+        shadow_rays++;
+        if constexpr (MODE == kGen) {  // no shading result depends on the answer but the final sums
+            const size_t s = slot0 + nslot++;
+            P.ray_o[s] = make_float4(from.x, from.y, from.z, tMax);
+            P.ray_d[s] = make_float4(L.x, L.y, L.z, 0.f);
+            return false;
+        } else if constexpr (MODE == kResolve) {
+            return P.occl[slot0 + nslot++] != 0;
+        } else {
+            DRay r = make_ray(from, L);
+            DHit h{tMax, 0.f, 0.f, -1};
+            return traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st);
+        }
+    }
+
+    // PointLight::sampleLight, src/PointLight.cpp:8-81
+    template <bool COUNT>
+    __device__ float point_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec) {
+        v3 L = sub(mk(l.pos[0], l.pos[1], l.pos[2]), from);
+        float nDotL = dot(normal, L);
+        if (!(nDotL > 0.0f)) { outSpec = 0.f; return 0.0f; }
+        float falloff = dot(L, L);
+        float distanceRecip = rsqrt_nr(falloff, rsqT);
+        falloff = rcp_nr(falloff, rcpT);
+        float distance = rcp_nr(distanceRecip, rcpT);
+        L = scale(L, distanceRecip);
+        nDotL *= distanceRecip;
+        // Everything the light returns except the shadow bit is formed before the
+        // shadow ray, so only three scalars stay live across its traversal.
+        const float A = (l.power * falloff) * (0.25f / 3.1415926f);
+        const float rdl = std_max(0.f, dot(rVec, L));
+        float attenuate = 1.0f;
+        if (l.cast_shadows && occluded<COUNT>(from, L, distance)) attenuate = 0.0f;
+        attenuate *= nDotL;
+        outSpec = rdl * attenuate;
+        return A * attenuate;
+    }
+
+    // RectangleLight::sampleLight, src/RectangleLight.cpp:42-136 (fast shadows)
+    template <bool COUNT>
+    __device__ v3 rect_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec) {
+        v3 v1 = mk(l.v1[0], l.v1[1], l.v1[2]), v2 = mk(l.v2[0], l.v2[1], l.v2[2]), w3 = mk(l.v3[0], l.v3[1], l.v3[2]);
+        v3 acc = mk(0, 0, 0);
+        float tmpSpec = 0.f, recip = 1.0f, falloff = 1.0f;
+        int done = 0;
+        bool cut = false;
+        do {
+            float e1 = next_rand();
+            float e2 = next_rand();
+            e2 = ((double)e2 > 0.99) ? (float)0.99 : e2;
+            v3 rd = sub(add(add(v1, scale(sub(v2, v1), e1)), scale(sub(w3, v1), e2)), from);
+            float nDotL = dot(normal, rd);
+            float att = 1.0f;
+            if (nDotL > 0.001f) {
+                falloff = dot(rd, rd);
+                float dr = rsqrt_nr(falloff, rsqT);
+                falloff = rcp_nr(falloff, rcpT);
+                float dist = rcp_nr(dr, rcpT);
+                rd = scale(rd, dr);
+                if (l.cast_shadows && occluded<COUNT>(from, rd, dist - 0.001f)) att = 0.0f;
+            } else {
+                att = 0.0f;
+            }
+            float E = (l.power * falloff) * (0.25f / 3.1415926f);
+            done++;
+            recip = 1.0f / (float)done;
+            float Es = E * recip;
+            cut = ((Es + Es + Es) * 0.333333f) < l.noise;
+            float Ea = E * att;
+            acc = add(acc, mk(Ea, Ea, Ea));
+            tmpSpec += std_max(0.f, dot(rVec, rd)) * att;
+        } while (done < l.samples && !cut);
+        outSpec = tmpSpec * recip;
+        return scale(acc, recip);
+    }
+
+    // DomeLight::sampleLight, src/DomeLight.cpp:80-160 (fast shadows; m_numSamples
+    // draws, one for secondary shading, :89).  A draw below the shading horizon is
+    // redrawn without counting it (`continue` at :106 skips samplesDone++); after
+    // kDomeMaxRejects such redraws in one call the loop stops (the reference would
+    // not terminate when the whole map lies below the horizon).
+    static constexpr int kDomeMaxRejects = 256;
+    template <bool COUNT>
+    __device__ v3 dome_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec, bool secondary) {
+        const DevDome& D = P.domes[l.dome];
+        const int numSamples = secondary ? 1 : l.samples;
+        v3 acc = mk(0, 0, 0);
+        float tmpSpec = 0.f, recip = 1.0f;
+        int done = 0, rejects = 0;
+        bool cut = false;
+        do {
+            const float e1 = next_rand();
+            const float e2 = next_rand();
+            float pdf0, pdf1;
+            const float fu = dist_sample(D.cdf_u, D.func_u, D.nu, D.inv_int_u, e1, pdf0);
+            const int iu = (int)fu;
+            const int u = iu == D.nu ? iu - 1 : iu;
+            const float fv = dist_sample(D.cdf_v + (size_t)u * (D.nv + 1), D.func_v + (size_t)u * D.nv, D.nv,
+                                         D.inv_int_v[u], e2, pdf1);
+            const int iv = (int)fv;
+            const float cosT = D.cos_v[iv], sinT = D.sin_v[iv], sinP = D.sin_u[iu], cosP = D.cos_u[iu];
+            const v3 dir = mk(-sinT * cosP, -cosT, -sinT * sinP);
+            if (dot(normal, dir) < 0.0f) {
+                if (++rejects >= kDomeMaxRejects) break;
+                continue;
+            }
+            const float pdf = (pdf0 * pdf1) / (kTwoPI2 * sinT);
+            const v3 img = tex_lookup_dir(D.tex, D.nu, D.nv, dir.x, dir.y, dir.z);
+            const float inv = 1.0f / pdf;  // E = m_Gain * imageSample / pdf (Vector3::operator/)
+            const v3 E = scale(scale(img, l.power), inv);
+            float att = 1.0f;
+            if (occluded<COUNT>(from, dir, 1e12f)) att = 0.0f;
+            done++;
+            recip = 1.0f / (float)done;
+            const v3 Es = scale(E, recip);
+            cut = (((Es.x + Es.y) + Es.z) * 0.333333f) < l.noise;
+            acc = add(acc, scale(E, att));
+            tmpSpec += dot(rVec, dir) * att;
+        } while (done < numSamples && !cut);
+        outSpec = tmpSpec * recip;
+        return scale(acc, recip);
+    }
+
+    // Light::sampleLight dispatch; `secondary` = the isSecondary argument
+    template <bool COUNT>
+    __device__ v3 sample_light(int li, v3 from, v3 normal, v3 rVec, float& spec, bool secondary = false) {
+        const DevLight& l = P.lights[li];
+        if (POINT_ONLY || l.type == MRT_POINT_LIGHT) {
+            float e = point_light<COUNT>(l, from, normal, rVec, spec);
+            return mk(e, e, e);
+        }
+        if constexpr (!POINT_ONLY) {
+            if (l.type == MRT_DOME_LIGHT) return dome_light<COUNT>(l, from, normal, rVec, spec, secondary);
+            return rect_light<COUNT>(l, from, normal, rVec, spec);
+        }
+        return mk(0, 0, 0);
+    }
+
+    // HitInfo::getAllInfos (normals), src/Ray.cpp:5-49
+    // an instance hit (id >= n_world) names instance i's BLAS object id - hit_base
+    __device__ void normals(const DHit& h, v3& N, v3& geoN, uint32_t& mat) {
+        int32_t ps_i = h.prim, inst = -1;
+        if (INST && h.prim >= P.n_world) {
+            int lo = 0, hi = P.n_insts - 1;  // the last instance with hit_base <= id
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (P.insts[mid].hit_base <= h.prim) lo = mid;
+                else hi = mid - 1;
+            }
+            inst = lo;
+            ps_i = P.insts[lo].shade_base + (h.prim - P.insts[lo].hit_base);
+        }
+        PrimShade ps = P.prims[ps_i];
+        float4 A = P.verts[ps.v[0]], B = P.verts[ps.v[1]], C = P.verts[ps.v[2]];
+        geoN = normalized(cross(mk(B.x - A.x, B.y - A.y, B.z - A.z), mk(C.x - A.x, C.y - A.y, C.z - A.z)), rsqT);
+        float c = 1.0f - h.a - h.b;
+        float4 n0 = P.normals[ps.n[0]], n1 = P.normals[ps.n[1]], n2 = P.normals[ps.n[2]];
+        v3 s = add(add(scale(mk(n0.x, n0.y, n0.z), c), scale(mk(n1.x, n1.y, n1.z), h.a)), scale(mk(n2.x, n2.y, n2.z), h.b));
+        N = normalized(s, rsqT);
+        if (INST && inst >= 0) {  // HitInfo::getAllInfos with m_proxy (src/Ray.cpp:27-31)
+            const float* T = P.insts[inst].inv_t;
+            geoN = normalized(xform_dir3(T, geoN), rsqT);
+            N = normalized(xform_dir3(T, N), rsqT);
+        }
+        mat = ps.mat;
+    }
+
+    // Scene::sampleScene hit branch (src/Scene.cpp:224-233): m_numPaths shade()
+    // calls on the camera ray, each path its own RNG sub-stream.
+    template <bool COUNT>
+    __device__ v3 shade(const DRay& r, const DHit& h) {
+        v3 N, geoN;
+        uint32_t mi;
+        normals(h, N, geoN, mi);
+        const DevMaterial& M = P.mats[mi];
+        v3 P_ = mk(r.o[0] + h.t * r.d[0], r.o[1] + h.t * r.d[1], r.o[2] + h.t * r.d[2]);  // Ray::getPoint
+        v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+        v3 result = mk(0, 0, 0);
+        // the camera ray's IOR history [1, 1.001]: Blinn::shade pops it on a
+        // back-face hit and the pop persists into the next path (src/Blinn.cpp:176-179)
+        IorCam cam;
+        for (int path = 0; path < P.num_paths; path++) {
+            skey = sample * 1024u + (uint32_t)path;
+            dim = level_key(0);
+            v3 sh;
+            if constexpr (MODE == kFused && REC) {   // secondary rays / path tracing in the scene
+                result = add(result, shade_path<COUNT>(r, h, cam));
+                continue;
+            }
+            if (M.type == MRT_LAMBERT) {  // Lambert::shade
+                v3 L = mk(0, 0, 0);
+                for (int i = 0; i < P.n_lights; i++) {
+                    float discard;
+                    v3 E = sample_light<COUNT>(i, P_, N, mk(0, 0, 0), discard);
+                    L = add(L, mul(E, kd));
+                }
+                sh = add(L, ka);
+            } else {  // Blinn::shade, direct branch
+                v3 rayD = mk(r.d[0], r.d[1], r.d[2]);
+                v3 viewDir = neg(rayD);
+                float vDotN = dot(viewDir, N), vDotGeoN = dot(viewDir, geoN);
+                bool same = (vDotN * vDotGeoN) >= 0.0f;
+                v3 n = same ? N : geoN;
+                vDotN = same ? vDotN : vDotGeoN;
+                if (vDotN < 0.0f) { vDotN = -vDotN; n = neg(n); }
+                v3 rVec = add(rayD, scale(n, 2.0f * vDotN));
+                (void)next_rand();  // Russian-roulette draw (src/Blinn.cpp:195); weight 1
+                v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
+                v3 Ld = mk(0, 0, 0), Ls = mk(0, 0, 0);
+                for (int i = 0; i < P.n_lights; i++) {
+                    float spec = 0.f;
+                    v3 E = sample_light<COUNT>(i, P_, n, rVec, spec);
+                    float pw = (M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
+                    Ls = add(Ls, scale(scale(mul(E, ks), M.spec_amt), pw));
+                    Ld = add(Ld, mul(E, kd));
+                }
+                Ld = add(Ld, ka);
+                v3 z = mk(0, 0, 0);
+                sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), mk(M.le[0], M.le[1], M.le[2]));
+            }
+            result = add(result, sh);
+        }
+        return scale(result, 1.0f / (float)P.num_paths);
+    }
+
+    // Material::fresnel, full form (src/Material.h:47-55); the reference's libm
+    // acos / sin evaluated in double and rounded once (as in the oracle)
+    __device__ static float fresnel(float n1, float n2, float c) {
+        const float n1CosTh = n1 * c;
+        const float th = (float)acos((double)c);
+        const float n1_n2SinTh = (n1 * (float)sin((double)th)) / n2;
+        const float n2CosTh = n2 * std_max(0.0f, sqrtf(1.0f - n1_n2SinTh * n1_n2SinTh));
+        const float Rs = (n1CosTh - n2CosTh) / (n1CosTh + n2CosTh);
+        return Rs * Rs;
+    }
+
+    // Material::getCosineDistributedSamples (src/Material.cpp:14-41): two draws,
+    // RSQRTSS/RCPSS square roots, libm cos / sin in double rounded once
+    __device__ v3 cosine_sample(v3 N) {
+        const float e1 = next_rand();
+        float e2 = next_rand();
+        e2 = ((double)e2 > 0.99) ? (float)0.99 : e2;
+        const v3 a = ((double)fabsf(N.x) > 0.1) ? mk(0, 1, 0) : mk(1, 0, 0);
+        const v3 u = normalized(cross(a, N), rsqT);
+        const v3 v = cross(N, u);
+        const float t = (2.0f * 3.1415926f) * e1;
+        const float sqrte2 = rcp_nr(rsqrt_nr(e2, rsqT), rcpT);
+        const float sqrt1_e2 = rcp_nr(rsqrt_nr(fabsf(1.0f - e2), rsqT), rcpT);
+        const float c = (float)cos((double)t), s = (float)sin((double)t);
+        return normalized(add(add(scale(u, c * sqrte2), scale(v, s * sqrte2)), scale(N, sqrt1_e2)), rsqT);
+    }
+
+    __device__ v3 env_color(v3 d) { return env_or_bg(P, d); }
+
+    // the camera ray's history: [1, 1.001, (a level-0 refraction push)] and its index
+    struct IorCam {
+        float v1 = 1.001f, v2 = 0.f;
+        int idx = 1;
+        __device__ float at(int i) const { return i == 0 ? 1.0f : (i == 1 ? v1 : v2); }
+    };
+    __device__ float& ior_at(int i) { return iorS[i * kWG]; }
+    // level record word w of chain level k of the fused kernels (global memory,
+    // one column per thread)
+    __device__ ChainRec rec_fused(int k) const { return ChainRec{lvl + (size_t)k * P.lvl_words * P.gstride, P.gstride}; }
+
+    // One level of Material::shade with Blinn's secondary rays and path tracing
+    // (src/Blinn.cpp:39-335): Fresnel-weighted Russian roulette between direct
+    // lighting (+ Blinn::calculatePathTracing's GI ray) and one reflection or
+    // refraction ray (bounces < 5), with each ray's IOR history (Ray::IORList,
+    // src/Ray.h:43-50; LDS column ior_at below the camera ray, `cam` for it).
+    // Either the level's value is final (o.spawn = false, o.val), or it spawns
+    // one child ray (o.r2): its terms go to the level record `rec` -- reflect /
+    // refract: rrWeightRecip, rrWeightRecipSpec; GI: also Ls, the translucency
+    // and each light's E * kd, all sampled before the child is traced (each
+    // level draws from its own RNG key) -- `cs` and the IOR column become the
+    // child's, and chain_combine() folds the child's value (or, if it misses,
+    // the environment / nothing, o.env_miss) into the level's in the reference's
+    // operation order.  The fused kernels trace the child inline (shade_path);
+    // the wavefront chain kernels queue it.
+    static constexpr int kMaxBounce = 5;
+    uint32_t secondary = 0;
+    template <bool COUNT>
+    __device__ void level(const DRay& r, const DHit& h, ChainState& cs, IorCam& cam, const ChainRec& rec, LevelOut& o) {
+        const v3 z = mk(0, 0, 0);
+        o.spawn = false;
+        dim = level_key(cs.depth);
+        v3 N, geoN;
+        uint32_t mi;
+        normals(h, N, geoN, mi);
+        const DevMaterial& M = P.mats[mi];
+        const v3 Pt = mk(r.o[0] + h.t * r.d[0], r.o[1] + h.t * r.d[1], r.o[2] + h.t * r.d[2]);
+        const v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+        if (M.type == MRT_LAMBERT) {   // Lambert::shade: no secondary rays (isSecondary not passed on)
+            v3 L = z;
+            for (int i = 0; i < P.n_lights; i++) {
+                float discard;
+                L = add(L, mul(sample_light<COUNT>(i, Pt, N, z, discard), kd));
+            }
+            o.val = add(L, ka);
+            return;
+        }
+        const v3 le = mk(M.le[0], M.le[1], M.le[2]);
+        const v3 rayD = mk(r.d[0], r.d[1], r.d[2]);
+        const v3 viewDir = neg(rayD);
+        float vDotN = dot(viewDir, N);
+        const float vDotGeoN = dot(viewDir, geoN);
+        const bool same = (vDotN * vDotGeoN) >= 0.0f;
+        v3 n = same ? N : geoN;
+        vDotN = same ? vDotN : vDotGeoN;
+        bool flip = false;
+        if (vDotN < 0.0f) { flip = true; vDotN = -vDotN; n = neg(n); }
+        v3 rVec = add(rayD, scale(n, 2.0f * vDotN));
+        if (M.gloss < 1.0f) {   // glossy reflection vector (src/Blinn.cpp:166-171)
+            const v3 rd = cosine_sample(n);
+            rVec = normalized(add(scale(rVec, M.gloss), scale(rd, 1.0f - M.gloss)), rsqT);
+        }
+        // inIOR, then a back-face hit pops the (mutable) history (src/Blinn.cpp:167-185)
+        float inIOR, outIOR = M.ior;
+        if (cs.depth == 0) {
+            inIOR = cam.at(cam.idx);
+            if (flip) { if (cam.idx > 0) cam.idx--; outIOR = cam.at(cam.idx); }
+        } else {
+            inIOR = ior_at(cs.idx);
+            if (flip) { if (cs.idx > 0) cs.idx--; outIOR = ior_at(cs.idx); }
+        }
+        const float curIOR = cs.depth == 0 ? cam.at(cam.idx) : ior_at(cs.idx);   // r_IOR() after the pop
+        float Rs = 0.f, Ts = 0.f;
+        if (M.reflect > 0.0f || M.refract > 0.0f) {
+            Rs = fresnel(inIOR, outIOR, vDotN);
+            Ts = 1.0f - Rs;
+        }
+        float rr = next_rand();
+        const float rrW = (1.0f - Rs * M.reflect) - Ts * M.refract;
+        const float rrRecip = (rrW > 0.f) ? 1.f / rrW : 1.f;
+        const float rrSpec = (1.f - rrW > 0.f) ? 1.f / (1.f - rrW) : 1.f;
+        const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
+        if (rr <= rrW) {   // direct lighting
+            bool child = false;
+            v3 randD = z;
+            v3 Ld = z;
+            if constexpr (REC == 2) {   // Blinn::calculatePathTracing (src/Blinn.cpp:39-89)
+                v3 pt = z;
+                if (M.emitter) {
+                    pt = add(z, scale(le, M.emitted));
+                } else if (cs.gi < P.max_bounces - 1) {
+                    randD = cosine_sample(n);
+                    child = true;
+                } else {   // last bounce: the lights directly, isSecondary, rVec = 0
+                    for (int i = 0; i < P.n_lights; i++) {
+                        float spec = 0.f;
+                        pt = add(pt, mul(sample_light<COUNT>(i, Pt, n, z, spec, true), kd));
+                    }
+                }
+                if (!child) Ld = add(Ld, pt);
+            }
+            v3 Ls = z;
+            for (int i = 0; i < P.n_lights; i++) {
+                float spec = 0.f;
+                v3 E = sample_light<COUNT>(i, Pt, n, rVec, spec, cs.secondary);
+                float pw = (M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
+                Ls = add(Ls, scale(scale(mul(E, ks), M.spec_amt), pw));
+                const v3 term = mul(E, kd);
+                if (child) { rec(9 + 3 * i) = term.x; rec(10 + 3 * i) = term.y; rec(11 + 3 * i) = term.z; }
+                else Ld = add(Ld, term);
+            }
+            v3 tr = z;
+            if (M.translucency > 0.01f) {   // lights seen through the surface (src/Blinn.cpp:224-236)
+                v3 total = z;
+                for (int i = 0; i < P.n_lights; i++) {
+                    float spec = 0.f;
+                    total = add(total, sample_light<COUNT>(i, Pt, neg(n), rVec, spec, cs.secondary));
+                }
+                tr = add(z, mul(scale(total, M.translucency), kd));
+            }
+            if (child) {   // descend into the GI ray: IOR history [1, current]
+                rec(0) = __int_as_float((int)mi | (kGI << 16));
+                rec(1) = rrRecip; rec(2) = rrSpec;
+                rec(3) = Ls.x; rec(4) = Ls.y; rec(5) = Ls.z;
+                rec(6) = tr.x; rec(7) = tr.y; rec(8) = tr.z;
+                ior_at(0) = 1.0f; ior_at(1) = curIOR; cs.idx = 1;
+                cs.depth++; cs.gi++;
+                cs.secondary = true;
+                o.spawn = true;
+                o.r2 = make_ray(Pt, randD);
+                o.dir = randD;
+                o.env_miss = M.sample_env && P.sample_env;
+                secondary++;
+                return;
+            }
+            Ld = add(Ld, ka);
+            o.val = add(add(scale(add(add(Ld, Ls), tr), rrRecip), scale(add(z, z), rrSpec)), le);
+            return;
+        }
+        const v3 base = scale(add(add(add(z, ka), z), z), rrRecip);   // (Ld + Ls + translucency) * rrWeightRecip
+        rr = next_rand();
+        bool refr, spawn;
+        v3 dir;
+        if (rr < M.reflect * Rs) {
+            refr = false;
+            dir = rVec;
+            spawn = M.reflect * Rs > 0.0f && cs.bounces < kMaxBounce;
+            if (spawn && cs.depth == 0) {   // the child copies the camera ray's history
+                ior_at(0) = 1.0f; ior_at(1) = cam.v1; ior_at(2) = cam.v2; cs.idx = cam.idx;
+            }
+        } else if (M.refract * Ts > 0.0f) {
+            refr = true;
+            const float q = inIOR / outIOR;
+            const float sq = std_max(0.0f, sqrtf(1.0f - (q * q) * (1.0f - vDotN * vDotN)));
+            dir = normalized(add(scale(rayD, q), scale(n, q * vDotN - sq)), rsqT);
+            spawn = cs.bounces < kMaxBounce;
+            if (spawn) {   // r_IOR.push(outIOR) on the mutable history, the child copies it
+                if (cs.depth == 0) {
+                    if (cam.idx == 0) cam.v1 = outIOR; else cam.v2 = outIOR;
+                    ior_at(0) = 1.0f; ior_at(1) = cam.v1; ior_at(2) = cam.v2; cs.idx = cam.idx + 1;
+                } else {
+                    ior_at(cs.idx + 1) = outIOR; cs.idx++;
+                }
+            }
+        } else {   // refraction branch with nothing to refract: Lr = Lt = 0
+            o.val = add(add(base, scale(add(z, z), rrSpec)), le);
+            return;
+        }
+        if (spawn) {
+            rec(0) = __int_as_float((int)mi | ((refr ? kRefr : kRefl) << 16));
+            rec(1) = rrRecip; rec(2) = rrSpec;
+            cs.depth++; cs.bounces++;
+            cs.secondary = false;   // shade(..) with the default isSecondary
+            o.spawn = true;
+            o.r2 = make_ray(Pt, dir);
+            o.dir = dir;
+            o.env_miss = true;
+            secondary++;
+            return;
+        }
+        const v3 L = add(z, mul(ks, env_color(dir)));   // Lr / Lt += m_ks * environment
+        o.val = add(add(base, scale(refr ? add(z, L) : add(L, z), rrSpec)), le);
+    }
+
+    // Blinn::shade's recursion for one path, fused: each level's child ray is
+    // traced inline and the levels are combined deepest first.
+    template <bool COUNT>
+    __device__ v3 shade_path(DRay r, DHit h, IorCam& cam) {
+        ChainState cs;
+        v3 val;
+        bool none = false;
+        for (;;) {
+            LevelOut o;
+            level<COUNT>(r, h, cs, cam, rec_fused(cs.depth), o);
+            if (!o.spawn) { val = o.val; break; }
+            DHit h2{1e12f, 0.f, 0.f, -1};
+            if (traverse<false, COUNT, FAST, INST>(T, o.r2, 0.001f, h2, st)) {
+                r = o.r2;
+                h = h2;
+                continue;
+            }
+            none = !o.env_miss;   // the missed child's value: environment, or nothing (GI, no env)
+            val = none ? mk(0, 0, 0) : env_color(o.dir);
+            break;
+        }
+        for (int k = cs.depth - 1; k >= 0; k--) {   // combine deepest first
+            val = chain_combine(P, rec_fused(k), val, none);
+            none = false;
+        }
+        return val;
+    }
+};
+
+__device__ __forceinline__ uint8_t map8(const uint8_t* lut, float v) { return lut[map_index(v)]; }
+
+// Tile schedule of a persistent wave (one 8x8 tile = one wave step).
+//   sched 0: static grid-stride over all tiles.
+//   sched 1: static XCD bands -- workgroups b, b+8, ... (observed to share one XCD
+//            and its L2; placement is a speed hint only) walk one eighth.
+//   sched 2: dynamic -- 8 tile counters (one 128-B line each), counter c hands
+//            out tiles c, c+8, ...; a wave starts at counter blockIdx & 7 and moves
+//            to the next counter when one runs dry, so every wave stays busy until
+//            the frame is done.
+//   sched 3: dynamic, counter c hands out the contiguous band c (L2 locality per
+//            XCD) with the same stealing.
+// Counters are zeroed per launch; every wave sees -1 after at most 8 empty probes.
+struct TileSched {
+    const RenderParams& P;
+    int lane, mode, cur, step, end, home, probe, band;
+    uint32_t deq_ticks = 0;  // count mode: wall-clock ticks of the last dequeue
+    __device__ TileSched(const RenderParams& P_, int wave, int lane_) : P(P_), lane(lane_) {
+        mode = P.sched;
+        home = blockIdx.x & 7;
+        probe = 0;
+        band = (P.n_tiles + 7) >> 3;
+        if (mode == 1 && (gridDim.x & 7) == 0) {
+            int local = blockIdx.x >> 3, per = gridDim.x >> 3;
+            int beg = home * band;
+            end = min(P.n_tiles, beg + band);
+            cur = beg + local * 4 + wave;
+            step = per * 4;
+        } else {
+            if (mode == 1) mode = 0;
+            cur = blockIdx.x * 4 + wave;
+            step = gridDim.x * 4;
+            end = P.n_tiles;
+        }
+    }
+    __device__ int dequeue() {
+        int item = -1;
+        const uint64_t q0 = P.wave_log ? wall_clock64() : 0;
+        if (lane == 0) {
+            // decline: later-dispatched blocks (issue priority goes to older waves)
+            // leave the last tiles to the older, faster waves
+            const int slot = blockIdx.x / P.cus;
+            const int keep = P.decline * slot;
+            while (probe < 8) {
+                const int c = (home + probe) & 7;
+                if (keep > 0 && mode == 2) {
+                    const unsigned seen = __hip_atomic_load(P.queue + c * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const long left = ((long)P.n_tiles - c + 7) / 8 - (long)seen;   // tiles left on counter c
+                    if (left * 8 < keep) { probe = 8; break; }
+                }
+                const unsigned v = atomicAdd(P.queue + c * 32, 1u);
+                const long idx = (mode == 3) ? (v < (unsigned)band ? (long)c * band + v : (long)P.n_tiles)
+                                             : (long)c + 8l * v;
+                if (idx < P.n_tiles) { item = (int)idx; break; }
+                probe++;
+            }
+        }
+        item = __shfl(item, 0);
+        if (P.wave_log) deq_ticks = (uint32_t)(wall_clock64() - q0);
+        return item;
+    }
+    // items are wave-uniform: readfirstlane puts them (and the frame / camera
+    // lookups derived from them) in SGPRs
+    // prio 1: a wave whose tile is among the last n_waves handed out raises its
+    // issue priority (those tiles bound the launch); prio 2: also lowers it back
+    // to 0 before earlier tiles (reset)
+    __device__ void boost(int item) {
+        if (P.prio && item >= 0 && mode >= 2 && item_rank(item) >= P.n_tiles - P.n_waves) __builtin_amdgcn_s_setprio(3);
+        else if (P.prio == 2) __builtin_amdgcn_s_setprio(0);
+    }
+    // dequeue position of a tile under sched 2 / 3
+    __device__ int item_rank(int item) const {
+        if (mode == 3) return (item % band) * 8 + item / band;
+        return item;  // interleaved counters hand out tiles in index order overall
+    }
+    __device__ int first() {
+        if (mode >= 2) { const int it = __builtin_amdgcn_readfirstlane(dequeue()); boost(it); return it; }
+        return __builtin_amdgcn_readfirstlane(cur < end ? cur : -1);
+    }
+    __device__ int next(int item) {
+        if (mode >= 2) { const int it = __builtin_amdgcn_readfirstlane(dequeue()); boost(it); return it; }
+        item += step;
+        return __builtin_amdgcn_readfirstlane(item < end ? item : -1);
+    }
+};
+
+// work item (8x8 tile, wave-uniform) -> frame of the item (frame mode: 0)
+__device__ __forceinline__ int item_frame(const RenderParams& P, int item) {
+    // clamped: an out-of-range id renders with the last camera instead of reading
+    // past the kernel argument block
+    return P.mode == 0 ? 0 : (int)min((uint32_t)P.buckets[item >> 4] / (uint32_t)P.buckets_per_frame, (uint32_t)(P.n_cams - 1));
+}
+
+// work item + lane -> pixel (x, y) and output slot
+__device__ __forceinline__ bool item_pixel(const RenderParams& P, int item, int lane, int& x, int& y, size_t& slot) {
+    if (P.mode == 0) {
+        const int t = P.order ? P.n_tiles - 1 - item : item;
+        int tx = t % P.tiles_x, ty = t / P.tiles_x;
+        x = tx * 8 + (lane & 7);
+        y = ty * 8 + (lane >> 3);
+        slot = (size_t)y * P.cam[0].W + x;
+    } else {
+        int bslot = item >> 4, sub = item & 15;
+        int b = (int)((uint32_t)P.buckets[bslot] % (uint32_t)P.buckets_per_frame);
+        int bx = b % P.buckets_x, by = b / P.buckets_x;
+        int lx = (sub & 3) * 8 + (lane & 7), ly = (sub >> 2) * 8 + (lane >> 3);
+        x = bx * 32 + lx;
+        y = by * 32 + ly;
+        slot = (size_t)bslot * 1024 + ly * 32 + lx;
+    }
+    return x < P.cam[0].W && y < P.cam[0].H;
+}
+
+__device__ __forceinline__ void load_tables(const uint16_t* g, uint16_t* s, int words32) {
+    for (int i = threadIdx.x; i < words32; i += kWG) reinterpret_cast<uint32_t*>(s)[i] = reinterpret_cast<const uint32_t*>(g)[i];
+    __syncthreads();
+}
+
+template <bool COUNT, bool PRIMARY = false>
+__device__ __forceinline__ void flush_stats(const RenderParams& P, const TravStats& st, uint32_t shadow, int lane,
+                                            uint64_t t0, uint32_t tiles) {
+    if ((COUNT || P.wave_log) && lane == 0) {   // ramp / tail of the persistent waves
+        const uint64_t t1 = wall_clock64();
+        if (P.wave_log) {
+            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6));
+            r[0] = t0; r[1] = t1; r[2] = tiles;
+        }
+        unsigned long long* c = P.ctr + (PRIMARY ? CTR_TP : CTR_TS);
+        atomicMax(c + 0, (unsigned long long)~t0);
+        atomicMax(c + 1, (unsigned long long)t0);
+        atomicMax(c + 2, (unsigned long long)~t1);
+        atomicMax(c + 3, (unsigned long long)t1);
+    }
+    // shadow rays (shade kernel) or primary hits (primary kernel), always counted
+    unsigned long long sh = shadow;
+    for (int off = 32; off > 0; off >>= 1) sh += __shfl_down(sh, off);
+    if (lane == 0 && sh) atomicAdd(&P.ctr[PRIMARY ? CTR_HITS : CTR_SHADOW], sh);
+    if (COUNT) {
+        unsigned long long nv = st.nodes, lv = st.leaves, uv = st.uniform;
+        int msp = st.max_sp;
+        for (int off = 32; off > 0; off >>= 1) {
+            nv += __shfl_down(nv, off);
+            lv += __shfl_down(lv, off);
+            uv += __shfl_down(uv, off);
+            msp = max(msp, __shfl_down(msp, off));
+        }
+        if (lane == 0) {
+            if (P.wave_log) P.wave_log[kLogWords * ((size_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6)) + 3] = nv;
+            atomicAdd(&P.ctr[CTR_NODES], nv);
+            atomicAdd(&P.ctr[CTR_LEAVES], lv);
+            if (PRIMARY) {
+                atomicAdd(&P.ctr[CTR_NODES_P], nv);
+                atomicAdd(&P.ctr[CTR_LEAVES_P], lv);
+                atomicAdd(&P.ctr[CTR_UNIFORM_P], uv);
+            }
+            atomicMax(&P.ctr[CTR_MAXSP], (unsigned long long)msp);
+        }
+    }
+    if (st.overflow) atomicOr(&P.ctr[CTR_OVERFLOW], 1ull);
+}
+
+// reflection / refraction rays of a wave (Shader::shade_path), always counted
+__device__ __forceinline__ void flush_secondary(const RenderParams& P, uint32_t n, int lane) {
+    unsigned long long v = n;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+    if (lane == 0 && v) atomicAdd(&P.ctr[CTR_SECONDARY], v);
+}
+
+// Camera::eyeRayAdaptive(x, y, .5, .5, .5, .5) (src/Camera.cpp:116-157): two
+// jitter draws (dims 0, 1; the offsets are exactly 0.5) and the time draw (dim 2,
+// unused).  Deterministic, so kernel 2 recomputes it instead of storing it.
+__device__ __forceinline__ v3 camera_dir(const CamParams& cam, uint32_t seed, int x, int y, const uint16_t* rsqT) {
+    const uint32_t pixel = (uint32_t)(y * cam.W + x);
+    float ur = rng(pixel, 0, 0, seed), vr = rng(pixel, 0, 1, seed);
+    float xo = (0.5f - 0.5f) * ur + 0.5f, yo = (0.5f - 0.5f) * vr + 0.5f;
+    float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
+    float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
+    v3 U = mk(cam.u[0], cam.u[1], cam.u[2]), Vv = mk(cam.v[0], cam.v[1], cam.v[2]), W = mk(cam.w[0], cam.w[1], cam.w[2]);
+    return normalized(sub(add(scale(U, Up), scale(Vv, Vp)), W), rsqT);
+}
+
+// Kernel 1: Camera::eyeRayAdaptive + closest-hit BVH::intersect per pixel.
+// Writes the HitInfo record (t, a, b, prim) to P.hits[slot].
+template <bool COUNT, int MINW, bool FAST, bool INST = false>
+__global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[2048];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    load_tables(P.tables, s_tab, 1024);
+    const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
+    const uint16_t* rcpT = s_tab;           // per triangle test: LDS
+    const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
+    TravStats st;
+    uint32_t nhits = 0;
+    unsigned long long wave_steps = 0;  // count mode: sum over tiles of max lane node visits
+    TileSched ts(P, wave, lane);
+    uint32_t ntiles = 0;
+    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
+        if (P.wave_log && lane == 0 && ntiles < kLogTiles)
+        {
+            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
+            r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
+            r[4 + kLogTiles + ntiles] = ts.deq_ticks;
+        }
+        ntiles++;
+        int x, y;
+        size_t slot;
+        const uint32_t n0 = st.nodes;
+        if (item_pixel(P, item, lane, x, y, slot)) {
+            const int f = item_frame(P, item);
+            const CamParams& cam = P.cam[f];
+            DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, P.seed + (uint32_t)f, x, y, rsqT));
+            DHit h{1e12f, 0.f, 0.f, -1};
+            if (!traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st)) h.prim = -1;
+            item_pixel(P, item, lane, x, y, slot);  // recompute: keeps it out of the traversal's live set
+            P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(h.prim));
+            nhits += h.prim >= 0 ? 1u : 0u;  // wave-reduced in flush_stats
+        }
+        if (COUNT) {
+            uint32_t dmax = st.nodes - n0;
+            for (int off = 32; off > 0; off >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, off));
+            wave_steps += dmax;
+        }
+    }
+    if (COUNT && lane == 0) atomicAdd(&P.ctr[CTR_WAVE_STEPS_P], wave_steps);
+    flush_stats<COUNT, true>(P, st, nhits, lane, t0, ntiles);
+}
+
+// Kernel 2: Scene::sampleScene shading of the primary hit with shadow rays.
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused, int REC = 0>
+__global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[2048];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    __shared__ float s_ior[REC ? kIorCap * kWG : 1];
+    load_tables(P.tables, s_tab, 1024);
+    const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
+    const uint16_t* rcpT = s_tab;           // per triangle test: LDS
+    const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
+    TravStats st;
+    uint32_t shadow_total = 0, secondary_total = 0;
+    TileSched ts(P, wave, lane);
+    uint32_t ntiles = 0;
+    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
+        if (P.wave_log && lane == 0 && ntiles < kLogTiles)
+        {
+            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
+            r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
+            r[4 + kLogTiles + ntiles] = ts.deq_ticks;
+        }
+        ntiles++;
+        int x, y;
+        size_t slot;
+        if (!item_pixel(P, item, lane, x, y, slot)) {
+            if (MODE == kGen && P.mode != 0) P.nrays[slot] = 0;  // bucket slot outside the frame
+            continue;
+        }
+        float4 hv = P.hits[slot];
+        DHit h{hv.x, hv.y, hv.z, __float_as_int(hv.w)};
+        v3 col;
+        if (h.prim >= 0) {
+            const int f = item_frame(P, item);
+            const CamParams& cam = P.cam[f];
+            const uint32_t seed = P.seed + (uint32_t)f;
+            DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, seed, x, y, rsqT));
+            Shader<POINT_ONLY, FAST, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 0u, seed,
+                                                   slot * (size_t)P.max_shadow, 0u};
+            if constexpr (REC) { S.iorS = s_ior + tid; S.lvl = P.lvl + (blockIdx.x * kWG + tid); }
+            col = S.template shade<COUNT>(r, h);
+            shadow_total += S.shadow_rays;
+            secondary_total += S.secondary;
+            if (MODE == kGen) P.nrays[slot] = (uint8_t)S.nslot;
+        } else if (MODE == kGen) {
+            P.nrays[slot] = 0;
+            continue;
+        } else if (P.env) {  // environment map lookup of the missed ray (src/Scene.cpp:236-239)
+            const int f = item_frame(P, item);
+            const v3 d = camera_dir(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
+            col = scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
+        } else {
+            col = mk(P.bg[0], P.bg[1], P.bg[2]);
+        }
+        if (MODE == kGen) continue;
+        if (P.out_rgb) {
+            float* o = P.out_rgb + 3 * slot;
+            o[0] = col.x; o[1] = col.y; o[2] = col.z;
+        }
+        if (P.out_rgb8) {
+            uint8_t* o8 = P.out_rgb8 + 3 * slot;
+            o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
+        }
+    }
+    flush_secondary(P, secondary_total, lane);
+    flush_stats<COUNT>(P, st, MODE == kResolve ? 0u : shadow_total, lane, t0, ntiles);
+}
+
+// getSum (src/Scene.cpp:245-248): 1^2 + ... + n^2 through the float 1/6
+__device__ __forceinline__ int sum_squares(int n) { return (int)((float)(n * (n + 1) * (2 * n + 1)) * 0.16666667f); }
+
+// Image::linear_to_gammaF[int(min(v, 1) * 32767)] (src/Scene.cpp:278-283).
+// Deviation: a negative / NaN channel (an out-of-bounds read there) uses entry 0.
+__device__ __forceinline__ float gamma_f(const float* lut, float v) {
+    const float c = (v > 1.f) ? 1.f : v;
+    const float f = c * 32767.f;
+    return lut[(f >= 0.f) ? (int)f : 0];
+}
+
+// Kernel 3: Scene::adaptiveSampleScene (src/Scene.cpp:252-293), fused.  One
+// persistent launch; a lane loops over its pixel's eye rays -- the centre
+// sample, then levels 2.. of n x n jittered sub-samples (eyeRayAdaptive with
+// offsets [i/n, (i+1)/n] x [j/n, (j+1)/n], src/Camera.cpp:144-150) -- each
+// through Scene::sampleScene (closest hit, shading with inline shadow rays,
+// environment / background on a miss), with the reference's running mean and
+// gamma-space stop test after every level.  Eye ray k of a pixel draws from
+// RNG stream (pixel, k): ray 0 is the 1-spp frame path's ray.  Lanes of a wave
+// stop independently; the wave runs until its last lane is done.
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST, int REC = 0>
+__global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[2048];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    __shared__ float s_ior[REC ? kIorCap * kWG : 1];
+    load_tables(P.tables, s_tab, 1024);
+    const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
+    const uint16_t* rcpT = s_tab;
+    const uint16_t* rsqT = P.tables + 2048;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
+    TravStats st;
+    uint32_t shadow_total = 0, eye_rays = 0, eye_hits = 0, secondary_total = 0;
+    TileSched ts(P, wave, lane);
+    uint32_t ntiles = 0;
+    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
+        ntiles++;
+        int x, y;
+        size_t slot;
+        if (!item_pixel(P, item, lane, x, y, slot)) continue;
+        const int f = item_frame(P, item);
+        const CamParams& cam = P.cam[f];
+        const uint32_t seed = P.seed + (uint32_t)f;
+        const uint32_t pixel = (uint32_t)(y * cam.W + x);
+        const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
+        const v3 U = mk(cam.u[0], cam.u[1], cam.u[2]), Vv = mk(cam.v[0], cam.v[1], cam.v[2]),
+                 W = mk(cam.w[0], cam.w[1], cam.w[2]);
+        v3 result = mk(0, 0, 0), cur = mk(0, 0, 0);
+        int level = 1, i = 0, j = 0;
+        bool cut = false;
+        for (uint32_t sample = 0;; sample++) {
+            float x0 = 0.5f, x1 = 0.5f, y0 = 0.5f, y1 = 0.5f;
+            if (level > 1) {
+                const float off = 1.0f / (float)level;
+                x0 = (float)i * off; x1 = (float)(i + 1) * off;
+                y0 = (float)j * off; y1 = (float)(j + 1) * off;
+            }
+            const float ur = rng(pixel, sample * 1024u, 0, seed), vr = rng(pixel, sample * 1024u, 1, seed);
+            const float xo = (x1 - x0) * ur + x0, yo = (y1 - y0) * vr + y0;
+            const float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
+            const float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
+            const v3 d = normalized(sub(add(scale(U, Up), scale(Vv, Vp)), W), rsqT);
+            const DRay r = make_ray(eye, d);
+            DHit h{1e12f, 0.f, 0.f, -1};
+            v3 col;
+            eye_rays++;
+            const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
+            if (sample == 0) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
+            if (hit) {
+                eye_hits++;
+                Shader<POINT_ONLY, FAST, INST, kFused, REC> S{P, T, rcpT, rsqT, st, pixel, 0u, seed, 0, 0u};
+                S.sample = sample;
+                if constexpr (REC) { S.iorS = s_ior + tid; S.lvl = P.lvl + (blockIdx.x * kWG + tid); }
+                col = S.template shade<COUNT>(r, h);
+                shadow_total += S.shadow_rays;
+                secondary_total += S.secondary;
+            } else if (P.env) {
+                col = scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
+            } else {
+                col = mk(P.bg[0], P.bg[1], P.bg[2]);
+            }
+            if (level == 1) {
+                result = col;
+                level = 2;
+            } else {
+                cur = add(cur, col);
+                if (++j < level) continue;
+                j = 0;
+                if (++i < level) continue;
+                i = 0;
+                const float pre = (float)sum_squares(level - 1), now = (float)(level * level);
+                const v3 nr = scale(add(scale(result, pre), cur), 1.0f / (pre + now));
+                const float tx = gamma_f(P.gammaF, result.x) - gamma_f(P.gammaF, nr.x);
+                const float ty = gamma_f(P.gammaF, result.y) - gamma_f(P.gammaF, nr.y);
+                const float tz = gamma_f(P.gammaF, result.z) - gamma_f(P.gammaF, nr.z);
+                cut = fmaxf(fabsf(tx), fmaxf(fabsf(ty), fabsf(tz))) < P.noise;
+                result = nr;
+                cur = mk(0, 0, 0);
+                level++;
+            }
+            if (!((level <= P.max_subdivs && !cut) || level <= P.min_subdivs)) break;
+        }
+        if (P.out_rgb) {
+            float* o = P.out_rgb + 3 * slot;
+            o[0] = result.x; o[1] = result.y; o[2] = result.z;
+        }
+        if (P.out_rgb8) {
+            uint8_t* o8 = P.out_rgb8 + 3 * slot;
+            o8[0] = map8(P.gamma, result.x); o8[1] = map8(P.gamma, result.y); o8[2] = map8(P.gamma, result.z);
+        }
+    }
+    unsigned long long er = eye_rays, eh = eye_hits;
+    for (int off = 32; off > 0; off >>= 1) {
+        er += __shfl_down(er, off);
+        eh += __shfl_down(eh, off);
+    }
+    if (lane == 0) {
+        atomicAdd(&P.ctr[CTR_RAYS_P], er);
+        atomicAdd(&P.ctr[CTR_HITS], eh);
+    }
+    flush_secondary(P, secondary_total, lane);
+    flush_stats<COUNT, false>(P, st, shadow_total, lane, t0, ntiles);
+}
+
+using KernelFn = void (*)(RenderParams);
+
+template <template <bool, bool, bool, bool, int> class K, int REC>
+static KernelFn pick4(bool c, bool po, bool f, bool inst) {
+    if (inst) return c ? (f ? K<true, false, true, true, REC>::fn : K<true, false, false, true, REC>::fn)
+                       : (f ? K<false, false, true, true, REC>::fn : K<false, false, false, true, REC>::fn);
+    if (po) return c ? (f ? K<true, true, true, false, REC>::fn : K<true, true, false, false, REC>::fn)
+                     : (f ? K<false, true, true, false, REC>::fn : K<false, true, false, false, REC>::fn);
+    return c ? (f ? K<true, false, true, false, REC>::fn : K<true, false, false, false, REC>::fn)
+             : (f ? K<false, false, true, false, REC>::fn : K<false, false, false, false, REC>::fn);
+}
+template <bool C, bool PO, bool F, bool I, int REC>
+struct ShadeK { static constexpr KernelFn fn = shade_kernel<C, PO, F, I, kFused, REC>; };
+
+// defined in mrt_rec.hip: the fused chain kernels (rec 1: reflection / refraction,
+// 2: + path tracing) and the adaptive supersampling kernels (any rec)
+KernelFn pick_shade_rec(bool c, bool po, bool f, bool inst, int rec);
+KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec);
+// defined in mrt_chain.hip: the wavefront chain engine
+KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec);
+KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec);
+KernelFn pick_chain_trace(bool c, bool f, bool inst);
+KernelFn pick_chain_compact();
+KernelFn pick_chain_finish();
+
+}  // namespace mrt
