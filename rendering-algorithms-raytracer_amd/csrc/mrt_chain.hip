@@ -22,9 +22,12 @@
 //            ends the path with the environment (or nothing, a GI ray without
 //            environment sampling), a hit runs Shader::level, which ends it or
 //            spawns again;
-//   finish   per pixel: each path's final value is folded up its chain with
-//            chain_combine (deepest first, the parent indices), the paths are
-//            averaged and the pixel written (float RGB + Image::Map 8-bit).
+//   resolve  (after the last level) every level shaded again with its shadow
+//            answers: level records and final values;
+//   path     per path: the final value folded up its chain with
+//            chain_combine (deepest first, the parent indices);
+//   finish   per pixel: the paths averaged and the pixel written (float RGB +
+//            Image::Map 8-bit).
 //
 // Every ray, every RNG draw (keyed by pixel, path and level) and every add is
 // the fused kernel's, so the two engines give bit-identical frames
@@ -49,6 +52,12 @@ __device__ __forceinline__ void unpack_state(uint32_t w, ChainState& cs, bool& e
 }
 
 __device__ __forceinline__ size_t lvl_off(const RenderParams& P, int k) { return (size_t)k * P.ch_cap; }
+// level record of entry e of level k: lvl_words consecutive floats (the combine
+// walks one path's chain, so a record is read as a unit)
+__device__ __forceinline__ ChainRec chain_rec(const RenderParams& P, int k, uint32_t e) {
+    return ChainRec{P.ch_rec + ((size_t)k * P.ch_cap + e) * (size_t)P.lvl_words, 1};
+}
+static constexpr uint32_t kDeadPath = 0xFFFFFFFFu;   // ch_te of a path whose camera ray missed
 
 // A spawned child at sparse slot s: its ray, state word and the IOR column
 // (the child's history, written by Shader::level).
@@ -68,12 +77,19 @@ __device__ __forceinline__ void write_final(const RenderParams& P, uint32_t path
     P.ch_te[path_id] = entry;
 }
 
+// shadow-ray slots of chain level k (each level keeps its own until the resolve pass)
+__device__ __forceinline__ size_t shadow_base(const RenderParams& P, int k) {
+    return (size_t)k * P.ch_cap * (size_t)P.max_shadow;
+}
+
 // Level 0 of every path of a chunk's pixels (tile schedule over the chunk's
 // work items).  Path id = (work item of the chunk * 64 + lane) * num_paths + path.
-// MODE kGen writes each path's shadow rays (slots p * max_shadow + j, count in
-// nrays[p]); kResolve runs the same shading with shadow_kernel's answers and
-// writes the path's final value or its spawned child.  No traversal runs in
-// either, so the shading state never has to live across one.
+// MODE kGen writes each path's shadow rays (level-0 slots p * max_shadow + j,
+// count in nrays[p]) and its spawned child (the spawn decision, the child ray
+// and its IOR history do not depend on the shadow answers); kResolve runs the
+// same shading with the answers and writes the level record or the path's
+// final value.  No traversal runs in either, so the shading state never has to
+// live across one.
 template <bool POINT_ONLY, bool INST, int REC, int MODE>
 __global__ void __launch_bounds__(kWG) chain0_kernel(RenderParams P) {
     __shared__ float s_ior[kIorCap * kWG];
@@ -95,10 +111,12 @@ __global__ void __launch_bounds__(kWG) chain0_kernel(RenderParams P) {
         }
         const uint32_t pbase = ((uint32_t)item * 64u + (uint32_t)lane) * (uint32_t)P.num_paths;
         if (!valid || h.prim < 0) {   // nothing to shade: no shadow rays, no spawns (finish writes env / background)
-            for (int path = 0; path < P.num_paths; path++) {
-                if (MODE == kGen) P.nrays[pbase + path] = 0;
-                else P.ch_flag[pbase + path] = 0;
-            }
+            if (MODE == kGen)
+                for (int path = 0; path < P.num_paths; path++) {
+                    P.nrays[pbase + path] = 0;
+                    P.ch_flag[pbase + path] = 0;
+                    P.ch_te[pbase + path] = kDeadPath;
+                }
             continue;
         }
         const int f = item_frame(P, P.item_base + item);
@@ -115,20 +133,22 @@ __global__ void __launch_bounds__(kWG) chain0_kernel(RenderParams P) {
             S.nslot = 0;
             ChainState cs;
             LevelOut o;
-            S.template level<false>(r, h, cs, icam, ChainRec{P.ch_rec + p, P.ch_cap}, o);
+            S.template level<false>(r, h, cs, icam, chain_rec(P, 0, p), o);
             if (MODE == kGen) {
                 P.nrays[p] = (uint8_t)S.nslot;
-            } else {
                 if (o.spawn) write_spawn(P, p, o, p, cs, S.iorS);
-                else write_final(P, p, o.val, 0, false, p);
                 P.ch_flag[p] = o.spawn ? 1 : 0;
+            } else if (!o.spawn) {
+                write_final(P, p, o.val, 0, false, p);
             }
         }
         shadow_total += S.shadow_rays;
         secondary_total += S.secondary;
     }
-    if (MODE == kGen) flush_stats<false>(P, st, shadow_total, lane, 0, 0);
-    else flush_secondary(P, secondary_total, lane);
+    if (MODE == kGen) {
+        flush_stats<false>(P, st, shadow_total, lane, 0, 0);
+        flush_secondary(P, secondary_total, lane);
+    }
 }
 
 // Spawn slots of level k (P.ch_level) -> dense entries of level k + 1.  A
@@ -180,29 +200,48 @@ __global__ void __launch_bounds__(kWG) chain_compact_kernel(RenderParams P) {
     }
 }
 
-// Closest hit of every entry of level P.ch_level (64 consecutive entries per wave step).
+// One launch per chain level k = P.ch_level: the closest hits of level k's
+// entries (nA of them; the children spawned by level k - 1) and the any-hit
+// answers of level k - 1's shadow rays (nB slots), which no longer wait for
+// each other -- a level's resolve needs its shadow answers only at the end of
+// the chunk.  Wave-uniform 64-slot chunks, the closest-hit chunks first.
 template <bool COUNT, bool FAST, bool INST>
 __global__ void __launch_bounds__(kWG) chain_trace_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     const int k = P.ch_level;
-    const uint32_t n = P.ch_cnt[k];
-    if ((uint32_t)blockIdx.x * kWG >= n) return;   // the block has no entries (before any barrier)
+    const uint32_t nA = k < P.ch_levels ? P.ch_cnt[k] : 0u;
+    const uint32_t m = (uint32_t)P.max_shadow;
+    const uint32_t nprev = k == 1 ? (uint32_t)P.n_tiles * 64u * (uint32_t)P.num_paths : P.ch_cnt[k - 1];
+    const uint32_t nB = nprev * m;
+    const uint32_t chA = (nA + 63u) >> 6, chunks = chA + ((nB + 63u) >> 6);
+    const uint32_t wave_id = (uint32_t)blockIdx.x * (kWG / 64) + (uint32_t)(threadIdx.x >> 6);
+    if ((uint32_t)blockIdx.x * (kWG / 64) >= chunks) return;   // the block has no chunks (before any barrier)
     load_tables(P.tables, s_tab, 1024);
     const int tid = threadIdx.x, lane = tid & 63;
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, s_tab, s_stack + tid,
            P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     TravStats st;
-    const size_t base = lvl_off(P, k), cap = P.ch_cap;
-    for (uint32_t e0 = (uint32_t)blockIdx.x * kWG + (uint32_t)(tid & ~63); e0 < n; e0 += gridDim.x * (uint32_t)kWG) {
-        const uint32_t e = e0 + (uint32_t)lane;
-        if (e >= n) continue;
-        const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
-        const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
-        DHit h{1e12f, 0.f, 0.f, -1};
-        const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
-        P.ch_hit[base + e] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
+    const size_t base = lvl_off(P, k), cap = P.ch_cap, sb = shadow_base(P, k - 1);
+    const uint8_t* nrays = P.nrays + (size_t)(k - 1) * cap;
+    for (uint32_t c = wave_id; c < chunks; c += gridDim.x * (kWG / 64)) {
+        if (c < chA) {   // closest hit of entry e
+            const uint32_t e = (c << 6) + (uint32_t)lane;
+            if (e >= nA) continue;
+            const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
+            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
+            DHit h{1e12f, 0.f, 0.f, -1};
+            const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
+            P.ch_hit[base + e] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
+        } else {         // shadow ray j of level k - 1's entry (or path) s, any hit
+            const uint32_t i = ((c - chA) << 6) + (uint32_t)lane, s = i / m;
+            if (i >= nB || i - s * m >= (uint32_t)nrays[s]) continue;
+            const float4 o = P.ray_o[sb + i], d = P.ray_d[sb + i];
+            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
+            DHit h{o.w, 0.f, 0.f, -1};
+            P.occl[sb + i] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
+        }
     }
     if (COUNT) {
         unsigned long long nv = st.nodes, lv = st.leaves;
@@ -218,91 +257,117 @@ __global__ void __launch_bounds__(kWG) chain_trace_kernel(RenderParams P) {
     if (st.overflow) atomicOr(&P.ctr[CTR_OVERFLOW], 1ull);
 }
 
-// Level P.ch_level (>= 1) of every entry: a missed child ends its path with the
-// environment (or nothing), a hit is shaded by Shader::level -- MODE kGen
-// writes its shadow rays (slots e * max_shadow + j), kResolve shades with the
-// answers and ends the path or spawns again.
+// Shading of chain level k >= 1.  kGen (one launch per level, k =
+// P.ch_level): every entry that hit writes its shadow rays (level-k slots
+// e * max_shadow + j) and its spawned child.  kResolve (one launch per chunk,
+// all levels 1 .. ch_levels - 1): a missed child ends its path with the
+// environment (or nothing: a GI ray without environment sampling), a hit is
+// shaded again with its shadow answers and writes its level record or the
+// path's final value.
 template <bool POINT_ONLY, bool INST, int REC, int MODE>
 __global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
     __shared__ float s_ior[kIorCap * kWG];
-    const int k = P.ch_level;
-    const uint32_t n = P.ch_cnt[k];
     const uint16_t* rcpT = P.tables;
     const uint16_t* rsqT = P.tables + 2048;
     const int tid = threadIdx.x, lane = tid & 63;
     Trav T{P.nodes, false, false, P.leaves, rcpT, nullptr, nullptr, P.gstride};   // unused: no traversal
     TravStats st;
     uint32_t shadow_total = 0, secondary_total = 0;
-    const size_t base = lvl_off(P, k), cap = P.ch_cap;
+    const size_t cap = P.ch_cap;
     const uint32_t np = (uint32_t)P.num_paths;
     float* iorS = s_ior + tid;
-    for (uint32_t e0 = (uint32_t)blockIdx.x * kWG + (uint32_t)(tid & ~63); e0 < n; e0 += gridDim.x * (uint32_t)kWG) {
-        const uint32_t e = e0 + (uint32_t)lane;
-        if (e >= n) continue;
-        const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
-        const uint32_t p = __float_as_uint(o.w);
-        ChainState cs;
-        bool env_miss;
-        unpack_state(__float_as_uint(d.w), cs, env_miss);
-        cs.depth = k;
-        const float4 hv = P.ch_hit[base + e];
-        const DHit h{hv.x, hv.y, hv.z, __float_as_int(hv.w)};
-        if (h.prim < 0) {   // the child missed: environment (Lr / Lt, or GI with sampleEnv) or nothing
-            if (MODE == kGen) {
-                P.nrays[e] = 0;
-            } else {
-                write_final(P, p, env_miss ? env_or_bg(P, mk(d.x, d.y, d.z)) : mk(0, 0, 0), k, !env_miss, e);
-                P.ch_flag[e] = 0;
+    const int k0 = MODE == kGen ? P.ch_level : 1, k1 = MODE == kGen ? P.ch_level + 1 : P.ch_levels;
+    for (int k = k0; k < k1; k++) {
+        const uint32_t n = P.ch_cnt[k];
+        const size_t base = lvl_off(P, k);
+        for (uint32_t e0 = (uint32_t)blockIdx.x * kWG + (uint32_t)(tid & ~63); e0 < n; e0 += gridDim.x * (uint32_t)kWG) {
+            const uint32_t e = e0 + (uint32_t)lane;
+            if (e >= n) continue;
+            const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
+            const uint32_t p = __float_as_uint(o.w);
+            ChainState cs;
+            bool env_miss;
+            unpack_state(__float_as_uint(d.w), cs, env_miss);
+            cs.depth = k;
+            const float4 hv = P.ch_hit[base + e];
+            const DHit h{hv.x, hv.y, hv.z, __float_as_int(hv.w)};
+            if (h.prim < 0) {   // the child missed: environment (Lr / Lt, or GI with sampleEnv) or nothing
+                if (MODE == kGen) {
+                    P.nrays[(size_t)k * cap + e] = 0;
+                    P.ch_flag[e] = 0;
+                } else {
+                    write_final(P, p, env_miss ? env_or_bg(P, mk(d.x, d.y, d.z)) : mk(0, 0, 0), k, !env_miss, e);
+                }
+                continue;
             }
-            continue;
+            // the pixel of path p (RNG key, frame of a batched launch)
+            const uint32_t pl = p / np, path = p - pl * np;
+            int x, y;
+            size_t slot;
+            item_pixel(P, P.item_base + (int)(pl >> 6), (int)(pl & 63u), x, y, slot);
+            const int f = item_frame(P, P.item_base + (int)(pl >> 6));
+            const float4 i0 = P.ch_ior[2 * base + e], i1 = P.ch_ior[2 * base + cap + e];
+            iorS[0] = 1.0f;
+            iorS[1 * kWG] = i0.x; iorS[2 * kWG] = i0.y; iorS[3 * kWG] = i0.z; iorS[4 * kWG] = i0.w;
+            iorS[5 * kWG] = i1.x; iorS[6 * kWG] = i1.y; iorS[7 * kWG] = i1.z;
+            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
+            Shader<POINT_ONLY, false, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * P.cam[f].W + x), 0u,
+                                                        P.seed + (uint32_t)f,
+                                                        shadow_base(P, k) + (size_t)e * (size_t)P.max_shadow, 0u};
+            S.iorS = iorS;
+            S.skey = path;
+            typename Shader<POINT_ONLY, false, INST, MODE, REC>::IorCam icam;   // unused below the camera ray
+            LevelOut lo;
+            S.template level<false>(r, h, cs, icam, chain_rec(P, k, e), lo);
+            shadow_total += S.shadow_rays;
+            secondary_total += S.secondary;
+            if (MODE == kGen) {
+                P.nrays[(size_t)k * cap + e] = (uint8_t)S.nslot;
+                const bool spawn = lo.spawn && k + 1 < P.ch_levels;
+                if (spawn) write_spawn(P, e, lo, p, cs, iorS);
+                P.ch_flag[e] = spawn ? 1 : 0;
+            } else if (lo.spawn && k + 1 >= P.ch_levels) {   // deeper than the chain bound (cannot happen)
+                atomicOr(&P.ctr[CTR_OVERFLOW], 2ull);
+                write_final(P, p, mk(0, 0, 0), k, false, e);
+            } else if (!lo.spawn) {
+                write_final(P, p, lo.val, k, false, e);
+            }
         }
-        // the pixel of path p (RNG key, frame of a batched launch)
-        const uint32_t pl = p / np, path = p - pl * np;
-        int x, y;
-        size_t slot;
-        item_pixel(P, P.item_base + (int)(pl >> 6), (int)(pl & 63u), x, y, slot);
-        const int f = item_frame(P, P.item_base + (int)(pl >> 6));
-        const float4 i0 = P.ch_ior[2 * base + e], i1 = P.ch_ior[2 * base + cap + e];
-        iorS[0] = 1.0f;
-        iorS[1 * kWG] = i0.x; iorS[2 * kWG] = i0.y; iorS[3 * kWG] = i0.z; iorS[4 * kWG] = i0.w;
-        iorS[5 * kWG] = i1.x; iorS[6 * kWG] = i1.y; iorS[7 * kWG] = i1.z;
-        const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
-        Shader<POINT_ONLY, false, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * P.cam[f].W + x), 0u,
-                                                    P.seed + (uint32_t)f, (size_t)e * (size_t)P.max_shadow, 0u};
-        S.iorS = iorS;
-        S.skey = path;
-        typename Shader<POINT_ONLY, false, INST, MODE, REC>::IorCam icam;   // unused below the camera ray
-        LevelOut lo;
-        S.template level<false>(r, h, cs, icam, ChainRec{P.ch_rec + (size_t)k * P.lvl_words * cap + e, cap}, lo);
-        shadow_total += S.shadow_rays;
-        secondary_total += S.secondary;
-        if (MODE == kGen) {
-            P.nrays[e] = (uint8_t)S.nslot;
-            continue;
-        }
-        bool spawn = false;
-        if (lo.spawn && k + 1 >= P.ch_levels) {   // deeper than the chain bound (cannot happen)
-            atomicOr(&P.ctr[CTR_OVERFLOW], 2ull);
-            write_final(P, p, mk(0, 0, 0), k, false, e);
-        } else if (lo.spawn) {
-            write_spawn(P, e, lo, p, cs, iorS);
-            spawn = true;
-        } else {
-            write_final(P, p, lo.val, k, false, e);
-        }
-        P.ch_flag[e] = spawn ? 1 : 0;
     }
-    if (MODE == kGen) flush_stats<false>(P, st, shadow_total, lane, 0, 0);
-    else flush_secondary(P, secondary_total, lane);
+    if (MODE == kGen) {
+        flush_stats<false>(P, st, shadow_total, lane, 0, 0);
+        flush_secondary(P, secondary_total, lane);
+    }
 }
 
-// Per pixel of the chunk: each path's value folded up its chain (deepest
-// first), the paths averaged as Scene::sampleScene does (src/Scene.cpp:224-233);
-// a missed camera ray takes the environment / background.
+// One lane per path of the chunk: the path's final value folded up its chain
+// with chain_combine, deepest level first (Blinn::shade's returns), into ch_tv.
+__global__ void __launch_bounds__(kWG) chain_path_kernel(RenderParams P) {
+    const size_t cap = P.ch_cap;
+    const uint32_t n = (uint32_t)P.n_tiles * 64u * (uint32_t)P.num_paths;
+    for (uint32_t p = blockIdx.x * kWG + threadIdx.x; p < n; p += gridDim.x * kWG) {
+        uint32_t e = P.ch_te[p];
+        if (e == kDeadPath) continue;
+        const float4 tv = P.ch_tv[p];
+        const uint32_t bits = __float_as_uint(tv.w);
+        v3 val = mk(tv.x, tv.y, tv.z);
+        bool none = (bits >> 8) & 1u;
+        for (int kk = (int)(bits & 255u) - 1; kk >= 0; kk--) {
+            const uint32_t pe = __float_as_uint(P.ch_ior[2 * lvl_off(P, kk + 1) + cap + e].w);   // parent entry
+            val = chain_combine(P, chain_rec(P, kk, pe), val, none);
+            none = false;
+            e = pe;
+        }
+        P.ch_tv[p] = make_float4(val.x, val.y, val.z, 0.f);
+    }
+}
+
+// Per pixel of the chunk: the paths' values summed in path order and averaged
+// as Scene::sampleScene does (src/Scene.cpp:224-233); a missed camera ray takes
+// the environment / background.  Float RGB + Image::Map 8-bit.
 __global__ void __launch_bounds__(kWG) chain_finish_kernel(RenderParams P) {
     const int tid = threadIdx.x, lane = tid & 63;
     const uint16_t* rsqT = P.tables + 2048;
-    const size_t cap = P.ch_cap;
     const uint32_t np = (uint32_t)P.num_paths;
     for (int item = (int)(blockIdx.x * (kWG / 64) + (tid >> 6)); item < P.n_tiles; item += (int)(gridDim.x * (kWG / 64))) {
         int x, y;
@@ -314,19 +379,8 @@ __global__ void __launch_bounds__(kWG) chain_finish_kernel(RenderParams P) {
             v3 result = mk(0, 0, 0);
             const uint32_t pbase = ((uint32_t)item * 64u + (uint32_t)lane) * np;
             for (uint32_t path = 0; path < np; path++) {
-                const uint32_t p = pbase + path;
-                const float4 tv = P.ch_tv[p];
-                const uint32_t bits = __float_as_uint(tv.w);
-                v3 val = mk(tv.x, tv.y, tv.z);
-                bool none = (bits >> 8) & 1u;
-                uint32_t e = P.ch_te[p];
-                for (int kk = (int)(bits & 255u) - 1; kk >= 0; kk--) {
-                    const uint32_t pe = __float_as_uint(P.ch_ior[2 * lvl_off(P, kk + 1) + cap + e].w);   // parent entry
-                    val = chain_combine(P, ChainRec{P.ch_rec + (size_t)kk * P.lvl_words * cap + pe, cap}, val, none);
-                    none = false;
-                    e = pe;
-                }
-                result = add(result, val);
+                const float4 v = P.ch_tv[pbase + path];
+                result = add(result, mk(v.x, v.y, v.z));
             }
             col = scale(result, 1.0f / (float)P.num_paths);
         } else {
@@ -371,5 +425,6 @@ KernelFn pick_chain_trace(bool c, bool f, bool inst) {
 }
 KernelFn pick_chain_compact() { return chain_compact_kernel; }
 KernelFn pick_chain_finish() { return chain_finish_kernel; }
+KernelFn pick_chain_path() { return chain_path_kernel; }
 
 }  // namespace mrt

@@ -444,7 +444,7 @@ static int g_shadow_sched = -1;   // shadow_kernel schedule: 0 grid-stride, 1 XC
                                   // -1 auto: refill for dome-light (incoherent) rays of uninstanced scenes, else bands
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
-static int g_chain_mb = 4096;     // chain scratch per stream (MB); larger frames run in chunks of work items
+static int g_chain_mb = 16384;    // chain scratch per stream (MB); larger frames run in chunks of work items
 
 static inline int fast_box(const DeviceState& d);
 
@@ -847,7 +847,7 @@ static KernelFn pick_shade(bool c, bool po, bool f, bool inst, int rec) {
 // per-pixel combine.  P holds the primary launch's parameters (hits, outputs,
 // cameras, work items); the chunks are sized so the per-level arrays fit
 // g_chain_mb.
-static constexpr int kMaxChainLevels = 64;
+static constexpr int kMaxChainLevels = 63;   // < the 64 level counts (level L's count stays 0)
 // shadow rays one chain level of one path traces at most: every light's
 // samples for the direct term, again for translucency, again for the last GI
 // bounce (0: more than the u8 ray count holds -> fused kernel)
@@ -866,16 +866,16 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     DeviceState& d = *s.dev;
     const int L = chain_levels(s), W = level_words(s), m = chain_shadow_rays(s);
     const size_t per_item = (size_t)64 * (size_t)P0.num_paths;
-    // per path slot: L x (ray, ior 2 x 16 B each, hit 16 B, record), spawn 64 B, final 16 + 4 B, flag,
-    // shadow rays m x (32 B + occlusion byte) + ray count
-    const size_t slot_bytes = (size_t)L * (2 * 16 + 2 * 16 + 16 + 4 * (size_t)W) + 4 * 16 + 16 + 4 + 1 + (size_t)m * 33 + 1;
+    // per path slot: L x (ray, ior 2 x 16 B each, hit 16 B, record, shadow rays m x (32 B + occlusion
+    // byte) + ray count), spawn 64 B, final 16 + 4 B, flag
+    const size_t slot_bytes = (size_t)L * (2 * 16 + 2 * 16 + 16 + 4 * (size_t)W + (size_t)m * 33 + 1) + 4 * 16 + 16 + 4 + 1;
     const size_t budget = (size_t)g_chain_mb << 20;
     size_t items = std::max<size_t>(1, budget / (slot_bytes * per_item));
     items = std::min(items, (size_t)P0.n_tiles);
     const size_t cap = items * per_item;
-    if (cap * (size_t)m >= (size_t(1) << 32)) { set_error("chain chunk too large"); return MRT_ERR_INVALID; }
+    if (cap * (size_t)m * (size_t)L >= (size_t(1) << 32)) { set_error("chain chunk too large"); return MRT_ERR_INVALID; }
     int rc;
-    if ((rc = ensure_rays(c, cap, (size_t)m))) return rc;
+    if ((rc = ensure_rays(c, cap * (size_t)L, (size_t)m))) return rc;   // every level keeps its shadow rays
     // layout: ray | ior | hit | sp | tv (float4), rec (float), te (u32), control (counts + queues), flag (u8)
     const size_t ctl = 256 + (size_t)(L + 2) * 1024;
     const size_t n4 = (size_t)L * 2 * cap + (size_t)L * 2 * cap + (size_t)L * cap + 4 * cap + cap;
@@ -904,7 +904,7 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     Q.order = 0;          // chunks index work items directly
     Q.wave_log = nullptr;
     Q.ray_o = c.rays;
-    Q.ray_d = c.rays + cap * (size_t)m;
+    Q.ray_d = c.rays + cap * (size_t)L * (size_t)m;
     Q.occl = c.occl;
     Q.nrays = c.nrays;
     Q.max_shadow = m;
@@ -912,50 +912,36 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive), r0 = pick_chain0(true, d.point_only, inst, d.recursive);
     const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive),
                    rk = pick_chain_shade(true, d.point_only, inst, d.recursive);
-    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, fb, inst), kf = pick_chain_finish();
-    const ShadowFn sf = pick_shadow(count, fb, inst);
+    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, fb, inst), kf = pick_chain_finish(),
+                   kp = pick_chain_path();
     auto go = [&](KernelFn f, int g) -> int {
         void* args[] = {&Q};
         HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(f), dim3(std::max(1, g)), dim3(kWG), args, 0, stream));
         return MRT_OK;
     };
     auto full = [&](KernelFn f) { return std::min(d.grid, d.cus * blocks_per_cu(f, 0)); };
-    bool dome = false;
-    for (const DevLight& l : s.lights) dome |= l.type == MRT_DOME_LIGHT;
-    int sg = std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(sf), 0));
-    int sched = g_shadow_sched >= 0 ? g_shadow_sched : (dome && !inst ? 2 : 1), refill = g_refill_min;
-    if (sched && (sg & 7)) sg &= ~7;   // XCD bands need a whole number of workgroups per XCD
-    if (sg < 8) sched = 0;
-    auto shadows = [&](size_t n_rays, const uint32_t* count_dev, unsigned int* q) -> int {
-        Q.sh_count = count_dev;
-        Q.queue = q;
-        void* args[] = {&Q, &n_rays, &sched, &refill};
-        HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(sf), dim3(std::max(1, sg)), dim3(kWG), args, 0, stream));
-        Q.sh_count = nullptr;
-        return MRT_OK;
-    };
     for (size_t b = 0; b < (size_t)P0.n_tiles; b += items) {
         const int n = (int)std::min(items, (size_t)P0.n_tiles - b);
-        const size_t paths = (size_t)n * per_item;
         Q.item_base = (int32_t)b;
         Q.n_tiles = n;
         HIP_OK(hipMemsetAsync(Q.ch_cnt, 0, ctl, stream));
-        Q.ch_level = 0;
         const int g0n = std::min(full(r0), (n + 3) / 4);
+        Q.ch_level = 0;
         Q.queue = queues;
-        if ((rc = go(g0, g0n))) return rc;
-        if ((rc = shadows(paths * (size_t)m, nullptr, queues + 256))) return rc;
-        Q.queue = queues + 2 * 256;
-        if ((rc = go(r0, g0n))) return rc;
+        if ((rc = go(g0, g0n))) return rc;                 // level 0: shadow rays + children
         for (int k = 0; k + 1 < L; k++) {
             Q.ch_level = k;
-            if ((rc = go(kc, full(kc)))) return rc;
+            if ((rc = go(kc, full(kc)))) return rc;        // children of level k -> entries of level k + 1
             Q.ch_level = k + 1;
-            if ((rc = go(kt, full(kt)))) return rc;
-            if ((rc = go(gk, full(gk)))) return rc;
-            if ((rc = shadows(cap * (size_t)m, Q.ch_cnt + k + 1, queues + (size_t)(k + 3) * 256))) return rc;
-            if ((rc = go(rk, full(rk)))) return rc;
+            if ((rc = go(kt, full(kt)))) return rc;        // their closest hits + level k's shadow rays
+            if ((rc = go(gk, full(gk)))) return rc;        // level k + 1: shadow rays + children
         }
+        Q.ch_level = L;
+        if ((rc = go(kt, full(kt)))) return rc;            // the last level's shadow rays
+        Q.queue = queues + 256;
+        if ((rc = go(r0, g0n))) return rc;                 // resolve level 0, then levels 1 .. L - 1
+        if ((rc = go(rk, full(rk)))) return rc;
+        if ((rc = go(kp, full(kp)))) return rc;            // fold each path up its chain
         if ((rc = go(kf, std::min(d.grid, (n + 3) / 4)))) return rc;
     }
     return MRT_OK;

@@ -1121,5 +1121,6 @@ KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec);
 KernelFn pick_chain_trace(bool c, bool f, bool inst);
 KernelFn pick_chain_compact();
 KernelFn pick_chain_finish();
+KernelFn pick_chain_path();
 
 }  // namespace mrt

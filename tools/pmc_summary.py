@@ -22,7 +22,11 @@ import re
 from collections import defaultdict
 
 PASS = {"primary_kernel": "primary", "shade1_kernel": "shade", "shade_kernel": "shade", "shadow_kernel": "shade",
-        "adaptive_kernel": "shade"}
+        "adaptive_kernel": "shade", "chain_trace_kernel": "shade", "chain0_kernel": "shade",
+        "chain_shade_kernel": "shade", "chain_compact_kernel": "shade", "chain_finish_kernel": "shade"}
+# kernels without a COUNT template argument: the instrumented frame runs the same
+# instantiation, so their dispatches are averaged over every frame
+NO_COUNT_ARG = {"chain0_kernel", "chain_shade_kernel", "chain_compact_kernel", "chain_finish_kernel"}
 
 
 def parse_name(name):
@@ -62,17 +66,33 @@ def summarise(cfg, root):
                 base, r.get("Calls"), float(r.get("AverageNs", 0)), float(r.get("TotalDurationNs", 0)), targs))
     per = counters(root)
     passes = defaultdict(float)
-    lines.append("PMC (mean per dispatch):")
+    # frames in each PMC pass: one primary_kernel (or adaptive_kernel) dispatch per frame
+    def frames(counter, timed_only):
+        n = 0
+        for k, cs in per.items():
+            base, targs = parse_name(k)
+            if base in ("primary_kernel", "adaptive_kernel") and cs.get(counter):
+                if not timed_only or targs.split(",")[0].strip() == "false":
+                    n += len(cs[counter])
+        return max(1, n)
+    lines.append("PMC (mean per dispatch; per-frame pass totals below):")
     for k in sorted(per):
         base, targs = parse_name(k)
         cs = per[k]
         f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) if cs.get("FETCH_SIZE") else None
         w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) if cs.get("WRITE_SIZE") else None
-        lines.append("    %-34s FETCH_SIZE %s KiB  WRITE_SIZE %s KiB  [%s]" % (
-            base, "-" if f is None else "%.1f" % f, "-" if w is None else "%.1f" % w, targs))
-        timed = targs.split(",")[0].strip() == "false"
-        if timed and base in PASS and f is not None and w is not None:
-            passes[PASS[base]] += 2 * f * 1024 + w * 1024
+        lines.append("    %-34s FETCH_SIZE %s KiB  WRITE_SIZE %s KiB  dispatches %s  [%s]" % (
+            base, "-" if f is None else "%.1f" % f, "-" if w is None else "%.1f" % w,
+            len(cs.get("FETCH_SIZE") or cs.get("WRITE_SIZE") or []), targs))
+        if base not in PASS or f is None or w is None:
+            continue
+        every = base in NO_COUNT_ARG
+        if not every and targs.split(",")[0].strip() != "false":
+            continue   # the instrumented (COUNT = true) launch
+        # bytes per frame: all of this kernel's dispatches over the frames they ran in
+        fb = sum(cs["FETCH_SIZE"]) / frames("FETCH_SIZE", not every)
+        wb = sum(cs["WRITE_SIZE"]) / frames("WRITE_SIZE", not every)
+        passes[PASS[base]] += 2 * fb * 1024 + wb * 1024
     for p, b in sorted(passes.items()):
         lines.append("    pass %-8s hbm_bytes_per_launch %16.0f   (2*FETCH_SIZE + WRITE_SIZE)" % (p, b))
     return lines, {p: int(b) for p, b in passes.items()}
@@ -87,7 +107,8 @@ def main():
     out = json.load(open(a.json)) if os.path.exists(a.json) else {}
     out.setdefault("configs", {})
     out.setdefault("source", {})
-    out["formula"] = "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per dispatch (gfx950 FETCH_SIZE half-count correction)"
+    out["formula"] = ("2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per frame, summed over the pass's dispatches "
+                      "(gfx950 FETCH_SIZE half-count correction)")
     for d in sorted(glob.glob(os.path.join(a.root, "*"))):
         if not os.path.isdir(d):
             continue
