@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 4
+#define MRT_ABI_VERSION 5
 
 enum {
     MRT_OK = 0,
@@ -73,10 +73,18 @@ typedef struct {
                                 mrt_scene_add_texture (-1 for the other lights)        */
 } mrt_light;
 
-/* Camera (src/Camera.h:26-45): eye, lookAt, up, vertical FOV in degrees. */
+/* Camera (src/Camera.h:26-45): eye, lookAt, up, vertical FOV in degrees, and
+ * the lens of Camera::eyeRayAdaptive (src/Camera.cpp:153-174; ABI 5):
+ * aperture < 0.001 (epsilon) is a pinhole; otherwise rays start on a
+ * rejection-sampled disc of radius aperture and pass through the point at
+ * distance focus_plane along the pinhole direction (setAperture / setFocusPlane,
+ * reference defaults 0 and 1).  shutter_speed scales getTimeSample's
+ * time = 1 - r^3 * shutter_speed (src/Camera.h:44-46, default 0.001), the ray
+ * time of motion-blurred objects. */
 typedef struct {
     float eye[3], look_at[3], up[3];
     float fov_deg;
+    float aperture, focus_plane, shutter_speed;
 } mrt_camera;
 
 /* Raw triangle mesh (TriangleMesh arrays, src/TriangleMesh.h:36-47).  The

@@ -1139,6 +1139,7 @@ typedef struct {
     uint64_t shadow_rays, nodes, leaves;
     uint64_t secondary_rays;        /* reflection / refraction / path-tracing GI rays */
     uint32_t shadow_mask;
+    float time;                     /* the camera ray's time (getTimeSample), inherited by every ray of it */
 } shade_ctx;
 
 /* Counter RNG keys: every shade() call (one chain level of one path) draws from
@@ -1540,7 +1541,12 @@ static v3 shade_hit(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior,
 }
 
 /* ---------------------------------------------------------------- camera */
-typedef struct { v3 eye, u, v, w; float left, right, bottom, top; int W, H; } cam_basis;
+typedef struct {
+    v3 eye, u, v, w;
+    float left, right, bottom, top;
+    int W, H;
+    float aperture, focus, shutter;
+} cam_basis;
 
 /* Camera::setEye/setLookAt/setUp + eyeRayAdaptive basis, src/Camera.h:82-124,
  * src/Camera.cpp:116-137 */
@@ -1559,25 +1565,36 @@ static cam_basis camera_basis(const oro_camera* cam, int W, int H) {
     b.bottom = -b.top;
     b.left = -b.right;
     b.W = W; b.H = H;
+    b.aperture = cam->aperture;
+    b.focus = cam->focusPlane;
+    b.shutter = cam->shutterSpeed;
     return b;
 }
-/* eyeRayAdaptive (aperture 0), src/Camera.cpp:138-157; offsets (0.5, 0.5). */
-static ray_t camera_ray_adaptive(const cam_basis* b, int x, int y, float minX, float maxX, float minY, float maxY,
-                                 float urand, float vrand) {
+/* Camera::eyeRayAdaptive, src/Camera.cpp:116-174: the two jitter draws over
+ * [minX, maxX] x [minY, maxY], the getTimeSample draw (src/Camera.h:46,
+ * time = 1 - r^3 * shutter), then for m_aperture >= epsilon the lens point
+ * rejection-sampled from the unit disc (1.0 - 2 * getRand per coordinate) and the
+ * ray from it through the focal point at m_focusPlane along the pinhole ray. */
+static ray_t eye_ray(shade_ctx* c, const cam_basis* b, int x, int y, float minX, float maxX, float minY, float maxY) {
+    float urand = next_rand(c), vrand = next_rand(c);
+    const float tr = next_rand(c);
+    c->time = 1.f - ((tr * tr) * tr) * b->shutter;
     float xOffset = (maxX - minX) * urand + minX;   /* src/Camera.cpp:146-147 */
     float yOffset = (maxY - minY) * vrand + minY;
     float U = b->left + (b->right - b->left) * (((float)x + xOffset) / (float)b->W);
     float Vp = b->bottom + (b->top - b->bottom) * (((float)y + yOffset) / (float)b->H);
     v3 dir = vnormalized(vsub(vadd(vscale(b->u, U), vscale(b->v, Vp)), b->w));
-    return make_ray(b->eye, dir);
-}
-static ray_t camera_ray(const cam_basis* b, int x, int y, float urand, float vrand) {
-    float xOffset = (0.5f - 0.5f) * urand + 0.5f;
-    float yOffset = (0.5f - 0.5f) * vrand + 0.5f;
-    float U = b->left + (b->right - b->left) * (((float)x + xOffset) / (float)b->W);
-    float Vp = b->bottom + (b->top - b->bottom) * (((float)y + yOffset) / (float)b->H);
-    v3 dir = vnormalized(vsub(vadd(vscale(b->u, U), vscale(b->v, Vp)), b->w));
-    return make_ray(b->eye, dir);
+    if (!(b->aperture >= 0.001f)) return make_ray(b->eye, dir);
+    v3 focal = vadd(vscale(dir, b->focus), b->eye);
+    float lu, lv;
+    int k = 0;
+    do {   /* bounded at 64 draws of the pair (the reference loops until one lands) */
+        lu = (float)(1.0 - (double)(2.0f * next_rand(c)));
+        lv = (float)(1.0 - (double)(2.0f * next_rand(c)));
+        k++;
+    } while (lu * lu + lv * lv > 1.0f && k < 64);
+    v3 o = vadd(vscale(vadd(vscale(b->u, lu), vscale(b->v, lv)), b->aperture), b->eye);
+    return make_ray(o, vnormalized(vsub(focal, o)));
 }
 
 /* ---------------------------------------------------------------- image */
@@ -1658,10 +1675,7 @@ static v3 adaptive_levels(shade_ctx* c, const cam_basis* b, int x, int y, v3 sha
                 float offset = 1.0f / (float)curLevel;
                 c->sample++;
                 begin_camera(c);
-                float urand = next_rand(c), vrand = next_rand(c);
-                (void)next_rand(c);      /* getTimeSample */
-                ray_t r = camera_ray_adaptive(b, x, y, i * offset, (i + 1) * offset, j * offset, (j + 1) * offset,
-                                              urand, vrand);
+                ray_t r = eye_ray(c, b, x, y, i * offset, (i + 1) * offset, j * offset, (j + 1) * offset);
                 hit_t h;
                 curResult = vadd(curResult, sample_scene(c, &r, &h, nv, lv));
                 (*eye)++;
@@ -1703,9 +1717,7 @@ int oro_render(const oro_scene* s, const oro_camera* cam, int W, int H, int x0, 
             shade_ctx c; memset(&c, 0, sizeof c);
             c.s = s; c.pixel = (uint32_t)(y * W + x);
             begin_camera(&c);
-            float urand = next_rand(&c), vrand = next_rand(&c);
-            (void)next_rand(&c);            /* getTimeSample draw, src/Camera.cpp:154 */
-            ray_t r = camera_ray(&b, x, y, urand, vrand);
+            ray_t r = eye_ray(&c, &b, x, y, 0.5f, 0.5f, 0.5f, 0.5f);
             hit_t h;
             uint32_t nv = 0, lv = 0;
             v3 col = sample_scene(&c, &r, &h, &nv, &lv);

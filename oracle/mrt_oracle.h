@@ -60,6 +60,8 @@ typedef struct {
 typedef struct {
     float eye[3], up[3], lookAt[3];
     float fov;              /* degrees, as setFOV()                            */
+    float aperture, focusPlane;   /* Camera::m_aperture / m_focusPlane (DOF)   */
+    float shutterSpeed;     /* Camera::m_shutterSpeed (getTimeSample)          */
 } oro_camera;
 
 typedef struct {

@@ -45,7 +45,8 @@ class Light(C.Structure):
 
 
 class Camera(C.Structure):
-    _fields_ = [("eye", C.c_float * 3), ("up", C.c_float * 3), ("lookAt", C.c_float * 3), ("fov", C.c_float)]
+    _fields_ = [("eye", C.c_float * 3), ("up", C.c_float * 3), ("lookAt", C.c_float * 3), ("fov", C.c_float),
+                ("aperture", C.c_float), ("focusPlane", C.c_float), ("shutterSpeed", C.c_float)]
 
 
 class Hit(C.Structure):
@@ -328,8 +329,10 @@ class OracleScene:
         return out, nv, lv
 
     def render(self, cam, W, H, rect=None, threads=1, want_hits=True):
-        """cam: dict(eye, lookAt, up, fov).  Returns dict of numpy arrays."""
-        c = Camera(_v3(cam["eye"]), _v3(cam.get("up", (0, 1, 0))), _v3(cam["lookAt"]), float(cam["fov"]))
+        """cam: dict(eye, lookAt, up, fov[, aperture, focusPlane, shutterSpeed]).  Returns dict of numpy arrays."""
+        c = Camera(_v3(cam["eye"]), _v3(cam.get("up", (0, 1, 0))), _v3(cam["lookAt"]), float(cam["fov"]),
+                   float(cam.get("aperture", 0.0)), float(cam.get("focusPlane", 1.0)),
+                   float(cam.get("shutterSpeed", 0.001)))
         x0, y0, x1, y1 = rect if rect is not None else (0, 0, W, H)
         rgb = np.zeros((H, W, 3), np.float32)
         rgb8 = np.zeros((H, W, 3), np.uint8)

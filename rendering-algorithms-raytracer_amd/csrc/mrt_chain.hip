@@ -122,7 +122,8 @@ __global__ void __launch_bounds__(kWG) chain0_kernel(RenderParams P) {
         const int f = item_frame(P, P.item_base + item);
         const CamParams& cam = P.cam[f];
         const uint32_t seed = P.seed + (uint32_t)f;
-        const DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, seed, x, y, rsqT));
+        const EyeRay er = camera_ray(cam, seed, x, y, rsqT);
+        const DRay r = make_ray(er.o, er.d);
         Shader<POINT_ONLY, false, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 0u, seed, 0, 0u};
         S.iorS = s_ior + tid;
         typename Shader<POINT_ONLY, false, INST, MODE, REC>::IorCam icam;
@@ -385,7 +386,7 @@ __global__ void __launch_bounds__(kWG) chain_finish_kernel(RenderParams P) {
             col = scale(result, 1.0f / (float)P.num_paths);
         } else {
             const int f = item_frame(P, P.item_base + item);
-            col = P.env ? env_or_bg(P, camera_dir(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT)) : mk(P.bg[0], P.bg[1], P.bg[2]);
+            col = P.env ? env_or_bg(P, camera_ray(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT).d) : mk(P.bg[0], P.bg[1], P.bg[2]);
         }
         if (P.out_rgb) {
             float* o = P.out_rgb + 3 * slot;

@@ -230,8 +230,9 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
             // HitInfo::getAllInfos + Ray::getPoint
             const int f = item_frame(P, item);
             const CamParams& cam = P.cam[f];
-            const v3 rayD = camera_dir(cam, P.seed + (uint32_t)f, x, y, rsqT);
-            const DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), rayD);
+            const EyeRay er = camera_ray(cam, P.seed + (uint32_t)f, x, y, rsqT);
+            const v3 rayD = er.d;
+            const DRay r = make_ray(er.o, rayD);
             const PrimShade ps = P.prims[prim];
             const uint32_t mi = ps.mat;
             const bool lambert = P.mats[mi].type == MRT_LAMBERT;
@@ -699,6 +700,9 @@ static int host_camera(const mrt_camera* c, int W, int H, CamParams& out) {
     out.w[0] = w.x; out.w[1] = w.y; out.w[2] = w.z;
     out.top = top; out.right = right; out.bottom = -top; out.left = -right;
     out.W = W; out.H = H;
+    out.aperture = c->aperture;
+    out.focus = c->focus_plane;
+    out.shutter = c->shutter_speed;
     return MRT_OK;
 }
 

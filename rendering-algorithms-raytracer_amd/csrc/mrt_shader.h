@@ -840,17 +840,40 @@ __device__ __forceinline__ void flush_secondary(const RenderParams& P, uint32_t 
     if (lane == 0 && v) atomicAdd(&P.ctr[CTR_SECONDARY], v);
 }
 
-// Camera::eyeRayAdaptive(x, y, .5, .5, .5, .5) (src/Camera.cpp:116-157): two
-// jitter draws (dims 0, 1; the offsets are exactly 0.5) and the time draw (dim 2,
-// unused).  Deterministic, so kernel 2 recomputes it instead of storing it.
-__device__ __forceinline__ v3 camera_dir(const CamParams& cam, uint32_t seed, int x, int y, const uint16_t* rsqT) {
+// Camera::eyeRayAdaptive (src/Camera.cpp:116-174) of eye-ray sample `skey`: two
+// jitter draws (dims 0, 1) over [x0, x1] x [y0, y1] of the pixel, the time draw
+// (dim 2, getTimeSample), then with an aperture >= epsilon the lens point,
+// rejection-sampled from the unit disc (dims 3, 4, 5, ...), and the ray from it
+// through the focal point.  Deterministic per (pixel, sample), so the shading
+// kernels recompute the camera ray instead of storing it.
+struct EyeRay {
+    v3 o, d;
+};
+__device__ __forceinline__ EyeRay eye_ray(const CamParams& cam, uint32_t seed, int x, int y, uint32_t skey, float x0,
+                                          float x1, float y0, float y1, const uint16_t* rsqT) {
     const uint32_t pixel = (uint32_t)(y * cam.W + x);
-    float ur = rng(pixel, 0, 0, seed), vr = rng(pixel, 0, 1, seed);
-    float xo = (0.5f - 0.5f) * ur + 0.5f, yo = (0.5f - 0.5f) * vr + 0.5f;
-    float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
-    float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
-    v3 U = mk(cam.u[0], cam.u[1], cam.u[2]), Vv = mk(cam.v[0], cam.v[1], cam.v[2]), W = mk(cam.w[0], cam.w[1], cam.w[2]);
-    return normalized(sub(add(scale(U, Up), scale(Vv, Vp)), W), rsqT);
+    const float ur = rng(pixel, skey, 0, seed), vr = rng(pixel, skey, 1, seed);
+    const float xo = (x1 - x0) * ur + x0, yo = (y1 - y0) * vr + y0;
+    const float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
+    const float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
+    const v3 U = mk(cam.u[0], cam.u[1], cam.u[2]), Vv = mk(cam.v[0], cam.v[1], cam.v[2]), W = mk(cam.w[0], cam.w[1], cam.w[2]);
+    const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
+    const v3 d = normalized(sub(add(scale(U, Up), scale(Vv, Vp)), W), rsqT);
+    if (!(cam.aperture >= 0.001f)) return EyeRay{eye, d};   // m_aperture < epsilon: pinhole
+    const v3 focal = add(scale(d, cam.focus), eye);
+    float lu, lv;
+    uint32_t k = 3;
+    do {   // 1.0 - 2 * getRand: exact in float (1 - 2r is representable or rounds once either way)
+        lu = 1.0f - 2.0f * rng(pixel, skey, k, seed);
+        lv = 1.0f - 2.0f * rng(pixel, skey, k + 1, seed);
+        k += 2;
+    } while (lu * lu + lv * lv > 1.0f && k < 3 + 2 * 64);
+    const v3 o = add(scale(add(scale(U, lu), scale(Vv, lv)), cam.aperture), eye);
+    return EyeRay{o, normalized(sub(focal, o), rsqT)};
+}
+// the 1-spp camera ray (eyeRayAdaptive(x, y, .5, .5, .5, .5), sample 0)
+__device__ __forceinline__ EyeRay camera_ray(const CamParams& cam, uint32_t seed, int x, int y, const uint16_t* rsqT) {
+    return eye_ray(cam, seed, x, y, 0u, 0.5f, 0.5f, 0.5f, 0.5f, rsqT);
 }
 
 // Kernel 1: Camera::eyeRayAdaptive + closest-hit BVH::intersect per pixel.
@@ -885,7 +908,8 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
         if (item_pixel(P, item, lane, x, y, slot)) {
             const int f = item_frame(P, item);
             const CamParams& cam = P.cam[f];
-            DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, P.seed + (uint32_t)f, x, y, rsqT));
+            const EyeRay er = camera_ray(cam, P.seed + (uint32_t)f, x, y, rsqT);
+            DRay r = make_ray(er.o, er.d);
             DHit h{1e12f, 0.f, 0.f, -1};
             if (!traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st)) h.prim = -1;
             item_pixel(P, item, lane, x, y, slot);  // recompute: keeps it out of the traversal's live set
@@ -940,7 +964,8 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             const int f = item_frame(P, item);
             const CamParams& cam = P.cam[f];
             const uint32_t seed = P.seed + (uint32_t)f;
-            DRay r = make_ray(mk(cam.eye[0], cam.eye[1], cam.eye[2]), camera_dir(cam, seed, x, y, rsqT));
+            const EyeRay er = camera_ray(cam, seed, x, y, rsqT);
+            DRay r = make_ray(er.o, er.d);
             Shader<POINT_ONLY, FAST, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 0u, seed,
                                                    slot * (size_t)P.max_shadow, 0u};
             if constexpr (REC) { S.iorS = s_ior + tid; S.lvl = P.lvl + (blockIdx.x * kWG + tid); }
@@ -953,7 +978,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             continue;
         } else if (P.env) {  // environment map lookup of the missed ray (src/Scene.cpp:236-239)
             const int f = item_frame(P, item);
-            const v3 d = camera_dir(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
+            const v3 d = camera_ray(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT).d;
             col = scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
         } else {
             col = mk(P.bg[0], P.bg[1], P.bg[2]);
@@ -1017,9 +1042,6 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
         const CamParams& cam = P.cam[f];
         const uint32_t seed = P.seed + (uint32_t)f;
         const uint32_t pixel = (uint32_t)(y * cam.W + x);
-        const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
-        const v3 U = mk(cam.u[0], cam.u[1], cam.u[2]), Vv = mk(cam.v[0], cam.v[1], cam.v[2]),
-                 W = mk(cam.w[0], cam.w[1], cam.w[2]);
         v3 result = mk(0, 0, 0), cur = mk(0, 0, 0);
         int level = 1, i = 0, j = 0;
         bool cut = false;
@@ -1030,12 +1052,9 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
                 x0 = (float)i * off; x1 = (float)(i + 1) * off;
                 y0 = (float)j * off; y1 = (float)(j + 1) * off;
             }
-            const float ur = rng(pixel, sample * 1024u, 0, seed), vr = rng(pixel, sample * 1024u, 1, seed);
-            const float xo = (x1 - x0) * ur + x0, yo = (y1 - y0) * vr + y0;
-            const float Up = cam.left + (cam.right - cam.left) * (((float)x + xo) / (float)cam.W);
-            const float Vp = cam.bottom + (cam.top - cam.bottom) * (((float)y + yo) / (float)cam.H);
-            const v3 d = normalized(sub(add(scale(U, Up), scale(Vv, Vp)), W), rsqT);
-            const DRay r = make_ray(eye, d);
+            const EyeRay er = eye_ray(cam, seed, x, y, sample * 1024u, x0, x1, y0, y1, rsqT);
+            const v3 d = er.d;
+            const DRay r = make_ray(er.o, d);
             DHit h{1e12f, 0.f, 0.f, -1};
             v3 col;
             eye_rays++;

@@ -102,6 +102,8 @@ struct CamParams {
     float eye[3], u[3], v[3], w[3];
     float left, right, bottom, top;
     int32_t W, H;
+    float aperture, focus;   // Camera::m_aperture / m_focusPlane (depth of field, src/Camera.cpp:155-174)
+    float shutter;           // Camera::m_shutterSpeed (getTimeSample, src/Camera.h:46)
 };
 
 static constexpr int kMaxLights = 8;

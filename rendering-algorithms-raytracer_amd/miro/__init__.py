@@ -272,18 +272,25 @@ class DomeLight(_Light):
 
 
 class Camera:
-    """Camera setters of src/Camera.h:26-45 (fov in degrees, like setFOV)."""
+    """Camera setters of src/Camera.h:26-45 (fov in degrees, like setFOV), with the
+    lens of eyeRayAdaptive: setAperture / setFocusPlane (depth of field,
+    src/Camera.cpp:153-174) and setShutterSpeed (getTimeSample, src/Camera.h:44-46)."""
 
     def __init__(self):
         self.eye, self.lookAt, self.up, self.fov = Vector3(0), Vector3(0, 0, -1), Vector3(0, 1, 0), 45.0
+        self.aperture, self.focusPlane, self.shutterSpeed = 0.0, 1.0, 0.001   # src/Camera.cpp:21-23
 
     def setEye(self, v): self.eye = Vector3(v)
     def setLookAt(self, v): self.lookAt = Vector3(v)
     def setUp(self, v): self.up = Vector3(v)
     def setFOV(self, f): self.fov = float(f)
+    def setAperture(self, a): self.aperture = float(a)
+    def setFocusPlane(self, f): self.focusPlane = float(f)
+    def setShutterSpeed(self, s): self.shutterSpeed = float(s)
 
     def _c(self):
-        return _lib.mrt_camera(f3(self.eye), f3(self.lookAt), f3(self.up), self.fov)
+        return _lib.mrt_camera(f3(self.eye), f3(self.lookAt), f3(self.up), self.fov, self.aperture, self.focusPlane,
+                               self.shutterSpeed)
 
 
 class Image:

@@ -40,7 +40,8 @@ class mrt_light(C.Structure):
 
 
 class mrt_camera(C.Structure):
-    _fields_ = [("eye", C.c_float * 3), ("look_at", C.c_float * 3), ("up", C.c_float * 3), ("fov_deg", C.c_float)]
+    _fields_ = [("eye", C.c_float * 3), ("look_at", C.c_float * 3), ("up", C.c_float * 3), ("fov_deg", C.c_float),
+                ("aperture", C.c_float), ("focus_plane", C.c_float), ("shutter_speed", C.c_float)]
 
 
 class mrt_mesh(C.Structure):

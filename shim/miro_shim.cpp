@@ -147,6 +147,9 @@ int Scene::raytraceImage(Camera* cam, Image* img) {
     f3(c.look_at, cam->m_lookAt);
     f3(c.up, cam->m_up);
     c.fov_deg = cam->m_fov;
+    c.aperture = cam->m_aperture;
+    c.focus_plane = cam->m_focusPlane;
+    c.shutter_speed = cam->m_shutterSpeed;
     mrt_render_opts o;
     memset(&o, 0, sizeof o);
     o.width = img->m_width;

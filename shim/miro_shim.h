@@ -90,6 +90,7 @@ using Lights = std::vector<Light*>;
 struct Camera {
     Vector3 m_eye, m_lookAt{0.f, 0.f, -1.f}, m_up{0.f, 1.f, 0.f};
     float m_fov = 45.f;
+    float m_focusPlane = 1.0f, m_aperture = 0.0f, m_shutterSpeed = 0.001f;   // src/Camera.cpp:21-23
 };
 
 struct Image {

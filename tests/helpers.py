@@ -143,6 +143,8 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
 def camera(c):
     cam = miro.Camera()
     cam.setEye(c["eye"]); cam.setLookAt(c["lookAt"]); cam.setUp(c.get("up", (0, 1, 0))); cam.setFOV(c["fov"])
+    cam.setAperture(c.get("aperture", 0.0)); cam.setFocusPlane(c.get("focusPlane", 1.0))
+    cam.setShutterSpeed(c.get("shutterSpeed", 0.001))
     return cam
 
 
