@@ -176,6 +176,13 @@ int mrt_scene_add_mesh(mrt_scene* s, const mrt_mesh* mesh, int material);
 int mrt_scene_mesh_info(const mrt_scene* s, int mesh, int32_t* nv, int32_t* nn, int32_t* nt);
 int mrt_scene_mesh_export(const mrt_scene* s, int mesh, float* verts, float* normals,
                           uint32_t* vidx, uint32_t* nidx);
+/* TriangleMesh m_texCoords / m_texCoordIndices of a mesh added with
+ * mrt_scene_add_mesh (OBJ files load their vt lines): n_texcoords (u, v) pairs
+ * and 3 indices per triangle.  HitInfo::getAllInfos interpolates (u, v) and the
+ * tangent frame TriangleMesh::preCalc derives (src/Ray.cpp:33-47,
+ * src/TriangleMesh.cpp:105-148); without texture coordinates (u, v) = (a, b). */
+int mrt_scene_mesh_set_texcoords(mrt_scene* s, int mesh, const float* uv, int32_t n_texcoords, const uint32_t* tidx);
+int mrt_scene_mesh_texcoords(const mrt_scene* s, int mesh, int32_t* n_texcoords, float* uv, uint32_t* tidx);
 /* Scene::setBGColor (src/Scene.h:37) */
 int mrt_scene_set_background(mrt_scene* s, const float rgb[3]);
 /* Scene::m_numPaths (src/Scene.h:61): shade() calls per primary hit */
@@ -225,6 +232,24 @@ int mrt_hdr_load(const char* path, float* rgb, int32_t width, int32_t height);
  * src/Texture.h:13): copies width*height*3 floats (row 0 = top).  Returns the
  * texture id (<= 16 per scene). */
 int mrt_scene_add_texture(mrt_scene* s, const float* rgb, int32_t width, int32_t height);
+/* RawImage::loadImage (src/RawImage.cpp:16-188) by extension: .tga (uncompressed
+ * 8/24/32-bit, rows flipped, colour through Image::gamma_to_linear, alpha / 255,
+ * B/R swapped), .ppm (P6, bytes / 255) or .hdr.  type: MRT_TEX_HDR (3 floats per
+ * texel), MRT_TEX_GRAY (1), MRT_TEX_RGB (3), MRT_TEX_RGBA (4); data holds
+ * width*height*channels floats in RawImage m_rawData order (ABI 5). */
+enum { MRT_TEX_HDR = 0, MRT_TEX_GRAY = 1, MRT_TEX_RGB = 3, MRT_TEX_RGBA = 4 };
+int mrt_image_info(const char* path, int32_t* width, int32_t* height, int32_t* type);
+int mrt_image_load(const char* path, float* data, int32_t width, int32_t height);
+/* new RawImage(w, h, data, type) + new Texture(image) for any RawImage type
+ * (Texture::getPixel per type, src/Texture.cpp:100-125).  Returns the texture id. */
+int mrt_scene_add_texture_typed(mrt_scene* s, const float* data, int32_t width, int32_t height, int32_t type);
+/* Material::setColorMap / setNormalMap / setSpecularMap / setReflectMap /
+ * setRefractMap / setAlphaMap (src/Material.h:20-25): maps[6] texture ids in that
+ * order, -1 = none.  Lambert uses the colour map (src/Lambert.cpp:32-36); Blinn all
+ * of them (src/Blinn.cpp:114-142); an alpha map makes intersect4 skip a
+ * triangle whose alpha at the hit is below 0.5 (src/BVH.cpp:1397-1445), for
+ * closest-hit and shadow rays.  Alpha maps apply to world (non-instanced) meshes. */
+int mrt_scene_set_material_maps(mrt_scene* s, int material, const int32_t maps[6]);
 /* Scene::setEnvMap + Scene::setEnvExposure (src/Scene.h:23-24): primary rays
  * that miss return the lat-long lookup x exposure instead of the background
  * (src/Scene.cpp:236-239).  texture = -1 clears. */

@@ -15,6 +15,7 @@
  */
 #include "mrt_oracle.h"
 #include "oro_ibl.h"
+#include "oro_tex.h"
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -164,6 +165,12 @@ typedef struct {
     v3* verts; v3* normals;
     uint32_t* vidx; uint32_t* nidx;
     int material;
+    /* texture coordinates (TriangleMesh m_texCoords / m_texCoordIndices) and the
+     * per-normal tangent frame of TriangleMesh::preCalc; ntc = 0: none */
+    int ntc;
+    float* uv;                  /* 2 * ntc */
+    uint32_t* tidx;             /* 3 * nt */
+    v3* tan; v3* btan;          /* nn each (built with the BVH) */
 } mesh_t;
 
 typedef struct { float mn[3], mx[3]; } aabb;
@@ -208,6 +215,7 @@ struct oro_scene {
     int min_subdivs, max_subdivs;     /* Scene::m_minSubdivs / m_maxSubdivs (src/Scene.cpp:21-22) */
     float noise;                      /* Scene::m_noiseThreshold (src/Scene.cpp:20) */
     int* mesh_blas;                  /* per mesh: owning BLAS, -1 = world geometry */
+    int (*maps)[6];                   /* per material: color, normal, specular, reflect, refract, alpha map (-1) */
     int* groups; int n_groups;        /* world objects in add order: mesh m >= 0, instance ~i */
     struct oro_scene** blas; int n_blas;   /* ProxyObject BVHs (sub-scenes sharing the meshes) */
     oro_inst* inst; int n_inst;
@@ -241,7 +249,9 @@ void oro_scene_destroy(oro_scene* s) {
     for (int i = 0; i < s->n_meshes; i++) {
         free(s->meshes[i].verts); free(s->meshes[i].normals);
         free(s->meshes[i].vidx); free(s->meshes[i].nidx);
+        free(s->meshes[i].uv); free(s->meshes[i].tidx); free(s->meshes[i].tan); free(s->meshes[i].btan);
     }
+    free(s->maps);
     for (int i = 0; i < s->n_lights; i++) ibl_dome_free(&s->domes[i]);
     for (int i = 0; i < s->n_tex; i++) free(s->tex[i].rgb);
     for (int i = 0; i < s->n_blas; i++) { free_build(s->blas[i]); free(s->blas[i]); }
@@ -253,6 +263,8 @@ void oro_scene_destroy(oro_scene* s) {
 int oro_scene_add_material(oro_scene* s, const oro_material* m) {
     s->mats = (oro_material*)realloc(s->mats, sizeof(oro_material) * (s->n_mats + 1));
     s->mats[s->n_mats] = *m;
+    s->maps = (int(*)[6])realloc(s->maps, sizeof(int[6]) * (s->n_mats + 1));
+    for (int k = 0; k < 6; k++) s->maps[s->n_mats][k] = -1;
     return s->n_mats++;
 }
 int oro_scene_add_light(oro_scene* s, const oro_light* l) {
@@ -291,6 +303,36 @@ int oro_scene_add_texture(oro_scene* s, const float* rgb, int w, int h) {
     t->W = w;
     t->H = h;
     return s->n_tex++;
+}
+/* new RawImage(w, h, data, type) + new Texture(image): 1 (GRAYSCALE), 3 (RGB),
+ * 4 (RGBA) or 0 (HDR, 3 floats) channels per texel */
+int oro_scene_add_texture_typed(oro_scene* s, const float* data, int w, int h, int type) {
+    if (type != ORO_TEX_HDR && type != ORO_TEX_GRAY && type != ORO_TEX_RGB && type != ORO_TEX_RGBA) return -1;
+    if (s->n_tex >= ORO_MAX_TEX || !data || w <= 0 || h <= 0) return -1;
+    size_t n = (size_t)w * h * tex_channels(type);
+    ibl_image* t = &s->tex[s->n_tex];
+    t->rgb = (float*)malloc(sizeof(float) * n);
+    memcpy(t->rgb, data, sizeof(float) * n);
+    t->W = w;
+    t->H = h;
+    t->type = type;
+    return s->n_tex++;
+}
+/* Material::setColorMap / setNormalMap / setSpecularMap / setReflectMap /
+ * setRefractMap / setAlphaMap (src/Material.h:20-25): texture ids or -1 */
+int oro_scene_set_material_maps(oro_scene* s, int material, const int maps[6]) {
+    if (material < 0 || material >= s->n_mats) return -1;
+    for (int k = 0; k < 6; k++)
+        if (maps[k] < -1 || maps[k] >= s->n_tex) return -1;
+    for (int k = 0; k < 6; k++) s->maps[material][k] = maps[k];
+    s->built = 0;
+    return 0;
+}
+/* RawImage::loadImage (TGA / PPM / HDR by extension) */
+int oro_image_info(const char* path, int* w, int* h, int* type) { return tex_image_read(path, NULL, 0, 0, w, h, type); }
+int oro_image_load(const char* path, float* data, int w, int h) {
+    int ww = 0, hh = 0, tt = 0;
+    return tex_image_read(path, data, w, h, &ww, &hh, &tt);
 }
 int oro_scene_set_env_map(oro_scene* s, int texture, float exposure) {
     if (texture < -1 || texture >= s->n_tex) return -1;
@@ -381,6 +423,11 @@ int oro_scene_add_obj(oro_scene* s, const char* path, const float* ctm16, int ma
     }
     fseek(fp, 0, 0);
     mesh_t m; memset(&m, 0, sizeof m);
+    if (nt) {   /* got texture coordinates */
+        m.uv = (float*)calloc((size_t)2 * nt, sizeof(float));
+        m.tidx = (uint32_t*)calloc((size_t)3 * nf + 3, sizeof(uint32_t));
+    }
+    int ntex = 0;
     m.normals = (v3*)calloc((size_t)3 * nv + 1, sizeof(v3));
     m.verts = (v3*)calloc((size_t)nv + 1, sizeof(v3));
     m.vidx = (uint32_t*)calloc((size_t)3 * nf + 3, sizeof(uint32_t));
@@ -398,7 +445,11 @@ int oro_scene_add_obj(oro_scene* s, const char* path, const float* ctm16, int ma
                 if (nnorm >= 3 * nv + 1) { err = 3; break; }
                 m.normals[nnorm++] = vnormalized(n);
             } else if (line[1] == 't') {
-                /* texture coordinates: not used by the hot-path materials */
+                float x = 0, y = 0;
+                sscanf(&line[2], "%f %f\n", &x, &y);
+                m.uv[2 * ntex] = x;
+                m.uv[2 * ntex + 1] = y;
+                ntex++;
             } else {
                 float x = 0, y = 0, z = 0;
                 sscanf(&line[1], "%f %f %f\n", &x, &y, &z);
@@ -413,14 +464,26 @@ int oro_scene_add_obj(oro_scene* s, const char* path, const float* ctm16, int ma
             if (v <= 0 || v > nv) { err = 1; break; }
             m.vidx[3 * ntris + 0] = (uint32_t)(v - 1);
             if (n) m.nidx[3 * ntris + 0] = (uint32_t)(n - 1);
+            if (t && nt) {
+                if (t < 0 || t > nt) { err = 4; break; }
+                m.tidx[3 * ntris + 0] = (uint32_t)(t - 1);
+            }
             get_indices(s2, &v, &t, &n);
             if (v <= 0 || v > nv) { err = 1; break; }
             m.vidx[3 * ntris + 1] = (uint32_t)(v - 1);
             if (n) m.nidx[3 * ntris + 1] = (uint32_t)(n - 1);
+            if (t && nt) {
+                if (t < 0 || t > nt) { err = 4; break; }
+                m.tidx[3 * ntris + 1] = (uint32_t)(t - 1);
+            }
             get_indices(s3, &v, &t, &n);
             if (v <= 0 || v > nv) { err = 1; break; }
             m.vidx[3 * ntris + 2] = (uint32_t)(v - 1);
             if (n) m.nidx[3 * ntris + 2] = (uint32_t)(n - 1);
+            if (t && nt) {
+                if (t < 0 || t > nt) { err = 4; break; }
+                m.tidx[3 * ntris + 2] = (uint32_t)(t - 1);
+            }
             if (!n) {
                 if (nn >= nf || nn >= 3 * nv) { err = 2; break; }
                 v3 e1 = vsub(m.verts[m.vidx[3 * ntris + 1]], m.verts[m.vidx[3 * ntris + 0]]);
@@ -433,8 +496,8 @@ int oro_scene_add_obj(oro_scene* s, const char* path, const float* ctm16, int ma
         }
     }
     fclose(fp);
-    if (err) { free(m.normals); free(m.verts); free(m.vidx); free(m.nidx); return -2 - err; }
-    m.nv = nv; m.nn = nn < 1 ? 1 : nn; m.nt = ntris;
+    if (err) { free(m.normals); free(m.verts); free(m.vidx); free(m.nidx); free(m.uv); free(m.tidx); return -2 - err; }
+    m.nv = nv; m.nn = nn < 1 ? 1 : nn; m.nt = ntris; m.ntc = nt;
     return push_mesh(s, &m);
 }
 
@@ -455,6 +518,31 @@ int oro_scene_add_mesh(oro_scene* s, int nv, const float* verts, int nn, const f
         m.vidx[i] = vidx[i]; m.nidx[i] = nidx[i];
     }
     return push_mesh(s, &m);
+}
+
+/* TriangleMesh m_texCoords / m_texCoordIndices of a raw mesh (as createSingleTriangle
+ * sets them, src/TriangleMeshLoad.cpp:11-42) */
+int oro_mesh_set_texcoords(oro_scene* s, int mesh, int ntc, const float* uv, const uint32_t* tidx) {
+    if (mesh < 0 || mesh >= s->n_meshes || ntc <= 0 || !uv || !tidx) return -1;
+    mesh_t* m = &s->meshes[mesh];
+    for (int i = 0; i < 3 * m->nt; i++)
+        if (tidx[i] >= (uint32_t)ntc) return -1;
+    free(m->uv); free(m->tidx);
+    m->uv = (float*)malloc(sizeof(float) * 2 * ntc);
+    m->tidx = (uint32_t*)malloc(sizeof(uint32_t) * 3 * (m->nt ? m->nt : 1));
+    memcpy(m->uv, uv, sizeof(float) * 2 * ntc);
+    memcpy(m->tidx, tidx, sizeof(uint32_t) * 3 * m->nt);
+    m->ntc = ntc;
+    s->built = 0;
+    return 0;
+}
+int oro_mesh_texcoords(const oro_scene* s, int mesh, int* ntc, float* uv, uint32_t* tidx) {
+    if (mesh < 0 || mesh >= s->n_meshes) return -1;
+    const mesh_t* m = &s->meshes[mesh];
+    *ntc = m->ntc;
+    if (m->ntc && uv) memcpy(uv, m->uv, sizeof(float) * 2 * m->ntc);
+    if (m->ntc && tidx) memcpy(tidx, m->tidx, sizeof(uint32_t) * 3 * m->nt);
+    return 0;
 }
 
 int oro_mesh_info(const oro_scene* s, int mesh, int* nv, int* nn, int* nt) {
@@ -829,8 +917,39 @@ static int build_objects(oro_scene* s) {
 
 /* Scene::preCalc: the world objects in add order -- each world mesh's triangles
  * (makeMeshObjs) and each ProxyObject -- then BVH::build. */
+/* TriangleMesh::preCalc, USE_TRI_PACKETS branch (src/TriangleMesh.cpp:105-148):
+ * for a mesh with texture coordinates, each triangle with a non-degenerate uv
+ * edge cross product sets the tangent frame of its three normal slots (later
+ * triangles overwrite earlier ones).  Deviation: slots no triangle sets are zero
+ * (uninitialised in the reference). */
+static void mesh_tangents(mesh_t* m) {
+    if (!m->ntc || m->tan) return;
+    m->tan = (v3*)calloc((size_t)(m->nn ? m->nn : 1), sizeof(v3));
+    m->btan = (v3*)calloc((size_t)(m->nn ? m->nn : 1), sizeof(v3));
+    for (int i = 0; i < m->nt; i++) {
+        const uint32_t* vi = m->vidx + 3 * i;
+        v3 A = m->verts[vi[0]], B = m->verts[vi[1]], C = m->verts[vi[2]];
+        v3 AC = vsub(C, A), AB = vsub(B, A);
+        const uint32_t* ti = m->tidx + 3 * i;
+        float e1x = m->uv[2 * ti[1]] - m->uv[2 * ti[0]], e1y = m->uv[2 * ti[1] + 1] - m->uv[2 * ti[0] + 1];
+        float e2x = m->uv[2 * ti[2]] - m->uv[2 * ti[0]], e2y = m->uv[2 * ti[2] + 1] - m->uv[2 * ti[0] + 1];
+        float cp = e1y * e2x - e1x * e2y;
+        if (cp != 0.0f) {
+            const uint32_t* ni = m->nidx + 3 * i;
+            float mul = 1.f / cp;
+            v3 tangent = vnormalized(vscale(vadd(vscale(AB, -e2x), vscale(AC, e1y)), mul));
+            for (int k = 0; k < 3; k++) {
+                v3 normal = m->normals[ni[k]];
+                m->tan[ni[k]] = vnormalized(vsub(tangent, vscale(normal, vdot(normal, tangent))));
+                m->btan[ni[k]] = vcross(m->tan[ni[k]], normal);
+            }
+        }
+    }
+}
+
 int oro_scene_build(oro_scene* s) {
     free_build(s);
+    for (int i = 0; i < s->n_meshes; i++) mesh_tangents(&s->meshes[i]);
     int n = 0;
     for (int g = 0; g < s->n_groups; g++) {
         int id = s->groups[g];
@@ -1030,6 +1149,29 @@ static int proxy_intersect(const oro_scene* s, int inst, const ray_t* r, float t
 /* intersect4, src/BVH.cpp:1298-1459: proxy (checkOut) lanes first, in lane
  * order (:1305-1315), then the packet's triangles against the updated t.
  * No motion blur / alpha maps on this path. */
+/* Material::m_alphaMap of object o's triangle (-1: none; ProxyObject lanes and
+ * BLAS sub-scenes have none) */
+static int lane_alpha_map(const oro_scene* s, int o) {
+    if (o < 0 || !s->maps || s->obj_inst[o] >= 0) return -1;
+    return s->maps[s->meshes[s->obj_mesh[o]].material][5];
+}
+/* getLookupAlpha at the lane's (u, v): interpolated texture coordinates, or
+ * (a, b) for a mesh without them (src/BVH.cpp:1401-1423) */
+static float lane_alpha(const oro_scene* s, int map, int o, float a, float b) {
+    const mesh_t* m = &s->meshes[s->obj_mesh[o]];
+    const int t = s->obj_tri[o];
+    const float c = 1.0f - a - b;
+    float u = a, v = b;
+    if (m->ntc) {
+        const uint32_t* ti = m->tidx + 3 * t;
+        u = m->uv[2 * ti[0]] * c + m->uv[2 * ti[1]] * a + m->uv[2 * ti[2]] * b;
+        v = m->uv[2 * ti[0] + 1] * c + m->uv[2 * ti[1] + 1] * a + m->uv[2 * ti[2] + 1] * b;
+    }
+    float tx[4];
+    tex_lookup4(&s->tex[map], u, v, tx);
+    return tx[3];
+}
+
 static int intersect4(const oro_scene* s, const qleaf* L, const ray_t* r, float tMin, hit_t* h, uint32_t* nv,
                       uint32_t* lv) {
     int proxyIntersect = 0;
@@ -1062,8 +1204,22 @@ static int intersect4(const oro_scene* s, const qleaf* L, const ray_t* r, float 
     for (int i = 0; i < 4; i++) newT[i] = (tMask & (1 << i)) ? newT[i] : 1e12f;
     float lowest = newT[0]; int li = 0;
     for (int i = 1; i < 4; i++) if (newT[i] < lowest) { lowest = newT[i]; li = i; }
-    if (lowest < h->t) {
+    newT[li] = 1e12f;
+    /* lanes in t order; an alpha-mapped triangle whose alpha is below 0.5 at the
+     * hit is skipped (src/BVH.cpp:1397-1445) */
+    for (int i = 0; i < 4; i++) {
+        if (!(lowest < h->t)) continue;
+        const int am = lane_alpha_map(s, L->prim[li]);
+        if (am >= 0 && lane_alpha(s, am, L->prim[li], A[li], B[li]) < 0.5f) {
+            if (i == 3) return proxyIntersect;
+            lowest = newT[0]; li = 0;
+            for (int j = 1; j < 4; j++) if (newT[j] < lowest) { lowest = newT[j]; li = j; }
+            if (newT[li] == 1e12f) return proxyIntersect;
+            newT[li] = 1e12f;
+            continue;
+        }
         h->t = lowest; h->a = A[li]; h->b = B[li]; h->prim = L->prim[li]; h->inst = -1;
+        return 1;
     }
     return 1;
 }
@@ -1316,6 +1472,27 @@ static void hit_normals(const oro_scene* s, const hit_t* h, v3* N, v3* geoN) {
     }
 }
 
+/* HitInfo::getAllInfos, texture part (src/Ray.cpp:33-47): with texture
+ * coordinates the interpolated tangent frame (over the NORMAL indices) and the
+ * interpolated (u, v); otherwise T = BT = 0 and (u, v) = (a, b). */
+static void hit_uv(const oro_scene* s, const hit_t* h, v3* T, v3* BT, float* u, float* v) {
+    int t;
+    const mesh_t* m = hit_mesh(s, h, &t);
+    float cc = 1.0f - h->a - h->b;
+    if (m->ntc) {
+        const uint32_t* ni = m->nidx + 3 * t;
+        *T = vnormalized(vadd(vadd(vscale(m->tan[ni[0]], cc), vscale(m->tan[ni[1]], h->a)), vscale(m->tan[ni[2]], h->b)));
+        *BT = vnormalized(vadd(vadd(vscale(m->btan[ni[0]], cc), vscale(m->btan[ni[1]], h->a)), vscale(m->btan[ni[2]], h->b)));
+        const uint32_t* ti = m->tidx + 3 * t;
+        *u = m->uv[2 * ti[0]] * cc + m->uv[2 * ti[1]] * h->a + m->uv[2 * ti[2]] * h->b;
+        *v = m->uv[2 * ti[0] + 1] * cc + m->uv[2 * ti[1] + 1] * h->a + m->uv[2 * ti[2] + 1] * h->b;
+    } else {
+        *T = *BT = V(0, 0, 0);
+        *u = h->a;
+        *v = h->b;
+    }
+}
+
 /* Ray::getPoint, src/Ray.h:168-177 */
 static v3 ray_point(const ray_t* r, float t) {
     return V(r->o[0] + t * r->d[0], r->o[1] + t * r->d[1], r->o[2] + t * r->d[2]);
@@ -1329,6 +1506,14 @@ static v3 shade_lambert(shade_ctx* c, const oro_material* mat, const ray_t* r, c
     v3 N, geoN;
     hit_normals(c->s, h, &N, &geoN);
     v3 kd = V(mat->kd[0], mat->kd[1], mat->kd[2]);
+    const int* maps = c->s->maps[mat - c->s->mats];
+    if (maps[0] >= 0) {   /* m_colorMap (src/Lambert.cpp:32-36) */
+        v3 T, BT;
+        float u, v, tc[4];
+        hit_uv(c->s, h, &T, &BT, &u, &v);
+        tex_lookup4(&c->s->tex[maps[0]], u, v, tc);
+        kd = V(tc[0], tc[1], tc[2]);
+    }
     for (int i = 0; i < c->s->n_lights; i++) {
         float discard;
         v3 E = sample_light(c, i, P, N, V(0, 0, 0), &discard, 0);
@@ -1433,8 +1618,9 @@ static v3 path_trace(shade_ctx* c, const oro_material* mat, v3 P, v3 theNormal, 
 
 /* Blinn::shade, src/Blinn.cpp:91-335: Fresnel-weighted Russian roulette between
  * direct lighting (+ path tracing) and one reflection or refraction ray (bounces
- * < 5), with the ray's IOR history, glossy reflection vector, translucency and
- * m_Le (no texture maps, no dispersion). */
+ * < 5), with the ray's IOR history, glossy reflection vector, translucency,
+ * m_Le and the colour / normal / specular / reflect / refract maps (no
+ * dispersion). */
 static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h, ior_list* ior,
                       chain_t ch) {
     begin_level(c, ch.level);
@@ -1444,6 +1630,23 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
     v3 N, geoN;
     hit_normals(c->s, h, &N, &geoN);
     v3 P = ray_point(r, h->t);
+    /* the texture maps, src/Blinn.cpp:114-142 */
+    v3 kd = V(mat->kd[0], mat->kd[1], mat->kd[2]);
+    float specAmt = mat->specAmt, reflectAmt = mat->reflect, refractAmt = mat->refract;
+    const int* maps = c->s->maps[mat - c->s->mats];
+    if (maps[0] >= 0 || maps[1] >= 0 || maps[2] >= 0 || maps[3] >= 0 || maps[4] >= 0) {
+        v3 T, BT;
+        float u, v, tx[4];
+        hit_uv(c->s, h, &T, &BT, &u, &v);
+        if (maps[0] >= 0) { tex_lookup4(&c->s->tex[maps[0]], u, v, tx); kd = V(tx[0], tx[1], tx[2]); }
+        if (maps[1] >= 0) {   /* N = texN.x*T + texN.y*BT + texN.z*N (not renormalised) */
+            tex_lookup4(&c->s->tex[maps[1]], u, v, tx);
+            N = vadd(vadd(vscale(T, tx[0]), vscale(BT, tx[1])), vscale(N, tx[2]));
+        }
+        if (maps[2] >= 0) { tex_lookup4(&c->s->tex[maps[2]], u, v, tx); specAmt = ((tx[0] + tx[1]) + tx[2]) * 0.3333333f * specAmt; }
+        if (maps[3] >= 0) { tex_lookup4(&c->s->tex[maps[3]], u, v, tx); reflectAmt = ((tx[0] + tx[1]) + tx[2]) * 0.3333333f * reflectAmt; }
+        if (maps[4] >= 0) { tex_lookup4(&c->s->tex[maps[4]], u, v, tx); refractAmt = ((tx[0] + tx[1]) + tx[2]) * 0.3333333f * refractAmt; }
+    }
     float vDotN = vdot(viewDir, N);
     float vDotGeoN = vdot(viewDir, geoN);
     int nEqGeoN = ((double)(vDotN * vDotGeoN) >= 0.0);
@@ -1470,11 +1673,10 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
         Ts = 1.0f - Rs;
     }
     float rrFloat = next_rand(c);        /* src/Blinn.cpp:195 */
-    float rrWeight = (1.0f - Rs * mat->reflect) - Ts * mat->refract;
+    float rrWeight = (1.0f - Rs * reflectAmt) - Ts * refractAmt;
     float rrWeightRecip = (rrWeight > 0.f) ? 1.f / rrWeight : 1.f;
     float rrWeightRecipSpec = (1.f - rrWeight > 0.f) ? 1.f / (1.f - rrWeight) : 1.f;
     v3 ks = V(mat->ks[0], mat->ks[1], mat->ks[2]);
-    v3 kd = V(mat->kd[0], mat->kd[1], mat->kd[2]);
     if (rrFloat <= rrWeight) {
         if (c->s->path_trace) Ld = vadd(Ld, path_trace(c, mat, P, theNormal, kd, ior->v[ior->idx], ch));
         for (int i = 0; i < c->s->n_lights; i++) {
@@ -1482,7 +1684,7 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
             v3 E = sample_light(c, i, P, theNormal, rVec, &lightSpec, ch.secondary);
             /* libm pow of the reference, evaluated in double and rounded once */
             float pw = (float)pow((double)lightSpec, (double)mat->specExp);
-            Ls = vadd(Ls, vscale(vscale(vmul(E, ks), mat->specAmt), pw));
+            Ls = vadd(Ls, vscale(vscale(vmul(E, ks), specAmt), pw));
             Ld = vadd(Ld, vmul(E, kd));
         }
         if (mat->translucency > 0.01f) {   /* src/Blinn.cpp:224-236 */
@@ -1497,8 +1699,8 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
         int doEnv = 1;
         rrFloat = next_rand(c);
         chain_t cc = {ch.bounces + 1, ch.gi, 0, ch.level + 1};   /* shade(..) default isSecondary = false */
-        if (rrFloat < mat->reflect * Rs) {
-            if (mat->reflect * Rs > 0.0f && ch.bounces < 5) {
+        if (rrFloat < reflectAmt * Rs) {
+            if (reflectAmt * Rs > 0.0f && ch.bounces < 5) {
                 ior_list child = *ior;
                 ray_t rr = make_ray(P, rVec);
                 hit_t nh;
@@ -1507,8 +1709,8 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
                     doEnv = 0;
                 }
             }
-            if (mat->reflect * Rs > 0.0f && doEnv) Lr = vadd(Lr, vmul(ks, env_color(c->s, rVec)));
-        } else if (mat->refract * Ts > 0.0f) {
+            if (reflectAmt * Rs > 0.0f && doEnv) Lr = vadd(Lr, vmul(ks, env_color(c->s, rVec)));
+        } else if (refractAmt * Ts > 0.0f) {
             float snellsQ = inIOR / outIOR;
             float sqrtPart = std_max(0.0f, sqrtf(1.0f - (snellsQ * snellsQ) * (1.0f - vDotN * vDotN)));
             v3 tVec = vnormalized(vadd(vscale(rayD, snellsQ), vscale(theNormal, snellsQ * vDotN - sqrtPart)));

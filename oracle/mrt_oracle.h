@@ -139,6 +139,17 @@ int oro_hdr_info(const char* path, int* w, int* h);
 int oro_hdr_load(const char* path, float* rgb, int w, int h);
 /* RawImage + Texture: copies W*H*3 floats (row 0 = top); returns texture id. */
 int oro_scene_add_texture(oro_scene* s, const float* rgb, int w, int h);
+/* RawImage::loadImage (TGA / PPM / HDR): size and type (0 HDR, 1 gray, 3 RGB, 4 RGBA), then
+ * w*h*channels floats in RawImage m_rawData order */
+int oro_image_info(const char* path, int* w, int* h, int* type);
+int oro_image_load(const char* path, float* data, int w, int h);
+/* a texture of any RawImage type (channels per texel: 1, 3, 4; 0 = HDR, 3) */
+int oro_scene_add_texture_typed(oro_scene* s, const float* data, int w, int h, int type);
+/* Material maps: color, normal, specular, reflect, refract, alpha (texture id or -1) */
+int oro_scene_set_material_maps(oro_scene* s, int material, const int maps[6]);
+/* TriangleMesh m_texCoords (ntc x 2 floats) / m_texCoordIndices (nt x 3) of a mesh */
+int oro_mesh_set_texcoords(oro_scene* s, int mesh, int ntc, const float* uv, const uint32_t* tidx);
+int oro_mesh_texcoords(const oro_scene* s, int mesh, int* ntc, float* uv, uint32_t* tidx);
 /* Scene::setEnvMap + setEnvExposure (src/Scene.h:23-24); texture -1 clears. */
 int oro_scene_set_env_map(oro_scene* s, int texture, float exposure);
 /* DomeLight::setTexture tables of light `light` (src/DomeLight.cpp:8-78):

@@ -90,6 +90,12 @@ def _declare(L):
     L.oro_hdr_info.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.oro_hdr_load.argtypes = [C.c_char_p, _fp, C.c_int, C.c_int]
     L.oro_scene_add_texture.argtypes = [C.c_void_p, _fp, C.c_int, C.c_int]
+    L.oro_image_info.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.oro_image_load.argtypes = [C.c_char_p, _fp, C.c_int, C.c_int]
+    L.oro_scene_add_texture_typed.argtypes = [C.c_void_p, _fp, C.c_int, C.c_int, C.c_int]
+    L.oro_scene_set_material_maps.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+    L.oro_mesh_set_texcoords.argtypes = [C.c_void_p, C.c_int, C.c_int, _fp, _u32p]
+    L.oro_mesh_texcoords.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), _fp, _u32p]
     L.oro_scene_set_env_map.argtypes = [C.c_void_p, C.c_int, C.c_float]
     L.oro_dome_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.oro_dome_export.argtypes = [C.c_void_p, C.c_int] + [_fp] * 9
@@ -120,6 +126,23 @@ def hdr_load(path):
     if r != 0:
         raise RuntimeError(f"oracle HDR load rejected ({r}): {path}")
     return rgb
+
+
+TEX_CHANNELS = {0: 3, 1: 1, 3: 3, 4: 4}   # RawImage types: HDR, GRAYSCALE, RGB, RGBA
+
+
+def image_load(path):
+    """RawImage::loadImage restated (TGA / PPM / HDR): (data (H, W, channels) float32, type)."""
+    L = lib()
+    w, h, t = C.c_int(), C.c_int(), C.c_int()
+    r = L.oro_image_info(str(path).encode(), C.byref(w), C.byref(h), C.byref(t))
+    if r != 0:
+        raise RuntimeError(f"oracle image header rejected ({r}): {path}")
+    data = np.zeros((h.value, w.value, TEX_CHANNELS[t.value]), np.float32)
+    r = L.oro_image_load(str(path).encode(), _p(data, _fp), w.value, h.value)
+    if r != 0:
+        raise RuntimeError(f"oracle image load rejected ({r}): {path}")
+    return data, t.value
 
 
 def _p(a, t):
@@ -209,6 +232,35 @@ class OracleScene:
         l.texture = -1
         self.n_lights += 1
         return self.L.oro_scene_add_light(self.h, C.byref(l))
+
+    def add_texture_typed(self, data, type_):
+        a = np.ascontiguousarray(data, np.float32)
+        r = self.L.oro_scene_add_texture_typed(self.h, _p(a, _fp), a.shape[1], a.shape[0], int(type_))
+        if r < 0:
+            raise RuntimeError("oracle add_texture_typed failed")
+        return r
+
+    def set_material_maps(self, material, color=-1, normal=-1, specular=-1, reflect=-1, refract=-1, alpha=-1):
+        m = (C.c_int * 6)(color, normal, specular, reflect, refract, alpha)
+        if self.L.oro_scene_set_material_maps(self.h, material, m) != 0:
+            raise RuntimeError("oracle set_material_maps failed")
+
+    def set_texcoords(self, mesh, uv, tidx):
+        uv = np.ascontiguousarray(uv, np.float32).reshape(-1, 2)
+        ti = np.ascontiguousarray(tidx, np.uint32).reshape(-1, 3)
+        if self.L.oro_mesh_set_texcoords(self.h, mesh, len(uv), _p(uv, _fp), _p(ti, _u32p)) != 0:
+            raise RuntimeError("oracle set_texcoords failed")
+
+    def texcoords(self, mesh):
+        n = C.c_int()
+        self.L.oro_mesh_texcoords(self.h, mesh, C.byref(n), None, None)
+        nv, nn, nt = C.c_int(), C.c_int(), C.c_int()
+        self.L.oro_mesh_info(self.h, mesh, C.byref(nv), C.byref(nn), C.byref(nt))
+        uv = np.zeros((n.value, 2), np.float32)
+        ti = np.zeros((nt.value if n.value else 0, 3), np.uint32)
+        if n.value:
+            self.L.oro_mesh_texcoords(self.h, mesh, C.byref(n), _p(uv, _fp), _p(ti, _u32p))
+        return uv, ti
 
     def add_texture(self, rgb):
         a = np.ascontiguousarray(rgb, np.float32)

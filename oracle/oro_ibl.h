@@ -6,9 +6,10 @@
 #ifndef ORO_IBL_H
 #define ORO_IBL_H
 
-typedef struct {            /* RawImage (src/RawImage.h): W*H*3 floats, row 0 = top */
+typedef struct {            /* RawImage (src/RawImage.h): W*H*channels floats, row 0 = top */
     float* rgb;
     int W, H;
+    int type;               /* ORO_TEX_HDR (0, 3 floats, the IBL maps), _GRAY (1), _RGB (3), _RGBA (4) */
 } ibl_image;
 
 typedef struct {            /* Distribution1D, src/DomeLight.h:10-42 */

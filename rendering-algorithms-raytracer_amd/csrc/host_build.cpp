@@ -189,8 +189,12 @@ int load_obj(const char* path, const float* ctm16, Mesh& out, std::string& err) 
             nf++;
         }
     }
-    (void)nt;
     fseek(fp, 0, SEEK_SET);
+    if (nt) {   // got texture coordinates
+        out.uv.assign((size_t)2 * nt, 0.f);
+        out.tidx.assign((size_t)3 * nf, 0u);
+    }
+    int ntex = 0;
     out.verts.assign((size_t)nv, v3{0, 0, 0});
     out.normals.assign((size_t)3 * nv + 1, v3{0, 0, 0});
     out.vidx.assign((size_t)3 * nf, 0u);
@@ -204,7 +208,12 @@ int load_obj(const char* path, const float* ctm16, Mesh& out, std::string& err) 
                 sscanf(&line[2], "%f %f %f\n", &x, &y, &z);
                 if (nnorm >= 3 * nv + 1) { rc = MRT_ERR_IO; err = "too many normals"; break; }
                 out.normals[nnorm++] = normalized(xform_dir(nctm, mk(x, y, z)), RS);
-            } else if (line[1] != 't') {
+            } else if (line[1] == 't') {
+                sscanf(&line[2], "%f %f\n", &x, &y);
+                out.uv[2 * (size_t)ntex] = x;
+                out.uv[2 * (size_t)ntex + 1] = y;
+                ntex++;
+            } else {
                 sscanf(&line[1], "%f %f %f\n", &x, &y, &z);
                 out.verts[nverts++] = xform_point(ctm, mk(x, y, z));
             }
@@ -218,6 +227,10 @@ int load_obj(const char* path, const float* ctm16, Mesh& out, std::string& err) 
                 if (v <= 0 || v > nv) { rc = MRT_ERR_IO; err = "face vertex index out of range"; break; }
                 out.vidx[3 * ntris + k] = (uint32_t)(v - 1);
                 if (n) out.nidx[3 * ntris + k] = (uint32_t)(n - 1);
+                if (t && nt) {
+                    if (t < 0 || t > nt) { rc = MRT_ERR_IO; err = "face texture-coordinate index out of range"; break; }
+                    out.tidx[3 * ntris + k] = (uint32_t)(t - 1);
+                }
             }
             if (rc != MRT_OK) break;
             if (!n) {
@@ -237,6 +250,7 @@ int load_obj(const char* path, const float* ctm16, Mesh& out, std::string& err) 
     out.normals.resize((size_t)std::max(nn, 1));
     out.vidx.resize((size_t)3 * ntris);
     out.nidx.resize((size_t)3 * ntris);
+    if (!out.tidx.empty()) out.tidx.resize((size_t)3 * ntris);
     for (uint32_t i : out.nidx)
         if (i >= out.normals.size()) { err = "normal index out of range"; return MRT_ERR_IO; }
     return MRT_OK;
@@ -834,6 +848,7 @@ class Builder {
 // Scene::preCalc -> BVH::build, src/Scene.cpp:62-79 + src/BVH.cpp:457-575.
 int build_qbvh(Scene& s, std::string& err) {
     auto t0 = std::chrono::steady_clock::now();
+    for (Mesh& m : s.meshes) mesh_tangents(m);   // TriangleMesh::preCalc (texture-mapped meshes)
     s.obj_mesh.clear();
     s.obj_tri.clear();
     s.obj_inst.clear();

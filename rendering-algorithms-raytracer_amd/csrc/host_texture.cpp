@@ -14,8 +14,10 @@
 // the end of a scanline, an old-style run with no previous pixel.
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <array>
 #include <cmath>
 #include <string>
@@ -212,6 +214,132 @@ int build_dome(const Texture& t, DomeTables& d, std::string& err) {
     for (int i = 0; i <= nv; i++) d.cos_v[i] = cosf((float)i * inv * kPI);
     for (int i = 0; i <= nv; i++) d.sin_v[i] = sinf((float)i * inv * kPI);
     return MRT_OK;
+}
+
+
+// ------------------------------------------------------------------ TGA / PPM
+// Image::gamma_to_linear (src/Image.cpp:19-27): (int)(powf(i / 255.0f, 2.2f) * 32768.0 + 0.5)
+static const unsigned short* gamma_to_linear() {
+    static unsigned short t[256];
+    static bool ready = false;
+    if (!ready) {
+        for (int i = 0; i < 256; i++) t[i] = (unsigned short)(int)((double)powf((float)i / 255.0f, 2.2f) * 32768.0 + 0.5);
+        ready = true;
+    }
+    return t;
+}
+
+// RawImage::loadTGA (src/RawImage.cpp:89-188): the 18-byte header read field by
+// field (the image-ID field is not skipped, as in the reference), uncompressed
+// types 2 / 3 only, rows flipped, colour bytes through gamma_to_linear / 32768,
+// the alpha byte / 255, B and R swapped.  A short body fails (reference: UB).
+static int load_tga(const char* path, int& W, int& H, int& type, std::vector<float>* data, std::string& err) {
+    FILE* f = fopen(path, "rb");
+    if (!f) { err = std::string("cannot open ") + path; return MRT_ERR_IO; }
+    unsigned char hdr[18];
+    if (fread(hdr, 1, 18, f) != 18) { fclose(f); err = "short TGA header"; return MRT_ERR_IO; }
+    const unsigned char tp = hdr[2], depth = hdr[16];
+    const int w = (int16_t)(hdr[12] | hdr[13] << 8), h = (int16_t)(hdr[14] | hdr[15] << 8);
+    const int mode = depth / 8;
+    if ((tp != 2 && tp != 3) || w <= 0 || h <= 0 || (mode != 1 && mode != 3 && mode != 4)) {
+        fclose(f);
+        err = "unsupported TGA (uncompressed 8/24/32-bit true colour or grey only)";
+        return MRT_ERR_IO;
+    }
+    W = w;
+    H = h;
+    type = mode == 1 ? kTexGray : mode == 3 ? kTexRGB : kTexRGBA;
+    if (!data) { fclose(f); return MRT_OK; }
+    const size_t row = (size_t)w * mode, total = row * h;
+    std::vector<unsigned char> img(total);
+    const size_t got = fread(img.data(), 1, total, f);
+    fclose(f);
+    if (got != total) { err = "short TGA body"; return MRT_ERR_IO; }
+    const unsigned short* g2l = gamma_to_linear();
+    data->assign(total, 0.f);
+    float* out = data->data();
+    for (int y = 0; y < h; y++) {   // file row y -> row h - 1 - y
+        const unsigned char* src = img.data() + (size_t)y * row;
+        float* dst = out + (size_t)(h - 1 - y) * row;
+        for (size_t j = 0; j < row; j++) dst[j] = (float)g2l[src[j]] / 32768.f;
+        if (mode == 4)
+            for (size_t j = 3; j < row; j += 4) dst[j] = (float)src[j] / 255.f;
+    }
+    if (mode >= 3)
+        for (size_t i = 0; i < total; i += (size_t)mode) std::swap(out[i], out[i + 2]);
+    return MRT_OK;
+}
+
+// RawImage::loadPPM (src/RawImage.cpp:33-88): binary P6; '#' lines skipped before
+// the size and the maxval lines; bytes / 255.
+static int load_ppm(const char* path, int& W, int& H, int& type, std::vector<float>* data, std::string& err) {
+    FILE* f = fopen(path, "rb");
+    if (!f) { err = std::string("cannot open ") + path; return MRT_ERR_IO; }
+    char buf[128], a[128], b[128];
+    bool ok = fgets(buf, 128, f) != nullptr;
+    do ok = ok && fgets(buf, 128, f) != nullptr;
+    while (ok && buf[0] == '#');
+    ok = ok && sscanf(buf, "%127s %127s", a, b) == 2;
+    const int w = ok ? atoi(a) : 0, h = ok ? atoi(b) : 0;
+    do ok = ok && fgets(buf, 128, f) != nullptr;
+    while (ok && buf[0] == '#');
+    if (!ok || w <= 0 || h <= 0) { fclose(f); err = "bad PPM header"; return MRT_ERR_IO; }
+    W = w;
+    H = h;
+    type = kTexRGB;
+    if (!data) { fclose(f); return MRT_OK; }
+    const size_t total = (size_t)w * h * 3;
+    std::vector<unsigned char> raw(total);
+    const size_t got = fread(raw.data(), total, 1, f);
+    fclose(f);
+    if (got != 1) { err = "short PPM body"; return MRT_ERR_IO; }
+    data->resize(total);
+    for (size_t i = 0; i < total; i++) (*data)[i] = (float)raw[i] / 255;
+    return MRT_OK;
+}
+
+int load_image(const char* path, int& W, int& H, int& type, std::vector<float>* data, std::string& err) {
+    const char* dot = strrchr(path, '.');
+    const std::string ext = dot ? dot + 1 : "";
+    if (ext == "tga" || ext == "TGA") return load_tga(path, W, H, type, data, err);
+    if (ext == "ppm" || ext == "PPM") return load_ppm(path, W, H, type, data, err);
+    if (ext == "hdr" || ext == "HDR") {
+        type = kTexHDR;
+        return load_hdr(path, W, H, data, err);
+    }
+    err = "RawImage::loadImage reads .tga, .ppm and .hdr only";
+    return MRT_ERR_IO;
+}
+
+// TriangleMesh::preCalc, USE_TRI_PACKETS branch (src/TriangleMesh.cpp:105-148):
+// every triangle with a non-zero uv edge cross product writes the tangent frame
+// of its three normal slots (later triangles overwrite).  Deviation: slots no
+// triangle writes are zero (uninitialised memory in the reference).
+void mesh_tangents(Mesh& m) {
+    m.tan.clear();
+    m.btan.clear();
+    if (m.tidx.empty()) return;
+    const uint16_t* RS = host_rsqrt_table();
+    m.tan.assign(m.normals.size(), v3{0, 0, 0});
+    m.btan.assign(m.normals.size(), v3{0, 0, 0});
+    for (int32_t i = 0; i < m.nt(); i++) {
+        const uint32_t* vi = &m.vidx[3 * (size_t)i];
+        const v3 A = m.verts[vi[0]], B = m.verts[vi[1]], C = m.verts[vi[2]];
+        const v3 AC = sub(C, A), AB = sub(B, A);
+        const uint32_t* ti = &m.tidx[3 * (size_t)i];
+        const float e1x = m.uv[2 * ti[1]] - m.uv[2 * ti[0]], e1y = m.uv[2 * ti[1] + 1] - m.uv[2 * ti[0] + 1];
+        const float e2x = m.uv[2 * ti[2]] - m.uv[2 * ti[0]], e2y = m.uv[2 * ti[2] + 1] - m.uv[2 * ti[0] + 1];
+        const float cp = e1y * e2x - e1x * e2y;
+        if (cp == 0.0f) continue;
+        const float mul = 1.f / cp;
+        const v3 tangent = normalized(scale(add(scale(AB, -e2x), scale(AC, e1y)), mul), RS);
+        const uint32_t* ni = &m.nidx[3 * (size_t)i];
+        for (int k = 0; k < 3; k++) {
+            const v3 normal = m.normals[ni[k]];
+            m.tan[ni[k]] = normalized(sub(tangent, scale(normal, dot(normal, tangent))), RS);
+            m.btan[ni[k]] = cross(m.tan[ni[k]], normal);
+        }
+    }
 }
 
 }  // namespace mrt

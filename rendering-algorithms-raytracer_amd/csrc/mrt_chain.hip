@@ -223,6 +223,7 @@ __global__ void __launch_bounds__(kWG) chain_trace_kernel(RenderParams P) {
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, s_tab, s_stack + tid,
            P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
+    trav_alpha(T, P);
     TravStats st;
     const size_t base = lvl_off(P, k), cap = P.ch_cap, sb = shadow_base(P, k - 1);
     const uint8_t* nrays = P.nrays + (size_t)(k - 1) * cap;

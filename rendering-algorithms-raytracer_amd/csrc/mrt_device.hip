@@ -64,6 +64,7 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, s_tab, s_stack + tid,
            P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
+    trav_alpha(T, P);
     TravStats st;
     unsigned long long wave_steps = 0;
     // chain levels: the entry count is on the device (n_rays is the capacity)
@@ -208,6 +209,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
+    trav_alpha(T, P);
     TravStats st;
     uint32_t shadow_total = 0;
     TileSched ts(P, wave, lane);
@@ -316,7 +318,7 @@ __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DL
                                                     int32_t* gstack, uint32_t gstride, const float* o, const float* d,
                                                     const float* tmin, const float* tmax, size_t n, mrt_hit* out,
                                                     unsigned long long* ctr, int fast_box,
-                                                    const DevInstance* insts) {
+                                                    const DevInstance* insts, Trav alpha) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     const int tid = threadIdx.x;
@@ -325,6 +327,7 @@ __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DL
     const uint32_t gtid = blockIdx.x * kWG + tid;
     Trav T{nodes, fast_box != 0, false, leaves, s_tab, s_stack + tid, gstack + gtid, gstride};
     T.inst = insts;
+    T.aprims = alpha.aprims; T.apuv = alpha.apuv; T.auv = alpha.auv; T.amats = alpha.amats; T.atex = alpha.atex;
     TravStats st;
     for (size_t i = (size_t)blockIdx.x * kWG + tid; i < n; i += (size_t)gridDim.x * kWG) {
         DRay r = make_ray(mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]));
@@ -404,6 +407,13 @@ struct DeviceState {
     DevDome* domes = nullptr;
     DevInstance* insts = nullptr;
     int n_insts = 0, n_world = 0;
+    DevTexture* texs = nullptr;   // material-map textures (bufs hold their data)
+    uint4* puv = nullptr;         // per prim texture-coordinate indices (nullptr: no texture-mapped mesh)
+    float2* uvs = nullptr;
+    float4* tans = nullptr;       // per normal: tangent / bitangent (texture-mapped meshes)
+    float4* btans = nullptr;
+    bool has_maps = false, has_alpha = false;
+    bool special = false;         // instances or alpha maps: leaf packets with special lanes (INST kernels)
     std::vector<void*> bufs;     // textures and dome tables (freed with the state)
     const float* env = nullptr;  // environment texture (one of bufs)
     uint16_t* tables = nullptr;
@@ -466,7 +476,7 @@ static void free_device(DeviceState* d) {
     for (StreamCtx* c : d->ctxs) free_ctx(c);
     for (hipStream_t st : d->share_streams) (void)hipStreamDestroy(st);
     void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts, d->tables,
-                    d->gamma, d->gammaF, d->d_rgb, d->d_rgb8};
+                    d->gamma, d->gammaF, d->d_rgb, d->d_rgb8, d->texs, d->puv, d->uvs, d->tans, d->btans};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (void* p : d->bufs)
@@ -553,13 +563,61 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
         p.mat = (uint32_t)m.material;
         return p;
     };
+    // texture coordinates of texture-mapped meshes: (u, v) pairs, per-prim indices,
+    // per-normal tangent frames (TriangleMesh::preCalc, host_texture.cpp)
+    bool any_uv = false;
+    for (const Mesh& m : s.meshes) any_uv |= !m.tidx.empty();
+    std::vector<float2> UV;
+    std::vector<float4> TN, BTN;
+    std::vector<uint32_t> ubase(s.meshes.size(), 0);
+    if (any_uv) {
+        TN.assign(N.size(), make_float4(0.f, 0.f, 0.f, 0.f));
+        BTN.assign(N.size(), make_float4(0.f, 0.f, 0.f, 0.f));
+        for (size_t m = 0; m < s.meshes.size(); m++) {
+            const Mesh& M = s.meshes[m];
+            ubase[m] = (uint32_t)UV.size();
+            if (M.tidx.empty()) continue;
+            for (size_t i = 0; i + 1 < M.uv.size(); i += 2) UV.push_back(make_float2(M.uv[i], M.uv[i + 1]));
+            for (size_t i = 0; i < M.tan.size(); i++) {
+                TN[nbase[m] + i] = make_float4(M.tan[i].x, M.tan[i].y, M.tan[i].z, 0.f);
+                BTN[nbase[m] + i] = make_float4(M.btan[i].x, M.btan[i].y, M.btan[i].z, 0.f);
+            }
+        }
+    }
+    auto uv_rec = [&](int32_t mesh, int32_t tri) {
+        uint4 u = make_uint4(0u, 0u, 0u, 0u);
+        if (mesh < 0 || s.meshes[mesh].tidx.empty()) return u;
+        const uint32_t* t = &s.meshes[mesh].tidx[3 * (size_t)tri];
+        return make_uint4(ubase[mesh] + t[0], ubase[mesh] + t[1], ubase[mesh] + t[2], 1u);
+    };
     std::vector<PrimShade> PS;
-    for (size_t i = 0; i < s.obj_mesh.size(); i++) PS.push_back(shade_rec(s.obj_mesh[i], s.obj_tri[i]));
+    std::vector<uint4> PUV;
+    for (size_t i = 0; i < s.obj_mesh.size(); i++) {
+        PS.push_back(shade_rec(s.obj_mesh[i], s.obj_tri[i]));
+        if (any_uv) PUV.push_back(uv_rec(s.obj_mesh[i], s.obj_tri[i]));
+    }
     std::vector<int32_t> shade_base(s.blas.size());
     for (size_t b = 0; b < s.blas.size(); b++) {
         shade_base[b] = (int32_t)PS.size();
-        for (size_t i = 0; i < s.blas[b].obj_mesh.size(); i++) PS.push_back(shade_rec(s.blas[b].obj_mesh[i], s.blas[b].obj_tri[i]));
+        for (size_t i = 0; i < s.blas[b].obj_mesh.size(); i++) {
+            PS.push_back(shade_rec(s.blas[b].obj_mesh[i], s.blas[b].obj_tri[i]));
+            if (any_uv) PUV.push_back(uv_rec(s.blas[b].obj_mesh[i], s.blas[b].obj_tri[i]));
+        }
     }
+    // materials with maps; world leaf packets holding alpha-mapped triangles
+    d.has_maps = false;
+    std::vector<char> alpha_mat(s.materials.size(), 0);
+    for (size_t m = 0; m < s.materials.size(); m++) {
+        const int32_t* mp = s.materials[m].maps;
+        d.has_maps |= mp[kMapColor] >= 0 || mp[kMapNormal] >= 0 || mp[kMapSpecular] >= 0 || mp[kMapReflect] >= 0 ||
+                      mp[kMapRefract] >= 0;
+        alpha_mat[m] = mp[kMapAlpha] >= 0;
+    }
+    auto alpha_obj = [&](int32_t p) {
+        return p >= 0 && (size_t)p < s.obj_mesh.size() && s.obj_mesh[p] >= 0 &&
+               alpha_mat[(size_t)s.meshes[s.obj_mesh[p]].material];
+    };
+    d.has_alpha = false;
     std::vector<uint16_t> tab(4096);
     memcpy(tab.data(), host_rcp_table(), 4096);
     memcpy(tab.data() + 2048, host_rsqrt_table(), 4096);
@@ -570,7 +628,7 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     // bit (leaf_child); a ProxyObject lane's prim is -2 - instance.
     size_t n_leaves = s.leaves.size();
     for (const Blas& B : s.blas) n_leaves += B.leaves.size();
-    if (n_leaves >= (size_t(1) << 28)) { set_error("too many leaf packets"); return MRT_ERR_OVERFLOW; }
+    if (n_leaves >= (size_t(1) << 27)) { set_error("too many leaf packets"); return MRT_ERR_OVERFLOW; }
     std::vector<QNode> DN;
     std::vector<DLeaf> DL;
     auto append = [&](const std::vector<QNode>& nodes, const std::vector<QLeaf>& leaves,
@@ -584,13 +642,15 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
                 if (c >= 0) { q.child[k] = c + nb; continue; }
                 const QLeaf& L = leaves[(size_t)~c];
                 int cnt = 0;
-                bool proxy = false;
+                bool proxy = false, alpha = false;
                 for (int j = 0; j < 4; j++)
                     if (L.prim[j] >= 0) {  // zero-filled lanes below cnt are rejected by det = 0
                         cnt = j + 1;
                         proxy |= proxy_of(L.prim[j]) >= 0;
+                        alpha |= oi != nullptr && proxy_of(L.prim[j]) < 0 && alpha_obj(L.prim[j]);   // world leaves only
                     }
-                q.child[k] = leaf_child((uint32_t)(~c + lb), cnt < 1 ? 1 : cnt, proxy);
+                d.has_alpha |= alpha;
+                q.child[k] = leaf_child((uint32_t)(~c + lb), cnt < 1 ? 1 : cnt, proxy, alpha);
             }
             DN.push_back(q);
         }
@@ -659,6 +719,16 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     }
     if ((rc = upload(d.domes, DD.data(), DD.size() * sizeof(DevDome), total))) return rc;
     d.env = s.env_tex >= 0 ? dtex[s.env_tex] : nullptr;
+    std::vector<DevTexture> DT(s.textures.size());
+    for (size_t i = 0; i < DT.size(); i++) DT[i] = DevTexture{dtex[i], s.textures[i].W, s.textures[i].H, s.textures[i].type, 0};
+    if ((rc = upload(d.texs, DT.data(), DT.size() * sizeof(DevTexture), total))) return rc;
+    if (any_uv) {
+        if ((rc = upload(d.puv, PUV.data(), PUV.size() * sizeof(uint4), total))) return rc;
+        if ((rc = upload(d.uvs, UV.data(), UV.size() * sizeof(float2), total))) return rc;
+        if ((rc = upload(d.tans, TN.data(), TN.size() * sizeof(float4), total))) return rc;
+        if ((rc = upload(d.btans, BTN.data(), BTN.size() * sizeof(float4), total))) return rc;
+    }
+    d.special = d.n_insts > 0 || d.has_alpha;
     d.bytes = total;
     // persistent grid: resident workgroups on every CU
     hipDeviceProp_t prop;
@@ -716,6 +786,12 @@ static void fill_params(const Scene& s, RenderParams& P) {
     P.noise = s.noise_threshold;
     P.domes = d.domes;
     P.insts = d.insts;
+    P.texs = d.texs;
+    P.puv = d.puv;
+    P.uvs = d.uvs;
+    P.tans = d.tans;
+    P.btans = d.btans;
+    P.has_maps = d.has_maps ? 1 : 0;
     P.n_insts = d.n_insts;
     P.n_world = d.n_world;
     P.env = d.env;
@@ -734,7 +810,7 @@ static void fill_params(const Scene& s, RenderParams& P) {
 // chain levels of the REC kernels: reflection / refraction bounces (< 5) plus
 // the GI bounces (giBounces < m_maxBounces - 1)
 static int chain_levels(const Scene& s) { return 6 + (s.path_trace ? s.max_bounces : 0); }
-static int level_words(const Scene& s) { return s.path_trace ? 9 + 3 * (int)s.lights.size() : 3; }
+static int level_words(const Scene& s) { return s.path_trace ? 12 + 3 * (int)s.lights.size() : 3; }
 
 static int ensure_levels(StreamCtx& c, size_t floats) {
     if (floats <= c.lvl_cap) return MRT_OK;
@@ -912,7 +988,7 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     Q.occl = c.occl;
     Q.nrays = c.nrays;
     Q.max_shadow = m;
-    const bool fb = Q.fast_box != 0, inst = d.n_insts > 0;
+    const bool fb = Q.fast_box != 0, inst = d.special;
     const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive), r0 = pick_chain0(true, d.point_only, inst, d.recursive);
     const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive),
                    rk = pick_chain_shade(true, d.point_only, inst, d.recursive);
@@ -998,7 +1074,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     };
     HIP_OK(hipEventRecord(c.ev0, stream));
     const bool fb = P.fast_box != 0;
-    const bool inst = d.n_insts > 0;
+    const bool inst = d.special;   // instances or alpha maps: the special-leaf kernels
     if (P.min_subdivs > 1 || P.max_subdivs > 1) {
         HIP_OK(hipEventRecord(c.evm, stream));   // primary_ms = 0: one launch
         if ((rc = launch(pick_adaptive(count, d.point_only, fb, inst, d.recursive)))) return rc;
@@ -1012,7 +1088,8 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst)))) return rc;
     HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
-    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst && !d.recursive;
+    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst && !d.recursive &&
+                     !d.has_maps;
     const int max_sh = max_shadow_rays(s);
     // secondary rays and their shadow rays depend on hits along the path: fused kernel
     const bool wave = !one && g_wavefront && max_sh > 0 && max_sh <= kMaxWaveShadow && !d.recursive;
@@ -1086,6 +1163,7 @@ int mrt_scene_add_material(mrt_scene* s, const mrt_material* m) {
     memcpy(d.le, m->le, 12);
     d.emitted = m->emitted;
     d.sample_env = 1;                                                 // Material::Material, src/Material.cpp:6
+    for (int k = 0; k < 6; k++) d.maps[k] = -1;                       // no maps (src/Material.cpp:4-5)
     d.emitter = (d.emitted > 0.0f || (d.le[0] + d.le[1]) + d.le[2] > 0.0f) ? 1 : 0;   // src/Blinn.cpp:47
     if (m->type != MRT_BLINN) { d.le[0] = d.le[1] = d.le[2] = 0.f; d.emitted = 0.f; d.emitter = 0; }
     s->impl.materials.push_back(d);
@@ -1104,8 +1182,9 @@ int mrt_scene_add_light(mrt_scene* s, const mrt_light* l) {
     d.dome = -1;
     if (l->type == MRT_DOME_LIGHT) {
         // DomeLight::setTexture (src/DomeLight.cpp:8-78): tables built now, on the host
-        if (l->texture < 0 || l->texture >= (int32_t)s->impl.textures.size()) {
-            set_error("dome light needs a texture id from mrt_scene_add_texture");
+        if (l->texture < 0 || l->texture >= (int32_t)s->impl.textures.size() ||
+            tex_channels(s->impl.textures[l->texture].type) != 3) {
+            set_error("dome light needs an RGB / HDR texture id from mrt_scene_add_texture");
             return MRT_ERR_INVALID;
         }
         DomeTables t;
@@ -1208,6 +1287,57 @@ int mrt_hdr_load(const char* path, float* rgb, int32_t width, int32_t height) {
     return MRT_OK;
 }
 
+int mrt_image_info(const char* path, int32_t* width, int32_t* height, int32_t* type) {
+    if (!path || !width || !height || !type) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    int W = 0, H = 0, T = 0;
+    std::string err;
+    const int rc = load_image(path, W, H, T, nullptr, err);
+    if (rc) { set_error(err); return rc; }
+    *width = W;
+    *height = H;
+    *type = T;
+    return MRT_OK;
+}
+
+int mrt_image_load(const char* path, float* data, int32_t width, int32_t height) {
+    if (!path || !data) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    int W = 0, H = 0, T = 0;
+    std::string err;
+    std::vector<float> buf;
+    const int rc = load_image(path, W, H, T, &buf, err);
+    if (rc) { set_error(err); return rc; }
+    if (W != width || H != height) { set_error("image size differs from width x height (see mrt_image_info)"); return MRT_ERR_INVALID; }
+    memcpy(data, buf.data(), buf.size() * sizeof(float));
+    return MRT_OK;
+}
+
+int mrt_scene_add_texture_typed(mrt_scene* s, const float* data, int32_t width, int32_t height, int32_t type) {
+    if (!s || !data || width <= 0 || height <= 0 || (int64_t)width * height > (int64_t(1) << 28) ||
+        (type != kTexHDR && type != kTexGray && type != kTexRGB && type != kTexRGBA)) {
+        set_error("bad texture");
+        return MRT_ERR_INVALID;
+    }
+    if (s->impl.textures.size() >= (size_t)kMaxTextures) { set_error("too many textures"); return MRT_ERR_INVALID; }
+    Texture t;
+    t.W = width;
+    t.H = height;
+    t.type = type;
+    t.rgb.assign(data, data + (size_t)width * height * tex_channels(type));
+    s->impl.textures.push_back(std::move(t));
+    s->impl.dev_dirty = true;
+    return (int)s->impl.textures.size() - 1;
+}
+
+int mrt_scene_set_material_maps(mrt_scene* s, int material, const int32_t maps[6]) {
+    if (!s || !maps || material < 0 || material >= (int)s->impl.materials.size()) { set_error("bad material"); return MRT_ERR_INVALID; }
+    for (int k = 0; k < 6; k++)
+        if (maps[k] < -1 || maps[k] >= (int32_t)s->impl.textures.size()) { set_error("bad texture id"); return MRT_ERR_INVALID; }
+    for (int k = 0; k < 6; k++) s->impl.materials[material].maps[k] = maps[k];
+    s->impl.built = false;   // alpha maps change which leaf packets need the alpha test
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
 int mrt_scene_add_texture(mrt_scene* s, const float* rgb, int32_t width, int32_t height) {
     if (!s || !rgb || width <= 0 || height <= 0 || (int64_t)width * height > (int64_t(1) << 28)) {
         set_error("bad texture");
@@ -1224,7 +1354,11 @@ int mrt_scene_add_texture(mrt_scene* s, const float* rgb, int32_t width, int32_t
 }
 
 int mrt_scene_set_env_map(mrt_scene* s, int32_t texture, float exposure) {
-    if (!s || texture < -1 || texture >= (int32_t)s->impl.textures.size()) { set_error("bad texture id"); return MRT_ERR_INVALID; }
+    if (!s || texture < -1 || texture >= (int32_t)s->impl.textures.size() ||
+        (texture >= 0 && tex_channels(s->impl.textures[texture].type) != 3)) {
+        set_error("bad texture id (the environment map needs an RGB / HDR texture)");
+        return MRT_ERR_INVALID;
+    }
     s->impl.env_tex = texture;
     s->impl.env_exposure = exposure;
     s->impl.dev_dirty = true;
@@ -1311,6 +1445,30 @@ int mrt_scene_mesh_export(const mrt_scene* s, int mesh, float* verts, float* nor
     for (size_t i = 0; i < m.normals.size(); i++) { normals[3*i] = m.normals[i].x; normals[3*i+1] = m.normals[i].y; normals[3*i+2] = m.normals[i].z; }
     memcpy(vidx, m.vidx.data(), m.vidx.size() * 4);
     memcpy(nidx, m.nidx.data(), m.nidx.size() * 4);
+    return MRT_OK;
+}
+
+int mrt_scene_mesh_set_texcoords(mrt_scene* s, int mesh, const float* uv, int32_t n_texcoords, const uint32_t* tidx) {
+    if (!s || mesh < 0 || mesh >= (int)s->impl.meshes.size() || !uv || !tidx || n_texcoords <= 0) {
+        set_error("bad texcoords");
+        return MRT_ERR_INVALID;
+    }
+    Mesh& m = s->impl.meshes[mesh];
+    for (size_t i = 0; i < m.vidx.size(); i++)
+        if (tidx[i] >= (uint32_t)n_texcoords) { set_error("texture-coordinate index out of range"); return MRT_ERR_INVALID; }
+    m.uv.assign(uv, uv + 2 * (size_t)n_texcoords);
+    m.tidx.assign(tidx, tidx + m.vidx.size());
+    s->impl.built = false;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
+int mrt_scene_mesh_texcoords(const mrt_scene* s, int mesh, int32_t* n_texcoords, float* uv, uint32_t* tidx) {
+    if (!s || mesh < 0 || mesh >= (int)s->impl.meshes.size() || !n_texcoords) { set_error("bad mesh id"); return MRT_ERR_INVALID; }
+    const Mesh& m = s->impl.meshes[mesh];
+    *n_texcoords = m.tidx.empty() ? 0 : (int32_t)(m.uv.size() / 2);
+    if (*n_texcoords && uv) memcpy(uv, m.uv.data(), m.uv.size() * sizeof(float));
+    if (*n_texcoords && tidx) memcpy(tidx, m.tidx.data(), m.tidx.size() * sizeof(uint32_t));
     return MRT_OK;
 }
 
@@ -1821,10 +1979,12 @@ int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const floa
     c.last_was_render = false;
     int grid = (int)std::min<size_t>((size_t)d.grid, (n + kWG - 1) / kWG);
     HIP_OK(hipEventRecord(c.ev0, (hipStream_t)stream));
-    auto kern = any_hit ? (d.n_insts ? trace_kernel<true, true> : trace_kernel<true, false>)
-                        : (d.n_insts ? trace_kernel<false, true> : trace_kernel<false, false>);
+    auto kern = any_hit ? (d.special ? trace_kernel<true, true> : trace_kernel<true, false>)
+                        : (d.special ? trace_kernel<false, true> : trace_kernel<false, false>);
+    Trav alpha{};
+    alpha.aprims = d.prims; alpha.apuv = d.puv; alpha.auv = d.uvs; alpha.amats = d.mats; alpha.atex = d.texs;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables, c.gstack,
-                       d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, c.ctr, fast_box(d), d.insts);
+                       d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, c.ctr, fast_box(d), d.insts, alpha);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(c.ev1, (hipStream_t)stream));
     d.last = &c;

@@ -14,6 +14,7 @@
 
 #include "../../include/mrt.h"
 #include "mrt_math.h"
+#include "mrt_texture.h"
 #include "mrt_types.h"
 
 namespace mrt {
@@ -60,6 +61,13 @@ struct Trav {
     int32_t* gstk;            // this thread's global spill column (stride gstride)
     uint32_t gstride;
     const DevInstance* inst = nullptr;  // ProxyObjects (instanced scenes)
+    // alpha-mapped triangles (Material::m_alphaMap, src/BVH.cpp:1397-1445): the
+    // shading records, texture coordinates, materials and map textures
+    const PrimShade* aprims = nullptr;
+    const uint4* apuv = nullptr;        // per prim: texture-coordinate indices, w = has texcoords
+    const float2* auv = nullptr;
+    const DevMaterial* amats = nullptr;
+    const DevTexture* atex = nullptr;
 };
 
 struct TravStats {
@@ -154,11 +162,35 @@ __device__ __forceinline__ int box_test_fast(const float4* bx, const DRay& r, fl
 }
 
 // Device child word of a QNode slot: >= 0 inner node; kEmptySlot; otherwise
-// ~(leaf << 3 | proxy << 2 | (count - 1)) with count = objects in the packet and
-// proxy = the packet has ProxyObject (checkOut) lanes (the host re-encodes the
-// canonical ~leaf on upload).
-__host__ __device__ __forceinline__ int32_t leaf_child(uint32_t leaf, int count, bool proxy = false) {
-    return ~(int32_t)((leaf << 3) | (proxy ? 4u : 0u) | (uint32_t)(count - 1));
+// ~(leaf << 4 | alpha << 3 | proxy << 2 | (count - 1)) with count = objects in
+// the packet, proxy = the packet has ProxyObject (checkOut) lanes and alpha = it
+// has alpha-mapped triangles (the host re-encodes the canonical ~leaf on upload).
+__host__ __device__ __forceinline__ int32_t leaf_child(uint32_t leaf, int count, bool proxy = false, bool alpha = false) {
+    return ~(int32_t)((leaf << 4) | (alpha ? 8u : 0u) | (proxy ? 4u : 0u) | (uint32_t)(count - 1));
+}
+
+// intersect4's alpha test (src/BVH.cpp:1401-1423) for lane k of leaf packet
+// `leaf`: the triangle's material has an alpha map and getLookupAlpha at the
+// hit's (u, v) -- interpolated texture coordinates, or (a, b) without them --
+// is below 0.5.  Such a triangle is skipped; with the lanes walked in slot order
+// and only t < best accepted, the first surviving lane of lowest t wins, as in
+// the reference's t-ordered retry loop.
+__device__ __noinline__ bool alpha_rejects(const Trav& c, uint32_t leaf, int k, float a, float b) {
+    const int32_t prim = c.leaves[leaf].prim[k];
+    const int am = c.amats[c.aprims[prim].mat].maps[kMapAlpha];
+    if (am < 0) return false;
+    float u = a, v = b;
+    if (c.apuv) {
+        const uint4 t = c.apuv[prim];
+        if (t.w) {
+            const float cc = 1.0f - a - b;
+            const float2 t0 = c.auv[t.x], t1 = c.auv[t.y], t2 = c.auv[t.z];
+            u = t0.x * cc + t1.x * a + t2.x * b;
+            v = t0.y * cc + t1.y * a + t2.y * b;
+        }
+    }
+    const DevTexture& T = c.atex[am];
+    return tex_lookup4(T.data, T.W, T.H, T.type, u, v).w < 0.5f;
 }
 
 __device__ __forceinline__ float dp4(const float* row, float x, float y, float z, float w) {
@@ -275,15 +307,17 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         if (lm) {
             uint32_t leaf = 0;
             int k = 0, cnt = 0;
+            bool alpha = false;
             while (true) {
                 if (k == cnt) {
                     if (!lm) break;
                     const int s = __builtin_ctz((unsigned)lm);
                     lm &= lm - 1;
                     const uint32_t v = ~(uint32_t)sel4(ch, s);
-                    leaf = v >> 3;
+                    leaf = v >> 4;
                     cnt = (int)(v & 3u) + 1;
                     k = 0;
+                    alpha = INST && (v & 8u);
                     if (COUNT) st.leaves++;
                     if (INST && (v & 4u)) {
                         for (int j = 0; j < cnt; j++) {
@@ -301,7 +335,8 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                     }
                 }
                 float t, a, b;
-                if (tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT)) {
+                if (tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT) &&
+                    !(INST && alpha && alpha_rejects(c, leaf, k, a, b))) {
                     if (ANY) return true;
                     h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
                     if (INST) h.inst = -1;
@@ -387,7 +422,7 @@ __device__ bool traverse_pf(const Trav& c, const DRay& r, float tMin, DHit& h, T
                     const int s = __builtin_ctz((unsigned)lm);
                     lm &= lm - 1;
                     const uint32_t v = ~(uint32_t)sel4(ch, s);
-                    leaf = v >> 3;
+                    leaf = v >> 4;
                     cnt = (int)(v & 3u) + 1;
                     k = 0;
                     if (COUNT) st.leaves++;
@@ -470,7 +505,7 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
                 const int s = __builtin_ctz((unsigned)lm);
                 lm &= lm - 1;
                 const uint32_t v = ~(uint32_t)sel4(ch, s);
-                leaf = v >> 3;
+                leaf = v >> 4;
                 cnt = (int)(v & 3u) + 1;
                 k = 0;
                 if (COUNT) st.leaves++;

@@ -21,12 +21,22 @@ struct Mesh {
     std::vector<v3> verts, normals;
     std::vector<uint32_t> vidx, nidx;
     int material = 0;
+    // TriangleMesh m_texCoords (u, v pairs) / m_texCoordIndices (empty: none), and
+    // the per-normal tangent frame TriangleMesh::preCalc derives from them
+    std::vector<float> uv;
+    std::vector<uint32_t> tidx;
+    std::vector<v3> tan, btan;
     int32_t nt() const { return (int32_t)(vidx.size() / 3); }
 };
 
-struct Texture {                // RawImage (src/RawImage.h): W*H*3 floats, row 0 = top
+// RawImage types (src/RawImage.h ImageType): floats per texel 3 (HDR), 1, 3, 4
+enum { kTexHDR = 0, kTexGray = 1, kTexRGB = 3, kTexRGBA = 4 };
+inline int tex_channels(int type) { return type == kTexGray ? 1 : type == kTexRGBA ? 4 : 3; }
+
+struct Texture {                // RawImage (src/RawImage.h): W*H*channels floats (m_rawData order)
     std::vector<float> rgb;
     int32_t W = 0, H = 0;
+    int32_t type = kTexHDR;
 };
 
 struct DomeTables {             // DomeLight::setTexture (src/DomeLight.cpp:8-78)
@@ -115,6 +125,10 @@ int add_instance(Scene& s, int32_t blas, const float* m16, std::string& err);
 // host_texture.cpp
 int load_hdr(const char* path, int& W, int& H, std::vector<float>* rgb, std::string& err);
 int build_dome(const Texture& t, DomeTables& d, std::string& err);
+// RawImage::loadImage (TGA / PPM / HDR by extension); data == nullptr: size + type only
+int load_image(const char* path, int& W, int& H, int& type, std::vector<float>* data, std::string& err);
+// TriangleMesh::preCalc's tangent frame (src/TriangleMesh.cpp:105-148)
+void mesh_tangents(Mesh& m);
 
 void set_error(const std::string& msg);
 

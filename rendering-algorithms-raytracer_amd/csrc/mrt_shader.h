@@ -47,6 +47,14 @@ struct RenderParams {
     const DevLight* lights;
     const DevDome* domes;    // dome-light tables (DevLight::dome)
     const DevInstance* insts;  // ProxyObjects (instanced scenes)
+    // material maps (src/Material.h:20-25): map textures, per-prim texture-coordinate
+    // indices (w = the mesh has texture coordinates), (u, v) pairs, per-normal tangents
+    const DevTexture* texs;
+    const uint4* puv;
+    const float2* uvs;
+    const float4* tans;
+    const float4* btans;
+    int32_t has_maps;          // some material has a colour / normal / specular / reflect / refract map
     int32_t n_insts, n_world;  // instances; world objects (instance hit ids start here)
     const float* env;        // environment map (nullable), env_w x env_h RGB, row 0 = top
     float4* ray_o;           // wavefront shadow rays: slot * max_shadow + j -> origin, tMax
@@ -133,6 +141,15 @@ __device__ __forceinline__ uint32_t level_key(int level) { return (uint32_t)(lev
 // src/Ray.h:43-50): a per-lane LDS column in the REC kernels.
 static constexpr int kIorCap = 8;
 
+// the alpha-test tables of a traversal (special-leaf kernels only read them)
+__device__ __forceinline__ void trav_alpha(Trav& T, const RenderParams& P) {
+    T.aprims = P.prims;
+    T.apuv = P.puv;
+    T.auv = P.uvs;
+    T.amats = P.mats;
+    T.atex = P.texs;
+}
+
 // Chain state of one path at its current level (Shader::level).
 enum { kRefl = 1, kRefr = 2, kGI = 3 };
 struct ChainState {
@@ -169,9 +186,9 @@ __device__ __forceinline__ v3 chain_combine(const RenderParams& P, const ChainRe
     const int kind = info >> 16;
     const float rrRecip = rec(1), rrSpec = rec(2);
     const v3 le = mk(M.le[0], M.le[1], M.le[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
-    if (kind == kGI) {   // Ld = 0 + (0 + kd * child) + each light's E * kd + ka
-        v3 Ld = add(z, none ? z : add(z, mul(mk(M.kd[0], M.kd[1], M.kd[2]), val)));
-        for (int i = 0; i < P.n_lights; i++) Ld = add(Ld, mk(rec(9 + 3 * i), rec(10 + 3 * i), rec(11 + 3 * i)));
+    if (kind == kGI) {   // Ld = 0 + (0 + diffuseColor * child) + each light's E * diffuseColor + ka
+        v3 Ld = add(z, none ? z : add(z, mul(mk(rec(9), rec(10), rec(11)), val)));
+        for (int i = 0; i < P.n_lights; i++) Ld = add(Ld, mk(rec(12 + 3 * i), rec(13 + 3 * i), rec(14 + 3 * i)));
         Ld = add(Ld, ka);
         const v3 Ls = mk(rec(3), rec(4), rec(5)), tr = mk(rec(6), rec(7), rec(8));
         return add(add(scale(add(add(Ld, Ls), tr), rrRecip), scale(add(z, z), rrSpec)), le);
@@ -370,6 +387,63 @@ struct Shader {
             N = normalized(xform_dir3(T, N), rsqT);
         }
         mat = ps.mat;
+        psi = ps_i;
+    }
+
+    // HitInfo::getAllInfos' texture part (src/Ray.cpp:33-47) and the maps of
+    // Lambert::shade (colour, src/Lambert.cpp:32-36) / Blinn::shade (colour,
+    // normal, specular, reflect, refract, src/Blinn.cpp:114-142) at the hit of the
+    // last normals() call.  (u, v) interpolate the texture coordinates, or are
+    // (a, b) without them; the tangent frame interpolates over the normal indices.
+    int32_t psi = 0;   // PrimShade index of the last normals() call
+    __device__ void maps(const DHit& h, const DevMaterial& M, bool blinn, v3& N, v3& kd, float& spec_amt, float& refl,
+                         float& refr) {
+        float u = h.a, v = h.b;
+        v3 T = mk(0, 0, 0), BT = mk(0, 0, 0);
+        const bool nmap = blinn && M.maps[kMapNormal] >= 0;
+        if (P.puv) {
+            const uint4 t = P.puv[psi];
+            if (t.w) {
+                const float c = 1.0f - h.a - h.b;
+                if (nmap) {
+                    const PrimShade ps = P.prims[psi];
+                    const float4 t0 = P.tans[ps.n[0]], t1 = P.tans[ps.n[1]], t2 = P.tans[ps.n[2]];
+                    const float4 b0 = P.btans[ps.n[0]], b1 = P.btans[ps.n[1]], b2 = P.btans[ps.n[2]];
+                    T = normalized(add(add(scale(mk(t0.x, t0.y, t0.z), c), scale(mk(t1.x, t1.y, t1.z), h.a)),
+                                       scale(mk(t2.x, t2.y, t2.z), h.b)), rsqT);
+                    BT = normalized(add(add(scale(mk(b0.x, b0.y, b0.z), c), scale(mk(b1.x, b1.y, b1.z), h.a)),
+                                        scale(mk(b2.x, b2.y, b2.z), h.b)), rsqT);
+                }
+                const float2 a0 = P.uvs[t.x], a1 = P.uvs[t.y], a2 = P.uvs[t.z];
+                u = a0.x * c + a1.x * h.a + a2.x * h.b;
+                v = a0.y * c + a1.y * h.a + a2.y * h.b;
+            }
+        }
+        auto look = [&](int tex) {
+            const DevTexture& X = P.texs[tex];
+            return tex_lookup4(X.data, X.W, X.H, X.type, u, v);
+        };
+        if (M.maps[kMapColor] >= 0) {
+            const float4 x = look(M.maps[kMapColor]);
+            kd = mk(x.x, x.y, x.z);
+        }
+        if (!blinn) return;
+        if (nmap) {   // N = texN.x*T + texN.y*BT + texN.z*N, not renormalised
+            const float4 x = look(M.maps[kMapNormal]);
+            N = add(add(scale(T, x.x), scale(BT, x.y)), scale(N, x.z));
+        }
+        if (M.maps[kMapSpecular] >= 0) {
+            const float4 x = look(M.maps[kMapSpecular]);
+            spec_amt = ((x.x + x.y) + x.z) * 0.3333333f * spec_amt;
+        }
+        if (M.maps[kMapReflect] >= 0) {
+            const float4 x = look(M.maps[kMapReflect]);
+            refl = ((x.x + x.y) + x.z) * 0.3333333f * refl;
+        }
+        if (M.maps[kMapRefract] >= 0) {
+            const float4 x = look(M.maps[kMapRefract]);
+            refr = ((x.x + x.y) + x.z) * 0.3333333f * refr;
+        }
     }
 
     // Scene::sampleScene hit branch (src/Scene.cpp:224-233): m_numPaths shade()
@@ -382,6 +456,8 @@ struct Shader {
         const DevMaterial& M = P.mats[mi];
         v3 P_ = mk(r.o[0] + h.t * r.d[0], r.o[1] + h.t * r.d[1], r.o[2] + h.t * r.d[2]);  // Ray::getPoint
         v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+        float spec_amt = M.spec_amt, refl_unused = M.reflect, refr_unused = M.refract;
+        if (P.has_maps) maps(h, M, M.type != MRT_LAMBERT, N, kd, spec_amt, refl_unused, refr_unused);
         v3 result = mk(0, 0, 0);
         // the camera ray's IOR history [1, 1.001]: Blinn::shade pops it on a
         // back-face hit and the pop persists into the next path (src/Blinn.cpp:176-179)
@@ -418,7 +494,7 @@ struct Shader {
                     float spec = 0.f;
                     v3 E = sample_light<COUNT>(i, P_, n, rVec, spec);
                     float pw = (M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
-                    Ls = add(Ls, scale(scale(mul(E, ks), M.spec_amt), pw));
+                    Ls = add(Ls, scale(scale(mul(E, ks), spec_amt), pw));
                     Ld = add(Ld, mul(E, kd));
                 }
                 Ld = add(Ld, ka);
@@ -496,7 +572,10 @@ struct Shader {
         normals(h, N, geoN, mi);
         const DevMaterial& M = P.mats[mi];
         const v3 Pt = mk(r.o[0] + h.t * r.d[0], r.o[1] + h.t * r.d[1], r.o[2] + h.t * r.d[2]);
-        const v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+        v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]);
+        const v3 ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+        float spec_amt = M.spec_amt, reflect = M.reflect, refract = M.refract;   // localSpecAmt / ReflectAmt / RefractAmt
+        if (P.has_maps) maps(h, M, M.type != MRT_LAMBERT, N, kd, spec_amt, reflect, refract);
         if (M.type == MRT_LAMBERT) {   // Lambert::shade: no secondary rays (isSecondary not passed on)
             v3 L = z;
             for (int i = 0; i < P.n_lights; i++) {
@@ -537,7 +616,7 @@ struct Shader {
             Ts = 1.0f - Rs;
         }
         float rr = next_rand();
-        const float rrW = (1.0f - Rs * M.reflect) - Ts * M.refract;
+        const float rrW = (1.0f - Rs * reflect) - Ts * refract;
         const float rrRecip = (rrW > 0.f) ? 1.f / rrW : 1.f;
         const float rrSpec = (1.f - rrW > 0.f) ? 1.f / (1.f - rrW) : 1.f;
         const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
@@ -565,9 +644,9 @@ struct Shader {
                 float spec = 0.f;
                 v3 E = sample_light<COUNT>(i, Pt, n, rVec, spec, cs.secondary);
                 float pw = (M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
-                Ls = add(Ls, scale(scale(mul(E, ks), M.spec_amt), pw));
+                Ls = add(Ls, scale(scale(mul(E, ks), spec_amt), pw));
                 const v3 term = mul(E, kd);
-                if (child) { rec(9 + 3 * i) = term.x; rec(10 + 3 * i) = term.y; rec(11 + 3 * i) = term.z; }
+                if (child) { rec(12 + 3 * i) = term.x; rec(13 + 3 * i) = term.y; rec(14 + 3 * i) = term.z; }
                 else Ld = add(Ld, term);
             }
             v3 tr = z;
@@ -584,6 +663,7 @@ struct Shader {
                 rec(1) = rrRecip; rec(2) = rrSpec;
                 rec(3) = Ls.x; rec(4) = Ls.y; rec(5) = Ls.z;
                 rec(6) = tr.x; rec(7) = tr.y; rec(8) = tr.z;
+                rec(9) = kd.x; rec(10) = kd.y; rec(11) = kd.z;   // diffuseColor (colour map) for the combine
                 ior_at(0) = 1.0f; ior_at(1) = curIOR; cs.idx = 1;
                 cs.depth++; cs.gi++;
                 cs.secondary = true;
@@ -602,14 +682,14 @@ struct Shader {
         rr = next_rand();
         bool refr, spawn;
         v3 dir;
-        if (rr < M.reflect * Rs) {
+        if (rr < reflect * Rs) {
             refr = false;
             dir = rVec;
-            spawn = M.reflect * Rs > 0.0f && cs.bounces < kMaxBounce;
+            spawn = reflect * Rs > 0.0f && cs.bounces < kMaxBounce;
             if (spawn && cs.depth == 0) {   // the child copies the camera ray's history
                 ior_at(0) = 1.0f; ior_at(1) = cam.v1; ior_at(2) = cam.v2; cs.idx = cam.idx;
             }
-        } else if (M.refract * Ts > 0.0f) {
+        } else if (refract * Ts > 0.0f) {
             refr = true;
             const float q = inIOR / outIOR;
             const float sq = std_max(0.0f, sqrtf(1.0f - (q * q) * (1.0f - vDotN * vDotN)));
@@ -889,6 +969,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
+    trav_alpha(T, P);
     TravStats st;
     uint32_t nhits = 0;
     unsigned long long wave_steps = 0;  // count mode: sum over tiles of max lane node visits
@@ -939,6 +1020,7 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
+    trav_alpha(T, P);
     TravStats st;
     uint32_t shadow_total = 0, secondary_total = 0;
     TileSched ts(P, wave, lane);
@@ -1029,6 +1111,7 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
+    trav_alpha(T, P);
     TravStats st;
     uint32_t shadow_total = 0, eye_rays = 0, eye_hits = 0, secondary_total = 0;
     TileSched ts(P, wave, lane);

@@ -54,6 +54,45 @@ MRT_HD v3 tex_lookup3(const float* rgb, int W, int H, float u, float v) {
     return add(scale(q1, wy), scale(q2, dy));
 }
 
+#if defined(__HIPCC__)   // float4 (device code; the host builds no material maps)
+// Texture::getPixel for every RawImage type (src/Texture.cpp:100-125): GRAYSCALE
+// (g, g, g, 1), RGB (r, g, b, 1), RGBA, HDR (r, g, b, the next texel's red -- 0
+// past the last texel, where the reference reads beyond the array).
+MRT_HD float4 tex_pixel4(const float* d, int W, int H, int type, int x, int y) {
+    x = x % W;
+    if (x < 0) x += W;
+    y = y % H;
+    if (y < 0) y += H;
+    const size_t i = (size_t)y * W + x;
+    if (type == 1) return make_float4(d[i], d[i], d[i], 1.0f);
+    if (type == 4) return make_float4(d[4 * i], d[4 * i + 1], d[4 * i + 2], d[4 * i + 3]);
+    if (type == 3) return make_float4(d[3 * i], d[3 * i + 1], d[3 * i + 2], 1.0f);
+    return make_float4(d[3 * i], d[3 * i + 1], d[3 * i + 2], i + 1 < (size_t)W * H ? d[3 * i + 3] : 0.0f);
+}
+
+// Texture::getLookup (src/Texture.cpp:43-72) of a material map: wrap to [0,1),
+// flip v, bilinear over four channels (getLookupAlpha = its w, :12-41).
+MRT_HD float4 tex_lookup4(const float* d, int W, int H, int type, float u, float v) {
+    u = u - (float)trunc_i32(u);
+    v = v - (float)trunc_i32(v);
+    if (u < 0.0f) u = u + 1.0f;
+    if (v < 0.0f) v = v + 1.0f;
+    v = 1.0f - v;
+    const float px = u * (float)W, py = v * (float)H;
+    const float x1 = floorf(px), x2 = x1 + 1.0f, dx = px - x1;
+    const float y1 = floorf(py), y2 = y1 + 1.0f, dy = py - y1;
+    const int ix1 = trunc_i32(x1), ix2 = trunc_i32(x2), iy1 = trunc_i32(y1), iy2 = trunc_i32(y2);
+    const float4 p11 = tex_pixel4(d, W, H, type, ix1, iy1), p21 = tex_pixel4(d, W, H, type, ix2, iy1);
+    const float4 p12 = tex_pixel4(d, W, H, type, ix1, iy2), p22 = tex_pixel4(d, W, H, type, ix2, iy2);
+    const float wx = 1.0f - dx, wy = 1.0f - dy;
+    const float4 q1 = make_float4(p11.x * wx + p21.x * dx, p11.y * wx + p21.y * dx, p11.z * wx + p21.z * dx,
+                                  p11.w * wx + p21.w * dx);
+    const float4 q2 = make_float4(p12.x * wx + p22.x * dx, p12.y * wx + p22.y * dx, p12.z * wx + p22.z * dx,
+                                  p12.w * wx + p22.w * dx);
+    return make_float4(q1.x * wy + q2.x * dy, q1.y * wy + q2.y * dy, q1.z * wy + q2.z * dy, q1.w * wy + q2.w * dy);
+}
+#endif
+
 // Texture::getLookupXYZ3 (src/Texture.cpp:80-98): direction -> (u, v).
 //   theta = atan2(z, x) + PI; phi = acos(y);
 //   u = theta * 0.5 * _1_PI   (double arithmetic, rounded to float)

@@ -65,6 +65,17 @@ struct DevMaterial {
     float emitted;           // Blinn m_lightEmitted (src/Blinn.h:63): path-tracing emitter intensity
     int32_t sample_env;      // Material::m_sampleEnv (src/Material.h:43; default true)
     int32_t emitter;         // host-derived: emitted > 0 || le.x + le.y + le.z > 0 (src/Blinn.cpp:47)
+    // Material m_colorMap, m_normalMap, m_specularMap, m_reflectMap, m_refractMap,
+    // m_alphaMap (src/Material.h:20-25,35-40): texture ids, -1 = none
+    int32_t maps[6];
+};
+enum { kMapColor = 0, kMapNormal = 1, kMapSpecular = 2, kMapReflect = 3, kMapRefract = 4, kMapAlpha = 5 };
+
+// A material-map texture on the device (Texture + RawImage, src/Texture.h)
+struct DevTexture {
+    const float* data;   // W*H*channels floats, RawImage m_rawData order
+    int32_t W, H, type;  // type: kTexHDR 0 (3 floats), kTexGray 1, kTexRGB 3, kTexRGBA 4
+    int32_t pad;
 };
 
 struct DevLight {

@@ -110,6 +110,13 @@ class TriangleMesh:
         self.vidx = np.ascontiguousarray(vidx, np.uint32).reshape(-1, 3)
         self.nidx = np.ascontiguousarray(nidx, np.uint32).reshape(-1, 3)
 
+    def setTexCoords(self, uv, tidx):
+        """m_texCoords ((u, v) per texture coordinate) / m_texCoordIndices (3 per triangle)."""
+        self.uv = np.ascontiguousarray(uv, np.float32).reshape(-1, 2)
+        self.tidx = np.ascontiguousarray(tidx, np.uint32).reshape(-1, 3)
+
+    uv = tidx = None
+
     def setV1(self, v): self.verts[0] = v
     def setV2(self, v): self.verts[1] = v
     def setV3(self, v): self.verts[2] = v
@@ -118,7 +125,23 @@ class TriangleMesh:
     def setN3(self, n): self.normals[2] = n
 
 
-class Lambert:
+class _Maps:
+    """Material::setColorMap / setAlphaMap / setNormalMap / setSpecularMap /
+    setReflectMap / setRefractMap (src/Material.h:20-25): Texture objects."""
+    colorMap = normalMap = specularMap = reflectMap = refractMap = alphaMap = None
+
+    def setColorMap(self, t): self.colorMap = t
+    def setNormalMap(self, t): self.normalMap = t
+    def setSpecularMap(self, t): self.specularMap = t
+    def setReflectMap(self, t): self.reflectMap = t
+    def setRefractMap(self, t): self.refractMap = t
+    def setAlphaMap(self, t): self.alphaMap = t
+
+    def _maps(self):
+        return (self.colorMap, self.normalMap, self.specularMap, self.reflectMap, self.refractMap, self.alphaMap)
+
+
+class Lambert(_Maps):
     """Lambert(kd = Vector3(1), ka = Vector3(0)), src/Lambert.h:11-13."""
 
     def __init__(self, kd=Vector3(1), ka=Vector3(0)):
@@ -135,12 +158,13 @@ class Lambert:
         return _lib.mrt_material(0, f3(self.kd), f3(self.ka), f3((1, 1, 1)), 1.0, 0.0, f3((0, 0, 0)), 0.0)
 
 
-class Blinn:
+class Blinn(_Maps):
     """Blinn(kd, ka, ks, kt, ior, specExp, specAmt, reflectAmt, refractAmt) defaults of
     src/Blinn.h:11-22: direct lighting plus Fresnel-weighted reflection / refraction
     rays (src/Blinn.cpp:91-335), glossy reflection vectors, translucency, emission
-    (setLightEmittedIntensity / setLightEmittedColor) and path tracing (Scene.setPathTrace).
-    Dispersion and texture maps are not on the MI355X path."""
+    (setLightEmittedIntensity / setLightEmittedColor), path tracing (Scene.setPathTrace)
+    and texture maps (colour, normal, specular, reflect, refract, alpha).  Dispersion
+    is not on the MI355X path."""
 
     def __init__(self, kd=Vector3(1), ka=Vector3(0), ks=Vector3(1), kt=Vector3(0), ior=1.5,
                  specExp=1.0, specAmt=0.0, reflectAmt=0.0, refractAmt=0.0, specGloss=1.0):
@@ -217,21 +241,32 @@ class RectangleLight(_Light):
                               self.samples, self.noiseThreshold, int(self.castShadows), -1)
 
 
+TEX_HDR, TEX_GRAY, TEX_RGB, TEX_RGBA = 0, 1, 3, 4   # RawImage ImageType (floats per texel 3, 1, 3, 4)
+_CHANNELS = {TEX_HDR: 3, TEX_GRAY: 1, TEX_RGB: 3, TEX_RGBA: 4}
+
+
 class RawImage:
-    """RawImage (src/RawImage.h:9-30): float RGB texels, row 0 = the top row,
-    as HDRLoader::load leaves them (m_rawData).  RawImage(w, h, data) wraps an
-    array; loadImage / loadHDR decode a Radiance .hdr file in libmrt."""
+    """RawImage (src/RawImage.h:9-30): float texels in m_rawData order (row 0 =
+    the top row for .hdr; TGA rows flipped as loadTGA does).  RawImage(w, h, data,
+    type) wraps an array; loadImage decodes .tga / .ppm / .hdr in libmrt."""
 
-    def __init__(self, w=0, h=0, data=None):
-        self.m_width, self.m_height = int(w), int(h)
-        self.m_rawData = None if data is None else np.ascontiguousarray(data, np.float32).reshape(self.m_height,
-                                                                                                   self.m_width, 3)
+    def __init__(self, w=0, h=0, data=None, imageType=TEX_HDR):
+        self.m_width, self.m_height, self.m_imageType = int(w), int(h), int(imageType)
+        self.m_rawData = None if data is None else np.ascontiguousarray(data, np.float32).reshape(
+            self.m_height, self.m_width, _CHANNELS[self.m_imageType])
 
-    def loadImage(self, filename):  # src/RawImage.cpp:16-26
+    def loadImage(self, filename):  # src/RawImage.cpp:16-26 (by extension)
         ext = str(filename).rsplit(".", 1)[-1]
         if ext in ("hdr", "HDR"):
             return self.loadHDR(filename)
-        raise MRTError(f".{ext} images are not on the MI355X path (Radiance .hdr only)")
+        L = lib()
+        w, h, t = C.c_int32(), C.c_int32(), C.c_int32()
+        check(L.mrt_image_info(str(filename).encode(), C.byref(w), C.byref(h), C.byref(t)), f"image {filename}")
+        data = np.zeros((h.value, w.value, _CHANNELS[t.value]), np.float32)
+        check(L.mrt_image_load(str(filename).encode(), data.ctypes.data_as(C.POINTER(C.c_float)), w.value, h.value),
+              f"image {filename}")
+        self.m_width, self.m_height, self.m_imageType, self.m_rawData = w.value, h.value, t.value, data
+        return True
 
     def loadHDR(self, filename):  # src/RawImage.cpp:29-32 -> HDRLoader::load
         L = lib()
@@ -245,8 +280,8 @@ class RawImage:
 
 
 class Texture:
-    """Texture(RawImage) (src/Texture.h:9-28): a lat-long map for DomeLight and
-    Scene.setEnvMap."""
+    """Texture(RawImage) (src/Texture.h:9-28): a material map, or a lat-long map
+    for DomeLight and Scene.setEnvMap."""
 
     def __init__(self, image: RawImage):
         self.m_image = image
@@ -429,9 +464,11 @@ class Scene:
             L.mrt_scene_destroy(self._h)
         self._h = L.mrt_scene_create()
         mats = {}
+        mat_objs = {}
 
         def add_mesh(mesh, mat):
             if id(mat) not in mats:
+                mat_objs[id(mat)] = mat
                 m = mat._c()
                 mats[id(mat)] = check(L.mrt_scene_add_material(self._h, C.byref(m)), "add_material")
                 if isinstance(mat, Blinn):
@@ -449,7 +486,12 @@ class Scene:
             mm = _lib.mrt_mesh(v.ctypes.data_as(C.POINTER(C.c_float)), n.ctypes.data_as(C.POINTER(C.c_float)),
                                vi.ctypes.data_as(C.POINTER(C.c_uint32)), ni.ctypes.data_as(C.POINTER(C.c_uint32)),
                                len(v), len(n), len(vi), v.shape[1] if v.ndim == 2 else 3, n.shape[1] if n.ndim == 2 else 3)
-            return check(L.mrt_scene_add_mesh(self._h, C.byref(mm), mid), "add_mesh")
+            mesh_id = check(L.mrt_scene_add_mesh(self._h, C.byref(mm), mid), "add_mesh")
+            if mesh.uv is not None:
+                check(L.mrt_scene_mesh_set_texcoords(self._h, mesh_id, mesh.uv.ctypes.data_as(C.POINTER(C.c_float)),
+                                                     len(mesh.uv), mesh.tidx.ctypes.data_as(C.POINTER(C.c_uint32))),
+                      "texcoords")
+            return mesh_id
 
         blas = {}   # BVH object -> BLAS id (built once, shared by its instances)
         self.blas_build_ms = 0.0
@@ -480,9 +522,17 @@ class Scene:
                 if img.m_rawData is None:
                     raise MRTError("texture image has no data (loadImage first)")
                 a = np.ascontiguousarray(img.m_rawData, np.float32)
-                tex_ids[id(t)] = check(L.mrt_scene_add_texture(self._h, a.ctypes.data_as(C.POINTER(C.c_float)),
-                                                               img.m_width, img.m_height), "add_texture")
+                tex_ids[id(t)] = check(L.mrt_scene_add_texture_typed(self._h, a.ctypes.data_as(C.POINTER(C.c_float)),
+                                                                     img.m_width, img.m_height,
+                                                                     getattr(img, "m_imageType", TEX_HDR)), "add_texture")
             return tex_ids[id(t)]
+
+        for key, mid in mats.items():   # Material::set*Map
+            mat = mat_objs[key]
+            maps = mat._maps() if isinstance(mat, _Maps) else (None,) * 6
+            if any(m is not None for m in maps):
+                arr = (C.c_int32 * 6)(*[tex_id(m) for m in maps])
+                check(L.mrt_scene_set_material_maps(self._h, mid, arr), "material maps")
 
         for light in self._lights:
             lc = light._c(tex_id(getattr(light, "texture", None)))

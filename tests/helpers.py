@@ -10,10 +10,32 @@ from miro import scenes
 
 from conftest import GOLDEN
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def fixture_mesh(name):
     f = np.load(os.path.join(GOLDEN, f"{name}_mesh.npz"))
     return f["verts"], f["normals"], f["vidx"], f["nidx"]
+
+
+MAP_KINDS = ("color", "normal", "specular", "reflect", "refract", "alpha")
+
+
+def material_maps(pm, O_, om, mat):
+    """mat["maps"]: {kind: (data (H, W, channels), RawImage type)} -> the same
+    Texture on the product material (Material::set*Map) and in the oracle."""
+    maps = mat.get("maps")
+    if not maps:
+        return
+    ids = {}
+    for kind in MAP_KINDS:
+        if kind not in maps:
+            continue
+        data, typ = maps[kind]
+        tex = miro.Texture(miro.RawImage(data.shape[1], data.shape[0], data, typ))
+        getattr(pm, "set%sMap" % kind.capitalize())(tex)
+        ids[kind] = O_.add_texture_typed(data, typ)
+    O_.set_material_maps(om, **ids)
 
 
 def materials_pair(P, O_, mat):
@@ -44,6 +66,7 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
     P = miro.Scene()
     O_ = O.OracleScene()
     pm, om = materials_pair(P, O_, mat)
+    material_maps(pm, O_, om, mat)
     for arrs in (meshes or []):
         tm = miro.TriangleMesh()
         tm.setArrays(*arrs)
@@ -67,16 +90,20 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
         for b, M in placed:
             P.addObject(miro.ProxyObject(*protos[b], miro.Matrix4x4(M)))
             O_.add_instance(oblas[b], M)
-    for arrs, emat in (extra or []):   # mesh arrays, or an OBJ path
+    for arrs, emat in (extra or []):   # mesh arrays (+ uv, tidx), or an OBJ path
         xm, oxm = materials_pair(P, O_, emat)
         tm = miro.TriangleMesh()
         if isinstance(arrs, str):
             tm.load(arrs)
             O_.add_obj(arrs, oxm)
         else:
-            tm.setArrays(*arrs)
-            O_.add_mesh(*arrs, oxm)
+            tm.setArrays(*arrs[:4])
+            mid = O_.add_mesh(*arrs[:4], oxm)
+            if len(arrs) == 6:   # texture coordinates
+                tm.setTexCoords(arrs[4], arrs[5])
+                O_.set_texcoords(mid, arrs[4], arrs[5])
         miro.makeMeshObjs(P, tm, xm)
+        material_maps(xm, O_, oxm, emat)
     if floor:
         fl = miro.TriangleMesh()
         fl.createSingleTriangle()
