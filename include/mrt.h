@@ -183,6 +183,12 @@ int mrt_scene_mesh_export(const mrt_scene* s, int mesh, float* verts, float* nor
  * src/TriangleMesh.cpp:105-148); without texture coordinates (u, v) = (a, b). */
 int mrt_scene_mesh_set_texcoords(mrt_scene* s, int mesh, const float* uv, int32_t n_texcoords, const uint32_t* tidx);
 int mrt_scene_mesh_texcoords(const mrt_scene* s, int mesh, int32_t* n_texcoords, float* uv, uint32_t* tidx);
+/* MBObject(material, mesh, mesh_t2, i) for every triangle of `mesh`
+ * (src/MBObject.cpp:7-11, src/MBObject.h): verts2 = m_mesh_t2's vertices,
+ * n_vertices x 3 floats, same topology.  A ray of time t meets
+ * t*verts2 + (1-t)*verts; shading uses the time-0 mesh.  World meshes only
+ * (instanced BLAS meshes stay static, as in the reference). */
+int mrt_scene_set_mesh_motion(mrt_scene* s, int mesh, const float* verts2);
 /* Scene::setBGColor (src/Scene.h:37) */
 int mrt_scene_set_background(mrt_scene* s, const float rgb[3]);
 /* Scene::m_numPaths (src/Scene.h:61): shade() calls per primary hit */

@@ -171,6 +171,7 @@ typedef struct {
     float* uv;                  /* 2 * ntc */
     uint32_t* tidx;             /* 3 * nt */
     v3* tan; v3* btan;          /* nn each (built with the BVH) */
+    v3* verts2;                 /* MBObject m_mesh_t2 vertices (motion blur), NULL: static */
 } mesh_t;
 
 typedef struct { float mn[3], mx[3]; } aabb;
@@ -226,6 +227,7 @@ struct oro_scene {
     qnode* qn; int n_qn, cap_qn;
     qleaf* ql; int n_ql;
     int built;
+    int is_blas;                      /* a ProxyObject's BVH (sub-scene borrowing the meshes) */
 };
 
 oro_scene* oro_scene_create(void) {
@@ -250,6 +252,7 @@ void oro_scene_destroy(oro_scene* s) {
         free(s->meshes[i].verts); free(s->meshes[i].normals);
         free(s->meshes[i].vidx); free(s->meshes[i].nidx);
         free(s->meshes[i].uv); free(s->meshes[i].tidx); free(s->meshes[i].tan); free(s->meshes[i].btan);
+        free(s->meshes[i].verts2);
     }
     free(s->maps);
     for (int i = 0; i < s->n_lights; i++) ibl_dome_free(&s->domes[i]);
@@ -536,6 +539,18 @@ int oro_mesh_set_texcoords(oro_scene* s, int mesh, int ntc, const float* uv, con
     s->built = 0;
     return 0;
 }
+/* MBObject(mat, m, m2, i) for every triangle of the mesh (src/MBObject.cpp:7-11):
+ * verts2 = m_mesh_t2's vertices (same topology), nv x 3 floats */
+int oro_mesh_set_motion(oro_scene* s, int mesh, const float* verts2) {
+    if (mesh < 0 || mesh >= s->n_meshes || !verts2) return -1;
+    mesh_t* m = &s->meshes[mesh];
+    free(m->verts2);
+    m->verts2 = (v3*)malloc(sizeof(v3) * (m->nv ? m->nv : 1));
+    for (int i = 0; i < m->nv; i++) m->verts2[i] = V(verts2[3 * i], verts2[3 * i + 1], verts2[3 * i + 2]);
+    s->built = 0;
+    return 0;
+}
+
 int oro_mesh_texcoords(const oro_scene* s, int mesh, int* ntc, float* uv, uint32_t* tidx) {
     if (mesh < 0 || mesh >= s->n_meshes) return -1;
     const mesh_t* m = &s->meshes[mesh];
@@ -567,12 +582,25 @@ static inline v3 overt(const oro_scene* s, int o, int k) {
     return m->verts[m->vidx[3 * s->obj_tri[o] + k]];
 }
 /* TriangleMesh::getAABB, src/TriangleMesh.cpp:156-195 */
-static aabb obj_aabb(const oro_scene* s, int o) {
-    if (s->obj_inst && s->obj_inst[o] >= 0) return s->inst[s->obj_inst[o]].box;   /* ProxyObject::getAABB */
-    v3 A = overt(s, o, 0), B = overt(s, o, 1), C = overt(s, o, 2);
+static aabb tri_aabb(v3 A, v3 B, v3 C) {
     aabb b;
     b.mn[0] = std_min(A.x, std_min(B.x, C.x)); b.mn[1] = std_min(A.y, std_min(B.y, C.y)); b.mn[2] = std_min(A.z, std_min(B.z, C.z));
     b.mx[0] = std_max(A.x, std_max(B.x, C.x)); b.mx[1] = std_max(A.y, std_max(B.y, C.y)); b.mx[2] = std_max(A.z, std_max(B.z, C.z));
+    return b;
+}
+static aabb aabb_union(aabb a, aabb b);
+/* an MBObject lane (world geometry only; a ProxyObject's BVH holds plain Objects) */
+static int obj_is_mb(const oro_scene* s, int o) {
+    return o >= 0 && !s->is_blas && s->meshes && (!s->obj_inst || s->obj_inst[o] < 0) && omesh(s, o)->verts2 != NULL;
+}
+static aabb obj_aabb(const oro_scene* s, int o) {
+    if (s->obj_inst && s->obj_inst[o] >= 0) return s->inst[s->obj_inst[o]].box;   /* ProxyObject::getAABB */
+    aabb b = tri_aabb(overt(s, o, 0), overt(s, o, 1), overt(s, o, 2));
+    if (obj_is_mb(s, o)) {   /* MBObject::getAABB: AABB(t0 triangle box, t2 triangle box), src/MBObject.cpp */
+        const mesh_t* m = omesh(s, o);
+        const uint32_t* vi = m->vidx + 3 * s->obj_tri[o];
+        b = aabb_union(b, tri_aabb(m->verts2[vi[0]], m->verts2[vi[1]], m->verts2[vi[2]]));
+    }
     return b;
 }
 static aabb aabb_empty(void) {  /* AABB() : bbMin(MIRO_TMAX), bbMax(-MIRO_TMAX), src/Object.h:13 */
@@ -780,6 +808,7 @@ static int build_tri_bundle(oro_scene* s, const int* objs_all, int bnode_i, int*
         int o = objs_all[b->start + i];
         L->prim[i] = o;
         if (s->obj_inst && s->obj_inst[o] >= 0) { L->inst[i] = s->obj_inst[o]; continue; }
+        if (obj_is_mb(s, o)) continue;   /* checkOut lane: geometry written per ray at its time */
         v3 A = overt(s, o, 0), B = overt(s, o, 1), C = overt(s, o, 2);
         L->t[0 + i] = A.x; L->t[4 + i] = A.y; L->t[8 + i] = A.z;
         L->t[12 + i] = B.x - A.x; L->t[16 + i] = B.y - A.y; L->t[20 + i] = B.z - A.z;
@@ -1020,6 +1049,7 @@ int oro_scene_make_blas(oro_scene* s, const int* meshes, int n_meshes) {
     }
     if (n <= 0) return -1;
     oro_scene* b = (oro_scene*)calloc(1, sizeof(oro_scene));
+    b->is_blas = 1;
     b->meshes = s->meshes; b->n_meshes = s->n_meshes;     /* borrowed for the build only */
     b->n_obj = n;
     b->obj_mesh = (int*)malloc(sizeof(int) * n);
@@ -1087,6 +1117,7 @@ int oro_qbvh_export(const oro_scene* s, float* node_boxes, int32_t* node_child, 
 /* ---------------------------------------------------------------- traversal */
 typedef struct {
     float o[3], d[3], id[3];
+    float time;               /* Ray::time (motion blur), src/Ray.h:71 */
 } ray_t;
 
 /* Ray(threadID, o, d, ...) / Ray::set, src/Ray.h:71-101,135-166 */
@@ -1098,6 +1129,12 @@ static ray_t make_ray(v3 o, v3 d) {
         r.id[k] = 1.0f / r.d[k];
         if (r.d[k] == 0.f) r.id[k] = (r.id[k] < -0.f) ? -1e12f : 1e12f;
     }
+    r.time = 0.f;
+    return r;
+}
+static ray_t make_ray_t(v3 o, v3 d, float time) {
+    ray_t r = make_ray(o, d);
+    r.time = time;
     return r;
 }
 
@@ -1139,7 +1176,7 @@ static int proxy_intersect(const oro_scene* s, int inst, const ray_t* r, float t
     float w = rcp_nr(dp4(I->inv.m[3], o4));
     v3 no = V(w * dp4(I->inv.m[0], o4), w * dp4(I->inv.m[1], o4), w * dp4(I->inv.m[2], o4));
     v3 nd = V(dp4(I->inv.m[0], d4), dp4(I->inv.m[1], d4), dp4(I->inv.m[2], d4));
-    ray_t nr = make_ray(no, nd);
+    ray_t nr = make_ray_t(no, nd, r->time);
     hit_t nh = {h->t, 0, 0, -1, -1};
     int hit = bvh_intersect(s->blas[I->blas], &nr, tMin, &nh, nv, lv);
     if (hit > 0) { h->a = nh.a; h->b = nh.b; h->t = nh.t; h->prim = nh.prim; h->inst = inst; return 1; }
@@ -1183,6 +1220,18 @@ static int intersect4(const oro_scene* s, const qleaf* L, const ray_t* r, float 
         float Ax = L->t[0 + i], Ay = L->t[4 + i], Az = L->t[8 + i];
         float e0x = L->t[12 + i], e0y = L->t[16 + i], e0z = L->t[20 + i];
         float e1x = L->t[24 + i], e1y = L->t[28 + i], e1z = L->t[32 + i];
+        if (obj_is_mb(s, L->prim[i])) {   /* MBObject lane: the triangle at the ray's time, src/BVH.cpp:1316-1334 */
+            const mesh_t* m = omesh(s, L->prim[i]);
+            const uint32_t* vi = m->vidx + 3 * s->obj_tri[L->prim[i]];
+            const float time = r->time, _1_time = 1.f - time;
+            const v3 a2 = m->verts2[vi[0]], a1 = m->verts[vi[0]], b2 = m->verts2[vi[1]], b1 = m->verts[vi[1]];
+            const v3 c2 = m->verts2[vi[2]], c1 = m->verts[vi[2]];
+            Ax = time * a2.x + _1_time * a1.x; Ay = time * a2.y + _1_time * a1.y; Az = time * a2.z + _1_time * a1.z;
+            e0x = (time * b2.x + _1_time * b1.x) - Ax; e0y = (time * b2.y + _1_time * b1.y) - Ay;
+            e0z = (time * b2.z + _1_time * b1.z) - Az;
+            e1x = (time * c2.x + _1_time * c1.x) - Ax; e1y = (time * c2.y + _1_time * c1.y) - Ay;
+            e1z = (time * c2.z + _1_time * c1.z) - Az;
+        }
         float px = r->d[1] * e1z - r->d[2] * e1y;
         float py = -1.0f * (r->d[0] * e1z - r->d[2] * e1x);
         float pz = r->d[0] * e1y - r->d[1] * e1x;
@@ -1296,6 +1345,7 @@ typedef struct {
     uint64_t secondary_rays;        /* reflection / refraction / path-tracing GI rays */
     uint32_t shadow_mask;
     float time;                     /* the camera ray's time (getTimeSample), inherited by every ray of it */
+    float shadow_time;              /* the time sampleLight's shadow rays get: time, or .001 for translucency */
 } shade_ctx;
 
 /* Counter RNG keys: every shade() call (one chain level of one path) draws from
@@ -1308,7 +1358,7 @@ static void begin_level(shade_ctx* c, int level) { c->dim = (uint32_t)(level + 1
 static void begin_camera(shade_ctx* c) { c->skey = c->sample * 1024u; c->dim = 0; }
 
 static int trace_shadow(shade_ctx* c, v3 from, v3 L, float tMax) {
-    ray_t r = make_ray(from, L);
+    ray_t r = make_ray_t(from, L, c->shadow_time);   /* sampleRay.set(.., time, ..): the shading ray's time */
     hit_t h = {tMax, 0, 0, -1, -1};
     uint32_t nv = 0, lv = 0;
     int rc = bvh_intersect(c->s, &r, 0.001f, &h, &nv, &lv);
@@ -1596,7 +1646,7 @@ static v3 path_trace(shade_ctx* c, const oro_material* mat, v3 P, v3 theNormal, 
     if (mat->emitted > 0.0f || (le.x + le.y) + le.z > 0.0f) return vadd(out, vscale(le, mat->emitted));
     if (ch.gi < s->max_bounces - 1) {
         v3 randD = cosine_sample(c, theNormal);
-        ray_t gr = make_ray(P, randD);
+        ray_t gr = make_ray_t(P, randD, c->time);
         hit_t nh;
         if (trace_secondary(c, &gr, &nh)) {
             ior_list child;
@@ -1689,10 +1739,12 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
         }
         if (mat->translucency > 0.01f) {   /* src/Blinn.cpp:224-236 */
             v3 lightTotal = V(0, 0, 0);
+            c->shadow_time = .001f;   /* sampleLight(.., -theNormal, .001f, ..), src/Blinn.cpp:229 */
             for (int i = 0; i < c->s->n_lights; i++) {
                 float lightSpec = 0;
                 lightTotal = vadd(lightTotal, sample_light(c, i, P, vneg(theNormal), rVec, &lightSpec, ch.secondary));
             }
+            c->shadow_time = c->time;
             translucency = vadd(translucency, vmul(vscale(lightTotal, mat->translucency), kd));
         }
     } else {
@@ -1702,7 +1754,7 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
         if (rrFloat < reflectAmt * Rs) {
             if (reflectAmt * Rs > 0.0f && ch.bounces < 5) {
                 ior_list child = *ior;
-                ray_t rr = make_ray(P, rVec);
+                ray_t rr = make_ray_t(P, rVec, c->time);
                 hit_t nh;
                 if (trace_secondary(c, &rr, &nh)) {
                     Lr = vadd(Lr, vmul(ks, shade_child(c, &rr, &nh, &child, cc)));
@@ -1719,7 +1771,7 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
                 ior->v[ior->idx + 1] = outIOR;
                 ior_list child = *ior;
                 child.idx = ior->idx + 1;
-                ray_t tr = make_ray(P, tVec);
+                ray_t tr = make_ray_t(P, tVec, c->time);
                 hit_t nh;
                 if (trace_secondary(c, &tr, &nh)) {
                     Lt = vadd(Lt, vmul(ks, shade_child(c, &tr, &nh, &child, cc)));
@@ -1781,12 +1833,13 @@ static ray_t eye_ray(shade_ctx* c, const cam_basis* b, int x, int y, float minX,
     float urand = next_rand(c), vrand = next_rand(c);
     const float tr = next_rand(c);
     c->time = 1.f - ((tr * tr) * tr) * b->shutter;
+    c->shadow_time = c->time;
     float xOffset = (maxX - minX) * urand + minX;   /* src/Camera.cpp:146-147 */
     float yOffset = (maxY - minY) * vrand + minY;
     float U = b->left + (b->right - b->left) * (((float)x + xOffset) / (float)b->W);
     float Vp = b->bottom + (b->top - b->bottom) * (((float)y + yOffset) / (float)b->H);
     v3 dir = vnormalized(vsub(vadd(vscale(b->u, U), vscale(b->v, Vp)), b->w));
-    if (!(b->aperture >= 0.001f)) return make_ray(b->eye, dir);
+    if (!(b->aperture >= 0.001f)) return make_ray_t(b->eye, dir, c->time);
     v3 focal = vadd(vscale(dir, b->focus), b->eye);
     float lu, lv;
     int k = 0;
@@ -1796,7 +1849,7 @@ static ray_t eye_ray(shade_ctx* c, const cam_basis* b, int x, int y, float minX,
         k++;
     } while (lu * lu + lv * lv > 1.0f && k < 64);
     v3 o = vadd(vscale(vadd(vscale(b->u, lu), vscale(b->v, lv)), b->aperture), b->eye);
-    return make_ray(o, vnormalized(vsub(focal, o)));
+    return make_ray_t(o, vnormalized(vsub(focal, o)), c->time);
 }
 
 /* ---------------------------------------------------------------- image */

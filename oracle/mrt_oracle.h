@@ -150,6 +150,9 @@ int oro_scene_set_material_maps(oro_scene* s, int material, const int maps[6]);
 /* TriangleMesh m_texCoords (ntc x 2 floats) / m_texCoordIndices (nt x 3) of a mesh */
 int oro_mesh_set_texcoords(oro_scene* s, int mesh, int ntc, const float* uv, const uint32_t* tidx);
 int oro_mesh_texcoords(const oro_scene* s, int mesh, int* ntc, float* uv, uint32_t* tidx);
+/* MBObject (src/MBObject.cpp): every triangle of the mesh moves from its vertices
+ * (time 0) to verts2 (time 1, nv x 3 floats) over the camera's time sample */
+int oro_mesh_set_motion(oro_scene* s, int mesh, const float* verts2);
 /* Scene::setEnvMap + setEnvExposure (src/Scene.h:23-24); texture -1 clears. */
 int oro_scene_set_env_map(oro_scene* s, int texture, float exposure);
 /* DomeLight::setTexture tables of light `light` (src/DomeLight.cpp:8-78):

@@ -96,6 +96,7 @@ def _declare(L):
     L.oro_scene_set_material_maps.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.oro_mesh_set_texcoords.argtypes = [C.c_void_p, C.c_int, C.c_int, _fp, _u32p]
     L.oro_mesh_texcoords.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), _fp, _u32p]
+    L.oro_mesh_set_motion.argtypes = [C.c_void_p, C.c_int, _fp]
     L.oro_scene_set_env_map.argtypes = [C.c_void_p, C.c_int, C.c_float]
     L.oro_dome_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.oro_dome_export.argtypes = [C.c_void_p, C.c_int] + [_fp] * 9
@@ -250,6 +251,11 @@ class OracleScene:
         ti = np.ascontiguousarray(tidx, np.uint32).reshape(-1, 3)
         if self.L.oro_mesh_set_texcoords(self.h, mesh, len(uv), _p(uv, _fp), _p(ti, _u32p)) != 0:
             raise RuntimeError("oracle set_texcoords failed")
+
+    def set_motion(self, mesh, verts2):
+        v = np.ascontiguousarray(verts2, np.float32).reshape(-1, 3)
+        if self.L.oro_mesh_set_motion(self.h, mesh, _p(v, _fp)) != 0:
+            raise RuntimeError("oracle set_motion failed")
 
     def texcoords(self, mesh):
         n = C.c_int()

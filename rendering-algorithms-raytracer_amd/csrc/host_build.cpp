@@ -470,6 +470,12 @@ class Builder {
 
     bool is_proxy(int o) const { return oi_ && (*oi_)[o] >= 0; }
     // TriangleMesh::getAABB (src/TriangleMesh.cpp:156-195) / ProxyObject::getAABB
+    // an MBObject lane: a world triangle of a mesh with time-1 vertices
+    bool is_mb(int o) const { return oi_ && !is_proxy(o) && !s_.meshes[om_[o]].verts2.empty(); }
+    static Box box3(v3 A, v3 B, v3 C) {
+        return Box{{std_min(A.x, std_min(B.x, C.x)), std_min(A.y, std_min(B.y, C.y)), std_min(A.z, std_min(B.z, C.z))},
+                   {std_max(A.x, std_max(B.x, C.x)), std_max(A.y, std_max(B.y, C.y)), std_max(A.z, std_max(B.z, C.z))}};
+    }
     Box tri_aabb(int o) const {
         if (is_proxy(o)) {
             const float* b = s_.instances[(*oi_)[o]].box;
@@ -477,9 +483,10 @@ class Builder {
         }
         const Mesh& m = s_.meshes[om_[o]];
         const uint32_t* f = &m.vidx[3 * (size_t)ot_[o]];
-        v3 A = m.verts[f[0]], B = m.verts[f[1]], C = m.verts[f[2]];
-        return Box{{std_min(A.x, std_min(B.x, C.x)), std_min(A.y, std_min(B.y, C.y)), std_min(A.z, std_min(B.z, C.z))},
-                   {std_max(A.x, std_max(B.x, C.x)), std_max(A.y, std_max(B.y, C.y)), std_max(A.z, std_max(B.z, C.z))}};
+        const Box b = box3(m.verts[f[0]], m.verts[f[1]], m.verts[f[2]]);
+        if (!is_mb(o)) return b;
+        // MBObject::getAABB: AABB(m_mesh->getAABB(i), m_mesh_t2->getAABB(i)) (src/MBObject.cpp)
+        return merge(b, box3(m.verts2[f[0]], m.verts2[f[1]], m.verts2[f[2]]));
     }
 
     // qsort(objs, n, sizeof(Object*), Object::sortBy{X,Y,Z}Component): glibc msort is
@@ -724,7 +731,7 @@ class Builder {
         for (int i = 0; i < bn_[b].count; i++) {
             int o = objs_[bn_[b].start + i];
             L.prim[i] = o;
-            if (is_proxy(o)) continue;
+            if (is_proxy(o) || is_mb(o)) continue;   // checkOut lanes: no triangle data
             const Mesh& m = s_.meshes[om_[o]];
             const uint32_t* f = &m.vidx[3 * (size_t)ot_[o]];
             v3 A = m.verts[f[0]], B = m.verts[f[1]], C = m.verts[f[2]];

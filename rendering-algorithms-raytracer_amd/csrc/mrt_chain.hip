@@ -82,6 +82,20 @@ __device__ __forceinline__ size_t shadow_base(const RenderParams& P, int k) {
     return (size_t)k * P.ch_cap * (size_t)P.max_shadow;
 }
 
+// The camera ray's time of path p of the chunk (every ray below the camera ray
+// carries it): the getTimeSample draw of the pixel's eye ray (sample 0, shared
+// by all its paths).
+__device__ __forceinline__ float path_time(const RenderParams& P, uint32_t p) {
+    const uint32_t pl = p / (uint32_t)P.num_paths;
+    int x, y;
+    size_t slot;
+    item_pixel(P, P.item_base + (int)(pl >> 6), (int)(pl & 63u), x, y, slot);
+    const int f = item_frame(P, P.item_base + (int)(pl >> 6));
+    const CamParams& cam = P.cam[f];
+    const float tr = rng((uint32_t)(y * cam.W + x), 0u, 2, P.seed + (uint32_t)f);
+    return 1.f - ((tr * tr) * tr) * cam.shutter;
+}
+
 // Level 0 of every path of a chunk's pixels (tile schedule over the chunk's
 // work items).  Path id = (work item of the chunk * 64 + lane) * num_paths + path.
 // MODE kGen writes each path's shadow rays (level-0 slots p * max_shadow + j,
@@ -123,9 +137,10 @@ __global__ void __launch_bounds__(kWG) chain0_kernel(RenderParams P) {
         const CamParams& cam = P.cam[f];
         const uint32_t seed = P.seed + (uint32_t)f;
         const EyeRay er = camera_ray(cam, seed, x, y, rsqT);
-        const DRay r = make_ray(er.o, er.d);
+        const DRay r = make_ray(er.o, er.d, er.time);
         Shader<POINT_ONLY, false, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 0u, seed, 0, 0u};
         S.iorS = s_ior + tid;
+        S.time = S.shadow_time = er.time;
         typename Shader<POINT_ONLY, false, INST, MODE, REC>::IorCam icam;
         for (int path = 0; path < P.num_paths; path++) {
             const uint32_t p = pbase + (uint32_t)path;
@@ -232,7 +247,8 @@ __global__ void __launch_bounds__(kWG) chain_trace_kernel(RenderParams P) {
             const uint32_t e = (c << 6) + (uint32_t)lane;
             if (e >= nA) continue;
             const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
-            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
+            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z),
+                                    INST && P.has_mb ? path_time(P, __float_as_uint(o.w)) : 0.f);
             DHit h{1e12f, 0.f, 0.f, -1};
             const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
             P.ch_hit[base + e] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
@@ -240,7 +256,7 @@ __global__ void __launch_bounds__(kWG) chain_trace_kernel(RenderParams P) {
             const uint32_t i = ((c - chA) << 6) + (uint32_t)lane, s = i / m;
             if (i >= nB || i - s * m >= (uint32_t)nrays[s]) continue;
             const float4 o = P.ray_o[sb + i], d = P.ray_d[sb + i];
-            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
+            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
             DHit h{o.w, 0.f, 0.f, -1};
             P.occl[sb + i] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
         }
@@ -318,6 +334,7 @@ __global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
                                                         shadow_base(P, k) + (size_t)e * (size_t)P.max_shadow, 0u};
             S.iorS = iorS;
             S.skey = path;
+            if (INST && P.has_mb) S.time = S.shadow_time = path_time(P, p);
             typename Shader<POINT_ONLY, false, INST, MODE, REC>::IorCam icam;   // unused below the camera ray
             LevelOut lo;
             S.template level<false>(r, h, cs, icam, chain_rec(P, k, e), lo);

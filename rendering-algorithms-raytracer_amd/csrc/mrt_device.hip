@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
     };
     auto trace_one = [&](size_t e) {
         const float4 o = P.ray_o[e], d = P.ray_d[e];
-        const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
+        const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
         DHit h{o.w, 0.f, 0.f, -1};
         const uint32_t n0 = st.nodes;
         P.occl[e] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
                         if (c < end && valid(c)) {
                             e = c;
                             const float4 o = P.ray_o[e], d = P.ray_d[e];
-                            r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
+                            r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
                             tmax = o.w;
                             cur = 0;
                             sp = 0;
@@ -328,6 +328,7 @@ __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DL
     Trav T{nodes, fast_box != 0, false, leaves, s_tab, s_stack + tid, gstack + gtid, gstride};
     T.inst = insts;
     T.aprims = alpha.aprims; T.apuv = alpha.apuv; T.auv = alpha.auv; T.amats = alpha.amats; T.atex = alpha.atex;
+    T.pflags = alpha.pflags; T.verts = alpha.verts; T.verts2 = alpha.verts2;   // Ray time 0 (src/Ray.h:71)
     TravStats st;
     for (size_t i = (size_t)blockIdx.x * kWG + tid; i < n; i += (size_t)gridDim.x * kWG) {
         DRay r = make_ray(mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]));
@@ -413,7 +414,10 @@ struct DeviceState {
     float4* tans = nullptr;       // per normal: tangent / bitangent (texture-mapped meshes)
     float4* btans = nullptr;
     bool has_maps = false, has_alpha = false;
-    bool special = false;         // instances or alpha maps: leaf packets with special lanes (INST kernels)
+    uint8_t* pflags = nullptr;    // motion blur: per world prim bit 0 = MBObject lane
+    float4* verts2 = nullptr;     //   time-1 vertices parallel to verts (copies of verts for static meshes)
+    bool has_mb = false;
+    bool special = false;         // instances, alpha maps or motion blur: leaf packets with special lanes (INST kernels)
     std::vector<void*> bufs;     // textures and dome tables (freed with the state)
     const float* env = nullptr;  // environment texture (one of bufs)
     uint16_t* tables = nullptr;
@@ -476,7 +480,8 @@ static void free_device(DeviceState* d) {
     for (StreamCtx* c : d->ctxs) free_ctx(c);
     for (hipStream_t st : d->share_streams) (void)hipStreamDestroy(st);
     void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts, d->tables,
-                    d->gamma, d->gammaF, d->d_rgb, d->d_rgb8, d->texs, d->puv, d->uvs, d->tans, d->btans};
+                    d->gamma, d->gammaF, d->d_rgb, d->d_rgb8, d->texs, d->puv, d->uvs, d->tans, d->btans,
+                    d->pflags, d->verts2};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (void* p : d->bufs)
@@ -617,6 +622,15 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
         return p >= 0 && (size_t)p < s.obj_mesh.size() && s.obj_mesh[p] >= 0 &&
                alpha_mat[(size_t)s.meshes[s.obj_mesh[p]].material];
     };
+    // MBObject world triangles (meshes with time-1 vertices)
+    auto mb_obj = [&](int32_t p) {
+        return p >= 0 && (size_t)p < s.obj_mesh.size() && s.obj_mesh[p] >= 0 &&
+               (s.obj_inst.empty() || s.obj_inst[(size_t)p] < 0) && !s.meshes[s.obj_mesh[p]].verts2.empty();
+    };
+    std::vector<uint8_t> PF(s.obj_mesh.size(), 0);
+    d.has_mb = false;
+    for (size_t i = 0; i < PF.size(); i++)
+        if (mb_obj((int32_t)i)) { PF[i] = 1; d.has_mb = true; }
     d.has_alpha = false;
     std::vector<uint16_t> tab(4096);
     memcpy(tab.data(), host_rcp_table(), 4096);
@@ -647,7 +661,8 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
                     if (L.prim[j] >= 0) {  // zero-filled lanes below cnt are rejected by det = 0
                         cnt = j + 1;
                         proxy |= proxy_of(L.prim[j]) >= 0;
-                        alpha |= oi != nullptr && proxy_of(L.prim[j]) < 0 && alpha_obj(L.prim[j]);   // world leaves only
+                        alpha |= oi != nullptr && proxy_of(L.prim[j]) < 0 &&
+                                 (alpha_obj(L.prim[j]) || mb_obj(L.prim[j]));   // world leaves only
                     }
                 d.has_alpha |= alpha;
                 q.child[k] = leaf_child((uint32_t)(~c + lb), cnt < 1 ? 1 : cnt, proxy, alpha);
@@ -728,7 +743,17 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
         if ((rc = upload(d.tans, TN.data(), TN.size() * sizeof(float4), total))) return rc;
         if ((rc = upload(d.btans, BTN.data(), BTN.size() * sizeof(float4), total))) return rc;
     }
-    d.special = d.n_insts > 0 || d.has_alpha;
+    if (d.has_mb) {
+        std::vector<float4> V2 = V;
+        for (size_t m = 0; m < s.meshes.size(); m++)
+            for (size_t i = 0; i < s.meshes[m].verts2.size(); i++) {
+                const v3& p = s.meshes[m].verts2[i];
+                V2[vbase[m] + i] = make_float4(p.x, p.y, p.z, 1.f);
+            }
+        if ((rc = upload(d.verts2, V2.data(), V2.size() * sizeof(float4), total))) return rc;
+        if ((rc = upload(d.pflags, PF.data(), PF.size(), total))) return rc;
+    }
+    d.special = d.n_insts > 0 || d.has_alpha || d.has_mb;
     d.bytes = total;
     // persistent grid: resident workgroups on every CU
     hipDeviceProp_t prop;
@@ -792,6 +817,9 @@ static void fill_params(const Scene& s, RenderParams& P) {
     P.tans = d.tans;
     P.btans = d.btans;
     P.has_maps = d.has_maps ? 1 : 0;
+    P.pflags = d.pflags;
+    P.verts2 = d.verts2;
+    P.has_mb = d.has_mb ? 1 : 0;
     P.n_insts = d.n_insts;
     P.n_world = d.n_world;
     P.env = d.env;
@@ -1463,6 +1491,16 @@ int mrt_scene_mesh_set_texcoords(mrt_scene* s, int mesh, const float* uv, int32_
     return MRT_OK;
 }
 
+int mrt_scene_set_mesh_motion(mrt_scene* s, int mesh, const float* verts2) {
+    if (!s || mesh < 0 || mesh >= (int)s->impl.meshes.size() || !verts2) { set_error("bad mesh id"); return MRT_ERR_INVALID; }
+    Mesh& m = s->impl.meshes[mesh];
+    m.verts2.resize(m.verts.size());
+    for (size_t i = 0; i < m.verts.size(); i++) m.verts2[i] = v3{verts2[3*i], verts2[3*i+1], verts2[3*i+2]};
+    s->impl.built = false;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
 int mrt_scene_mesh_texcoords(const mrt_scene* s, int mesh, int32_t* n_texcoords, float* uv, uint32_t* tidx) {
     if (!s || mesh < 0 || mesh >= (int)s->impl.meshes.size() || !n_texcoords) { set_error("bad mesh id"); return MRT_ERR_INVALID; }
     const Mesh& m = s->impl.meshes[mesh];
@@ -1983,6 +2021,7 @@ int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const floa
                         : (d.special ? trace_kernel<false, true> : trace_kernel<false, false>);
     Trav alpha{};
     alpha.aprims = d.prims; alpha.apuv = d.puv; alpha.auv = d.uvs; alpha.amats = d.mats; alpha.atex = d.texs;
+    alpha.pflags = d.pflags; alpha.verts = d.verts; alpha.verts2 = d.verts2;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kWG), 0, (hipStream_t)stream, d.nodes, d.leaves, d.tables, c.gstack,
                        d.gthreads, d_o, d_d, d_tmin, d_tmax, n, d_out, c.ctr, fast_box(d), d.insts, alpha);
     HIP_OK(hipGetLastError());

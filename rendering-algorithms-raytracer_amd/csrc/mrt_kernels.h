@@ -27,6 +27,7 @@ static constexpr int kTableWords = 4096; // rcp[2048] + rsqrt[2048] (u16)
 struct DRay {
     float o[3], d[3], id[3];
     bool finite;  // o and id finite: no box-test value can be NaN (see box_test_fast)
+    float time;   // Ray::time (src/Ray.h): where an MBObject lane's triangle is (motion blur)
 };
 
 // Ray(threadID, o, d, ...), src/Ray.h:71-101: id = 1/d, +-1e12 for d == 0.
@@ -42,6 +43,12 @@ __device__ __forceinline__ DRay make_ray(v3 o, v3 d) {
     }
     r.finite = __builtin_isfinite(r.o[0]) & __builtin_isfinite(r.o[1]) & __builtin_isfinite(r.o[2]) &
                __builtin_isfinite(r.id[0]) & __builtin_isfinite(r.id[1]) & __builtin_isfinite(r.id[2]);
+    r.time = 0.f;
+    return r;
+}
+__device__ __forceinline__ DRay make_ray(v3 o, v3 d, float time) {
+    DRay r = make_ray(o, d);
+    r.time = time;
     return r;
 }
 
@@ -68,6 +75,11 @@ struct Trav {
     const float2* auv = nullptr;
     const DevMaterial* amats = nullptr;
     const DevTexture* atex = nullptr;
+    // motion-blurred triangles (MBObject, src/MBObject.cpp): per world prim bit 0
+    // = MBObject lane; vertices at time 0 / time 1 (PrimShade vertex indices)
+    const uint8_t* pflags = nullptr;
+    const float4* verts = nullptr;
+    const float4* verts2 = nullptr;
 };
 
 struct TravStats {
@@ -162,11 +174,30 @@ __device__ __forceinline__ int box_test_fast(const float4* bx, const DRay& r, fl
 }
 
 // Device child word of a QNode slot: >= 0 inner node; kEmptySlot; otherwise
-// ~(leaf << 4 | alpha << 3 | proxy << 2 | (count - 1)) with count = objects in
-// the packet, proxy = the packet has ProxyObject (checkOut) lanes and alpha = it
-// has alpha-mapped triangles (the host re-encodes the canonical ~leaf on upload).
-__host__ __device__ __forceinline__ int32_t leaf_child(uint32_t leaf, int count, bool proxy = false, bool alpha = false) {
-    return ~(int32_t)((leaf << 4) | (alpha ? 8u : 0u) | (proxy ? 4u : 0u) | (uint32_t)(count - 1));
+// ~(leaf << 4 | check << 3 | proxy << 2 | (count - 1)) with count = objects in
+// the packet, proxy = the packet has ProxyObject (checkOut) lanes and check = it
+// has alpha-mapped or motion-blurred triangles (the host re-encodes the
+// canonical ~leaf on upload).
+__host__ __device__ __forceinline__ int32_t leaf_child(uint32_t leaf, int count, bool proxy = false, bool check = false) {
+    return ~(int32_t)((leaf << 4) | (check ? 8u : 0u) | (proxy ? 4u : 0u) | (uint32_t)(count - 1));
+}
+
+// An MBObject lane of intersect4 (src/BVH.cpp:1316-1334): the triangle at the
+// ray's time, A = time * A2 + (1 - time) * A1 and the edges from the
+// interpolated B and C, then the lane's usual test.
+__device__ __noinline__ bool mb_tri_test(const Trav& c, int32_t prim, const DRay& r, float tMin, float tBest, float& ot,
+                                         float& oa, float& ob) {
+    const PrimShade& ps = c.aprims[prim];
+    const float time = r.time, _1_time = 1.f - time;
+    const float4 a1 = c.verts[ps.v[0]], b1 = c.verts[ps.v[1]], c1 = c.verts[ps.v[2]];
+    const float4 a2 = c.verts2[ps.v[0]], b2 = c.verts2[ps.v[1]], c2 = c.verts2[ps.v[2]];
+    float T[9];
+    T[0] = time * a2.x + _1_time * a1.x; T[1] = time * a2.y + _1_time * a1.y; T[2] = time * a2.z + _1_time * a1.z;
+    T[3] = (time * b2.x + _1_time * b1.x) - T[0]; T[4] = (time * b2.y + _1_time * b1.y) - T[1];
+    T[5] = (time * b2.z + _1_time * b1.z) - T[2];
+    T[6] = (time * c2.x + _1_time * c1.x) - T[0]; T[7] = (time * c2.y + _1_time * c1.y) - T[1];
+    T[8] = (time * c2.z + _1_time * c1.z) - T[2];
+    return tri_test(T, r, tMin, tBest, ot, oa, ob, c.rcpT);
 }
 
 // intersect4's alpha test (src/BVH.cpp:1401-1423) for lane k of leaf packet
@@ -207,7 +238,7 @@ __device__ __forceinline__ DRay object_ray(const DevInstance& I, const DRay& r, 
     const v3 o = mk(w * dp4(I.inv, ox, oy, oz, 1.0f), w * dp4(I.inv + 4, ox, oy, oz, 1.0f),
                     w * dp4(I.inv + 8, ox, oy, oz, 1.0f));
     const v3 d = mk(dp4(I.inv, dx, dy, dz, 0.0f), dp4(I.inv + 4, dx, dy, dz, 0.0f), dp4(I.inv + 8, dx, dy, dz, 0.0f));
-    return make_ray(o, d);
+    return make_ray(o, d, r.time);
 }
 
 template <bool ANY, bool COUNT, bool FAST, bool INST = false>
@@ -307,7 +338,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         if (lm) {
             uint32_t leaf = 0;
             int k = 0, cnt = 0;
-            bool alpha = false;
+            bool check = false;
             while (true) {
                 if (k == cnt) {
                     if (!lm) break;
@@ -317,7 +348,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                     leaf = v >> 4;
                     cnt = (int)(v & 3u) + 1;
                     k = 0;
-                    alpha = INST && (v & 8u);
+                    check = INST && (v & 8u);
                     if (COUNT) st.leaves++;
                     if (INST && (v & 4u)) {
                         for (int j = 0; j < cnt; j++) {
@@ -335,8 +366,16 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                     }
                 }
                 float t, a, b;
-                if (tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT) &&
-                    !(INST && alpha && alpha_rejects(c, leaf, k, a, b))) {
+                bool ok;
+                if (INST && check) {   // alpha-mapped / motion-blurred lanes
+                    const int32_t pm = c.leaves[leaf].prim[k];
+                    ok = (pm >= 0 && (c.pflags[pm] & 1u)) ? mb_tri_test(c, pm, r, tMin, h.t, t, a, b)
+                                                          : tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT);
+                    ok = ok && !alpha_rejects(c, leaf, k, a, b);
+                } else {
+                    ok = tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT);
+                }
+                if (ok) {
                     if (ANY) return true;
                     h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
                     if (INST) h.inst = -1;

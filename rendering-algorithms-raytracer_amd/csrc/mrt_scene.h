@@ -26,6 +26,8 @@ struct Mesh {
     std::vector<float> uv;
     std::vector<uint32_t> tidx;
     std::vector<v3> tan, btan;
+    // MBObject m_mesh_t2 vertices (motion blur, src/MBObject.cpp): empty = static
+    std::vector<v3> verts2;
     int32_t nt() const { return (int32_t)(vidx.size() / 3); }
 };
 

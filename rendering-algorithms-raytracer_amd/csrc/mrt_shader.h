@@ -115,6 +115,11 @@ struct RenderParams {
     int32_t ch_levels;           // levels allocated
     int32_t item_base;           // chain launches: first work item of the chunk
     const uint32_t* sh_count;    // shadow_kernel: pixel / entry count on the device (nullable)
+    // motion blur (MBObject, src/MBObject.cpp): per world prim bit 0 = MBObject
+    // lane; time-1 vertices parallel to verts (nullptr: no motion blur)
+    const uint8_t* pflags;
+    const float4* verts2;
+    int32_t has_mb;
 };
 
 // pow(spec, specExp) of Blinn::shade (src/Blinn.cpp:219-220; libm powf in the
@@ -148,6 +153,9 @@ __device__ __forceinline__ void trav_alpha(Trav& T, const RenderParams& P) {
     T.auv = P.uvs;
     T.amats = P.mats;
     T.atex = P.texs;
+    T.pflags = P.pflags;
+    T.verts = P.verts;
+    T.verts2 = P.verts2;
 }
 
 // Chain state of one path at its current level (Shader::level).
@@ -217,6 +225,8 @@ struct Shader {
     uint32_t skey = 0, dim = 0;  // RNG sub-stream / draw key
     float* iorS = nullptr;   // REC: LDS IOR column (stride kWG)
     float* lvl = nullptr;    // REC: this thread's level records (stride P.gstride)
+    float time = 0.f;        // the camera ray's time (getTimeSample), inherited by the rays below it
+    float shadow_time = 0.f; // sampleLight's shadow-ray time: time, or .001 for translucency (src/Blinn.cpp:229)
 
     __device__ float next_rand() { return rng(pixel, skey, dim++, seed); }
 
@@ -226,12 +236,12 @@ struct Shader {
         if constexpr (MODE == kGen) {  // no shading result depends on the answer but the final sums
             const size_t s = slot0 + nslot++;
             P.ray_o[s] = make_float4(from.x, from.y, from.z, tMax);
-            P.ray_d[s] = make_float4(L.x, L.y, L.z, 0.f);
+            P.ray_d[s] = make_float4(L.x, L.y, L.z, shadow_time);
             return false;
         } else if constexpr (MODE == kResolve) {
             return P.occl[slot0 + nslot++] != 0;
         } else {
-            DRay r = make_ray(from, L);
+            DRay r = make_ray(from, L, shadow_time);
             DHit h{tMax, 0.f, 0.f, -1};
             return traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st);
         }
@@ -652,10 +662,12 @@ struct Shader {
             v3 tr = z;
             if (M.translucency > 0.01f) {   // lights seen through the surface (src/Blinn.cpp:224-236)
                 v3 total = z;
+                shadow_time = .001f;
                 for (int i = 0; i < P.n_lights; i++) {
                     float spec = 0.f;
                     total = add(total, sample_light<COUNT>(i, Pt, neg(n), rVec, spec, cs.secondary));
                 }
+                shadow_time = time;
                 tr = add(z, mul(scale(total, M.translucency), kd));
             }
             if (child) {   // descend into the GI ray: IOR history [1, current]
@@ -668,7 +680,7 @@ struct Shader {
                 cs.depth++; cs.gi++;
                 cs.secondary = true;
                 o.spawn = true;
-                o.r2 = make_ray(Pt, randD);
+                o.r2 = make_ray(Pt, randD, time);
                 o.dir = randD;
                 o.env_miss = M.sample_env && P.sample_env;
                 secondary++;
@@ -713,7 +725,7 @@ struct Shader {
             cs.depth++; cs.bounces++;
             cs.secondary = false;   // shade(..) with the default isSecondary
             o.spawn = true;
-            o.r2 = make_ray(Pt, dir);
+            o.r2 = make_ray(Pt, dir, time);
             o.dir = dir;
             o.env_miss = true;
             secondary++;
@@ -928,6 +940,7 @@ __device__ __forceinline__ void flush_secondary(const RenderParams& P, uint32_t 
 // kernels recompute the camera ray instead of storing it.
 struct EyeRay {
     v3 o, d;
+    float time;
 };
 __device__ __forceinline__ EyeRay eye_ray(const CamParams& cam, uint32_t seed, int x, int y, uint32_t skey, float x0,
                                           float x1, float y0, float y1, const uint16_t* rsqT) {
@@ -939,7 +952,9 @@ __device__ __forceinline__ EyeRay eye_ray(const CamParams& cam, uint32_t seed, i
     const v3 U = mk(cam.u[0], cam.u[1], cam.u[2]), Vv = mk(cam.v[0], cam.v[1], cam.v[2]), W = mk(cam.w[0], cam.w[1], cam.w[2]);
     const v3 eye = mk(cam.eye[0], cam.eye[1], cam.eye[2]);
     const v3 d = normalized(sub(add(scale(U, Up), scale(Vv, Vp)), W), rsqT);
-    if (!(cam.aperture >= 0.001f)) return EyeRay{eye, d};   // m_aperture < epsilon: pinhole
+    const float tr = rng(pixel, skey, 2, seed);
+    const float time = 1.f - ((tr * tr) * tr) * cam.shutter;   // getTimeSample, src/Camera.h:46
+    if (!(cam.aperture >= 0.001f)) return EyeRay{eye, d, time};   // m_aperture < epsilon: pinhole
     const v3 focal = add(scale(d, cam.focus), eye);
     float lu, lv;
     uint32_t k = 3;
@@ -949,7 +964,7 @@ __device__ __forceinline__ EyeRay eye_ray(const CamParams& cam, uint32_t seed, i
         k += 2;
     } while (lu * lu + lv * lv > 1.0f && k < 3 + 2 * 64);
     const v3 o = add(scale(add(scale(U, lu), scale(Vv, lv)), cam.aperture), eye);
-    return EyeRay{o, normalized(sub(focal, o), rsqT)};
+    return EyeRay{o, normalized(sub(focal, o), rsqT), time};
 }
 // the 1-spp camera ray (eyeRayAdaptive(x, y, .5, .5, .5, .5), sample 0)
 __device__ __forceinline__ EyeRay camera_ray(const CamParams& cam, uint32_t seed, int x, int y, const uint16_t* rsqT) {
@@ -990,7 +1005,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
             const int f = item_frame(P, item);
             const CamParams& cam = P.cam[f];
             const EyeRay er = camera_ray(cam, P.seed + (uint32_t)f, x, y, rsqT);
-            DRay r = make_ray(er.o, er.d);
+            DRay r = make_ray(er.o, er.d, er.time);
             DHit h{1e12f, 0.f, 0.f, -1};
             if (!traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st)) h.prim = -1;
             item_pixel(P, item, lane, x, y, slot);  // recompute: keeps it out of the traversal's live set
@@ -1047,9 +1062,10 @@ __global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
             const CamParams& cam = P.cam[f];
             const uint32_t seed = P.seed + (uint32_t)f;
             const EyeRay er = camera_ray(cam, seed, x, y, rsqT);
-            DRay r = make_ray(er.o, er.d);
+            DRay r = make_ray(er.o, er.d, er.time);
             Shader<POINT_ONLY, FAST, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 0u, seed,
                                                    slot * (size_t)P.max_shadow, 0u};
+            S.time = S.shadow_time = er.time;
             if constexpr (REC) { S.iorS = s_ior + tid; S.lvl = P.lvl + (blockIdx.x * kWG + tid); }
             col = S.template shade<COUNT>(r, h);
             shadow_total += S.shadow_rays;
@@ -1137,7 +1153,7 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
             }
             const EyeRay er = eye_ray(cam, seed, x, y, sample * 1024u, x0, x1, y0, y1, rsqT);
             const v3 d = er.d;
-            const DRay r = make_ray(er.o, d);
+            const DRay r = make_ray(er.o, d, er.time);
             DHit h{1e12f, 0.f, 0.f, -1};
             v3 col;
             eye_rays++;
@@ -1147,6 +1163,7 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
                 eye_hits++;
                 Shader<POINT_ONLY, FAST, INST, kFused, REC> S{P, T, rcpT, rsqT, st, pixel, 0u, seed, 0, 0u};
                 S.sample = sample;
+                S.time = S.shadow_time = er.time;
                 if constexpr (REC) { S.iorS = s_ior + tid; S.lvl = P.lvl + (blockIdx.x * kWG + tid); }
                 col = S.template shade<COUNT>(r, h);
                 shadow_total += S.shadow_rays;

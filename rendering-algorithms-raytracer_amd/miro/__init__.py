@@ -369,6 +369,39 @@ def makeMeshObjs(scene: "Scene", mesh: TriangleMesh, material):
     scene.addMesh(mesh, material)
 
 
+def _mesh_vertices(mesh: TriangleMesh) -> np.ndarray:
+    """The vertices of a TriangleMesh: its arrays, or its OBJ parsed by libmrt's
+    loader (through a scratch scene)."""
+    if mesh.path is None:
+        return mesh.verts
+    L = lib()
+    h = L.mrt_scene_create()
+    try:
+        ctm = mesh.ctm.ctypes.data_as(C.POINTER(C.c_float)) if mesh.ctm is not None else None
+        mid = check(L.mrt_scene_add_material(h, C.byref(Lambert()._c())), "add_material")
+        mesh_id = check(L.mrt_scene_add_obj(h, mesh.path.encode(), ctm, mid), f"load {mesh.path}")
+        nv, nn, nt = C.c_int32(), C.c_int32(), C.c_int32()
+        check(L.mrt_scene_mesh_info(h, mesh_id, C.byref(nv), C.byref(nn), C.byref(nt)), "mesh_info")
+        v = np.zeros((nv.value, 3), np.float32)
+        n = np.zeros((nn.value, 3), np.float32)
+        vi = np.zeros((nt.value, 3), np.uint32)
+        ni = np.zeros((nt.value, 3), np.uint32)
+        check(L.mrt_scene_mesh_export(h, mesh_id, v.ctypes.data_as(C.POINTER(C.c_float)),
+                                      n.ctypes.data_as(C.POINTER(C.c_float)), vi.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                      ni.ctypes.data_as(C.POINTER(C.c_uint32))), "mesh_export")
+        return v
+    finally:
+        L.mrt_scene_destroy(h)
+
+
+def makeMBMeshObjs(scene: "Scene", mesh: TriangleMesh, mesh2: TriangleMesh, material):
+    """makeMBMeshObjs (src/main.cpp:23, :202): one MBObject(material, mesh, mesh2, i)
+    per triangle (src/MBObject.cpp:7-11) -- mesh at time 0, mesh2 (same topology)
+    at time 1; a ray of time t meets the blend t * mesh2 + (1 - t) * mesh."""
+    scene.addMesh(mesh, material)
+    scene._motion[id(mesh)] = mesh2
+
+
 class Objects(list):
     """Objects (std::vector<Object*>) of a proxy: (mesh, material) pairs here."""
 
@@ -408,6 +441,7 @@ class Scene:
 
     def __init__(self, device: int = 0):
         self._meshes: List[tuple] = []
+        self._motion: dict = {}          # id(time-0 mesh) -> time-1 mesh (makeMBMeshObjs)
         self._lights: List[_Light] = []
         self.bg = Vector3(0)
         self.m_numPaths = 1
@@ -493,13 +527,25 @@ class Scene:
                       "texcoords")
             return mesh_id
 
+        def set_motion(mesh_id, mesh2):
+            v2 = np.ascontiguousarray(_mesh_vertices(mesh2), np.float32).reshape(-1, 3)
+            nv = C.c_int32()
+            check(L.mrt_scene_mesh_info(self._h, mesh_id, C.byref(nv), C.byref(C.c_int32()), C.byref(C.c_int32())),
+                  "mesh_info")
+            if len(v2) != nv.value:
+                raise MRTError(f"motion mesh has {len(v2)} vertices, the time-0 mesh {nv.value}")
+            check(L.mrt_scene_set_mesh_motion(self._h, mesh_id, v2.ctypes.data_as(C.POINTER(C.c_float))), "mesh motion")
+
         blas = {}   # BVH object -> BLAS id (built once, shared by its instances)
         self.blas_build_ms = 0.0
         self.blas_prims = 0
         self.blas_ids = blas
+        motion = self._motion
         for item, mat in self._meshes:
             if not isinstance(item, ProxyObject):
-                add_mesh(item, mat)
+                mesh_id = add_mesh(item, mat)
+                if id(item) in motion:
+                    set_motion(mesh_id, motion[id(item)])
                 continue
             key = id(item.bvh)
             if key not in blas:

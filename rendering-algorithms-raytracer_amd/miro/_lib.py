@@ -26,7 +26,7 @@ EXPORTS = [
     "mrt_scene_add_instance", "mrt_scene_blas_info", "mrt_scene_blas_export", "mrt_scene_set_material_emission",
     "mrt_scene_set_material_sample_env", "mrt_scene_set_path_trace", "mrt_scene_prim_object",
     "mrt_image_info", "mrt_image_load", "mrt_scene_add_texture_typed", "mrt_scene_set_material_maps",
-    "mrt_scene_mesh_set_texcoords", "mrt_scene_mesh_texcoords",
+    "mrt_scene_mesh_set_texcoords", "mrt_scene_mesh_texcoords", "mrt_scene_set_mesh_motion",
 ]
 
 
@@ -157,6 +157,7 @@ def load():
     L.mrt_scene_add_texture_typed.argtypes = [C.c_void_p, _fp, C.c_int32, C.c_int32, C.c_int32]
     L.mrt_scene_set_material_maps.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int32)]
     L.mrt_scene_mesh_set_texcoords.argtypes = [C.c_void_p, C.c_int, _fp, C.c_int32, C.POINTER(C.c_uint32)]
+    L.mrt_scene_set_mesh_motion.argtypes = [C.c_void_p, C.c_int, _fp]
     L.mrt_scene_mesh_texcoords.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int32), _fp, C.POINTER(C.c_uint32)]
     L.mrt_scene_set_env_map.argtypes = [C.c_void_p, C.c_int32, C.c_float]
     L.mrt_scene_dome_info.argtypes = [C.c_void_p, C.c_int32, _ip, _ip]

@@ -57,9 +57,11 @@ def materials_pair(P, O_, mat):
 
 
 def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1, instances=None, subdivs=None,
-               extra=None, path_trace=None):
+               extra=None, path_trace=None, moving=None):
     """Build (miro.Scene, OracleScene, camera dict) for a config dict.
     extra: [(mesh arrays, material dict), ...] added after the main geometry;
+    moving: [(mesh arrays, time-1 vertices, material dict), ...] MBObject meshes
+    (makeMBMeshObjs) added after those;
     path_trace: (max_bounces, sample_env) turns Scene::m_pathTrace on."""
     lights = cfg["lights"] if lights is None else lights
     mat = cfg["material"]
@@ -104,6 +106,14 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
                 O_.set_texcoords(mid, arrs[4], arrs[5])
         miro.makeMeshObjs(P, tm, xm)
         material_maps(xm, O_, oxm, emat)
+    for arrs, v2, emat in (moving or []):
+        xm, oxm = materials_pair(P, O_, emat)
+        tm, tm2 = miro.TriangleMesh(), miro.TriangleMesh()
+        tm.setArrays(*arrs[:4])
+        tm2.setArrays(v2, *arrs[1:4])
+        mid = O_.add_mesh(*arrs[:4], oxm)
+        O_.set_motion(mid, v2)
+        miro.makeMBMeshObjs(P, tm, tm2, xm)
     if floor:
         fl = miro.TriangleMesh()
         fl.createSingleTriangle()
