@@ -76,7 +76,8 @@ struct Trav {
     const DevMaterial* amats = nullptr;
     const DevTexture* atex = nullptr;
     // motion-blurred triangles (MBObject, src/MBObject.cpp): per world prim bit 0
-    // = MBObject lane; vertices at time 0 / time 1 (PrimShade vertex indices)
+    // = MBObject lane (nullptr: no motion blur); vertices at time 0 / time 1
+    // (PrimShade vertex indices)
     const uint8_t* pflags = nullptr;
     const float4* verts = nullptr;
     const float4* verts2 = nullptr;
@@ -369,7 +370,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                 bool ok;
                 if (INST && check) {   // alpha-mapped / motion-blurred lanes
                     const int32_t pm = c.leaves[leaf].prim[k];
-                    ok = (pm >= 0 && (c.pflags[pm] & 1u)) ? mb_tri_test(c, pm, r, tMin, h.t, t, a, b)
+                    ok = (pm >= 0 && c.pflags && (c.pflags[pm] & 1u)) ? mb_tri_test(c, pm, r, tMin, h.t, t, a, b)
                                                           : tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT);
                     ok = ok && !alpha_rejects(c, leaf, k, a, b);
                 } else {

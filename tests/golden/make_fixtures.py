@@ -55,7 +55,20 @@ def oracle_scene(cfg, mesh_arrays=None, obj=None, floor=False):
     return s
 
 
+def motion_fixture():
+    """cannonBallT1/T2 (the reference's makeMBMeshObjs pair, src/main.cpp:216-221)
+    and its groundPlane: time-0 arrays, time-1 vertices (same topology)."""
+    v1, n1, vi1, ni1 = load_mesh("Final/cannonBallT1.obj")
+    v2, _, vi2, _ = load_mesh("Final/cannonBallT2.obj")
+    assert v1.shape == v2.shape and np.array_equal(vi1, vi2), "MBObject meshes need one topology"
+    gv, gn, gvi, gni = load_mesh("Final/groundPlane.obj")
+    np.savez_compressed(os.path.join(HERE, "cannonball_mb.npz"), verts=v1, normals=n1, vidx=vi1, nidx=ni1,
+                        verts2=v2, ground_verts=gv, ground_normals=gn, ground_vidx=gvi, ground_nidx=gni)
+
+
 def main():
+    if sys.argv[1:] == ["motion"]:
+        return motion_fixture()
     meta = {}
     for name, rel in MESHES.items():
         v, n, vi, ni = load_mesh(rel)

@@ -17,11 +17,13 @@ a long shutter the hits spread over the swept region and stay inside it.  GPU
 tests compare the HIP path with the oracle bit for bit (direct lighting, the
 wavefront shadow pass, the chain engine with mirrors and path tracing,
 translucency, adaptive supersampling, depth of field)."""
+import os
+
 import numpy as np
 import pytest
 
 import miro
-from helpers import bits, camera, fixture_mesh, scene_pair
+from helpers import ROOT, bits, camera, fixture_mesh, scene_pair
 from miro import scenes
 
 CAM = dict(eye=(2.75, 2.75, 5.0), lookAt=(2.75, 2.75, 0.0), up=(0, 1, 0), fov=55.0)
@@ -204,3 +206,49 @@ def test_motion_blur_supersampling_and_depth_of_field_match_oracle():
     gpu_vs_oracle(P, O_, MB, 40, 32)
     P, O_, _ = cornell(moving=[(ball, moved(ball), BALL)])
     gpu_vs_oracle(P, O_, dict(MB, aperture=0.3, focusPlane=7.0), 64, 48)
+
+
+# ------------------------------------------- the reference's own MBObject pair
+def cannonball_parts():
+    """cannonBallT1 -> cannonBallT2 over the groundPlane (src/main.cpp:216-225),
+    lit by a point light; fixture tests/golden/cannonball_mb.npz
+    (tests/golden/make_fixtures.py motion)."""
+    f = np.load(os.path.join(ROOT, "tests", "golden", "cannonball_mb.npz"))
+    ball = (f["verts"], f["normals"], f["vidx"], f["nidx"])
+    ground = (f["ground_verts"], f["ground_normals"], f["ground_vidx"], f["ground_nidx"])
+    cfg = dict(scenes.CONFIGS["C1"], material=dict(kind="lambert", kd=(0.5, 0.45, 0.4)),
+               lights=[dict(type="point", pos=(2.0, 3.0, 2.0), power=60.0)])
+    return cfg, ground, ball, f["verts2"]
+
+
+def cannonball(mat=None, **kw):
+    cfg, ground, ball, v2 = cannonball_parts()
+    return scene_pair(cfg, meshes=[ground], moving=[(ball, v2, mat or BALL)], **kw)
+
+
+BALL_CAM = dict(eye=(0.75, 0.62, 0.38), lookAt=(0.0, 0.5, 0.38), up=(0, 1, 0), fov=60.0)
+N_GROUND = 32   # the ground plane's triangles come first
+
+
+def test_cannonball_shutter_zero_is_the_time_one_mesh():
+    cfg, ground, ball, v2 = cannonball_parts()
+    _, Om, _ = cannonball()
+    _, Os, _ = scene_pair(cfg, meshes=[ground], extra=[((v2,) + ball[1:], BALL)])
+    cam = dict(BALL_CAM, shutterSpeed=0.0)
+    a, b = Om.render(cam, 96, 72, threads=8), Os.render(cam, 96, 72, threads=8)
+    on = (a["hits"]["prim"] >= N_GROUND) | (b["hits"]["prim"] >= N_GROUND)
+    assert on.sum() > 200
+    assert np.array_equal(a["hits"]["prim"][on], b["hits"]["prim"][on])
+    assert np.array_equal(bits(a["hits"]["t"][on]), bits(b["hits"]["t"][on]))
+
+
+@pytest.mark.gpu
+def test_cannonball_motion_blur_matches_oracle():
+    need_gpu()
+    P, O_, _ = cannonball()
+    ref = gpu_vs_oracle(P, O_, dict(BALL_CAM, shutterSpeed=1.0), 96, 72)
+    assert (ref["hits"]["prim"] >= N_GROUND).sum() > 200
+    shiny = dict(kind="blinn", kd=(0.01, 0.01, 0.01), reflectAmt=0.5, ior=1.8)   # cBallMat without specAmt
+    P, O_, _ = cannonball(shiny, num_paths=2)
+    ref = gpu_vs_oracle(P, O_, dict(BALL_CAM, shutterSpeed=0.6), 96, 72)
+    assert ref["secondary_rays"] > 0
