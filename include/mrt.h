@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 5
+#define MRT_ABI_VERSION 6
 
 enum {
     MRT_OK = 0,
@@ -198,6 +198,13 @@ int mrt_scene_set_num_paths(mrt_scene* s, int num_paths);
  * Fresnel-weighted Russian roulette, at most 5 bounces, IOR history per ray.
  * No effect on Lambert materials. */
 int mrt_scene_set_material_optics(mrt_scene* s, int material, float reflect_amt, float refract_amt, float ior);
+/* Material::m_disperse + Blinn::setIor(ior, i) for i = 0..2 (src/Material.h:45,
+ * src/Blinn.h:38,59; ABI 6).  `ior` replaces all three m_ior; ior[1] is also the
+ * optics IOR above (the non-dispersive refraction reads m_ior[1], src/Blinn.cpp:183).
+ * With disperse set, a ray that is not itself a refraction ray and refracts at
+ * this material splits into three refraction rays through ior[0], ior[1], ior[2],
+ * each child's colour masked to its channel (src/Blinn.cpp:169-173,275-301). */
+int mrt_scene_set_material_dispersion(mrt_scene* s, int material, int disperse, const float ior[3]);
 /* Blinn::setReflectGloss (src/Blinn.h:42; default 1): below 1 the reflection
  * vector is blended with a cosine-distributed sample
  * (Material::getCosineDistributedSamples, src/Material.cpp:14-41; src/Blinn.cpp:166-171). */

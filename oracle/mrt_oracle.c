@@ -1340,7 +1340,7 @@ typedef struct {
     uint32_t pixel;
     uint32_t sample;                /* eye ray of the pixel (adaptive supersampling) */
     uint32_t skey;                  /* RNG sub-stream: sample * 1024 + path */
-    uint32_t dim;                   /* RNG draw key: (level + 1) << 24 | k (camera: 0-2) */
+    uint32_t dim;                   /* RNG draw key: (level + 1) << 24 | branch << 16 | k (camera: 0-2) */
     uint64_t shadow_rays, nodes, leaves;
     uint64_t secondary_rays;        /* reflection / refraction / path-tracing GI rays */
     uint32_t shadow_mask;
@@ -1354,7 +1354,12 @@ typedef struct {
  * reference draws one global sequence (src/Scene.cpp:39-47); both are
  * independent uniforms per draw. */
 static float next_rand(shade_ctx* c) { return oro_rand(c->pixel, c->skey, c->dim++, 0x5EEDu); }
-static void begin_level(shade_ctx* c, int level) { c->dim = (uint32_t)(level + 1) << 24; }
+/* branch: the dispersion branch code of the shade() call (0 outside dispersive
+ * splits; each split appends its child index + 1 in two bits), so sibling rays
+ * at one level draw from their own keys */
+static void begin_level(shade_ctx* c, int level, int branch) {
+    c->dim = (uint32_t)(level + 1) << 24 | (uint32_t)(branch & 0xFF) << 16;
+}
 static void begin_camera(shade_ctx* c) { c->skey = c->sample * 1024u; c->dim = 0; }
 
 static int trace_shadow(shade_ctx* c, v3 from, v3 L, float tMax) {
@@ -1549,8 +1554,8 @@ static v3 ray_point(const ray_t* r, float t) {
 }
 
 /* Lambert::shade, src/Lambert.cpp:19-53 (sampleLight without isSecondary) */
-static v3 shade_lambert(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h, int level) {
-    begin_level(c, level);
+static v3 shade_lambert(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h, int level, int branch) {
+    begin_level(c, level, branch);
     v3 L = V(0, 0, 0);
     v3 P = ray_point(r, h->t);
     v3 N, geoN;
@@ -1576,8 +1581,10 @@ static v3 shade_lambert(shade_ctx* c, const oro_material* mat, const ray_t* r, c
 typedef struct { float v[12]; unsigned idx; } ior_list;
 
 /* chain position of a shade() call: Ray bounces / giBounces (src/Ray.h:24-25,97),
- * isSecondary, and the chain level (bounces + giBounces) that keys its draws */
-typedef struct { int bounces, gi, secondary, level; } chain_t;
+ * isSecondary, the chain level (bounces + giBounces) that keys its draws, the
+ * ray's IS_REFRACT_RAY flag (src/Ray.h:18: set on refraction children only) and
+ * the dispersion branch code (begin_level) */
+typedef struct { int bounces, gi, secondary, level, refr, branch; } chain_t;
 
 static v3 shade_hit(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior, chain_t ch);
 
@@ -1651,7 +1658,7 @@ static v3 path_trace(shade_ctx* c, const oro_material* mat, v3 P, v3 theNormal, 
         if (trace_secondary(c, &gr, &nh)) {
             ior_list child;
             child.v[0] = 1.0f; child.v[1] = curIOR; child.idx = 1;   /* Ray(threadID) + set(.., r_IOR(), ..) */
-            chain_t cc = {ch.bounces, ch.gi + 1, 1, ch.level + 1};
+            chain_t cc = {ch.bounces, ch.gi + 1, 1, ch.level + 1, 0, ch.branch};   /* IS_PRIMARY_RAY */
             out = vadd(out, vmul(kd, shade_child(c, &gr, &nh, &child, cc)));
         } else if (mat->sample_env && s->sample_env) {
             out = vadd(out, vmul(kd, env_color(s, randD)));
@@ -1669,11 +1676,11 @@ static v3 path_trace(shade_ctx* c, const oro_material* mat, v3 P, v3 theNormal, 
 /* Blinn::shade, src/Blinn.cpp:91-335: Fresnel-weighted Russian roulette between
  * direct lighting (+ path tracing) and one reflection or refraction ray (bounces
  * < 5), with the ray's IOR history, glossy reflection vector, translucency,
- * m_Le and the colour / normal / specular / reflect / refract maps (no
- * dispersion). */
+ * m_Le, the colour / normal / specular / reflect / refract maps and dispersion
+ * (three refraction rays, one per colour channel). */
 static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, const hit_t* h, ior_list* ior,
                       chain_t ch) {
-    begin_level(c, ch.level);
+    begin_level(c, ch.level, ch.branch);
     v3 Ld = V(0, 0, 0), Ls = V(0, 0, 0), Lr = V(0, 0, 0), Lt = V(0, 0, 0), translucency = V(0, 0, 0);
     v3 rayD = V(r->d[0], r->d[1], r->d[2]);
     v3 viewDir = vneg(rayD);
@@ -1709,17 +1716,23 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
         v3 randD = cosine_sample(c, theNormal);
         rVec = vnormalized(vadd(vscale(rVec, mat->gloss), vscale(randD, 1 - mat->gloss)));
     }
-    float outIOR;
+    /* outIOR: the medium the ray goes into; a dispersive material hit by a ray
+     * that is not itself a refraction ray takes all three m_ior and does not pop
+     * the history (src/Blinn.cpp:167-185) */
+    const int disp = mat->disperse && !ch.refr;
+    float outIOR[3] = {0, 0, 0};
     const float inIOR = ior->v[ior->idx];
-    if (flip) {             /* leaving the material: pop the ray's (mutable) history */
+    if (disp) {
+        outIOR[0] = mat->ior3[0]; outIOR[1] = mat->ior3[1]; outIOR[2] = mat->ior3[2];
+    } else if (flip) {      /* leaving the material: pop the ray's (mutable) history */
         if (ior->idx > 0) ior->idx--;
-        outIOR = ior->v[ior->idx];
+        outIOR[0] = ior->v[ior->idx];
     } else {
-        outIOR = mat->ior;
+        outIOR[0] = mat->ior;   /* m_ior[1] */
     }
     float Rs = 0, Ts = 0;
     if ((double)mat->reflect > 0.0 || (double)mat->refract > 0.0) {
-        Rs = fresnel(inIOR, outIOR, vDotN);
+        Rs = fresnel(inIOR, outIOR[0], vDotN);
         Ts = 1.0f - Rs;
     }
     float rrFloat = next_rand(c);        /* src/Blinn.cpp:195 */
@@ -1750,7 +1763,7 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
     } else {
         int doEnv = 1;
         rrFloat = next_rand(c);
-        chain_t cc = {ch.bounces + 1, ch.gi, 0, ch.level + 1};   /* shade(..) default isSecondary = false */
+        chain_t cc = {ch.bounces + 1, ch.gi, 0, ch.level + 1, 0, ch.branch};   /* shade(..) default isSecondary = false */
         if (rrFloat < reflectAmt * Rs) {
             if (reflectAmt * Rs > 0.0f && ch.bounces < 5) {
                 ior_list child = *ior;
@@ -1762,15 +1775,45 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
                 }
             }
             if (reflectAmt * Rs > 0.0f && doEnv) Lr = vadd(Lr, vmul(ks, env_color(c->s, rVec)));
+        } else if (refractAmt * Ts > 0.0f && disp) {
+            /* dispersion (src/Blinn.cpp:275-301): one refraction ray per colour
+             * channel i through m_ior[i]; each child's colour is masked to its
+             * channel; a missed child adds nothing, and only when all three miss
+             * (or none is traced, bounces >= 5) does Lt take the environment, in the
+             * last direction computed (i = 2) */
+            v3 tVec = V(0, 0, 0);
+            for (int i = 0; i < 3; i++) {
+                float snellsQ = inIOR / outIOR[i];
+                float sqrtPart = std_max(0.0f, sqrtf(1.0f - (snellsQ * snellsQ) * (1.0f - vDotN * vDotN)));
+                tVec = vnormalized(vadd(vscale(rayD, snellsQ), vscale(theNormal, snellsQ * vDotN - sqrtPart)));
+                if (ch.bounces < 5) {
+                    ior->v[ior->idx + 1] = outIOR[i];   /* r_IOR.push(outIOR[i]), copied, then popped */
+                    ior_list child = *ior;
+                    child.idx = ior->idx + 1;
+                    chain_t ci = cc;
+                    ci.refr = 1;
+                    ci.branch = ((ch.branch << 2) | (i + 1)) & 0xFF;
+                    ray_t tr = make_ray_t(P, tVec, c->time);
+                    hit_t nh;
+                    if (trace_secondary(c, &tr, &nh)) {
+                        v3 mask = V(i == 0 ? 1.0f : 0.0f, i == 1 ? 1.0f : 0.0f, i == 2 ? 1.0f : 0.0f);
+                        v3 refraction = vmul(shade_child(c, &tr, &nh, &child, ci), mask);
+                        Lt = vadd(Lt, vmul(ks, refraction));
+                        doEnv = 0;
+                    }
+                }
+            }
+            if (doEnv) Lt = vadd(Lt, vmul(ks, env_color(c->s, tVec)));
         } else if (refractAmt * Ts > 0.0f) {
-            float snellsQ = inIOR / outIOR;
+            float snellsQ = inIOR / outIOR[0];
             float sqrtPart = std_max(0.0f, sqrtf(1.0f - (snellsQ * snellsQ) * (1.0f - vDotN * vDotN)));
             v3 tVec = vnormalized(vadd(vscale(rayD, snellsQ), vscale(theNormal, snellsQ * vDotN - sqrtPart)));
             if (ch.bounces < 5) {
                 /* ray.r_IOR.push(outIOR) on the mutable history, the child copies it, then pop */
-                ior->v[ior->idx + 1] = outIOR;
+                ior->v[ior->idx + 1] = outIOR[0];
                 ior_list child = *ior;
                 child.idx = ior->idx + 1;
+                cc.refr = 1;   /* IS_REFRACT_RAY */
                 ray_t tr = make_ray_t(P, tVec, c->time);
                 hit_t nh;
                 if (trace_secondary(c, &tr, &nh)) {
@@ -1791,7 +1834,7 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
 static v3 shade_hit(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior, chain_t ch) {
     int tri;
     const oro_material* mat = &c->s->mats[hit_mesh(c->s, h, &tri)->material];
-    return mat->type == ORO_LAMBERT ? shade_lambert(c, mat, r, h, ch.level) : shade_blinn(c, mat, r, h, ior, ch);
+    return mat->type == ORO_LAMBERT ? shade_lambert(c, mat, r, h, ch.level, ch.branch) : shade_blinn(c, mat, r, h, ior, ch);
 }
 
 /* ---------------------------------------------------------------- camera */
@@ -1894,7 +1937,7 @@ static v3 sample_scene(shade_ctx* c, const ray_t* r, hit_t* h, uint32_t* prim_nv
         ior.v[0] = 1.0f; ior.v[1] = 1.001f; ior.idx = 1;
         for (int i = 0; i < s->num_paths; i++) {
             c->skey = c->sample * 1024u + (uint32_t)i;
-            chain_t ch = {0, 0, 0, 0};
+            chain_t ch = {0, 0, 0, 0, 0, 0};
             result = vadd(result, shade_hit(c, r, h, &ior, ch));
         }
         return vscale(result, 1.0f / (float)s->num_paths);

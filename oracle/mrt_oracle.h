@@ -44,6 +44,8 @@ typedef struct {
     float le[3];            /* Blinn m_Le (src/Blinn.h:64), added to shade()   */
     float emitted;          /* Blinn m_lightEmitted (src/Blinn.h:63)           */
     int sample_env;         /* Material::m_sampleEnv (src/Material.h:43)       */
+    int disperse;           /* Material::m_disperse (src/Material.h:45)        */
+    float ior3[3];          /* Blinn m_ior[0..2] (src/Blinn.h:59): dispersion  */
 } oro_material;
 
 typedef struct {

@@ -35,7 +35,8 @@ class Material(C.Structure):
     _fields_ = [("type", C.c_int), ("kd", C.c_float * 3), ("ka", C.c_float * 3), ("ks", C.c_float * 3),
                 ("specExp", C.c_float), ("specAmt", C.c_float),
                 ("reflect", C.c_float), ("refract", C.c_float), ("ior", C.c_float), ("gloss", C.c_float),
-                ("translucency", C.c_float), ("le", C.c_float * 3), ("emitted", C.c_float), ("sample_env", C.c_int)]
+                ("translucency", C.c_float), ("le", C.c_float * 3), ("emitted", C.c_float), ("sample_env", C.c_int),
+                ("disperse", C.c_int), ("ior3", C.c_float * 3)]
 
 
 class Light(C.Structure):
@@ -172,11 +173,15 @@ class OracleScene:
 
     def add_material(self, kind="lambert", kd=(1, 1, 1), ka=(0, 0, 0), ks=(1, 1, 1), specExp=1.0, specAmt=0.0,
                      reflectAmt=0.0, refractAmt=0.0, ior=1.5, specGloss=1.0, translucency=0.0, le=(0, 0, 0),
-                     emitted=0.0, sampleEnv=True):
+                     emitted=0.0, sampleEnv=True, disperse=False, ior3=None):
         """Lambert / Blinn (src/Blinn.h:11-22 defaults: ior 1.5, no reflection / refraction;
-        setLightEmittedColor / setLightEmittedIntensity -> le / emitted; Material::setSampleEnv)."""
+        setLightEmittedColor / setLightEmittedIntensity -> le / emitted; Material::setSampleEnv).
+        ior is m_ior[1] (the non-dispersive refraction); disperse / ior3 = m_disperse and
+        m_ior[0..2] (default: ior three times, as the Blinn constructor sets them)."""
+        i3 = (ior, ior, ior) if ior3 is None else tuple(ior3)
         m = Material(0 if kind == "lambert" else 1, _v3(kd), _v3(ka), _v3(ks), specExp, specAmt,
-                     reflectAmt, refractAmt, ior, specGloss, translucency, _v3(le), emitted, int(bool(sampleEnv)))
+                     reflectAmt, refractAmt, ior, specGloss, translucency, _v3(le), emitted, int(bool(sampleEnv)),
+                     int(bool(disperse)), _v3(i3))
         return self.L.oro_scene_add_material(self.h, C.byref(m))
 
     def add_obj(self, path, material, ctm=None):

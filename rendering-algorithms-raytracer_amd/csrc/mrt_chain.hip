@@ -38,10 +38,10 @@
 namespace mrt {
 
 // per-entry chain state word: IOR index, GI levels, reflect / refract levels,
-// isSecondary, env_miss (the entry's own miss rule)
+// isSecondary, env_miss (the entry's own miss rule), refraction ray, branch code
 __device__ __forceinline__ uint32_t pack_state(const ChainState& cs, bool env_miss) {
     return (uint32_t)cs.idx | (uint32_t)cs.gi << 4 | (uint32_t)cs.bounces << 12 | (cs.secondary ? 1u << 16 : 0u) |
-           (env_miss ? 1u << 17 : 0u);
+           (env_miss ? 1u << 17 : 0u) | (cs.refr ? 1u << 18 : 0u) | (uint32_t)(cs.br & 0xFF) << 19;
 }
 __device__ __forceinline__ void unpack_state(uint32_t w, ChainState& cs, bool& env_miss) {
     cs.idx = (int)(w & 15u);
@@ -49,6 +49,8 @@ __device__ __forceinline__ void unpack_state(uint32_t w, ChainState& cs, bool& e
     cs.bounces = (int)((w >> 12) & 15u);
     cs.secondary = (w >> 16) & 1u;
     env_miss = (w >> 17) & 1u;
+    cs.refr = (w >> 18) & 1u;
+    cs.br = (int)((w >> 19) & 255u);
 }
 
 __device__ __forceinline__ size_t lvl_off(const RenderParams& P, int k) { return (size_t)k * P.ch_cap; }

@@ -433,6 +433,7 @@ struct DeviceState {
     int cus = 0;
     bool point_only = false;
     int recursive = 0;           // chain shading (Shader REC): 1 reflection / refraction, 2 + path tracing
+    bool disperse = false;       // a dispersive Blinn material with secondary rays: the fused (tree) engine
     int wall_khz = 0;            // wall_clock64() rate
     size_t bytes = 0;
     // per-stream launch scratch: frames on different streams are in flight at once
@@ -770,6 +771,9 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     for (const DevMaterial& m : s.materials)
         if (m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f || m.gloss < 1.f || m.translucency > 0.01f)) d.recursive = 1;
     if (s.path_trace) d.recursive = 2;
+    d.disperse = false;
+    for (const DevMaterial& m : s.materials)
+        d.disperse |= m.type == MRT_BLINN && m.disperse && (m.reflect > 0.f || m.refract > 0.f);
     d.gthreads = (uint32_t)d.grid * kWG;
     s.info.device_bytes = total;
     return MRT_OK;
@@ -838,7 +842,13 @@ static void fill_params(const Scene& s, RenderParams& P) {
 // chain levels of the REC kernels: reflection / refraction bounces (< 5) plus
 // the GI bounces (giBounces < m_maxBounces - 1)
 static int chain_levels(const Scene& s) { return 6 + (s.path_trace ? s.max_bounces : 0); }
-static int level_words(const Scene& s) { return s.path_trace ? 12 + 3 * (int)s.lights.size() : 3; }
+// words of a level record: reflect / refract 3; GI 12 + 3 per light; a
+// dispersive split in the fused engine 26 + the IOR history (Shader::level)
+static constexpr int kDispWords = 26 + kIorCap;
+static int level_words(const Scene& s) {
+    const int w = s.path_trace ? 12 + 3 * (int)s.lights.size() : 3;
+    return s.dev && s.dev->disperse ? std::max(w, kDispWords) : w;
+}
 
 static int ensure_levels(StreamCtx& c, size_t floats) {
     if (floats <= c.lvl_cap) return MRT_OK;
@@ -968,7 +978,8 @@ static int chain_shadow_rays(const Scene& s) {
     return m <= 255 ? std::max(1, m) : 0;
 }
 static bool use_chain(const Scene& s) {
-    return s.dev->recursive && g_chain && chain_levels(s) <= kMaxChainLevels && chain_shadow_rays(s) > 0;
+    return s.dev->recursive && !s.dev->disperse && g_chain && chain_levels(s) <= kMaxChainLevels &&
+           chain_shadow_rays(s) > 0;
 }
 static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool count, hipStream_t stream) {
     DeviceState& d = *s.dev;
@@ -1187,6 +1198,7 @@ int mrt_scene_add_material(mrt_scene* s, const mrt_material* m) {
     memcpy(d.kd, m->kd, 12); memcpy(d.ka, m->ka, 12); memcpy(d.ks, m->ks, 12);
     d.spec_exp = m->spec_exp; d.spec_amt = m->spec_amt;
     d.reflect = 0.f; d.refract = 0.f; d.ior = 1.5f; d.gloss = 1.f;   // Blinn defaults (src/Blinn.h:11-22)
+    d.disperse = 0; d.ior3[0] = d.ior3[1] = d.ior3[2] = 1.5f;
     d.translucency = 0.f;
     memcpy(d.le, m->le, 12);
     d.emitted = m->emitted;
@@ -1583,6 +1595,20 @@ int mrt_scene_set_material_optics(mrt_scene* s, int material, float reflect_amt,
     m.reflect = reflect_amt;
     m.refract = refract_amt;
     m.ior = ior;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
+}
+
+int mrt_scene_set_material_dispersion(mrt_scene* s, int material, int disperse, const float ior[3]) {
+    if (!s || material < 0 || material >= (int)s->impl.materials.size() || !ior || !(ior[0] > 0.f) ||
+        !(ior[1] > 0.f) || !(ior[2] > 0.f)) {
+        set_error("bad dispersion: need a valid material and three IORs > 0");
+        return MRT_ERR_INVALID;
+    }
+    DevMaterial& m = s->impl.materials[(size_t)material];
+    m.disperse = disperse ? 1 : 0;
+    for (int i = 0; i < 3; i++) m.ior3[i] = ior[i];
+    m.ior = ior[1];   // m_ior[1]: the IOR of the non-dispersive refraction
     s->impl.dev_dirty = true;
     return MRT_OK;
 }

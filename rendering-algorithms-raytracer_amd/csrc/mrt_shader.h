@@ -139,8 +139,13 @@ __device__ __forceinline__ v3 xform_dir3(const float* T, v3 u) {
 // shade_path); compiled only into the kernels that run such scenes, so the
 // direct-lighting kernels keep their register budget.
 // RNG keys of the counter RNG (mrt_math.h): sub-stream skey = eye-ray sample *
-// 1024 + path, draw key dim = (chain level + 1) << 24 | k (camera: dims 0-2).
-__device__ __forceinline__ uint32_t level_key(int level) { return (uint32_t)(level + 1) << 24; }
+// 1024 + path, draw key dim = (chain level + 1) << 24 | branch << 16 | k
+// (camera: dims 0-2).  branch: the dispersion branch code of the ray (0 outside
+// dispersive splits; each split appends child index + 1 in two bits), so
+// sibling rays of one level draw from their own keys.
+__device__ __forceinline__ uint32_t level_key(int level, int branch = 0) {
+    return (uint32_t)(level + 1) << 24 | (uint32_t)(branch & 0xFF) << 16;
+}
 
 // Working IOR history of the rays below the camera ray (Ray::IORList,
 // src/Ray.h:43-50): a per-lane LDS column in the REC kernels.
@@ -159,10 +164,12 @@ __device__ __forceinline__ void trav_alpha(Trav& T, const RenderParams& P) {
 }
 
 // Chain state of one path at its current level (Shader::level).
-enum { kRefl = 1, kRefr = 2, kGI = 3 };
+enum { kRefl = 1, kRefr = 2, kGI = 3, kDisp = 4 };
 struct ChainState {
     int idx = 0, depth = 0, gi = 0, bounces = 0;  // IOR history index, level, GI / reflect-refract levels so far
     bool secondary = false;                       // isSecondary of this level's shade()
+    bool refr = false;                            // the ray is a refraction ray (IS_REFRACT_RAY, src/Ray.h:18)
+    int br = 0;                                   // dispersion branch code (level_key)
 };
 // A chain level's record (the terms of the level that spawned a child): word w at p[w * stride]
 struct ChainRec {
@@ -175,6 +182,7 @@ struct LevelOut {
     v3 val, dir;     // the level's final value / the child's direction
     bool spawn;      // a child ray was spawned (its terms are in the level record)
     bool env_miss;   // a missed child takes the environment colour (false: GI with no environment sampling)
+    bool split = false;   // dispersion: three refraction children (Shader::disp_child), not r2
 };
 
 // Material::getEnvironmentColor (src/Material.cpp:44-62): scene map or background
@@ -576,7 +584,8 @@ struct Shader {
     __device__ void level(const DRay& r, const DHit& h, ChainState& cs, IorCam& cam, const ChainRec& rec, LevelOut& o) {
         const v3 z = mk(0, 0, 0);
         o.spawn = false;
-        dim = level_key(cs.depth);
+        o.split = false;
+        dim = level_key(cs.depth, cs.br);
         v3 N, geoN;
         uint32_t mi;
         normals(h, N, geoN, mi);
@@ -610,9 +619,15 @@ struct Shader {
             const v3 rd = cosine_sample(n);
             rVec = normalized(add(scale(rVec, M.gloss), scale(rd, 1.0f - M.gloss)), rsqT);
         }
-        // inIOR, then a back-face hit pops the (mutable) history (src/Blinn.cpp:167-185)
+        // inIOR, then a back-face hit pops the (mutable) history (src/Blinn.cpp:167-185);
+        // a dispersive material hit by a ray that is not a refraction ray takes
+        // outIOR = m_ior[0..2] and does not pop
+        const bool disp = MODE == kFused && M.disperse && !cs.refr;
         float inIOR, outIOR = M.ior;
-        if (cs.depth == 0) {
+        if (disp) {
+            inIOR = cs.depth == 0 ? cam.at(cam.idx) : ior_at(cs.idx);
+            outIOR = M.ior3[0];
+        } else if (cs.depth == 0) {
             inIOR = cam.at(cam.idx);
             if (flip) { if (cam.idx > 0) cam.idx--; outIOR = cam.at(cam.idx); }
         } else {
@@ -679,6 +694,7 @@ struct Shader {
                 ior_at(0) = 1.0f; ior_at(1) = curIOR; cs.idx = 1;
                 cs.depth++; cs.gi++;
                 cs.secondary = true;
+                cs.refr = false;   // IS_PRIMARY_RAY
                 o.spawn = true;
                 o.r2 = make_ray(Pt, randD, time);
                 o.dir = randD;
@@ -701,6 +717,30 @@ struct Shader {
             if (spawn && cs.depth == 0) {   // the child copies the camera ray's history
                 ior_at(0) = 1.0f; ior_at(1) = cam.v1; ior_at(2) = cam.v2; cs.idx = cam.idx;
             }
+        } else if (disp && refract * Ts > 0.0f) {
+            // dispersion (src/Blinn.cpp:275-301): three refraction children, one per
+            // colour channel, traced by the caller in channel order (disp_child)
+            if (cs.bounces >= kMaxBounce) {   // none traced: Lt = ks * environment along channel 2's direction
+                const v3 L = add(z, mul(ks, env_color(disp_dir(rayD, n, vDotN, inIOR / M.ior3[2]))));
+                o.val = add(add(base, scale(add(z, L), rrSpec)), le);
+                return;
+            }
+            rec(0) = __int_as_float((int)mi | (kDisp << 16));
+            rec(1) = rrRecip; rec(2) = rrSpec;
+            rec(3) = 0.f; rec(4) = 0.f; rec(5) = 0.f;   // Lt
+            rec(6) = __int_as_float(0); rec(7) = __int_as_float(0);   // next child, some child hit
+            rec(8) = Pt.x; rec(9) = Pt.y; rec(10) = Pt.z;
+            rec(11) = rayD.x; rec(12) = rayD.y; rec(13) = rayD.z;
+            rec(14) = n.x; rec(15) = n.y; rec(16) = n.z;
+            rec(17) = vDotN; rec(18) = inIOR;
+            rec(19) = M.ior3[0]; rec(20) = M.ior3[1]; rec(21) = M.ior3[2];
+            rec(22) = __int_as_float(cs.depth == 0 ? cam.idx : cs.idx);
+            rec(23) = __int_as_float(cs.gi); rec(24) = __int_as_float(cs.bounces); rec(25) = __int_as_float(cs.br);
+            if (cs.depth > 0)
+                for (int j = 0; j < kIorCap; j++) rec(26 + j) = ior_at(j);
+            o.spawn = true;
+            o.split = true;
+            return;
         } else if (refract * Ts > 0.0f) {
             refr = true;
             const float q = inIOR / outIOR;
@@ -724,6 +764,7 @@ struct Shader {
             rec(1) = rrRecip; rec(2) = rrSpec;
             cs.depth++; cs.bounces++;
             cs.secondary = false;   // shade(..) with the default isSecondary
+            cs.refr = refr;         // IS_REFRACT_RAY / IS_REFLECT_RAY
             o.spawn = true;
             o.r2 = make_ray(Pt, dir, time);
             o.dir = dir;
@@ -735,32 +776,115 @@ struct Shader {
         o.val = add(add(base, scale(refr ? add(z, L) : add(L, z), rrSpec)), le);
     }
 
+    // the refraction direction of Blinn::shade (src/Blinn.cpp:281-283,307-309)
+    __device__ v3 disp_dir(v3 rayD, v3 n, float vDotN, float q) const {
+        const float sq = std_max(0.0f, sqrtf(1.0f - (q * q) * (1.0f - vDotN * vDotN)));
+        return normalized(add(scale(rayD, q), scale(n, q * vDotN - sq)), rsqT);
+    }
+    // Child i of the dispersive split recorded at level k: its ray, its chain state
+    // and its IOR history (the parent's with outIOR[i] pushed, src/Blinn.cpp:285-286;
+    // on the camera ray the push persists into its later paths, as at level 0 above).
+    __device__ DRay disp_child(const ChainRec& rec, int k, int i, ChainState& cs, IorCam& cam) {
+        const float outI = rec(19 + i);
+        const v3 dir = disp_dir(mk(rec(11), rec(12), rec(13)), mk(rec(14), rec(15), rec(16)), rec(17), rec(18) / outI);
+        const int pidx = __float_as_int(rec(22));
+        if (k == 0) {
+            if (cam.idx == 0) cam.v1 = outI; else cam.v2 = outI;
+            ior_at(0) = 1.0f; ior_at(1) = cam.v1; ior_at(2) = cam.v2;
+        } else {
+            for (int j = 0; j < kIorCap; j++) ior_at(j) = rec(26 + j);
+            ior_at(pidx + 1) = outI;
+        }
+        cs.idx = pidx + 1;
+        cs.depth = k + 1;
+        cs.gi = __float_as_int(rec(23));
+        cs.bounces = __float_as_int(rec(24)) + 1;
+        cs.secondary = false;
+        cs.refr = true;
+        cs.br = ((__float_as_int(rec(25)) << 2) | (i + 1)) & 0xFF;
+        secondary++;
+        return make_ray(mk(rec(8), rec(9), rec(10)), dir, time);
+    }
+
     // Blinn::shade's recursion for one path, fused: each level's child ray is
-    // traced inline and the levels are combined deepest first.
+    // traced inline, depth first, and a finished level's value is folded into
+    // its parent's.  A chain level (one child) folds with chain_combine; a
+    // dispersive level (three children, src/Blinn.cpp:275-301) adds each hit
+    // child's colour masked to its channel, then traces the next child; a missed
+    // dispersive child adds nothing, and with no child hit Lt takes the
+    // environment along channel 2's direction.
     template <bool COUNT>
     __device__ v3 shade_path(DRay r, DHit h, IorCam& cam) {
+        const v3 z = mk(0, 0, 0);
         ChainState cs;
-        v3 val;
-        bool none = false;
         for (;;) {
             LevelOut o;
-            level<COUNT>(r, h, cs, cam, rec_fused(cs.depth), o);
-            if (!o.spawn) { val = o.val; break; }
-            DHit h2{1e12f, 0.f, 0.f, -1};
-            if (traverse<false, COUNT, FAST, INST>(T, o.r2, 0.001f, h2, st)) {
-                r = o.r2;
-                h = h2;
-                continue;
+            const int d = cs.depth;
+            level<COUNT>(r, h, cs, cam, rec_fused(d), o);
+            v3 val = z;
+            bool none = false, start = false;
+            int k;
+            if (!o.spawn) {
+                val = o.val;
+                k = d - 1;
+            } else if (o.split) {
+                start = true;   // level d starts its dispersive children
+                k = d;
+            } else {
+                DHit h2{1e12f, 0.f, 0.f, -1};
+                if (traverse<false, COUNT, FAST, INST>(T, o.r2, 0.001f, h2, st)) {
+                    r = o.r2;
+                    h = h2;
+                    continue;
+                }
+                none = !o.env_miss;   // the missed child's value: environment, or nothing (GI, no env)
+                val = none ? z : env_color(o.dir);
+                k = d;
             }
-            none = !o.env_miss;   // the missed child's value: environment, or nothing (GI, no env)
-            val = none ? mk(0, 0, 0) : env_color(o.dir);
-            break;
+            bool descend = false;
+            for (; k >= 0; k--) {   // fold up until a level has a child left to trace
+                const ChainRec rec = rec_fused(k);
+                const int info = __float_as_int(rec(0));
+                if ((info >> 16) != kDisp) {
+                    val = chain_combine(P, rec, val, none);
+                    none = false;
+                    continue;
+                }
+                const DevMaterial& M = P.mats[info & 0xFFFF];
+                const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
+                int i = __float_as_int(rec(6));
+                if (!start) {   // child i - 1 hit and has its value: Lt += m_ks * (refraction * mask)
+                    const v3 mask = mk(i == 1 ? 1.0f : 0.0f, i == 2 ? 1.0f : 0.0f, i == 3 ? 1.0f : 0.0f);
+                    const v3 Lt = add(mk(rec(3), rec(4), rec(5)), mul(ks, mul(val, mask)));
+                    rec(3) = Lt.x; rec(4) = Lt.y; rec(5) = Lt.z;
+                    rec(7) = __int_as_float(1);
+                }
+                start = false;
+                while (i < 3) {
+                    const DRay c = disp_child(rec, k, i, cs, cam);
+                    rec(6) = __int_as_float(++i);
+                    DHit h2{1e12f, 0.f, 0.f, -1};
+                    if (traverse<false, COUNT, FAST, INST>(T, c, 0.001f, h2, st)) {
+                        r = c;
+                        h = h2;
+                        descend = true;
+                        break;
+                    }
+                }
+                if (descend) break;
+                v3 Lt = mk(rec(3), rec(4), rec(5));
+                if (__float_as_int(rec(7)) == 0) {   // doEnv: no child hit
+                    const v3 dir2 = disp_dir(mk(rec(11), rec(12), rec(13)), mk(rec(14), rec(15), rec(16)), rec(17),
+                                             rec(18) / rec(21));
+                    Lt = add(Lt, mul(ks, env_color(dir2)));
+                }
+                const v3 ka = mk(M.ka[0], M.ka[1], M.ka[2]), le = mk(M.le[0], M.le[1], M.le[2]);
+                const v3 base = scale(add(add(add(z, ka), z), z), rec(1));
+                val = add(add(base, scale(add(z, Lt), rec(2))), le);
+                none = false;
+            }
+            if (!descend) return val;
         }
-        for (int k = cs.depth - 1; k >= 0; k--) {   // combine deepest first
-            val = chain_combine(P, rec_fused(k), val, none);
-            none = false;
-        }
-        return val;
     }
 };
 

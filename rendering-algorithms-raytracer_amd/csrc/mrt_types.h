@@ -58,7 +58,7 @@ struct DevMaterial {
     float kd[3], ka[3], ks[3];
     float spec_exp, spec_amt;
     float reflect, refract;  // Blinn m_reflectAmt / m_refractAmt (src/Blinn.h:62, src/Material.h:73)
-    float ior;               // Blinn m_ior (src/Blinn.cpp:25-27)
+    float ior;               // Blinn m_ior[1] (src/Blinn.cpp:25-27): the non-dispersive refraction (src/Blinn.cpp:183)
     float gloss;             // Blinn m_specGloss (src/Blinn.h:42,65): < 1 jitters the reflection vector
     float translucency;      // Material::m_translucency (src/Material.h:30,44): > 0.01 lights the back side
     float le[3];             // Blinn m_Le (src/Blinn.h:64): added to every shade() result (src/Blinn.cpp:335)
@@ -68,6 +68,10 @@ struct DevMaterial {
     // Material m_colorMap, m_normalMap, m_specularMap, m_reflectMap, m_refractMap,
     // m_alphaMap (src/Material.h:20-25,35-40): texture ids, -1 = none
     int32_t maps[6];
+    // Material::m_disperse + Blinn m_ior[0..2] (src/Material.h:45, src/Blinn.h:59):
+    // a ray that is not a refraction ray splits into one refraction ray per channel
+    int32_t disperse;
+    float ior3[3];
 };
 enum { kMapColor = 0, kMapNormal = 1, kMapSpecular = 2, kMapReflect = 3, kMapRefract = 4, kMapAlpha = 5 };
 

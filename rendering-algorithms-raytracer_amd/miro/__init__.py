@@ -163,13 +163,17 @@ class Blinn(_Maps):
     src/Blinn.h:11-22: direct lighting plus Fresnel-weighted reflection / refraction
     rays (src/Blinn.cpp:91-335), glossy reflection vectors, translucency, emission
     (setLightEmittedIntensity / setLightEmittedColor), path tracing (Scene.setPathTrace)
-    and texture maps (colour, normal, specular, reflect, refract, alpha).  Dispersion
-    is not on the MI355X path."""
+    texture maps (colour, normal, specular, reflect, refract, alpha) and dispersion
+    (m_disperse with m_ior[0..2]: one refraction ray per colour channel).  As in the
+    reference, setIor(ior, i) sets m_ior[i] and the non-dispersive refraction reads
+    m_ior[1] (src/Blinn.cpp:183), so setIor(x) alone changes only dispersion."""
 
     def __init__(self, kd=Vector3(1), ka=Vector3(0), ks=Vector3(1), kt=Vector3(0), ior=1.5,
                  specExp=1.0, specAmt=0.0, reflectAmt=0.0, refractAmt=0.0, specGloss=1.0):
         self.kd, self.ka, self.ks, self.kt = Vector3(kd), Vector3(ka), Vector3(ks), Vector3(kt)
-        self.ior, self.specExp, self.specAmt = float(ior), float(specExp), float(specAmt)
+        self.m_ior = [float(ior)] * 3      # src/Blinn.cpp:25-27
+        self.m_disperse = False            # Material::m_disperse (src/Material.cpp:6)
+        self.specExp, self.specAmt = float(specExp), float(specAmt)
         self.reflectAmt, self.refractAmt = float(reflectAmt), float(refractAmt)
         self.specGloss = float(specGloss)
         self.translucency = 0.0
@@ -187,8 +191,12 @@ class Blinn(_Maps):
 
     def setReflectAmt(self, a): self.reflectAmt = float(a)     # src/Blinn.h:41
     def setRefractAmt(self, a): self.refractAmt = float(a)     # src/Material.h:32
-    def setIor(self, ior, i=0):                                # src/Blinn.h:38 (m_ior[1] is used)
-        self.ior = float(ior)
+    def setIor(self, ior, i=0):                                # src/Blinn.h:38
+        self.m_ior[i] = float(ior)
+
+    @property
+    def ior(self):                                             # the refraction IOR: m_ior[1] (src/Blinn.cpp:183)
+        return self.m_ior[1]
 
     def setKd(self, v): self.kd = Vector3(v)
     def setKa(self, v): self.ka = Vector3(v)
@@ -509,6 +517,9 @@ class Scene:
                     check(L.mrt_scene_set_material_optics(self._h, mats[id(mat)], mat.reflectAmt, mat.refractAmt,
                                                           mat.ior), "material optics")
                     check(L.mrt_scene_set_material_gloss(self._h, mats[id(mat)], mat.specGloss), "material gloss")
+                    if mat.m_disperse:
+                        i3 = (C.c_float * 3)(*mat.m_ior)
+                        check(L.mrt_scene_set_material_dispersion(self._h, mats[id(mat)], 1, i3), "dispersion")
                     check(L.mrt_scene_set_material_translucency(self._h, mats[id(mat)], mat.translucency),
                           "material translucency")
                 check(L.mrt_scene_set_material_sample_env(self._h, mats[id(mat)], int(mat.sampleEnv)), "sampleEnv")

@@ -16,7 +16,7 @@ ERRORS = {-1: "MRT_ERR_INVALID", -2: "MRT_ERR_IO", -3: "MRT_ERR_HIP", -4: "MRT_E
 EXPORTS = [
     "mrt_last_error", "mrt_abi_version", "mrt_device_count", "mrt_scene_create", "mrt_scene_destroy",
     "mrt_scene_add_material", "mrt_scene_add_light", "mrt_scene_add_obj", "mrt_scene_add_mesh",
-    "mrt_scene_mesh_info", "mrt_scene_mesh_export", "mrt_scene_set_background", "mrt_scene_set_num_paths", "mrt_scene_set_subdivs", "mrt_scene_set_material_optics", "mrt_scene_set_material_gloss", "mrt_scene_set_material_translucency",
+    "mrt_scene_mesh_info", "mrt_scene_mesh_export", "mrt_scene_set_background", "mrt_scene_set_num_paths", "mrt_scene_set_subdivs", "mrt_scene_set_material_optics", "mrt_scene_set_material_dispersion", "mrt_scene_set_material_gloss", "mrt_scene_set_material_translucency",
     "mrt_scene_build_bvh", "mrt_scene_bvh_info", "mrt_scene_bvh_export", "mrt_scene_bvh_import",
     "mrt_scene_upload", "mrt_render", "mrt_render_buckets_async", "mrt_unpack_buckets_async",
     "mrt_render_frame_async", "mrt_trace", "mrt_trace_async", "mrt_scene_last_stats", "mrt_rcp_nr",
@@ -121,6 +121,7 @@ def load():
     L.mrt_scene_set_subdivs.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float]
     L.mrt_scene_set_material_optics.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float]
     L.mrt_scene_set_material_gloss.argtypes = [C.c_void_p, C.c_int, C.c_float]
+    L.mrt_scene_set_material_dispersion.argtypes = [C.c_void_p, C.c_int, C.c_int, _fp]
     L.mrt_scene_set_material_translucency.argtypes = [C.c_void_p, C.c_int, C.c_float]
     L.mrt_scene_set_material_emission.argtypes = [C.c_void_p, C.c_int, C.c_float, _fp]
     L.mrt_scene_set_material_sample_env.argtypes = [C.c_void_p, C.c_int, C.c_int]

@@ -50,6 +50,7 @@ static int add_material(mrt_scene* s, const Material* m) {
         (rc = mrt_scene_set_material_translucency(s, id, b->m_translucency)) ||
         (rc = mrt_scene_set_material_sample_env(s, id, b->m_sampleEnv ? 1 : 0)))
         return rc;
+    if (b->m_disperse && (rc = mrt_scene_set_material_dispersion(s, id, 1, b->m_ior))) return rc;
     return id;
 }
 

@@ -48,6 +48,7 @@ struct TriangleMesh {
 };
 
 struct Material {
+    bool m_disperse = false;   // src/Material.h:45 (read by Blinn::shade only)
     virtual ~Material() = default;
 };
 struct Lambert : Material {

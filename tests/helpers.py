@@ -46,13 +46,19 @@ def materials_pair(P, O_, mat):
         pm = miro.Lambert(mat["kd"])
         return pm, O_.add_material("lambert", kd=mat["kd"])
     pm = miro.Blinn(mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0), **optics)
+    if "ior3" in mat:   # setIor(ior, i) for i = 0..2, src/Blinn.h:38
+        for i, v in enumerate(mat["ior3"]):
+            pm.setIor(v, i)
+    pm.m_disperse = bool(mat.get("disperse", False))
     pm.setTranslucency(mat.get("translucency", 0.0))
     pm.setLightEmittedIntensity(mat.get("emitted", 0.0))
     pm.setLightEmittedColor(mat.get("le", (0, 0, 0)))
     pm.setSampleEnv(mat.get("sampleEnv", True))
     om = O_.add_material("blinn", kd=mat["kd"], specExp=mat.get("specExp", 1.0), specAmt=mat.get("specAmt", 0.0),
                          translucency=mat.get("translucency", 0.0), le=mat.get("le", (0, 0, 0)),
-                         emitted=mat.get("emitted", 0.0), sampleEnv=mat.get("sampleEnv", True), **optics)
+                         emitted=mat.get("emitted", 0.0), sampleEnv=mat.get("sampleEnv", True),
+                         disperse=mat.get("disperse", False), ior3=mat.get("ior3"),
+                         **dict(optics, ior=mat["ior3"][1] if "ior3" in mat else optics["ior"]))
     return pm, om
 
 
