@@ -213,6 +213,22 @@ int build_dome(const Texture& t, DomeTables& d, std::string& err) {
     inv = 1.f / (float)nv;
     for (int i = 0; i <= nv; i++) d.cos_v[i] = cosf((float)i * inv * kPI);
     for (int i = 0; i <= nv; i++) d.sin_v[i] = sinf((float)i * inv * kPI);
+    // derived tables of the device sampler: the lat-long lookup of every table
+    // direction (Shader::dome_light reads it instead of evaluating atan2 / acos
+    // per sample; the same tex_lookup_dir code, evaluated here once per cell) and
+    // the CDF guide tables
+    d.rad.assign((size_t)4 * (nu + 1) * (nv + 1), 0.f);
+    for (int iv = 0; iv <= nv; iv++)
+        for (int iu = 0; iu <= nu; iu++) {
+            const float cosT = d.cos_v[iv], sinT = d.sin_v[iv], sinP = d.sin_u[iu], cosP = d.cos_u[iu];
+            const v3 L = tex_lookup_dir(t.rgb.data(), t.W, t.H, -sinT * cosP, -cosT, -sinT * sinP);
+            float* q = &d.rad[4 * ((size_t)iv * (nu + 1) + iu)];
+            q[0] = L.x; q[1] = L.y; q[2] = L.z;
+        }
+    d.guide_u.resize((size_t)nu + 1);
+    guide_table(d.cdf_u.data(), nu, d.guide_u.data());
+    d.guide_v.resize((size_t)nu * (nv + 1));
+    for (int u = 0; u < nu; u++) guide_table(&d.cdf_v[(size_t)u * (nv + 1)], nv, &d.guide_v[(size_t)u * (nv + 1)]);
     return MRT_OK;
 }
 

@@ -728,6 +728,15 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
             (rc = upload_floats(t.sin_u, g.sin_u)) || (rc = upload_floats(t.cos_v, g.cos_v)) ||
             (rc = upload_floats(t.sin_v, g.sin_v)))
             return rc;
+        float *rad = nullptr, *gu = nullptr, *gv = nullptr;
+        if ((rc = upload(rad, t.rad.data(), t.rad.size() * sizeof(float), total)) ||
+            (rc = upload(gu, t.guide_u.data(), t.guide_u.size() * sizeof(int32_t), total)) ||
+            (rc = upload(gv, t.guide_v.data(), t.guide_v.size() * sizeof(int32_t), total)))
+            return rc;
+        for (float* p : {rad, gu, gv}) d.bufs.push_back(p);
+        g.rad = rad;
+        g.guide_u = reinterpret_cast<const int32_t*>(gu);
+        g.guide_v = reinterpret_cast<const int32_t*>(gv);
         g.tex = dtex[t.tex];
         g.inv_int_u = t.inv_int_u;
         g.nu = t.nu;

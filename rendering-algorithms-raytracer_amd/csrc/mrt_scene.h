@@ -45,6 +45,11 @@ struct DomeTables {             // DomeLight::setTexture (src/DomeLight.cpp:8-78
     int32_t tex = -1, nu = 0, nv = 0;
     std::vector<float> func_u, cdf_u, func_v, cdf_v, int_v, inv_int_v, cos_u, sin_u, cos_v, sin_v;
     float int_u = 0.f, inv_int_u = 0.f;
+    // derived lookup tables of the device sampler (not reference state):
+    // rad = the lat-long lookup of every table direction (iu, iv) in 0..nu x 0..nv,
+    // 4 floats per cell; guide_u / guide_v = CDF guide tables (guide_table)
+    std::vector<float> rad;
+    std::vector<int32_t> guide_u, guide_v;
 };
 
 // A ProxyObject's BVH (ProxyObject::setupMultiProxy, src/ProxyObject.cpp:149-167):

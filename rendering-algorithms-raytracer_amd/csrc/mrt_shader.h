@@ -334,11 +334,12 @@ struct Shader {
             const float e1 = next_rand();
             const float e2 = next_rand();
             float pdf0, pdf1;
-            const float fu = dist_sample(D.cdf_u, D.func_u, D.nu, D.inv_int_u, e1, pdf0);
+            const float fu = dist_sample_guided(D.cdf_u, D.func_u, D.guide_u, D.nu, D.inv_int_u, e1, pdf0);
             const int iu = (int)fu;
             const int u = iu == D.nu ? iu - 1 : iu;
-            const float fv = dist_sample(D.cdf_v + (size_t)u * (D.nv + 1), D.func_v + (size_t)u * D.nv, D.nv,
-                                         D.inv_int_v[u], e2, pdf1);
+            const size_t cv = (size_t)u * (D.nv + 1);
+            const float fv = dist_sample_guided(D.cdf_v + cv, D.func_v + (size_t)u * D.nv, D.guide_v + cv, D.nv,
+                                                D.inv_int_v[u], e2, pdf1);
             const int iv = (int)fv;
             const float cosT = D.cos_v[iv], sinT = D.sin_v[iv], sinP = D.sin_u[iu], cosP = D.cos_u[iu];
             const v3 dir = mk(-sinT * cosP, -cosT, -sinT * sinP);
@@ -347,7 +348,8 @@ struct Shader {
                 continue;
             }
             const float pdf = (pdf0 * pdf1) / (kTwoPI2 * sinT);
-            const v3 img = tex_lookup_dir(D.tex, D.nu, D.nv, dir.x, dir.y, dir.z);
+            const float4 rc = reinterpret_cast<const float4*>(D.rad)[(size_t)iv * (D.nu + 1) + iu];   // tex_lookup_dir of dir (host table)
+            const v3 img = mk(rc.x, rc.y, rc.z);
             const float inv = 1.0f / pdf;  // E = m_Gain * imageSample / pdf (Vector3::operator/)
             const v3 E = scale(scale(img, l.power), inv);
             float att = 1.0f;

@@ -127,4 +127,46 @@ MRT_HD float dist_sample(const float* cdf, const float* func, int n, float inv_f
     return (float)o + du;
 }
 
+// CDF guide table of a Distribution1D with n entries (cdf[0..n]): bucket b(x) =
+// clamp((int)(x * n), 0, n - 1); g[b] = the first index i with b(cdf[i]) >= b,
+// b = 0..n.  b() is monotone and the CDF non-decreasing, so for any u the
+// lower_bound of u lies in [g[b(u)], g[b(u) + 1]] (entries before g[b(u)] have
+// a smaller bucket, so are < u; entry g[b(u) + 1] has a larger one, so is > u;
+// with no such entry cdf[n] = 1 >= u).  A derived table of the device sampler.
+MRT_HD int guide_bucket(float x, int n) {
+    const int b = trunc_i32(x * (float)n);
+    return b < 0 ? 0 : (b > n - 1 ? n - 1 : b);
+}
+inline void guide_table(const float* cdf, int n, int32_t* g) {
+    int i = 0;
+    for (int b = 0; b <= n; b++) {
+        while (i <= n && guide_bucket(cdf[i], n) < b) i++;
+        g[b] = i;
+    }
+}
+
+// Distribution1D::sample with the search narrowed by the guide table: the same
+// lower_bound position, so the same sample and pdf as dist_sample.
+MRT_HD float dist_sample_guided(const float* cdf, const float* func, const int32_t* guide, int n, float inv_func_int,
+                                float u, float& pdf) {
+    const int b = guide_bucket(u, n);
+    const int lo = guide[b], hi = guide[b + 1] < n ? guide[b + 1] : n;
+    int first = lo, len = hi - lo + 1;
+    while (len > 0) {
+        const int half = len >> 1;
+        if (cdf[first + half] < u) {
+            first += half + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
+    }
+    int o = first - 1;
+    o = o < 0 ? 0 : (o > n - 1 ? n - 1 : o);
+    const float c0 = cdf[o], c1 = cdf[o + 1];
+    const float du = (u - c0) / (c1 - c0);
+    pdf = func[o] * inv_func_int;
+    return (float)o + du;
+}
+
 }  // namespace mrt

@@ -109,6 +109,9 @@ struct DevDome {
     const float* sin_v;
     float inv_int_u;
     int32_t nu, nv;
+    const float* rad;        // (nu + 1) x (nv + 1) x 4: texture lookup of each table direction, row iv
+    const int32_t* guide_u;  // nu + 1: CDF guide table of cdf_u (mrt_texture.h dist_sample_guided)
+    const int32_t* guide_v;  // nu * (nv + 1): one per column's cdf_v
 };
 
 // Camera basis hoisted to the host (bit-identical to the per-ray recompute of
