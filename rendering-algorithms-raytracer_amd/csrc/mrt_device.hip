@@ -47,13 +47,17 @@ void set_error(const std::string& m) { g_err = m; }
 //            b mod 8 from that band's counter, then steals from the others: the
 //            rays one XCD traces touch the geometry of one image band, so its
 //            4 MB L2 holds that band's share of the hierarchy.
-//   sched 2: sched 1 + lane refill (non-instanced scenes): a lane whose ray is
-//            done (an any-hit ray ends at its first accepted triangle) or whose
-//            slot is empty takes a new slot as soon as `refill_min` lanes of its
-//            wave are idle; traversal runs one node visit per wave step
-//            (anyhit_step), so the wave no longer waits for its longest ray.
-// Every ray is traced with the same visit order and tests as traverse(), so
-// the answers are identical under every schedule.
+//   sched 2: sched 1 + lane refill: a lane whose ray is done (an any-hit ray
+//            ends at its first accepted triangle) or whose slot is empty takes
+//            a new slot as soon as `refill_min` lanes of its wave are idle;
+//            traversal runs one node visit per wave step (anyhit_step; in
+//            special-leaf scenes anyhit_step_inst, which defers ProxyObject
+//            lanes onto the stack), so the wave no longer waits for its longest
+//            ray.
+// Every ray is traced with traverse()'s box and triangle tests (the same
+// visit order, except the deferred instance walks of sched 2, which an
+// any-hit answer does not depend on), so the answers are identical under
+// every schedule.
 static constexpr int kShadowChunk = 64;
 template <bool COUNT, bool FAST, bool INST>
 __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_rays, int sched, int refill_min) {
@@ -122,7 +126,7 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
             end = (size_t)hi;
             return got != ~0ull;
         };
-        if (INST || sched == 1) {   // wave-uniform chunks, one ray per lane
+        if (sched == 1) {   // wave-uniform chunks, one ray per lane
             size_t first, end;
             while (dequeue(kShadowChunk, first, end)) {
                 const size_t e = first + lane;
@@ -132,13 +136,14 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
                     wave_steps += v;
                 }
             }
-        } else if constexpr (!INST) {   // lane refill
+        } else {   // lane refill
             bool active = false;
             size_t e = 0;
             DRay r{};
             float tmax = 0.f;
             int32_t cur = 0;
             int sp = 0;
+            AnyState as{};
             for (;;) {
                 const unsigned long long idle = __ballot(!active);
                 const int nidle = __popcll(idle);
@@ -156,6 +161,9 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
                             tmax = o.w;
                             cur = 0;
                             sp = 0;
+                            as.cur = 0;
+                            as.sp = 0;
+                            as.inst = -1;
                             active = true;
                         }
                     }
@@ -167,8 +175,10 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
                 if (COUNT) wave_steps++;
                 if (active) {
                     bool hit = false;
-                    const bool done = (FAST && r.finite) ? anyhit_step<COUNT, true>(T, r, 0.001f, tmax, cur, sp, hit, st)
-                                                         : anyhit_step<COUNT, false>(T, r, 0.001f, tmax, cur, sp, hit, st);
+                    bool done;
+                    if constexpr (INST) done = anyhit_step_inst<COUNT, FAST>(T, r, 0.001f, tmax, as, hit, st);
+                    else done = (FAST && r.finite) ? anyhit_step<COUNT, true>(T, r, 0.001f, tmax, cur, sp, hit, st)
+                                                   : anyhit_step<COUNT, false>(T, r, 0.001f, tmax, cur, sp, hit, st);
                     if (done) {
                         P.occl[e] = hit ? 1 : 0;
                         active = false;
@@ -457,7 +467,7 @@ static int g_scalar_nodes = 1;    // scalar-cache fetch of wave-uniform nodes
 static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
 static int g_wavefront = 1;       // general shading: gen / trace / resolve kernels instead of one fused kernel
 static int g_shadow_sched = -1;   // shadow_kernel schedule: 0 grid-stride, 1 XCD bands, 2 bands + lane refill,
-                                  // -1 auto: refill for dome-light (incoherent) rays of uninstanced scenes, else bands
+                                  // -1 auto: refill for dome-light (incoherent) rays, else bands
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
 static int g_chain_mb = 16384;    // chain scratch per stream (MB); larger frames run in chunks of work items
@@ -1157,7 +1167,9 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         int g = std::max(1, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(sf), 0)));
         bool dome = false;
         for (const DevLight& l : s.lights) dome |= l.type == MRT_DOME_LIGHT;
-        int sched = g_shadow_sched >= 0 ? g_shadow_sched : (dome && !inst ? 2 : 1), refill = g_refill_min;
+        // lane refill for dome-light (incoherent) rays: D1 -7%, C5 -13% shade pass; coherent
+        // area-light rays keep the bands (C4: refill +9%)
+        int sched = g_shadow_sched >= 0 ? g_shadow_sched : (dome ? 2 : 1), refill = g_refill_min;
         if (sched && (g & 7)) g &= ~7;          // XCD bands need a whole number of workgroups per XCD
         if (g < 8) sched = 0;
         size_t n_rays = slots * (size_t)max_sh;

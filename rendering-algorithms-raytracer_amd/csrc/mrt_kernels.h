@@ -561,6 +561,106 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
     return false;
 }
 
+// Resumable any-hit step over the world hierarchy AND the instance BLASes
+// (special-leaf scenes: ProxyObject, alpha-mapped and motion-blurred lanes),
+// for the lane-refill schedule of shadow_kernel.  An any-hit answer does not
+// depend on the visit order -- it is "some triangle of the leaves whose boxes
+// all pass with tMax is accepted", a set fixed by the ray -- so the proxy lanes
+// of a world leaf are deferred: pushed as stack entries (-2 - instance).
+// Popping one enters the instance: its object-space ray (object_ray) becomes
+// the lane's current ray, a -1 entry below the BLAS root marks the return to
+// the world ray.  Every box and triangle test is traverse_impl's.
+struct AnyState {
+    int32_t cur;   // node to visit; -1: leave the instance; <= -2: enter instance -2 - cur
+    int sp;
+    int inst;      // -1: world ray
+    DRay ro;       // object-space ray of `inst`
+};
+template <bool COUNT, bool FAST>
+__device__ __forceinline__ bool anyhit_step_inst(const Trav& c, const DRay& r, float tMin, float tMax, AnyState& s,
+                                                 bool& hit, TravStats& st) {
+    if (s.cur < 0) {
+        if (s.cur == -1) {
+            s.inst = -1;
+        } else {
+            const int i = -2 - s.cur;
+            s.ro = object_ray(c.inst[i], r, c.rcpT);
+            if (!stk_push(c, s.sp, -1)) { st.overflow = true; return true; }
+            s.inst = i;
+            s.cur = c.inst[i].root;
+            return false;
+        }
+        if (s.sp == 0) return true;
+        s.cur = stk_pop(c, s.sp);
+        return false;
+    }
+    const bool in_blas = s.inst >= 0;
+    DRay q;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        q.o[k] = in_blas ? s.ro.o[k] : r.o[k];
+        q.d[k] = in_blas ? s.ro.d[k] : r.d[k];
+        q.id[k] = in_blas ? s.ro.id[k] : r.id[k];
+    }
+    q.finite = in_blas ? s.ro.finite : r.finite;
+    q.time = r.time;
+    const float4* qn = reinterpret_cast<const float4*>(c.nodes + s.cur);
+    const int4 ch = reinterpret_cast<const int4*>(qn)[6];
+    const int m = (FAST && q.finite) ? box_test_fast(qn, q, tMin, tMax) : box_test(qn, q, tMin, tMax);
+    if (COUNT) st.nodes++;
+    const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
+    const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
+                       (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
+    const int inner = m & isinner;
+    int lm = m & isleaf;
+    bool have_next = false;
+    int32_t nxt = 0;
+    if (inner) {
+        const int top = 31 - __builtin_clz((unsigned)inner);
+        const int rest = inner ^ (1 << top);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if ((rest >> i) & 1)
+                if (!stk_push(c, s.sp, sel4(ch, i))) { st.overflow = true; return true; }
+        if (COUNT && s.sp > st.max_sp) st.max_sp = s.sp;
+        nxt = sel4(ch, top);
+        have_next = true;
+    }
+    while (lm) {
+        const int sl = __builtin_ctz((unsigned)lm);
+        lm &= lm - 1;
+        const uint32_t v = ~(uint32_t)sel4(ch, sl);
+        const uint32_t leaf = v >> 4;
+        const int cnt = (int)(v & 3u) + 1;
+        const bool check = (v & 8u) != 0;
+        if (COUNT) st.leaves++;
+        for (int k = 0; k < cnt; k++) {
+            float t, a, b;
+            bool ok;
+            if (v & 4u) {   // proxy lanes (world packets only): deferred instance walks
+                const int32_t pm = c.leaves[leaf].prim[k];
+                if (pm <= -2) {
+                    if (!stk_push(c, s.sp, pm)) { st.overflow = true; return true; }
+                    continue;
+                }
+            }
+            if (check) {
+                const int32_t pm = c.leaves[leaf].prim[k];
+                ok = (pm >= 0 && c.pflags && (c.pflags[pm] & 1u)) ? mb_tri_test(c, pm, q, tMin, tMax, t, a, b)
+                                                                : tri_test(c.leaves[leaf].tri[k], q, tMin, tMax, t, a, b, c.rcpT);
+                ok = ok && !alpha_rejects(c, leaf, k, a, b);
+            } else {
+                ok = tri_test(c.leaves[leaf].tri[k], q, tMin, tMax, t, a, b, c.rcpT);
+            }
+            if (ok) { hit = true; return true; }
+        }
+    }
+    if (have_next) { s.cur = nxt; return false; }
+    if (s.sp == 0) return true;
+    s.cur = stk_pop(c, s.sp);
+    return false;
+}
+
 // FAST (node boxes known finite) uses the hardware min/max slab test for rays
 // whose origin and 1/d are finite; any other ray takes the exact loop.  A
 // closest hit's packed slot is resolved to the global prim id here.

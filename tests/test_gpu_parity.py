@@ -360,6 +360,35 @@ def test_c5_instanced_dome_matches_oracle():
     assert exact > 0.99, exact
 
 
+def shadow_schedules(P, cam, W, H):
+    """Frames of one scene under every shadow_kernel schedule (grid-stride, XCD
+    bands, bands + lane refill): the any-hit answers -- and so every bit of the
+    frame and the ray counts -- must not depend on the schedule or on the deferred
+    instance walks of the lane-refill step."""
+    L = miro.lib()
+    out = []
+    try:
+        for sched in (0, 1, 2):
+            assert L.mrt_set_tuning(b"shadow_sched", sched) == 0
+            img, hits = render(P, cam, W, H)
+            out.append((img, hits, P.last_stats))
+    finally:
+        L.mrt_set_tuning(b"shadow_sched", -1)
+    img0, hits0, st0 = out[0]
+    for img, hits, st in out[1:]:
+        assert np.array_equal(hits0["prim"], hits["prim"])
+        assert np.array_equal(bits(img0.rgb), bits(img.rgb))
+        assert np.array_equal(img0.pixels, img.pixels)
+        assert st0["shadow_rays"] == st["shadow_rays"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key,W,H", [("C4", 120, 68), ("D1", 96, 96), ("C5", 128, 72)])
+def test_shadow_schedules_give_identical_frames(key, W, H):
+    P, _, cam = config_scene(key)
+    shadow_schedules(P, cam, W, H)
+
+
 @pytest.mark.parametrize("key,W,H", [("C4", 120, 68), ("D1", 96, 96), ("C5", 96, 54)])
 def test_wavefront_shadow_pass_equals_fused_kernel(key, W, H):
     """Kernel 2a/2b/2c (shadow rays written, traced any-hit in a separate launch,

@@ -288,3 +288,14 @@ def test_obj_leaf_with_alpha_map_matches_oracle():
     cam = dict(eye=(0.0, 3.0, 0.5), lookAt=(0.0, 0.0, 0.0), up=(0, 0, -1), fov=60.0)
     ref = gpu_vs_oracle(P, Osc, cam, 64, 64)
     assert ((ref["hits"]["prim"] >= 36) & (ref["hits"]["prim"] < 38)).any()
+
+
+@pytest.mark.gpu
+def test_alpha_leaves_shadow_schedules_give_identical_frames():
+    """The lane-refill any-hit step of special-leaf scenes (anyhit_step_inst)
+    applies the alpha test like the traversal of the other schedules."""
+    from test_gpu_parity import shadow_schedules
+    lights = [dict(type="rect", v1=(3.0, 5.4, -2.5), v2=(3.0, 5.4, -3.0), v3=(2.5, 5.4, -2.5), power=15.0,
+                   samples=4, noise=0.001)]
+    P, _, cam = leaves_scene(lights=lights)
+    shadow_schedules(P, cam, 64, 48)
