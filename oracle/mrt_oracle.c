@@ -228,6 +228,7 @@ struct oro_scene {
     qleaf* ql; int n_ql;
     int built;
     int is_blas;                      /* a ProxyObject's BVH (sub-scene borrowing the meshes) */
+    const struct oro_scene* parent;   /* BLAS: the scene whose meshes, materials and maps it uses */
 };
 
 oro_scene* oro_scene_create(void) {
@@ -1050,6 +1051,7 @@ int oro_scene_make_blas(oro_scene* s, const int* meshes, int n_meshes) {
     if (n <= 0) return -1;
     oro_scene* b = (oro_scene*)calloc(1, sizeof(oro_scene));
     b->is_blas = 1;
+    b->parent = s;
     b->meshes = s->meshes; b->n_meshes = s->n_meshes;     /* borrowed for the build only */
     b->n_obj = n;
     b->obj_mesh = (int*)malloc(sizeof(int) * n);
@@ -1183,19 +1185,20 @@ static int proxy_intersect(const oro_scene* s, int inst, const ray_t* r, float t
     return hit < 0 ? hit : 0;
 }
 
-/* intersect4, src/BVH.cpp:1298-1459: proxy (checkOut) lanes first, in lane
- * order (:1305-1315), then the packet's triangles against the updated t.
- * No motion blur / alpha maps on this path. */
-/* Material::m_alphaMap of object o's triangle (-1: none; ProxyObject lanes and
- * BLAS sub-scenes have none) */
+/* Material::m_alphaMap of object o's triangle (-1: none; ProxyObject lanes have
+ * none).  A BLAS sub-scene's objects are triangles of its parent's meshes, with
+ * their materials: the alpha test applies inside instances too (the reference's
+ * tree proxies carry alpha-mapped leaves, src/main.cpp:240-274). */
 static int lane_alpha_map(const oro_scene* s, int o) {
-    if (o < 0 || !s->maps || s->obj_inst[o] >= 0) return -1;
-    return s->maps[s->meshes[s->obj_mesh[o]].material][5];
+    const oro_scene* ms = s->is_blas ? s->parent : s;
+    if (o < 0 || !ms->maps || (!s->is_blas && s->obj_inst[o] >= 0)) return -1;
+    return ms->maps[ms->meshes[s->obj_mesh[o]].material][5];
 }
 /* getLookupAlpha at the lane's (u, v): interpolated texture coordinates, or
  * (a, b) for a mesh without them (src/BVH.cpp:1401-1423) */
 static float lane_alpha(const oro_scene* s, int map, int o, float a, float b) {
-    const mesh_t* m = &s->meshes[s->obj_mesh[o]];
+    const oro_scene* ms = s->is_blas ? s->parent : s;
+    const mesh_t* m = &ms->meshes[s->obj_mesh[o]];
     const int t = s->obj_tri[o];
     const float c = 1.0f - a - b;
     float u = a, v = b;
@@ -1205,10 +1208,12 @@ static float lane_alpha(const oro_scene* s, int map, int o, float a, float b) {
         v = m->uv[2 * ti[0] + 1] * c + m->uv[2 * ti[1] + 1] * a + m->uv[2 * ti[2] + 1] * b;
     }
     float tx[4];
-    tex_lookup4(&s->tex[map], u, v, tx);
+    tex_lookup4(&ms->tex[map], u, v, tx);
     return tx[3];
 }
 
+/* intersect4, src/BVH.cpp:1298-1459: proxy (checkOut) lanes first, in lane
+ * order (:1305-1315), then the packet's triangles against the updated t. */
 static int intersect4(const oro_scene* s, const qleaf* L, const ray_t* r, float tMin, hit_t* h, uint32_t* nv,
                       uint32_t* lv) {
     int proxyIntersect = 0;

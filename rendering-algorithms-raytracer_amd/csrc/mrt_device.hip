@@ -59,7 +59,10 @@ void set_error(const std::string& m) { g_err = m; }
 // any-hit answer does not depend on), so the answers are identical under
 // every schedule.
 static constexpr int kShadowChunk = 64;
-template <bool COUNT, bool FAST, bool INST>
+// REFILL: sched 2 (its own kernel, so the chunked schedules' nested traversal
+// does not set its register budget); CHECK: the lane-refill step of a
+// special-leaf scene handles alpha-mapped / motion-blurred lanes.
+template <bool COUNT, bool FAST, bool INST, bool REFILL, bool CHECK>
 __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_rays, int sched, int refill_min) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -90,43 +93,42 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
         P.occl[e] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
         return st.nodes - n0;
     };
-    if (sched == 0) {
-        for (size_t e0 = (size_t)blockIdx.x * kWG + (tid & ~63); e0 < n_rays; e0 += (size_t)gridDim.x * kWG) {
-            const size_t e = e0 + lane;
-            uint32_t v = valid(e) ? trace_one(e) : 0u;
-            if (COUNT) {
-                for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off));
-                wave_steps += v;
+    // per-XCD band of ray slots and its chunk counter (own 128-B line)
+    const int home = blockIdx.x & 7;
+    auto band_lo = [&](int k) { return n_rays * (size_t)k / 8; };
+    int band = home, probes = 0;
+    // wave-level dequeue of `want` consecutive slots of the current band (or
+    // the next band with slots left); returns the first slot (lane 0's atomic,
+    // broadcast) and the end of its band, or exhausted
+    auto dequeue = [&](uint32_t want, size_t& first, size_t& end) {
+        unsigned long long got = ~0ull, hi = 0;
+        if (lane == 0) {
+            while (probes < 8) {
+                const size_t lo = band_lo(band), bend = band_lo(band + 1);
+                const unsigned long long v = atomicAdd(reinterpret_cast<unsigned long long*>(P.queue + band * 32),
+                                                       (unsigned long long)want);
+                if (lo + v < bend) { got = lo + v; hi = bend; break; }
+                band = (band + 1) & 7;
+                probes++;
             }
         }
-    } else {
-        // per-XCD band of ray slots and its chunk counter (own 128-B line)
-        const int home = blockIdx.x & 7;
-        auto band_lo = [&](int k) { return n_rays * (size_t)k / 8; };
-        int band = home, probes = 0;
-        bool exhausted = false;   // wave-uniform
-        // wave-level dequeue of `want` consecutive slots of the current band (or
-        // the next band with slots left); returns the first slot (lane 0's atomic,
-        // broadcast) and the end of its band, or exhausted
-        auto dequeue = [&](uint32_t want, size_t& first, size_t& end) {
-            unsigned long long got = ~0ull, hi = 0;
-            if (lane == 0) {
-                while (probes < 8) {
-                    const size_t lo = band_lo(band), bend = band_lo(band + 1);
-                    const unsigned long long v = atomicAdd(reinterpret_cast<unsigned long long*>(P.queue + band * 32),
-                                                           (unsigned long long)want);
-                    if (lo + v < bend) { got = lo + v; hi = bend; break; }
-                    band = (band + 1) & 7;
-                    probes++;
+        got = __shfl(got, 0);
+        hi = __shfl(hi, 0);
+        first = (size_t)got;
+        end = (size_t)hi;
+        return got != ~0ull;
+    };
+    if constexpr (!REFILL) {
+        if (sched == 0) {
+            for (size_t e0 = (size_t)blockIdx.x * kWG + (tid & ~63); e0 < n_rays; e0 += (size_t)gridDim.x * kWG) {
+                const size_t e = e0 + lane;
+                uint32_t v = valid(e) ? trace_one(e) : 0u;
+                if (COUNT) {
+                    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off));
+                    wave_steps += v;
                 }
             }
-            got = __shfl(got, 0);
-            hi = __shfl(hi, 0);
-            first = (size_t)got;
-            end = (size_t)hi;
-            return got != ~0ull;
-        };
-        if (sched == 1) {   // wave-uniform chunks, one ray per lane
+        } else {   // XCD bands: wave-uniform chunks, one ray per lane
             size_t first, end;
             while (dequeue(kShadowChunk, first, end)) {
                 const size_t e = first + lane;
@@ -136,53 +138,49 @@ __global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_ra
                     wave_steps += v;
                 }
             }
-        } else {   // lane refill
-            bool active = false;
-            size_t e = 0;
-            DRay r{};
-            float tmax = 0.f;
-            int32_t cur = 0;
-            int sp = 0;
-            AnyState as{};
-            for (;;) {
-                const unsigned long long idle = __ballot(!active);
-                const int nidle = __popcll(idle);
-                if (!exhausted && (nidle >= refill_min || nidle == 64)) {
-                    size_t first, end;
-                    if (!dequeue((uint32_t)nidle, first, end)) {
-                        exhausted = true;
-                    } else if (!active) {
-                        const size_t c = first + (size_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                        if (c < end && valid(c)) {
-                            e = c;
-                            const float4 o = P.ray_o[e], d = P.ray_d[e];
-                            r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
-                            tmax = o.w;
-                            cur = 0;
-                            sp = 0;
-                            as.cur = 0;
-                            as.sp = 0;
-                            as.inst = -1;
-                            active = true;
-                        }
+        }
+    } else {   // lane refill
+        bool exhausted = false;   // wave-uniform
+        bool active = false;
+        size_t e = 0;
+        float tmax = 0.f;
+        AnyState as{};
+        for (;;) {
+            const unsigned long long idle = __ballot(!active);
+            const int nidle = __popcll(idle);
+            if (!exhausted && (nidle >= refill_min || nidle == 64)) {
+                size_t first, end;
+                if (!dequeue((uint32_t)nidle, first, end)) {
+                    exhausted = true;
+                } else if (!active) {
+                    const size_t c = first + (size_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    if (c < end && valid(c)) {
+                        e = c;
+                        const float4 o = P.ray_o[e], d = P.ray_d[e];
+                        as.q = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
+                        tmax = o.w;
+                        as.cur = 0;
+                        as.sp = 0;
+                        as.aoff = -1;
+                        active = true;
                     }
                 }
-                if (__ballot(active) == 0) {
-                    if (exhausted) break;
-                    continue;
-                }
-                if (COUNT) wave_steps++;
-                if (active) {
-                    bool hit = false;
-                    bool done;
-                    if constexpr (INST) done = anyhit_step_inst<COUNT, FAST>(T, r, 0.001f, tmax, as, hit, st);
-                    else done = (FAST && r.finite) ? anyhit_step<COUNT, true>(T, r, 0.001f, tmax, cur, sp, hit, st)
-                                                   : anyhit_step<COUNT, false>(T, r, 0.001f, tmax, cur, sp, hit, st);
-                    if (done) {
-                        P.occl[e] = hit ? 1 : 0;
-                        active = false;
-                    }
+            }
+            if (__ballot(active) == 0) {
+                if (exhausted) break;
+                continue;
+            }
+            if (COUNT) wave_steps++;
+            if (active) {
+                bool hit = false;
+                bool done;
+                if constexpr (INST) done = anyhit_step_inst<COUNT, FAST, CHECK>(T, 0.001f, tmax, as, P.ray_o, P.ray_d, e, hit, st);
+                else done = (FAST && as.q.finite) ? anyhit_step<COUNT, true>(T, as.q, 0.001f, tmax, as.cur, as.sp, hit, st)
+                                                  : anyhit_step<COUNT, false>(T, as.q, 0.001f, tmax, as.cur, as.sp, hit, st);
+                if (done) {
+                    P.occl[e] = hit ? 1 : 0;
+                    active = false;
                 }
             }
         }
@@ -456,7 +454,7 @@ struct DeviceState {
 // Tuning knobs (mrt_set_tuning): A/B switches for performance work.
 static int g_fast_box = 1;        // hardware min/max box test when its precondition holds
 static int g_primary_waves = 7;   // launch-bounds occupancy target of the primary kernel: 0 (none), 6, 7, 8
-static int g_shade_waves = 6;     // same for shade1_kernel: 6, 7, 8
+static int g_shade_waves = 5;     // same for shade1_kernel: 1 (none), 4..8 (5: 96 VGPRs, 64 B spill; -2.5% vs 6)
 static int g_lds_pad_kb = 0;      // extra dynamic LDS per workgroup (occupancy sweeps)
 static int g_sched = 2;           // TileSched mode 0..3 (2 measured fastest)
 static int g_order = 0;           // frame-mode tile dequeue order (0 bottom-up, 1 top-down)
@@ -657,7 +655,7 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     std::vector<QNode> DN;
     std::vector<DLeaf> DL;
     auto append = [&](const std::vector<QNode>& nodes, const std::vector<QLeaf>& leaves,
-                      const std::vector<int32_t>* oi) -> int32_t {
+                      const std::vector<int32_t>* oi, const Blas* B) -> int32_t {
         const int32_t nb = (int32_t)DN.size(), lb = (int32_t)DL.size();
         auto proxy_of = [&](int32_t p) { return (oi && p >= 0 && (size_t)p < oi->size()) ? (*oi)[p] : -1; };
         for (QNode q : nodes) {
@@ -673,7 +671,9 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
                         cnt = j + 1;
                         proxy |= proxy_of(L.prim[j]) >= 0;
                         alpha |= oi != nullptr && proxy_of(L.prim[j]) < 0 &&
-                                 (alpha_obj(L.prim[j]) || mb_obj(L.prim[j]));   // world leaves only
+                                 (alpha_obj(L.prim[j]) || mb_obj(L.prim[j]));   // world: alpha / motion blur
+                        alpha |= B != nullptr && (size_t)L.prim[j] < B->obj_mesh.size() &&
+                                 alpha_mat[(size_t)s.meshes[B->obj_mesh[(size_t)L.prim[j]]].material];   // BLAS: alpha
                     }
                 d.has_alpha |= alpha;
                 q.child[k] = leaf_child((uint32_t)(~c + lb), cnt < 1 ? 1 : cnt, proxy, alpha);
@@ -691,9 +691,9 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
         }
         return nb;
     };
-    append(s.nodes, s.leaves, &s.obj_inst);
+    append(s.nodes, s.leaves, &s.obj_inst, nullptr);
     std::vector<int32_t> blas_root(s.blas.size());
-    for (size_t b = 0; b < s.blas.size(); b++) blas_root[b] = append(s.blas[b].nodes, s.blas[b].leaves, nullptr);
+    for (size_t b = 0; b < s.blas.size(); b++) blas_root[b] = append(s.blas[b].nodes, s.blas[b].leaves, nullptr, &s.blas[b]);
     if ((rc = upload(d.nodes, DN.data(), DN.size() * sizeof(QNode), total))) return rc;
     std::vector<DevInstance> DI(s.instances.size());
     for (size_t i = 0; i < DI.size(); i++) {
@@ -947,6 +947,9 @@ static KernelFn shade1_fn(bool c, bool f) {
 }
 static KernelFn pick_shade1(int w, bool c, bool f) {
     switch (w) {
+        case 1: return shade1_fn<1>(c, f);
+        case 4: return shade1_fn<4>(c, f);
+        case 5: return shade1_fn<5>(c, f);
         case 7: return shade1_fn<7>(c, f);
         case 8: return shade1_fn<8>(c, f);
         default: return shade1_fn<6>(c, f);
@@ -959,11 +962,15 @@ static KernelFn shade_mode_fn(bool c, bool po, bool inst) {   // kGen / kResolve
     return c ? shade_kernel<true, false, false, false, MODE> : shade_kernel<false, false, false, false, MODE>;
 }
 using ShadowFn = void (*)(RenderParams, size_t, int, int);
-static ShadowFn pick_shadow(bool c, bool f, bool inst) {
-    if (inst) return c ? (f ? shadow_kernel<true, true, true> : shadow_kernel<true, false, true>)
-                       : (f ? shadow_kernel<false, true, true> : shadow_kernel<false, false, true>);
-    return c ? (f ? shadow_kernel<true, true, false> : shadow_kernel<true, false, false>)
-             : (f ? shadow_kernel<false, true, false> : shadow_kernel<false, false, false>);
+template <bool INST, bool REFILL, bool CHECK>
+static ShadowFn shadow_fn(bool c, bool f) {
+    return c ? (f ? shadow_kernel<true, true, INST, REFILL, CHECK> : shadow_kernel<true, false, INST, REFILL, CHECK>)
+             : (f ? shadow_kernel<false, true, INST, REFILL, CHECK> : shadow_kernel<false, false, INST, REFILL, CHECK>);
+}
+static ShadowFn pick_shadow(bool c, bool f, bool inst, bool refill, bool check) {
+    if (!refill) return inst ? shadow_fn<true, false, true>(c, f) : shadow_fn<false, false, false>(c, f);
+    if (!inst) return shadow_fn<false, true, false>(c, f);
+    return check ? shadow_fn<true, true, true>(c, f) : shadow_fn<true, true, false>(c, f);
 }
 // shadow rays per pixel at most: num_paths x (1 per point light, m_numSamples per area / dome light)
 static int max_shadow_rays(const Scene& s) {
@@ -1163,15 +1170,18 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         P.nrays = c.nrays;
         P.max_shadow = max_sh;
         if ((rc = launch(shade_mode_fn<kGen>(count, d.point_only, inst)))) return rc;
-        const ShadowFn sf = pick_shadow(count, fb, inst);
-        int g = std::max(1, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(sf), 0)));
         bool dome = false;
         for (const DevLight& l : s.lights) dome |= l.type == MRT_DOME_LIGHT;
         // lane refill for dome-light (incoherent) rays: D1 -7%, C5 -13% shade pass; coherent
         // area-light rays keep the bands (C4: refill +9%)
         int sched = g_shadow_sched >= 0 ? g_shadow_sched : (dome ? 2 : 1), refill = g_refill_min;
+        ShadowFn sf = pick_shadow(count, fb, inst, sched == 2, d.has_alpha);
+        int g = std::max(1, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(sf), 0)));
         if (sched && (g & 7)) g &= ~7;          // XCD bands need a whole number of workgroups per XCD
-        if (g < 8) sched = 0;
+        if (g < 8) {                            // too few workgroups for the bands: grid-stride
+            sched = 0;
+            sf = pick_shadow(count, fb, inst, false, d.has_alpha);
+        }
         size_t n_rays = slots * (size_t)max_sh;
         if (n_rays >= (size_t(1) << 32)) { set_error("too many wavefront shadow-ray slots (2^32)"); return MRT_ERR_INVALID; }
         void* args[] = {&P, &n_rays, &sched, &refill};
@@ -2137,7 +2147,7 @@ int mrt_set_tuning(const char* key, int value) {
         if (value != 0 && value != 1 && (value < 6 || value > 8)) { set_error("primary_waves must be 0 or 6..8"); return MRT_ERR_INVALID; }
         g_primary_waves = value;
     } else if (k == "shade_waves") {
-        if (value != 6 && value != 7 && value != 8) { set_error("shade_waves must be 6, 7 or 8"); return MRT_ERR_INVALID; }
+        if (value != 1 && (value < 4 || value > 8)) { set_error("shade_waves must be 1 or 4..8"); return MRT_ERR_INVALID; }
         g_shade_waves = value;
     } else if (k == "scalar_nodes") {
         g_scalar_nodes = value ? 1 : 0;

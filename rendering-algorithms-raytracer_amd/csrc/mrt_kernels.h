@@ -206,9 +206,11 @@ __device__ __noinline__ bool mb_tri_test(const Trav& c, int32_t prim, const DRay
 // hit's (u, v) -- interpolated texture coordinates, or (a, b) without them --
 // is below 0.5.  Such a triangle is skipped; with the lanes walked in slot order
 // and only t < best accepted, the first surviving lane of lowest t wins, as in
-// the reference's t-ordered retry loop.
-__device__ __noinline__ bool alpha_rejects(const Trav& c, uint32_t leaf, int k, float a, float b) {
-    const int32_t prim = c.leaves[leaf].prim[k];
+// the reference's t-ordered retry loop.  aoff: PrimShade index of the leaf's
+// prim 0 (0 in the world; an instance's shade_base inside its BLAS, whose
+// alpha-mapped triangles -- the reference's tree proxies -- are tested too).
+__device__ __noinline__ bool alpha_rejects(const Trav& c, uint32_t leaf, int k, float a, float b, int32_t aoff) {
+    const int32_t prim = c.leaves[leaf].prim[k] + aoff;
     const int am = c.amats[c.aprims[prim].mat].maps[kMapAlpha];
     if (am < 0) return false;
     float u = a, v = b;
@@ -242,9 +244,9 @@ __device__ __forceinline__ DRay object_ray(const DevInstance& I, const DRay& r, 
     return make_ray(o, d, r.time);
 }
 
-template <bool ANY, bool COUNT, bool FAST, bool INST = false>
+template <bool ANY, bool COUNT, bool FAST, bool INST = false, bool BL = false>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root = 0,
-                              int sp0 = 0);
+                              int sp0 = 0, int32_t aoff = 0);
 
 // One ProxyObject lane: its BLAS traversed with the object-space ray, the
 // current t as tMax, on the same stack above the caller's entries.
@@ -253,8 +255,9 @@ __device__ __forceinline__ bool proxy_hit(const Trav& c, int inst, const DRay& r
                                           TravStats& st, int sp) {
     const DevInstance& I = c.inst[inst];
     const DRay ro = object_ray(I, r, c.rcpT);
-    if (FAST && ro.finite) return traverse_impl<ANY, COUNT, true, false>(c, ro, tMin, h, st, I.root, sp);
-    return traverse_impl<ANY, COUNT, false, false>(c, ro, tMin, h, st, I.root, sp);
+    // BLAS packets with alpha-mapped triangles (check bit): PrimShade = shade_base + BLAS object
+    if (FAST && ro.finite) return traverse_impl<ANY, COUNT, true, false, true>(c, ro, tMin, h, st, I.root, sp, I.shade_base);
+    return traverse_impl<ANY, COUNT, false, false, true>(c, ro, tMin, h, st, I.root, sp, I.shade_base);
 }
 
 // BVH::intersect, QBVH branch (src/BVH.cpp:1128-1178).  Returns hit; h.prim is
@@ -272,9 +275,11 @@ __device__ __forceinline__ bool proxy_hit(const Trav& c, int inst, const DRay& r
 // INST: leaf packets with ProxyObject lanes (child-word bit 2) intersect those
 // lanes first, in lane order (intersect4, src/BVH.cpp:1305-1315), each through
 // a nested BLAS traversal (proxy_hit); root / sp0 start such a nested walk.
-template <bool ANY, bool COUNT, bool FAST, bool INST>
+// INST / BL (a BLAS walk): packets with the check bit (3) test alpha-mapped
+// lanes -- and, in the world, motion-blurred ones.
+template <bool ANY, bool COUNT, bool FAST, bool INST, bool BL>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root,
-                              int sp0) {
+                              int sp0, int32_t aoff) {
     int sp = sp0;
     int32_t cur = root;
     bool hit = false;
@@ -349,7 +354,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                     leaf = v >> 4;
                     cnt = (int)(v & 3u) + 1;
                     k = 0;
-                    check = INST && (v & 8u);
+                    check = (INST || BL) && (v & 8u);
                     if (COUNT) st.leaves++;
                     if (INST && (v & 4u)) {
                         for (int j = 0; j < cnt; j++) {
@@ -368,11 +373,12 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                 }
                 float t, a, b;
                 bool ok;
-                if (INST && check) {   // alpha-mapped / motion-blurred lanes
+                if ((INST || BL) && check) {   // alpha-mapped / motion-blurred lanes
                     const int32_t pm = c.leaves[leaf].prim[k];
-                    ok = (pm >= 0 && c.pflags && (c.pflags[pm] & 1u)) ? mb_tri_test(c, pm, r, tMin, h.t, t, a, b)
-                                                          : tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT);
-                    ok = ok && !alpha_rejects(c, leaf, k, a, b);
+                    ok = (!BL && pm >= 0 && c.pflags && (c.pflags[pm] & 1u))
+                             ? mb_tri_test(c, pm, r, tMin, h.t, t, a, b)
+                             : tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT);
+                    ok = ok && !alpha_rejects(c, leaf, k, a, b, aoff);
                 } else {
                     ok = tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT);
                 }
@@ -567,43 +573,39 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
 // depend on the visit order -- it is "some triangle of the leaves whose boxes
 // all pass with tMax is accepted", a set fixed by the ray -- so the proxy lanes
 // of a world leaf are deferred: pushed as stack entries (-2 - instance).
-// Popping one enters the instance: its object-space ray (object_ray) becomes
-// the lane's current ray, a -1 entry below the BLAS root marks the return to
-// the world ray.  Every box and triangle test is traverse_impl's.
+// Proxy entries are pushed, and so popped, in the world context; popping one
+// enters the instance: the lane's ray becomes its object-space ray
+// (object_ray) and a -1 entry below the BLAS root marks the return, where the
+// world ray is rebuilt from its slot (one ray in registers, not two).  Every
+// box and triangle test is traverse_impl's.  CHECK: the scene has alpha-mapped
+// or motion-blurred lanes (child-word bit 3).
 struct AnyState {
+    DRay q;        // the current ray: the world ray, or the object-space ray inside an instance
     int32_t cur;   // node to visit; -1: leave the instance; <= -2: enter instance -2 - cur
     int sp;
-    int inst;      // -1: world ray
-    DRay ro;       // object-space ray of `inst`
+    int32_t aoff;  // -1 in the world, else the instance's shade_base (alpha lanes of its BLAS)
 };
-template <bool COUNT, bool FAST>
-__device__ __forceinline__ bool anyhit_step_inst(const Trav& c, const DRay& r, float tMin, float tMax, AnyState& s,
-                                                 bool& hit, TravStats& st) {
+template <bool COUNT, bool FAST, bool CHECK>
+__device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, float tMax, AnyState& s,
+                                                 const float4* ray_o, const float4* ray_d, size_t e, bool& hit,
+                                                 TravStats& st) {
     if (s.cur < 0) {
-        if (s.cur == -1) {
-            s.inst = -1;
-        } else {
-            const int i = -2 - s.cur;
-            s.ro = object_ray(c.inst[i], r, c.rcpT);
-            if (!stk_push(c, s.sp, -1)) { st.overflow = true; return true; }
-            s.inst = i;
-            s.cur = c.inst[i].root;
+        if (s.cur == -1) {   // back to the world ray
+            const float4 o = ray_o[e], d = ray_d[e];
+            s.q = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
+            s.aoff = -1;
+            if (s.sp == 0) return true;
+            s.cur = stk_pop(c, s.sp);
             return false;
         }
-        if (s.sp == 0) return true;
-        s.cur = stk_pop(c, s.sp);
+        const int i = -2 - s.cur;
+        if (!stk_push(c, s.sp, -1)) { st.overflow = true; return true; }
+        s.q = object_ray(c.inst[i], s.q, c.rcpT);
+        s.cur = c.inst[i].root;
+        s.aoff = c.inst[i].shade_base;
         return false;
     }
-    const bool in_blas = s.inst >= 0;
-    DRay q;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        q.o[k] = in_blas ? s.ro.o[k] : r.o[k];
-        q.d[k] = in_blas ? s.ro.d[k] : r.d[k];
-        q.id[k] = in_blas ? s.ro.id[k] : r.id[k];
-    }
-    q.finite = in_blas ? s.ro.finite : r.finite;
-    q.time = r.time;
+    const DRay& q = s.q;
     const float4* qn = reinterpret_cast<const float4*>(c.nodes + s.cur);
     const int4 ch = reinterpret_cast<const int4*>(qn)[6];
     const int m = (FAST && q.finite) ? box_test_fast(qn, q, tMin, tMax) : box_test(qn, q, tMin, tMax);
@@ -618,11 +620,20 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, const DRay& r, f
     if (inner) {
         const int top = 31 - __builtin_clz((unsigned)inner);
         const int rest = inner ^ (1 << top);
+        if (rest) {
+            if (s.sp + 4 <= kLdsStack) {
+                c.lds[s.sp * kWG] = ch.x; s.sp += rest & 1;
+                c.lds[s.sp * kWG] = ch.y; s.sp += (rest >> 1) & 1;
+                c.lds[s.sp * kWG] = ch.z; s.sp += (rest >> 2) & 1;
+                c.lds[s.sp * kWG] = ch.w; s.sp += (rest >> 3) & 1;
+            } else {
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-            if ((rest >> i) & 1)
-                if (!stk_push(c, s.sp, sel4(ch, i))) { st.overflow = true; return true; }
-        if (COUNT && s.sp > st.max_sp) st.max_sp = s.sp;
+                for (int i = 0; i < 4; i++)
+                    if ((rest >> i) & 1)
+                        if (!stk_push(c, s.sp, sel4(ch, i))) { st.overflow = true; return true; }
+            }
+            if (COUNT && s.sp > st.max_sp) st.max_sp = s.sp;
+        }
         nxt = sel4(ch, top);
         have_next = true;
     }
@@ -632,11 +643,8 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, const DRay& r, f
         const uint32_t v = ~(uint32_t)sel4(ch, sl);
         const uint32_t leaf = v >> 4;
         const int cnt = (int)(v & 3u) + 1;
-        const bool check = (v & 8u) != 0;
         if (COUNT) st.leaves++;
         for (int k = 0; k < cnt; k++) {
-            float t, a, b;
-            bool ok;
             if (v & 4u) {   // proxy lanes (world packets only): deferred instance walks
                 const int32_t pm = c.leaves[leaf].prim[k];
                 if (pm <= -2) {
@@ -644,11 +652,14 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, const DRay& r, f
                     continue;
                 }
             }
-            if (check) {
+            float t, a, b;
+            bool ok;
+            if (CHECK && (v & 8u)) {   // world: alpha / motion blur; BLAS: alpha
                 const int32_t pm = c.leaves[leaf].prim[k];
-                ok = (pm >= 0 && c.pflags && (c.pflags[pm] & 1u)) ? mb_tri_test(c, pm, q, tMin, tMax, t, a, b)
-                                                                : tri_test(c.leaves[leaf].tri[k], q, tMin, tMax, t, a, b, c.rcpT);
-                ok = ok && !alpha_rejects(c, leaf, k, a, b);
+                ok = (s.aoff < 0 && pm >= 0 && c.pflags && (c.pflags[pm] & 1u))
+                         ? mb_tri_test(c, pm, q, tMin, tMax, t, a, b)
+                         : tri_test(c.leaves[leaf].tri[k], q, tMin, tMax, t, a, b, c.rcpT);
+                ok = ok && !alpha_rejects(c, leaf, k, a, b, s.aoff < 0 ? 0 : s.aoff);
             } else {
                 ok = tri_test(c.leaves[leaf].tri[k], q, tMin, tMax, t, a, b, c.rcpT);
             }

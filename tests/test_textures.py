@@ -299,3 +299,68 @@ def test_alpha_leaves_shadow_schedules_give_identical_frames():
                    samples=4, noise=0.001)]
     P, _, cam = leaves_scene(lights=lights)
     shadow_schedules(P, cam, 64, 48)
+
+
+# ------------------------------------------------------------------ alpha inside instances
+def leaf_instances(alpha_img, lights=None):
+    """The leaf OBJ as a ProxyObject BLAS with an alpha-mapped material, six
+    overlapping instances at three heights (the reference's tree proxies carry
+    alpha-mapped leaves inside their BLAS, src/main.cpp:240-274)."""
+    img, typ = leaf_image()
+    leaf = dict(kind="blinn", kd=(1, 1, 1), translucency=0.4, specExp=8.0, specAmt=0.3,
+                maps=dict(color=(img, typ), alpha=(alpha_img, typ)))
+    cfg = dict(scenes.CONFIGS["C1"], material=leaf)
+    placed = []
+    for i in range(6):
+        a = 0.9 * i
+        c, s = np.cos(a), np.sin(a)
+        sc = 0.55 + 0.05 * i
+        placed.append((0, np.array([[c * sc, 0, s * sc, 0.45 * np.cos(2.1 * i)], [0, sc, 0, 0.25 * (i % 3)],
+                                    [-s * sc, 0, c * sc, 0.45 * np.sin(2.1 * i)], [0, 0, 0, 1]], np.float32)))
+    lights = lights or [dict(type="point", pos=(0.5, 4.0, 0.5), power=30.0),
+                        dict(type="rect", v1=(-0.5, 3.0, -0.5), v2=(0.5, 3.0, -0.5), v3=(-0.5, 3.0, 0.5), power=20.0,
+                             samples=3, noise=0.001)]
+    return scene_pair(cfg, instances=([LEAF_OBJ], placed), lights=lights)
+
+
+LEAF_CAM = dict(eye=(0.0, 3.0, 0.5), lookAt=(0.0, 0.0, 0.0), up=(0, 0, -1), fov=60.0)
+
+
+def test_transparent_alpha_removes_instanced_leaves():
+    img, _ = leaf_image()
+    clear = img.copy(); clear[..., 3] = 0.0
+    _, Oc, _ = leaf_instances(clear)
+    r = Oc.render(LEAF_CAM, 40, 40, threads=4)
+    assert (r["hits"]["prim"] < 0).all()
+    _, Oo, _ = leaf_instances(img)
+    assert (Oo.render(LEAF_CAM, 40, 40, threads=4)["hits"]["prim"] >= 0).mean() > 0.05
+
+
+def test_opaque_alpha_on_instanced_leaves_hits_every_quad_pixel():
+    """An opaque map keeps every instanced quad; the real map cuts holes through
+    which some rays reach a lower leaf or nothing."""
+    img, _ = leaf_image()
+    opaque = img.copy(); opaque[..., 3] = 1.0
+    _, Oo, _ = leaf_instances(opaque)
+    _, Oa, _ = leaf_instances(img)
+    a, b = Oo.render(LEAF_CAM, 48, 48, threads=4), Oa.render(LEAF_CAM, 48, 48, threads=4)
+    ha, hb = a["hits"]["prim"] >= 0, b["hits"]["prim"] >= 0
+    assert (hb <= ha).all() and hb.sum() < ha.sum()
+    assert not np.array_equal(a["hits"]["t"][hb], b["hits"]["t"][hb])   # some rays pass a hole to a lower leaf
+
+
+@pytest.mark.gpu
+def test_alpha_leaves_inside_instances_match_oracle():
+    need_gpu()
+    img, _ = leaf_image()
+    P, Osc, _ = leaf_instances(img)
+    ref = gpu_vs_oracle(P, Osc, LEAF_CAM, 64, 64)
+    assert (ref["hits"]["prim"] >= 0).mean() > 0.05
+
+
+@pytest.mark.gpu
+def test_alpha_leaves_inside_instances_shadow_schedules_give_identical_frames():
+    from test_gpu_parity import shadow_schedules
+    img, _ = leaf_image()
+    P, _, _ = leaf_instances(img)
+    shadow_schedules(P, LEAF_CAM, 48, 48)
