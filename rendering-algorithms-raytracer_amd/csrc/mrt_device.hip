@@ -62,8 +62,8 @@ static constexpr int kShadowChunk = 64;
 // REFILL: sched 2 (its own kernel, so the chunked schedules' nested traversal
 // does not set its register budget); CHECK: the lane-refill step of a
 // special-leaf scene handles alpha-mapped / motion-blurred lanes.
-template <bool COUNT, bool FAST, bool INST, bool REFILL, bool CHECK>
-__global__ void __launch_bounds__(kWG) shadow_kernel(RenderParams P, size_t n_rays, int sched, int refill_min) {
+template <bool COUNT, bool FAST, bool INST, bool REFILL, bool CHECK, int MINW = 1>
+__global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_t n_rays, int sched, int refill_min) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     load_tables(P.tables, s_tab, 1024);
@@ -466,6 +466,10 @@ static int g_shade1 = 1;          // specialised shade kernel for one point ligh
 static int g_wavefront = 1;       // general shading: gen / trace / resolve kernels instead of one fused kernel
 static int g_shadow_sched = -1;   // shadow_kernel schedule: 0 grid-stride, 1 XCD bands, 2 bands + lane refill,
                                   // -1 auto: refill for dome-light (incoherent) rays, else bands
+static int g_shadow_waves = 8;    // shadow_kernel launch-bounds occupancy: 1 (none), 7, 8 (8: C4 / C5 -5.5%)
+static int g_primary_inst_waves = 6;   // primary kernel of special-leaf scenes: 1 (none), 5, 6 (6: C5 -5%)
+static int g_resolve_waves = 4;   // resolve pass (kernel 2c) of dome-light scenes: 1 (none), 3 (special-leaf only), 4
+static int g_adapt_refill = 32;   // adaptive_kernel pixel refill: idle lanes that trigger a dequeue (0: tiles; 32: A3 -13%)
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
 static int g_chain_mb = 16384;    // chain scratch per stream (MB); larger frames run in chunks of work items
@@ -932,7 +936,13 @@ static KernelFn primary_fn(bool c, bool f) {
              : (f ? primary_kernel<false, W, true, I> : primary_kernel<false, W, false, I>);
 }
 static KernelFn pick_primary(int w, bool c, bool f, bool inst) {
-    if (inst) return primary_fn<1, true>(c, f);  // instanced scenes: no occupancy bound
+    if (inst) {   // special-leaf scenes (instances: nested BLAS walks)
+        switch (g_primary_inst_waves) {
+            case 5: return primary_fn<5, true>(c, f);
+            case 6: return primary_fn<6, true>(c, f);
+            default: return primary_fn<1, true>(c, f);
+        }
+    }
     switch (w) {
         case 6: return primary_fn<6>(c, f);
         case 7: return primary_fn<7>(c, f);
@@ -955,22 +965,37 @@ static KernelFn pick_shade1(int w, bool c, bool f) {
         default: return shade1_fn<6>(c, f);
     }
 }
+// bound: the resolve pass at its g_resolve_waves occupancy target (~240 VGPRs unbounded)
 template <int MODE>
-static KernelFn shade_mode_fn(bool c, bool po, bool inst) {   // kGen / kResolve: no traversal, FAST unused
+static KernelFn shade_mode_fn(bool c, bool po, bool inst, bool bound = false) {   // kGen / kResolve: no traversal, FAST unused
+    if (!c && MODE == kResolve && bound && g_resolve_waves == 4) {
+        if (inst) return shade_kernel<false, false, false, true, MODE, 0, 4>;
+        return po ? shade_kernel<false, true, false, false, MODE, 0, 4> : shade_kernel<false, false, false, false, MODE, 0, 4>;
+    }
+    if (inst && !c && MODE == kResolve && bound && g_resolve_waves == 3) return shade_kernel<false, false, false, true, MODE, 0, 3>;
     if (inst) return c ? shade_kernel<true, false, false, true, MODE> : shade_kernel<false, false, false, true, MODE>;
     if (po) return c ? shade_kernel<true, true, false, false, MODE> : shade_kernel<false, true, false, false, MODE>;
     return c ? shade_kernel<true, false, false, false, MODE> : shade_kernel<false, false, false, false, MODE>;
 }
 using ShadowFn = void (*)(RenderParams, size_t, int, int);
-template <bool INST, bool REFILL, bool CHECK>
+// MINW: launch-bounds occupancy target of the timed (COUNT = false) variants
+template <bool INST, bool REFILL, bool CHECK, int MINW = 1>
 static ShadowFn shadow_fn(bool c, bool f) {
     return c ? (f ? shadow_kernel<true, true, INST, REFILL, CHECK> : shadow_kernel<true, false, INST, REFILL, CHECK>)
-             : (f ? shadow_kernel<false, true, INST, REFILL, CHECK> : shadow_kernel<false, false, INST, REFILL, CHECK>);
+             : (f ? shadow_kernel<false, true, INST, REFILL, CHECK, MINW> : shadow_kernel<false, false, INST, REFILL, CHECK, MINW>);
 }
-static ShadowFn pick_shadow(bool c, bool f, bool inst, bool refill, bool check) {
-    if (!refill) return inst ? shadow_fn<true, false, true>(c, f) : shadow_fn<false, false, false>(c, f);
-    if (!inst) return shadow_fn<false, true, false>(c, f);
-    return check ? shadow_fn<true, true, true>(c, f) : shadow_fn<true, true, false>(c, f);
+template <bool INST, bool REFILL, bool CHECK>
+static ShadowFn shadow_fn_w(int w, bool c, bool f) {
+    switch (w) {
+        case 7: return shadow_fn<INST, REFILL, CHECK, 7>(c, f);
+        case 8: return shadow_fn<INST, REFILL, CHECK, 8>(c, f);
+        default: return shadow_fn<INST, REFILL, CHECK>(c, f);
+    }
+}
+static ShadowFn pick_shadow(bool c, bool f, bool inst, bool refill, bool check, int w) {
+    if (!refill) return inst ? shadow_fn<true, false, true>(c, f) : shadow_fn_w<false, false, false>(w, c, f);
+    if (!inst) return shadow_fn_w<false, true, false>(w, c, f);
+    return check ? shadow_fn<true, true, true>(c, f) : shadow_fn_w<true, true, false>(w, c, f);
 }
 // shadow rays per pixel at most: num_paths x (1 per point light, m_numSamples per area / dome light)
 static int max_shadow_rays(const Scene& s) {
@@ -1142,6 +1167,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     const bool inst = d.special;   // instances or alpha maps: the special-leaf kernels
     if (P.min_subdivs > 1 || P.max_subdivs > 1) {
         HIP_OK(hipEventRecord(c.evm, stream));   // primary_ms = 0: one launch
+        P.refill_min = g_adapt_refill;
         if ((rc = launch(pick_adaptive(count, d.point_only, fb, inst, d.recursive)))) return rc;
         c.last_was_render = true;
         HIP_OK(hipGetLastError());
@@ -1175,12 +1201,12 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         // lane refill for dome-light (incoherent) rays: D1 -7%, C5 -13% shade pass; coherent
         // area-light rays keep the bands (C4: refill +9%)
         int sched = g_shadow_sched >= 0 ? g_shadow_sched : (dome ? 2 : 1), refill = g_refill_min;
-        ShadowFn sf = pick_shadow(count, fb, inst, sched == 2, d.has_alpha);
+        ShadowFn sf = pick_shadow(count, fb, inst, sched == 2, d.has_alpha, g_shadow_waves);
         int g = std::max(1, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(sf), 0)));
         if (sched && (g & 7)) g &= ~7;          // XCD bands need a whole number of workgroups per XCD
         if (g < 8) {                            // too few workgroups for the bands: grid-stride
             sched = 0;
-            sf = pick_shadow(count, fb, inst, false, d.has_alpha);
+            sf = pick_shadow(count, fb, inst, false, d.has_alpha, g_shadow_waves);
         }
         size_t n_rays = slots * (size_t)max_sh;
         if (n_rays >= (size_t(1) << 32)) { set_error("too many wavefront shadow-ray slots (2^32)"); return MRT_ERR_INVALID; }
@@ -1189,7 +1215,8 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         P.queue = qbase + 24 * 32;
         HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(sf), dim3(g), dim3(kWG), args, 0, stream));
         P.queue = qbase + 16 * 32;
-        if ((rc = launch(shade_mode_fn<kResolve>(count, d.point_only, inst)))) return rc;
+        // dome-light resolve passes run faster at 4 waves (D1 -4%, C5 -1.2 ms), the rect-light one not (C4 +2%)
+        if ((rc = launch(shade_mode_fn<kResolve>(count, d.point_only, inst, dome)))) return rc;
     }
     c.last_was_render = true;
     HIP_OK(hipGetLastError());
@@ -2173,6 +2200,18 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "shadow_sched") {
         if (value < -1 || value > 2) { set_error("shadow_sched must be -1..2"); return MRT_ERR_INVALID; }
         g_shadow_sched = value;
+    } else if (k == "primary_inst_waves") {
+        if (value != 1 && value != 5 && value != 6) { set_error("primary_inst_waves must be 1, 5 or 6"); return MRT_ERR_INVALID; }
+        g_primary_inst_waves = value;
+    } else if (k == "resolve_waves") {
+        if (value != 1 && value != 3 && value != 4) { set_error("resolve_waves must be 1, 3 or 4"); return MRT_ERR_INVALID; }
+        g_resolve_waves = value;
+    } else if (k == "shadow_waves") {
+        if (value != 1 && value != 7 && value != 8) { set_error("shadow_waves must be 1, 7 or 8"); return MRT_ERR_INVALID; }
+        g_shadow_waves = value;
+    } else if (k == "adapt_refill") {
+        if (value < 0 || value > 64) { set_error("adapt_refill must be 0..64"); return MRT_ERR_INVALID; }
+        g_adapt_refill = value;
     } else if (k == "refill_min") {
         if (value < 1 || value > 64) { set_error("refill_min must be 1..64"); return MRT_ERR_INVALID; }
         g_refill_min = value;

@@ -86,6 +86,7 @@ struct RenderParams {
     int32_t prio;                // 1: waves on their final tiles raise their issue priority
     int32_t n_waves;             // waves in this launch (prio heuristic)
     int32_t decline;             // >0: a wave in CU slot s stops taking tiles when fewer than s * decline remain
+    int32_t refill_min;          // adaptive_kernel: 0 tile schedule, > 0 pixel refill at this many idle lanes
     int32_t cus;                 // compute units (slot of a persistent block = blockIdx / cus)
     int32_t scalar_nodes;        // scalar fetch of wave-uniform nodes
     unsigned int* queue;         // 8 tile counters, 32 words apart (sched >= 2)
@@ -1149,8 +1150,8 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
 }
 
 // Kernel 2: Scene::sampleScene shading of the primary hit with shadow rays.
-template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused, int REC = 0>
-__global__ void __launch_bounds__(kWG) shade_kernel(RenderParams P) {
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST = false, int MODE = kFused, int REC = 0, int MINW = 1>
+__global__ void __launch_bounds__(kWG, MINW) shade_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     __shared__ float s_ior[REC ? kIorCap * kWG : 1];
@@ -1239,8 +1240,13 @@ __device__ __forceinline__ float gamma_f(const float* lut, float v) {
 // through Scene::sampleScene (closest hit, shading with inline shadow rays,
 // environment / background on a miss), with the reference's running mean and
 // gamma-space stop test after every level.  Eye ray k of a pixel draws from
-// RNG stream (pixel, k): ray 0 is the 1-spp frame path's ray.  Lanes of a wave
-// stop independently; the wave runs until its last lane is done.
+// RNG stream (pixel, k): ray 0 is the 1-spp frame path's ray.
+// Schedules: P.refill_min == 0: a wave takes an 8x8 tile and runs until its
+// last lane's pixel stops.  P.refill_min > 0 (lane refill): a lane whose pixel
+// has stopped takes the next pixel as soon as refill_min lanes of its wave are
+// idle (pixels dealt in tile order from 8 per-XCD bands), so a wave runs one
+// eye ray per busy lane per step instead of waiting for its slowest pixel.
+// Every pixel's eye rays, draws and sums are the same under both schedules.
 template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST, int REC = 0>
 __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
@@ -1256,70 +1262,78 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
     trav_alpha(T, P);
     TravStats st;
     uint32_t shadow_total = 0, eye_rays = 0, eye_hits = 0, secondary_total = 0;
-    TileSched ts(P, wave, lane);
     uint32_t ntiles = 0;
-    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
-        ntiles++;
-        int x, y;
-        size_t slot;
-        if (!item_pixel(P, item, lane, x, y, slot)) continue;
-        const int f = item_frame(P, item);
+    // the lane's pixel and its running state
+    int x = 0, y = 0, f = 0;
+    size_t slot = 0;
+    uint32_t pixel = 0, seed = 0, sample = 0;
+    v3 result = mk(0, 0, 0), cur = mk(0, 0, 0);
+    int level = 1, i = 0, j = 0;
+    // start pixel `lane_` of work item `item` (false: outside the frame)
+    auto start = [&](int item, int lane_) {
+        if (!item_pixel(P, item, lane_, x, y, slot)) return false;
+        f = item_frame(P, item);
+        seed = P.seed + (uint32_t)f;
+        pixel = (uint32_t)(y * P.cam[f].W + x);
+        sample = 0;
+        result = mk(0, 0, 0);
+        cur = mk(0, 0, 0);
+        level = 1; i = 0; j = 0;
+        return true;
+    };
+    // one eye ray of the lane's pixel; true when the pixel is done (written)
+    auto step = [&]() {
         const CamParams& cam = P.cam[f];
-        const uint32_t seed = P.seed + (uint32_t)f;
-        const uint32_t pixel = (uint32_t)(y * cam.W + x);
-        v3 result = mk(0, 0, 0), cur = mk(0, 0, 0);
-        int level = 1, i = 0, j = 0;
-        bool cut = false;
-        for (uint32_t sample = 0;; sample++) {
-            float x0 = 0.5f, x1 = 0.5f, y0 = 0.5f, y1 = 0.5f;
-            if (level > 1) {
-                const float off = 1.0f / (float)level;
-                x0 = (float)i * off; x1 = (float)(i + 1) * off;
-                y0 = (float)j * off; y1 = (float)(j + 1) * off;
-            }
-            const EyeRay er = eye_ray(cam, seed, x, y, sample * 1024u, x0, x1, y0, y1, rsqT);
-            const v3 d = er.d;
-            const DRay r = make_ray(er.o, d, er.time);
-            DHit h{1e12f, 0.f, 0.f, -1};
-            v3 col;
-            eye_rays++;
-            const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
-            if (sample == 0) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
-            if (hit) {
-                eye_hits++;
-                Shader<POINT_ONLY, FAST, INST, kFused, REC> S{P, T, rcpT, rsqT, st, pixel, 0u, seed, 0, 0u};
-                S.sample = sample;
-                S.time = S.shadow_time = er.time;
-                if constexpr (REC) { S.iorS = s_ior + tid; S.lvl = P.lvl + (blockIdx.x * kWG + tid); }
-                col = S.template shade<COUNT>(r, h);
-                shadow_total += S.shadow_rays;
-                secondary_total += S.secondary;
-            } else if (P.env) {
-                col = scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
-            } else {
-                col = mk(P.bg[0], P.bg[1], P.bg[2]);
-            }
-            if (level == 1) {
-                result = col;
-                level = 2;
-            } else {
-                cur = add(cur, col);
-                if (++j < level) continue;
-                j = 0;
-                if (++i < level) continue;
-                i = 0;
-                const float pre = (float)sum_squares(level - 1), now = (float)(level * level);
-                const v3 nr = scale(add(scale(result, pre), cur), 1.0f / (pre + now));
-                const float tx = gamma_f(P.gammaF, result.x) - gamma_f(P.gammaF, nr.x);
-                const float ty = gamma_f(P.gammaF, result.y) - gamma_f(P.gammaF, nr.y);
-                const float tz = gamma_f(P.gammaF, result.z) - gamma_f(P.gammaF, nr.z);
-                cut = fmaxf(fabsf(tx), fmaxf(fabsf(ty), fabsf(tz))) < P.noise;
-                result = nr;
-                cur = mk(0, 0, 0);
-                level++;
-            }
-            if (!((level <= P.max_subdivs && !cut) || level <= P.min_subdivs)) break;
+        float x0 = 0.5f, x1 = 0.5f, y0 = 0.5f, y1 = 0.5f;
+        if (level > 1) {
+            const float off = 1.0f / (float)level;
+            x0 = (float)i * off; x1 = (float)(i + 1) * off;
+            y0 = (float)j * off; y1 = (float)(j + 1) * off;
         }
+        const EyeRay er = eye_ray(cam, seed, x, y, sample * 1024u, x0, x1, y0, y1, rsqT);
+        const v3 d = er.d;
+        const DRay r = make_ray(er.o, d, er.time);
+        DHit h{1e12f, 0.f, 0.f, -1};
+        v3 col;
+        eye_rays++;
+        const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
+        if (sample == 0) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
+        if (hit) {
+            eye_hits++;
+            Shader<POINT_ONLY, FAST, INST, kFused, REC> S{P, T, rcpT, rsqT, st, pixel, 0u, seed, 0, 0u};
+            S.sample = sample;
+            S.time = S.shadow_time = er.time;
+            if constexpr (REC) { S.iorS = s_ior + tid; S.lvl = P.lvl + (blockIdx.x * kWG + tid); }
+            col = S.template shade<COUNT>(r, h);
+            shadow_total += S.shadow_rays;
+            secondary_total += S.secondary;
+        } else if (P.env) {
+            col = scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
+        } else {
+            col = mk(P.bg[0], P.bg[1], P.bg[2]);
+        }
+        sample++;
+        bool cut = false;
+        if (level == 1) {
+            result = col;
+            level = 2;
+        } else {
+            cur = add(cur, col);
+            if (++j < level) return false;
+            j = 0;
+            if (++i < level) return false;
+            i = 0;
+            const float pre = (float)sum_squares(level - 1), now = (float)(level * level);
+            const v3 nr = scale(add(scale(result, pre), cur), 1.0f / (pre + now));
+            const float tx = gamma_f(P.gammaF, result.x) - gamma_f(P.gammaF, nr.x);
+            const float ty = gamma_f(P.gammaF, result.y) - gamma_f(P.gammaF, nr.y);
+            const float tz = gamma_f(P.gammaF, result.z) - gamma_f(P.gammaF, nr.z);
+            cut = fmaxf(fabsf(tx), fmaxf(fabsf(ty), fabsf(tz))) < P.noise;
+            result = nr;
+            cur = mk(0, 0, 0);
+            level++;
+        }
+        if ((level <= P.max_subdivs && !cut) || level <= P.min_subdivs) return false;
         if (P.out_rgb) {
             float* o = P.out_rgb + 3 * slot;
             o[0] = result.x; o[1] = result.y; o[2] = result.z;
@@ -1327,6 +1341,56 @@ __global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
         if (P.out_rgb8) {
             uint8_t* o8 = P.out_rgb8 + 3 * slot;
             o8[0] = map8(P.gamma, result.x); o8[1] = map8(P.gamma, result.y); o8[2] = map8(P.gamma, result.z);
+        }
+        return true;
+    };
+    if (P.refill_min <= 0) {
+        TileSched ts(P, wave, lane);
+        for (int item = ts.first(); item >= 0; item = ts.next(item)) {
+            ntiles++;
+            if (!start(item, lane)) continue;
+            while (!step()) {}
+        }
+    } else {
+        // pixels p = item * 64 + lane of the work items, dealt from 8 bands (one
+        // counter each, 128 B apart); a wave dequeues as many as it has idle lanes
+        const size_t n_px = (size_t)P.n_tiles * 64;
+        auto band_lo = [&](int k) { return n_px * (size_t)k / 8; };
+        int band = blockIdx.x & 7, probes = 0;
+        bool exhausted = false, active = false;
+        for (;;) {
+            const unsigned long long idle = __ballot(!active);
+            const int nidle = __popcll(idle);
+            if (!exhausted && (nidle >= P.refill_min || nidle == 64)) {
+                unsigned long long got = ~0ull, hi = 0;
+                if (lane == 0) {
+                    while (probes < 8) {
+                        const size_t lo = band_lo(band), bend = band_lo(band + 1);
+                        const unsigned long long v =
+                            atomicAdd(reinterpret_cast<unsigned long long*>(P.queue + band * 32), (unsigned long long)nidle);
+                        if (lo + v < bend) { got = lo + v; hi = bend; break; }
+                        band = (band + 1) & 7;
+                        probes++;
+                    }
+                }
+                got = __shfl(got, 0);
+                hi = __shfl(hi, 0);
+                if (got == ~0ull) {
+                    exhausted = true;
+                } else if (!active) {
+                    const size_t p = (size_t)got + (size_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    if (p < (size_t)hi) {
+                        ntiles++;
+                        active = start((int)(p >> 6), (int)(p & 63));
+                    }
+                }
+            }
+            if (__ballot(active) == 0) {
+                if (exhausted) break;
+                continue;
+            }
+            if (active && step()) active = false;
         }
     }
     unsigned long long er = eye_rays, eh = eye_hits;

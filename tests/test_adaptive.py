@@ -175,3 +175,31 @@ def test_adaptive_bucket_batch_equals_frame():
                                         None, P.handle, stream), "unpack")
     torch.cuda.synchronize()
     assert np.array_equal(bits(frame.cpu().numpy().reshape(H, W, 3)), bits(img.rgb))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("refill", [1, 32, 64])
+def test_adaptive_pixel_refill_equals_tile_schedule(refill):
+    """Lane refill (a lane takes the next pixel when its own has stopped) and the
+    tile schedule give the same frame bit for bit: every pixel's eye rays, draws
+    and running mean are the same, whichever lane runs them."""
+    lights = [dict(type="rect", v1=(3.0, 5.4, -2.5), v2=(3.0, 5.4, -3.0), v3=(2.5, 5.4, -2.5), power=15.0,
+                   samples=3, noise=0.001)]
+    cfg = dict(scenes.CONFIGS["C1"])
+    cfg["material"] = dict(kind="blinn", kd=(0.7, 0.6, 0.5), specExp=12.0, specAmt=0.3)
+    P, _, cam = scene_pair(cfg, meshes=[fixture_mesh("cornell_box")], lights=lights, subdivs=(1, 4, 0.004))
+    L = miro.lib()
+    try:
+        assert L.mrt_set_tuning(b"adapt_refill", 0) == 0
+        img0, hits0 = gpu_render(P, cam, 97, 61)
+        st0 = P.last_stats
+        assert L.mrt_set_tuning(b"adapt_refill", refill) == 0
+        img1, hits1 = gpu_render(P, cam, 97, 61)
+        st1 = P.last_stats
+    finally:
+        L.mrt_set_tuning(b"adapt_refill", 32)
+    assert np.array_equal(hits0["prim"], hits1["prim"])
+    assert np.array_equal(bits(img0.rgb), bits(img1.rgb))
+    assert np.array_equal(img0.pixels, img1.pixels)
+    assert st0["shadow_rays"] == st1["shadow_rays"] > 0
+    assert st0["primary_rays"] == st1["primary_rays"]
