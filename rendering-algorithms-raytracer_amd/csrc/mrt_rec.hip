@@ -14,7 +14,24 @@ KernelFn pick_shade_rec(bool c, bool po, bool f, bool inst, int rec) {
     return pick4<ShadeK, 1>(c, po, f, inst);
 }
 
-KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec) {
+// direct-lighting adaptive kernels (timed variants) at an occupancy target:
+// unbounded, the compiler gives them all 256 VGPRs (one wave per SIMD)
+template <int W>
+static KernelFn adapt_direct(bool po, bool f, bool inst) {
+    if (inst) return f ? adaptive_kernel<false, false, true, true, 0, W> : adaptive_kernel<false, false, false, true, 0, W>;
+    if (po) return f ? adaptive_kernel<false, true, true, false, 0, W> : adaptive_kernel<false, true, false, false, 0, W>;
+    return f ? adaptive_kernel<false, false, true, false, 0, W> : adaptive_kernel<false, false, false, false, 0, W>;
+}
+
+KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec, int waves) {
+    if (rec == 0 && !c) {
+        switch (waves) {
+            case 4: return adapt_direct<4>(po, f, inst);
+            case 5: return adapt_direct<5>(po, f, inst);
+            case 6: return adapt_direct<6>(po, f, inst);
+            default: break;
+        }
+    }
     if (rec == 2) return pick4<AdaptK, 2>(c, po, f, inst);
     if (rec == 1) return pick4<AdaptK, 1>(c, po, f, inst);
     return pick4<AdaptK, 0>(c, po, f, inst);

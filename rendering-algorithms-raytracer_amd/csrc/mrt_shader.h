@@ -1247,8 +1247,8 @@ __device__ __forceinline__ float gamma_f(const float* lut, float v) {
 // idle (pixels dealt in tile order from 8 per-XCD bands), so a wave runs one
 // eye ray per busy lane per step instead of waiting for its slowest pixel.
 // Every pixel's eye rays, draws and sums are the same under both schedules.
-template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST, int REC = 0>
-__global__ void __launch_bounds__(kWG) adaptive_kernel(RenderParams P) {
+template <bool COUNT, bool POINT_ONLY, bool FAST, bool INST, int REC = 0, int MINW = 1>
+__global__ void __launch_bounds__(kWG, MINW) adaptive_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     __shared__ float s_ior[REC ? kIorCap * kWG : 1];
@@ -1423,7 +1423,7 @@ struct ShadeK { static constexpr KernelFn fn = shade_kernel<C, PO, F, I, kFused,
 // defined in mrt_rec.hip: the fused chain kernels (rec 1: reflection / refraction,
 // 2: + path tracing) and the adaptive supersampling kernels (any rec)
 KernelFn pick_shade_rec(bool c, bool po, bool f, bool inst, int rec);
-KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec);
+KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec, int waves);
 // defined in mrt_chain.hip: the wavefront chain engine
 KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec);
 KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec);
