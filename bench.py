@@ -157,7 +157,8 @@ def cpu_baseline(cfg_key, seconds):
                               refractAmt=mat.get("refractAmt", 0.0), ior=mat.get("ior", 1.5),
                               specGloss=mat.get("specGloss", 1.0), translucency=mat.get("translucency", 0.0),
                               le=mat.get("le", (0, 0, 0)), emitted=mat.get("emitted", 0.0),
-                              sampleEnv=mat.get("sampleEnv", True))
+                              sampleEnv=mat.get("sampleEnv", True), disperse=mat.get("disperse", False),
+                              ior3=mat.get("ior3"))
 
     m = material(cfg["material"])
     if cfg["mesh"] == "sponza":

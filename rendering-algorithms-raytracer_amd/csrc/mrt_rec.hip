@@ -16,11 +16,11 @@ KernelFn pick_shade_rec(bool c, bool po, bool f, bool inst, int rec) {
 
 // direct-lighting adaptive kernels (timed variants) at an occupancy target:
 // unbounded, the compiler gives them all 256 VGPRs (one wave per SIMD)
-template <int W>
+template <int W, int REC = 0>
 static KernelFn adapt_direct(bool po, bool f, bool inst) {
-    if (inst) return f ? adaptive_kernel<false, false, true, true, 0, W> : adaptive_kernel<false, false, false, true, 0, W>;
-    if (po) return f ? adaptive_kernel<false, true, true, false, 0, W> : adaptive_kernel<false, true, false, false, 0, W>;
-    return f ? adaptive_kernel<false, false, true, false, 0, W> : adaptive_kernel<false, false, false, false, 0, W>;
+    if (inst) return f ? adaptive_kernel<false, false, true, true, REC, W> : adaptive_kernel<false, false, false, true, REC, W>;
+    if (po) return f ? adaptive_kernel<false, true, true, false, REC, W> : adaptive_kernel<false, true, false, false, REC, W>;
+    return f ? adaptive_kernel<false, false, true, false, REC, W> : adaptive_kernel<false, false, false, false, REC, W>;
 }
 
 KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec, int waves) {
@@ -32,6 +32,7 @@ KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec, int waves) {
             default: break;
         }
     }
+    // (REC 1 / 2 kernels bounded to 2 or 3 waves still end at one: no variants)
     if (rec == 2) return pick4<AdaptK, 2>(c, po, f, inst);
     if (rec == 1) return pick4<AdaptK, 1>(c, po, f, inst);
     return pick4<AdaptK, 0>(c, po, f, inst);

@@ -412,6 +412,18 @@ CONFIGS = {
                lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
                material=dict(kind="blinn", kd=(1, 1, 1), reflectAmt=0.5, refractAmt=0.5, ior=1.5),
                bg=(0.0, 0.0, 0.2), mesh="sponza"),
+    # G3: R3's Fresnel glass made dispersive with the Assignment 3 prism IORs
+    # (src/Assignment3.h:169-177: m_disperse, m_ior 1.57 / 1.60 / 1.62) under adaptive
+    # supersampling 1..3 (the reference's final scene supersamples its dispersive glass,
+    # src/main.cpp:143-174): the fused tree walk (dispersion splits) in adaptive_kernel
+    "G3": dict(name="sponza stand-in (~66k tris) 1920x1080 dispersive Blinn glass (m_ior 1.57/1.60/1.62) "
+                    "+ adaptive supersampling 1..3 + PointLight",
+               W=1920, H=1080,
+               camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
+               lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
+               material=dict(kind="blinn", kd=(1, 1, 1), reflectAmt=0.5, refractAmt=0.5, ior=1.60,
+                             disperse=True, ior3=(1.57, 1.60, 1.62)),
+               bg=(0.0, 0.0, 0.2), mesh="sponza", subdivs=(1, 3, 0.01)),
     # C4: Sponza stand-in, RectangleLight (8,10,2)/(8,10,-2)/(-8,10,2) power 1.5 and
     # Scene::m_numPaths = 16 (makeSponzaScenePathTrace, src/assignment2.h:663-708, direct
     # lighting only): 16 shade() calls per hit, one area-light shadow ray each;
@@ -493,6 +505,9 @@ def make_material(mat):
     m.setLightEmittedIntensity(mat.get("emitted", 0.0))
     m.setLightEmittedColor(mat.get("le", (0, 0, 0)))
     m.setSampleEnv(mat.get("sampleEnv", True))
+    for i, v in enumerate(mat.get("ior3", ())):   # Blinn::setIor(ior, i), src/Blinn.h:38
+        m.setIor(v, i)
+    m.m_disperse = bool(mat.get("disperse", False))
     return m
 
 

@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export MRT_SCENE_CACHE=/tmp/mrt_scenes
-CONFIGS="${CONFIGS:-C3 C2 C4 D1 C5 A3 R3 P4}"
+CONFIGS="${CONFIGS:-C3 C2 C4 D1 C5 A3 R3 P4 G3}"
 EXTRA="${EXTRA:---steps 5 --warmup 1 --no-cpu-baseline}"
 for c in $CONFIGS; do
     timeout -k 10 400 python bench.py --config $c $EXTRA > gpurun_out/bench_$c.log 2>&1

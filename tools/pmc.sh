@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "$ROOT" || exit 1
 mkdir -p gpurun_out/pmc
 export MRT_SCENE_CACHE=/tmp/mrt_scenes
-CONFIGS="${CONFIGS:-C3 C2 C4 D1 C5 A3 R3 P4}"
+CONFIGS="${CONFIGS:-C3 C2 C4 D1 C5 A3 R3 P4 G3}"
 STEPS="${STEPS:-5}"
 
 run() {
