@@ -472,6 +472,9 @@ static int g_resolve_waves = 4;   // resolve pass (kernel 2c) of dome-light scen
 static int g_adapt_waves = 6;     // direct-lighting adaptive kernel occupancy target: 1 (none), 4, 5, 6
                                   // (unbounded it takes 256 VGPRs, 1 wave: A3 30.7 -> 12.8 ms at 6)
 static int g_adapt_refill = 32;   // adaptive_kernel pixel refill: idle lanes that trigger a dequeue (0: tiles; 32: A3 -13%)
+static int g_near_first = -1;     // any-hit walks take the nearest hit child first: 0 off, 1 on, -1 auto
+                                  // (auto: on in the chunked shadow kernel only -- C4 shade -12.6%; off in
+                                  // the refill one, C5 +4.5%, and in the fused kernels, C3 +5%, A3 / R3 +2%)
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
 static int g_chain_mb = 16384;    // chain scratch per stream (MB); larger frames run in chunks of work items
@@ -1145,6 +1148,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     P.decline = g_decline;
     P.cus = d.cus;
     P.scalar_nodes = g_scalar_nodes;
+    P.near_first = g_near_first > 0 ? 1 : 0;
     HIP_OK(hipMemsetAsync(c.ctr, 0, kCtrBytes, stream));
     unsigned int* qbase = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(c.ctr) + CTR_N * sizeof(unsigned long long));
     P.queue = qbase;
@@ -1212,6 +1216,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         }
         size_t n_rays = slots * (size_t)max_sh;
         if (n_rays >= (size_t(1) << 32)) { set_error("too many wavefront shadow-ray slots (2^32)"); return MRT_ERR_INVALID; }
+        P.near_first = g_near_first >= 0 ? g_near_first : (sched == 2 ? 0 : 1);
         void* args[] = {&P, &n_rays, &sched, &refill};
         P.wave_log = nullptr;
         P.queue = qbase + 24 * 32;
@@ -2217,6 +2222,9 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "adapt_refill") {
         if (value < 0 || value > 64) { set_error("adapt_refill must be 0..64"); return MRT_ERR_INVALID; }
         g_adapt_refill = value;
+    } else if (k == "near_first") {
+        if (value < -1 || value > 1) { set_error("near_first must be -1..1"); return MRT_ERR_INVALID; }
+        g_near_first = value;
     } else if (k == "refill_min") {
         if (value < 1 || value > 64) { set_error("refill_min must be 1..64"); return MRT_ERR_INVALID; }
         g_refill_min = value;

@@ -81,6 +81,7 @@ struct Trav {
     const uint8_t* pflags = nullptr;
     const float4* verts = nullptr;
     const float4* verts2 = nullptr;
+    bool near_first = false;   // any-hit walks descend into the nearest hit child first (order-free answer)
 };
 
 struct TravStats {
@@ -172,6 +173,37 @@ __device__ __forceinline__ int box_test_fast(const float4* bx, const DRay& r, fl
         m |= (int)(t0 <= t1) << i;
     }
     return m;
+}
+
+// box_test_fast that also returns each slot's entry distance (the slab max of
+// the mins, clamped by tMin): any-hit walks may visit the nearest child first.
+__device__ __forceinline__ int box_test_fast_t(const float4* bx, const DRay& r, float tMin, float tMax, float (&tn)[4]) {
+    float4 mnx = bx[0], mny = bx[1], mnz = bx[2], mxx = bx[3], mxy = bx[4], mxz = bx[5];
+    float lx[4] = {mnx.x, mnx.y, mnx.z, mnx.w}, ly[4] = {mny.x, mny.y, mny.z, mny.w}, lz[4] = {mnz.x, mnz.y, mnz.z, mnz.w};
+    float hx[4] = {mxx.x, mxx.y, mxx.z, mxx.w}, hy[4] = {mxy.x, mxy.y, mxy.z, mxy.w}, hz[4] = {mxz.x, mxz.y, mxz.z, mxz.w};
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        float t0x = (lx[i] - r.o[0]) * r.id[0], t1x = (hx[i] - r.o[0]) * r.id[0];
+        float t0y = (ly[i] - r.o[1]) * r.id[1], t1y = (hy[i] - r.o[1]) * r.id[1];
+        float t0z = (lz[i] - r.o[2]) * r.id[2], t1z = (hz[i] - r.o[2]) * r.id[2];
+        float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
+                                   __builtin_fmaxf(__builtin_fminf(t0z, t1z), tMin));
+        float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
+                                   __builtin_fminf(__builtin_fmaxf(t0z, t1z), tMax));
+        tn[i] = t0;
+        m |= (int)(t0 <= t1) << i;
+    }
+    return m;
+}
+// the slot of `bits` (non-empty) with the smallest entry distance
+__device__ __forceinline__ int nearest_slot(int bits, const float (&tn)[4]) {
+    int best = 31 - __builtin_clz((unsigned)bits);
+    float bt = tn[best];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        if (((bits >> i) & 1) && tn[i] < bt) { bt = tn[i]; best = i; }
+    return best;
 }
 
 // Device child word of a QNode slot: >= 0 inner node; kEmptySlot; otherwise
@@ -293,6 +325,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         // steps): fetch it once through the scalar cache into SGPRs instead of
         // 64 copies through the vector memory path.
         const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
+        float tn[4] = {0.f, 0.f, 0.f, 0.f};   // slot entry distances (any-hit near-first order)
         if (FAST && c.scalar_nodes && __ballot(cur != c0) == 0) {
             // constant address space + uniform address -> s_load_dwordx16 (node
             // data is read-only for the whole launch)
@@ -304,11 +337,12 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
             float4 bx[6];
 #pragma unroll
             for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
-            m = box_test_fast(bx, r, tMin, h.t);
+            m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_fast(bx, r, tMin, h.t);
         } else {
             const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
             ch = reinterpret_cast<const int4*>(q)[6];
-            m = FAST ? box_test_fast(q, r, tMin, h.t) : box_test(q, r, tMin, h.t);
+            m = FAST ? ((ANY && c.near_first) ? box_test_fast_t(q, r, tMin, h.t, tn) : box_test_fast(q, r, tMin, h.t))
+                     : box_test(q, r, tMin, h.t);
         }
         if (COUNT) {
             st.nodes++;
@@ -322,7 +356,9 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         bool have_next = false;
         int32_t nxt = 0;
         if (inner) {
-            const int top = 31 - __builtin_clz((unsigned)inner);
+            // next: the highest hit slot (the reference's order); an any-hit walk in
+            // near-first mode takes the nearest instead (its answer is order-free)
+            const int top = (FAST && ANY && c.near_first) ? nearest_slot(inner, tn) : 31 - __builtin_clz((unsigned)inner);
             const int rest = inner ^ (1 << top);
             if (rest) {
                 if (sp + 4 <= kLdsStack) {
@@ -499,6 +535,7 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
     int m;
     int4 ch;
     const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
+    float tn[4] = {0.f, 0.f, 0.f, 0.f};
     if (FAST && c.scalar_nodes && __ballot(cur != c0) == 0) {   // wave-uniform node: scalar fetch
         typedef const __attribute__((address_space(4))) float cfloat;
         typedef const __attribute__((address_space(4))) int32_t cint;
@@ -508,11 +545,12 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
         float4 bx[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
-        m = box_test_fast(bx, r, tMin, tMax);
+        m = c.near_first ? box_test_fast_t(bx, r, tMin, tMax, tn) : box_test_fast(bx, r, tMin, tMax);
     } else {
         const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
         ch = reinterpret_cast<const int4*>(q)[6];
-        m = FAST ? box_test_fast(q, r, tMin, tMax) : box_test(q, r, tMin, tMax);
+        m = FAST ? (c.near_first ? box_test_fast_t(q, r, tMin, tMax, tn) : box_test_fast(q, r, tMin, tMax))
+                 : box_test(q, r, tMin, tMax);
     }
     if (COUNT) st.nodes++;
     const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
@@ -523,7 +561,7 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
     bool have_next = false;
     int32_t nxt = 0;
     if (inner) {
-        const int top = 31 - __builtin_clz((unsigned)inner);
+        const int top = (FAST && c.near_first) ? nearest_slot(inner, tn) : 31 - __builtin_clz((unsigned)inner);
         const int rest = inner ^ (1 << top);
         if (rest) {
             if (sp + 4 <= kLdsStack) {
@@ -608,7 +646,10 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
     const DRay& q = s.q;
     const float4* qn = reinterpret_cast<const float4*>(c.nodes + s.cur);
     const int4 ch = reinterpret_cast<const int4*>(qn)[6];
-    const int m = (FAST && q.finite) ? box_test_fast(qn, q, tMin, tMax) : box_test(qn, q, tMin, tMax);
+    float tn[4] = {0.f, 0.f, 0.f, 0.f};
+    const bool fast = FAST && q.finite;
+    const int m = fast ? (c.near_first ? box_test_fast_t(qn, q, tMin, tMax, tn) : box_test_fast(qn, q, tMin, tMax))
+                       : box_test(qn, q, tMin, tMax);
     if (COUNT) st.nodes++;
     const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
     const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
@@ -618,7 +659,7 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
     bool have_next = false;
     int32_t nxt = 0;
     if (inner) {
-        const int top = 31 - __builtin_clz((unsigned)inner);
+        const int top = (fast && c.near_first) ? nearest_slot(inner, tn) : 31 - __builtin_clz((unsigned)inner);
         const int rest = inner ^ (1 << top);
         if (rest) {
             if (s.sp + 4 <= kLdsStack) {

@@ -87,6 +87,7 @@ struct RenderParams {
     int32_t n_waves;             // waves in this launch (prio heuristic)
     int32_t decline;             // >0: a wave in CU slot s stops taking tiles when fewer than s * decline remain
     int32_t refill_min;          // adaptive_kernel: 0 tile schedule, > 0 pixel refill at this many idle lanes
+    int32_t near_first;          // any-hit walks take the nearest hit child first (their answer is order-free)
     int32_t cus;                 // compute units (slot of a persistent block = blockIdx / cus)
     int32_t scalar_nodes;        // scalar fetch of wave-uniform nodes
     unsigned int* queue;         // 8 tile counters, 32 words apart (sched >= 2)
@@ -162,6 +163,7 @@ __device__ __forceinline__ void trav_alpha(Trav& T, const RenderParams& P) {
     T.pflags = P.pflags;
     T.verts = P.verts;
     T.verts2 = P.verts2;
+    T.near_first = P.near_first != 0;
 }
 
 // Chain state of one path at its current level (Shader::level).

@@ -362,18 +362,21 @@ def test_c5_instanced_dome_matches_oracle():
 
 def shadow_schedules(P, cam, W, H):
     """Frames of one scene under every shadow_kernel schedule (grid-stride, XCD
-    bands, bands + lane refill): the any-hit answers -- and so every bit of the
-    frame and the ray counts -- must not depend on the schedule or on the deferred
-    instance walks of the lane-refill step."""
+    bands, bands + lane refill) and child order (reference order, nearest first):
+    the any-hit answers -- and so every bit of the frame and the ray counts -- must
+    not depend on the schedule, the visit order or the deferred instance walks of
+    the lane-refill step."""
     L = miro.lib()
     out = []
     try:
-        for sched in (0, 1, 2):
+        for sched, near in ((0, 0), (1, 0), (1, 1), (2, 0), (2, 1)):   # near: nearest hit child first
             assert L.mrt_set_tuning(b"shadow_sched", sched) == 0
+            assert L.mrt_set_tuning(b"near_first", near) == 0
             img, hits = render(P, cam, W, H)
             out.append((img, hits, P.last_stats))
     finally:
         L.mrt_set_tuning(b"shadow_sched", -1)
+        L.mrt_set_tuning(b"near_first", -1)
     img0, hits0, st0 = out[0]
     for img, hits, st in out[1:]:
         assert np.array_equal(hits0["prim"], hits["prim"])
