@@ -473,8 +473,9 @@ static int g_adapt_waves = 6;     // direct-lighting adaptive kernel occupancy t
                                   // (unbounded it takes 256 VGPRs, 1 wave: A3 30.7 -> 12.8 ms at 6)
 static int g_adapt_refill = 32;   // adaptive_kernel pixel refill: idle lanes that trigger a dequeue (0: tiles; 32: A3 -13%)
 static int g_near_first = -1;     // any-hit walks take the nearest hit child first: 0 off, 1 on, -1 auto
-                                  // (auto: on in the chunked shadow kernel only -- C4 shade -12.6%; off in
-                                  // the refill one, C5 +4.5%, and in the fused kernels, C3 +5%, A3 / R3 +2%)
+                                  // (auto: on in the chunked shadow kernel of plain scenes only -- C4 shade
+                                  // -12.6%; off in the refill one, C5 +4.5%, the instanced chunked one,
+                                  // C5 +15%, and the fused kernels, C3 +5%, A3 / R3 +2%)
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
 static int g_chain_mb = 16384;    // chain scratch per stream (MB); larger frames run in chunks of work items
@@ -1216,7 +1217,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         }
         size_t n_rays = slots * (size_t)max_sh;
         if (n_rays >= (size_t(1) << 32)) { set_error("too many wavefront shadow-ray slots (2^32)"); return MRT_ERR_INVALID; }
-        P.near_first = g_near_first >= 0 ? g_near_first : (sched == 2 ? 0 : 1);
+        P.near_first = g_near_first >= 0 ? g_near_first : (sched == 2 || inst ? 0 : 1);
         void* args[] = {&P, &n_rays, &sched, &refill};
         P.wave_log = nullptr;
         P.queue = qbase + 24 * 32;

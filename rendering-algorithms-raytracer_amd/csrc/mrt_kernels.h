@@ -656,11 +656,17 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
                        (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
     const int inner = m & isinner;
     int lm = m & isleaf;
+    // a hit leaf packet with proxy lanes: its instance walks run before the
+    // descent (all hit inner children go onto the stack below them), so deferred
+    // proxies never pile up along the path -- the stack stays near 4 per level
+    bool proxies = false;
+#pragma unroll
+    for (int i = 0; i < 4; i++) proxies |= ((lm >> i) & 1) && (~(uint32_t)sel4(ch, i) & 4u);
     bool have_next = false;
     int32_t nxt = 0;
     if (inner) {
         const int top = (fast && c.near_first) ? nearest_slot(inner, tn) : 31 - __builtin_clz((unsigned)inner);
-        const int rest = inner ^ (1 << top);
+        const int rest = proxies ? inner : inner ^ (1 << top);
         if (rest) {
             if (s.sp + 4 <= kLdsStack) {
                 c.lds[s.sp * kWG] = ch.x; s.sp += rest & 1;
@@ -676,7 +682,7 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
             if (COUNT && s.sp > st.max_sp) st.max_sp = s.sp;
         }
         nxt = sel4(ch, top);
-        have_next = true;
+        have_next = !proxies;
     }
     while (lm) {
         const int sl = __builtin_ctz((unsigned)lm);
