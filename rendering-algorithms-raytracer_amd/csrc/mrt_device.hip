@@ -469,7 +469,7 @@ static int g_shadow_sched = -1;   // shadow_kernel schedule: 0 grid-stride, 1 XC
 static int g_shadow_waves = 8;    // shadow_kernel launch-bounds occupancy: 1 (none), 7, 8 (8: C4 / C5 -5.5%)
 static int g_primary_inst_waves = 6;   // primary kernel of special-leaf scenes: 1 (none), 5, 6 (6: C5 -5%)
 static int g_resolve_waves = 4;   // resolve pass (kernel 2c) of dome-light scenes: 1 (none), 3 (special-leaf only), 4
-static int g_adapt_waves = 6;     // direct-lighting adaptive kernel occupancy target: 1 (none), 4, 5, 6
+static int g_adapt_waves = 6;     // direct-lighting adaptive kernel occupancy target: 1 (none) or 6
                                   // (unbounded it takes 256 VGPRs, 1 wave: A3 30.7 -> 12.8 ms at 6)
 static int g_adapt_refill = 32;   // adaptive_kernel pixel refill: idle lanes that trigger a dequeue (0: tiles; 32: A3 -13%)
 static int g_near_first = -1;     // any-hit walks take the nearest hit child first: 0 off, 1 on, -1 auto
@@ -2218,7 +2218,7 @@ int mrt_set_tuning(const char* key, int value) {
         if (value != 1 && value != 7 && value != 8) { set_error("shadow_waves must be 1, 7 or 8"); return MRT_ERR_INVALID; }
         g_shadow_waves = value;
     } else if (k == "adapt_waves") {
-        if (value != 1 && (value < 4 || value > 6)) { set_error("adapt_waves must be 1 or 4..6"); return MRT_ERR_INVALID; }
+        if (value != 1 && value != 6) { set_error("adapt_waves must be 1 or 6"); return MRT_ERR_INVALID; }
         g_adapt_waves = value;
     } else if (k == "adapt_refill") {
         if (value < 0 || value > 64) { set_error("adapt_refill must be 0..64"); return MRT_ERR_INVALID; }
