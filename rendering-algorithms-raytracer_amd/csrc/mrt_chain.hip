@@ -223,8 +223,8 @@ __global__ void __launch_bounds__(kWG) chain_compact_kernel(RenderParams P) {
 // answers of level k - 1's shadow rays (nB slots), which no longer wait for
 // each other -- a level's resolve needs its shadow answers only at the end of
 // the chunk.  Wave-uniform 64-slot chunks, the closest-hit chunks first.
-template <bool COUNT, bool FAST, bool INST>
-__global__ void __launch_bounds__(kWG) chain_trace_kernel(RenderParams P) {
+template <bool COUNT, bool FAST, bool INST, int MINW = 1>
+__global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     const int k = P.ch_level;
@@ -438,7 +438,9 @@ KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec) {
     if (rec == 2) return resolve ? chain_shade_fn<kResolve, 2>(po, inst) : chain_shade_fn<kGen, 2>(po, inst);
     return resolve ? chain_shade_fn<kResolve, 1>(po, inst) : chain_shade_fn<kGen, 1>(po, inst);
 }
-KernelFn pick_chain_trace(bool c, bool f, bool inst) {
+KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves) {
+    if (waves == 8 && !c && !inst)   // occupancy target of the plain-scene trace (timed variants)
+        return f ? chain_trace_kernel<false, true, false, 8> : chain_trace_kernel<false, false, false, 8>;
     if (inst) return c ? (f ? chain_trace_kernel<true, true, true> : chain_trace_kernel<true, false, true>)
                        : (f ? chain_trace_kernel<false, true, true> : chain_trace_kernel<false, false, true>);
     return c ? (f ? chain_trace_kernel<true, true, false> : chain_trace_kernel<true, false, false>)

@@ -472,6 +472,7 @@ static int g_resolve_waves = 4;   // resolve pass (kernel 2c) of dome-light scen
 static int g_adapt_waves = 6;     // direct-lighting adaptive kernel occupancy target: 1 (none) or 6
                                   // (unbounded it takes 256 VGPRs, 1 wave: A3 30.7 -> 12.8 ms at 6)
 static int g_adapt_refill = 32;   // adaptive_kernel pixel refill: idle lanes that trigger a dequeue (0: tiles; 32: A3 -13%)
+static int g_chain_trace_waves = 8;   // chain_trace_kernel occupancy target: 1 (none) or 8 (P4 -17%, R3 -3.5%)
 static int g_near_first = -1;     // any-hit walks take the nearest hit child first: 0 off, 1 on, -1 auto
                                   // (auto: on in the chunked shadow kernel of plain scenes only -- C4 shade
                                   // -12.6%; off in the refill one, C5 +4.5%, the instanced chunked one,
@@ -1088,7 +1089,7 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive), r0 = pick_chain0(true, d.point_only, inst, d.recursive);
     const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive),
                    rk = pick_chain_shade(true, d.point_only, inst, d.recursive);
-    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, fb, inst), kf = pick_chain_finish(),
+    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, fb, inst, g_chain_trace_waves), kf = pick_chain_finish(),
                    kp = pick_chain_path();
     auto go = [&](KernelFn f, int g) -> int {
         void* args[] = {&Q};
@@ -2223,6 +2224,9 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "adapt_refill") {
         if (value < 0 || value > 64) { set_error("adapt_refill must be 0..64"); return MRT_ERR_INVALID; }
         g_adapt_refill = value;
+    } else if (k == "chain_trace_waves") {
+        if (value != 1 && value != 8) { set_error("chain_trace_waves must be 1 or 8"); return MRT_ERR_INVALID; }
+        g_chain_trace_waves = value;
     } else if (k == "near_first") {
         if (value < -1 || value > 1) { set_error("near_first must be -1..1"); return MRT_ERR_INVALID; }
         g_near_first = value;
