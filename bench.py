@@ -81,9 +81,26 @@ def spawn(args):
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=None if r == 0 else subprocess.DEVNULL))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    # poll every rank: when one exits non-zero the others would block in a
+    # collective (or in init_process_group) forever, so they are terminated
+    # and that rank's code is returned
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return bad[0]
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.2)
 
 
 # ------------------------------------------------------------------ helpers
@@ -271,7 +288,8 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        import datetime
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=datetime.timedelta(seconds=300))
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -470,7 +488,12 @@ def main():
                   "chain engine (per level: chain gen + compact + chain_trace [closest hits + any-hit shadow rays]; "
                   "resolve + combine)" if chain else
                   "shade pass (shade_kernel<gen> + shadow_kernel any-hit + shade_kernel<resolve>)")
-    if adaptive:   # one fused launch: eye rays, shading, inline shadow rays (its time is shade_ms)
+    if st.get("fused"):   # frame1_kernel: the whole frame in one launch (its time is primary_ms)
+        dom, dom_key, dom_ms = ("frame1_kernel (camera rays + closest hit + shading + any-hit shadow rays, "
+                                "one launch)"), "primary", pm
+        dom_b = (st["node_visits"] * NODE_B + st["leaf_visits"] * LEAF_B
+                 + px_mine * ((12 if use_frame_path else 0) + 3) + hits_px * (32 + 3 * 16 + 3 * 16))
+    elif adaptive:   # one fused launch: eye rays, shading, inline shadow rays (its time is shade_ms)
         dom, dom_key, dom_ms = "adaptive_kernel (eye rays + shading + any-hit shadow rays)", "shade", sm
         dom_b = (st["node_visits"] * NODE_B + st["leaf_visits"] * LEAF_B
                  + px_mine * (16 + (12 if use_frame_path else 0) + 3) + hits_px * (32 + 3 * 16 + 3 * 16))

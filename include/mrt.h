@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 6
+#define MRT_ABI_VERSION 7
 
 enum {
     MRT_OK = 0,
@@ -154,6 +154,10 @@ typedef struct {
     /* count mode, wavefront shadow_kernel: wave loop steps and node visits (lane
      * utilisation = shadow_node_visits / (64 * shadow_wave_steps)) */
     uint64_t shadow_wave_steps, shadow_node_visits;
+    /* 1: the frame ran as ONE launch (frame1_kernel: camera rays, closest hits,
+     * shading and shadow rays fused; one point light, one path); primary_ms is
+     * then the whole frame and shade_ms ~0 (ABI 7) */
+    int32_t fused;
 } mrt_stats;
 
 const char* mrt_last_error(void);
@@ -198,6 +202,8 @@ int mrt_scene_set_num_paths(mrt_scene* s, int num_paths);
  * Fresnel-weighted Russian roulette, at most 5 bounces, IOR history per ray.
  * No effect on Lambert materials. */
 int mrt_scene_set_material_optics(mrt_scene* s, int material, float reflect_amt, float refract_amt, float ior);
+/* (ior is m_ior[1]: it also replaces the middle IOR of mrt_scene_set_material_dispersion,
+ * as the reference keeps one m_ior[3] array.) */
 /* Material::m_disperse + Blinn::setIor(ior, i) for i = 0..2 (src/Material.h:45,
  * src/Blinn.h:38,59; ABI 6).  `ior` replaces all three m_ior; ior[1] is also the
  * optics IOR above (the non-dispersive refraction reads m_ior[1], src/Blinn.cpp:183).

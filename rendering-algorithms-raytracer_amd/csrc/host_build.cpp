@@ -20,7 +20,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <fcntl.h>
 #include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <condition_variable>
@@ -144,6 +148,27 @@ v3 xform_dir(const Mat4& M, v3 u) {
               M.m[2][0] * u.x + M.m[2][1] * u.y + M.m[2][2] * u.z);
 }
 
+// atoi(s) = (int)strtol(s, NULL, 10) (glibc): leading white space, a sign,
+// decimal digits; out of long range -> LONG_MAX / LONG_MIN; then the long is
+// truncated to int
+int atoi_exact(const char* s) {
+    while (*s == ' ' || (*s >= '\t' && *s <= '\r')) s++;
+    bool neg = false;
+    if (*s == '+' || *s == '-') neg = *s++ == '-';
+    uint64_t v = 0;
+    bool sat = false;
+    for (; *s >= '0' && *s <= '9'; s++) {
+        if (!sat) {
+            v = v * 10 + (uint64_t)(*s - '0');
+            if (v > (uint64_t)LONG_MAX + (neg ? 1u : 0u)) sat = true;
+        }
+    }
+    long r;
+    if (sat) r = neg ? LONG_MIN : LONG_MAX;
+    else r = neg ? (long)(0 - v) : (long)v;
+    return (int)r;
+}
+
 // getIndices, src/TriangleMeshLoad.cpp:67-97
 void split_indices(char* word, int& vi, int& ti, int& ni) {
     static char blank[] = " ";
@@ -155,102 +180,341 @@ void split_indices(char* word, int& vi, int& ti, int& ni) {
         else np = p + 1;
         *p = '\0';
     }
-    vi = atoi(word);
-    ti = atoi(tp);
-    ni = atoi(np);
+    vi = atoi_exact(word);
+    ti = atoi_exact(tp);
+    ni = atoi_exact(np);
 }
 }  // namespace
 
-// TriangleMesh::loadObj, src/TriangleMeshLoad.cpp:99-214.  Two passes over
-// 79-character fgets chunks; vertices through ctm with the rcp_nr w-divide;
-// normals through the inverse transpose and renormalised; a face without a
-// normal on its last corner gets a face normal appended at slot `nn`
-// (the reference also stores its index triple at m_normalIndices[nn]).
-// Reference UB (negative / out-of-range indices, slot overflow) -> MRT_ERR_IO.
+namespace {
+int build_threads();
+}  // namespace
+
+namespace {
+inline bool is_space(char c) { return c == ' ' || (c >= '\t' && c <= '\r'); }   // isspace, C locale
+
+// sscanf(s, "%f %f ... %f", out...) for n floats, exact: a plain decimal token
+// ([+-] digits [. digits] [(e|E) [+-] digits], at most 19 significant digits,
+// ended by white space or the end) is converted as m * 10^e in double -- one
+// correctly rounded operation while m < 2^53 and |e| <= 22 -- and rounded to
+// float, which equals strtof's correctly rounded result unless the double lands
+// exactly on a float rounding midpoint.  Anything else (that midpoint, hex, inf,
+// nan, subnormal or out-of-range values, fewer than n tokens, malformed
+// tokens) returns false and the caller runs sscanf itself.
+bool fast_floats(const char* s, int n, float* out) {
+    static const double p10[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
+                                   1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    for (int k = 0; k < n; k++) {
+        while (is_space(*s)) s++;
+        bool neg = false;
+        if (*s == '+' || *s == '-') neg = *s++ == '-';
+        uint64_t m = 0;
+        int sig = 0, digits = 0, e10 = 0;
+        for (; *s >= '0' && *s <= '9'; s++, digits++) {
+            if (m || *s != '0') { if (++sig > 19) return false; m = m * 10 + (uint64_t)(*s - '0'); }
+        }
+        if (*s == '.') {
+            for (s++; *s >= '0' && *s <= '9'; s++, digits++) {
+                if (m || *s != '0') { if (++sig > 19) return false; m = m * 10 + (uint64_t)(*s - '0'); }
+                e10--;
+            }
+        }
+        if (!digits) return false;
+        if (*s == 'e' || *s == 'E') {
+            s++;
+            bool eneg = false;
+            if (*s == '+' || *s == '-') eneg = *s++ == '-';
+            if (!(*s >= '0' && *s <= '9')) return false;
+            int x = 0;
+            for (; *s >= '0' && *s <= '9'; s++) { if (x < 10000) x = x * 10 + (*s - '0'); }
+            e10 += eneg ? -x : x;
+        }
+        if (*s && !is_space(*s)) return false;
+        if (m == 0) { out[k] = neg ? -0.0f : 0.0f; continue; }
+        if (m > (1ull << 53) || e10 > 22 || e10 < -22) return false;
+        double d = (double)m;
+        d = e10 < 0 ? d / p10[-e10] : d * p10[e10];
+        if (!(d >= 1.1754943508222875e-38 && d <= 3.4028234663852886e38)) return false;   // normal floats only
+        uint64_t bits;
+        memcpy(&bits, &d, sizeof bits);
+        if ((bits & 0x1FFFFFFFull) == 0x10000000ull) return false;   // a float midpoint: ambiguous
+        const float f = (float)d;
+        out[k] = neg ? -f : f;
+    }
+    return true;
+}
+// sscanf(s, "%31s %31s %31s") into tok (tokens not reached stay as they are)
+void scan_tokens(const char* s, char (&tok)[3][32]) {
+    for (int k = 0; k < 3; k++) {
+        while (is_space(*s)) s++;
+        if (!*s) return;
+        int i = 0;
+        while (*s && !is_space(*s) && i < 31) tok[k][i++] = *s++;
+        tok[k][i] = '\0';
+    }
+}
+
+// One fgets(line, 80, fp) chunk of the file at p (end = file end): up to 79
+// bytes, through the first '\n'.  A line longer than 79 characters is several
+// chunks, each parsed as a line of its own (the reference's behaviour); a chunk
+// boundary is fixed by its line's start, so cutting the file at line starts
+// keeps the chunk sequence.
+inline size_t chunk_len(const char* p, const char* end) {
+    const size_t lim = std::min<size_t>(79, (size_t)(end - p));
+    const void* nl = memchr(p, '\n', lim);
+    return nl ? (size_t)((const char*)nl - p) + 1 : lim;
+}
+inline void chunk_copy(char (&line)[81], const char* p, size_t n) {
+    memcpy(line, p, n);
+    line[n] = '\0';
+}
+
+// A byte range of the file (starting at a line start) and what it holds.
+struct ObjRange {
+    size_t b = 0, e = 0;
+    int nv = 0, nt = 0, nn = 0, nf = 0;   // pass 1: v / vt / vn / f chunks
+    // pass 2: faces without a normal on their last corner (face-normal events)
+    struct FaceNormal {
+        uint32_t tri, verts_loaded;        // triangle index; vertices loaded before the face
+        size_t pos;                        // chunk offset (error order)
+    };
+    std::vector<FaceNormal> fn;
+    size_t err_pos = SIZE_MAX;             // first error of the range (file offset)
+    std::string err;
+};
+
+// Runs f(r) for every range on up to `threads` threads.
+template <typename F>
+void for_ranges(std::vector<ObjRange>& rs, int threads, F f) {
+    if (threads <= 1 || rs.size() <= 1) {
+        for (ObjRange& r : rs) f(r);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> ts;
+    const int n = std::min<int>(threads, (int)rs.size());
+    for (int i = 0; i < n; i++)
+        ts.emplace_back([&] {
+            for (size_t k; (k = next.fetch_add(1)) < rs.size();) f(rs[k]);
+        });
+    for (auto& t : ts) t.join();
+}
+}  // namespace
+
+// TriangleMesh::loadObj, src/TriangleMeshLoad.cpp:99-214: vertices through
+// ctm with the rcp_nr w-divide; normals through the inverse transpose and
+// renormalised; a face without a normal on its last corner gets a face normal
+// appended at slot `nn` (the reference also stores its index triple at
+// m_normalIndices[nn]).  Reference UB (negative / out-of-range indices, slot
+// overflow) -> MRT_ERR_IO.
+//
+// Parallel form of the reference's two sequential passes over 79-character
+// fgets chunks, with the same result bit for bit at any thread count: the
+// mapped file is cut into ranges at line starts; pass 1 counts each range's
+// v / vt / vn / f chunks, prefix sums give every range its first vertex,
+// normal, texture-coordinate and triangle index, and pass 2 parses the ranges
+// concurrently into their slots (sscanf per chunk, as the reference).  The
+// face normals then run as a third pass in file order of their slots:
+//   * the reference reads the face's vertices as loaded at that point of the
+//     file -- a vertex defined further down is still the zero vector -- so each
+//     event keeps the count of vertices loaded before it;
+//   * the index triple it writes at m_normalIndices[nn] is overwritten by
+//     triangle nn's own corners (those with a normal index) when triangle nn
+//     comes later in the file, and overwrites them when it came earlier.
+// Errors are reported for the first offending chunk in file order.
 int load_obj(const char* path, const float* ctm16, Mesh& out, std::string& err) {
-    FILE* fp = fopen(path, "rb");
-    if (!fp) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) {
         err = std::string("cannot open ") + path;
         return MRT_ERR_IO;
     }
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) {
+        close(fd);
+        err = std::string("cannot stat ") + path;
+        return MRT_ERR_IO;
+    }
+    const size_t size = (size_t)sb.st_size;
+    const char* base = nullptr;
+    if (size) {
+        void* m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) {
+            close(fd);
+            err = std::string("cannot map ") + path;
+            return MRT_ERR_IO;
+        }
+        base = static_cast<const char*>(m);
+    }
+    close(fd);
+    struct Unmap {
+        const char* p;
+        size_t n;
+        ~Unmap() { if (p) munmap(const_cast<char*>(p), n); }
+    } unmap{base, size};
+    const char* end = base + size;
+    const bool trace = getenv("MRT_BUILD_TRACE") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t0 = now();
+
     Mat4 ctm = identity();
     if (ctm16) memcpy(ctm.m, ctm16, sizeof(float) * 16);
     const Mat4 nctm = transpose(inverse(ctm));
     const uint16_t* RS = host_rsqrt_table();
 
-    char line[81];
-    int nv = 0, nt = 0, nn = 0, nf = 0;
-    while (fgets(line, 80, fp)) {
-        if (line[0] == 'v') {
-            if (line[1] == 'n') nn++;
-            else if (line[1] == 't') nt++;
-            else nv++;
-        } else if (line[0] == 'f') {
-            nf++;
-        }
+    // ranges: about MRT_OBJ_RANGE_BYTES (default 1 MiB) each, cut after a '\n'
+    int threads = build_threads();
+    size_t per = 1u << 20;
+    if (const char* e = getenv("MRT_OBJ_RANGE_BYTES")) {
+        const long v = atol(e);
+        if (v >= 1) per = (size_t)v;
     }
-    fseek(fp, 0, SEEK_SET);
+    std::vector<ObjRange> rs;
+    for (size_t b = 0; b < size;) {
+        size_t e = std::min(size, b + per);
+        if (e < size) {
+            const void* nl = memchr(base + e, '\n', size - e);
+            e = nl ? (size_t)((const char*)nl - base) + 1 : size;
+        }
+        ObjRange r;
+        r.b = b;
+        r.e = e;
+        rs.push_back(std::move(r));
+        b = e;
+    }
+    // pass 1: counts
+    for_ranges(rs, threads, [&](ObjRange& r) {
+        char line[81];
+        for (const char* p = base + r.b; p < base + r.e;) {
+            const size_t n = chunk_len(p, end);
+            chunk_copy(line, p, n);
+            p += n;
+            if (line[0] == 'v') {
+                if (line[1] == 'n') r.nn++;
+                else if (line[1] == 't') r.nt++;
+                else r.nv++;
+            } else if (line[0] == 'f') {
+                r.nf++;
+            }
+        }
+    });
+    const auto t1 = now();
+    int nv = 0, nt = 0, nn = 0, nf = 0;
+    std::vector<int> bv(rs.size()), bt(rs.size()), bn(rs.size()), bf(rs.size());
+    for (size_t k = 0; k < rs.size(); k++) {
+        bv[k] = nv; bt[k] = nt; bn[k] = nn; bf[k] = nf;
+        nv += rs[k].nv; nt += rs[k].nt; nn += rs[k].nn; nf += rs[k].nf;
+    }
     if (nt) {   // got texture coordinates
         out.uv.assign((size_t)2 * nt, 0.f);
         out.tidx.assign((size_t)3 * nf, 0u);
     }
-    int ntex = 0;
     out.verts.assign((size_t)nv, v3{0, 0, 0});
     out.normals.assign((size_t)3 * nv + 1, v3{0, 0, 0});
     out.vidx.assign((size_t)3 * nf, 0u);
     out.nidx.assign((size_t)3 * nf, 0u);
-    int nverts = 0, nnorm = 0, ntris = 0;
-    int rc = MRT_OK;
-    while (rc == MRT_OK && fgets(line, 80, fp)) {
-        if (line[0] == 'v') {
-            float x = 0, y = 0, z = 0;
-            if (line[1] == 'n') {
-                sscanf(&line[2], "%f %f %f\n", &x, &y, &z);
-                if (nnorm >= 3 * nv + 1) { rc = MRT_ERR_IO; err = "too many normals"; break; }
-                out.normals[nnorm++] = normalized(xform_dir(nctm, mk(x, y, z)), RS);
-            } else if (line[1] == 't') {
-                sscanf(&line[2], "%f %f\n", &x, &y);
-                out.uv[2 * (size_t)ntex] = x;
-                out.uv[2 * (size_t)ntex + 1] = y;
-                ntex++;
-            } else {
-                sscanf(&line[1], "%f %f %f\n", &x, &y, &z);
-                out.verts[nverts++] = xform_point(ctm, mk(x, y, z));
-            }
-        } else if (line[0] == 'f') {
-            char tok[3][32];
-            tok[0][0] = tok[1][0] = tok[2][0] = 0;
-            sscanf(&line[1], "%31s %31s %31s\n", tok[0], tok[1], tok[2]);
-            int v = 0, t = 0, n = 0;
-            for (int k = 0; k < 3; k++) {
-                split_indices(tok[k], v, t, n);
-                if (v <= 0 || v > nv) { rc = MRT_ERR_IO; err = "face vertex index out of range"; break; }
-                out.vidx[3 * ntris + k] = (uint32_t)(v - 1);
-                if (n) out.nidx[3 * ntris + k] = (uint32_t)(n - 1);
-                if (t && nt) {
-                    if (t < 0 || t > nt) { rc = MRT_ERR_IO; err = "face texture-coordinate index out of range"; break; }
-                    out.tidx[3 * ntris + k] = (uint32_t)(t - 1);
+    std::vector<uint8_t> own((size_t)nf, 0);   // corners whose normal index the face itself wrote
+    const auto t2 = now();
+    // pass 2: parse into the slots
+    for_ranges(rs, threads, [&](ObjRange& r) {
+        const size_t k = (size_t)(&r - rs.data());
+        int nverts = bv[k], nnorm = bn[k], ntex = bt[k], ntris = bf[k];
+        char line[81];
+        for (const char* p = base + r.b; p < base + r.e;) {
+            const size_t pos = (size_t)(p - base), len = chunk_len(p, end);
+            chunk_copy(line, p, len);
+            p += len;
+            if (line[0] == 'v') {
+                float x = 0, y = 0, z = 0;
+                if (line[1] == 'n') {
+                    float f3[3];
+                    if (fast_floats(&line[2], 3, f3)) { x = f3[0]; y = f3[1]; z = f3[2]; }
+                    else sscanf(&line[2], "%f %f %f\n", &x, &y, &z);
+                    if (nnorm >= 3 * nv + 1) { r.err_pos = pos; r.err = "too many normals"; return; }
+                    out.normals[nnorm++] = normalized(xform_dir(nctm, mk(x, y, z)), RS);
+                } else if (line[1] == 't') {
+                    float f2[2];
+                    if (fast_floats(&line[2], 2, f2)) { x = f2[0]; y = f2[1]; }
+                    else sscanf(&line[2], "%f %f\n", &x, &y);
+                    out.uv[2 * (size_t)ntex] = x;
+                    out.uv[2 * (size_t)ntex + 1] = y;
+                    ntex++;
+                } else {
+                    float f3[3];
+                    if (fast_floats(&line[1], 3, f3)) { x = f3[0]; y = f3[1]; z = f3[2]; }
+                    else sscanf(&line[1], "%f %f %f\n", &x, &y, &z);
+                    out.verts[nverts++] = xform_point(ctm, mk(x, y, z));
                 }
+            } else if (line[0] == 'f') {
+                char tok[3][32];
+                tok[0][0] = tok[1][0] = tok[2][0] = 0;
+                scan_tokens(&line[1], tok);
+                int v = 0, t = 0, n = 0;
+                for (int c = 0; c < 3; c++) {
+                    split_indices(tok[c], v, t, n);
+                    if (v <= 0 || v > nv) { r.err_pos = pos; r.err = "face vertex index out of range"; return; }
+                    out.vidx[3 * (size_t)ntris + c] = (uint32_t)(v - 1);
+                    if (n) {
+                        out.nidx[3 * (size_t)ntris + c] = (uint32_t)(n - 1);
+                        own[(size_t)ntris] |= (uint8_t)(1u << c);
+                    }
+                    if (t && nt) {
+                        if (t < 0 || t > nt) { r.err_pos = pos; r.err = "face texture-coordinate index out of range"; return; }
+                        out.tidx[3 * (size_t)ntris + c] = (uint32_t)(t - 1);
+                    }
+                }
+                if (!n) r.fn.push_back(ObjRange::FaceNormal{(uint32_t)ntris, (uint32_t)nverts, pos});
+                ntris++;
             }
-            if (rc != MRT_OK) break;
-            if (!n) {
-                if (nn >= nf || nn >= 3 * nv) { rc = MRT_ERR_IO; err = "face-normal slot overflow"; break; }
-                const uint32_t* f = &out.vidx[3 * ntris];
-                v3 e1 = sub(out.verts[f[1]], out.verts[f[0]]);
-                v3 e2 = sub(out.verts[f[2]], out.verts[f[0]]);
-                out.normals[nn] = normalized(cross(e1, e2), RS);
-                out.nidx[3 * nn + 0] = out.nidx[3 * nn + 1] = out.nidx[3 * nn + 2] = (uint32_t)nn;
-                nn++;
-            }
-            ntris++;
         }
+    });
+    const auto t3 = now();
+    // pass 3: face normals, slot nn = (vn lines) + (earlier such faces)
+    size_t err_pos = SIZE_MAX;
+    for (const ObjRange& r : rs)
+        if (r.err_pos < err_pos) { err_pos = r.err_pos; err = r.err; }
+    std::vector<size_t> fbase(rs.size());
+    size_t nfn = 0;
+    for (size_t k = 0; k < rs.size(); k++) { fbase[k] = nfn; nfn += rs[k].fn.size(); }
+    const long slot_lim = std::min<long>((long)nf, 3l * nv);   // nn >= nf || nn >= 3 nv: overflow
+    for (size_t k = 0; k < rs.size(); k++) {
+        for (size_t i = 0; i < rs[k].fn.size(); i++) {
+            if ((long)nn + (long)(fbase[k] + i) >= slot_lim) {   // the first overflowing face (slots only grow)
+                if (rs[k].fn[i].pos < err_pos) { err_pos = rs[k].fn[i].pos; err = "face-normal slot overflow"; }
+                k = rs.size();
+                break;
+            }
+        }
+        if (k == rs.size()) break;
     }
-    fclose(fp);
-    if (rc != MRT_OK) return rc;
-    out.normals.resize((size_t)std::max(nn, 1));
-    out.vidx.resize((size_t)3 * ntris);
-    out.nidx.resize((size_t)3 * ntris);
-    if (!out.tidx.empty()) out.tidx.resize((size_t)3 * ntris);
+    if (err_pos != SIZE_MAX) return MRT_ERR_IO;
+    for_ranges(rs, threads, [&](ObjRange& r) {
+        const size_t k = (size_t)(&r - rs.data());
+        for (size_t i = 0; i < r.fn.size(); i++) {
+            const ObjRange::FaceNormal& F = r.fn[i];
+            const uint32_t slot = (uint32_t)((size_t)nn + fbase[k] + i);
+            const uint32_t* f = &out.vidx[3 * (size_t)F.tri];
+            auto vert = [&](uint32_t j) { return j < F.verts_loaded ? out.verts[j] : v3{0, 0, 0}; };
+            const v3 a = vert(f[0]);
+            const v3 e1 = sub(vert(f[1]), a);
+            const v3 e2 = sub(vert(f[2]), a);
+            out.normals[slot] = normalized(cross(e1, e2), RS);
+            const uint8_t keep = slot > F.tri ? own[slot] : 0;   // triangle `slot` parsed later keeps its own corners
+            for (int c = 0; c < 3; c++)
+                if (!((keep >> c) & 1)) out.nidx[3 * (size_t)slot + c] = slot;
+        }
+    });
+    const auto t4 = now();
+    if (trace)
+        fprintf(stderr, "[mrt] load_obj %s: %zu ranges, %d threads: count %.1f ms, alloc %.1f ms, parse %.1f ms, "
+                "face normals %.1f ms\n", path, rs.size(), threads, ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
+    const int nn_final = nn + (int)nfn;
+    out.normals.resize((size_t)std::max(nn_final, 1));
+    out.vidx.resize((size_t)3 * nf);
+    out.nidx.resize((size_t)3 * nf);
+    if (!out.tidx.empty()) out.tidx.resize((size_t)3 * nf);
     for (uint32_t i : out.nidx)
         if (i >= out.normals.size()) { err = "normal index out of range"; return MRT_ERR_IO; }
     return MRT_OK;

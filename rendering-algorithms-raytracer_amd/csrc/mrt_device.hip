@@ -202,10 +202,95 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
 }
 
 
-// Kernel 2, specialised for one point light and num_paths == 1 (the BASELINE
-// configs C1-C3): straight-line PointLight::sampleLight + Lambert/Blinn with only
-// the light's three pre-shadow scalars live across the any-hit traversal.
-// Same operations in the same order as Shader::shade.
+// Shading of one primary hit for one point light and num_paths == 1 (the
+// BASELINE configs C1-C3): HitInfo::getAllInfos + Ray::getPoint, the
+// Lambert/Blinn set-up, straight-line PointLight::sampleLight with only the
+// light's three pre-shadow scalars live across the any-hit traversal, then the
+// material sums.  Same operations in the same order as Shader::shade.  r is the
+// camera ray, (ht, ha, hb, prim) its closest hit.
+template <bool COUNT, bool FAST>
+__device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, TravStats& st, const DRay& r, float ht,
+                                         float ha, float hb, int prim, const uint16_t* rcpT, const uint16_t* rsqT,
+                                         uint32_t& shadow_total) {
+    const v3 rayD = mk(r.d[0], r.d[1], r.d[2]);
+    const PrimShade ps = P.prims[prim];
+    const uint32_t mi = ps.mat;
+    const bool lambert = P.mats[mi].type == MRT_LAMBERT;
+    const float4 A = P.verts[ps.v[0]], B = P.verts[ps.v[1]], C = P.verts[ps.v[2]];
+    const v3 geoN = normalized(cross(mk(B.x - A.x, B.y - A.y, B.z - A.z), mk(C.x - A.x, C.y - A.y, C.z - A.z)), rsqT);
+    const float c = 1.0f - ha - hb;
+    const float4 n0 = P.normals[ps.n[0]], n1 = P.normals[ps.n[1]], n2 = P.normals[ps.n[2]];
+    const v3 N = normalized(add(add(scale(mk(n0.x, n0.y, n0.z), c), scale(mk(n1.x, n1.y, n1.z), ha)),
+                                scale(mk(n2.x, n2.y, n2.z), hb)), rsqT);
+    const v3 from = mk(r.o[0] + ht * r.d[0], r.o[1] + ht * r.d[1], r.o[2] + ht * r.d[2]);
+    // Lambert::shade uses the shading normal and no reflection vector;
+    // Blinn::shade flips to the viewer's side (src/Blinn.cpp:150-170).
+    v3 n = N, rVec = mk(0, 0, 0);
+    if (!lambert) {
+        const v3 viewDir = neg(rayD);
+        float vDotN = dot(viewDir, N);
+        const float vDotGeoN = dot(viewDir, geoN);
+        const bool same = (vDotN * vDotGeoN) >= 0.0f;
+        n = same ? N : geoN;
+        vDotN = same ? vDotN : vDotGeoN;
+        if (vDotN < 0.0f) { vDotN = -vDotN; n = neg(n); }
+        rVec = add(rayD, scale(n, 2.0f * vDotN));
+    }
+    // PointLight::sampleLight (src/PointLight.cpp:8-81), as Shader::point_light
+    const DevLight& l = P.lights[0];
+    v3 L = sub(mk(l.pos[0], l.pos[1], l.pos[2]), from);
+    float nDotL = dot(n, L);
+    float e = 0.f, spec = 0.f;
+    if (nDotL > 0.0f) {
+        float falloff = dot(L, L);
+        const float distanceRecip = rsqrt_nr(falloff, rsqT);
+        falloff = rcp_nr(falloff, rcpT);
+        const float distance = rcp_nr(distanceRecip, rcpT);
+        L = scale(L, distanceRecip);
+        nDotL *= distanceRecip;
+        const float Aterm = (l.power * falloff) * (0.25f / 3.1415926f);
+        const float rdl = std_max(0.f, dot(rVec, L));
+        float attenuate = 1.0f;
+        if (l.cast_shadows) {
+            const DRay sr = make_ray(from, L);
+            DHit sh{distance, 0.f, 0.f, -1};
+            shadow_total++;
+            if (traverse<true, COUNT, FAST>(T, sr, 0.001f, sh, st)) attenuate = 0.0f;
+        }
+        attenuate *= nDotL;
+        spec = rdl * attenuate;
+        e = Aterm * attenuate;
+    }
+    const DevMaterial& M = P.mats[mi];
+    const v3 E = mk(e, e, e);
+    const v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
+    v3 sh;
+    if (lambert) {
+        sh = add(add(mk(0, 0, 0), mul(E, kd)), ka);
+    } else {
+        const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
+        const float pw = (M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
+        const v3 Ls = add(mk(0, 0, 0), scale(scale(mul(E, ks), M.spec_amt), pw));
+        const v3 Ld = add(add(mk(0, 0, 0), mul(E, kd)), ka);
+        const v3 z = mk(0, 0, 0);
+        sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), mk(M.le[0], M.le[1], M.le[2]));
+    }
+    return scale(add(mk(0, 0, 0), sh), 1.0f / (float)P.num_paths);
+}
+
+__device__ __forceinline__ void write_pixel(const RenderParams& P, size_t slot, v3 col) {
+    if (P.out_rgb) {
+        float* o = P.out_rgb + 3 * slot;
+        o[0] = col.x; o[1] = col.y; o[2] = col.z;
+    }
+    if (P.out_rgb8) {
+        uint8_t* o8 = P.out_rgb8 + 3 * slot;
+        o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
+    }
+}
+
+// Kernel 2, specialised for one point light and num_paths == 1: shade1_hit of
+// every pixel's hit record (the two-launch path; frame1_kernel fuses both).
 template <bool COUNT, bool FAST, int MINW>
 __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
@@ -237,87 +322,76 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
         const int prim = __float_as_int(hv.w);
         v3 col = mk(P.bg[0], P.bg[1], P.bg[2]);
         if (prim >= 0) {
-            // HitInfo::getAllInfos + Ray::getPoint
             const int f = item_frame(P, item);
-            const CamParams& cam = P.cam[f];
-            const EyeRay er = camera_ray(cam, P.seed + (uint32_t)f, x, y, rsqT);
-            const v3 rayD = er.d;
-            const DRay r = make_ray(er.o, rayD);
-            const PrimShade ps = P.prims[prim];
-            const uint32_t mi = ps.mat;
-            const bool lambert = P.mats[mi].type == MRT_LAMBERT;
-            const float4 A = P.verts[ps.v[0]], B = P.verts[ps.v[1]], C = P.verts[ps.v[2]];
-            const v3 geoN = normalized(cross(mk(B.x - A.x, B.y - A.y, B.z - A.z), mk(C.x - A.x, C.y - A.y, C.z - A.z)), rsqT);
-            const float c = 1.0f - hv.y - hv.z;
-            const float4 n0 = P.normals[ps.n[0]], n1 = P.normals[ps.n[1]], n2 = P.normals[ps.n[2]];
-            const v3 N = normalized(add(add(scale(mk(n0.x, n0.y, n0.z), c), scale(mk(n1.x, n1.y, n1.z), hv.y)),
-                                        scale(mk(n2.x, n2.y, n2.z), hv.z)), rsqT);
-            const v3 from = mk(r.o[0] + hv.x * r.d[0], r.o[1] + hv.x * r.d[1], r.o[2] + hv.x * r.d[2]);
-            // Lambert::shade uses the shading normal and no reflection vector;
-            // Blinn::shade flips to the viewer's side (src/Blinn.cpp:150-170).
-            v3 n = N, rVec = mk(0, 0, 0);
-            if (!lambert) {
-                const v3 viewDir = neg(rayD);
-                float vDotN = dot(viewDir, N);
-                const float vDotGeoN = dot(viewDir, geoN);
-                const bool same = (vDotN * vDotGeoN) >= 0.0f;
-                n = same ? N : geoN;
-                vDotN = same ? vDotN : vDotGeoN;
-                if (vDotN < 0.0f) { vDotN = -vDotN; n = neg(n); }
-                rVec = add(rayD, scale(n, 2.0f * vDotN));
-            }
-            // PointLight::sampleLight (src/PointLight.cpp:8-81), as Shader::point_light
-            const DevLight& l = P.lights[0];
-            v3 L = sub(mk(l.pos[0], l.pos[1], l.pos[2]), from);
-            float nDotL = dot(n, L);
-            float e = 0.f, spec = 0.f;
-            if (nDotL > 0.0f) {
-                float falloff = dot(L, L);
-                const float distanceRecip = rsqrt_nr(falloff, rsqT);
-                falloff = rcp_nr(falloff, rcpT);
-                const float distance = rcp_nr(distanceRecip, rcpT);
-                L = scale(L, distanceRecip);
-                nDotL *= distanceRecip;
-                const float Aterm = (l.power * falloff) * (0.25f / 3.1415926f);
-                const float rdl = std_max(0.f, dot(rVec, L));
-                float attenuate = 1.0f;
-                if (l.cast_shadows) {
-                    const DRay sr = make_ray(from, L);
-                    DHit sh{distance, 0.f, 0.f, -1};
-                    shadow_total++;
-                    if (traverse<true, COUNT, FAST>(T, sr, 0.001f, sh, st)) attenuate = 0.0f;
-                }
-                attenuate *= nDotL;
-                spec = rdl * attenuate;
-                e = Aterm * attenuate;
-            }
-            const DevMaterial& M = P.mats[mi];
-            const v3 E = mk(e, e, e);
-            const v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
-            v3 sh;
-            if (lambert) {
-                sh = add(add(mk(0, 0, 0), mul(E, kd)), ka);
-            } else {
-                const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
-                const float pw = (M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
-                const v3 Ls = add(mk(0, 0, 0), scale(scale(mul(E, ks), M.spec_amt), pw));
-                const v3 Ld = add(add(mk(0, 0, 0), mul(E, kd)), ka);
-                const v3 z = mk(0, 0, 0);
-                sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), mk(M.le[0], M.le[1], M.le[2]));
-            }
-            col = scale(add(mk(0, 0, 0), sh), 1.0f / (float)P.num_paths);
+            const EyeRay er = camera_ray(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
+            col = shade1_hit<COUNT, FAST>(P, T, st, make_ray(er.o, er.d), hv.x, hv.y, hv.z, prim, rcpT, rsqT, shadow_total);
         }
         item_pixel(P, item, lane, x, y, slot);
-        if (P.out_rgb) {
-            float* o = P.out_rgb + 3 * slot;
-            o[0] = col.x; o[1] = col.y; o[2] = col.z;
-        }
-        if (P.out_rgb8) {
-            uint8_t* o8 = P.out_rgb8 + 3 * slot;
-            o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
-        }
+        write_pixel(P, slot, col);
     }
     flush_stats<COUNT, false>(P, st, shadow_total, lane, t0, ntiles);
+}
+
+// Kernel 1+2 fused for one point light and num_paths == 1 (C1-C3): per pixel
+// the camera ray, its closest hit, then shade1_hit (the shadow ray any-hit) in
+// the same lane -- one persistent launch per frame, no hit-record hand-off
+// (the record is written only when the caller asks for hits, P.hits != null),
+// one launch tail instead of two.  Every ray's visits and every operation are
+// those of primary_kernel + shade1_kernel, so the frame is bit-identical.
+template <bool COUNT, bool FAST, int MINW>
+__global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[2048];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    load_tables(P.tables, s_tab, 1024);
+    const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
+    const uint16_t* rcpT = s_tab;
+    const uint16_t* rsqT = P.tables + 2048;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
+    trav_alpha(T, P);
+    TravStats st, ss;   // primary / shadow rays (count mode)
+    uint32_t nhits = 0, shadow_total = 0;
+    unsigned long long wave_steps = 0;
+    TileSched ts(P, wave, lane);
+    uint32_t ntiles = 0;
+    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
+        if (P.wave_log && lane == 0 && ntiles < kLogTiles)
+        {
+            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
+            r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
+            r[4 + kLogTiles + ntiles] = ts.deq_ticks;
+        }
+        ntiles++;
+        int x, y;
+        size_t slot;
+        const uint32_t n0 = st.nodes;
+        const uint64_t tc0 = P.tile_cost ? clock64() : 0;
+        if (item_pixel(P, item, lane, x, y, slot)) {
+            const int f = item_frame(P, item);
+            const EyeRay er = camera_ray(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
+            const DRay r = make_ray(er.o, er.d);
+            DHit h{1e12f, 0.f, 0.f, -1};
+            const bool hit = traverse<false, COUNT, FAST>(T, r, 0.001f, h, st);
+            v3 col = mk(P.bg[0], P.bg[1], P.bg[2]);
+            if (hit) {
+                nhits++;
+                col = shade1_hit<COUNT, FAST>(P, T, ss, r, h.t, h.a, h.b, h.prim, rcpT, rsqT, shadow_total);
+            }
+            item_pixel(P, item, lane, x, y, slot);   // recompute: keeps it out of the traversals' live set
+            if (P.hits) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
+            write_pixel(P, slot, col);
+        }
+        if (P.tile_cost && lane == 0) P.tile_cost[item] = (uint32_t)min(clock64() - tc0, (uint64_t)0xFFFFFFFFu);
+        if (COUNT) {
+            uint32_t dmax = st.nodes - n0;
+            for (int off = 32; off > 0; off >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, off));
+            wave_steps += dmax;
+        }
+    }
+    if (COUNT && lane == 0) atomicAdd(&P.ctr[CTR_WAVE_STEPS_P], wave_steps);
+    flush_stats<COUNT, true>(P, st, nhits, lane, t0, ntiles);
+    flush_stats<COUNT, false>(P, ss, shadow_total, lane, t0, ntiles);
 }
 
 // Batched Scene::trace: one lane per query ray.
@@ -378,6 +452,35 @@ __global__ void unpack_kernel(const int32_t* items, int32_t n_items, const float
     }
 }
 
+// Next frame's tile queue order from this frame's tile costs, slowest first
+// (longest-processing-time-first: the launch then ends on cheap tiles, so its
+// drain -- waves finishing their last tile at falling occupancy -- is short).
+// One workgroup: a 64-bin histogram of the costs on a half-octave scale, bin
+// offsets, then a scatter; the order inside a bin does not matter (every
+// schedule renders the same frame).
+static constexpr int kOrderBins = 64;
+__global__ void __launch_bounds__(1024) tile_order_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
+                                                          int n) {
+    __shared__ uint32_t hist[kOrderBins];
+    const int tid = threadIdx.x;
+    if (tid < kOrderBins) hist[tid] = 0;
+    __syncthreads();
+    auto bin = [](uint32_t c) {   // descending: costly tiles in low bins
+        if (c < 2) return kOrderBins - 1;
+        const int l = 31 - __builtin_clz(c);                 // 1..31
+        const int half = (int)((c >> (l - 1)) & 1u);         // the next bit: half an octave
+        return kOrderBins - 1 - min(kOrderBins - 1, 2 * l + half - 1);
+    };
+    for (int i = tid; i < n; i += 1024) atomicAdd(&hist[bin(cost[i])], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int b = 0; b < kOrderBins; b++) { const uint32_t h = hist[b]; hist[b] = run; run += h; }
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) order[atomicAdd(&hist[bin(cost[i])], 1u)] = (uint32_t)i;
+}
+
 // ------------------------------------------------------------------ device state
 // Launch scratch of one stream: everything a render / trace launch writes
 // besides the caller's outputs.  Two launches on different streams never share
@@ -400,6 +503,10 @@ struct StreamCtx {
     void* chain = nullptr;                   // wavefront chain engine scratch (mrt_chain.hip)
     size_t chain_bytes = 0;
     bool last_was_render = false;
+    bool fused = false;                      // the last render ran frame1_kernel (one launch)
+    uint32_t* tile_cost = nullptr;           // frame1_kernel: per-tile cycles of the last frame on this stream
+    uint32_t* tile_order = nullptr;          //   and the queue order derived from them
+    int tile_cap = 0, order_tiles = 0;       //   capacity; tiles of the frame the order is valid for (0: none)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
 };
 static constexpr int kMaxStreamCtx = 16;
@@ -480,11 +587,15 @@ static int g_near_first = -1;     // any-hit walks take the nearest hit child fi
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
 static int g_chain_mb = 16384;    // chain scratch per stream (MB); larger frames run in chunks of work items
+static int g_fused = 1;           // one point light, one path: frame1_kernel (primary + shading in one launch)
+static int g_frame1_waves = 6;    // frame1_kernel launch-bounds occupancy target: 1 (none), 5..8
+static int g_tile_lpt = 1;        // frame1_kernel: tile queue ordered by the previous frame's tile costs
 
 static inline int fast_box(const DeviceState& d);
 
 static void free_ctx(StreamCtx* c) {
-    void* ptrs[] = {c->gstack, c->ctr, c->wave_log, c->hitbuf, c->rays, c->occl, c->nrays, c->lvl, c->chain};
+    void* ptrs[] = {c->gstack, c->ctr, c->wave_log, c->hitbuf, c->rays, c->occl, c->nrays, c->lvl, c->chain,
+                    c->tile_cost, c->tile_order};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -962,6 +1073,20 @@ static KernelFn shade1_fn(bool c, bool f) {
     return c ? (f ? shade1_kernel<true, true, W> : shade1_kernel<true, false, W>)
              : (f ? shade1_kernel<false, true, W> : shade1_kernel<false, false, W>);
 }
+template <int W>
+static KernelFn frame1_fn(bool c, bool f) {
+    return c ? (f ? frame1_kernel<true, true, W> : frame1_kernel<true, false, W>)
+             : (f ? frame1_kernel<false, true, W> : frame1_kernel<false, false, W>);
+}
+static KernelFn pick_frame1(int w, bool c, bool f) {
+    switch (w) {
+        case 1: return frame1_fn<1>(c, f);
+        case 5: return frame1_fn<5>(c, f);
+        case 7: return frame1_fn<7>(c, f);
+        case 8: return frame1_fn<8>(c, f);
+        default: return frame1_fn<6>(c, f);
+    }
+}
 static KernelFn pick_shade1(int w, bool c, bool f) {
     switch (w) {
         case 1: return shade1_fn<1>(c, f);
@@ -1127,7 +1252,7 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
 // Two launches on `stream`: primary rays -> hit records, then shading with
 // shadow rays.  Events bracket both (kernel_ms covers the whole frame).  With
 // adaptive supersampling (subdivs > 1) one fused launch (kernel 3) instead.
-static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hipStream_t stream) {
+static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hipStream_t stream, bool want_hits) {
     DeviceState& d = *s.dev;
     StreamCtx* cp = nullptr;
     int rc = get_ctx(d, stream, cp);
@@ -1184,11 +1309,40 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         s.last = mrt_stats{};
         return MRT_OK;
     }
+    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst && !d.recursive &&
+                     !d.has_maps;
+    c.fused = one && g_fused;
+    if (c.fused) {   // one launch: camera rays, closest hits, shading, shadow rays
+        if (!want_hits) P.hits = nullptr;
+        const bool lpt = g_tile_lpt && P.mode == 0 && !count && P.sched == 2;
+        if (lpt && P.n_tiles > c.tile_cap) {
+            HIP_OK(hipStreamSynchronize(stream));   // the previous launch may still use them
+            if (c.tile_cost) (void)hipFree(c.tile_cost);
+            if (c.tile_order) (void)hipFree(c.tile_order);
+            c.tile_cost = c.tile_order = nullptr;
+            c.tile_cap = c.order_tiles = 0;
+            HIP_OK(hipMalloc((void**)&c.tile_cost, (size_t)P.n_tiles * sizeof(uint32_t)));
+            HIP_OK(hipMalloc((void**)&c.tile_order, (size_t)P.n_tiles * sizeof(uint32_t)));
+            c.tile_cap = P.n_tiles;
+        }
+        P.tile_cost = lpt ? c.tile_cost : nullptr;
+        P.tile_order = lpt && c.order_tiles == P.n_tiles ? c.tile_order : nullptr;
+        if ((rc = launch(pick_frame1(g_frame1_waves, count, fb)))) return rc;
+        HIP_OK(hipEventRecord(c.evm, stream));
+        if (lpt) {   // the next frame on this stream dequeues this frame's slowest tiles first
+            hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, c.tile_cost, c.tile_order, P.n_tiles);
+            c.order_tiles = P.n_tiles;
+        }
+        c.last_was_render = true;
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipEventRecord(c.ev1, stream));
+        d.last = &c;
+        s.last = mrt_stats{};
+        return MRT_OK;
+    }
     if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst)))) return rc;
     HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
-    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst && !d.recursive &&
-                     !d.has_maps;
     const int max_sh = max_shadow_rays(s);
     // secondary rays and their shadow rays depend on hits along the path: fused kernel
     const bool wave = !one && g_wavefront && max_sh > 0 && max_sh <= kMaxWaveShadow && !d.recursive;
@@ -1662,6 +1816,7 @@ int mrt_scene_set_material_optics(mrt_scene* s, int material, float reflect_amt,
     m.reflect = reflect_amt;
     m.refract = refract_amt;
     m.ior = ior;
+    m.ior3[1] = ior;   // one m_ior[3] in the reference: m_ior[1] is both the optics and the middle dispersion IOR
     s->impl.dev_dirty = true;
     return MRT_OK;
 }
@@ -1794,7 +1949,8 @@ int mrt_render_frame_async(mrt_scene* s, const mrt_camera* cam, const mrt_render
     P.n_tiles = P.tiles_x * ((opts->height + 7) / 8);
     P.out_rgb = d_rgb;
     P.out_rgb8 = d_rgb8;
-    rc = launch_render(S, P, (size_t)opts->width * opts->height, opts->count_visits != 0, (hipStream_t)stream);
+    rc = launch_render(S, P, (size_t)opts->width * opts->height, opts->count_visits != 0, (hipStream_t)stream,
+                       opts->want_hits != 0);
     S.last.primary_rays = (uint64_t)opts->width * opts->height;
     return rc;
 }
@@ -1823,7 +1979,7 @@ int mrt_render_batch_async(mrt_scene* s, const mrt_camera* cams, int32_t n_cams,
     P.out_rgb = d_tiles;
     P.out_rgb8 = d_tiles8;
     if (n_items == 0) return MRT_OK;
-    rc = launch_render(S, P, (size_t)n_items * 1024, opts->count_visits != 0, (hipStream_t)stream);
+    rc = launch_render(S, P, (size_t)n_items * 1024, opts->count_visits != 0, (hipStream_t)stream, opts->want_hits != 0);
     S.last.primary_rays = 0;
     return rc;
 }
@@ -1899,7 +2055,6 @@ static int render_shared(mrt_scene* s, const mrt_camera* cam, const mrt_render_o
         std::vector<float4> hitrec;
     };
     std::vector<Share> sh((size_t)n);
-    std::vector<int> used(n, 0);   // share index within its device (stream per share)
     int rc = MRT_OK;
     for (int k = 0; k < n && rc == MRT_OK; k++) {
         Share& q = sh[k];
@@ -1928,6 +2083,7 @@ static int render_shared(mrt_scene* s, const mrt_camera* cam, const mrt_render_o
         }
         mrt_render_opts o = *opts;
         o.device = q.device; o.devices = nullptr; o.n_devices = 0;
+        o.want_hits = hits ? 1 : 0;
         rc = mrt_render_batch_async(s, cam, 1, &o, q.d_items, (int32_t)ni, q.d_tiles, nullptr, q.stream);
     }
     mrt_stats total{};
@@ -1961,6 +2117,7 @@ static int render_shared(mrt_scene* s, const mrt_camera* cam, const mrt_render_o
         total.primary_hits += st.primary_hits; total.primary_wave_steps += st.primary_wave_steps;
         total.primary_uniform_visits += st.primary_uniform_visits;
         total.kernel_ms = std::max(total.kernel_ms, st.kernel_ms);
+        total.fused = st.fused;
         total.max_stack = std::max(total.max_stack, st.max_stack);
         if (src == MRT_ERR_OVERFLOW) rc = src;
         // scatter the share's buckets into the frame (row 0 = bottom)
@@ -1984,6 +2141,10 @@ static int render_shared(mrt_scene* s, const mrt_camera* cam, const mrt_render_o
         if (q.d_items) (void)hipFree(q.d_items);
         if (q.d_tiles) (void)hipFree(q.d_tiles);
     }
+    // the scene's current replica goes back to the caller's device (mrt_trace /
+    // mrt_trace_async launch on S.dev->device), not the last share's
+    for (DeviceState* d : S.devs)
+        if (d->device == opts->device) S.dev = d;
     if (rc && rc != MRT_ERR_OVERFLOW) return rc;
     total.primary_rays = (uint64_t)W * H;
     S.last = total;
@@ -2023,7 +2184,7 @@ int mrt_render(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
     P.n_tiles = P.tiles_x * ((opts->height + 7) / 8);
     P.out_rgb = d.d_rgb;
     P.out_rgb8 = d.d_rgb8;
-    if ((rc = launch_render(S, P, px, opts->count_visits != 0, nullptr))) return rc;
+    if ((rc = launch_render(S, P, px, opts->count_visits != 0, nullptr, hits != nullptr || opts->want_hits))) return rc;
     HIP_OK(hipMemcpy(rgb, d.d_rgb, px * 12, hipMemcpyDeviceToHost));
     if (rgb8) HIP_OK(hipMemcpy(rgb8, d.d_rgb8, px * 3, hipMemcpyDeviceToHost));
     if (hits) {
@@ -2087,6 +2248,7 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
         }
     }
     S.last.kernel_ms = ms;
+    S.last.fused = x.last_was_render && x.fused ? 1 : 0;
     *out = S.last;
     if (c[CTR_OVERFLOW]) { set_error("traversal stack overflow"); return MRT_ERR_OVERFLOW; }
     return MRT_OK;
@@ -2233,6 +2395,13 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "refill_min") {
         if (value < 1 || value > 64) { set_error("refill_min must be 1..64"); return MRT_ERR_INVALID; }
         g_refill_min = value;
+    } else if (k == "fused") {
+        g_fused = value ? 1 : 0;
+    } else if (k == "tile_lpt") {
+        g_tile_lpt = value ? 1 : 0;
+    } else if (k == "frame1_waves") {
+        if (value != 1 && (value < 5 || value > 8)) { set_error("frame1_waves must be 1 or 5..8"); return MRT_ERR_INVALID; }
+        g_frame1_waves = value;
     } else if (k == "sched") {
         if (value < 0 || value > 3) { set_error("sched must be 0..3"); return MRT_ERR_INVALID; }
         g_sched = value;

@@ -91,6 +91,12 @@ struct RenderParams {
     int32_t cus;                 // compute units (slot of a persistent block = blockIdx / cus)
     int32_t scalar_nodes;        // scalar fetch of wave-uniform nodes
     unsigned int* queue;         // 8 tile counters, 32 words apart (sched >= 2)
+    // cost-ordered tile queue (frame1_kernel, frame mode): dequeue rank r hands
+    // out tile tile_order[r] (the previous frame's slowest tiles first, so the
+    // launch drains on cheap tiles); tile_cost[t] receives this frame's cycles
+    // per tile for the next frame's order.  Either may be null.
+    const uint32_t* tile_order;
+    uint32_t* tile_cost;
     // work: 8x8 tiles
     int32_t tiles_x, n_tiles;    // frame mode: tiles_x = ceil(W/8)
     const int32_t* buckets;      // bucket mode: bucket ids (row-major bucket grid)
@@ -946,7 +952,7 @@ struct TileSched {
                 const unsigned v = atomicAdd(P.queue + c * 32, 1u);
                 const long idx = (mode == 3) ? (v < (unsigned)band ? (long)c * band + v : (long)P.n_tiles)
                                              : (long)c + 8l * v;
-                if (idx < P.n_tiles) { item = (int)idx; break; }
+                if (idx < P.n_tiles) { item = P.tile_order ? (int)P.tile_order[idx] : (int)idx; break; }
                 probe++;
             }
         }

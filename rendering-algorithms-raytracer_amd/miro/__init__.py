@@ -406,8 +406,9 @@ def makeMBMeshObjs(scene: "Scene", mesh: TriangleMesh, mesh2: TriangleMesh, mate
     """makeMBMeshObjs (src/main.cpp:23, :202): one MBObject(material, mesh, mesh2, i)
     per triangle (src/MBObject.cpp:7-11) -- mesh at time 0, mesh2 (same topology)
     at time 1; a ray of time t meets the blend t * mesh2 + (1 - t) * mesh."""
-    scene.addMesh(mesh, material)
-    scene._motion[id(mesh)] = mesh2
+    # mesh2 rides on this entry only: other entries of the same TriangleMesh
+    # (makeMeshObjs) stay static, as their Objects are plain Objects
+    scene._meshes.append((mesh, material, mesh2))
 
 
 class Objects(list):
@@ -448,8 +449,7 @@ class Scene:
     HitInfo are global triangle indices in insertion order."""
 
     def __init__(self, device: int = 0):
-        self._meshes: List[tuple] = []
-        self._motion: dict = {}          # id(time-0 mesh) -> time-1 mesh (makeMBMeshObjs)
+        self._meshes: List[tuple] = []   # (mesh, material) / (mesh, material, time-1 mesh) / (ProxyObject, None)
         self._lights: List[_Light] = []
         self.bg = Vector3(0)
         self.m_numPaths = 1
@@ -551,12 +551,12 @@ class Scene:
         self.blas_build_ms = 0.0
         self.blas_prims = 0
         self.blas_ids = blas
-        motion = self._motion
-        for item, mat in self._meshes:
+        for entry in self._meshes:
+            item, mat = entry[0], entry[1]
             if not isinstance(item, ProxyObject):
                 mesh_id = add_mesh(item, mat)
-                if id(item) in motion:
-                    set_motion(mesh_id, motion[id(item)])
+                if len(entry) > 2:   # makeMBMeshObjs: MBObjects of this entry only
+                    set_motion(mesh_id, entry[2])
                 continue
             key = id(item.bvh)
             if key not in blas:

@@ -21,7 +21,7 @@ import os
 import re
 from collections import defaultdict
 
-PASS = {"primary_kernel": "primary", "shade1_kernel": "shade", "shade_kernel": "shade", "shadow_kernel": "shade",
+PASS = {"primary_kernel": "primary", "frame1_kernel": "primary", "shade1_kernel": "shade", "shade_kernel": "shade", "shadow_kernel": "shade",
         "adaptive_kernel": "shade", "chain_trace_kernel": "shade", "chain0_kernel": "shade",
         "chain_shade_kernel": "shade", "chain_compact_kernel": "shade", "chain_finish_kernel": "shade"}
 # kernels without a COUNT template argument: the instrumented frame runs the same
@@ -71,7 +71,7 @@ def summarise(cfg, root):
         n = 0
         for k, cs in per.items():
             base, targs = parse_name(k)
-            if base in ("primary_kernel", "adaptive_kernel") and cs.get(counter):
+            if base in ("primary_kernel", "adaptive_kernel", "frame1_kernel") and cs.get(counter):
                 if not timed_only or targs.split(",")[0].strip() == "false":
                     n += len(cs[counter])
         return max(1, n)
