@@ -15,14 +15,14 @@ overlaps the start of the next frame.
 N > 1: one process per GPU (torch.distributed, backend nccl = RCCL).  `python
 bench.py --gpus N` spawns the N ranks itself when WORLD_SIZE is not set (the
 parent never touches torch or HIP); under torch.distributed.run WORLD_SIZE must
-equal --gpus.  The headline `value` is weak scaling: a step renders a camera
-path of N frames (frame 0 is the config camera, then 2.5-degree pans), the
-32x32 buckets of all N frames are dealt id mod N (reference bucket grid,
-src/Scene.cpp:90-95), every rank renders its share in one launch pair into
-packed 8-bit tiles, one RCCL gather per step brings them to rank 0, which
-scatters them into the N frames; the gather of step k overlaps the render of
-step k + 1 (miro/tiles.py BatchPipeline).  `strong` times the north-star split
-of ONE frame: its buckets dealt id mod N, float tiles gathered to rank 0.
+equal --gpus.  The headline `value` is the north-star split (strong scaling):
+ONE frame per step, its 32x32 buckets dealt id mod N (reference bucket grid,
+src/Scene.cpp:90-95), every rank renders its share in one launch into packed
+float tiles, one RCCL gather of the framebuffer brings them to rank 0, which
+scatters them into the frame; the gather of step k overlaps the render of
+step k + 1 (miro/tiles.py BatchPipeline).  `split_times` gives each rank's
+render and the gather alone; `weak` times a camera path of N frames per step
+(buckets of all N frames dealt id mod N, 8-bit tiles), i.e. weak scaling.
 
 value = rays of all frames of all steps / max-over-ranks wall time.  Rank 0
 prints one JSON line.
@@ -44,7 +44,10 @@ sys.path.insert(0, os.path.join(ROOT, "rendering-algorithms-raytracer_amd"))
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 ~34.5 TB/s aggregate
 NODE_B, LEAF_B = 128, 160      # QNode / DLeaf bytes (csrc/mrt_types.h)
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+# rocprofv3 evidence of this round (tools/prof_all.sh + tools/prof3.py): per config and
+# bench pass, HBM bytes per launch (PMC) and the rocprof average duration at one
+# frame in flight; per kernel, the SQ / TCP latency counters
+PROFILE_FILE = os.path.join(ROOT, "profiles", "r03_profile.json")
 CPU_CAL_FILE = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
 
 
@@ -61,7 +64,10 @@ def parse():
                          "streams, so one frame's launch tail overlaps the next frame's start)")
     ap.add_argument("--path", choices=["auto", "batch"], default="auto",
                     help="batch: use the bucket-batch path even for one frame on one GPU (A/B)")
-    ap.add_argument("--strong-steps", type=int, default=0, help="N > 1: single-frame steps timed (default --steps)")
+    ap.add_argument("--split", choices=["frame", "batch"], default="frame",
+                    help="N > 1: frame = one frame per step split over the GPUs (headline); batch = N frames per step "
+                         "(weak scaling; also reported as the `weak` key of a frame-split line)")
+    ap.add_argument("--strong-steps", type=int, default=0, help="N > 1: steps of the secondary (weak) measurement")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-thread-seconds for the oracle sample")
     return ap.parse_args()
 
@@ -232,8 +238,12 @@ def cpu_baseline(cfg_key, seconds):
         y += band
         frames += 1
     value = rays / t_total / 1e6
+    omp = os.environ.get("OMP_NUM_THREADS")
     out = {"value": round(value, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
            "cpu": cpu_model(), "affinity_cpus": len(os.sched_getaffinity(0)),
+           "cores_reason": (f"OMP_NUM_THREADS={omp}: the CPU share the GPU pool grants one GPU's job (the affinity "
+                            f"mask lists the whole host, whose other cores belong to other GPUs' jobs)")
+           if omp and omp.isdigit() and int(omp) < len(os.sched_getaffinity(0)) else "every core in the affinity mask",
            "sample": f"{cfg_key} {W}x{H}: {frames} bands of {band} rows ({rays} rays, {t_total:.1f} s wall, "
                      f"{threads} OpenMP threads, oracle/mrt_oracle.c -O2)"}
     if os.path.exists(CPU_CAL_FILE):   # oracle vs the reference's own 1-thread rate, same Xeon
@@ -242,7 +252,9 @@ def cpu_baseline(cfg_key, seconds):
         out["calibration"] = (f"x{cal['ratio_reference_over_oracle']}: the reference renders explosion01 1920x1080 "
                               f"at {cal['reference_mray_s'][0]}-{cal['reference_mray_s'][1]} Mray/s on 1 thread, the "
                               f"oracle at {cal['oracle_mray_s']} on the same {cal['cpu']} "
-                              f"(profiles/r02_cpu_calibration.json)")
+                              f"(profiles/r02_cpu_calibration.json); ASSUMED to carry over to this host's CPU: the "
+                              f"reference (SSE, MSVC-shaped) cannot be built or run on the GPU box, so the ratio is "
+                              f"measured on the build container's Intel CPU only")
     return out
 
 
@@ -257,14 +269,12 @@ def _scene_setup(scene):
             "blas_prims": getattr(scene, "blas_prims", 0)}
 
 
-def pmc_traffic(config):
-    """HBM bytes per launch of each pass, from the committed rocprofv3 --pmc
-    passes of this config (tools/pmc.sh + tools/pmc_summary.py)."""
-    if not os.path.exists(PMC_FILE):
-        return None, None
-    prof = json.load(open(PMC_FILE))
-    entry = prof.get("configs", {}).get(config)
-    return (entry or {}).get("per_launch_hbm_bytes"), prof.get("source", {}).get(config)
+def profile_evidence(config):
+    """This config's tracked rocprofv3 record (profiles/r03_profile.json): per pass
+    {hbm_bytes, avg_us, kernels}, per kernel {latency, code_object, ...}, source."""
+    if not os.path.exists(PROFILE_FILE):
+        return None
+    return json.load(open(PROFILE_FILE)).get("configs", {}).get(config)
 
 
 # ------------------------------------------------------------------ worker
@@ -297,11 +307,15 @@ def main():
     W, H = cfg["W"], cfg["H"]
     L = miro.lib()
     stream = torch.cuda.current_stream()
-    # frames per step: 1 at N = 1; N > 1 renders a camera path of N frames per
-    # step (weak scaling: one frame of work per GPU per step), every frame's
-    # buckets dealt over all ranks, 8-bit tiles gathered once per step
-    n_frames = args.frames or (1 if world == 1 else min(world, 16))
-    cams = [cam] if n_frames == 1 else [_camera(c) for c in scenes.camera_path(cfg["camera"], n_frames)]
+    # N = 1: one frame per step through the whole-frame path.  N > 1 (default
+    # --split frame): the north-star split, ONE frame per step, its 32x32 buckets
+    # dealt id mod N, float tiles, one RCCL gather of the framebuffer to rank 0,
+    # consecutive frames double-buffered (BatchPipeline); --split batch: weak
+    # scaling, a camera path of N frames per step (8-bit tiles), measured as the
+    # secondary key of the split line.
+    # (--path batch at N = 1 runs the split path on one GPU: same pipeline, N = 1)
+    split = (world > 1 and args.split == "frame") or (world == 1 and args.path == "batch")
+    n_frames = 1 if (world == 1 or split) else (args.frames or min(world, 16))
     bx, by = (W + 31) // 32, (H + 31) // 32
     bpf = bx * by
     use_frame_path = world == 1 and n_frames == 1 and args.path == "auto"
@@ -309,150 +323,141 @@ def main():
     streams = [stream] + [torch.cuda.Stream() for _ in range(inflight - 1)]
     frame = [torch.empty(H * W * 3, dtype=torch.float32, device="cuda") for _ in range(inflight)]
     frame8 = [torch.empty(H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(inflight)]
-    frames8 = [frame8[0]] if use_frame_path else \
-        [torch.empty(n_frames * H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(2)]
-    camc = (_lib.mrt_camera * n_frames)(*[c._c() for c in cams])
     opts_count = _lib.mrt_render_opts(W, H, dev, 1, 1, 0, 0)
     opts = _lib.mrt_render_opts(W, H, dev, 0, 1, 0, 0)
+    camc = (_lib.mrt_camera * 1)(cam._c())
 
-    def render_items(ids, n, cams_, n_cams, tiles_f, tiles_8, o=opts):
-        _lib.check(L.mrt_render_batch_async(scene.handle, cams_, n_cams, C.byref(o), ids.data_ptr(), n,
-                                            tiles_f, tiles_8, torch.cuda.current_stream().cuda_stream), "render batch")
-
-    if not use_frame_path:
-        # this rank's items, unpadded; the gather needs equal sizes, so every rank's
-        # buffer holds `per` slots and the unused ones are unpacked as id -1 (skipped)
-        mine = tiles_mod.rank_buckets(bpf * n_frames, world, rank)
-        per = -(-bpf * n_frames // world)
+    def make_pipe(nf, float_tiles):
+        """This rank's share of an nf-frame step (items id mod N), its render /
+        unpack closures and the double-buffered gather pipeline."""
+        cams_ = [cam] if nf == 1 else [_camera(c) for c in scenes.camera_path(cfg["camera"], nf)]
+        cc = (_lib.mrt_camera * nf)(*[c._c() for c in cams_])
+        mine, all_ids, per = tiles_mod.split_items(bpf * nf, world, rank)
         items = torch.tensor(mine, dtype=torch.int32, device="cuda")
-        all_items = torch.tensor([i for r in range(world) for i in tiles_mod.padded_items(bpf * n_frames, world, r)],
-                                 dtype=torch.int32, device="cuda")
+        all_items = torch.tensor(all_ids, dtype=torch.int32, device="cuda")
+        out_f = [torch.empty(nf * H * W * 3, dtype=torch.float32, device="cuda") for _ in range(2)] if float_tiles \
+            else None
+        out_8 = [torch.empty(nf * H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        dt = torch.float32 if float_tiles else torch.uint8
 
         def render(ids, out, o=opts):
-            render_items(ids, len(mine), camc, n_frames, None, out.data_ptr(), o)
+            tf, t8 = (out.data_ptr(), None) if float_tiles else (None, out.data_ptr())
+            _lib.check(L.mrt_render_batch_async(scene.handle, cc, nf, C.byref(o), ids.data_ptr(), len(mine), tf, t8,
+                                                torch.cuda.current_stream().cuda_stream), "render batch")
 
         def unpack(ids, gathered, b):
-            _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(ids), None, gathered.data_ptr(), W, H, n_frames,
-                                                None, frames8[b].data_ptr(), scene.handle,
-                                                torch.cuda.current_stream().cuda_stream), "unpack")
+            gf, g8 = (gathered.data_ptr(), None) if float_tiles else (None, gathered.data_ptr())
+            _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(ids), gf, g8, W, H, nf,
+                                                out_f[b].data_ptr() if float_tiles else None, out_8[b].data_ptr(),
+                                                scene.handle, torch.cuda.current_stream().cuda_stream), "unpack")
 
-        # two streams: consecutive steps' launch pairs overlap (libmrt keeps scratch per stream)
+        # two streams: consecutive steps' launches overlap (libmrt keeps scratch per stream)
         pipe = tiles_mod.BatchPipeline(world, rank, dist, items, all_items,
-                                       lambda k: torch.empty(k * per * 1024 * 3, dtype=torch.uint8, device="cuda"),
+                                       lambda k: torch.empty(k * per * 1024 * 3, dtype=dt, device="cuda"),
                                        render, unpack, streams=[torch.cuda.Stream(), torch.cuda.Stream()])
+        for b in range(2):   # per-stream scratch allocated before any timing
+            with torch.cuda.stream(pipe.streams[b]):
+                render(items, pipe.tiles[b])
+        torch.cuda.synchronize()
+        return pipe, render, items, mine, out_f
+
+    def count_rays(render_count):
+        """Rays of one step over all ranks from an instrumented launch (+ this rank's stats)."""
+        render_count()
+        torch.cuda.synchronize()
+        st_ = scene.stats()
+        adaptive_ = bool(cfg.get("subdivs")) and max(cfg["subdivs"][:2]) > 1
+        v = [st_["shadow_rays"], st_["primary_rays"] if adaptive_ else 0, st_["secondary_rays"]]
+        if world > 1:
+            t_ = torch.tensor(v, dtype=torch.float64, device="cuda")
+            dist.all_reduce(t_)
+            v = [int(x) for x in t_.tolist()]
+        return st_, v
+
+    def timed(step_fn, flush, k):
+        for _ in range(args.warmup):
+            step_fn()
+        flush()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0_ = time.perf_counter()
+        for _ in range(k):
+            step_fn()
+        flush()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        e = time.perf_counter() - t0_
+        if world > 1:
+            t_ = torch.tensor([e], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t_, op=dist.ReduceOp.MAX)
+            e = t_.item()
+        return e
 
     nstep = [0]
 
-    def frame_step(o, serial=False):
+    def frame_step(o=opts, serial=False):
         i = 0 if serial else nstep[0] % inflight
         nstep[0] += 1
         _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(o), frame[i].data_ptr(),
                                             frame8[i].data_ptr(), streams[i].cuda_stream), "render")
 
-    def step(o, serial=False):
-        if use_frame_path:
-            frame_step(o, serial)
-        elif o is opts_count:
-            render(items, pipe.tiles[0], opts_count)     # instrumented launch only (no gather)
-        else:
-            pipe.step()
-
-    # setup: every in-flight stream renders once, so libmrt's per-stream scratch
-    # (hit records, stacks, counters) is allocated before the warmup / timed steps
+    adaptive = bool(cfg.get("subdivs")) and max(cfg["subdivs"][:2]) > 1
     if use_frame_path:
+        # setup: every in-flight stream renders once, so libmrt's per-stream scratch
+        # (hit records, stacks, counters) is allocated before the warmup / timed steps
         for i in range(inflight):
             _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(opts), frame[i].data_ptr(),
                                                 frame8[i].data_ptr(), streams[i].cuda_stream), "render")
+        torch.cuda.synchronize()
+        st, (shadow_total, eye_total, second_total) = count_rays(lambda: frame_step(opts_count, serial=True))
+        mine, items = None, None
+        elapsed = timed(frame_step, lambda: None, args.steps)
     else:
-        for b in range(2):
-            with torch.cuda.stream(pipe.streams[b]):
-                render(items, pipe.tiles[b])
-    torch.cuda.synchronize()
-    # instrumented frame: node/leaf visits + per-launch times (not timed below)
-    step(opts_count, serial=True)
-    torch.cuda.synchronize()
-    st = scene.stats()
-    shadow_mine = st["shadow_rays"]
-    # adaptive supersampling (subdivs > 1): eye rays per pixel vary, counted by the kernel
-    adaptive = bool(cfg.get("subdivs")) and max(cfg["subdivs"][:2]) > 1
-    eye_mine = st["primary_rays"] if adaptive else 0
-    second_mine = st["secondary_rays"]   # Blinn reflection / refraction / GI rays
-    if world > 1:
-        t = torch.tensor([shadow_mine, eye_mine, second_mine], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t)
-        shadow_total, eye_total, second_total = int(t[0].item()), int(t[1].item()), int(t[2].item())
-    else:
-        shadow_total, eye_total, second_total = shadow_mine, eye_mine, second_mine
+        pipe, render, items, mine, _ = make_pipe(n_frames, float_tiles=split)
+        st, (shadow_total, eye_total, second_total) = count_rays(lambda: render(items, pipe.tiles[0], opts_count))
+        elapsed = timed(pipe.step, pipe.flush, args.steps)
+    shadow_mine, eye_mine, second_mine = st["shadow_rays"], (st["primary_rays"] if adaptive else 0), st["secondary_rays"]
     primary_total = eye_total if adaptive else n_frames * W * H
     rays_per_step = primary_total + shadow_total + second_total      # all frames of the batch, all ranks
     hits_px = st["primary_hits"]
 
-    for _ in range(args.warmup):
-        step(opts)
-    if not use_frame_path:
-        pipe.flush()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(opts)
-    if not use_frame_path:
-        pipe.flush()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-
-    # strong scaling: ONE frame per step, its buckets dealt id mod N, float tiles
-    # gathered to rank 0 and scattered into the frame (the north-star split)
-    strong = None
-    if world > 1:
-        sb = tiles_mod.rank_buckets(bpf, world, rank)
-        sper = -(-bpf // world)
-        s_items = torch.tensor(sb, dtype=torch.int32, device="cuda")
-        s_all = torch.tensor([i for r in range(world) for i in tiles_mod.padded_items(bpf, world, r)],
-                             dtype=torch.int32, device="cuda")
-        s_tiles = torch.empty(sper * 1024 * 3, dtype=torch.float32, device="cuda")
-        s_recv = torch.empty(world * sper * 1024 * 3, dtype=torch.float32, device="cuda") if rank == 0 else None
-        cam1 = (_lib.mrt_camera * 1)(cams[0]._c())
-
-        def strong_step():
-            render_items(s_items, len(sb), cam1, 1, s_tiles.data_ptr(), None)
-            dist.gather(s_tiles, list(s_recv.chunk(world)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                _lib.check(L.mrt_unpack_batch_async(s_all.data_ptr(), len(s_all), s_recv.data_ptr(), None, W, H, 1,
-                                                    frame[0].data_ptr(), frame8[0].data_ptr(), scene.handle,
-                                                    torch.cuda.current_stream().cuda_stream), "unpack strong")
-
-        render_items(s_items, len(sb), cam1, 1, s_tiles.data_ptr(), None, opts_count)
-        torch.cuda.synchronize()
-        sst = scene.stats()
-        t = torch.tensor([sst["shadow_rays"], sst["secondary_rays"]], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t)
-        s_rays = W * H + int(t[0].item()) + int(t[1].item())
-        for _ in range(max(1, args.warmup)):
-            strong_step()
-        torch.cuda.synchronize()
-        dist.barrier()
-        k_strong = args.strong_steps or args.steps
-        t0 = time.perf_counter()
-        for _ in range(k_strong):
-            strong_step()
-        torch.cuda.synchronize()
-        dist.barrier()
-        se = time.perf_counter() - t0
-        t = torch.tensor([se], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        se = t.item()
-        strong = {"value": round(s_rays * k_strong / se / 1e6, 2), "unit": "Mray/s", "frames_per_step": 1,
-                  "steps": k_strong, "ms_per_frame": round(se / k_strong * 1e3, 4), "rays_per_frame": s_rays,
-                  "split": f"one {W}x{H} frame, 32x32 buckets dealt id mod {world}, float32 tiles gathered to rank 0 "
-                           f"(RCCL) and unpacked there, serial steps"}
+    # N > 1: per-rank render and gather times of the split (median of 5, each
+    # alone: render = HIP events of one launch on this rank's stream, gather =
+    # one RCCL gather of the tile buffer between barriers), and the weak-scaling
+    # batch of N frames per step as the secondary key
+    split_times, weak = None, None
+    if world > 1 and split:
+        r_ms, g_ms = [], []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            dist.barrier()
+            e0.record()
+            render(items, pipe.tiles[0])
+            e1.record()
+            torch.cuda.synchronize()
+            r_ms.append(e0.elapsed_time(e1))
+            dist.barrier()
+            tg = time.perf_counter()
+            dist.gather(pipe.tiles[0], list(pipe.recv[0].chunk(world)) if rank == 0 else None, dst=0)
+            torch.cuda.synchronize()
+            g_ms.append((time.perf_counter() - tg) * 1e3)
+        t_ = torch.tensor([float(np.median(r_ms)), float(np.median(g_ms))], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t_, op=dist.ReduceOp.MAX)
+        split_times = {"render_ms_max_rank": round(t_[0].item(), 4), "gather_ms": round(t_[1].item(), 4),
+                       "gather_bytes_per_rank": int(pipe.tiles[0].numel() * 4)}
+        nf_w = args.frames or min(world, 16)
+        wpipe, wrender, witems, _, _ = make_pipe(nf_w, float_tiles=False)
+        _, (wsh, weye, wsec) = count_rays(lambda: wrender(witems, wpipe.tiles[0], opts_count))
+        w_rays = (weye if adaptive else nf_w * W * H) + wsh + wsec
+        k_w = args.strong_steps or args.steps
+        we = timed(wpipe.step, wpipe.flush, k_w)
+        weak = {"value": round(w_rays * k_w / we / 1e6, 2), "unit": "Mray/s", "scaling": "weak",
+                "frames_per_step": nf_w, "steps": k_w, "ms_per_step": round(we / k_w * 1e3, 4),
+                "split": f"{nf_w}-frame camera path per step, 32x32 buckets of all frames dealt id mod {world}, one "
+                         f"RCCL gather of 8-bit tiles per step (double-buffered)"}
 
     # per-launch durations of the uninstrumented kernels (HIP events on the
     # launch's stream), and the latency of one frame with nothing else in flight
@@ -461,7 +466,7 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         if use_frame_path:
-            step(opts, serial=True)
+            frame_step(opts, serial=True)
         else:
             render(items, pipe.tiles[0])
         torch.cuda.synchronize()
@@ -479,7 +484,7 @@ def main():
     chain = scenes.chain_level(cfg)
     one_light = (len(cfg["lights"]) == 1 and cfg["lights"][0]["type"] == "point" and cfg.get("num_paths", 1) == 1
                  and not cfg.get("env") and chain == 0 and not cfg.get("extra"))
-    b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=use_frame_path,
+    b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=use_frame_path or split,
                                    wavefront=not one_light and chain == 0)
     if chain:   # each secondary / GI hit gathers its PrimShade + 3 vertices + 3 normals (+ its level record)
         b_shade += second_mine * (16 + 32 + 3 * 16 + 3 * 16 + 12)
@@ -492,7 +497,7 @@ def main():
         dom, dom_key, dom_ms = ("frame1_kernel (camera rays + closest hit + shading + any-hit shadow rays, "
                                 "one launch)"), "primary", pm
         dom_b = (st["node_visits"] * NODE_B + st["leaf_visits"] * LEAF_B
-                 + px_mine * ((12 if use_frame_path else 0) + 3) + hits_px * (32 + 3 * 16 + 3 * 16))
+                 + px_mine * ((12 if use_frame_path or split else 0) + 3) + hits_px * (32 + 3 * 16 + 3 * 16))
     elif adaptive:   # one fused launch: eye rays, shading, inline shadow rays (its time is shade_ms)
         dom, dom_key, dom_ms = "adaptive_kernel (eye rays + shading + any-hit shadow rays)", "shade", sm
         dom_b = (st["node_visits"] * NODE_B + st["leaf_visits"] * LEAF_B
@@ -502,13 +507,31 @@ def main():
     else:
         dom, dom_key, dom_ms, dom_b = "primary_kernel (camera rays, closest hit)", "primary", pm, b_prim
     achieved = dom_b / (dom_ms * 1e-3) / 1e9
-    traffic, pmc_src = pmc_traffic(args.config) if use_frame_path else (None, None)
-    dom_traffic = (traffic or {}).get(dom_key)
+    prof = profile_evidence(args.config) if use_frame_path else None
+    ppass = ((prof or {}).get("passes") or {}).get(dom_key) or {}
+    dom_traffic = ppass.get("hbm_bytes") or None
     hbm = None
     if dom_traffic:
         hbm_gbs = dom_traffic / (dom_ms * 1e-3) / 1e9
         hbm = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": int(dom_traffic), "source": pmc_src}
+               "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": int(dom_traffic),
+               "source": prof.get("source")}
+    # the tracked rocprofv3 average of the same pass (one frame in flight): the
+    # fraction recomputed from it must agree with `frac` (HIP events, live)
+    tracked = None
+    if ppass.get("avg_us"):
+        f_t = dom_b / (ppass["avg_us"] * 1e-6) / 1e9 / L2_PEAK_GBS
+        tracked = {"avg_us": ppass["avg_us"], "frac": round(f_t, 4), "kernels": ppass.get("kernels"),
+                   "source": prof.get("source")}
+    # latency evidence of the pass's longest kernel (SQ wave-state shares, VALU busy,
+    # L2 requests per vector load): why neither bandwidth roofline binds
+    latency = None
+    for kname, ent in sorted(((prof or {}).get("kernels") or {}).items(), key=lambda kv: -kv[1].get("avg_us", 0)):
+        if kname in (ppass.get("kernels") or []) and ent.get("latency"):
+            latency = dict(ent["latency"], kernel=kname)
+            if ent.get("code_object"):
+                latency["code_object"] = ent["code_object"]
+            break
     # primary-kernel lanes doing node work per issued wave step (adaptive: no primary launch)
     lane_util = round(st["primary_node_visits"] / (64 * st["primary_wave_steps"]), 4) if st["primary_wave_steps"] else None
     out = {
@@ -516,7 +539,9 @@ def main():
                    f"Mray/s (primary+shadow{'+secondary' if second_total else ''}) [{args.config}: {cfg['name']}]"),
         "value": round(value, 2), "unit": "Mray/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        # N = 1 and the split: one frame per step whatever N is (total work fixed);
+        # --split batch: N frames per step (work per GPU fixed)
+        "scaling": "strong" if (world == 1 or split) else "weak", "vs_baseline": None, "dtype": "f32",
         "data": ("synthetic (deterministic %s stand-in, %d tris; %s.obj is not in the reference snapshot%s)"
                  % ({"sponza": "Sponza", "bunny": "bunny", "instances": "dragon_2 / buddha_smooth"}.get(
                      cfg["mesh"], cfg["mesh"]), scene.bvh_info["prims"],
@@ -530,8 +555,11 @@ def main():
                    "qbvh_nodes": scene.bvh_info["nodes"], "qbvh_leaves": scene.bvh_info["leaves"],
                    "frames_in_flight": inflight,
                    "parallelism": "single GPU, whole frame" if use_frame_path else
-                   f"{n_frames}-frame camera path per step, 32x32 buckets dealt id mod {world}, "
-                   f"one RCCL gather of 8-bit tiles per step (double-buffered)"},
+                   (f"one {W}x{H} frame per step split over {world} GPUs: its 32x32 buckets dealt id mod {world} "
+                    f"(src/Scene.cpp:90-174), float32 tiles, one RCCL gather of the framebuffer to rank 0 per frame, "
+                    f"consecutive frames double-buffered" if split else
+                    f"{n_frames}-frame camera path per step, 32x32 buckets dealt id mod {world}, "
+                    f"one RCCL gather of 8-bit tiles per step (double-buffered)")},
         # The traversal is bound by latency along each wave's dependent chain
         # (~35% VALU busy, 41% memory wait); its algorithmic bytes
         # are served by L1/L2, so the ceiling they are priced against is the L2
@@ -539,7 +567,7 @@ def main():
         "roofline": {"bound": "l2", "kernel": dom, "achieved": round(achieved, 1), "peak": L2_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / L2_PEAK_GBS, 4),
                      "traffic": None if dom_traffic is None else int(dom_traffic),
-                     "hbm": hbm, "lane_util": lane_util,
+                     "hbm": hbm, "tracked_profile": tracked, "latency": latency, "lane_util": lane_util,
                      "launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(dom_b),
                      "visits_per_ray": round(st["node_visits"] / max(1, (eye_mine if adaptive else px_mine)
                                                                     + shadow_mine + second_mine), 3)},
@@ -553,8 +581,10 @@ def main():
                            for k in ("primary_span_us", "primary_ramp_us", "primary_tail_us",
                                      "shade_span_us", "shade_ramp_us", "shade_tail_us")},
     }
-    if strong is not None:
-        out["strong"] = strong
+    if split_times is not None:
+        out["split_times"] = split_times
+    if weak is not None:
+        out["weak"] = weak
     if not args.no_cpu_baseline and world == 1:
         try:
             out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)

@@ -455,30 +455,63 @@ __global__ void unpack_kernel(const int32_t* items, int32_t n_items, const float
 // Next frame's tile queue order from this frame's tile costs, slowest first
 // (longest-processing-time-first: the launch then ends on cheap tiles, so its
 // drain -- waves finishing their last tile at falling occupancy -- is short).
-// One workgroup: a 64-bin histogram of the costs on a half-octave scale, bin
-// offsets, then a scatter; the order inside a bin does not matter (every
-// schedule renders the same frame).
-static constexpr int kOrderBins = 64;
+// One workgroup of 16 waves: a 64-bin histogram of the costs on a half-octave
+// scale (one copy per wave, so LDS atomics rarely collide), bin offsets, then a
+// scatter; the order inside a bin does not matter (every schedule renders the
+// same frame).  Each thread keeps kOrderBatch bins in registers, so the cost
+// loads of a batch are in flight together.
+static constexpr int kOrderBins = 64, kOrderWaves = 16, kOrderBatch = 16;
+__device__ __forceinline__ int order_bin(uint32_t c) {   // descending: costly tiles in low bins
+    if (c < 2) return kOrderBins - 1;
+    const int l = 31 - __builtin_clz(c);              // 1..31
+    const int half = (int)((c >> (l - 1)) & 1u);      // the next bit: half an octave
+    return kOrderBins - 1 - min(kOrderBins - 1, 2 * l + half - 1);
+}
 __global__ void __launch_bounds__(1024) tile_order_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
                                                           int n) {
-    __shared__ uint32_t hist[kOrderBins];
-    const int tid = threadIdx.x;
-    if (tid < kOrderBins) hist[tid] = 0;
+    __shared__ uint32_t hist[kOrderBins * kOrderWaves];   // [bin][wave]
+    const int tid = threadIdx.x, wave = tid >> 6;
+    hist[tid] = 0;
     __syncthreads();
-    auto bin = [](uint32_t c) {   // descending: costly tiles in low bins
-        if (c < 2) return kOrderBins - 1;
-        const int l = 31 - __builtin_clz(c);                 // 1..31
-        const int half = (int)((c >> (l - 1)) & 1u);         // the next bit: half an octave
-        return kOrderBins - 1 - min(kOrderBins - 1, 2 * l + half - 1);
-    };
-    for (int i = tid; i < n; i += 1024) atomicAdd(&hist[bin(cost[i])], 1u);
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t run = 0;
-        for (int b = 0; b < kOrderBins; b++) { const uint32_t h = hist[b]; hist[b] = run; run += h; }
+    for (int base = 0; base < n; base += 1024 * kOrderBatch) {
+        int bin[kOrderBatch];
+#pragma unroll
+        for (int j = 0; j < kOrderBatch; j++) {
+            const int i = base + j * 1024 + tid;
+            bin[j] = i < n ? order_bin(cost[i]) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < kOrderBatch; j++)
+            if (bin[j] >= 0) atomicAdd(&hist[bin[j] * kOrderWaves + wave], 1u);
     }
     __syncthreads();
-    for (int i = tid; i < n; i += 1024) order[atomicAdd(&hist[bin(cost[i])], 1u)] = (uint32_t)i;
+    {   // exclusive scan over (bin, wave) = thread tid: bins in order, waves inside a bin
+        __shared__ uint32_t part[kOrderWaves];
+        const uint32_t h = hist[tid];
+        uint32_t v = h;
+        const int lane = tid & 63;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t u = __shfl_up(v, off);
+            if (lane >= off) v += u;
+        }
+        if (lane == 63) part[wave] = v;
+        __syncthreads();
+        uint32_t before = 0;
+        for (int w = 0; w < wave; w++) before += part[w];
+        hist[tid] = before + v - h;
+    }
+    __syncthreads();
+    for (int base = 0; base < n; base += 1024 * kOrderBatch) {
+        int bin[kOrderBatch];
+#pragma unroll
+        for (int j = 0; j < kOrderBatch; j++) {
+            const int i = base + j * 1024 + tid;
+            bin[j] = i < n ? order_bin(cost[i]) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < kOrderBatch; j++)
+            if (bin[j] >= 0) order[atomicAdd(&hist[bin[j] * kOrderWaves + wave], 1u)] = (uint32_t)(base + j * 1024 + tid);
+    }
 }
 
 // ------------------------------------------------------------------ device state
@@ -1438,6 +1471,10 @@ int mrt_scene_add_light(mrt_scene* s, const mrt_light* l) {
         return MRT_ERR_INVALID;
     }
     if (s->impl.lights.size() >= (size_t)kMaxLights) { set_error("too many lights"); return MRT_ERR_INVALID; }
+    if (l->transparent_shadows) {   // Light::setFastShadows(false): no reference scene sets it
+        set_error("transparent shadows (Light::setFastShadows(false)) are not implemented; fast shadows only");
+        return MRT_ERR_INVALID;
+    }
     DevLight d;
     memset(&d, 0, sizeof d);
     d.dome = -1;

@@ -215,12 +215,14 @@ class _Light:
         self.power = 0.0
         self.samples = 1
         self.castShadows = True
+        self.fastShadows = True           # src/Light.h:16; False is rejected by libmrt (not implemented)
         self.noiseThreshold = 0.001
 
     def setColor(self, c): self.color = Vector3(c)
     def setPower(self, p): self.power = float(p)
     def setSamples(self, n): self.samples = int(n)
     def setCastShadows(self, c): self.castShadows = bool(c)
+    def setFastShadows(self, c): self.fastShadows = bool(c)
     def setNoiseThreshold(self, t): self.noiseThreshold = float(t)
 
 
@@ -233,7 +235,7 @@ class PointLight(_Light):
 
     def _c(self, texture=-1):
         return _lib.mrt_light(0, f3(self.position), f3((0, 0, 0)), f3((0, 0, 0)), f3((0, 0, 0)), self.power,
-                              self.samples, self.noiseThreshold, int(self.castShadows), -1)
+                              self.samples, self.noiseThreshold, int(self.castShadows), -1, int(not self.fastShadows))
 
 
 class RectangleLight(_Light):
@@ -246,7 +248,7 @@ class RectangleLight(_Light):
 
     def _c(self, texture=-1):
         return _lib.mrt_light(1, f3((0, 0, 0)), f3(self.v1), f3(self.v2), f3(self.v3), self.power,
-                              self.samples, self.noiseThreshold, int(self.castShadows), -1)
+                              self.samples, self.noiseThreshold, int(self.castShadows), -1, int(not self.fastShadows))
 
 
 TEX_HDR, TEX_GRAY, TEX_RGB, TEX_RGBA = 0, 1, 3, 4   # RawImage ImageType (floats per texel 3, 1, 3, 4)
@@ -311,7 +313,8 @@ class DomeLight(_Light):
 
     def _c(self, texture=-1):
         return _lib.mrt_light(2, f3((0, 0, 0)), f3((0, 0, 0)), f3((0, 0, 0)), f3((0, 0, 0)), self.power,
-                              self.samples, self.noiseThreshold, int(self.castShadows), int(texture))
+                              self.samples, self.noiseThreshold, int(self.castShadows), int(texture),
+                              int(not self.fastShadows))
 
 
 class Camera:

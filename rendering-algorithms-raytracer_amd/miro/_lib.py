@@ -38,7 +38,8 @@ class mrt_material(C.Structure):
 class mrt_light(C.Structure):
     _fields_ = [("type", C.c_int32), ("pos", C.c_float * 3), ("v1", C.c_float * 3), ("v2", C.c_float * 3),
                 ("v3", C.c_float * 3), ("power", C.c_float), ("samples", C.c_int32),
-                ("noise_threshold", C.c_float), ("cast_shadows", C.c_int32), ("texture", C.c_int32)]
+                ("noise_threshold", C.c_float), ("cast_shadows", C.c_int32), ("texture", C.c_int32),
+                ("transparent_shadows", C.c_int32)]
 
 
 class mrt_camera(C.Structure):

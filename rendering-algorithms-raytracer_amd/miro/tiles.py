@@ -77,6 +77,15 @@ def padded_items(n: int, world: int, rank: int) -> List[int]:
     return mine + [-1] * (-(-n // world) - len(mine))
 
 
+def split_items(n: int, world: int, rank: int):
+    """The split of an n-item step used by bench.py and the gloo tests: (this
+    rank's items id mod world, unpadded -- what it renders; every rank's items
+    padded with -1 to ceil(n / world), concatenated in rank order -- the layout
+    of the gathered buffer that rank 0 unpacks; that common length)."""
+    all_ids = [i for r in range(world) for i in padded_items(n, world, r)]
+    return rank_buckets(n, world, rank), all_ids, -(-n // world)
+
+
 def batch_items(buckets_per_frame: int, n_frames: int, world: int, rank: int) -> List[int]:
     """This rank's item ids (frame * buckets_per_frame + bucket) of a batch,
     padded by repeating its last id to ceil(total / world) (equal gather sizes;

@@ -264,3 +264,129 @@ def test_libmrt_multi_process_frame_equals_single_process(tmp_path, key, world, 
     img = miro.Image(); img.resize(W, H)
     P.raytraceImage(camera(cam), img)
     assert np.array_equal(frame.view(np.uint32), img.rgb.view(np.uint32))
+
+
+def _split_worker(rank, world, port, W, H, steps, result_path):
+    """bench.py's N > 1 headline path on the CPU: ONE frame per step, its buckets
+    dealt id mod N (tiles.split_items: unpadded renders, -1-padded gather layout),
+    float tiles gathered to rank 0 through BatchPipeline (double-buffered), rank 0
+    unpacks; the renderer is the oracle (the code under test is the split)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, cam = _oracle_scene()
+        bx, by = tiles.bucket_grid(W, H)
+        bpf = bx * by
+        mine, all_ids, per = tiles.split_items(bpf, world, rank)
+        path = scenes.camera_path(cam, steps, step_deg=4.0)
+        state = {"render": 0}
+        outs = []
+
+        def render(ids, out):
+            k = state["render"]
+            state["render"] += 1
+            assert list(ids) == mine
+            t = out.view(-1, 32, 32, 3)
+            for slot, b in enumerate(ids):
+                x0, y0 = (b % bx) * 32, (b // bx) * 32
+                r = s.render(path[k], W, H, rect=(x0, y0, x0 + 32, y0 + 32), want_hits=False)
+                h, w = min(32, H - y0), min(32, W - x0)
+                t[slot, :h, :w] = torch.from_numpy(r["rgb"][y0:y0 + h, x0:x0 + w])
+
+        def unpack(ids, gathered, b):
+            assert len(ids) == world * per
+            frame = np.zeros((H, W, 3), np.float32)
+            t = gathered.view(-1, 32, 32, 3).numpy()
+            for slot, i in enumerate(ids):
+                if i < 0:          # padding of a rank with fewer buckets
+                    continue
+                x0, y0 = (i % bx) * 32, (i // bx) * 32
+                h, w = min(32, H - y0), min(32, W - x0)
+                frame[y0:y0 + h, x0:x0 + w] = t[slot, :h, :w]
+            outs.append(frame)
+
+        pipe = tiles.BatchPipeline(world, rank, dist, mine, all_ids,
+                                   lambda k: torch.zeros(k * per * 1024 * 3, dtype=torch.float32), render, unpack)
+        for _ in range(steps):
+            pipe.step()
+        pipe.flush()
+        if rank == 0:
+            np.save(result_path, np.stack(outs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_single_frame_split_pipeline_equals_single_rank(tmp_path, world):
+    """The headline N > 1 split (bench.py --split frame) reproduces the single-rank
+    frames bit for bit, step after step (ragged frame: 7 buckets over 2 / 3 ranks)."""
+    W, H, steps = 70, 40, 3
+    path = str(tmp_path / "frames.npy")
+    mp.start_processes(_split_worker, args=(world, _free_port(), W, H, steps, path), nprocs=world,
+                       start_method="spawn")
+    got = np.load(path)
+    assert got.shape == (steps, H, W, 3)
+    s, cam = _oracle_scene()
+    cams = scenes.camera_path(cam, steps, step_deg=4.0)
+    for k in range(steps):
+        ref = s.render(cams[k], W, H, want_hits=False)["rgb"]
+        assert np.array_equal(got[k].view(np.uint32), ref.view(np.uint32)), k
+
+
+def test_split_items_layout():
+    for n in (7, 60 * 34, 120 * 68):
+        for world in (1, 2, 3, 8):
+            per_rank = [tiles.split_items(n, world, r) for r in range(world)]
+            all_ids, per = per_rank[0][1], per_rank[0][2]
+            assert all(p[1] == all_ids and p[2] == per for p in per_rank)
+            assert len(all_ids) == world * per
+            for r, (mine, _, _) in enumerate(per_rank):
+                assert all_ids[r * per:r * per + len(mine)] == mine     # rank r's slots, in order
+            assert sorted(i for i in all_ids if i >= 0) == list(range(n))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ["C3", "C4"])
+def test_split_path_at_one_gpu_equals_frame_path(key):
+    """bench.py's split path (tiles.split_items + BatchPipeline + libmrt batch
+    render into float tiles + unpack) at N = 1 equals the whole-frame path bit
+    for bit (float RGB and 8-bit)."""
+    import ctypes as C
+    import miro
+    from miro import _lib
+    from helpers import config_scene, camera
+    if miro.device_count() < 1:
+        pytest.skip("no HIP device")
+    W, H = 200, 120
+    P, _, cam = config_scene(key)
+    img = miro.Image(); img.resize(W, H)
+    P.raytraceImage(camera(cam), img)
+    L = miro.lib()
+    bx, by = tiles.bucket_grid(W, H)
+    mine, all_ids, per = tiles.split_items(bx * by, 1, 0)
+    items = torch.tensor(mine, dtype=torch.int32, device="cuda")
+    all_items = torch.tensor(all_ids, dtype=torch.int32, device="cuda")
+    camc = (_lib.mrt_camera * 1)(camera(cam)._c())
+    opts = _lib.mrt_render_opts(W, H, 0, 0, 1, 0, 0)
+    out_f = [torch.zeros(H * W * 3, dtype=torch.float32, device="cuda") for _ in range(2)]
+    out_8 = [torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(2)]
+
+    def render(ids, out):
+        _lib.check(L.mrt_render_batch_async(P.handle, camc, 1, C.byref(opts), ids.data_ptr(), len(mine),
+                                            out.data_ptr(), None, torch.cuda.current_stream().cuda_stream), "render")
+
+    def unpack(ids, gathered, b):
+        _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(ids), gathered.data_ptr(), None, W, H, 1,
+                                            out_f[b].data_ptr(), out_8[b].data_ptr(), P.handle,
+                                            torch.cuda.current_stream().cuda_stream), "unpack")
+
+    pipe = tiles.BatchPipeline(1, 0, None, items, all_items,
+                               lambda k: torch.zeros(k * per * 1024 * 3, dtype=torch.float32, device="cuda"),
+                               render, unpack, streams=[torch.cuda.Stream(), torch.cuda.Stream()])
+    for _ in range(3):
+        pipe.step()
+    pipe.flush()
+    torch.cuda.synchronize()
+    for b in range(2):
+        assert np.array_equal(out_f[b].cpu().numpy().reshape(H, W, 3).view(np.uint32), img.rgb.view(np.uint32))
+        assert np.array_equal(out_8[b].cpu().numpy().reshape(H, W, 3), img.pixels)

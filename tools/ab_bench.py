@@ -1,5 +1,7 @@
 """Interleaved A/B of tuning switches on config C3 (one process, one device).
-Usage: python tools/ab_bench.py key=v1,v2 [key2=...] [--rounds R]"""
+Usage: python tools/ab_bench.py key=v1,v2 [key2=...] [--rounds R] [--inflight K]
+Per variant: serial kernel times (HIP events of single frames) and the
+pipelined rate with K frames in flight on K streams (bench.py's N = 1 mode)."""
 import ctypes as C
 import json
 import os
@@ -20,6 +22,7 @@ def main():
     if "--rounds" in sys.argv:
         rounds = int(sys.argv[sys.argv.index("--rounds") + 1])
     cfgkey = os.environ.get("AB_CONFIG", "C3")
+    inflight = int(sys.argv[sys.argv.index("--inflight") + 1]) if "--inflight" in sys.argv else 4
     variants = [{}]
     for a in args:
         k, vs = a.split("=")
@@ -31,6 +34,25 @@ def main():
     frame8 = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")
     sh = torch.cuda.current_stream().cuda_stream
     camc = cam._c()
+    streams = [torch.cuda.Stream() for _ in range(inflight)]
+    fr = [torch.empty(H * W * 3, dtype=torch.float32, device="cuda") for _ in range(inflight)]
+    fr8 = [torch.empty(H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(inflight)]
+
+    def pipelined(v, frames=40):
+        for k, x in v.items():
+            _lib.check(L.mrt_set_tuning(k.encode(), x), k)
+        o = _lib.mrt_render_opts(W, H, 0, 0, 1, 0, 0)
+        for i in range(inflight):   # per-stream scratch + warm
+            _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc), C.byref(o), fr[i].data_ptr(),
+                                                fr8[i].data_ptr(), streams[i].cuda_stream), "render")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for f in range(frames):
+            i = f % inflight
+            _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc), C.byref(o), fr[i].data_ptr(),
+                                                fr8[i].data_ptr(), streams[i].cuda_stream), "render")
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / frames * 1e3
     ref = None
 
     def run(v, count=False, reps=10):
@@ -47,6 +69,7 @@ def main():
         return pm, sm, st
 
     res = {json.dumps(v): ([], []) for v in variants}
+    pipe = {json.dumps(v): [] for v in variants}
     for v in variants:  # warm + correctness vs the first variant
         run(v, reps=2)
         out = frame.cpu().numpy().view(np.uint32).copy()
@@ -63,11 +86,14 @@ def main():
             pm, sm, _ = run(v)
             res[json.dumps(v)][0].extend(pm)
             res[json.dumps(v)][1].extend(sm)
+            pipe[json.dumps(v)].append(pipelined(v))
     rays = W * H + st["shadow_rays"]
     for k, (pm, sm) in res.items():
         p, s = np.median(pm), np.median(sm)
+        q = np.median(pipe[k])
         print(f"{k:64s} primary {p:.4f} ms  shade {s:.4f} ms  "
-              f"frame {p + s:.4f} ms  -> {rays / (p + s) / 1e3:.0f} Mray/s (kernel time)", flush=True)
+              f"frame {p + s:.4f} ms  -> {rays / (p + s) / 1e3:.0f} Mray/s (kernel time); "
+              f"{inflight} in flight {q:.4f} ms/frame -> {rays / q / 1e3:.0f} Mray/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -37,9 +37,9 @@ def main():
     pat = sys.argv[2] if len(sys.argv) > 2 else ""
     for r in kernels(obj):
         name = r.get("name", "?")
-        if pat and not re.search(pat, name):
-            continue
         dm = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip()
+        if pat and not (re.search(pat, name) or pat in dm):
+            continue
         dm = dm.replace("mrt::", "").replace("(RenderParams)", "").replace("void ", "")
         print("%-60s vgpr %4s sgpr %4s lds %6s scratch %5s vspill %4s" % (
             dm[:60], r.get("vgpr_count"), r.get("sgpr_count"), r.get("group_segment_fixed_size"),
