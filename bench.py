@@ -69,6 +69,8 @@ def parse():
                          "(weak scaling; also reported as the `weak` key of a frame-split line)")
     ap.add_argument("--strong-steps", type=int, default=0, help="N > 1: steps of the secondary (weak) measurement")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-thread-seconds for the oracle sample")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="libmrt tuning switch (mrt_set_tuning) for A/B and profiling runs; reported in the line")
     return ap.parse_args()
 
 
@@ -303,6 +305,11 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
+    tuning = {}
+    for kv in args.tune:
+        k, v = kv.split("=")
+        _lib.check(miro.lib().mrt_set_tuning(k.encode(), int(v)), f"tuning {k}")
+        tuning[k] = int(v)
     scene, cam, cfg = scenes.build_config(args.config, device=dev)
     W, H = cfg["W"], cfg["H"]
     L = miro.lib()
@@ -498,6 +505,9 @@ def main():
                                 "one launch)"), "primary", pm
         dom_b = (st["node_visits"] * NODE_B + st["leaf_visits"] * LEAF_B
                  + px_mine * ((12 if use_frame_path or split else 0) + 3) + hits_px * (32 + 3 * 16 + 3 * 16))
+    elif adaptive and st.get("chain"):   # adaptive passes, each a chain-engine tree walk (G3)
+        dom, dom_key, dom_ms, dom_b = ("chain engine, adaptive passes (per pass: unit_eye + per level chain gen + compact "
+                                       "+ chain_trace + resolve, per-level folds, adapt_combine)"), "shade", sm, b_shade
     elif adaptive:   # one fused launch: eye rays, shading, inline shadow rays (its time is shade_ms)
         dom, dom_key, dom_ms = "adaptive_kernel (eye rays + shading + any-hit shadow rays)", "shade", sm
         dom_b = (st["node_visits"] * NODE_B + st["leaf_visits"] * LEAF_B
@@ -581,6 +591,8 @@ def main():
                            for k in ("primary_span_us", "primary_ramp_us", "primary_tail_us",
                                      "shade_span_us", "shade_ramp_us", "shade_tail_us")},
     }
+    if tuning:
+        out["tuning"] = tuning
     if split_times is not None:
         out["split_times"] = split_times
     if weak is not None:

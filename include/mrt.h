@@ -164,6 +164,10 @@ typedef struct {
      * shading and shadow rays fused; one point light, one path); primary_ms is
      * then the whole frame and shade_ms ~0 (ABI 7) */
     int32_t fused;
+    /* 1: the frame's shading ran the wavefront chain engine (secondary rays,
+     * dispersive splits, path tracing; with adaptive supersampling as passes
+     * over it) rather than one fused kernel (ABI 7) */
+    int32_t chain;
 } mrt_stats;
 
 const char* mrt_last_error(void);

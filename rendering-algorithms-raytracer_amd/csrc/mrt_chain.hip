@@ -1,38 +1,49 @@
 // mrt_chain.hip -- the wavefront chain engine: Blinn reflection / refraction
-// rays and path tracing (Shader REC 1 / 2) level by level instead of one lane
-// walking its whole chain.
+// rays, dispersive three-way splits, path tracing (Shader REC 1 / 2) and
+// adaptive supersampling, level by level instead of one lane walking its
+// whole recursion.
 //
-// The fused kernels (shade_kernel<REC>) keep every level's shading state live
-// across each secondary and shadow traversal: 256 VGPRs plus scratch, one
-// wave per SIMD.  Here the chain of Shader::level calls
-// of one path (src/Blinn.cpp:39-335) is cut at each child ray:
+// The fused kernels (shade_kernel<REC>, adaptive_kernel<REC>) keep every
+// level's shading state live across each secondary and shadow traversal: 256
+// VGPRs plus scratch, one wave per SIMD.  Here the recursion of Shader::level
+// calls of one path (src/Blinn.cpp:39-335) is cut at each child ray and run as
+// a tree of entries, one level at a time over all paths of a chunk:
 //
-//   chain0   (per pixel, tile schedule)  level 0 of every path of the pixel
-//            (the camera ray's IOR history persists across its paths) in two
-//            passes around shadow_kernel, as the direct path's 2a / 2b / 2c:
-//            kGen writes the shadow rays, kResolve shades with the answers.
-//            A path either ends (final value -> ch_tv / ch_te) or spawns a
-//            child into the sparse spawn slots at its own index, with its
-//            level record (ch_rec) written for the combine;
-//   compact  spawn slots of level k -> dense level k+1 (block-aggregated:
-//            one atomic per 1024 slots), each entry keeping its parent index;
-//   trace    closest hit of every level-k+1 entry (traversal only: few
-//            registers, full occupancy);
-//   shade    level k+1 of every entry (kGen, shadow_kernel, kResolve): a miss
-//            ends the path with the environment (or nothing, a GI ray without
-//            environment sampling), a hit runs Shader::level, which ends it or
-//            spawns again;
+//   chain0   (per work unit: one eye ray of a pixel) level 0 of every path of
+//            the unit (the camera ray's IOR history persists across its paths)
+//            in two passes around the shadow rays: kGen writes the shadow rays,
+//            kResolve shades with the answers.  A level either ends (its value
+//            -> ch_val) or spawns children into the sparse spawn slots of its
+//            entry (entry * ch_split + i): one reflection / refraction / GI
+//            ray, or, at a dispersive material, three refraction rays (one per
+//            colour channel, Shader::disp_child), with its level record written
+//            for the fold;
+//   compact  spawn slots of level k -> dense entries of level k + 1
+//            (block-aggregated: one atomic per 1024 slots), each keeping its
+//            parent entry; ch_map[slot] = the dense child, for the fold;
+//   trace    closest hit of every level-k + 1 entry, and the any-hit answers of
+//            level k's shadow rays (traversal only: few registers, full
+//            occupancy);
+//   shade    level k + 1 of every entry (kGen): shadow rays and children;
 //   resolve  (after the last level) every level shaded again with its shadow
-//            answers: level records and final values;
-//   path     per path: the final value folded up its chain with
-//            chain_combine (deepest first, the parent indices);
-//   finish   per pixel: the paths averaged and the pixel written (float RGB +
-//            Image::Map 8-bit).
+//            answers: ch_val of the entries that end, level records;
+//   fold     per level, deepest first: every spawning entry gathers its
+//            children's values through ch_map -- chain_combine for one child,
+//            the masked channel sums of src/Blinn.cpp:275-301 for a split;
+//   finish   per unit: the paths averaged (Scene::sampleScene); the pixel
+//            written, or, under adaptive supersampling, the unit's colour.
 //
-// Every ray, every RNG draw (keyed by pixel, path and level) and every add is
-// the fused kernel's, so the two engines give bit-identical frames
-// (tests/test_secondary.py, tests/test_path_trace.py).  A frame whose slots do
-// not fit the scratch budget runs in chunks of work items.
+// Adaptive supersampling (Scene::adaptiveSampleScene, src/Scene.cpp:252-293)
+// runs as passes n = 1, 2, .. over the pixels still refining: pass n renders
+// n^2 jittered eye rays per such pixel through the engine above (unit_eye
+// traces them), then adapt_combine forms the running mean, applies the stop
+// test and lists the pixels of pass n + 1.
+//
+// Every ray, every RNG draw (keyed by pixel, eye sample, path, level and
+// dispersion branch) and every add is the fused kernel's, so the two engines
+// give bit-identical frames (tests/test_chain.py, test_secondary.py,
+// test_path_trace.py, test_dispersion.py, test_adaptive.py).  A pass whose
+// entries do not fit the scratch budget runs in chunks of units.
 #include "mrt_shader.h"
 
 namespace mrt {
@@ -53,112 +64,187 @@ __device__ __forceinline__ void unpack_state(uint32_t w, ChainState& cs, bool& e
     cs.br = (int)((w >> 19) & 255u);
 }
 
-__device__ __forceinline__ size_t lvl_off(const RenderParams& P, int k) { return (size_t)k * P.ch_cap; }
-// level record of entry e of level k: lvl_words consecutive floats (the combine
-// walks one path's chain, so a record is read as a unit)
+// ch_val flags (.w bits): the entry's ray missed (a split parent skips it); its
+// value is "nothing" (a GI ray missed without environment sampling); its value
+// is still to be folded from its children (pending), which are a split
+enum { kValMissed = 1, kValNone = 2, kValPending = 4, kValSplit = 8 };
+
+__device__ __forceinline__ uint32_t lofs(const RenderParams& P, int k) { return P.ch_lofs[k]; }
+__device__ __forceinline__ uint32_t lcap(const RenderParams& P, int k) { return P.ch_lofs[k + 1] - P.ch_lofs[k]; }
+// level record of entry e of level k: lvl_words consecutive floats
 __device__ __forceinline__ ChainRec chain_rec(const RenderParams& P, int k, uint32_t e) {
-    return ChainRec{P.ch_rec + ((size_t)k * P.ch_cap + e) * (size_t)P.lvl_words, 1};
+    return ChainRec{P.ch_rec + ((size_t)lofs(P, k) + e) * (size_t)P.lvl_words, 1};
 }
-static constexpr uint32_t kDeadPath = 0xFFFFFFFFu;   // ch_te of a path whose camera ray missed
+__device__ __forceinline__ void write_val(const RenderParams& P, int k, uint32_t e, v3 v, uint32_t flags) {
+    P.ch_val[(size_t)lofs(P, k) + e] = make_float4(v.x, v.y, v.z, __uint_as_float(flags));
+}
+// shadow-ray slots of chain level k (each level keeps its own until the resolve pass)
+__device__ __forceinline__ size_t shadow_base(const RenderParams& P, int k) {
+    return (size_t)lofs(P, k) * (size_t)P.max_shadow;
+}
+
+// ------------------------------------------------------------------ units
+// units of this chunk (the pass's count is on the device under adaptive passes)
+__device__ __forceinline__ uint32_t chunk_units(const RenderParams& P) {
+    const uint32_t nn = P.adapt_n > 1 ? (uint32_t)(P.adapt_n * P.adapt_n) : 1u;
+    const uint32_t total = P.unit_cnt ? *P.unit_cnt * nn : P.units_total;
+    return total > P.unit_base ? min(P.n_units, total - P.unit_base) : 0u;
+}
+struct UnitPix {
+    int x, y, f;
+    size_t slot;
+    uint32_t sample;   // eye-ray sample of the pixel (RNG sub-stream sample * 1024 + path)
+    int i, j;          // sub-cell of an adaptive pass n >= 2
+    bool valid;
+};
+// unit ug of the pass (global index)
+__device__ __forceinline__ UnitPix unit_pixel(const RenderParams& P, uint32_t ug) {
+    UnitPix U;
+    int item, lane;
+    U.sample = 0;
+    U.i = U.j = 0;
+    if (P.units && P.adapt_n > 1) {
+        const uint32_t nn = (uint32_t)(P.adapt_n * P.adapt_n), r = ug % nn;
+        const uint32_t id = P.units[ug / nn];
+        item = (int)(id >> 6);
+        lane = (int)(id & 63u);
+        U.i = (int)(r / (uint32_t)P.adapt_n);
+        U.j = (int)(r % (uint32_t)P.adapt_n);
+        U.sample = (uint32_t)sum_squares(P.adapt_n - 1) + r;   // rays 0 .. of the pixel, level by level
+    } else {
+        item = (int)(ug >> 6);
+        lane = (int)(ug & 63u);
+    }
+    U.valid = item_pixel(P, item, lane, U.x, U.y, U.slot);
+    U.f = item_frame(P, item);
+    return U;
+}
+// the unit's eye ray: Camera::eyeRayAdaptive over the unit's cell (the centre
+// at pass 1 and without supersampling)
+__device__ __forceinline__ EyeRay unit_eye(const RenderParams& P, const UnitPix& U, const uint16_t* rsqT) {
+    const CamParams& cam = P.cam[U.f];
+    const uint32_t seed = P.seed + (uint32_t)U.f;
+    if (P.adapt_n <= 1) return camera_ray(cam, seed, U.x, U.y, rsqT);
+    const float off = 1.0f / (float)P.adapt_n;
+    return eye_ray(cam, seed, U.x, U.y, U.sample * 1024u, (float)U.i * off, (float)(U.i + 1) * off, (float)U.j * off,
+                   (float)(U.j + 1) * off, rsqT);
+}
+__device__ __forceinline__ float4 unit_hit(const RenderParams& P, uint32_t u, const UnitPix& U) {
+    return P.uhits ? P.uhits[u] : P.hits[U.slot];
+}
+// The camera ray's time of chunk path p (every ray below the camera ray carries
+// it): the getTimeSample draw of the unit's eye ray (shared by all its paths).
+__device__ __forceinline__ float unit_time(const RenderParams& P, const UnitPix& U) {
+    const CamParams& cam = P.cam[U.f];
+    const float tr = rng((uint32_t)(U.y * cam.W + U.x), U.sample * 1024u, 2, P.seed + (uint32_t)U.f);
+    return 1.f - ((tr * tr) * tr) * cam.shutter;
+}
 
 // A spawned child at sparse slot s: its ray, state word and the IOR column
-// (the child's history, written by Shader::level).
-__device__ __forceinline__ void write_spawn(const RenderParams& P, uint32_t s, const LevelOut& o, uint32_t path_id,
-                                            const ChainState& cs, const float* iorS) {
-    const size_t cap = P.ch_cap;
-    P.ch_sp[s] = make_float4(o.r2.o[0], o.r2.o[1], o.r2.o[2], __uint_as_float(path_id));
-    P.ch_sp[cap + s] = make_float4(o.r2.d[0], o.r2.d[1], o.r2.d[2], __uint_as_float(pack_state(cs, o.env_miss)));
+// (the child's history, written by Shader::level / disp_child).
+__device__ __forceinline__ void write_spawn(const RenderParams& P, uint32_t s, const DRay& r2, uint32_t path_id,
+                                            const ChainState& cs, bool env_miss, const float* iorS) {
+    const size_t cap = P.ch_spcap;
+    P.ch_sp[s] = make_float4(r2.o[0], r2.o[1], r2.o[2], __uint_as_float(path_id));
+    P.ch_sp[cap + s] = make_float4(r2.d[0], r2.d[1], r2.d[2], __uint_as_float(pack_state(cs, env_miss)));
     P.ch_sp[2 * cap + s] = make_float4(iorS[1 * kWG], iorS[2 * kWG], iorS[3 * kWG], iorS[4 * kWG]);
     P.ch_sp[3 * cap + s] = make_float4(iorS[5 * kWG], iorS[6 * kWG], iorS[7 * kWG], 0.f);
 }
 
-// a path's final value: level k's value (or a missed child's) and where it ended
-__device__ __forceinline__ void write_final(const RenderParams& P, uint32_t path_id, v3 v, int level, bool none,
-                                            uint32_t entry) {
-    P.ch_tv[path_id] = make_float4(v.x, v.y, v.z, __uint_as_float((uint32_t)level | (none ? 1u << 8 : 0u)));
-    P.ch_te[path_id] = entry;
+// After Shader::level of entry e (level k) spawned: kGen writes the children
+// (a split: the three channel rays, in channel order) and their flags; kResolve
+// marks the entry pending.  A split child's history / state come from the
+// recorded level (disp_child), whose camera-ray push (k == 0) also carries on
+// into the unit's next path -- so it runs in both modes.
+template <class SH>
+__device__ __forceinline__ void spawn_children(const RenderParams& P, SH& S, int k, uint32_t e, uint32_t path_id,
+                                               ChainState& cs, typename SH::IorCam& cam, const LevelOut& o, bool gen) {
+    const uint32_t s0 = e * (uint32_t)P.ch_split;
+    if (o.split) {
+        const ChainRec rec = chain_rec(P, k, e);
+        for (int i = 0; i < 3; i++) {
+            ChainState c2 = cs;
+            const DRay r2 = S.disp_child(rec, k, i, c2, cam);
+            if (gen) {
+                write_spawn(P, s0 + (uint32_t)i, r2, path_id, c2, true, S.iorS);
+                P.ch_flag[s0 + (uint32_t)i] = 1;
+            }
+        }
+        if (!gen) write_val(P, k, e, mk(0, 0, 0), kValPending | kValSplit);
+        return;
+    }
+    if (gen) {
+        write_spawn(P, s0, o.r2, path_id, cs, o.env_miss, S.iorS);
+        P.ch_flag[s0] = 1;
+        for (int i = 1; i < P.ch_split; i++) P.ch_flag[s0 + (uint32_t)i] = 0;
+    } else {
+        write_val(P, k, e, mk(0, 0, 0), kValPending);
+    }
+}
+__device__ __forceinline__ void no_children(const RenderParams& P, uint32_t e) {
+    const uint32_t s0 = e * (uint32_t)P.ch_split;
+    for (int i = 0; i < P.ch_split; i++) P.ch_flag[s0 + (uint32_t)i] = 0;
 }
 
-// shadow-ray slots of chain level k (each level keeps its own until the resolve pass)
-__device__ __forceinline__ size_t shadow_base(const RenderParams& P, int k) {
-    return (size_t)k * P.ch_cap * (size_t)P.max_shadow;
-}
-
-// The camera ray's time of path p of the chunk (every ray below the camera ray
-// carries it): the getTimeSample draw of the pixel's eye ray (sample 0, shared
-// by all its paths).
-__device__ __forceinline__ float path_time(const RenderParams& P, uint32_t p) {
-    const uint32_t pl = p / (uint32_t)P.num_paths;
-    int x, y;
-    size_t slot;
-    item_pixel(P, P.item_base + (int)(pl >> 6), (int)(pl & 63u), x, y, slot);
-    const int f = item_frame(P, P.item_base + (int)(pl >> 6));
-    const CamParams& cam = P.cam[f];
-    const float tr = rng((uint32_t)(y * cam.W + x), 0u, 2, P.seed + (uint32_t)f);
-    return 1.f - ((tr * tr) * tr) * cam.shutter;
-}
-
-// Level 0 of every path of a chunk's pixels (tile schedule over the chunk's
-// work items).  Path id = (work item of the chunk * 64 + lane) * num_paths + path.
-// MODE kGen writes each path's shadow rays (level-0 slots p * max_shadow + j,
-// count in nrays[p]) and its spawned child (the spawn decision, the child ray
-// and its IOR history do not depend on the shadow answers); kResolve runs the
-// same shading with the answers and writes the level record or the path's
-// final value.  No traversal runs in either, so the shading state never has to
-// live across one.
+// Level 0 of every path of the chunk's units, one lane per unit.  Path id =
+// chunk unit * num_paths + path.  MODE kGen writes each path's shadow rays
+// (level-0 slots p * max_shadow + j, count in nrays[p]) and its spawned
+// children (the spawn decision, the child rays and their IOR histories do not
+// depend on the shadow answers); kResolve runs the same shading with the
+// answers and writes the path's value or marks it pending.  No traversal runs
+// in either, so the shading state never has to live across one.
 template <bool POINT_ONLY, bool INST, int REC, int MODE>
 __global__ void __launch_bounds__(kWG) chain0_kernel(RenderParams P) {
     __shared__ float s_ior[kIorCap * kWG];
     const uint16_t* rcpT = P.tables;          // no triangle tests here: both tables from global (L1)
     const uint16_t* rsqT = P.tables + 2048;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
     Trav T{P.nodes, false, false, P.leaves, rcpT, nullptr, nullptr, P.gstride};   // unused: no traversal
     TravStats st;
     uint32_t shadow_total = 0, secondary_total = 0;
-    TileSched ts(P, wave, lane);
-    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
-        int x, y;
-        size_t slot;
-        const bool valid = item_pixel(P, P.item_base + item, lane, x, y, slot);
+    const uint32_t n = chunk_units(P), np = (uint32_t)P.num_paths;
+    for (uint32_t u0 = (uint32_t)blockIdx.x * kWG + (uint32_t)(tid & ~63); u0 < n; u0 += gridDim.x * (uint32_t)kWG) {
+        const uint32_t u = u0 + (uint32_t)lane;
+        if (u >= n) continue;
+        const UnitPix U = unit_pixel(P, P.unit_base + u);
         DHit h{1e12f, 0.f, 0.f, -1};
-        if (valid) {
-            const float4 hv = P.hits[slot];
+        if (U.valid) {
+            const float4 hv = unit_hit(P, u, U);
             h = DHit{hv.x, hv.y, hv.z, __float_as_int(hv.w)};
         }
-        const uint32_t pbase = ((uint32_t)item * 64u + (uint32_t)lane) * (uint32_t)P.num_paths;
-        if (!valid || h.prim < 0) {   // nothing to shade: no shadow rays, no spawns (finish writes env / background)
-            if (MODE == kGen)
-                for (int path = 0; path < P.num_paths; path++) {
+        const uint32_t pbase = u * np;
+        if (!U.valid || h.prim < 0) {   // nothing to shade: no shadow rays, no spawns (finish writes env / background)
+            for (uint32_t path = 0; path < np; path++) {
+                if (MODE == kGen) {
                     P.nrays[pbase + path] = 0;
-                    P.ch_flag[pbase + path] = 0;
-                    P.ch_te[pbase + path] = kDeadPath;
+                    no_children(P, pbase + path);
+                } else {
+                    write_val(P, 0, pbase + path, mk(0, 0, 0), kValMissed);   // never pending (the fold skips it)
                 }
+            }
             continue;
         }
-        const int f = item_frame(P, P.item_base + item);
-        const CamParams& cam = P.cam[f];
-        const uint32_t seed = P.seed + (uint32_t)f;
-        const EyeRay er = camera_ray(cam, seed, x, y, rsqT);
+        const CamParams& cam = P.cam[U.f];
+        const uint32_t seed = P.seed + (uint32_t)U.f;
+        const EyeRay er = unit_eye(P, U, rsqT);
         const DRay r = make_ray(er.o, er.d, er.time);
-        Shader<POINT_ONLY, false, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 0u, seed, 0, 0u};
+        Shader<POINT_ONLY, false, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(U.y * cam.W + U.x), 0u, seed, 0,
+                                                     0u};
         S.iorS = s_ior + tid;
         S.time = S.shadow_time = er.time;
         typename Shader<POINT_ONLY, false, INST, MODE, REC>::IorCam icam;
-        for (int path = 0; path < P.num_paths; path++) {
-            const uint32_t p = pbase + (uint32_t)path;
-            S.skey = (uint32_t)path;   // eye-ray sample 0
+        for (uint32_t path = 0; path < np; path++) {
+            const uint32_t p = pbase + path;
+            S.skey = U.sample * 1024u + path;
             S.slot0 = (size_t)p * (size_t)P.max_shadow;
             S.nslot = 0;
             ChainState cs;
             LevelOut o;
             S.template level<false>(r, h, cs, icam, chain_rec(P, 0, p), o);
-            if (MODE == kGen) {
-                P.nrays[p] = (uint8_t)S.nslot;
-                if (o.spawn) write_spawn(P, p, o, p, cs, S.iorS);
-                P.ch_flag[p] = o.spawn ? 1 : 0;
-            } else if (!o.spawn) {
-                write_final(P, p, o.val, 0, false, p);
-            }
+            if (MODE == kGen) P.nrays[p] = (uint8_t)S.nslot;
+            if (o.spawn) spawn_children(P, S, 0, p, p, cs, icam, o, MODE == kGen);
+            else if (MODE == kGen) no_children(P, p);
+            else write_val(P, 0, p, o.val, 0u);
         }
         shadow_total += S.shadow_rays;
         secondary_total += S.secondary;
@@ -171,15 +257,17 @@ __global__ void __launch_bounds__(kWG) chain0_kernel(RenderParams P) {
 
 // Spawn slots of level k (P.ch_level) -> dense entries of level k + 1.  A
 // block takes 1024 slots (4 per thread), orders its spawns by (round, wave,
-// lane) and reserves their entries with one atomic.
+// lane) and reserves their entries with one atomic; ch_map[slot] = the entry.
 static constexpr int kCompactGroup = 4 * kWG;
 __global__ void __launch_bounds__(kWG) chain_compact_kernel(RenderParams P) {
     __shared__ uint32_t s_cnt[4 * (kWG / 64)];
     __shared__ uint32_t s_base;
     const int k = P.ch_level;
-    const uint32_t n = k == 0 ? (uint32_t)P.n_tiles * 64u * (uint32_t)P.num_paths : P.ch_cnt[k];
+    const uint32_t ne = k == 0 ? chunk_units(P) * (uint32_t)P.num_paths : P.ch_cnt[k];
+    const uint32_t n = ne * (uint32_t)P.ch_split;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const size_t cap = P.ch_cap, dst0 = lvl_off(P, k + 1);
+    const size_t cap = P.ch_spcap, dst0 = lofs(P, k + 1), dcap = lcap(P, k + 1);
+    uint32_t* map = P.ch_map + (size_t)P.ch_split * lofs(P, k);
     for (uint32_t g = blockIdx.x * (uint32_t)kCompactGroup; g < n; g += gridDim.x * (uint32_t)kCompactGroup) {
         bool f[4];
         uint32_t rank[4];
@@ -207,12 +295,17 @@ __global__ void __launch_bounds__(kWG) chain_compact_kernel(RenderParams P) {
             if (!f[j]) continue;
             const uint32_t e = g + (uint32_t)(j * kWG + tid);
             const uint32_t d = s_base + s_cnt[j * (kWG / 64) + wave] + rank[j];
-            if (d >= P.ch_cap) { atomicOr(&P.ctr[CTR_OVERFLOW], 2ull); continue; }   // cannot happen: <= one child per slot
+            if (d >= dcap) {   // cannot happen: level capacities bound the children per entry
+                atomicOr(&P.ctr[CTR_OVERFLOW], 2ull);
+                map[e] = 0xFFFFFFFFu;
+                continue;
+            }
+            map[e] = d;
             const float4 o = P.ch_sp[e], dd = P.ch_sp[cap + e], i0 = P.ch_sp[2 * cap + e], i1 = P.ch_sp[3 * cap + e];
             P.ch_ray[2 * dst0 + d] = o;
-            P.ch_ray[2 * dst0 + cap + d] = dd;
+            P.ch_ray[2 * dst0 + dcap + d] = dd;
             P.ch_ior[2 * dst0 + d] = i0;
-            P.ch_ior[2 * dst0 + cap + d] = make_float4(i1.x, i1.y, i1.z, __uint_as_float(e));
+            P.ch_ior[2 * dst0 + dcap + d] = make_float4(i1.x, i1.y, i1.z, __uint_as_float(e / (uint32_t)P.ch_split));
         }
         __syncthreads();   // s_cnt / s_base reused by the next group
     }
@@ -230,7 +323,7 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
     const int k = P.ch_level;
     const uint32_t nA = k < P.ch_levels ? P.ch_cnt[k] : 0u;
     const uint32_t m = (uint32_t)P.max_shadow;
-    const uint32_t nprev = k == 1 ? (uint32_t)P.n_tiles * 64u * (uint32_t)P.num_paths : P.ch_cnt[k - 1];
+    const uint32_t nprev = k == 1 ? chunk_units(P) * (uint32_t)P.num_paths : P.ch_cnt[k - 1];
     const uint32_t nB = nprev * m;
     const uint32_t chA = (nA + 63u) >> 6, chunks = chA + ((nB + 63u) >> 6);
     const uint32_t wave_id = (uint32_t)blockIdx.x * (kWG / 64) + (uint32_t)(threadIdx.x >> 6);
@@ -242,15 +335,17 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
     T.inst = P.insts;
     trav_alpha(T, P);
     TravStats st;
-    const size_t base = lvl_off(P, k), cap = P.ch_cap, sb = shadow_base(P, k - 1);
-    const uint8_t* nrays = P.nrays + (size_t)(k - 1) * cap;
+    const size_t base = lofs(P, k), cap = k < P.ch_levels ? lcap(P, k) : 0, sb = shadow_base(P, k - 1);
+    const uint8_t* nrays = P.nrays + lofs(P, k - 1);
+    const uint32_t np = (uint32_t)P.num_paths;
     for (uint32_t c = wave_id; c < chunks; c += gridDim.x * (kWG / 64)) {
         if (c < chA) {   // closest hit of entry e
             const uint32_t e = (c << 6) + (uint32_t)lane;
             if (e >= nA) continue;
             const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
-            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z),
-                                    INST && P.has_mb ? path_time(P, __float_as_uint(o.w)) : 0.f);
+            float time = 0.f;
+            if (INST && P.has_mb) time = unit_time(P, unit_pixel(P, P.unit_base + __float_as_uint(o.w) / np));
+            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), time);
             DHit h{1e12f, 0.f, 0.f, -1};
             const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
             P.ch_hit[base + e] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
@@ -279,11 +374,11 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
 
 // Shading of chain level k >= 1.  kGen (one launch per level, k =
 // P.ch_level): every entry that hit writes its shadow rays (level-k slots
-// e * max_shadow + j) and its spawned child.  kResolve (one launch per chunk,
-// all levels 1 .. ch_levels - 1): a missed child ends its path with the
-// environment (or nothing: a GI ray without environment sampling), a hit is
-// shaded again with its shadow answers and writes its level record or the
-// path's final value.
+// e * max_shadow + j) and its spawned children.  kResolve (one launch per
+// chunk, all levels 1 .. ch_levels - 1): a missed ray ends its path with the
+// environment (or nothing: a GI ray without environment sampling; a split
+// child: nothing, flagged missed), a hit is shaded again with its shadow
+// answers and writes its value or marks itself pending.
 template <bool POINT_ONLY, bool INST, int REC, int MODE>
 __global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
     __shared__ float s_ior[kIorCap * kWG];
@@ -293,13 +388,12 @@ __global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
     Trav T{P.nodes, false, false, P.leaves, rcpT, nullptr, nullptr, P.gstride};   // unused: no traversal
     TravStats st;
     uint32_t shadow_total = 0, secondary_total = 0;
-    const size_t cap = P.ch_cap;
     const uint32_t np = (uint32_t)P.num_paths;
     float* iorS = s_ior + tid;
     const int k0 = MODE == kGen ? P.ch_level : 1, k1 = MODE == kGen ? P.ch_level + 1 : P.ch_levels;
     for (int k = k0; k < k1; k++) {
         const uint32_t n = P.ch_cnt[k];
-        const size_t base = lvl_off(P, k);
+        const size_t base = lofs(P, k), cap = lcap(P, k);
         for (uint32_t e0 = (uint32_t)blockIdx.x * kWG + (uint32_t)(tid & ~63); e0 < n; e0 += gridDim.x * (uint32_t)kWG) {
             const uint32_t e = e0 + (uint32_t)lane;
             if (e >= n) continue;
@@ -313,46 +407,46 @@ __global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
             const DHit h{hv.x, hv.y, hv.z, __float_as_int(hv.w)};
             if (h.prim < 0) {   // the child missed: environment (Lr / Lt, or GI with sampleEnv) or nothing
                 if (MODE == kGen) {
-                    P.nrays[(size_t)k * cap + e] = 0;
-                    P.ch_flag[e] = 0;
+                    P.nrays[base + e] = 0;
+                    if (k + 1 < P.ch_levels) no_children(P, e);
                 } else {
-                    write_final(P, p, env_miss ? env_or_bg(P, mk(d.x, d.y, d.z)) : mk(0, 0, 0), k, !env_miss, e);
+                    write_val(P, k, e, env_miss ? env_or_bg(P, mk(d.x, d.y, d.z)) : mk(0, 0, 0),
+                              kValMissed | (env_miss ? 0u : kValNone));
                 }
                 continue;
             }
-            // the pixel of path p (RNG key, frame of a batched launch)
-            const uint32_t pl = p / np, path = p - pl * np;
-            int x, y;
-            size_t slot;
-            item_pixel(P, P.item_base + (int)(pl >> 6), (int)(pl & 63u), x, y, slot);
-            const int f = item_frame(P, P.item_base + (int)(pl >> 6));
+            // the unit of path p (pixel, eye sample: the RNG keys; frame of a batched launch)
+            const uint32_t u = p / np, path = p - u * np;
+            const UnitPix U = unit_pixel(P, P.unit_base + u);
             const float4 i0 = P.ch_ior[2 * base + e], i1 = P.ch_ior[2 * base + cap + e];
             iorS[0] = 1.0f;
             iorS[1 * kWG] = i0.x; iorS[2 * kWG] = i0.y; iorS[3 * kWG] = i0.z; iorS[4 * kWG] = i0.w;
             iorS[5 * kWG] = i1.x; iorS[6 * kWG] = i1.y; iorS[7 * kWG] = i1.z;
             const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z));
-            Shader<POINT_ONLY, false, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * P.cam[f].W + x), 0u,
-                                                        P.seed + (uint32_t)f,
+            Shader<POINT_ONLY, false, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(U.y * P.cam[U.f].W + U.x), 0u,
+                                                        P.seed + (uint32_t)U.f,
                                                         shadow_base(P, k) + (size_t)e * (size_t)P.max_shadow, 0u};
             S.iorS = iorS;
-            S.skey = path;
-            if (INST && P.has_mb) S.time = S.shadow_time = path_time(P, p);
+            S.skey = U.sample * 1024u + path;
+            if (INST && P.has_mb) S.time = S.shadow_time = unit_time(P, U);
             typename Shader<POINT_ONLY, false, INST, MODE, REC>::IorCam icam;   // unused below the camera ray
             LevelOut lo;
             S.template level<false>(r, h, cs, icam, chain_rec(P, k, e), lo);
-            shadow_total += S.shadow_rays;
-            secondary_total += S.secondary;
-            if (MODE == kGen) {
-                P.nrays[(size_t)k * cap + e] = (uint8_t)S.nslot;
-                const bool spawn = lo.spawn && k + 1 < P.ch_levels;
-                if (spawn) write_spawn(P, e, lo, p, cs, iorS);
-                P.ch_flag[e] = spawn ? 1 : 0;
-            } else if (lo.spawn && k + 1 >= P.ch_levels) {   // deeper than the chain bound (cannot happen)
-                atomicOr(&P.ctr[CTR_OVERFLOW], 2ull);
-                write_final(P, p, mk(0, 0, 0), k, false, e);
-            } else if (!lo.spawn) {
-                write_final(P, p, lo.val, k, false, e);
+            if (MODE == kGen) P.nrays[base + e] = (uint8_t)S.nslot;
+            if (lo.spawn && k + 1 >= P.ch_levels) {   // deeper than the chain bound (cannot happen)
+                if (MODE != kGen) {
+                    atomicOr(&P.ctr[CTR_OVERFLOW], 2ull);
+                    write_val(P, k, e, mk(0, 0, 0), 0u);
+                }
+            } else if (lo.spawn) {
+                spawn_children(P, S, k, e, p, cs, icam, lo, MODE == kGen);
+            } else if (MODE == kGen) {
+                if (k + 1 < P.ch_levels) no_children(P, e);
+            } else {
+                write_val(P, k, e, lo.val, 0u);
             }
+            shadow_total += S.shadow_rays;
+            secondary_total += S.secondary;   // after spawn_children: a split's children count there
         }
     }
     if (MODE == kGen) {
@@ -361,60 +455,198 @@ __global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
     }
 }
 
-// One lane per path of the chunk: the path's final value folded up its chain
-// with chain_combine, deepest level first (Blinn::shade's returns), into ch_tv.
-__global__ void __launch_bounds__(kWG) chain_path_kernel(RenderParams P) {
-    const size_t cap = P.ch_cap;
-    const uint32_t n = (uint32_t)P.n_tiles * 64u * (uint32_t)P.num_paths;
-    for (uint32_t p = blockIdx.x * kWG + threadIdx.x; p < n; p += gridDim.x * kWG) {
-        uint32_t e = P.ch_te[p];
-        if (e == kDeadPath) continue;
-        const float4 tv = P.ch_tv[p];
-        const uint32_t bits = __float_as_uint(tv.w);
-        v3 val = mk(tv.x, tv.y, tv.z);
-        bool none = (bits >> 8) & 1u;
-        for (int kk = (int)(bits & 255u) - 1; kk >= 0; kk--) {
-            const uint32_t pe = __float_as_uint(P.ch_ior[2 * lvl_off(P, kk + 1) + cap + e].w);   // parent entry
-            val = chain_combine(P, chain_rec(P, kk, pe), val, none);
-            none = false;
-            e = pe;
+// Fold of level k (deepest first): every pending entry takes its value from its
+// children at level k + 1 (Blinn::shade's returns): one child through
+// chain_combine; a dispersive split adds each child that hit, masked to its
+// channel, Lt += m_ks * (refraction * mask) in channel order, and with no child
+// hit Lt takes m_ks * the environment along channel 2's direction
+// (src/Blinn.cpp:275-301, Shader::shade_path's fold).
+__global__ void __launch_bounds__(kWG) chain_fold_kernel(RenderParams P) {
+    const int k = P.ch_level;
+    const uint32_t n = k == 0 ? chunk_units(P) * (uint32_t)P.num_paths : P.ch_cnt[k];
+    const uint16_t* rsqT = P.tables + 2048;
+    const uint32_t* map = P.ch_map + (size_t)P.ch_split * lofs(P, k);
+    const size_t cb = lofs(P, k + 1);
+    const v3 z = mk(0, 0, 0);
+    for (uint32_t e = blockIdx.x * kWG + threadIdx.x; e < n; e += gridDim.x * kWG) {
+        const size_t g = (size_t)lofs(P, k) + e;
+        const float4 v = P.ch_val[g];
+        const uint32_t fl = __float_as_uint(v.w);
+        if (!(fl & kValPending)) continue;
+        const ChainRec rec = chain_rec(P, k, e);
+        v3 val;
+        if (!(fl & kValSplit)) {
+            const float4 c = P.ch_val[cb + map[(size_t)e * P.ch_split]];
+            val = chain_combine(P, rec, mk(c.x, c.y, c.z), (__float_as_uint(c.w) & kValNone) != 0);
+        } else {
+            const DevMaterial& M = P.mats[__float_as_int(rec(0)) & 0xFFFF];
+            const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
+            v3 Lt = mk(rec(3), rec(4), rec(5));
+            bool any = false;
+            for (int i = 0; i < 3; i++) {
+                const float4 c = P.ch_val[cb + map[(size_t)e * P.ch_split + i]];
+                if (__float_as_uint(c.w) & kValMissed) continue;   // a missed child adds nothing
+                const v3 mask = mk(i == 0 ? 1.0f : 0.0f, i == 1 ? 1.0f : 0.0f, i == 2 ? 1.0f : 0.0f);
+                Lt = add(Lt, mul(ks, mul(mk(c.x, c.y, c.z), mask)));
+                any = true;
+            }
+            if (!any) {   // doEnv: no child hit
+                const v3 rayD = mk(rec(11), rec(12), rec(13)), nn = mk(rec(14), rec(15), rec(16));
+                const float vDotN = rec(17), q = rec(18) / rec(21);
+                const float sq = std_max(0.0f, sqrtf(1.0f - (q * q) * (1.0f - vDotN * vDotN)));
+                const v3 dir2 = normalized(add(scale(rayD, q), scale(nn, q * vDotN - sq)), rsqT);
+                Lt = add(Lt, mul(ks, env_or_bg(P, dir2)));
+            }
+            const v3 ka = mk(M.ka[0], M.ka[1], M.ka[2]), le = mk(M.le[0], M.le[1], M.le[2]);
+            const v3 base = scale(add(add(add(z, ka), z), z), rec(1));
+            val = add(add(base, scale(add(z, Lt), rec(2))), le);
         }
-        P.ch_tv[p] = make_float4(val.x, val.y, val.z, 0.f);
+        P.ch_val[g] = make_float4(val.x, val.y, val.z, __uint_as_float(0u));
     }
 }
 
-// Per pixel of the chunk: the paths' values summed in path order and averaged
-// as Scene::sampleScene does (src/Scene.cpp:224-233); a missed camera ray takes
-// the environment / background.  Float RGB + Image::Map 8-bit.
+// Per unit of the chunk: the paths' values summed in path order and averaged
+// as Scene::sampleScene does (src/Scene.cpp:224-233); a missed eye ray takes
+// the environment / background.  Frame / bucket mode: float RGB + Image::Map
+// 8-bit of the pixel; adaptive passes: the unit's colour (ucol).
 __global__ void __launch_bounds__(kWG) chain_finish_kernel(RenderParams P) {
-    const int tid = threadIdx.x, lane = tid & 63;
     const uint16_t* rsqT = P.tables + 2048;
-    const uint32_t np = (uint32_t)P.num_paths;
-    for (int item = (int)(blockIdx.x * (kWG / 64) + (tid >> 6)); item < P.n_tiles; item += (int)(gridDim.x * (kWG / 64))) {
-        int x, y;
-        size_t slot;
-        if (!item_pixel(P, P.item_base + item, lane, x, y, slot)) continue;
-        const float4 hv = P.hits[slot];
+    const uint32_t np = (uint32_t)P.num_paths, n = chunk_units(P);
+    for (uint32_t u = blockIdx.x * kWG + threadIdx.x; u < n; u += gridDim.x * kWG) {
+        const UnitPix U = unit_pixel(P, P.unit_base + u);
+        if (!U.valid) continue;
+        const float4 hv = unit_hit(P, u, U);
         v3 col;
         if (__float_as_int(hv.w) >= 0) {
             v3 result = mk(0, 0, 0);
-            const uint32_t pbase = ((uint32_t)item * 64u + (uint32_t)lane) * np;
             for (uint32_t path = 0; path < np; path++) {
-                const float4 v = P.ch_tv[pbase + path];
+                const float4 v = P.ch_val[u * np + path];
                 result = add(result, mk(v.x, v.y, v.z));
             }
             col = scale(result, 1.0f / (float)P.num_paths);
         } else {
-            const int f = item_frame(P, P.item_base + item);
-            col = P.env ? env_or_bg(P, camera_ray(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT).d) : mk(P.bg[0], P.bg[1], P.bg[2]);
+            col = P.env ? env_or_bg(P, unit_eye(P, U, rsqT).d) : mk(P.bg[0], P.bg[1], P.bg[2]);
+        }
+        if (P.ucol) {
+            P.ucol[P.unit_base + u] = make_float4(col.x, col.y, col.z, 0.f);
+            continue;
         }
         if (P.out_rgb) {
-            float* o = P.out_rgb + 3 * slot;
+            float* o = P.out_rgb + 3 * U.slot;
             o[0] = col.x; o[1] = col.y; o[2] = col.z;
         }
         if (P.out_rgb8) {
-            uint8_t* o8 = P.out_rgb8 + 3 * slot;
+            uint8_t* o8 = P.out_rgb8 + 3 * U.slot;
             o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
+        }
+    }
+}
+
+// Adaptive pass n: the eye rays of the chunk's units, closest hits into uhits
+// (the centre ray of pass 1 is also the pixel's hit record, as the fused
+// adaptive kernel writes it).  Counts eye rays and eye-ray hits.
+template <bool COUNT, bool FAST, bool INST, int MINW = 1>
+__global__ void __launch_bounds__(kWG, MINW) unit_eye_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[2048];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    const uint32_t n = chunk_units(P);
+    if ((uint32_t)blockIdx.x * kWG >= n) return;   // before any barrier
+    load_tables(P.tables, s_tab, 1024);
+    const uint16_t* rsqT = P.tables + 2048;
+    const int tid = threadIdx.x, lane = tid & 63;
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, s_tab, s_stack + tid,
+           P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
+    trav_alpha(T, P);
+    TravStats st;
+    uint32_t rays = 0, hits = 0;
+    for (uint32_t u0 = (uint32_t)blockIdx.x * kWG + (uint32_t)(tid & ~63); u0 < n; u0 += gridDim.x * (uint32_t)kWG) {
+        const uint32_t u = u0 + (uint32_t)lane;
+        if (u >= n) continue;
+        const UnitPix U = unit_pixel(P, P.unit_base + u);
+        DHit h{1e12f, 0.f, 0.f, -1};
+        bool hit = false;
+        if (U.valid) {
+            const EyeRay er = unit_eye(P, U, rsqT);
+            hit = traverse<false, COUNT, FAST, INST>(T, make_ray(er.o, er.d, er.time), 0.001f, h, st);
+            rays++;
+            hits += hit ? 1u : 0u;
+        }
+        const float4 rec = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
+        P.uhits[u] = rec;
+        if (U.valid && U.sample == 0) P.hits[U.slot] = rec;
+    }
+    unsigned long long er = rays, eh = hits;
+    for (int off = 32; off > 0; off >>= 1) {
+        er += __shfl_down(er, off);
+        eh += __shfl_down(eh, off);
+    }
+    if (lane == 0) {
+        if (er) atomicAdd(&P.ctr[CTR_RAYS_P], er);
+        if (eh) atomicAdd(&P.ctr[CTR_HITS], eh);
+    }
+    if (COUNT) {
+        unsigned long long nv = st.nodes, lv = st.leaves;
+        for (int off = 32; off > 0; off >>= 1) {
+            nv += __shfl_down(nv, off);
+            lv += __shfl_down(lv, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&P.ctr[CTR_NODES], nv);
+            atomicAdd(&P.ctr[CTR_LEAVES], lv);
+        }
+    }
+    if (st.overflow) atomicOr(&P.ctr[CTR_OVERFLOW], 1ull);
+}
+
+// After adaptive pass n: per pixel of the pass, Scene::adaptiveSampleScene's
+// bookkeeping in the fused adaptive kernel's order -- pass 1 sets the result;
+// pass n >= 2 adds its n^2 colours in (i, j) order, forms the running mean with
+// getSum's float 1/6 and the gamma-space change; then the pixel either refines
+// (listed for pass n + 1) or is written (float RGB + Image::Map 8-bit).
+__global__ void __launch_bounds__(kWG) adapt_combine_kernel(RenderParams P) {
+    const int n = P.adapt_n;
+    const uint32_t nn = (uint32_t)(n * n);
+    const uint32_t npx = P.unit_cnt ? *P.unit_cnt : P.units_total;
+    for (uint32_t r = blockIdx.x * kWG + threadIdx.x; r < npx; r += gridDim.x * kWG) {
+        const uint32_t id = P.units ? P.units[r] : r;   // item << 6 | lane
+        int x, y;
+        size_t slot;
+        if (!item_pixel(P, (int)(id >> 6), (int)(id & 63u), x, y, slot)) continue;
+        v3 result;
+        bool cut = false;
+        if (n == 1) {
+            const float4 c = P.ucol[r];
+            result = mk(c.x, c.y, c.z);
+        } else {
+            const float4 rv = P.adapt_res[slot];
+            result = mk(rv.x, rv.y, rv.z);
+            v3 cur = mk(0, 0, 0);
+            for (uint32_t q = 0; q < nn; q++) {
+                const float4 c = P.ucol[(size_t)r * nn + q];
+                cur = add(cur, mk(c.x, c.y, c.z));
+            }
+            const float pre = (float)sum_squares(n - 1), now = (float)(n * n);
+            const v3 nr = scale(add(scale(result, pre), cur), 1.0f / (pre + now));
+            const float tx = gamma_f(P.gammaF, result.x) - gamma_f(P.gammaF, nr.x);
+            const float ty = gamma_f(P.gammaF, result.y) - gamma_f(P.gammaF, nr.y);
+            const float tz = gamma_f(P.gammaF, result.z) - gamma_f(P.gammaF, nr.z);
+            cut = fmaxf(fabsf(tx), fmaxf(fabsf(ty), fabsf(tz))) < P.noise;
+            result = nr;
+        }
+        const int level = n + 1;
+        if ((level <= P.max_subdivs && !cut) || level <= P.min_subdivs) {
+            P.adapt_res[slot] = make_float4(result.x, result.y, result.z, 0.f);
+            P.next_units[atomicAdd(P.next_cnt, 1u)] = id;
+            continue;
+        }
+        if (P.out_rgb) {
+            float* o = P.out_rgb + 3 * slot;
+            o[0] = result.x; o[1] = result.y; o[2] = result.z;
+        }
+        if (P.out_rgb8) {
+            uint8_t* o8 = P.out_rgb8 + 3 * slot;
+            o8[0] = map8(P.gamma, result.x); o8[1] = map8(P.gamma, result.y); o8[2] = map8(P.gamma, result.z);
         }
     }
 }
@@ -446,8 +678,15 @@ KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves) {
     return c ? (f ? chain_trace_kernel<true, true, false> : chain_trace_kernel<true, false, false>)
              : (f ? chain_trace_kernel<false, true, false> : chain_trace_kernel<false, false, false>);
 }
+KernelFn pick_unit_eye(bool c, bool f, bool inst) {
+    if (inst) return c ? (f ? unit_eye_kernel<true, true, true> : unit_eye_kernel<true, false, true>)
+                       : (f ? unit_eye_kernel<false, true, true> : unit_eye_kernel<false, false, true>);
+    if (!c) return f ? unit_eye_kernel<false, true, false, 7> : unit_eye_kernel<false, false, false, 7>;
+    return f ? unit_eye_kernel<true, true, false> : unit_eye_kernel<true, false, false>;
+}
 KernelFn pick_chain_compact() { return chain_compact_kernel; }
 KernelFn pick_chain_finish() { return chain_finish_kernel; }
-KernelFn pick_chain_path() { return chain_path_kernel; }
+KernelFn pick_chain_fold() { return chain_fold_kernel; }
+KernelFn pick_adapt_combine() { return adapt_combine_kernel; }
 
 }  // namespace mrt

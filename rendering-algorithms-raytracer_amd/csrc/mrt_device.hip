@@ -535,8 +535,11 @@ struct StreamCtx {
     size_t lvl_cap = 0;                      //   floats
     void* chain = nullptr;                   // wavefront chain engine scratch (mrt_chain.hip)
     size_t chain_bytes = 0;
+    void* adapt = nullptr;                   // chain-engine adaptive supersampling: means, pixel lists, unit colours
+    size_t adapt_bytes = 0;
     bool last_was_render = false;
     bool fused = false;                      // the last render ran frame1_kernel (one launch)
+    bool chain_used = false;                 // the last render's shading ran the wavefront chain engine
     uint32_t* tile_cost = nullptr;           // frame1_kernel: per-tile cycles of the last frame on this stream
     uint32_t* tile_order = nullptr;          //   and the queue order derived from them
     int tile_cap = 0, order_tiles = 0;       //   capacity; tiles of the frame the order is valid for (0: none)
@@ -620,15 +623,17 @@ static int g_near_first = -1;     // any-hit walks take the nearest hit child fi
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
 static int g_chain_mb = 16384;    // chain scratch per stream (MB); larger frames run in chunks of work items
+static int g_chain_adapt = 1;     // adaptive supersampling of REC scenes: passes over the chain engine (0: fused kernel)
 static int g_fused = 1;           // one point light, one path: frame1_kernel (primary + shading in one launch)
 static int g_frame1_waves = 6;    // frame1_kernel launch-bounds occupancy target: 1 (none), 5..8
-static int g_tile_lpt = 1;        // frame1_kernel: tile queue ordered by the previous frame's tile costs
+static int g_tile_lpt = 0;        // frame1_kernel: tile queue ordered by the previous frame's tile costs (off: -2% single-frame latency
+                                  // but +10% ms/frame with 4 frames in flight, the bench mode; profiles/r03_lpt_ab.txt)
 
 static inline int fast_box(const DeviceState& d);
 
 static void free_ctx(StreamCtx* c) {
     void* ptrs[] = {c->gstack, c->ctr, c->wave_log, c->hitbuf, c->rays, c->occl, c->nrays, c->lvl, c->chain,
-                    c->tile_cost, c->tile_order};
+                    c->tile_cost, c->tile_order, c->adapt};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1176,11 +1181,11 @@ static KernelFn pick_shade(bool c, bool po, bool f, bool inst, int rec) {
 }
 
 // The wavefront chain engine (mrt_chain.hip) for the shading of a REC scene:
-// per chunk of work items, level 0 of every path (gen, shadow rays, resolve),
-// then per level compact / trace / gen / shadow rays / resolve, then the
-// per-pixel combine.  P holds the primary launch's parameters (hits, outputs,
-// cameras, work items); the chunks are sized so the per-level arrays fit
-// g_chain_mb.
+// per chunk of work units (eye rays), level 0 of every path (gen, shadow rays,
+// resolve), then per level compact / trace / gen / shadow rays / resolve, the
+// per-level folds and the per-unit finish.  P holds the primary launch's
+// parameters (hits, outputs, cameras, work items, or an adaptive pass's units);
+// the chunks are sized so the per-level arrays fit g_chain_mb.
 static constexpr int kMaxChainLevels = 63;   // < the 64 level counts (level L's count stays 0)
 // shadow rays one chain level of one path traces at most: every light's
 // samples for the direct term, again for translucency, again for the last GI
@@ -1193,28 +1198,97 @@ static int chain_shadow_rays(const Scene& s) {
     const int m = per * (1 + (tr ? 1 : 0) + (s.path_trace ? 1 : 0));
     return m <= 255 ? std::max(1, m) : 0;
 }
-static bool use_chain(const Scene& s) {
-    return s.dev->recursive && !s.dev->disperse && g_chain && chain_levels(s) <= kMaxChainLevels &&
-           chain_shadow_rays(s) > 0;
+// Entries of chain level k per path at most: one child per level, except a
+// dispersive split's three (src/Blinn.cpp:275-301).  Split children are
+// refraction rays, which do not split again, so splits are at least two levels
+// apart: 3^ceil(k/2).  (Dispersion with path tracing -- GI levels without a
+// bounce bound on splits -- stays on the fused kernel.)
+static uint64_t level_mult(const Scene& s, int k) {
+    uint64_t m = 1;
+    if (s.dev->disperse)
+        for (int i = 0; i < (k + 1) / 2; i++) m *= 3;
+    return m;
 }
-static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool count, hipStream_t stream) {
+static bool use_chain(const Scene& s) {
+    return s.dev->recursive && g_chain && chain_levels(s) <= kMaxChainLevels && chain_shadow_rays(s) > 0 &&
+           !(s.dev->disperse && s.path_trace);
+}
+// One chunk of the engine over units [Q.unit_base, Q.unit_base + Q.n_units) of
+// Q's pass (the chunk layout -- ch_lofs, arrays -- is set by the caller).
+static int chain_chunk(Scene& s, RenderParams& Q, bool count, hipStream_t stream, size_t ctl, unsigned int* queues) {
     DeviceState& d = *s.dev;
-    const int L = chain_levels(s), W = level_words(s), m = chain_shadow_rays(s);
-    const size_t per_item = (size_t)64 * (size_t)P0.num_paths;
-    // per path slot: L x (ray, ior 2 x 16 B each, hit 16 B, record, shadow rays m x (32 B + occlusion
-    // byte) + ray count), spawn 64 B, final 16 + 4 B, flag
-    const size_t slot_bytes = (size_t)L * (2 * 16 + 2 * 16 + 16 + 4 * (size_t)W + (size_t)m * 33 + 1) + 4 * 16 + 16 + 4 + 1;
-    const size_t budget = (size_t)g_chain_mb << 20;
-    size_t items = std::max<size_t>(1, budget / (slot_bytes * per_item));
-    items = std::min(items, (size_t)P0.n_tiles);
-    const size_t cap = items * per_item;
-    if (cap * (size_t)m * (size_t)L >= (size_t(1) << 32)) { set_error("chain chunk too large"); return MRT_ERR_INVALID; }
+    const int L = Q.ch_levels;
+    const bool inst = d.special;
+    const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive), r0 = pick_chain0(true, d.point_only, inst, d.recursive);
+    const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive),
+                   rk = pick_chain_shade(true, d.point_only, inst, d.recursive);
+    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, Q.fast_box != 0, inst, g_chain_trace_waves),
+                   kf = pick_chain_finish(), kd = pick_chain_fold();
+    auto go = [&](KernelFn f, int g) -> int {
+        void* args[] = {&Q};
+        HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(f), dim3(std::max(1, g)), dim3(kWG), args, 0, stream));
+        return MRT_OK;
+    };
+    auto full = [&](KernelFn f) { return std::min(d.grid, d.cus * blocks_per_cu(f, 0)); };
+    const int ug = (int)std::min<uint64_t>((uint64_t)full(r0), ((uint64_t)Q.n_units + kWG - 1) / kWG);
     int rc;
-    if ((rc = ensure_rays(c, cap * (size_t)L, (size_t)m))) return rc;   // every level keeps its shadow rays
-    // layout: ray | ior | hit | sp | tv (float4), rec (float), te (u32), control (counts + queues), flag (u8)
+    HIP_OK(hipMemsetAsync(Q.ch_cnt, 0, ctl, stream));
+    Q.queue = queues;
+    if (Q.uhits) {   // adaptive pass: the chunk's eye rays and their closest hits
+        const KernelFn ke = pick_unit_eye(count, Q.fast_box != 0, inst);
+        if ((rc = go(ke, (int)std::min<uint64_t>((uint64_t)full(ke), ((uint64_t)Q.n_units + kWG - 1) / kWG)))) return rc;
+    }
+    Q.ch_level = 0;
+    if ((rc = go(g0, ug))) return rc;                 // level 0: shadow rays + children
+    for (int k = 0; k + 1 < L; k++) {
+        Q.ch_level = k;
+        if ((rc = go(kc, full(kc)))) return rc;        // children of level k -> entries of level k + 1
+        Q.ch_level = k + 1;
+        if ((rc = go(kt, full(kt)))) return rc;        // their closest hits + level k's shadow rays
+        if ((rc = go(gk, full(gk)))) return rc;        // level k + 1: shadow rays + children
+    }
+    Q.ch_level = L;
+    if ((rc = go(kt, full(kt)))) return rc;            // the last level's shadow rays
+    Q.queue = queues + 256;
+    if ((rc = go(r0, ug))) return rc;                  // resolve level 0, then levels 1 .. L - 1
+    if ((rc = go(rk, full(rk)))) return rc;
+    for (int k = L - 2; k >= 0; k--) {                 // fold the values up, deepest level first
+        Q.ch_level = k;
+        if ((rc = go(kd, full(kd)))) return rc;
+    }
+    return go(kf, ug);                                 // per unit: paths averaged, pixel / unit colour
+}
+
+// The chain engine over a pass of `units_max` units (at most; the adaptive
+// passes' counts live on the device): the scratch layout for `per_chunk`
+// units, then the chunks.
+static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool count, hipStream_t stream,
+                        uint64_t units_max, int unit_align) {
+    DeviceState& d = *s.dev;
+    const int L = chain_levels(s), W = level_words(s), m = chain_shadow_rays(s), split = d.disperse ? 3 : 1;
+    const uint64_t np = (uint64_t)P0.num_paths;
+    uint64_t mult_sum = 0, mult_max = 0;
+    for (int k = 0; k < L; k++) { mult_sum += level_mult(s, k); mult_max = std::max(mult_max, level_mult(s, k)); }
+    // per path over all levels: ray + ior 2 x 32 B, hit 16, value 16, record 4 W, child map 4 split,
+    // shadow rays m x (32 B + occlusion byte) + ray count; sparse spawn slots 65 B x split x the widest level
+    const uint64_t entry_bytes = 32 + 32 + 16 + 16 + 4 * (uint64_t)W + 4 * (uint64_t)split + (uint64_t)m * 33 + 1;
+    const uint64_t path_bytes = mult_sum * entry_bytes + mult_max * (uint64_t)split * 65;
+    const uint64_t unit_bytes = np * path_bytes + (P0.adapt_n ? 16 : 0);
+    const uint64_t budget = (uint64_t)g_chain_mb << 20;
+    uint64_t per = std::max<uint64_t>(1, budget / unit_bytes);
+    per = std::max<uint64_t>(unit_align, per / unit_align * unit_align);
+    per = std::min<uint64_t>(per, (units_max + unit_align - 1) / unit_align * unit_align);
+    const uint64_t paths = per * np, entries = paths * mult_sum, spcap = paths * mult_max * (uint64_t)split;
+    if (entries * (uint64_t)m >= (uint64_t(1) << 32) || spcap >= (uint64_t(1) << 32)) {
+        set_error("chain chunk too large"); return MRT_ERR_INVALID;
+    }
+    int rc;
+    if ((rc = ensure_rays(c, entries, (size_t)m))) return rc;   // every level keeps its shadow rays
+    // layout: ray | ior (2 per entry) | hit | val | spawn (4 per slot) | uhits (float4), rec (float),
+    // map (u32), control (counts + queues), flag (u8)
     const size_t ctl = 256 + (size_t)(L + 2) * 1024;
-    const size_t n4 = (size_t)L * 2 * cap + (size_t)L * 2 * cap + (size_t)L * cap + 4 * cap + cap;
-    const size_t bytes = n4 * 16 + (size_t)L * W * cap * 4 + cap * 4 + ctl + cap;
+    const uint64_t n4 = 2 * entries + 2 * entries + entries + entries + 4 * spcap + (P0.adapt_n ? per : 0);
+    const uint64_t bytes = n4 * 16 + entries * (uint64_t)W * 4 + entries * (uint64_t)split * 4 + ctl + spcap;
     if (bytes > c.chain_bytes) {
         if (c.chain) { HIP_OK(hipStreamSynchronize(c.stream)); (void)hipFree(c.chain); }
         c.chain = nullptr; c.chain_bytes = 0;
@@ -1223,61 +1297,80 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     }
     RenderParams Q = P0;
     float4* f4 = static_cast<float4*>(c.chain);
-    Q.ch_ray = f4; f4 += (size_t)L * 2 * cap;
-    Q.ch_ior = f4; f4 += (size_t)L * 2 * cap;
-    Q.ch_hit = f4; f4 += (size_t)L * cap;
-    Q.ch_sp = f4; f4 += 4 * cap;
-    Q.ch_tv = f4; f4 += cap;
+    Q.ch_ray = f4; f4 += 2 * entries;
+    Q.ch_ior = f4; f4 += 2 * entries;
+    Q.ch_hit = f4; f4 += entries;
+    Q.ch_val = f4; f4 += entries;
+    Q.ch_sp = f4; f4 += 4 * spcap;
+    Q.uhits = P0.adapt_n ? f4 : nullptr; f4 += P0.adapt_n ? per : 0;
     Q.ch_rec = reinterpret_cast<float*>(f4);
-    Q.ch_te = reinterpret_cast<uint32_t*>(Q.ch_rec + (size_t)L * W * cap);
-    Q.ch_cnt = Q.ch_te + cap;                                                  // 64 counts, then L + 2 queues
+    Q.ch_map = reinterpret_cast<uint32_t*>(Q.ch_rec + entries * (uint64_t)W);
+    Q.ch_cnt = Q.ch_map + entries * (uint64_t)split;           // 64 counts, then L + 2 queues
     unsigned int* queues = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(Q.ch_cnt) + 256);
     Q.ch_flag = reinterpret_cast<uint8_t*>(Q.ch_cnt) + ctl;
-    Q.ch_cap = (uint32_t)cap;
+    Q.ch_spcap = (uint32_t)spcap;
+    Q.ch_split = split;
     Q.ch_levels = L;
+    uint64_t off = 0;
+    for (int k = 0; k <= L; k++) {
+        Q.ch_lofs[k] = (uint32_t)off;
+        if (k < L) off += paths * level_mult(s, k);
+    }
     Q.lvl_words = W;
     Q.order = 0;          // chunks index work items directly
     Q.wave_log = nullptr;
     Q.ray_o = c.rays;
-    Q.ray_d = c.rays + cap * (size_t)L * (size_t)m;
+    Q.ray_d = c.rays + entries * (uint64_t)m;
     Q.occl = c.occl;
     Q.nrays = c.nrays;
     Q.max_shadow = m;
-    const bool fb = Q.fast_box != 0, inst = d.special;
-    const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive), r0 = pick_chain0(true, d.point_only, inst, d.recursive);
-    const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive),
-                   rk = pick_chain_shade(true, d.point_only, inst, d.recursive);
-    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, fb, inst, g_chain_trace_waves), kf = pick_chain_finish(),
-                   kp = pick_chain_path();
-    auto go = [&](KernelFn f, int g) -> int {
-        void* args[] = {&Q};
-        HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(f), dim3(std::max(1, g)), dim3(kWG), args, 0, stream));
-        return MRT_OK;
-    };
-    auto full = [&](KernelFn f) { return std::min(d.grid, d.cus * blocks_per_cu(f, 0)); };
-    for (size_t b = 0; b < (size_t)P0.n_tiles; b += items) {
-        const int n = (int)std::min(items, (size_t)P0.n_tiles - b);
-        Q.item_base = (int32_t)b;
-        Q.n_tiles = n;
-        HIP_OK(hipMemsetAsync(Q.ch_cnt, 0, ctl, stream));
-        const int g0n = std::min(full(r0), (n + 3) / 4);
-        Q.ch_level = 0;
-        Q.queue = queues;
-        if ((rc = go(g0, g0n))) return rc;                 // level 0: shadow rays + children
-        for (int k = 0; k + 1 < L; k++) {
-            Q.ch_level = k;
-            if ((rc = go(kc, full(kc)))) return rc;        // children of level k -> entries of level k + 1
-            Q.ch_level = k + 1;
-            if ((rc = go(kt, full(kt)))) return rc;        // their closest hits + level k's shadow rays
-            if ((rc = go(gk, full(gk)))) return rc;        // level k + 1: shadow rays + children
-        }
-        Q.ch_level = L;
-        if ((rc = go(kt, full(kt)))) return rc;            // the last level's shadow rays
-        Q.queue = queues + 256;
-        if ((rc = go(r0, g0n))) return rc;                 // resolve level 0, then levels 1 .. L - 1
-        if ((rc = go(rk, full(rk)))) return rc;
-        if ((rc = go(kp, full(kp)))) return rc;            // fold each path up its chain
-        if ((rc = go(kf, std::min(d.grid, (n + 3) / 4)))) return rc;
+    Q.n_units = (uint32_t)per;
+    for (uint64_t b = 0; b < units_max; b += per) {
+        Q.unit_base = (uint32_t)b;
+        if ((rc = chain_chunk(s, Q, count, stream, ctl, queues))) return rc;
+    }
+    return MRT_OK;
+}
+
+// Adaptive supersampling of a REC scene on the chain engine: passes n = 1 ..
+// max_subdivs over the pixels still refining (each pass: the units' eye rays,
+// the chain engine, then adapt_combine's running mean + stop test, which lists
+// the next pass's pixels or writes the pixel).
+static int launch_chain_adaptive(Scene& s, StreamCtx& c, RenderParams& P, bool count, hipStream_t stream) {
+    DeviceState& d = *s.dev;
+    const uint64_t lanes = (uint64_t)P.n_tiles * 64;   // pixels of the frame / batch (work-item lanes)
+    const int maxs = std::max(P.min_subdivs, P.max_subdivs);
+    // per stream: running means, two pixel lists + counts, unit colours of the largest pass
+    const uint64_t ucol_n = lanes * (uint64_t)maxs * (uint64_t)maxs;
+    const uint64_t bytes = lanes * 16 + 2 * lanes * 4 + 256 + ucol_n * 16;
+    if (bytes > c.adapt_bytes) {
+        if (c.adapt) { HIP_OK(hipStreamSynchronize(c.stream)); (void)hipFree(c.adapt); }
+        c.adapt = nullptr; c.adapt_bytes = 0;
+        HIP_OK(hipMalloc(&c.adapt, bytes));
+        c.adapt_bytes = bytes;
+    }
+    float4* res = static_cast<float4*>(c.adapt);
+    float4* ucol = res + lanes;
+    uint32_t* lists = reinterpret_cast<uint32_t*>(ucol + ucol_n);
+    uint32_t* cnts = lists + 2 * lanes;   // 2 counts (own 256 B)
+    P.adapt_res = res;
+    P.ucol = ucol;
+    int cur = 0, rc;
+    const KernelFn kcomb = pick_adapt_combine();
+    for (int n = 1; n <= maxs; n++) {
+        const int nxt = cur ^ 1;
+        P.adapt_n = n;
+        P.units = n == 1 ? nullptr : lists + (size_t)cur * lanes;
+        P.unit_cnt = n == 1 ? nullptr : cnts + cur;
+        P.units_total = (uint32_t)lanes;
+        P.next_units = lists + (size_t)nxt * lanes;
+        P.next_cnt = cnts + nxt;
+        HIP_OK(hipMemsetAsync(cnts + nxt, 0, 4, stream));
+        if ((rc = launch_chain(s, c, P, count, stream, lanes * (uint64_t)n * (uint64_t)n, 64))) return rc;
+        void* args[] = {&P};
+        const int g = std::min<int>(d.grid, (int)((lanes + kWG - 1) / kWG));
+        HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(kcomb), dim3(std::max(1, g)), dim3(kWG), args, 0, stream));
+        cur = nxt;
     }
     return MRT_OK;
 }
@@ -1331,10 +1424,16 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     HIP_OK(hipEventRecord(c.ev0, stream));
     const bool fb = P.fast_box != 0;
     const bool inst = d.special;   // instances or alpha maps: the special-leaf kernels
+    c.chain_used = false;
     if (P.min_subdivs > 1 || P.max_subdivs > 1) {
         HIP_OK(hipEventRecord(c.evm, stream));   // primary_ms = 0: one launch
         P.refill_min = g_adapt_refill;
-        if ((rc = launch(pick_adaptive(count, d.point_only, fb, inst, d.recursive, g_adapt_waves)))) return rc;
+        if (use_chain(s) && g_chain_adapt) {     // secondary rays: passes over the chain engine
+            c.chain_used = true;
+            if ((rc = launch_chain_adaptive(s, c, P, count, stream))) return rc;
+        } else if ((rc = launch(pick_adaptive(count, d.point_only, fb, inst, d.recursive, g_adapt_waves)))) {
+            return rc;
+        }
         c.last_was_render = true;
         HIP_OK(hipGetLastError());
         HIP_OK(hipEventRecord(c.ev1, stream));
@@ -1380,7 +1479,12 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     // secondary rays and their shadow rays depend on hits along the path: fused kernel
     const bool wave = !one && g_wavefront && max_sh > 0 && max_sh <= kMaxWaveShadow && !d.recursive;
     if (use_chain(s)) {
-        if ((rc = launch_chain(s, c, P, count, stream))) return rc;
+        c.chain_used = true;
+        P.units = nullptr;
+        P.unit_cnt = nullptr;
+        P.adapt_n = 0;
+        P.units_total = (uint32_t)P.n_tiles * 64u;
+        if ((rc = launch_chain(s, c, P, count, stream, (uint64_t)P.n_tiles * 64, 64))) return rc;
     } else if (one || !wave) {
         if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb, inst, d.recursive)))) return rc;
     } else {
@@ -2155,6 +2259,7 @@ static int render_shared(mrt_scene* s, const mrt_camera* cam, const mrt_render_o
         total.primary_uniform_visits += st.primary_uniform_visits;
         total.kernel_ms = std::max(total.kernel_ms, st.kernel_ms);
         total.fused = st.fused;
+        total.chain = st.chain;
         total.max_stack = std::max(total.max_stack, st.max_stack);
         if (src == MRT_ERR_OVERFLOW) rc = src;
         // scatter the share's buckets into the frame (row 0 = bottom)
@@ -2286,6 +2391,7 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     }
     S.last.kernel_ms = ms;
     S.last.fused = x.last_was_render && x.fused ? 1 : 0;
+    S.last.chain = x.last_was_render && x.chain_used ? 1 : 0;
     *out = S.last;
     if (c[CTR_OVERFLOW]) { set_error("traversal stack overflow"); return MRT_ERR_OVERFLOW; }
     return MRT_OK;
@@ -2402,6 +2508,8 @@ int mrt_set_tuning(const char* key, int value) {
         g_wavefront = value ? 1 : 0;
     } else if (k == "chain") {
         g_chain = value ? 1 : 0;
+    } else if (k == "chain_adapt") {
+        g_chain_adapt = value ? 1 : 0;
     } else if (k == "chain_mb") {
         if (value < 1 || value > 1 << 20) { set_error("chain_mb out of range"); return MRT_ERR_INVALID; }
         g_chain_mb = value;

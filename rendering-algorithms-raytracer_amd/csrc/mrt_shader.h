@@ -36,6 +36,7 @@ static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 4 * 8 *
 // across each traversal.
 enum ShadowMode { kFused = 0, kGen = 1, kResolve = 2 };
 static constexpr int kMaxWaveShadow = 64;  // rays per pixel beyond this use the fused kernel
+static constexpr int kMaxLevelsP1 = 64;     // chain levels + 1 (kMaxChainLevels = 63)
 
 struct RenderParams {
     const QNode* nodes;
@@ -108,20 +109,39 @@ struct RenderParams {
     uint8_t* out_rgb8;           // same slots as out_rgb (nullable)
     float4* hits;                // per slot: t, a, b, prim bits (kernel 1 -> kernel 2)
     // wavefront chain engine (mrt_chain.hip; REC scenes on the frame / bucket
-    // path): level k's entries live in arrays of ch_cap slots each
-    float4* ch_ray;              // [level][2][cap]: origin | path id bits, direction | state bits
-    float4* ch_ior;              // [level][2][cap]: IOR history 1..7 | parent entry bits
-    float4* ch_hit;              // [level][cap]: closest hit (t, a, b, prim bits)
-    float* ch_rec;               // [level][lvl_words][cap]: level records of spawning entries
-    float4* ch_sp;               // [4][cap]: the current level's spawned children, at the parent's index
-    uint8_t* ch_flag;            // [cap]: spawned (ch_sp slot valid)
-    float4* ch_tv;               // [paths]: final value of the path's deepest level | (level | none << 8) bits
-    uint32_t* ch_te;             // [paths]: entry of that level
+    // path): chain level k's entries are [ch_lofs[k], ch_lofs[k + 1]) of every
+    // per-entry array (capacity of level k = ch_lofs[k + 1] - ch_lofs[k]);
+    // two-array fields hold level k's first array at 2 * lofs and its second at
+    // 2 * lofs + capacity (coalesced SoA per level)
+    float4* ch_ray;              // origin | path id bits; direction | state bits
+    float4* ch_ior;              // IOR history 1..4; 5..7 | parent entry bits
+    float4* ch_hit;              // closest hit (t, a, b, prim bits)
+    float* ch_rec;               // lvl_words per entry: the level record of a spawning entry
+    float4* ch_val;              // the entry's value (rgb) | kVal* flags
+    uint32_t* ch_map;            // ch_split per entry: dense entry of the child spawned from that slot
+    float4* ch_sp;               // [4][ch_spcap]: the current level's spawned children, sparse (entry * split + i)
+    uint8_t* ch_flag;            // [ch_spcap]: spawned (ch_sp slot valid)
     uint32_t* ch_cnt;            // [level]: entries (level 0: unused, the chunk's paths)
-    uint32_t ch_cap;             // slots per level array (= paths of a chunk)
+    uint32_t ch_spcap;           // sparse spawn slots
+    int32_t ch_split;            // spawn slots per entry: 3 where dispersive splits can occur, else 1
     int32_t ch_level;            // the level a chain launch works on
     int32_t ch_levels;           // levels allocated
-    int32_t item_base;           // chain launches: first work item of the chunk
+    uint32_t ch_lofs[kMaxLevelsP1 + 1];
+    // work units of the chain engine: one eye ray of a pixel.  Without a unit
+    // list, unit u is lane u & 63 of work item u >> 6 with the centre sample
+    // (adapt_n <= 1); adaptive pass n >= 2: unit u is sample (i, j) = ((u % n^2) / n,
+    // u % n) of pixel units[u / n^2] (item << 6 | lane).  A chunk covers units
+    // [unit_base, unit_base + n_units) of the pass.
+    const uint32_t* units;
+    const uint32_t* unit_cnt;    // device count of `units` (pixels), or null: units_total units
+    uint32_t units_total;
+    uint32_t unit_base, n_units;
+    int32_t adapt_n;             // adaptive supersampling pass (level) n; 0: no adaptive supersampling
+    float4* uhits;               // adaptive: closest hit per unit of the chunk (null: hits[pixel slot])
+    float4* ucol;                // adaptive: colour per unit of the pass
+    float4* adapt_res;           // adaptive: running mean per pixel slot
+    uint32_t* next_units;        // adaptive combine: the pixels that refine further
+    uint32_t* next_cnt;
     const uint32_t* sh_count;    // shadow_kernel: pixel / entry count on the device (nullable)
     // motion blur (MBObject, src/MBObject.cpp): per world prim bit 0 = MBObject
     // lane; time-1 vertices parallel to verts (nullptr: no motion blur)
@@ -633,7 +653,7 @@ struct Shader {
         // inIOR, then a back-face hit pops the (mutable) history (src/Blinn.cpp:167-185);
         // a dispersive material hit by a ray that is not a refraction ray takes
         // outIOR = m_ior[0..2] and does not pop
-        const bool disp = MODE == kFused && M.disperse && !cs.refr;
+        const bool disp = M.disperse && !cs.refr;
         float inIOR, outIOR = M.ior;
         if (disp) {
             inIOR = cs.depth == 0 ? cam.at(cam.idx) : ior_at(cs.idx);
@@ -1438,6 +1458,8 @@ KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec);
 KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves);
 KernelFn pick_chain_compact();
 KernelFn pick_chain_finish();
-KernelFn pick_chain_path();
+KernelFn pick_chain_fold();
+KernelFn pick_unit_eye(bool c, bool f, bool inst);
+KernelFn pick_adapt_combine();
 
 }  // namespace mrt

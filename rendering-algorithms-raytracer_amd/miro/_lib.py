@@ -79,7 +79,7 @@ class mrt_stats(C.Structure):
                 ("primary_span_us", C.c_float), ("primary_ramp_us", C.c_float), ("primary_tail_us", C.c_float),
                 ("shade_span_us", C.c_float), ("shade_ramp_us", C.c_float), ("shade_tail_us", C.c_float),
                 ("secondary_rays", C.c_uint64), ("shadow_wave_steps", C.c_uint64), ("shadow_node_visits", C.c_uint64),
-                ("fused", C.c_int32)]
+                ("fused", C.c_int32), ("chain", C.c_int32)]
 
 
 _fp = C.POINTER(C.c_float)

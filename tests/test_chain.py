@@ -40,6 +40,18 @@ def panel(y=5.45, x=(2.0, 3.5), z=(-3.5, -2.0)):
 
 
 EMIT = dict(kind="blinn", kd=(1, 1, 1), emitted=1.5, le=(1, 1, 1))
+PRISM = dict(kind="blinn", kd=(0.2, 0.3, 0.3), reflectAmt=1.0, refractAmt=1.0, specExp=30.0,
+             disperse=True, ior3=(1.57, 1.60, 1.62))          # src/Assignment3.h:169-177 (mat2)
+FINAL = dict(kind="blinn", kd=(0.9, 0.9, 0.9), reflectAmt=1.0, refractAmt=1.0, specExp=30.0,
+             disperse=True, ior3=(1.56, 1.5, 1.5))            # src/main.cpp:167-174
+
+
+def quad(z=1.0, lo=0.5, hi=5.0):
+    """A two-triangle sheet at depth z facing the C1 camera (+z geometric normal)."""
+    v = np.array([[lo, lo, z], [hi, lo, z], [hi, hi, z], [lo, hi, z]], np.float32)
+    n = np.tile(np.array([[0, 0, 1]], np.float32), (4, 1))
+    idx = np.array([[0, 1, 2], [0, 2, 3]], np.uint32)
+    return v, n, idx, idx.copy()
 
 
 def cornell(material, lights=None, **kw):
@@ -107,16 +119,48 @@ CASES = {
                                                 meshes=[fixture_mesh("cornell_box")], path_trace=(4, False), num_paths=2),
     "dome_bunny_mixed": lambda: scene_pair(dict(scenes.CONFIGS["D1"], material=dict(MIXED, kd=(0.8, 0.8, 0.8))),
                                            obj=scenes.bunny_obj(), floor=True),
+    # dispersive splits (three refraction children per split, folded per level)
+    "disp_sheet_env": lambda: scene_pair(dict(scenes.CONFIGS["C1"], env=dict(sky=(64, 32), exposure=0.7)),
+                                         meshes=[fixture_mesh("cornell_box")], extra=[(quad(), PRISM)]),
+    "disp_cornell_mixed": lambda: cornell(dict(PRISM, kd=(0.6, 0.5, 0.4), ior3=(1.3, 1.5, 1.9)), lights=[RECT, POINT],
+                                          num_paths=2),
+    "disp_bunny_dome": lambda: scene_pair(dict(scenes.CONFIGS["D1"], material=dict(PRISM, kd=(0.8, 0.8, 0.8))),
+                                          obj=scenes.bunny_obj(), floor=True),
+    # adaptive supersampling as passes over the chain engine
+    "adapt_mixed_rect": lambda: cornell(MIXED, lights=[RECT, POINT], subdivs=(1, 3, 0.01)),
+    "adapt_glossy_paths": lambda: cornell(GLOSSY, num_paths=2, subdivs=(2, 3, 0.02)),
+    "adapt_disp_env": lambda: scene_pair(dict(scenes.CONFIGS["C1"], env=dict(sky=(64, 32), exposure=0.7)),
+                                         meshes=[fixture_mesh("cornell_box")], extra=[(quad(), FINAL)],
+                                         subdivs=(1, 3, 0.01)),
+    "adapt_pt_panel": lambda: cornell(dict(kind="blinn", kd=(0.7, 0.7, 0.7), reflectAmt=0.3), lights=[dict(RECT, samples=1)],
+                                      path_trace=(3, False), extra=[(panel(), EMIT)], subdivs=(1, 2, 0.0)),
 }
 
 
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_chain_engine_equals_fused_kernel(case):
     P, _, cam = CASES[case]()
-    W, H = (40, 40) if case.startswith("dome") else (64, 48)
+    W, H = (40, 40) if "dome" in case else (64, 48)
     fused, chain = both_engines(P, cam, W, H)
     assert_same(fused, chain)
+    assert chain[2]["chain"] == 1 and fused[2]["chain"] == 0
     assert chain[2]["secondary_rays"] > 0 or case in ("leaf_translucent", "pt_point_nosample_env")
+    if case.startswith("adapt"):   # eye rays per pixel beyond one: the passes refined
+        assert chain[2]["primary_rays"] == fused[2]["primary_rays"] > W * H
+
+
+@pytest.mark.parametrize("case", ["disp_cornell_mixed", "adapt_disp_env"])
+def test_chain_tree_and_adaptive_chunks_equal_one_chunk(case):
+    """Dispersive trees and adaptive passes with a 2-MB scratch budget (many
+    chunks of units per pass) equal the one-chunk frame."""
+    P, _, cam = CASES[case]()
+    one = render(P, cam, 48, 40)
+    try:
+        tuned(chain_mb=2)
+        many = render(P, cam, 48, 40)
+    finally:
+        tuned(chain_mb=16384)
+    assert_same(one, many)
 
 
 def test_chain_engine_on_instances_with_mirrors():

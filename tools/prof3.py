@@ -39,9 +39,10 @@ SIMDS = 256 * 4
 PASS = {"primary_kernel": "primary", "frame1_kernel": "primary", "shade1_kernel": "shade", "shade_kernel": "shade",
         "shadow_kernel": "shade", "adaptive_kernel": "shade", "chain_trace_kernel": "shade",
         "chain0_kernel": "shade", "chain_shade_kernel": "shade", "chain_compact_kernel": "shade",
-        "chain_finish_kernel": "shade", "chain_path_kernel": "shade", "tile_order_kernel": "shade"}
+        "chain_finish_kernel": "shade", "chain_path_kernel": "shade", "tile_order_kernel": "shade",
+        "chain_fold_kernel": "shade", "unit_eye_kernel": "shade", "adapt_combine_kernel": "shade"}
 NO_COUNT_ARG = {"chain0_kernel", "chain_shade_kernel", "chain_compact_kernel", "chain_finish_kernel",
-                "chain_path_kernel", "tile_order_kernel"}
+                "chain_path_kernel", "tile_order_kernel", "chain_fold_kernel", "adapt_combine_kernel"}
 FRAME_KERNELS = ("primary_kernel", "frame1_kernel", "adaptive_kernel")
 
 

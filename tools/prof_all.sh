@@ -13,7 +13,7 @@ set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd /tmp && export TMPDIR=/tmp
 cd "$ROOT" || exit 1
-OUT=gpurun_out/prof3
+OUT=${OUT:-gpurun_out/prof3}
 mkdir -p $OUT
 export MRT_SCENE_CACHE=/tmp/mrt_scenes
 CONFIGS="${CONFIGS:-C3 C2 C4 D1 C5 A3 R3 P4 G3}"
@@ -32,7 +32,7 @@ run() {
     local cfg="$1" name="$2" lim="$3"; shift 3
     echo "== $cfg $name: $*"
     timeout -s KILL $lim rocprofv3 "$@" --output-format csv -d "$OUT/$cfg/$name" -o run \
-        -- python3 bench.py --config "$cfg" --inflight 1 --steps "$STEPS" --warmup 1 --no-cpu-baseline \
+        -- python3 bench.py --config "$cfg" --inflight 1 --steps "$STEPS" --warmup 1 --no-cpu-baseline $BENCH_EXTRA \
         > "$OUT/$cfg/$name.log" 2>&1
     local rc=$?
     tail -1 "$OUT/$cfg/$name.log" | cut -c1-200
