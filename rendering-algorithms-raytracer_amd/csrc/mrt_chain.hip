@@ -324,7 +324,9 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
     const uint32_t nA = k < P.ch_levels ? P.ch_cnt[k] : 0u;
     const uint32_t m = (uint32_t)P.max_shadow;
     const uint32_t nprev = k == 1 ? chunk_units(P) * (uint32_t)P.num_paths : P.ch_cnt[k - 1];
-    const uint32_t nB = nprev * m;
+    // binned orders (mrt_bin.h): sh_perm lists level k - 1's valid shadow-ray slots, tr_perm
+    // level k's entries; a ray's answer does not depend on which lane traces it
+    const uint32_t nB = P.sh_perm ? *P.sh_perm_n : nprev * m;
     const uint32_t chA = (nA + 63u) >> 6, chunks = chA + ((nB + 63u) >> 6);
     const uint32_t wave_id = (uint32_t)blockIdx.x * (kWG / 64) + (uint32_t)(threadIdx.x >> 6);
     if ((uint32_t)blockIdx.x * (kWG / 64) >= chunks) return;   // the block has no chunks (before any barrier)
@@ -340,8 +342,9 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
     const uint32_t np = (uint32_t)P.num_paths;
     for (uint32_t c = wave_id; c < chunks; c += gridDim.x * (kWG / 64)) {
         if (c < chA) {   // closest hit of entry e
-            const uint32_t e = (c << 6) + (uint32_t)lane;
+            uint32_t e = (c << 6) + (uint32_t)lane;
             if (e >= nA) continue;
+            if (P.tr_perm) e = P.tr_perm[e];
             const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
             float time = 0.f;
             if (INST && P.has_mb) time = unit_time(P, unit_pixel(P, P.unit_base + __float_as_uint(o.w) / np));
@@ -350,8 +353,14 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
             const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
             P.ch_hit[base + e] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
         } else {         // shadow ray j of level k - 1's entry (or path) s, any hit
-            const uint32_t i = ((c - chA) << 6) + (uint32_t)lane, s = i / m;
-            if (i >= nB || i - s * m >= (uint32_t)nrays[s]) continue;
+            uint32_t i = ((c - chA) << 6) + (uint32_t)lane;
+            if (i >= nB) continue;
+            if (P.sh_perm) {
+                i = P.sh_perm[i];
+            } else {
+                const uint32_t s = i / m;
+                if (i - s * m >= (uint32_t)nrays[s]) continue;
+            }
             const float4 o = P.ray_o[sb + i], d = P.ray_d[sb + i];
             const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
             DHit h{o.w, 0.f, 0.f, -1};

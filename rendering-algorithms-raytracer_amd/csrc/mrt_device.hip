@@ -19,6 +19,7 @@
 #include <string>
 #include <vector>
 
+#include "mrt_bin.h"
 #include "mrt_kernels.h"
 #include "mrt_scene.h"
 #include "mrt_texture.h"
@@ -79,12 +80,17 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
         const size_t nd = (size_t)*P.sh_count * (size_t)P.max_shadow;
         if (nd < n_rays) n_rays = nd;
     }
+    // binned order (mrt_bin.h): position c traces slot perm[c]; the list holds valid slots only
+    const uint32_t* perm = P.sh_perm;
+    if (perm) n_rays = *P.sh_perm_n;
     // slot e = pixel slot * max_shadow + j (n_rays < 2^32, checked on the host: 32-bit division)
     const uint32_t m = (uint32_t)P.max_shadow, nr32 = (uint32_t)n_rays;
     auto valid = [&](size_t e64) {
+        if (perm) return e64 < n_rays;
         const uint32_t e = (uint32_t)e64, px = e / m;
         return e64 < n_rays && e < nr32 && e - px * m < (uint32_t)P.nrays[px];
     };
+    auto slot_at = [&](size_t c) -> size_t { return perm ? (size_t)perm[c] : c; };
     auto trace_one = [&](size_t e) {
         const float4 o = P.ray_o[e], d = P.ray_d[e];
         const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
@@ -122,7 +128,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
         if (sched == 0) {
             for (size_t e0 = (size_t)blockIdx.x * kWG + (tid & ~63); e0 < n_rays; e0 += (size_t)gridDim.x * kWG) {
                 const size_t e = e0 + lane;
-                uint32_t v = valid(e) ? trace_one(e) : 0u;
+                uint32_t v = valid(e) ? trace_one(slot_at(e)) : 0u;
                 if (COUNT) {
                     for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off));
                     wave_steps += v;
@@ -132,7 +138,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
             size_t first, end;
             while (dequeue(kShadowChunk, first, end)) {
                 const size_t e = first + lane;
-                uint32_t v = (e < end && valid(e)) ? trace_one(e) : 0u;
+                uint32_t v = (e < end && valid(e)) ? trace_one(slot_at(e)) : 0u;
                 if (COUNT) {
                     for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off));
                     wave_steps += v;
@@ -156,7 +162,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
                     const size_t c = first + (size_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                     if (c < end && valid(c)) {
-                        e = c;
+                        e = slot_at(c);
                         const float4 o = P.ray_o[e], d = P.ray_d[e];
                         as.q = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
                         tmax = o.w;
@@ -543,6 +549,13 @@ struct StreamCtx {
     uint32_t* tile_cost = nullptr;           // frame1_kernel: per-tile cycles of the last frame on this stream
     uint32_t* tile_order = nullptr;          //   and the queue order derived from them
     int tile_cap = 0, order_tiles = 0;       //   capacity; tiles of the frame the order is valid for (0: none)
+    uint16_t* bin_keys = nullptr;            // ray binning (mrt_bin.h): per-ray keys, two permutations
+    uint32_t* bin_perm = nullptr;            //   [2][bin_cap] (0: shadow rays, 1: chain closest-hit entries)
+    uint32_t* bin_hist = nullptr;            //   [2][kBinHist] bins + valid count
+    size_t bin_cap = 0;
+    float4* ray_e = nullptr;                 // dome-light replay (RenderParams::ray_e / lrec)
+    uint32_t* lrec = nullptr;
+    size_t ray_e_cap = 0, lrec_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
 };
 static constexpr int kMaxStreamCtx = 16;
@@ -581,8 +594,10 @@ struct DeviceState {
     size_t frame_px = 0;
     int grid = 0;                // upper bound of any launch (kMaxBlocksPerCU per CU)
     bool boxes_finite = false;
+    float bb_lo[3] = {0, 0, 0}, bb_hi[3] = {0, 0, 0};   // world root box (ray-binning origin cells)
     int cus = 0;
     bool point_only = false;
+    bool dome = false;           // a dome light (incoherent shadow rays)
     int recursive = 0;           // chain shading (Shader REC): 1 reflection / refraction, 2 + path tracing
     bool disperse = false;       // a dispersive Blinn material with secondary rays: the fused (tree) engine
     int wall_khz = 0;            // wall_clock64() rate
@@ -626,6 +641,16 @@ static int g_chain_mb = 16384;    // chain scratch per stream (MB); larger frame
 static int g_chain_adapt = 1;     // adaptive supersampling of REC scenes: passes over the chain engine (0: fused kernel)
 static int g_fused = 1;           // one point light, one path: frame1_kernel (primary + shading in one launch)
 static int g_frame1_waves = 6;    // frame1_kernel launch-bounds occupancy target: 1 (none), 5..8
+static int g_bin = -1;            // ray binning (mrt_bin.h) before tracing: bit 0 the wavefront shadow pass (kernel 2b),
+                                  // bit 1 the chain levels' closest-hit entries, bit 2 the chain levels' shadow rays;
+                                  // -1 auto (bin_mode): chain levels of path-traced scenes (P4 -18% frame; the
+                                  // coherent mirror / glass levels of R3 / G3 lose their pixel order: +22% / +44%)
+                                  // and the dome shadow rays of instanced scenes (C5 -2.6%; D1 +2%)
+static int g_dome_replay = 1;      // dome-light resolve (2c) sums 2a's recorded samples instead of sampling again
+static int g_bin_dbits = 2;       // binning key: direction cells per octahedral axis = 2^dbits
+static int g_bin_obits = 2;       //   origin cells per scene-box axis = 2^obits (2 dbits + 3 obits <= 12);
+                                  //   sweep of 12 pairs: (2, 2) best on P4 (-18%) and C5 (-2.6%), finer
+                                  //   direction cells lose (P4 (6, 0) -11%), profiles/r03_bin_sweep.txt
 static int g_tile_lpt = 0;        // frame1_kernel: tile queue ordered by the previous frame's tile costs (off: -2% single-frame latency
                                   // but +10% ms/frame with 4 frames in flight, the bench mode; profiles/r03_lpt_ab.txt)
 
@@ -633,7 +658,7 @@ static inline int fast_box(const DeviceState& d);
 
 static void free_ctx(StreamCtx* c) {
     void* ptrs[] = {c->gstack, c->ctr, c->wave_log, c->hitbuf, c->rays, c->occl, c->nrays, c->lvl, c->chain,
-                    c->tile_cost, c->tile_order, c->adapt};
+                    c->tile_cost, c->tile_order, c->adapt, c->bin_keys, c->bin_perm, c->bin_hist, c->ray_e, c->lrec};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -944,8 +969,25 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     d.boxes_finite = true;
     for (const QNode& q : DN)
         for (int k = 0; k < 24; k++) d.boxes_finite &= std::isfinite(q.box[k]);
+    if (!DN.empty()) {   // union of the root's used slot boxes
+        bool any = false;
+        for (int i = 0; i < 4; i++) {
+            if (DN[0].child[i] == kEmptySlot) continue;
+            for (int a = 0; a < 3; a++) {
+                const float lo = DN[0].box[a * 4 + i], hi = DN[0].box[12 + a * 4 + i];
+                if (!std::isfinite(lo) || !std::isfinite(hi)) continue;
+                d.bb_lo[a] = any ? std::min(d.bb_lo[a], lo) : lo;
+                d.bb_hi[a] = any ? std::max(d.bb_hi[a], hi) : hi;
+            }
+            any = true;
+        }
+    }
     d.point_only = true;
-    for (const DevLight& l : s.lights) d.point_only &= (l.type == MRT_POINT_LIGHT);
+    d.dome = false;
+    for (const DevLight& l : s.lights) {
+        d.point_only &= (l.type == MRT_POINT_LIGHT);
+        d.dome |= l.type == MRT_DOME_LIGHT;
+    }
     d.recursive = 0;
     for (const DevMaterial& m : s.materials)
         if (m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f || m.gloss < 1.f || m.translucency > 0.01f)) d.recursive = 1;
@@ -1055,6 +1097,65 @@ static int ensure_rays(StreamCtx& c, size_t slots, size_t per_slot) {
     c.ray_cap = n;
     c.nrays_cap = slots;
     return MRT_OK;
+}
+
+// Dome-light replay scratch of a stream: n ray slots, calls call records.
+static int ensure_replay(StreamCtx& c, size_t n, size_t calls) {
+    if (n <= c.ray_e_cap && calls <= c.lrec_cap) return MRT_OK;
+    HIP_OK(hipStreamSynchronize(c.stream));   // the previous launch may still read them
+    if (c.ray_e) (void)hipFree(c.ray_e);
+    if (c.lrec) (void)hipFree(c.lrec);
+    c.ray_e = nullptr; c.lrec = nullptr; c.ray_e_cap = c.lrec_cap = 0;
+    HIP_OK(hipMalloc((void**)&c.ray_e, n * sizeof(float4)));
+    HIP_OK(hipMalloc((void**)&c.lrec, calls * sizeof(uint32_t)));
+    c.ray_e_cap = n;
+    c.lrec_cap = calls;
+    return MRT_OK;
+}
+
+// The binning switches in effect for a scene (g_bin, or the auto choice).
+static int bin_mode(const DeviceState& d) {
+    if (g_bin >= 0) return g_bin;
+    return (d.recursive == 2 ? 6 : 0) | (d.n_insts > 0 && d.dome ? 1 : 0);
+}
+
+// Ray-binning scratch of a stream (mrt_bin.h) for batches of up to n rays.
+static constexpr size_t kBinHist = (size_t(1) << kBinBits) + 64;   // bins + the valid count, padded
+static int ensure_bin(StreamCtx& c, size_t n) {
+    if (n <= c.bin_cap) return MRT_OK;
+    HIP_OK(hipStreamSynchronize(c.stream));   // the previous launch may still read them
+    void* ptrs[] = {c.bin_keys, c.bin_perm, c.bin_hist};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    c.bin_keys = nullptr; c.bin_perm = nullptr; c.bin_hist = nullptr; c.bin_cap = 0;
+    HIP_OK(hipMalloc((void**)&c.bin_keys, n * sizeof(uint16_t)));
+    HIP_OK(hipMalloc((void**)&c.bin_perm, 2 * n * sizeof(uint32_t)));
+    HIP_OK(hipMalloc((void**)&c.bin_hist, 2 * kBinHist * sizeof(uint32_t)));
+    c.bin_cap = n;
+    return MRT_OK;
+}
+
+// Binning of a ray batch o[i] / d[i], i < n (host bound), into permutation
+// `which` of the stream's scratch; keys from the scene box and the tuning
+// knobs.  The caller sets the validity / device-count fields, then bins.
+static BinArgs bin_args(const DeviceState& d, const StreamCtx& c, int which, const float4* o, const float4* dd, size_t n) {
+    BinArgs A{};
+    A.o = o; A.d = dd; A.n = (uint32_t)n;
+    A.mul1 = 1; A.cap1 = 0xFFFFFFFFu; A.mul2 = 1; A.m = 1;
+    A.dbits = g_bin_dbits; A.obits = g_bin_obits;
+    for (int a = 0; a < 3; a++) {
+        const float ext = d.bb_hi[a] - d.bb_lo[a];
+        A.lo[a] = d.bb_lo[a];
+        A.inv[a] = ext > 0.f ? (float)(1 << A.obits) / ext : 0.f;
+    }
+    A.keys = c.bin_keys;
+    A.hist = c.bin_hist + (size_t)which * kBinHist;
+    A.perm = c.bin_perm + (size_t)which * c.bin_cap;
+    return A;
+}
+static const uint32_t* bin_total(const BinArgs& A) { return A.hist + (size_t(1) << (2 * A.dbits + 3 * A.obits)); }
+static int bin_grid(const DeviceState& d, size_t n) {
+    return (int)std::max<size_t>(1, std::min<size_t>((size_t)d.cus * 4, (n + 255) / 256));
 }
 
 static int ensure_slots(StreamCtx& c, size_t slots) {
@@ -1215,7 +1316,8 @@ static bool use_chain(const Scene& s) {
 }
 // One chunk of the engine over units [Q.unit_base, Q.unit_base + Q.n_units) of
 // Q's pass (the chunk layout -- ch_lofs, arrays -- is set by the caller).
-static int chain_chunk(Scene& s, RenderParams& Q, bool count, hipStream_t stream, size_t ctl, unsigned int* queues) {
+static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipStream_t stream, size_t ctl,
+                       unsigned int* queues) {
     DeviceState& d = *s.dev;
     const int L = Q.ch_levels;
     const bool inst = d.special;
@@ -1232,6 +1334,54 @@ static int chain_chunk(Scene& s, RenderParams& Q, bool count, hipStream_t stream
     auto full = [&](KernelFn f) { return std::min(d.grid, d.cus * blocks_per_cu(f, 0)); };
     const int ug = (int)std::min<uint64_t>((uint64_t)full(r0), ((uint64_t)Q.n_units + kWG - 1) / kWG);
     int rc;
+    // ray binning before each trace launch (g_bin bits 1 / 2): level k's closest-hit entries
+    // and level k - 1's shadow rays, each in its own permutation
+    const uint32_t m = (uint32_t)Q.max_shadow;
+    auto lcap_h = [&](int k) { return (size_t)Q.ch_lofs[k + 1] - Q.ch_lofs[k]; };
+    const int bm = bin_mode(d);
+    if (bm & 6) {
+        size_t need = 1;
+        for (int k = 0; k < L; k++) need = std::max(need, std::max(lcap_h(k), lcap_h(k) * m));
+        if ((rc = ensure_bin(c, need))) return rc;
+    }
+    auto trace = [&](int k) -> int {   // Q.ch_level == k
+        if ((bm & 2) && k < L) {
+            const size_t lo = Q.ch_lofs[k], cap = lcap_h(k);
+            BinArgs A = bin_args(d, c, 1, Q.ch_ray + 2 * lo, Q.ch_ray + 2 * lo + cap, cap);
+            A.n_dev = Q.ch_cnt + k;
+            int r2;
+            if ((r2 = bin_rays(A, bin_grid(d, cap), stream))) return r2;
+            Q.tr_perm = A.perm;
+        }
+        if (bm & 4) {
+            const size_t lo = Q.ch_lofs[k - 1], nb = lcap_h(k - 1) * m;
+            BinArgs B = bin_args(d, c, 0, Q.ray_o + lo * m, Q.ray_d + lo * m, nb);
+            B.nrays = Q.nrays + lo;
+            B.m = m;
+            if (k - 1 > 0) {
+                B.n_dev = Q.ch_cnt + (k - 1);
+                B.mul2 = m;
+            } else if (Q.unit_cnt) {   // adaptive pass: chunk_units on the device
+                B.n_dev = Q.unit_cnt;
+                B.mul1 = Q.adapt_n > 1 ? (uint32_t)(Q.adapt_n * Q.adapt_n) : 1u;
+                B.sub = Q.unit_base;
+                B.cap1 = Q.n_units;
+                B.mul2 = (uint32_t)Q.num_paths * m;
+            } else {
+                const uint32_t units = Q.units_total > Q.unit_base ? std::min(Q.n_units, Q.units_total - Q.unit_base) : 0u;
+                B.n = (uint32_t)std::min<uint64_t>(nb, (uint64_t)units * (uint64_t)Q.num_paths * m);
+            }
+            int r2;
+            if ((r2 = bin_rays(B, bin_grid(d, nb), stream))) return r2;
+            Q.sh_perm = B.perm;
+            Q.sh_perm_n = bin_total(B);
+        }
+        const int r3 = go(kt, full(kt));
+        Q.tr_perm = nullptr;
+        Q.sh_perm = nullptr;
+        Q.sh_perm_n = nullptr;
+        return r3;
+    };
     HIP_OK(hipMemsetAsync(Q.ch_cnt, 0, ctl, stream));
     Q.queue = queues;
     if (Q.uhits) {   // adaptive pass: the chunk's eye rays and their closest hits
@@ -1244,11 +1394,11 @@ static int chain_chunk(Scene& s, RenderParams& Q, bool count, hipStream_t stream
         Q.ch_level = k;
         if ((rc = go(kc, full(kc)))) return rc;        // children of level k -> entries of level k + 1
         Q.ch_level = k + 1;
-        if ((rc = go(kt, full(kt)))) return rc;        // their closest hits + level k's shadow rays
+        if ((rc = trace(k + 1))) return rc;            // their closest hits + level k's shadow rays
         if ((rc = go(gk, full(gk)))) return rc;        // level k + 1: shadow rays + children
     }
     Q.ch_level = L;
-    if ((rc = go(kt, full(kt)))) return rc;            // the last level's shadow rays
+    if ((rc = trace(L))) return rc;                    // the last level's shadow rays
     Q.queue = queues + 256;
     if ((rc = go(r0, ug))) return rc;                  // resolve level 0, then levels 1 .. L - 1
     if ((rc = go(rk, full(rk)))) return rc;
@@ -1327,7 +1477,7 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     Q.n_units = (uint32_t)per;
     for (uint64_t b = 0; b < units_max; b += per) {
         Q.unit_base = (uint32_t)b;
-        if ((rc = chain_chunk(s, Q, count, stream, ctl, queues))) return rc;
+        if ((rc = chain_chunk(s, c, Q, count, stream, ctl, queues))) return rc;
     }
     return MRT_OK;
 }
@@ -1494,9 +1644,16 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         P.occl = c.occl;
         P.nrays = c.nrays;
         P.max_shadow = max_sh;
+        int ndome = 0;
+        for (const DevLight& l : s.lights) ndome += l.type == MRT_DOME_LIGHT ? 1 : 0;
+        const bool dome = ndome > 0;
+        if (dome && g_dome_replay) {   // 2a records the dome samples, 2c replays them
+            P.lcalls = P.num_paths * ndome;
+            if ((rc = ensure_replay(c, slots * (size_t)max_sh, slots * (size_t)P.lcalls))) return rc;
+            P.ray_e = c.ray_e;
+            P.lrec = c.lrec;
+        }
         if ((rc = launch(shade_mode_fn<kGen>(count, d.point_only, inst)))) return rc;
-        bool dome = false;
-        for (const DevLight& l : s.lights) dome |= l.type == MRT_DOME_LIGHT;
         // lane refill for dome-light (incoherent) rays: D1 -7%, C5 -13% shade pass; coherent
         // area-light rays keep the bands (C4: refill +9%)
         int sched = g_shadow_sched >= 0 ? g_shadow_sched : (dome ? 2 : 1), refill = g_refill_min;
@@ -1510,13 +1667,27 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         size_t n_rays = slots * (size_t)max_sh;
         if (n_rays >= (size_t(1) << 32)) { set_error("too many wavefront shadow-ray slots (2^32)"); return MRT_ERR_INVALID; }
         P.near_first = g_near_first >= 0 ? g_near_first : (sched == 2 || inst ? 0 : 1);
+        if (bin_mode(d) & 1) {   // the rays in binned order (valid slots only)
+            if ((rc = ensure_bin(c, n_rays))) return rc;
+            BinArgs A = bin_args(d, c, 0, P.ray_o, P.ray_d, n_rays);
+            A.nrays = P.nrays;
+            A.m = (uint32_t)max_sh;
+            if ((rc = bin_rays(A, bin_grid(d, n_rays), stream))) return rc;
+            P.sh_perm = A.perm;
+            P.sh_perm_n = bin_total(A);
+        }
         void* args[] = {&P, &n_rays, &sched, &refill};
         P.wave_log = nullptr;
         P.queue = qbase + 24 * 32;
         HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(sf), dim3(g), dim3(kWG), args, 0, stream));
+        P.sh_perm = nullptr;
+        P.sh_perm_n = nullptr;
         P.queue = qbase + 16 * 32;
         // dome-light resolve passes run faster at 4 waves (D1 -4%, C5 -1.2 ms), the rect-light one not (C4 +2%)
         if ((rc = launch(shade_mode_fn<kResolve>(count, d.point_only, inst, dome)))) return rc;
+        P.ray_e = nullptr;
+        P.lrec = nullptr;
+        P.lcalls = 0;
     }
     c.last_was_render = true;
     HIP_OK(hipGetLastError());
@@ -2544,6 +2715,17 @@ int mrt_set_tuning(const char* key, int value) {
         g_fused = value ? 1 : 0;
     } else if (k == "tile_lpt") {
         g_tile_lpt = value ? 1 : 0;
+    } else if (k == "dome_replay") {
+        g_dome_replay = value ? 1 : 0;
+    } else if (k == "bin") {
+        if (value < -1 || value > 7) { set_error("bin must be -1 (auto) or 0..7"); return MRT_ERR_INVALID; }
+        g_bin = value;
+    } else if (k == "bin_dbits") {   // the pair is checked when a batch is binned (2 dbits + 3 obits = 1..12)
+        if (value < 0 || value > 6) { set_error("bin_dbits must be 0..6"); return MRT_ERR_INVALID; }
+        g_bin_dbits = value;
+    } else if (k == "bin_obits") {
+        if (value < 0 || value > 4) { set_error("bin_obits must be 0..4"); return MRT_ERR_INVALID; }
+        g_bin_obits = value;
     } else if (k == "frame1_waves") {
         if (value != 1 && (value < 5 || value > 8)) { set_error("frame1_waves must be 1 or 5..8"); return MRT_ERR_INVALID; }
         g_frame1_waves = value;

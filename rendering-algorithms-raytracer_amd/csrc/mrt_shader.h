@@ -143,6 +143,19 @@ struct RenderParams {
     uint32_t* next_units;        // adaptive combine: the pixels that refine further
     uint32_t* next_cnt;
     const uint32_t* sh_count;    // shadow_kernel: pixel / entry count on the device (nullable)
+    // ray binning (mrt_bin.h): the trace kernels take their rays in this order
+    // (nullable: slot order).  sh_perm lists the valid shadow-ray slots (sh_perm_n
+    // of them, on the device); tr_perm the chain level's closest-hit entries.
+    const uint32_t* sh_perm;
+    const uint32_t* sh_perm_n;
+    const uint32_t* tr_perm;
+    // dome-light replay (kernels 2a / 2c of the direct shading): 2a records, per
+    // shadow-ray slot, the sample's E and dot(rVec, dir) (ray_e), and per dome
+    // call (lcalls per pixel slot) its sample count | RNG draws << 8 (lrec); 2c
+    // then sums the recorded samples with the answers instead of sampling again
+    float4* ray_e;
+    uint32_t* lrec;
+    int32_t lcalls;
     // motion blur (MBObject, src/MBObject.cpp): per world prim bit 0 = MBObject
     // lane; time-1 vertices parallel to verts (nullptr: no motion blur)
     const uint8_t* pflags;
@@ -264,6 +277,8 @@ struct Shader {
     float* lvl = nullptr;    // REC: this thread's level records (stride P.gstride)
     float time = 0.f;        // the camera ray's time (getTimeSample), inherited by the rays below it
     float shadow_time = 0.f; // sampleLight's shadow-ray time: time, or .001 for translucency (src/Blinn.cpp:229)
+    size_t lrec0 = 0;        // dome-light replay: this pixel's first call record (P.lrec)
+    uint32_t lcall = 0;      //   dome calls so far
 
     __device__ float next_rand() { return rng(pixel, skey, dim++, seed); }
 
@@ -357,6 +372,26 @@ struct Shader {
         const int numSamples = secondary ? 1 : l.samples;
         v3 acc = mk(0, 0, 0);
         float tmpSpec = 0.f, recip = 1.0f;
+        if constexpr (MODE == kResolve) {
+            if (P.lrec) {   // replay 2a's samples: which samples were taken, their E and the RNG
+                            // draws do not depend on the answers; the sums are the loop's below
+                const uint32_t rc = P.lrec[lrec0 + lcall++];
+                dim += rc >> 8;
+                const int ns = (int)(rc & 0xFFu);
+                for (int j = 0; j < ns; j++) {
+                    const size_t s = slot0 + nslot++;
+                    const float4 e = P.ray_e[s];
+                    const float att = P.occl[s] != 0 ? 0.0f : 1.0f;
+                    shadow_rays++;
+                    recip = 1.0f / (float)(j + 1);
+                    acc = add(acc, scale(mk(e.x, e.y, e.z), att));
+                    tmpSpec += e.w * att;
+                }
+                outSpec = tmpSpec * recip;
+                return scale(acc, recip);
+            }
+        }
+        const uint32_t dim0 = dim;
         int done = 0, rejects = 0;
         bool cut = false;
         do {
@@ -382,6 +417,7 @@ struct Shader {
             const float inv = 1.0f / pdf;  // E = m_Gain * imageSample / pdf (Vector3::operator/)
             const v3 E = scale(scale(img, l.power), inv);
             float att = 1.0f;
+            if (MODE == kGen && P.lrec) P.ray_e[slot0 + nslot] = make_float4(E.x, E.y, E.z, dot(rVec, dir));
             if (occluded<COUNT>(from, dir, 1e12f)) att = 0.0f;
             done++;
             recip = 1.0f / (float)done;
@@ -390,6 +426,7 @@ struct Shader {
             acc = add(acc, scale(E, att));
             tmpSpec += dot(rVec, dir) * att;
         } while (done < numSamples && !cut);
+        if (MODE == kGen && P.lrec) P.lrec[lrec0 + lcall++] = (uint32_t)done | ((dim - dim0) << 8);
         outSpec = tmpSpec * recip;
         return scale(acc, recip);
     }
@@ -1221,6 +1258,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade_kernel(RenderParams P) {
             Shader<POINT_ONLY, FAST, INST, MODE, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(y * cam.W + x), 0u, seed,
                                                    slot * (size_t)P.max_shadow, 0u};
             S.time = S.shadow_time = er.time;
+            S.lrec0 = slot * (size_t)P.lcalls;
             if constexpr (REC) { S.iorS = s_ior + tid; S.lvl = P.lvl + (blockIdx.x * kWG + tid); }
             col = S.template shade<COUNT>(r, h);
             shadow_total += S.shadow_rays;

@@ -24,9 +24,10 @@ def main():
     cfgkey = os.environ.get("AB_CONFIG", "C3")
     inflight = int(sys.argv[sys.argv.index("--inflight") + 1]) if "--inflight" in sys.argv else 4
     variants = [{}]
-    for a in args:
+    for a in args:   # key=v1,v2 (product with the other keys); k1+k2=a1+a2,b1+b2 (paired values)
         k, vs = a.split("=")
-        variants = [dict(v, **{k: int(x)}) for v in variants for x in vs.split(",")]
+        ks = k.split("+")
+        variants = [dict(v, **{kk: int(xx) for kk, xx in zip(ks, x.split("+"))}) for v in variants for x in vs.split(",")]
     scene, cam, cfg = scenes.build_config(cfgkey)
     W, H = cfg["W"], cfg["H"]
     L = miro.lib()

@@ -17,8 +17,11 @@ Latency evidence (SQ counters count quad-cycles; WAIT_ANY + WAIT_INST_ANY +
 ACTIVE_INST_ANY ~= WAVE_CYCLES, MI355X_MICROARCH.md PMC section):
   wave_active / wave_wait_mem / wave_issue_stall = the three shares of WAVE_CYCLES
   valu_share = ACTIVE_INST_VALU / WAVE_CYCLES (a wave's cycles issuing VALU)
-  simd_valu_busy = 4 * ACTIVE_INST_VALU / (SIMDs * clock * duration), clock from
-      GRBM_GUI_ACTIVE / 8 XCDs / duration
+  simd_valu_busy = 2 * INSTS_VALU / (SIMDs * clock * duration): the share of the SIMDs'
+      VALU throughput used -- a wave64 f32 VALU instruction occupies a SIMD for 2 cycles
+      (SIMD-32; MI355X_MICROARCH.md cycle constants); clock from GRBM_GUI_ACTIVE / 8 XCDs / duration
+  wave_issue_share = 4 * ACTIVE_INST_VALU / (SIMDs * clock * duration): the same instructions at
+      one wave's own issue cost (4 cycles each); above 1 only because waves of a SIMD overlap
   l2_req_per_vmem_load = TCP_TCC_READ_REQ_sum / SQ_INSTS_VMEM_RD
   l1_hit = 1 - TCP_TCC_READ_REQ_sum / TCP_TOTAL_CACHE_ACCESSES_sum
 Only the timed (COUNT = false) instantiations enter the pass totals."""
@@ -161,7 +164,9 @@ def summarise(cfg, d):
             if m.get("GRBM_GUI_ACTIVE") and dur and m.get("SQ_ACTIVE_INST_VALU") is not None:
                 clk = m["GRBM_GUI_ACTIVE"] / 8 / (dur * 1e-6)
                 lat["clock_ghz"] = round(clk / 1e9, 3)
-                lat["simd_valu_busy"] = round(4 * m["SQ_ACTIVE_INST_VALU"] / (SIMDS * clk * dur * 1e-6), 4)
+                if m.get("SQ_INSTS_VALU") is not None:
+                    lat["simd_valu_busy"] = round(2 * m["SQ_INSTS_VALU"] / (SIMDS * clk * dur * 1e-6), 4)
+                lat["wave_issue_share"] = round(4 * m["SQ_ACTIVE_INST_VALU"] / (SIMDS * clk * dur * 1e-6), 4)
             if m.get("TCP_TCC_READ_REQ_sum") is not None and m.get("SQ_INSTS_VMEM_RD"):
                 lat["l2_req_per_vmem_load"] = round(m["TCP_TCC_READ_REQ_sum"] / m["SQ_INSTS_VMEM_RD"], 4)
             if m.get("TCP_TCC_READ_REQ_sum") is not None and m.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
