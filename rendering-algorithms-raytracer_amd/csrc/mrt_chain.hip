@@ -316,7 +316,12 @@ __global__ void __launch_bounds__(kWG) chain_compact_kernel(RenderParams P) {
 // answers of level k - 1's shadow rays (nB slots), which no longer wait for
 // each other -- a level's resolve needs its shadow answers only at the end of
 // the chunk.  Wave-uniform 64-slot chunks, the closest-hit chunks first.
-template <bool COUNT, bool FAST, bool INST, int MINW = 1>
+// REFILL (plain scenes): lane refill instead of 64-slot chunks -- a lane whose
+// ray is done takes the next position as soon as P.refill_min lanes of its wave
+// are idle, and the wave advances every busy lane by one node visit per step
+// (trav_step: closest-hit and any-hit rays side by side), so a wave no longer
+// waits for its longest ray.  Positions are dealt from the same 8 XCD bands.
+template <bool COUNT, bool FAST, bool INST, int MINW = 1, bool REFILL = false>
 __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -340,32 +345,154 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
     const size_t base = lofs(P, k), cap = k < P.ch_levels ? lcap(P, k) : 0, sb = shadow_base(P, k - 1);
     const uint8_t* nrays = P.nrays + lofs(P, k - 1);
     const uint32_t np = (uint32_t)P.num_paths;
-    for (uint32_t c = wave_id; c < chunks; c += gridDim.x * (kWG / 64)) {
+    unsigned long long wave_steps = 0;
+    auto chunk = [&](uint32_t c) {   // one 64-slot chunk, one ray per lane
+        const uint32_t n0 = st.nodes;
         if (c < chA) {   // closest hit of entry e
             uint32_t e = (c << 6) + (uint32_t)lane;
-            if (e >= nA) continue;
-            if (P.tr_perm) e = P.tr_perm[e];
-            const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
-            float time = 0.f;
-            if (INST && P.has_mb) time = unit_time(P, unit_pixel(P, P.unit_base + __float_as_uint(o.w) / np));
-            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), time);
-            DHit h{1e12f, 0.f, 0.f, -1};
-            const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
-            P.ch_hit[base + e] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
+            if (e < nA) {
+                if (P.tr_perm) e = P.tr_perm[e];
+                const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
+                float time = 0.f;
+                if (INST && P.has_mb) time = unit_time(P, unit_pixel(P, P.unit_base + __float_as_uint(o.w) / np));
+                const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), time);
+                DHit h{1e12f, 0.f, 0.f, -1};
+                const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
+                P.ch_hit[base + e] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
+            }
         } else {         // shadow ray j of level k - 1's entry (or path) s, any hit
             uint32_t i = ((c - chA) << 6) + (uint32_t)lane;
-            if (i >= nB) continue;
-            if (P.sh_perm) {
+            bool ok = i < nB;
+            if (ok && P.sh_perm) {
                 i = P.sh_perm[i];
-            } else {
+            } else if (ok) {
                 const uint32_t s = i / m;
-                if (i - s * m >= (uint32_t)nrays[s]) continue;
+                ok = i - s * m < (uint32_t)nrays[s];
             }
-            const float4 o = P.ray_o[sb + i], d = P.ray_d[sb + i];
-            const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
-            DHit h{o.w, 0.f, 0.f, -1};
-            P.occl[sb + i] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
+            if (ok) {
+                const float4 o = P.ray_o[sb + i], d = P.ray_d[sb + i];
+                const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
+                DHit h{o.w, 0.f, 0.f, -1};
+                P.occl[sb + i] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
+            }
         }
+        if (COUNT) {   // the chunk's wave steps: its longest ray's node visits
+            uint32_t v = st.nodes - n0;
+            for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off));
+            wave_steps += v;
+        }
+    };
+    if constexpr (REFILL && !INST) {
+        // positions 0 .. nA - 1: closest-hit entries; nA .. nA + nB - 1: shadow rays
+        const uint32_t npos = nA + nB;
+        unsigned int* q = P.queue + (size_t)(k + 1) * 256;
+        int band = blockIdx.x & 7, probes = 0;
+        bool exhausted = false, active = false, any = false;
+        uint32_t dst = 0;   // closest: entry; any: shadow slot
+        DRay r{};
+        DHit h{};
+        int32_t cur = 0;
+        int sp = 0;
+        for (;;) {
+            const unsigned long long idle = __ballot(!active);
+            const int nidle = __popcll(idle);
+            if (!exhausted && (nidle >= P.refill_min || nidle == 64)) {
+                uint32_t got = 0xFFFFFFFFu, hi = 0;
+                if (lane == 0) {
+                    while (probes < 8) {
+                        const uint32_t lo = (uint32_t)((uint64_t)npos * (uint32_t)band / 8u);
+                        const uint32_t bh = (uint32_t)((uint64_t)npos * (uint32_t)(band + 1) / 8u);
+                        const uint32_t v = lo < bh ? atomicAdd(q + band * 32, (uint32_t)nidle) : 0u;
+                        if (lo < bh && lo + v < bh) { got = lo + v; hi = bh; break; }
+                        band = (band + 1) & 7;
+                        probes++;
+                    }
+                }
+                got = __shfl(got, 0);
+                hi = __shfl(hi, 0);
+                if (got == 0xFFFFFFFFu) {
+                    exhausted = true;
+                } else if (!active) {
+                    const uint32_t p = got + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    if (p < hi) {
+                        if (p < nA) {
+                            const uint32_t e = P.tr_perm ? P.tr_perm[p] : p;
+                            const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
+                            r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.f);
+                            h = DHit{1e12f, 0.f, 0.f, -1};
+                            dst = e;
+                            any = false;
+                            active = true;
+                        } else {
+                            uint32_t i = p - nA;
+                            bool ok = true;
+                            if (P.sh_perm) {
+                                i = P.sh_perm[i];
+                            } else {
+                                const uint32_t s = i / m;
+                                ok = i - s * m < (uint32_t)nrays[s];
+                            }
+                            if (ok) {
+                                const float4 o = P.ray_o[sb + i], d = P.ray_d[sb + i];
+                                r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
+                                h = DHit{o.w, 0.f, 0.f, -1};
+                                dst = i;
+                                any = true;
+                                active = true;
+                            }
+                        }
+                        cur = 0;
+                        sp = 0;
+                    }
+                }
+            }
+            if (__ballot(active) == 0) {
+                if (exhausted) break;
+                continue;
+            }
+            if (COUNT) wave_steps++;
+            if (active) {
+                bool hit = false;
+                const bool done = (FAST && r.finite) ? trav_step<COUNT, true>(T, r, 0.001f, any, h, cur, sp, hit, st)
+                                                     : trav_step<COUNT, false>(T, r, 0.001f, any, h, cur, sp, hit, st);
+                if (done) {
+                    if (any) {
+                        P.occl[sb + dst] = hit ? 1 : 0;
+                    } else {   // a closest hit found in any earlier step left its packed slot in h.prim
+                        const int32_t prim = h.prim >= 0 ? T.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3] : -1;
+                        P.ch_hit[base + dst] = make_float4(h.t, h.a, h.b, __int_as_float(prim));
+                    }
+                    active = false;
+                }
+            }
+        }
+    } else if (P.ch_bands) {
+        // XCD bands: the chunk range is cut into 8 contiguous bands and a workgroup
+        // on XCD b mod 8 takes chunks of band b mod 8 from that band's counter,
+        // then steals from the others -- with binned rays (mrt_bin.h) a band holds
+        // neighbouring direction / origin cells, so one XCD's 4 MB L2 holds the
+        // nodes of its share of the rays instead of the whole hierarchy's
+        unsigned int* q = P.queue + (size_t)(k + 1) * 256;   // this level's 8 counters, 32 words apart
+        int band = blockIdx.x & 7, probes = 0;
+        for (;;) {
+            uint32_t c = 0xFFFFFFFFu;
+            if (lane == 0) {
+                while (probes < 8) {
+                    const uint32_t lo = (uint32_t)((uint64_t)chunks * (uint32_t)band / 8u);
+                    const uint32_t hi = (uint32_t)((uint64_t)chunks * (uint32_t)(band + 1) / 8u);
+                    const uint32_t v = lo < hi ? atomicAdd(q + band * 32, 1u) : 0u;
+                    if (lo + v < hi) { c = lo + v; break; }
+                    band = (band + 1) & 7;
+                    probes++;
+                }
+            }
+            c = __shfl(c, 0);
+            if (c == 0xFFFFFFFFu) break;
+            chunk(c);
+        }
+    } else {
+        for (uint32_t c = wave_id; c < chunks; c += gridDim.x * (kWG / 64)) chunk(c);
     }
     if (COUNT) {
         unsigned long long nv = st.nodes, lv = st.leaves;
@@ -376,6 +503,8 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
         if (lane == 0) {
             atomicAdd(&P.ctr[CTR_NODES], nv);
             atomicAdd(&P.ctr[CTR_LEAVES], lv);
+            atomicAdd(&P.ctr[CTR_NODES_S], nv);          // chain engine: the trace launches' visits
+            atomicAdd(&P.ctr[CTR_WAVE_STEPS_S], wave_steps);   //   and wave steps (lane utilisation)
         }
     }
     if (st.overflow) atomicOr(&P.ctr[CTR_OVERFLOW], 1ull);
@@ -679,7 +808,11 @@ KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec) {
     if (rec == 2) return resolve ? chain_shade_fn<kResolve, 2>(po, inst) : chain_shade_fn<kGen, 2>(po, inst);
     return resolve ? chain_shade_fn<kResolve, 1>(po, inst) : chain_shade_fn<kGen, 1>(po, inst);
 }
-KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves) {
+KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves, bool refill) {
+    if (refill && !inst) {   // lane refill (plain scenes)
+        if (c) return f ? chain_trace_kernel<true, true, false, 1, true> : chain_trace_kernel<true, false, false, 1, true>;
+        return f ? chain_trace_kernel<false, true, false, 8, true> : chain_trace_kernel<false, false, false, 8, true>;
+    }
     if (waves == 8 && !c && !inst)   // occupancy target of the plain-scene trace (timed variants)
         return f ? chain_trace_kernel<false, true, false, 8> : chain_trace_kernel<false, false, false, 8>;
     if (inst) return c ? (f ? chain_trace_kernel<true, true, true> : chain_trace_kernel<true, false, true>)

@@ -151,6 +151,8 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
         size_t e = 0;
         float tmax = 0.f;
         AnyState as{};
+        AnyLeaf lf{};
+        const bool leaf_steps = P.leaf_steps != 0;
         for (;;) {
             const unsigned long long idle = __ballot(!active);
             const int nidle = __popcll(idle);
@@ -169,6 +171,8 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
                         as.cur = 0;
                         as.sp = 0;
                         as.aoff = -1;
+                        lf.v = 0;
+                        lf.pend = 0;
                         active = true;
                     }
                 }
@@ -181,7 +185,9 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
             if (active) {
                 bool hit = false;
                 bool done;
-                if constexpr (INST) done = anyhit_step_inst<COUNT, FAST, CHECK>(T, 0.001f, tmax, as, P.ray_o, P.ray_d, e, hit, st);
+                if (leaf_steps)   // one box or one triangle test per lane per step
+                    done = anyhit_step_inst2<COUNT, FAST, CHECK>(T, 0.001f, tmax, as, lf, P.ray_o, P.ray_d, e, hit, st);
+                else if constexpr (INST) done = anyhit_step_inst<COUNT, FAST, CHECK>(T, 0.001f, tmax, as, P.ray_o, P.ray_d, e, hit, st);
                 else done = (FAST && as.q.finite) ? anyhit_step<COUNT, true>(T, as.q, 0.001f, tmax, as.cur, as.sp, hit, st)
                                                   : anyhit_step<COUNT, false>(T, as.q, 0.001f, tmax, as.cur, as.sp, hit, st);
                 if (done) {
@@ -646,6 +652,10 @@ static int g_bin = -1;            // ray binning (mrt_bin.h) before tracing: bit
                                   // -1 auto (bin_mode): chain levels of path-traced scenes (P4 -18% frame; the
                                   // coherent mirror / glass levels of R3 / G3 lose their pixel order: +22% / +44%)
                                   // and the dome shadow rays of instanced scenes (C5 -2.6%; D1 +2%)
+static int g_leaf_steps = 0;      // shadow_kernel lane refill: leaf lanes in steps of their own (anyhit_step_inst2)
+static int g_chain_refill = 0;    // chain_trace_kernel (plain scenes): lane refill at this many idle lanes (0: 64-slot chunks)
+static int g_chain_bands = -1;    // chain_trace_kernel: XCD-banded chunk queue (binned rays: one XCD's L2 holds its share);
+                                  // -1 auto: on when the level is binned (P4 -3.4%; unbinned R3 +5.7%, G3 +3%)
 static int g_dome_replay = 1;      // dome-light resolve (2c) sums 2a's recorded samples instead of sampling again
 static int g_bin_dbits = 2;       // binning key: direction cells per octahedral axis = 2^dbits
 static int g_bin_obits = 2;       //   origin cells per scene-box axis = 2^obits (2 dbits + 3 obits <= 12);
@@ -1324,7 +1334,8 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
     const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive), r0 = pick_chain0(true, d.point_only, inst, d.recursive);
     const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive),
                    rk = pick_chain_shade(true, d.point_only, inst, d.recursive);
-    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, Q.fast_box != 0, inst, g_chain_trace_waves),
+    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, Q.fast_box != 0, inst, g_chain_trace_waves,
+                                                       g_chain_refill > 0),
                    kf = pick_chain_finish(), kd = pick_chain_fold();
     auto go = [&](KernelFn f, int g) -> int {
         void* args[] = {&Q};
@@ -1467,6 +1478,8 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
         if (k < L) off += paths * level_mult(s, k);
     }
     Q.lvl_words = W;
+    Q.ch_bands = g_chain_bands > 0 || (g_chain_bands < 0 && (bin_mode(d) & 6)) || g_chain_refill > 0;
+    Q.refill_min = g_chain_refill;
     Q.order = 0;          // chunks index work items directly
     Q.wave_log = nullptr;
     Q.ray_o = c.rays;
@@ -1676,6 +1689,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
             P.sh_perm = A.perm;
             P.sh_perm_n = bin_total(A);
         }
+        P.leaf_steps = g_leaf_steps;
         void* args[] = {&P, &n_rays, &sched, &refill};
         P.wave_log = nullptr;
         P.queue = qbase + 24 * 32;
@@ -2715,6 +2729,14 @@ int mrt_set_tuning(const char* key, int value) {
         g_fused = value ? 1 : 0;
     } else if (k == "tile_lpt") {
         g_tile_lpt = value ? 1 : 0;
+    } else if (k == "leaf_steps") {
+        g_leaf_steps = value ? 1 : 0;
+    } else if (k == "chain_refill") {
+        if (value < 0 || value > 64) { set_error("chain_refill must be 0..64"); return MRT_ERR_INVALID; }
+        g_chain_refill = value;
+    } else if (k == "chain_bands") {
+        if (value < -1 || value > 1) { set_error("chain_bands must be -1..1"); return MRT_ERR_INVALID; }
+        g_chain_bands = value;
     } else if (k == "dome_replay") {
         g_dome_replay = value ? 1 : 0;
     } else if (k == "bin") {
