@@ -193,8 +193,8 @@ __device__ __forceinline__ void no_children(const RenderParams& P, uint32_t e) {
 // depend on the shadow answers); kResolve runs the same shading with the
 // answers and writes the path's value or marks it pending.  No traversal runs
 // in either, so the shading state never has to live across one.
-template <bool POINT_ONLY, bool INST, int REC, int MODE>
-__global__ void __launch_bounds__(kWG) chain0_kernel(RenderParams P) {
+template <bool POINT_ONLY, bool INST, int REC, int MODE, int MINW = 1>
+__global__ void __launch_bounds__(kWG, MINW) chain0_kernel(RenderParams P) {
     __shared__ float s_ior[kIorCap * kWG];
     const uint16_t* rcpT = P.tables;          // no triangle tests here: both tables from global (L1)
     const uint16_t* rsqT = P.tables + 2048;
@@ -316,12 +316,7 @@ __global__ void __launch_bounds__(kWG) chain_compact_kernel(RenderParams P) {
 // answers of level k - 1's shadow rays (nB slots), which no longer wait for
 // each other -- a level's resolve needs its shadow answers only at the end of
 // the chunk.  Wave-uniform 64-slot chunks, the closest-hit chunks first.
-// REFILL (plain scenes): lane refill instead of 64-slot chunks -- a lane whose
-// ray is done takes the next position as soon as P.refill_min lanes of its wave
-// are idle, and the wave advances every busy lane by one node visit per step
-// (trav_step: closest-hit and any-hit rays side by side), so a wave no longer
-// waits for its longest ray.  Positions are dealt from the same 8 XCD bands.
-template <bool COUNT, bool FAST, bool INST, int MINW = 1, bool REFILL = false>
+template <bool COUNT, bool FAST, bool INST, int MINW = 1>
 __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -382,92 +377,7 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
             wave_steps += v;
         }
     };
-    if constexpr (REFILL && !INST) {
-        // positions 0 .. nA - 1: closest-hit entries; nA .. nA + nB - 1: shadow rays
-        const uint32_t npos = nA + nB;
-        unsigned int* q = P.queue + (size_t)(k + 1) * 256;
-        int band = blockIdx.x & 7, probes = 0;
-        bool exhausted = false, active = false, any = false;
-        uint32_t dst = 0;   // closest: entry; any: shadow slot
-        DRay r{};
-        DHit h{};
-        int32_t cur = 0;
-        int sp = 0;
-        for (;;) {
-            const unsigned long long idle = __ballot(!active);
-            const int nidle = __popcll(idle);
-            if (!exhausted && (nidle >= P.refill_min || nidle == 64)) {
-                uint32_t got = 0xFFFFFFFFu, hi = 0;
-                if (lane == 0) {
-                    while (probes < 8) {
-                        const uint32_t lo = (uint32_t)((uint64_t)npos * (uint32_t)band / 8u);
-                        const uint32_t bh = (uint32_t)((uint64_t)npos * (uint32_t)(band + 1) / 8u);
-                        const uint32_t v = lo < bh ? atomicAdd(q + band * 32, (uint32_t)nidle) : 0u;
-                        if (lo < bh && lo + v < bh) { got = lo + v; hi = bh; break; }
-                        band = (band + 1) & 7;
-                        probes++;
-                    }
-                }
-                got = __shfl(got, 0);
-                hi = __shfl(hi, 0);
-                if (got == 0xFFFFFFFFu) {
-                    exhausted = true;
-                } else if (!active) {
-                    const uint32_t p = got + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                    if (p < hi) {
-                        if (p < nA) {
-                            const uint32_t e = P.tr_perm ? P.tr_perm[p] : p;
-                            const float4 o = P.ch_ray[2 * base + e], d = P.ch_ray[2 * base + cap + e];
-                            r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.f);
-                            h = DHit{1e12f, 0.f, 0.f, -1};
-                            dst = e;
-                            any = false;
-                            active = true;
-                        } else {
-                            uint32_t i = p - nA;
-                            bool ok = true;
-                            if (P.sh_perm) {
-                                i = P.sh_perm[i];
-                            } else {
-                                const uint32_t s = i / m;
-                                ok = i - s * m < (uint32_t)nrays[s];
-                            }
-                            if (ok) {
-                                const float4 o = P.ray_o[sb + i], d = P.ray_d[sb + i];
-                                r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
-                                h = DHit{o.w, 0.f, 0.f, -1};
-                                dst = i;
-                                any = true;
-                                active = true;
-                            }
-                        }
-                        cur = 0;
-                        sp = 0;
-                    }
-                }
-            }
-            if (__ballot(active) == 0) {
-                if (exhausted) break;
-                continue;
-            }
-            if (COUNT) wave_steps++;
-            if (active) {
-                bool hit = false;
-                const bool done = (FAST && r.finite) ? trav_step<COUNT, true>(T, r, 0.001f, any, h, cur, sp, hit, st)
-                                                     : trav_step<COUNT, false>(T, r, 0.001f, any, h, cur, sp, hit, st);
-                if (done) {
-                    if (any) {
-                        P.occl[sb + dst] = hit ? 1 : 0;
-                    } else {   // a closest hit found in any earlier step left its packed slot in h.prim
-                        const int32_t prim = h.prim >= 0 ? T.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3] : -1;
-                        P.ch_hit[base + dst] = make_float4(h.t, h.a, h.b, __int_as_float(prim));
-                    }
-                    active = false;
-                }
-            }
-        }
-    } else if (P.ch_bands) {
+    if (P.ch_bands) {
         // XCD bands: the chunk range is cut into 8 contiguous bands and a workgroup
         // on XCD b mod 8 takes chunks of band b mod 8 from that band's counter,
         // then steals from the others -- with binned rays (mrt_bin.h) a band holds
@@ -517,8 +427,8 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
 // environment (or nothing: a GI ray without environment sampling; a split
 // child: nothing, flagged missed), a hit is shaded again with its shadow
 // answers and writes its value or marks itself pending.
-template <bool POINT_ONLY, bool INST, int REC, int MODE>
-__global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
+template <bool POINT_ONLY, bool INST, int REC, int MODE, int MINW = 1>
+__global__ void __launch_bounds__(kWG, MINW) chain_shade_kernel(RenderParams P) {
     __shared__ float s_ior[kIorCap * kWG];
     const uint16_t* rcpT = P.tables;
     const uint16_t* rsqT = P.tables + 2048;
@@ -789,30 +699,35 @@ __global__ void __launch_bounds__(kWG) adapt_combine_kernel(RenderParams P) {
     }
 }
 
-// kernel variants: point lights only x instanced scene x REC (1, 2) x MODE (gen, resolve)
-template <int MODE, int REC>
+// kernel variants: point lights only x instanced scene x REC (1, 2) x MODE (gen, resolve);
+// waves 2: the occupancy target of the shading kernels (they take 200-270 VGPRs unbounded)
+template <int MODE, int REC, int W>
 static KernelFn chain0_fn(bool po, bool inst) {
-    return po ? (inst ? chain0_kernel<true, true, REC, MODE> : chain0_kernel<true, false, REC, MODE>)
-              : (inst ? chain0_kernel<false, true, REC, MODE> : chain0_kernel<false, false, REC, MODE>);
+    return po ? (inst ? chain0_kernel<true, true, REC, MODE, W> : chain0_kernel<true, false, REC, MODE, W>)
+              : (inst ? chain0_kernel<false, true, REC, MODE, W> : chain0_kernel<false, false, REC, MODE, W>);
 }
-template <int MODE, int REC>
+template <int MODE, int REC, int W>
 static KernelFn chain_shade_fn(bool po, bool inst) {
-    return po ? (inst ? chain_shade_kernel<true, true, REC, MODE> : chain_shade_kernel<true, false, REC, MODE>)
-              : (inst ? chain_shade_kernel<false, true, REC, MODE> : chain_shade_kernel<false, false, REC, MODE>);
+    return po ? (inst ? chain_shade_kernel<true, true, REC, MODE, W> : chain_shade_kernel<true, false, REC, MODE, W>)
+              : (inst ? chain_shade_kernel<false, true, REC, MODE, W> : chain_shade_kernel<false, false, REC, MODE, W>);
 }
-KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec) {
-    if (rec == 2) return resolve ? chain0_fn<kResolve, 2>(po, inst) : chain0_fn<kGen, 2>(po, inst);
-    return resolve ? chain0_fn<kResolve, 1>(po, inst) : chain0_fn<kGen, 1>(po, inst);
+template <int W>
+static KernelFn pick_chain0_w(bool resolve, bool po, bool inst, int rec) {
+    if (rec == 2) return resolve ? chain0_fn<kResolve, 2, W>(po, inst) : chain0_fn<kGen, 2, W>(po, inst);
+    return resolve ? chain0_fn<kResolve, 1, W>(po, inst) : chain0_fn<kGen, 1, W>(po, inst);
 }
-KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec) {
-    if (rec == 2) return resolve ? chain_shade_fn<kResolve, 2>(po, inst) : chain_shade_fn<kGen, 2>(po, inst);
-    return resolve ? chain_shade_fn<kResolve, 1>(po, inst) : chain_shade_fn<kGen, 1>(po, inst);
+template <int W>
+static KernelFn pick_chain_shade_w(bool resolve, bool po, bool inst, int rec) {
+    if (rec == 2) return resolve ? chain_shade_fn<kResolve, 2, W>(po, inst) : chain_shade_fn<kGen, 2, W>(po, inst);
+    return resolve ? chain_shade_fn<kResolve, 1, W>(po, inst) : chain_shade_fn<kGen, 1, W>(po, inst);
 }
-KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves, bool refill) {
-    if (refill && !inst) {   // lane refill (plain scenes)
-        if (c) return f ? chain_trace_kernel<true, true, false, 1, true> : chain_trace_kernel<true, false, false, 1, true>;
-        return f ? chain_trace_kernel<false, true, false, 8, true> : chain_trace_kernel<false, false, false, 8, true>;
-    }
+KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec, int waves) {
+    return waves == 2 ? pick_chain0_w<2>(resolve, po, inst, rec) : pick_chain0_w<1>(resolve, po, inst, rec);
+}
+KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec, int waves) {
+    return waves == 2 ? pick_chain_shade_w<2>(resolve, po, inst, rec) : pick_chain_shade_w<1>(resolve, po, inst, rec);
+}
+KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves) {
     if (waves == 8 && !c && !inst)   // occupancy target of the plain-scene trace (timed variants)
         return f ? chain_trace_kernel<false, true, false, 8> : chain_trace_kernel<false, false, false, 8>;
     if (inst) return c ? (f ? chain_trace_kernel<true, true, true> : chain_trace_kernel<true, false, true>)

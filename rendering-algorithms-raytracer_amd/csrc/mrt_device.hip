@@ -151,8 +151,6 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
         size_t e = 0;
         float tmax = 0.f;
         AnyState as{};
-        AnyLeaf lf{};
-        const bool leaf_steps = P.leaf_steps != 0;
         for (;;) {
             const unsigned long long idle = __ballot(!active);
             const int nidle = __popcll(idle);
@@ -171,8 +169,6 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
                         as.cur = 0;
                         as.sp = 0;
                         as.aoff = -1;
-                        lf.v = 0;
-                        lf.pend = 0;
                         active = true;
                     }
                 }
@@ -185,9 +181,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
             if (active) {
                 bool hit = false;
                 bool done;
-                if (leaf_steps)   // one box or one triangle test per lane per step
-                    done = anyhit_step_inst2<COUNT, FAST, CHECK>(T, 0.001f, tmax, as, lf, P.ray_o, P.ray_d, e, hit, st);
-                else if constexpr (INST) done = anyhit_step_inst<COUNT, FAST, CHECK>(T, 0.001f, tmax, as, P.ray_o, P.ray_d, e, hit, st);
+                if constexpr (INST) done = anyhit_step_inst<COUNT, FAST, CHECK>(T, 0.001f, tmax, as, P.ray_o, P.ray_d, e, hit, st);
                 else done = (FAST && as.q.finite) ? anyhit_step<COUNT, true>(T, as.q, 0.001f, tmax, as.cur, as.sp, hit, st)
                                                   : anyhit_step<COUNT, false>(T, as.q, 0.001f, tmax, as.cur, as.sp, hit, st);
                 if (done) {
@@ -631,7 +625,8 @@ static int g_wavefront = 1;       // general shading: gen / trace / resolve kern
 static int g_shadow_sched = -1;   // shadow_kernel schedule: 0 grid-stride, 1 XCD bands, 2 bands + lane refill,
                                   // -1 auto: refill for dome-light (incoherent) rays, else bands
 static int g_shadow_waves = 8;    // shadow_kernel launch-bounds occupancy: 1 (none), 7, 8 (8: C4 / C5 -5.5%)
-static int g_primary_inst_waves = 6;   // primary kernel of special-leaf scenes: 1 (none), 5, 6 (6: C5 -5%)
+static int g_primary_inst_waves = 5;   // primary kernel of special-leaf scenes: 1 (none), 5, 6 (r02: 6 beat 1 by 5% on C5;
+                                       // r03: 5 = 6 within 0.3% with binned shadow rays, and 96 VGPRs spill less)
 static int g_resolve_waves = 4;   // resolve pass (kernel 2c) of dome-light scenes: 1 (none), 3 (special-leaf only), 4
 static int g_adapt_waves = 6;     // direct-lighting adaptive kernel occupancy target: 1 (none) or 6
                                   // (unbounded it takes 256 VGPRs, 1 wave: A3 30.7 -> 12.8 ms at 6)
@@ -652,8 +647,7 @@ static int g_bin = -1;            // ray binning (mrt_bin.h) before tracing: bit
                                   // -1 auto (bin_mode): chain levels of path-traced scenes (P4 -18% frame; the
                                   // coherent mirror / glass levels of R3 / G3 lose their pixel order: +22% / +44%)
                                   // and the dome shadow rays of instanced scenes (C5 -2.6%; D1 +2%)
-static int g_leaf_steps = 0;      // shadow_kernel lane refill: leaf lanes in steps of their own (anyhit_step_inst2)
-static int g_chain_refill = 0;    // chain_trace_kernel (plain scenes): lane refill at this many idle lanes (0: 64-slot chunks)
+static int g_chain_shade_waves = 1;   // chain0 / chain_shade occupancy target: 1 (none) or 2
 static int g_chain_bands = -1;    // chain_trace_kernel: XCD-banded chunk queue (binned rays: one XCD's L2 holds its share);
                                   // -1 auto: on when the level is binned (P4 -3.4%; unbinned R3 +5.7%, G3 +3%)
 static int g_dome_replay = 1;      // dome-light resolve (2c) sums 2a's recorded samples instead of sampling again
@@ -1331,11 +1325,12 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
     DeviceState& d = *s.dev;
     const int L = Q.ch_levels;
     const bool inst = d.special;
-    const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive), r0 = pick_chain0(true, d.point_only, inst, d.recursive);
-    const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive),
-                   rk = pick_chain_shade(true, d.point_only, inst, d.recursive);
-    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, Q.fast_box != 0, inst, g_chain_trace_waves,
-                                                       g_chain_refill > 0),
+    const int sw = g_chain_shade_waves;
+    const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive, sw),
+                   r0 = pick_chain0(true, d.point_only, inst, d.recursive, sw);
+    const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive, sw),
+                   rk = pick_chain_shade(true, d.point_only, inst, d.recursive, sw);
+    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, Q.fast_box != 0, inst, g_chain_trace_waves),
                    kf = pick_chain_finish(), kd = pick_chain_fold();
     auto go = [&](KernelFn f, int g) -> int {
         void* args[] = {&Q};
@@ -1478,8 +1473,7 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
         if (k < L) off += paths * level_mult(s, k);
     }
     Q.lvl_words = W;
-    Q.ch_bands = g_chain_bands > 0 || (g_chain_bands < 0 && (bin_mode(d) & 6)) || g_chain_refill > 0;
-    Q.refill_min = g_chain_refill;
+    Q.ch_bands = g_chain_bands > 0 || (g_chain_bands < 0 && (bin_mode(d) & 6));
     Q.order = 0;          // chunks index work items directly
     Q.wave_log = nullptr;
     Q.ray_o = c.rays;
@@ -1689,7 +1683,6 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
             P.sh_perm = A.perm;
             P.sh_perm_n = bin_total(A);
         }
-        P.leaf_steps = g_leaf_steps;
         void* args[] = {&P, &n_rays, &sched, &refill};
         P.wave_log = nullptr;
         P.queue = qbase + 24 * 32;
@@ -2729,11 +2722,9 @@ int mrt_set_tuning(const char* key, int value) {
         g_fused = value ? 1 : 0;
     } else if (k == "tile_lpt") {
         g_tile_lpt = value ? 1 : 0;
-    } else if (k == "leaf_steps") {
-        g_leaf_steps = value ? 1 : 0;
-    } else if (k == "chain_refill") {
-        if (value < 0 || value > 64) { set_error("chain_refill must be 0..64"); return MRT_ERR_INVALID; }
-        g_chain_refill = value;
+    } else if (k == "chain_shade_waves") {
+        if (value != 1 && value != 2) { set_error("chain_shade_waves must be 1 or 2"); return MRT_ERR_INVALID; }
+        g_chain_shade_waves = value;
     } else if (k == "chain_bands") {
         if (value < -1 || value > 1) { set_error("chain_bands must be -1..1"); return MRT_ERR_INVALID; }
         g_chain_bands = value;

@@ -605,93 +605,6 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
     return false;
 }
 
-// One node visit of a closest-hit OR any-hit traversal, resumable (traverse_impl's
-// loop body, no instancing; the mode is a per-lane flag, so lanes of one wave may
-// trace rays of both kinds in the same step).  `h.t` is the closest hit so far
-// (any: the ray's tMax, never lowered -- the first accepted triangle ends it).
-// The visit order and every box and triangle test are traverse_impl's, so a
-// closest hit found in steps equals traverse()'s; h.prim is the packed slot
-// until the caller resolves it (leaves[prim >> 2].prim[prim & 3]).  Returns true
-// when the ray is done: `hit` = some triangle was accepted; st.overflow on a
-// stack overflow.
-template <bool COUNT, bool FAST>
-__device__ __forceinline__ bool trav_step(const Trav& c, const DRay& r, float tMin, bool any, DHit& h, int32_t& cur,
-                                          int& sp, bool& hit, TravStats& st) {
-    int m;
-    int4 ch;
-    const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
-    if (FAST && c.scalar_nodes && __ballot(cur != c0) == 0) {   // wave-uniform node: scalar fetch
-        typedef const __attribute__((address_space(4))) float cfloat;
-        typedef const __attribute__((address_space(4))) int32_t cint;
-        cfloat* q = (cfloat*)(const void*)(c.nodes + c0);
-        cint* qc = (cint*)(q + 24);
-        ch = make_int4(qc[0], qc[1], qc[2], qc[3]);
-        float4 bx[6];
-#pragma unroll
-        for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
-        m = box_test_fast(bx, r, tMin, h.t);
-    } else {
-        const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
-        ch = reinterpret_cast<const int4*>(q)[6];
-        m = FAST ? box_test_fast(q, r, tMin, h.t) : box_test(q, r, tMin, h.t);
-    }
-    if (COUNT) st.nodes++;
-    const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
-    const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
-                       (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
-    const int inner = m & isinner;
-    int lm = m & isleaf;
-    bool have_next = false;
-    int32_t nxt = 0;
-    if (inner) {
-        const int top = 31 - __builtin_clz((unsigned)inner);
-        const int rest = inner ^ (1 << top);
-        if (rest) {
-            if (sp + 4 <= kLdsStack) {
-                c.lds[sp * kWG] = ch.x; sp += rest & 1;
-                c.lds[sp * kWG] = ch.y; sp += (rest >> 1) & 1;
-                c.lds[sp * kWG] = ch.z; sp += (rest >> 2) & 1;
-                c.lds[sp * kWG] = ch.w; sp += (rest >> 3) & 1;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if ((rest >> i) & 1)
-                        if (!stk_push(c, sp, sel4(ch, i))) { st.overflow = true; return true; }
-            }
-            if (COUNT && sp > st.max_sp) st.max_sp = sp;
-        }
-        nxt = sel4(ch, top);
-        have_next = true;
-    }
-    if (lm) {
-        uint32_t leaf = 0;
-        int k = 0, cnt = 0;
-        while (true) {
-            if (k == cnt) {
-                if (!lm) break;
-                const int s = __builtin_ctz((unsigned)lm);
-                lm &= lm - 1;
-                const uint32_t v = ~(uint32_t)sel4(ch, s);
-                leaf = v >> 4;
-                cnt = (int)(v & 3u) + 1;
-                k = 0;
-                if (COUNT) st.leaves++;
-            }
-            float t, a, b;
-            if (tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT)) {
-                hit = true;
-                if (any) return true;
-                h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
-            }
-            k++;
-        }
-    }
-    if (have_next) { cur = nxt; return false; }
-    if (sp == 0) return true;
-    cur = stk_pop(c, sp);
-    return false;
-}
-
 // Resumable any-hit step over the world hierarchy AND the instance BLASes
 // (special-leaf scenes: ProxyObject, alpha-mapped and motion-blurred lanes),
 // for the lane-refill schedule of shadow_kernel.  An any-hit answer does not
@@ -804,119 +717,6 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
     if (s.sp == 0) return true;
     s.cur = stk_pop(c, s.sp);
     return false;
-}
-
-// anyhit_step_inst with the leaf work cut into steps of its own: a node visit
-// only records its hit leaf slots (AnyLeaf), and every later step tests ONE
-// lane of them -- a triangle, or a proxy lane deferred onto the stack -- until
-// none is left; then the walk goes on with the node the visit chose (or the
-// stack).  A wave step then costs one box test or one triangle test per lane
-// instead of one box test plus the longest lane's whole leaf loop, which with
-// lanes on different nodes (refilled, incoherent rays) is most of the work.
-// The set of nodes and triangles tested before the first accepted triangle is
-// traversal-order dependent, the any-hit answer is not (see anyhit_step_inst).
-struct AnyLeaf {
-    int4 ch;        // child words of the node whose leaf slots are pending
-    uint32_t v;     // the packet being tested (its child word, inverted); 0: none
-    int pend;       // bits 0-3: pending leaf slots of ch; bits 4-6: next lane of packet v
-};
-static constexpr int32_t kNoNode = 0x7FFFFFFF;   // AnyState::cur after a visit with no next node: pop
-template <bool COUNT, bool FAST, bool CHECK>
-__device__ __forceinline__ bool anyhit_step_inst2(const Trav& c, float tMin, float tMax, AnyState& s, AnyLeaf& lf,
-                                                  const float4* ray_o, const float4* ray_d, size_t e, bool& hit,
-                                                  TravStats& st) {
-    if (lf.v != 0 || (lf.pend & 15)) {   // one lane of the pending leaf packets
-        if (lf.v == 0) {
-            const int sl = __builtin_ctz((unsigned)(lf.pend & 15));
-            lf.pend &= ~(1 << sl);
-            lf.v = ~(uint32_t)sel4(lf.ch, sl);
-            if (COUNT) st.leaves++;
-        }
-        const uint32_t v = lf.v, leaf = v >> 4;
-        const int k = (lf.pend >> 4) & 7, cnt = (int)(v & 3u) + 1;
-        if (k + 1 >= cnt) { lf.v = 0; lf.pend &= 15; }
-        else lf.pend = (lf.pend & 15) | ((k + 1) << 4);
-        if (v & 4u) {   // proxy lanes (world packets only): deferred instance walks
-            const int32_t pm = c.leaves[leaf].prim[k];
-            if (pm <= -2) {
-                if (!stk_push(c, s.sp, pm)) { st.overflow = true; return true; }
-                if (COUNT && s.sp > st.max_sp) st.max_sp = s.sp;
-                return false;
-            }
-        }
-        float t, a, b;
-        bool ok;
-        if (CHECK && (v & 8u)) {   // world: alpha / motion blur; BLAS: alpha
-            const int32_t pm = c.leaves[leaf].prim[k];
-            ok = (s.aoff < 0 && pm >= 0 && c.pflags && (c.pflags[pm] & 1u))
-                     ? mb_tri_test(c, pm, s.q, tMin, tMax, t, a, b)
-                     : tri_test(c.leaves[leaf].tri[k], s.q, tMin, tMax, t, a, b, c.rcpT);
-            ok = ok && !alpha_rejects(c, leaf, k, a, b, s.aoff < 0 ? 0 : s.aoff);
-        } else {
-            ok = tri_test(c.leaves[leaf].tri[k], s.q, tMin, tMax, t, a, b, c.rcpT);
-        }
-        if (ok) { hit = true; return true; }
-        return false;
-    }
-    if (s.cur == kNoNode) {
-        if (s.sp == 0) return true;
-        s.cur = stk_pop(c, s.sp);
-    }
-    if (s.cur < 0) {
-        if (s.cur == -1) {   // back to the world ray
-            const float4 o = ray_o[e], d = ray_d[e];
-            s.q = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
-            s.aoff = -1;
-            if (s.sp == 0) return true;
-            s.cur = stk_pop(c, s.sp);
-            return false;
-        }
-        const int i = -2 - s.cur;
-        if (!stk_push(c, s.sp, -1)) { st.overflow = true; return true; }
-        s.q = object_ray(c.inst[i], s.q, c.rcpT);
-        s.cur = c.inst[i].root;
-        s.aoff = c.inst[i].shade_base;
-        return false;
-    }
-    const DRay& q = s.q;
-    const float4* qn = reinterpret_cast<const float4*>(c.nodes + s.cur);
-    const int4 ch = reinterpret_cast<const int4*>(qn)[6];
-    const bool fast = FAST && q.finite;
-    const int m = fast ? box_test_fast(qn, q, tMin, tMax) : box_test(qn, q, tMin, tMax);
-    if (COUNT) st.nodes++;
-    const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
-    const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
-                       (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
-    const int inner = m & isinner;
-    const int lm = m & isleaf;
-    bool proxies = false;   // as anyhit_step_inst: instance walks before the descent
-#pragma unroll
-    for (int i = 0; i < 4; i++) proxies |= ((lm >> i) & 1) && (~(uint32_t)sel4(ch, i) & 4u);
-    int32_t nxt = kNoNode;
-    if (inner) {
-        const int top = 31 - __builtin_clz((unsigned)inner);
-        const int rest = proxies ? inner : inner ^ (1 << top);
-        if (rest) {
-            if (s.sp + 4 <= kLdsStack) {
-                c.lds[s.sp * kWG] = ch.x; s.sp += rest & 1;
-                c.lds[s.sp * kWG] = ch.y; s.sp += (rest >> 1) & 1;
-                c.lds[s.sp * kWG] = ch.z; s.sp += (rest >> 2) & 1;
-                c.lds[s.sp * kWG] = ch.w; s.sp += (rest >> 3) & 1;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if ((rest >> i) & 1)
-                        if (!stk_push(c, s.sp, sel4(ch, i))) { st.overflow = true; return true; }
-            }
-            if (COUNT && s.sp > st.max_sp) st.max_sp = s.sp;
-        }
-        if (!proxies) nxt = sel4(ch, top);
-    }
-    s.cur = nxt;
-    lf.ch = ch;
-    lf.pend = lm;
-    lf.v = 0;
-    return lm == 0 && nxt == kNoNode && s.sp == 0;
 }
 
 // FAST (node boxes known finite) uses the hardware min/max slab test for rays

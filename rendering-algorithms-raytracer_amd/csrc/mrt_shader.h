@@ -150,7 +150,6 @@ struct RenderParams {
     const uint32_t* sh_perm_n;
     const uint32_t* tr_perm;
     int32_t ch_bands;            // chain_trace: XCD-banded chunk queue (P.queue + (level + 1) * 256 words)
-    int32_t leaf_steps;          // shadow_kernel lane refill: anyhit_step_inst2 (leaf lanes in steps of their own)
     // dome-light replay (kernels 2a / 2c of the direct shading): 2a records, per
     // shadow-ray slot, the sample's E and dot(rVec, dir) (ray_e), and per dome
     // call (lcalls per pixel slot) its sample count | RNG draws << 8 (lrec); 2c
@@ -1493,9 +1492,9 @@ struct ShadeK { static constexpr KernelFn fn = shade_kernel<C, PO, F, I, kFused,
 KernelFn pick_shade_rec(bool c, bool po, bool f, bool inst, int rec);
 KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec, int waves);
 // defined in mrt_chain.hip: the wavefront chain engine
-KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec);
-KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec);
-KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves, bool refill);
+KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec, int waves);
+KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec, int waves);
+KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves);
 KernelFn pick_chain_compact();
 KernelFn pick_chain_finish();
 KernelFn pick_chain_fold();

@@ -12,7 +12,7 @@ from helpers import bits, camera, config_scene
 from test_chain import CASES
 
 KNOB_DEFAULTS = dict(bin=-1, bin_dbits=2, bin_obits=2, dome_replay=1, chain=1, chain_mb=16384, chain_bands=-1,
-                     chain_refill=0, leaf_steps=0, shadow_sched=-1)
+                     shadow_sched=-1)
 
 
 def tuned(**knobs):
@@ -111,25 +111,11 @@ def test_binned_chain_chunks_equal_one_chunk():
 @pytest.mark.parametrize("case", ["pt_rect_panel", "pt_panel_env", "mixed_rect_point", "disp_cornell_mixed",
                                   "adapt_mixed_rect", "leaf_translucent"])
 def test_chain_trace_schedules_give_identical_frames(case):
-    """The chain trace kernel's schedules -- grid-stride chunks, XCD-banded chunks,
-    lane refill at several thresholds (closest-hit and shadow rays stepped side by
-    side, trav_step), each binned and unbinned -- trace every ray with the same
-    visits, so frames, hit ids and ray counts are identical."""
+    """The chain trace kernel's schedules -- grid-stride chunks and XCD-banded
+    chunks, each binned and unbinned -- trace every ray with the same visits, so
+    frames, hit ids and ray counts are identical."""
     P, _, cam = CASES[case]()
-    out = runs(P, cam, 64, 48, [dict(bin=0, chain_bands=0), dict(bin=0, chain_bands=1), dict(bin=0, chain_refill=1),
-                                dict(bin=0, chain_refill=32), dict(bin=6, chain_refill=48), dict(bin=6, chain_refill=64),
-                                dict(bin=6, chain_bands=1)])
+    out = runs(P, cam, 64, 48, [dict(bin=0, chain_bands=0), dict(bin=0, chain_bands=1), dict(bin=6, chain_bands=0),
+                                dict(bin=6, chain_bands=1), dict(bin=2), dict(bin=4, chain_bands=1)])
     assert_all_same(out)
 
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("key,W,H", [("D1", 96, 96), ("C5", 128, 72), ("C4", 120, 68)])
-def test_leaf_steps_give_identical_frames(key, W, H):
-    """The lane-refill shadow kernel with leaf lanes in steps of their own
-    (anyhit_step_inst2: one box or one triangle test per lane per step, proxy
-    lanes deferred onto the stack) answers every shadow ray as before."""
-    P, _, cam = config_scene(key)
-    out = runs(P, cam, W, H, [dict(shadow_sched=2), dict(shadow_sched=2, leaf_steps=1),
-                              dict(shadow_sched=2, leaf_steps=1, bin=1), dict(shadow_sched=1)])
-    assert out[0][2]["shadow_rays"] > 0
-    assert_all_same(out)

@@ -373,17 +373,14 @@ def shadow_schedules(P, cam, W, H):
     L = miro.lib()
     out = []
     try:
-        # near: nearest hit child first; leaf: the refill step with leaf lanes in steps of their own
-        for sched, near, leaf in ((0, 0, 0), (1, 0, 0), (1, 1, 0), (2, 0, 0), (2, 1, 0), (2, 0, 1)):
+        for sched, near in ((0, 0), (1, 0), (1, 1), (2, 0), (2, 1)):   # near: nearest hit child first
             assert L.mrt_set_tuning(b"shadow_sched", sched) == 0
             assert L.mrt_set_tuning(b"near_first", near) == 0
-            assert L.mrt_set_tuning(b"leaf_steps", leaf) == 0
             img, hits = render(P, cam, W, H)
             out.append((img, hits, P.last_stats))
     finally:
         L.mrt_set_tuning(b"shadow_sched", -1)
         L.mrt_set_tuning(b"near_first", -1)
-        L.mrt_set_tuning(b"leaf_steps", 0)
     img0, hits0, st0 = out[0]
     for img, hits, st in out[1:]:
         assert np.array_equal(hits0["prim"], hits["prim"])
