@@ -193,8 +193,8 @@ __device__ __forceinline__ void no_children(const RenderParams& P, uint32_t e) {
 // depend on the shadow answers); kResolve runs the same shading with the
 // answers and writes the path's value or marks it pending.  No traversal runs
 // in either, so the shading state never has to live across one.
-template <bool POINT_ONLY, bool INST, int REC, int MODE, int MINW = 1>
-__global__ void __launch_bounds__(kWG, MINW) chain0_kernel(RenderParams P) {
+template <bool POINT_ONLY, bool INST, int REC, int MODE>
+__global__ void __launch_bounds__(kWG) chain0_kernel(RenderParams P) {
     __shared__ float s_ior[kIorCap * kWG];
     const uint16_t* rcpT = P.tables;          // no triangle tests here: both tables from global (L1)
     const uint16_t* rsqT = P.tables + 2048;
@@ -427,8 +427,8 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
 // environment (or nothing: a GI ray without environment sampling; a split
 // child: nothing, flagged missed), a hit is shaded again with its shadow
 // answers and writes its value or marks itself pending.
-template <bool POINT_ONLY, bool INST, int REC, int MODE, int MINW = 1>
-__global__ void __launch_bounds__(kWG, MINW) chain_shade_kernel(RenderParams P) {
+template <bool POINT_ONLY, bool INST, int REC, int MODE>
+__global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
     __shared__ float s_ior[kIorCap * kWG];
     const uint16_t* rcpT = P.tables;
     const uint16_t* rsqT = P.tables + 2048;
@@ -699,33 +699,24 @@ __global__ void __launch_bounds__(kWG) adapt_combine_kernel(RenderParams P) {
     }
 }
 
-// kernel variants: point lights only x instanced scene x REC (1, 2) x MODE (gen, resolve);
-// waves 2: the occupancy target of the shading kernels (they take 200-270 VGPRs unbounded)
-template <int MODE, int REC, int W>
+// kernel variants: point lights only x instanced scene x REC (1, 2) x MODE (gen, resolve)
+template <int MODE, int REC>
 static KernelFn chain0_fn(bool po, bool inst) {
-    return po ? (inst ? chain0_kernel<true, true, REC, MODE, W> : chain0_kernel<true, false, REC, MODE, W>)
-              : (inst ? chain0_kernel<false, true, REC, MODE, W> : chain0_kernel<false, false, REC, MODE, W>);
+    return po ? (inst ? chain0_kernel<true, true, REC, MODE> : chain0_kernel<true, false, REC, MODE>)
+              : (inst ? chain0_kernel<false, true, REC, MODE> : chain0_kernel<false, false, REC, MODE>);
 }
-template <int MODE, int REC, int W>
+template <int MODE, int REC>
 static KernelFn chain_shade_fn(bool po, bool inst) {
-    return po ? (inst ? chain_shade_kernel<true, true, REC, MODE, W> : chain_shade_kernel<true, false, REC, MODE, W>)
-              : (inst ? chain_shade_kernel<false, true, REC, MODE, W> : chain_shade_kernel<false, false, REC, MODE, W>);
+    return po ? (inst ? chain_shade_kernel<true, true, REC, MODE> : chain_shade_kernel<true, false, REC, MODE>)
+              : (inst ? chain_shade_kernel<false, true, REC, MODE> : chain_shade_kernel<false, false, REC, MODE>);
 }
-template <int W>
-static KernelFn pick_chain0_w(bool resolve, bool po, bool inst, int rec) {
-    if (rec == 2) return resolve ? chain0_fn<kResolve, 2, W>(po, inst) : chain0_fn<kGen, 2, W>(po, inst);
-    return resolve ? chain0_fn<kResolve, 1, W>(po, inst) : chain0_fn<kGen, 1, W>(po, inst);
+KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec) {
+    if (rec == 2) return resolve ? chain0_fn<kResolve, 2>(po, inst) : chain0_fn<kGen, 2>(po, inst);
+    return resolve ? chain0_fn<kResolve, 1>(po, inst) : chain0_fn<kGen, 1>(po, inst);
 }
-template <int W>
-static KernelFn pick_chain_shade_w(bool resolve, bool po, bool inst, int rec) {
-    if (rec == 2) return resolve ? chain_shade_fn<kResolve, 2, W>(po, inst) : chain_shade_fn<kGen, 2, W>(po, inst);
-    return resolve ? chain_shade_fn<kResolve, 1, W>(po, inst) : chain_shade_fn<kGen, 1, W>(po, inst);
-}
-KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec, int waves) {
-    return waves == 2 ? pick_chain0_w<2>(resolve, po, inst, rec) : pick_chain0_w<1>(resolve, po, inst, rec);
-}
-KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec, int waves) {
-    return waves == 2 ? pick_chain_shade_w<2>(resolve, po, inst, rec) : pick_chain_shade_w<1>(resolve, po, inst, rec);
+KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec) {
+    if (rec == 2) return resolve ? chain_shade_fn<kResolve, 2>(po, inst) : chain_shade_fn<kGen, 2>(po, inst);
+    return resolve ? chain_shade_fn<kResolve, 1>(po, inst) : chain_shade_fn<kGen, 1>(po, inst);
 }
 KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves) {
     if (waves == 8 && !c && !inst)   // occupancy target of the plain-scene trace (timed variants)

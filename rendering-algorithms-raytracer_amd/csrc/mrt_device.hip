@@ -647,10 +647,10 @@ static int g_bin = -1;            // ray binning (mrt_bin.h) before tracing: bit
                                   // -1 auto (bin_mode): chain levels of path-traced scenes (P4 -18% frame; the
                                   // coherent mirror / glass levels of R3 / G3 lose their pixel order: +22% / +44%)
                                   // and the dome shadow rays of instanced scenes (C5 -2.6%; D1 +2%)
-static int g_chain_shade_waves = 1;   // chain0 / chain_shade occupancy target: 1 (none) or 2
 static int g_chain_bands = -1;    // chain_trace_kernel: XCD-banded chunk queue (binned rays: one XCD's L2 holds its share);
                                   // -1 auto: on when the level is binned (P4 -3.4%; unbinned R3 +5.7%, G3 +3%)
 static int g_dome_replay = 1;      // dome-light resolve (2c) sums 2a's recorded samples instead of sampling again
+static int g_bin_blocks = 4;      // binning launches: workgroups per CU (each reserves its range of every bin atomically)
 static int g_bin_dbits = 2;       // binning key: direction cells per octahedral axis = 2^dbits
 static int g_bin_obits = 2;       //   origin cells per scene-box axis = 2^obits (2 dbits + 3 obits <= 12);
                                   //   sweep of 12 pairs: (2, 2) best on P4 (-18%) and C5 (-2.6%), finer
@@ -1158,8 +1158,8 @@ static BinArgs bin_args(const DeviceState& d, const StreamCtx& c, int which, con
     return A;
 }
 static const uint32_t* bin_total(const BinArgs& A) { return A.hist + (size_t(1) << (2 * A.dbits + 3 * A.obits)); }
-static int bin_grid(const DeviceState& d, size_t n) {
-    return (int)std::max<size_t>(1, std::min<size_t>((size_t)d.cus * 4, (n + 255) / 256));
+static int bin_grid(const DeviceState& d, size_t n) {   // fewer blocks: fewer per-bin global atomics
+    return (int)std::max<size_t>(1, std::min<size_t>((size_t)d.cus * (size_t)g_bin_blocks, (n + 255) / 256));
 }
 
 static int ensure_slots(StreamCtx& c, size_t slots) {
@@ -1325,11 +1325,9 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
     DeviceState& d = *s.dev;
     const int L = Q.ch_levels;
     const bool inst = d.special;
-    const int sw = g_chain_shade_waves;
-    const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive, sw),
-                   r0 = pick_chain0(true, d.point_only, inst, d.recursive, sw);
-    const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive, sw),
-                   rk = pick_chain_shade(true, d.point_only, inst, d.recursive, sw);
+    const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive), r0 = pick_chain0(true, d.point_only, inst, d.recursive);
+    const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive),
+                   rk = pick_chain_shade(true, d.point_only, inst, d.recursive);
     const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, Q.fast_box != 0, inst, g_chain_trace_waves),
                    kf = pick_chain_finish(), kd = pick_chain_fold();
     auto go = [&](KernelFn f, int g) -> int {
@@ -2722,9 +2720,6 @@ int mrt_set_tuning(const char* key, int value) {
         g_fused = value ? 1 : 0;
     } else if (k == "tile_lpt") {
         g_tile_lpt = value ? 1 : 0;
-    } else if (k == "chain_shade_waves") {
-        if (value != 1 && value != 2) { set_error("chain_shade_waves must be 1 or 2"); return MRT_ERR_INVALID; }
-        g_chain_shade_waves = value;
     } else if (k == "chain_bands") {
         if (value < -1 || value > 1) { set_error("chain_bands must be -1..1"); return MRT_ERR_INVALID; }
         g_chain_bands = value;
@@ -2733,6 +2728,9 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "bin") {
         if (value < -1 || value > 7) { set_error("bin must be -1 (auto) or 0..7"); return MRT_ERR_INVALID; }
         g_bin = value;
+    } else if (k == "bin_blocks") {
+        if (value < 1 || value > 16) { set_error("bin_blocks must be 1..16"); return MRT_ERR_INVALID; }
+        g_bin_blocks = value;
     } else if (k == "bin_dbits") {   // the pair is checked when a batch is binned (2 dbits + 3 obits = 1..12)
         if (value < 0 || value > 6) { set_error("bin_dbits must be 0..6"); return MRT_ERR_INVALID; }
         g_bin_dbits = value;

@@ -627,21 +627,22 @@ template <bool COUNT, bool FAST, bool CHECK>
 __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, float tMax, AnyState& s,
                                                  const float4* ray_o, const float4* ray_d, size_t e, bool& hit,
                                                  TravStats& st) {
-    if (s.cur < 0) {
-        if (s.cur == -1) {   // back to the world ray
-            const float4 o = ray_o[e], d = ray_d[e];
-            s.q = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
-            s.aoff = -1;
-            if (s.sp == 0) return true;
-            s.cur = stk_pop(c, s.sp);
-            return false;
-        }
+    // Leaving and entering an instance share the step with the node visit that
+    // follows, so every lane runs the same box test in every step (no step in
+    // which some lanes only transform a ray while the others visit nodes).
+    if (s.cur == -1) {   // back to the world ray, then the next stack entry
+        const float4 o = ray_o[e], d = ray_d[e];
+        s.q = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
+        s.aoff = -1;
+        if (s.sp == 0) return true;
+        s.cur = stk_pop(c, s.sp);
+    }
+    if (s.cur <= -2) {   // enter instance -2 - cur: object-space ray, its BLAS root
         const int i = -2 - s.cur;
         if (!stk_push(c, s.sp, -1)) { st.overflow = true; return true; }
         s.q = object_ray(c.inst[i], s.q, c.rcpT);
         s.cur = c.inst[i].root;
         s.aoff = c.inst[i].shade_base;
-        return false;
     }
     const DRay& q = s.q;
     const float4* qn = reinterpret_cast<const float4*>(c.nodes + s.cur);

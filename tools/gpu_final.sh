@@ -1,18 +1,20 @@
 #!/bin/bash
-# Round-end evidence: GPU parity suite, smoke, and single-stream rocprofv3
-# kernel-trace summaries of the A3 / R3 legs (one frame in flight, so each
-# kernel's average duration is its own launch time).  Each GPU step has its
-# own time limit; the first failure ends the script.
+# Round-end evidence, part 1: GPU parity suite, smoke, then one bench line per
+# config with the CPU baseline (the C3 headline at the driver's own settings).
+# Part 2 is tools/prof_all.sh (rocprofv3 kernel trace + PMC passes per config).
+# Each GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export MRT_SCENE_CACHE=/tmp/mrt_scenes
-timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+bash tools/gpu_pytest.sh || exit $?
+if [ -f rendering-algorithms-raytracer_amd/lib/libmrt_domeseq.so ]; then   # batched vs sequential dome sampling
+    echo "== C5 dome"; AB_ROUNDS=2 AB_CONFIG=C5 bash tools/gpu_ab_libs.sh domeseq > gpurun_out/ab_dome_C5.log 2>&1 || exit $?
+    echo "== D1 dome"; AB_ROUNDS=4 AB_CONFIG=D1 bash tools/gpu_ab_libs.sh domeseq > gpurun_out/ab_dome_D1.log 2>&1 || exit $?
+    cat gpurun_out/ab_dome_C5.log gpurun_out/ab_dome_D1.log | cut -c1-200
+fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; tail -1 gpurun_out/smoke.log | cut -c1-200; [ $rc -eq 0 ] || exit $rc
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-for c in A3 R3; do
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1_$c -o run -- python3 bench.py --config $c --steps 5 --warmup 2 --inflight 1 --no-cpu-baseline > gpurun_out/prof1_$c.log 2>&1
-    rc=$?; tail -1 gpurun_out/prof1_$c.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc
-done
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_C3_driver.log 2>&1
+rc=$?; tail -1 gpurun_out/bench_C3_driver.log | cut -c1-200; [ $rc -eq 0 ] || exit $rc
+CONFIGS="${CONFIGS:-C2 C4 D1 C5 A3 R3 P4 G3}" EXTRA="--steps 10 --warmup 2" bash tools/gpu_bench_all.sh
