@@ -386,11 +386,18 @@ int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
  * "shadow_sched" [-1]..2 (wavefront shadow rays: auto, grid-stride, XCD bands,
  * bands + lane refill), "refill_min" 1..64 [40] (idle lanes that trigger a refill),
  * "fast_box" 0/[1] (hardware min/max slab test when its finiteness precondition
- * holds), "primary_waves" 0/[6] (occupancy target of the primary-ray kernel),
+ * holds), "primary_waves" 0/6/[7]/8 (occupancy target of the primary-ray kernel),
  * "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands, dynamic
  * interleaved, dynamic banded; see TileSched), "shade1" 0/[1] (specialised shading
  * kernel for one point light and one path), "lds_pad_kb" [0]..128 (extra LDS per
- * workgroup, lowers occupancy for sweeps).  Process-wide. */
+ * workgroup, lowers occupancy for sweeps), "fused" 0/[1] (one-launch frame kernel
+ * for one point light), "bin" [-1] / 0..7 (ray binning before tracing: bit 0 the
+ * wavefront shadow pass, bit 1 the chain levels' closest-hit entries, bit 2 their
+ * shadow rays; -1 auto), "bin_dbits" 0..6 [2] / "bin_obits" 0..4 [2] (binning key:
+ * direction and origin cells per axis as powers of two, 2 dbits + 3 obits <= 12),
+ * "bin_blocks" 1..16 [4] (binning workgroups per CU), "dome_replay" 0/[1] (the
+ * dome-light resolve pass sums the recorded samples), "chain_bands" [-1]..1
+ * (XCD-banded chain trace queue; -1: on for binned levels).  Process-wide. */
 int mrt_set_tuning(const char* key, int value);
 
 /* Diagnostics: per-wave records of the last count-mode render (count_visits = 1)

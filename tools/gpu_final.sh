@@ -8,11 +8,6 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export MRT_SCENE_CACHE=/tmp/mrt_scenes
 bash tools/gpu_pytest.sh || exit $?
-if [ -f rendering-algorithms-raytracer_amd/lib/libmrt_domeseq.so ]; then   # batched vs sequential dome sampling
-    echo "== C5 dome"; AB_ROUNDS=2 AB_CONFIG=C5 bash tools/gpu_ab_libs.sh domeseq > gpurun_out/ab_dome_C5.log 2>&1 || exit $?
-    echo "== D1 dome"; AB_ROUNDS=4 AB_CONFIG=D1 bash tools/gpu_ab_libs.sh domeseq > gpurun_out/ab_dome_D1.log 2>&1 || exit $?
-    cat gpurun_out/ab_dome_C5.log gpurun_out/ab_dome_D1.log | cut -c1-200
-fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; tail -1 gpurun_out/smoke.log | cut -c1-200; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_C3_driver.log 2>&1

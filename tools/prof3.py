@@ -47,6 +47,9 @@ PASS = {"primary_kernel": "primary", "frame1_kernel": "primary", "shade1_kernel"
 NO_COUNT_ARG = {"chain0_kernel", "chain_shade_kernel", "chain_compact_kernel", "chain_finish_kernel",
                 "chain_path_kernel", "tile_order_kernel", "chain_fold_kernel", "adapt_combine_kernel"}
 FRAME_KERNELS = ("primary_kernel", "frame1_kernel", "adaptive_kernel")
+# frames of one tools/prof_all.sh run (bench.py --inflight 1 --steps 6 --warmup 1): one
+# setup frame, the instrumented (count-mode) frame, 1 warmup, 6 timed, 5 latency frames
+FRAMES_TIMED, FRAMES_COUNT = 13, 1
 
 
 def parse_name(name):
@@ -189,6 +192,11 @@ def summarise(cfg, d):
             for c, v in cs.items():
                 frames[c] = max(frames[c], len(v))
     n_trace = sum(len(v) for k, v in durs.items() if parse_name(k)[0] in FRAME_KERNELS and timed(*parse_name(k)))
+    if not n_trace:   # no frame kernel (adaptive passes over the chain engine): the run's own frame count
+        n_trace = FRAMES_TIMED
+    # kernels without a count-mode variant also ran in the instrumented frame(s)
+    def per_frame(base, n):
+        return n + FRAMES_COUNT if base in NO_COUNT_ARG else n
     passes = defaultdict(lambda: {"hbm_bytes": 0.0, "avg_us": 0.0, "kernels": []})
     for k in set(list(cnt) + list(durs)):
         base, targs = parse_name(k)
@@ -197,11 +205,13 @@ def summarise(cfg, d):
         p = passes[PASS[base]]
         p["kernels"].append(base + "<" + targs + ">")
         if k in durs and n_trace:
-            p["avg_us"] += sum(durs[k]) / n_trace          # per frame, all of this kernel's launches
+            p["avg_us"] += sum(durs[k]) / per_frame(base, n_trace)   # per frame, all of this kernel's launches
         cs = cnt.get(k, {})
         if cs.get("FETCH_SIZE") and cs.get("WRITE_SIZE"):
-            p["hbm_bytes"] += (2 * sum(cs["FETCH_SIZE"]) * 1024 / max(1, frames["FETCH_SIZE"])
-                               + sum(cs["WRITE_SIZE"]) * 1024 / max(1, frames["WRITE_SIZE"]))
+            ff = frames["FETCH_SIZE"] or FRAMES_TIMED
+            fw = frames["WRITE_SIZE"] or FRAMES_TIMED
+            p["hbm_bytes"] += (2 * sum(cs["FETCH_SIZE"]) * 1024 / per_frame(base, ff)
+                               + sum(cs["WRITE_SIZE"]) * 1024 / per_frame(base, fw))
     for name, p in sorted(passes.items()):
         p["hbm_bytes"] = int(p["hbm_bytes"])
         p["avg_us"] = round(p["avg_us"], 3)
