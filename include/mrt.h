@@ -71,10 +71,13 @@ typedef struct {
     int32_t cast_shadows;    /* Light::setCastShadows (a dome light always casts)      */
     int32_t texture;         /* MRT_DOME_LIGHT: DomeLight::setTexture, a texture id of
                                 mrt_scene_add_texture (-1 for the other lights)        */
-    int32_t transparent_shadows; /* 1 = Light::setFastShadows(false) (src/Light.h:24): the
-                                transparent-shadow walks of src/PointLight.cpp:49-70,
-                                src/RectangleLight.cpp:93-116, src/DomeLight.cpp:115-;
-                                not implemented: mrt_scene_add_light returns
+    int32_t transparent_shadows; /* 1 = Light::setFastShadows(false) (src/Light.h:24).
+                                Point light: its walk (src/PointLight.cpp:49-70) starts
+                                with sampleHit.t = distance and loops while t < distance,
+                                so it never traces -- the light casts no shadow, as the
+                                reference.  Rectangle / dome lights (the walks of
+                                src/RectangleLight.cpp:93-116, src/DomeLight.cpp:123-145):
+                                not implemented, mrt_scene_add_light returns
                                 MRT_ERR_INVALID.  0 (zero-initialised) = m_fastShadows
                                 true, the reference default (ABI 7)                   */
 } mrt_light;

@@ -641,7 +641,8 @@ static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_cha
 static int g_chain_mb = 16384;    // chain scratch per stream (MB); larger frames run in chunks of work items
 static int g_chain_adapt = 1;     // adaptive supersampling of REC scenes: passes over the chain engine (0: fused kernel)
 static int g_fused = 1;           // one point light, one path: frame1_kernel (primary + shading in one launch)
-static int g_frame1_waves = 6;    // frame1_kernel launch-bounds occupancy target: 1 (none), 5..8
+static int g_frame1_waves = 7;    // frame1_kernel launch-bounds occupancy target: 1 (none), 5..8 (7: -0.9% per frame with
+                                  // 4 frames in flight, +0.8% single-frame latency; profiles/r03_c3_scalar_waves_ab.txt)
 static int g_bin = -1;            // ray binning (mrt_bin.h) before tracing: bit 0 the wavefront shadow pass (kernel 2b),
                                   // bit 1 the chain levels' closest-hit entries, bit 2 the chain levels' shadow rays;
                                   // -1 auto (bin_mode): chain levels of path-traced scenes (P4 -18% frame; the
@@ -1751,8 +1752,13 @@ int mrt_scene_add_light(mrt_scene* s, const mrt_light* l) {
         return MRT_ERR_INVALID;
     }
     if (s->impl.lights.size() >= (size_t)kMaxLights) { set_error("too many lights"); return MRT_ERR_INVALID; }
-    if (l->transparent_shadows) {   // Light::setFastShadows(false): no reference scene sets it
-        set_error("transparent shadows (Light::setFastShadows(false)) are not implemented; fast shadows only");
+    // Light::setFastShadows(false).  A point light's "full method" (src/PointLight.cpp:49-70)
+    // sets sampleHit.t = distance and then loops while sampleHit.t < distance: it never
+    // traces, so the light casts no shadow -- exactly cast_shadows = 0.  The rectangle and
+    // dome lights' transparency walks (src/RectangleLight.cpp:93-116, src/DomeLight.cpp:
+    // 123-145) are not implemented; no reference scene sets the flag.
+    if (l->transparent_shadows && l->type != MRT_POINT_LIGHT) {
+        set_error("transparent shadows (Light::setFastShadows(false)) of rectangle / dome lights are not implemented");
         return MRT_ERR_INVALID;
     }
     DevLight d;
@@ -1777,7 +1783,7 @@ int mrt_scene_add_light(mrt_scene* s, const mrt_light* l) {
     memcpy(d.pos, l->pos, 12); memcpy(d.v1, l->v1, 12); memcpy(d.v2, l->v2, 12); memcpy(d.v3, l->v3, 12);
     d.samples = l->samples < 1 ? 1 : l->samples;
     d.noise = l->noise_threshold;
-    d.cast_shadows = l->cast_shadows;
+    d.cast_shadows = l->cast_shadows && !l->transparent_shadows;
     d.power = l->power;
     if (l->type == MRT_RECT_LIGHT) {
         // RectangleLight::setPower (src/RectangleLight.cpp:14-40)

@@ -367,7 +367,6 @@ struct Shader {
     // kDomeMaxRejects such redraws in one call the loop stops (the reference would
     // not terminate when the whole map lies below the horizon).
     static constexpr int kDomeMaxRejects = 256;
-    static constexpr int kDomeBatch = 4;   // dome-sample attempts looked up together
     template <bool COUNT>
     __device__ v3 dome_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec, bool secondary) {
         const DevDome& D = P.domes[l.dome];
@@ -393,7 +392,6 @@ struct Shader {
                 return scale(acc, recip);
             }
         }
-#ifdef MRT_DOME_SEQ
         const uint32_t dim0 = dim;
         int done = 0, rejects = 0;
         bool cut = false;
@@ -429,68 +427,6 @@ struct Shader {
             acc = add(acc, scale(E, att));
             tmpSpec += dot(rVec, dir) * att;
         } while (done < numSamples && !cut);
-#else
-        const uint32_t dim0 = dim;
-        int done = 0, rejects = 0;
-        bool cut = false, go = true;
-        // The draws are attempts a = 0, 1, .. with dims dim0 + 2a, + 2a + 1 whether or
-        // not an attempt is rejected, so kDomeBatch attempts are looked up at once:
-        // their Distribution1D searches run in lockstep and their table loads
-        // overlap, instead of one dependent chain of loads per attempt.  They are
-        // then consumed in order with the reference loop's logic; lookups past the
-        // loop's end are discarded (no ray, no draw counted).
-        do {
-            float e1[kDomeBatch], e2[kDomeBatch], fu[kDomeBatch], fv[kDomeBatch], p0[kDomeBatch], p1[kDomeBatch];
-#pragma unroll
-            for (int a = 0; a < kDomeBatch; a++) {
-                e1[a] = rng(pixel, skey, dim + 2 * a, seed);
-                e2[a] = rng(pixel, skey, dim + 2 * a + 1, seed);
-            }
-            dist_sample_batch<kDomeBatch>(D.cdf_u, D.func_u, D.guide_u, D.nu, nullptr, 0, D.inv_int_u, nullptr, e1, fu, p0);
-            int ucol[kDomeBatch];
-#pragma unroll
-            for (int a = 0; a < kDomeBatch; a++) {
-                const int iu = (int)fu[a];
-                ucol[a] = iu == D.nu ? iu - 1 : iu;
-            }
-            dist_sample_batch<kDomeBatch>(D.cdf_v, D.func_v, D.guide_v, D.nv, ucol, D.nv + 1, 0.f, D.inv_int_v, e2, fv, p1);
-            float4 tex[kDomeBatch];
-            v3 dirs[kDomeBatch];
-            float sinTs[kDomeBatch];
-#pragma unroll
-            for (int a = 0; a < kDomeBatch; a++) {
-                const int iu = (int)fu[a], iv = (int)fv[a];
-                const float cosT = D.cos_v[iv], sinT = D.sin_v[iv], sinP = D.sin_u[iu], cosP = D.cos_u[iu];
-                dirs[a] = mk(-sinT * cosP, -cosT, -sinT * sinP);
-                sinTs[a] = sinT;
-                tex[a] = reinterpret_cast<const float4*>(D.rad)[(size_t)iv * (D.nu + 1) + iu];   // tex_lookup_dir of dir
-            }
-#pragma unroll
-            for (int a = 0; a < kDomeBatch; a++) {
-                if (!go) break;
-                dim += 2;   // this attempt's two draws
-                const v3 dir = dirs[a];
-                if (dot(normal, dir) < 0.0f) {
-                    go = ++rejects < kDomeMaxRejects && done < numSamples && !cut;
-                    continue;
-                }
-                const float pdf = (p0[a] * p1[a]) / (kTwoPI2 * sinTs[a]);
-                const v3 img = mk(tex[a].x, tex[a].y, tex[a].z);
-                const float inv = 1.0f / pdf;  // E = m_Gain * imageSample / pdf (Vector3::operator/)
-                const v3 E = scale(scale(img, l.power), inv);
-                float att = 1.0f;
-                if (MODE == kGen && P.lrec) P.ray_e[slot0 + nslot] = make_float4(E.x, E.y, E.z, dot(rVec, dir));
-                if (occluded<COUNT>(from, dir, 1e12f)) att = 0.0f;
-                done++;
-                recip = 1.0f / (float)done;
-                const v3 Es = scale(E, recip);
-                cut = (((Es.x + Es.y) + Es.z) * 0.333333f) < l.noise;
-                acc = add(acc, scale(E, att));
-                tmpSpec += dot(rVec, dir) * att;
-                go = done < numSamples && !cut;
-            }
-        } while (go);
-#endif
         if (MODE == kGen && P.lrec) P.lrec[lrec0 + lcall++] = (uint32_t)done | ((dim - dim0) << 8);
         outSpec = tmpSpec * recip;
         return scale(acc, recip);

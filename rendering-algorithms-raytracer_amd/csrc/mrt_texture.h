@@ -169,56 +169,4 @@ MRT_HD float dist_sample_guided(const float* cdf, const float* func, const int32
     return (float)o + du;
 }
 
-// dist_sample_guided for K draws at once (device): the K lower_bound searches
-// advance in lockstep, so each round issues up to K independent loads and the
-// rounds number max over the draws instead of their sum.  Draw a searches
-// row col[a] (cdf + col[a] * stride, func + col[a] * (n), guide likewise; inv
-// per row from inv_rows) when col is given, else the one table (inv_one).
-// Every result equals dist_sample_guided's for the same draw.
-#ifdef __HIPCC__
-template <int K>
-__device__ __forceinline__ void dist_sample_batch(const float* cdf, const float* func, const int32_t* guide, int n,
-                                                  const int* col, int stride, float inv_one, const float* inv_rows,
-                                                  const float (&u)[K], float (&out)[K], float (&pdf)[K]) {
-    int first[K], len[K];
-    size_t rc[K], rf[K];
-#pragma unroll
-    for (int a = 0; a < K; a++) {
-        rc[a] = col ? (size_t)col[a] * (size_t)stride : 0;
-        rf[a] = col ? (size_t)col[a] * (size_t)n : 0;
-        const int b = guide_bucket(u[a], n);
-        const int lo = guide[rc[a] + b], g1 = guide[rc[a] + b + 1];
-        const int hi = g1 < n ? g1 : n;
-        first[a] = lo;
-        len[a] = hi - lo + 1;
-    }
-    bool any = true;
-    while (any) {
-        any = false;
-#pragma unroll
-        for (int a = 0; a < K; a++) {
-            if (len[a] > 0) {
-                const int half = len[a] >> 1;
-                if (cdf[rc[a] + first[a] + half] < u[a]) {
-                    first[a] += half + 1;
-                    len[a] -= half + 1;
-                } else {
-                    len[a] = half;
-                }
-            }
-            any |= len[a] > 0;
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < K; a++) {
-        int o = first[a] - 1;
-        o = o < 0 ? 0 : (o > n - 1 ? n - 1 : o);
-        const float c0 = cdf[rc[a] + o], c1 = cdf[rc[a] + o + 1];
-        const float du = (u[a] - c0) / (c1 - c0);
-        pdf[a] = func[rf[a] + o] * (col ? inv_rows[col[a]] : inv_one);
-        out[a] = (float)o + du;
-    }
-}
-#endif
-
 }  // namespace mrt

@@ -215,7 +215,7 @@ class _Light:
         self.power = 0.0
         self.samples = 1
         self.castShadows = True
-        self.fastShadows = True           # src/Light.h:16; False is rejected by libmrt (not implemented)
+        self.fastShadows = True           # src/Light.h:16; False: a point light casts no shadow (its walk never traces), rect / dome lights are rejected by libmrt
         self.noiseThreshold = 0.001
 
     def setColor(self, c): self.color = Vector3(c)

@@ -141,7 +141,7 @@ struct Light {
     float m_power = 0.f;
     int m_numSamples = 1;
     bool m_castShadows = true;
-    bool m_fastShadows = true;   // src/Light.h:16 (false: transparent shadows, rejected by the C-ABI)
+    bool m_fastShadows = true;   // src/Light.h:16 (false: a point light casts no shadow, its walk never traces; rect / dome: rejected by the C-ABI)
     float m_noiseThreshold = 0.001f;
     void setPower(float f) { m_power = f; }
     void setSamples(int n) { m_numSamples = n; }

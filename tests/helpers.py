@@ -148,8 +148,13 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
     for l in lights:
         if l["type"] == "point":
             pl = miro.PointLight(); pl.setPosition(l["pos"]); pl.setPower(l["power"])
+            fast = l.get("fast_shadows", True)
+            pl.setFastShadows(fast)
             P.addLight(pl)
-            O_.add_point_light(l["pos"], l["power"])
+            # Light::setFastShadows(false): the point light's transparent-shadow walk never
+            # traces (src/PointLight.cpp:49-70 loops while sampleHit.t < distance, from t =
+            # distance), so the oracle's light casts no shadow ray
+            O_.add_point_light(l["pos"], l["power"], cast_shadows=fast)
         elif l["type"] == "dome":
             rgb = sky(l["sky"])
             l = dict(l, sky=rgb)

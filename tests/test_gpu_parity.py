@@ -91,6 +91,22 @@ def test_lambert_and_blinn_multi_light():
         assert np.array_equal(bits(img.rgb), bits(ref["rgb"]))
 
 
+def test_point_light_transparent_shadows_match_oracle():
+    """Light::setFastShadows(false) on a point light: the reference's walk never
+    traces (src/PointLight.cpp:49-70), so the frame has no shadows; it equals the
+    oracle's bit for bit and differs from the fast-shadow frame."""
+    cfg = dict(scenes.CONFIGS["C1"], material=dict(kind="blinn", kd=(0.8, 0.5, 0.25), specExp=10.0, specAmt=0.4))
+    light = dict(type="point", pos=(2.75, 5.0, -2.75), power=40.0)
+    P, Osc, cam = scene_pair(cfg, meshes=[fixture_mesh("cornell_box")], lights=[dict(light, fast_shadows=False)])
+    img, hits = render(P, cam, 96, 64)
+    ref = Osc.render(cam, 96, 64)
+    assert np.array_equal(bits(img.rgb), bits(ref["rgb"]))
+    assert P.last_stats["shadow_rays"] == 0
+    P2, _, _ = scene_pair(cfg, meshes=[fixture_mesh("cornell_box")], lights=[light])
+    img2, _ = render(P2, cam, 96, 64)
+    assert P2.last_stats["shadow_rays"] > 0 and not np.array_equal(bits(img.rgb), bits(img2.rgb))
+
+
 def test_trace_batch_matches_oracle():
     arrs = fixture_mesh("explosion01")
     P, Osc, _ = scene_pair(scenes.CONFIGS["C1"] | {"material": dict(kind="lambert", kd=(1, 1, 1))}, meshes=[arrs])

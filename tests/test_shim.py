@@ -170,19 +170,24 @@ def test_shim_renders_c5_instances_dome_and_env_like_the_oracle(tmp_path):
 
 
 def test_shim_rejects_transparent_shadows_and_material_env_maps():
-    """Light::setFastShadows(false) and Material::setEnvMap have no C-ABI
-    implementation: the C-ABI rejects them loudly (MRT_ERR_INVALID) rather than
-    rendering fast shadows / the scene's environment silently."""
+    """Light::setFastShadows(false): a point light's transparent-shadow walk
+    (src/PointLight.cpp:49-70) never traces (it loops while sampleHit.t <
+    distance, starting at t = distance), so the C-ABI accepts it as a light that
+    casts no shadow; the rectangle / dome lights' walks have no implementation and
+    are rejected loudly (MRT_ERR_INVALID) rather than rendered with fast shadows."""
     from miro import _lib
     L = miro.lib()
     s = L.mrt_scene_create()
     try:
         l = _lib.mrt_light(0, _lib.f3((0, 1, 0)), _lib.f3((0, 0, 0)), _lib.f3((0, 0, 0)), _lib.f3((0, 0, 0)), 1.0, 1,
                            0.001, 1, -1, 1)
-        assert L.mrt_scene_add_light(s, C.byref(l)) == -1
+        assert L.mrt_scene_add_light(s, C.byref(l)) >= 0       # point light: no shadow ray, as the reference
+        r = _lib.mrt_light(1, _lib.f3((0, 0, 0)), _lib.f3((0, 2, 0)), _lib.f3((1, 2, 0)), _lib.f3((0, 2, 1)), 1.0, 1,
+                           0.001, 1, -1, 1)
+        assert L.mrt_scene_add_light(s, C.byref(r)) == -1
         assert b"transparent shadows" in L.mrt_last_error()
-        l.transparent_shadows = 0
-        assert L.mrt_scene_add_light(s, C.byref(l)) == 0
+        r.transparent_shadows = 0
+        assert L.mrt_scene_add_light(s, C.byref(r)) >= 0
     finally:
         L.mrt_scene_destroy(s)
     p = miro.PointLight()
