@@ -685,7 +685,6 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
         nxt = sel4(ch, top);
         have_next = !proxies;
     }
-#ifdef MRT_NESTED_LEAF
     while (lm) {
         const int sl = __builtin_ctz((unsigned)lm);
         lm &= lm - 1;
@@ -715,45 +714,6 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
             if (ok) { hit = true; return true; }
         }
     }
-#else
-    // the hit leaf slots' lanes in ONE flattened per-lane loop (as traverse_impl):
-    // a wave runs max over lanes of (lanes in its hit packets) iterations instead
-    // of one packet loop per slot index
-    if (lm) {
-        uint32_t v = 0, leaf = 0;
-        int k = 0, cnt = 0;
-        while (true) {
-            if (k == cnt) {
-                if (!lm) break;
-                const int sl = __builtin_ctz((unsigned)lm);
-                lm &= lm - 1;
-                v = ~(uint32_t)sel4(ch, sl);
-                leaf = v >> 4;
-                cnt = (int)(v & 3u) + 1;
-                k = 0;
-                if (COUNT) st.leaves++;
-            }
-            const int32_t pm = (v & 4u) || (CHECK && (v & 8u)) ? c.leaves[leaf].prim[k] : 0;
-            if ((v & 4u) && pm <= -2) {   // proxy lane (world packets only): a deferred instance walk
-                if (!stk_push(c, s.sp, pm)) { st.overflow = true; return true; }
-                k++;
-                continue;
-            }
-            float t, a, b;
-            bool ok;
-            if (CHECK && (v & 8u)) {   // world: alpha / motion blur; BLAS: alpha
-                ok = (s.aoff < 0 && pm >= 0 && c.pflags && (c.pflags[pm] & 1u))
-                         ? mb_tri_test(c, pm, q, tMin, tMax, t, a, b)
-                         : tri_test(c.leaves[leaf].tri[k], q, tMin, tMax, t, a, b, c.rcpT);
-                ok = ok && !alpha_rejects(c, leaf, k, a, b, s.aoff < 0 ? 0 : s.aoff);
-            } else {
-                ok = tri_test(c.leaves[leaf].tri[k], q, tMin, tMax, t, a, b, c.rcpT);
-            }
-            if (ok) { hit = true; return true; }
-            k++;
-        }
-    }
-#endif
     if (have_next) { s.cur = nxt; return false; }
     if (s.sp == 0) return true;
     s.cur = stk_pop(c, s.sp);
