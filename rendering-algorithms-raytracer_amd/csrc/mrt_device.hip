@@ -638,7 +638,9 @@ static int g_near_first = -1;     // any-hit walks take the nearest hit child fi
                                   // C5 +15%, and the fused kernels, C3 +5%, A3 / R3 +2%)
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
-static int g_chain_mb = 16384;    // chain scratch per stream (MB); larger frames run in chunks of work items
+static int g_chain_mb = 49152;    // chain scratch per stream (MB), at most 80% of the device's free memory; larger
+                                  // frames run in chunks of work items (G3: 16 GB -> 48 GB, 76.9 -> 47.2 ms per frame,
+                                  // profiles/r03_g3_chain_mb_ab.txt)
 static int g_chain_adapt = 1;     // adaptive supersampling of REC scenes: passes over the chain engine (0: fused kernel)
 static int g_fused = 1;           // one point light, one path: frame1_kernel (primary + shading in one launch)
 static int g_frame1_waves = 7;    // frame1_kernel launch-bounds occupancy target: 1 (none), 5..8 (7: -0.9% per frame with
@@ -1429,7 +1431,10 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     const uint64_t entry_bytes = 32 + 32 + 16 + 16 + 4 * (uint64_t)W + 4 * (uint64_t)split + (uint64_t)m * 33 + 1;
     const uint64_t path_bytes = mult_sum * entry_bytes + mult_max * (uint64_t)split * 65;
     const uint64_t unit_bytes = np * path_bytes + (P0.adapt_n ? 16 : 0);
-    const uint64_t budget = (uint64_t)g_chain_mb << 20;
+    uint64_t budget = (uint64_t)g_chain_mb << 20;
+    size_t mem_free = 0, mem_total = 0;   // this stream's current chunk can be reused: count it as free
+    if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess)
+        budget = std::min<uint64_t>(budget, ((uint64_t)mem_free + c.chain_bytes) / 5 * 4);
     uint64_t per = std::max<uint64_t>(1, budget / unit_bytes);
     per = std::max<uint64_t>(unit_align, per / unit_align * unit_align);
     per = std::min<uint64_t>(per, (units_max + unit_align - 1) / unit_align * unit_align);

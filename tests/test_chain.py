@@ -86,7 +86,7 @@ def both_engines(P, cam, W, H):
         tuned(chain=1)
         chain = render(P, cam, W, H)
     finally:
-        tuned(chain=1, chain_mb=16384)
+        tuned(chain=1, chain_mb=49152)
     return fused, chain
 
 
@@ -159,7 +159,7 @@ def test_chain_tree_and_adaptive_chunks_equal_one_chunk(case):
         tuned(chain_mb=2)
         many = render(P, cam, 48, 40)
     finally:
-        tuned(chain_mb=16384)
+        tuned(chain_mb=49152)
     assert_same(one, many)
 
 
@@ -183,7 +183,7 @@ def test_chain_chunks_equal_one_chunk():
         tuned(chain_mb=1)
         many = render(P, cam, 70, 50)
     finally:
-        tuned(chain_mb=16384)
+        tuned(chain_mb=49152)
     assert_same(one, many)
 
 
