@@ -49,6 +49,8 @@ NODE_B, LEAF_B = 128, 160      # QNode / DLeaf bytes (csrc/mrt_types.h)
 # frame in flight; per kernel, the SQ / TCP latency counters
 PROFILE_FILE = os.path.join(ROOT, "profiles", "r03_profile.json")
 CPU_CAL_FILE = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
+# kernel traces of the driver-settings runs (tools/step_trace.py): busy union per timed step
+STEP_TRACE_FILE = os.path.join(ROOT, "profiles", "r04_steptrace.json")
 
 
 def parse():
@@ -69,6 +71,13 @@ def parse():
                          "(weak scaling; also reported as the `weak` key of a frame-split line)")
     ap.add_argument("--strong-steps", type=int, default=0, help="N > 1: steps of the secondary (weak) measurement")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-thread-seconds for the oracle sample")
+    ap.add_argument("--share", default="",
+                    help="N = 1 only: comma list of split widths (e.g. 2,4,8); renders rank 0's bucket share of each "
+                         "N-way split alone (no gather) with --inflight streams, times the full-frame unpack, and "
+                         "prints a modeled N-GPU curve (gather modeled from --xgmi-gbs; unmeasured on hardware)")
+    ap.add_argument("--xgmi-gbs", type=float, default=50.0,
+                    help="--share model: assumed effective RCCL point-to-point rate per xGMI link and direction (GB/s)")
+    ap.add_argument("--xgmi-lat-us", type=float, default=15.0, help="--share model: assumed per-gather latency (us)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="libmrt tuning switch (mrt_set_tuning) for A/B and profiling runs; reported in the line")
     return ap.parse_args()
@@ -271,6 +280,19 @@ def _scene_setup(scene):
             "blas_prims": getattr(scene, "blas_prims", 0)}
 
 
+def step_trace_evidence(config):
+    """This config's tracked kernel trace of a driver-settings run (profiles/r04_steptrace.json,
+    tools/step_trace.py): kernel-busy union per timed step, overlap, per-step fraction."""
+    if not os.path.exists(STEP_TRACE_FILE):
+        return None
+    rec = json.load(open(STEP_TRACE_FILE)).get("configs", {}).get(config)
+    if not rec:
+        return None
+    keep = ("busy_union_ms_per_step", "ms_per_step_traced_run", "union_over_step", "kernel_sum_over_union",
+            "frac_l2_per_step", "frac_hbm_per_step", "dispatches_per_step", "command", "source")
+    return {k: rec[k] for k in keep if k in rec}
+
+
 def profile_evidence(config):
     """This config's tracked rocprofv3 record (profiles/r03_profile.json): per pass
     {hbm_bytes, avg_us, kernels}, per kernel {latency, code_object, ...}, source."""
@@ -334,17 +356,25 @@ def main():
     opts = _lib.mrt_render_opts(W, H, dev, 0, 1, 0, 0)
     camc = (_lib.mrt_camera * 1)(cam._c())
 
-    def make_pipe(nf, float_tiles):
+    depth = max(1, args.inflight)
+
+    def make_pipe(nf, float_tiles, nsplit=None, srank=None):
         """This rank's share of an nf-frame step (items id mod N), its render /
-        unpack closures and the double-buffered gather pipeline."""
+        unpack closures and the gather pipeline over `depth` buffers and streams
+        (--inflight).  nsplit / srank: the share of rank srank of an nsplit-way
+        split rendered without the gather (bench.py --share)."""
+        nsplit = world if nsplit is None else nsplit
+        srank = rank if srank is None else srank
         cams_ = [cam] if nf == 1 else [_camera(c) for c in scenes.camera_path(cfg["camera"], nf)]
         cc = (_lib.mrt_camera * nf)(*[c._c() for c in cams_])
-        mine, all_ids, per = tiles_mod.split_items(bpf * nf, world, rank)
+        mine, all_ids, per = tiles_mod.split_items(bpf * nf, nsplit, srank)
+        if nsplit != world:   # one share on its own: its unpadded items are the whole "gathered" buffer
+            all_ids = mine
         items = torch.tensor(mine, dtype=torch.int32, device="cuda")
         all_items = torch.tensor(all_ids, dtype=torch.int32, device="cuda")
-        out_f = [torch.empty(nf * H * W * 3, dtype=torch.float32, device="cuda") for _ in range(2)] if float_tiles \
-            else None
-        out_8 = [torch.empty(nf * H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        out_f = [torch.empty(nf * H * W * 3, dtype=torch.float32, device="cuda") for _ in range(depth)] \
+            if float_tiles else None
+        out_8 = [torch.empty(nf * H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(depth)]
         dt = torch.float32 if float_tiles else torch.uint8
 
         def render(ids, out, o=opts):
@@ -358,11 +388,11 @@ def main():
                                                 out_f[b].data_ptr() if float_tiles else None, out_8[b].data_ptr(),
                                                 scene.handle, torch.cuda.current_stream().cuda_stream), "unpack")
 
-        # two streams: consecutive steps' launches overlap (libmrt keeps scratch per stream)
+        # `depth` streams: consecutive steps' launches overlap (libmrt keeps scratch per stream)
         pipe = tiles_mod.BatchPipeline(world, rank, dist, items, all_items,
                                        lambda k: torch.empty(k * per * 1024 * 3, dtype=dt, device="cuda"),
-                                       render, unpack, streams=[torch.cuda.Stream(), torch.cuda.Stream()])
-        for b in range(2):   # per-stream scratch allocated before any timing
+                                       render, unpack, streams=[torch.cuda.Stream() for _ in range(depth)])
+        for b in range(depth):   # per-stream scratch allocated before any timing
             with torch.cuda.stream(pipe.streams[b]):
                 render(items, pipe.tiles[b])
         torch.cuda.synchronize()
@@ -381,6 +411,12 @@ def main():
             v = [int(x) for x in t_.tolist()]
         return st_, v
 
+    region = {}
+
+    def clocks():
+        return {"monotonic_ns": time.clock_gettime_ns(time.CLOCK_MONOTONIC),
+                "boottime_ns": time.clock_gettime_ns(time.CLOCK_BOOTTIME)}
+
     def timed(step_fn, flush, k):
         for _ in range(args.warmup):
             step_fn()
@@ -388,6 +424,7 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        c0 = clocks()
         t0_ = time.perf_counter()
         for _ in range(k):
             step_fn()
@@ -396,6 +433,11 @@ def main():
         if world > 1:
             dist.barrier()
         e = time.perf_counter() - t0_
+        c1 = clocks()
+        # the timed region on the host clocks a kernel trace may use (tools/step_trace.py
+        # selects the dispatches inside it); the first timed region is the headline's
+        if not region:
+            region.update({key: [c0[key], c1[key]] for key in c0})
         if world > 1:
             t_ = torch.tensor([e], dtype=torch.float64, device="cuda")
             dist.all_reduce(t_, op=dist.ReduceOp.MAX)
@@ -411,6 +453,9 @@ def main():
                                             frame8[i].data_ptr(), streams[i].cuda_stream), "render")
 
     adaptive = bool(cfg.get("subdivs")) and max(cfg["subdivs"][:2]) > 1
+    if args.share:
+        share_mode(args, dict(scene=scene, cfg=cfg, W=W, H=H, bpf=bpf, L=L, _lib=_lib, tiles_mod=tiles_mod, torch=torch, np=np, make_pipe=make_pipe, count_rays=count_rays, timed=timed, frame_step=frame_step, streams=streams, frame=frame, frame8=frame8, opts=opts, opts_count=opts_count, camc=camc, adaptive=adaptive, inflight=inflight), [int(x) for x in args.share.split(",") if x.strip()])
+        return
     if use_frame_path:
         # setup: every in-flight stream renders once, so libmrt's per-stream scratch
         # (hit records, stacks, counters) is allocated before the warmup / timed steps
@@ -517,6 +562,12 @@ def main():
     else:
         dom, dom_key, dom_ms, dom_b = "primary_kernel (camera rays, closest hit)", "primary", pm, b_prim
     achieved = dom_b / (dom_ms * 1e-3) / 1e9
+    # the whole step: algorithmic bytes of every pass of one step (all frames of the
+    # step on this rank) over the timed ms_per_step -- what the timed region achieved,
+    # frames in flight included (the per-launch `frac` above is one launch alone)
+    ms_step = elapsed / args.steps * 1e3
+    step_b = (dom_b if st.get("fused") or adaptive else b_prim + b_shade) * (n_frames if not split else 1)
+    step_gbs = step_b / (ms_step * 1e-3) / 1e9
     prof = profile_evidence(args.config) if use_frame_path else None
     ppass = ((prof or {}).get("passes") or {}).get(dom_key) or {}
     dom_traffic = ppass.get("hbm_bytes") or None
@@ -533,6 +584,16 @@ def main():
         f_t = dom_b / (ppass["avg_us"] * 1e-6) / 1e9 / L2_PEAK_GBS
         tracked = {"avg_us": ppass["avg_us"], "frac": round(f_t, 4), "kernels": ppass.get("kernels"),
                    "source": prof.get("source")}
+    per_step = {"algorithmic_bytes_per_step": int(step_b), "ms_per_step": round(ms_step, 4),
+                "achieved": round(step_gbs, 1), "unit": "GB/s",
+                "frac_l2": round(step_gbs / L2_PEAK_GBS, 4), "frac_hbm": round(step_gbs / HBM_PEAK_GBS, 4)}
+    frame_hbm = sum((p_ or {}).get("hbm_bytes") or 0 for p_ in ((prof or {}).get("passes") or {}).values())
+    if frame_hbm:   # PMC DRAM-side bytes of one frame (tracked profile) over the timed step
+        per_step["hbm_traffic_per_step"] = int(frame_hbm)
+        per_step["hbm_frac_counters"] = round(frame_hbm / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    st_rec = step_trace_evidence(args.config)
+    if st_rec:      # the kernel trace of this config's driver-settings run: busy union per step
+        per_step["tracked_trace"] = st_rec
     # latency evidence of the pass's longest kernel (SQ wave-state shares, VALU busy,
     # L2 requests per vector load): why neither bandwidth roofline binds
     latency = None
@@ -579,6 +640,7 @@ def main():
                      "traffic": None if dom_traffic is None else int(dom_traffic),
                      "hbm": hbm, "tracked_profile": tracked, "latency": latency, "lane_util": lane_util,
                      "launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(dom_b),
+                     "per_step": per_step,
                      "visits_per_ray": round(st["node_visits"] / max(1, (eye_mine if adaptive else px_mine)
                                                                     + shadow_mine + second_mine), 3)},
         "launch_ms": {"primary": round(pm, 4), "shade": round(sm, 4)},
@@ -591,6 +653,8 @@ def main():
                            for k in ("primary_span_us", "primary_ramp_us", "primary_tail_us",
                                      "shade_span_us", "shade_ramp_us", "shade_tail_us")},
     }
+    if region:
+        out["timed_region"] = region
     if tuning:
         out["tuning"] = tuning
     if split_times is not None:
@@ -605,6 +669,83 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def share_mode(args, E, widths):
+    """--share N1,N2,...: the strong split's per-rank work measured on ONE GPU.
+
+    The whole frame first (the N = 1 frame path with --inflight streams); then, per
+    split width N, every rank r's share of buckets (id mod N == r) rendered alone
+    through the split pipeline (render into float tiles + unpack of its own tiles,
+    --inflight buffers and streams, no gather), and rank 0's unpack of a whole
+    gathered frame.  The N-GPU step is modeled as
+        max(slowest share + rank 0's full-frame unpack, gather)
+    with gather = latency + (one rank's float tiles) / (per-link xGMI rate): rank 0
+    receives the N - 1 other shares over N - 1 point-to-point links at once, and the
+    pipeline overlaps step k's gather with step k + 1's renders.  The xGMI rate and
+    latency are ASSUMED (--xgmi-gbs, --xgmi-lat-us); nothing here ran on more than
+    one GPU."""
+    torch, np, C_ = E["torch"], E["np"], C
+    scene, L, _lib, tiles_mod = E["scene"], E["L"], E["_lib"], E["tiles_mod"]
+    W, H, bpf = E["W"], E["H"], E["bpf"]
+    for i in range(E["inflight"]):
+        _lib.check(L.mrt_render_frame_async(scene.handle, C_.byref(E["camc"][0]), C_.byref(E["opts"]),
+                                            E["frame"][i].data_ptr(), E["frame8"][i].data_ptr(),
+                                            E["streams"][i].cuda_stream), "render")
+    torch.cuda.synchronize()
+    _, (sh_full, eye_full, sec_full) = E["count_rays"](lambda: E["frame_step"](E["opts_count"], serial=True))
+    rays_full = (eye_full if E["adaptive"] else W * H) + sh_full + sec_full
+    e_full = E["timed"](E["frame_step"], lambda: None, args.steps)
+    frame_ms = e_full / args.steps * 1e3
+    out = {"metric": f"modeled strong-split curve from single-GPU share measurements [{args.config}]",
+           "config": {"workload": E["cfg"]["name"], "config": args.config, "width": W, "height": H,
+                      "buckets": bpf, "inflight": E["inflight"], "steps": args.steps, "warmup": args.warmup},
+           "frame": {"ms_per_step": round(frame_ms, 4), "mray_s": round(rays_full / (frame_ms * 1e-3) / 1e6, 1)},
+           "assumptions": {"xgmi_gbs_per_link": args.xgmi_gbs, "gather_latency_us": args.xgmi_lat_us,
+                           "note": "xGMI rate and latency assumed, not measured: this box has one GPU; every "
+                                   "other number in this line is measured on it"},
+           "shares": {}}
+    for N in widths:
+        per_rank = []
+        for r in range(N):
+            pipe, render, items, mine, _ = E["make_pipe"](1, True, nsplit=N, srank=r)
+            _, (sh, eye, sec) = E["count_rays"](lambda: render(items, pipe.tiles[0], E["opts_count"]))
+            px = sum(min(32, W - (b % ((W + 31) // 32)) * 32) * min(32, H - (b // ((W + 31) // 32)) * 32) for b in mine)
+            e = E["timed"](pipe.step, pipe.flush, args.steps)
+            ms = e / args.steps * 1e3
+            per_rank.append({"rank": r, "buckets": len(mine), "pixels": px, "ms_per_step": round(ms, 4),
+                             "rays": (eye if E["adaptive"] else px) + sh + sec})
+            del pipe
+        # rank 0's unpack of the whole gathered frame (N ranks' padded float tiles)
+        _, all_ids, per = tiles_mod.split_items(bpf, N, 0)
+        ids = torch.tensor(all_ids, dtype=torch.int32, device="cuda")
+        gathered = torch.zeros(len(all_ids) * 1024 * 3, dtype=torch.float32, device="cuda")
+        ff = torch.empty(W * H * 3, dtype=torch.float32, device="cuda")
+        f8 = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
+        un = []
+        for _ in range(7):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(all_ids), gathered.data_ptr(), None, W, H, 1,
+                                                ff.data_ptr(), f8.data_ptr(), scene.handle,
+                                                torch.cuda.current_stream().cuda_stream), "unpack")
+            e1.record()
+            torch.cuda.synchronize()
+            un.append(e0.elapsed_time(e1))
+        unpack_ms = float(np.median(un[2:]))
+        tile_bytes = per * 1024 * 3 * 4
+        gather_ms = args.xgmi_lat_us * 1e-3 + tile_bytes / (args.xgmi_gbs * 1e9) * 1e3
+        slow = max(per_rank, key=lambda x: x["ms_per_step"])
+        step_ms = max(slow["ms_per_step"] + unpack_ms, gather_ms)
+        out["shares"][str(N)] = {
+            "per_rank": per_rank, "slowest_rank_ms": slow["ms_per_step"],
+            "mean_rank_ms": round(sum(x["ms_per_step"] for x in per_rank) / N, 4),
+            "unpack_ms_rank0": round(unpack_ms, 4), "gather_bytes_per_rank": tile_bytes,
+            "gather_ms_model": round(gather_ms, 4), "step_ms_model": round(step_ms, 4),
+            "bound": "render" if slow["ms_per_step"] + unpack_ms >= gather_ms else "gather",
+            "predicted_mray_s": round(rays_full / (step_ms * 1e-3) / 1e6, 1),
+            "predicted_speedup": round(frame_ms / step_ms, 3)}
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -214,7 +214,10 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
 // light's three pre-shadow scalars live across the any-hit traversal, then the
 // material sums.  Same operations in the same order as Shader::shade.  r is the
 // camera ray, (ht, ha, hb, prim) its closest hit.
-template <bool COUNT, bool FAST>
+// POW: some Blinn material has specExp != 1 (Blinn::shade's pow, src/Blinn.cpp:220).  Scenes
+// without one run the POW = false kernels, which carry no double-precision pow: its
+// polynomial constants, hoisted out of the tile loop, took VGPRs and scratch.
+template <bool COUNT, bool FAST, bool POW>
 __device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, TravStats& st, const DRay& r, float ht,
                                          float ha, float hb, int prim, const uint16_t* rcpT, const uint16_t* rsqT,
                                          uint32_t& shadow_total) {
@@ -275,7 +278,7 @@ __device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, T
         sh = add(add(mk(0, 0, 0), mul(E, kd)), ka);
     } else {
         const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
-        const float pw = (M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
+        const float pw = (!POW || M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
         const v3 Ls = add(mk(0, 0, 0), scale(scale(mul(E, ks), M.spec_amt), pw));
         const v3 Ld = add(add(mk(0, 0, 0), mul(E, kd)), ka);
         const v3 z = mk(0, 0, 0);
@@ -297,7 +300,7 @@ __device__ __forceinline__ void write_pixel(const RenderParams& P, size_t slot, 
 
 // Kernel 2, specialised for one point light and num_paths == 1: shade1_hit of
 // every pixel's hit record (the two-launch path; frame1_kernel fuses both).
-template <bool COUNT, bool FAST, int MINW>
+template <bool COUNT, bool FAST, int MINW, bool POW>
 __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -330,7 +333,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
         if (prim >= 0) {
             const int f = item_frame(P, item);
             const EyeRay er = camera_ray(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
-            col = shade1_hit<COUNT, FAST>(P, T, st, make_ray(er.o, er.d), hv.x, hv.y, hv.z, prim, rcpT, rsqT, shadow_total);
+            col = shade1_hit<COUNT, FAST, POW>(P, T, st, make_ray(er.o, er.d), hv.x, hv.y, hv.z, prim, rcpT, rsqT, shadow_total);
         }
         item_pixel(P, item, lane, x, y, slot);
         write_pixel(P, slot, col);
@@ -344,7 +347,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
 // (the record is written only when the caller asks for hits, P.hits != null),
 // one launch tail instead of two.  Every ray's visits and every operation are
 // those of primary_kernel + shade1_kernel, so the frame is bit-identical.
-template <bool COUNT, bool FAST, int MINW>
+template <bool COUNT, bool FAST, int MINW, bool POW>
 __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -382,7 +385,7 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
             v3 col = mk(P.bg[0], P.bg[1], P.bg[2]);
             if (hit) {
                 nhits++;
-                col = shade1_hit<COUNT, FAST>(P, T, ss, r, h.t, h.a, h.b, h.prim, rcpT, rsqT, shadow_total);
+                col = shade1_hit<COUNT, FAST, POW>(P, T, ss, r, h.t, h.a, h.b, h.prim, rcpT, rsqT, shadow_total);
             }
             item_pixel(P, item, lane, x, y, slot);   // recompute: keeps it out of the traversals' live set
             if (P.hits) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
@@ -600,6 +603,7 @@ struct DeviceState {
     bool dome = false;           // a dome light (incoherent shadow rays)
     int recursive = 0;           // chain shading (Shader REC): 1 reflection / refraction, 2 + path tracing
     bool disperse = false;       // a dispersive Blinn material with secondary rays: the fused (tree) engine
+    bool pow_spec = false;       // a Blinn material with specExp != 1 (frame1 / shade1 kernels with pow)
     int wall_khz = 0;            // wall_clock64() rate
     size_t bytes = 0;
     // per-stream launch scratch: frames on different streams are in flight at once
@@ -976,17 +980,18 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     d.boxes_finite = true;
     for (const QNode& q : DN)
         for (int k = 0; k < 24; k++) d.boxes_finite &= std::isfinite(q.box[k]);
-    if (!DN.empty()) {   // union of the root's used slot boxes
-        bool any = false;
+    for (int a = 0; a < 3; a++) d.bb_lo[a] = d.bb_hi[a] = 0.f;
+    if (!DN.empty()) {   // union of the root's used slot boxes (finite values only, per axis)
+        bool any[3] = {false, false, false};
         for (int i = 0; i < 4; i++) {
             if (DN[0].child[i] == kEmptySlot) continue;
             for (int a = 0; a < 3; a++) {
                 const float lo = DN[0].box[a * 4 + i], hi = DN[0].box[12 + a * 4 + i];
                 if (!std::isfinite(lo) || !std::isfinite(hi)) continue;
-                d.bb_lo[a] = any ? std::min(d.bb_lo[a], lo) : lo;
-                d.bb_hi[a] = any ? std::max(d.bb_hi[a], hi) : hi;
+                d.bb_lo[a] = any[a] ? std::min(d.bb_lo[a], lo) : lo;
+                d.bb_hi[a] = any[a] ? std::max(d.bb_hi[a], hi) : hi;
+                any[a] = true;
             }
-            any = true;
         }
     }
     d.point_only = true;
@@ -1000,6 +1005,8 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
         if (m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f || m.gloss < 1.f || m.translucency > 0.01f)) d.recursive = 1;
     if (s.path_trace) d.recursive = 2;
     d.disperse = false;
+    d.pow_spec = false;
+    for (const DevMaterial& m : s.materials) d.pow_spec |= m.type == MRT_BLINN && m.spec_exp != 1.0f;
     for (const DevMaterial& m : s.materials)
         d.disperse |= m.type == MRT_BLINN && m.disperse && (m.reflect > 0.f || m.refract > 0.f);
     d.gthreads = (uint32_t)d.grid * kWG;
@@ -1214,33 +1221,36 @@ static KernelFn pick_primary(int w, bool c, bool f, bool inst) {
         default: return primary_fn<1>(c, f);
     }
 }
-template <int W>
+template <int W, bool POW>
 static KernelFn shade1_fn(bool c, bool f) {
-    return c ? (f ? shade1_kernel<true, true, W> : shade1_kernel<true, false, W>)
-             : (f ? shade1_kernel<false, true, W> : shade1_kernel<false, false, W>);
+    return c ? (f ? shade1_kernel<true, true, W, POW> : shade1_kernel<true, false, W, POW>)
+             : (f ? shade1_kernel<false, true, W, POW> : shade1_kernel<false, false, W, POW>);
 }
-template <int W>
+template <int W, bool POW>
 static KernelFn frame1_fn(bool c, bool f) {
-    return c ? (f ? frame1_kernel<true, true, W> : frame1_kernel<true, false, W>)
-             : (f ? frame1_kernel<false, true, W> : frame1_kernel<false, false, W>);
+    return c ? (f ? frame1_kernel<true, true, W, POW> : frame1_kernel<true, false, W, POW>)
+             : (f ? frame1_kernel<false, true, W, POW> : frame1_kernel<false, false, W, POW>);
 }
-static KernelFn pick_frame1(int w, bool c, bool f) {
+// pow: a Blinn material with specExp != 1 (those scenes run at 6 waves, or unbounded)
+static KernelFn pick_frame1(int w, bool c, bool f, bool pow) {
+    if (pow) return w == 1 ? frame1_fn<1, true>(c, f) : frame1_fn<6, true>(c, f);
     switch (w) {
-        case 1: return frame1_fn<1>(c, f);
-        case 5: return frame1_fn<5>(c, f);
-        case 7: return frame1_fn<7>(c, f);
-        case 8: return frame1_fn<8>(c, f);
-        default: return frame1_fn<6>(c, f);
+        case 1: return frame1_fn<1, false>(c, f);
+        case 5: return frame1_fn<5, false>(c, f);
+        case 7: return frame1_fn<7, false>(c, f);
+        case 8: return frame1_fn<8, false>(c, f);
+        default: return frame1_fn<6, false>(c, f);
     }
 }
-static KernelFn pick_shade1(int w, bool c, bool f) {
+static KernelFn pick_shade1(int w, bool c, bool f, bool pow) {
+    if (pow) return w == 1 ? shade1_fn<1, true>(c, f) : shade1_fn<5, true>(c, f);
     switch (w) {
-        case 1: return shade1_fn<1>(c, f);
-        case 4: return shade1_fn<4>(c, f);
-        case 5: return shade1_fn<5>(c, f);
-        case 7: return shade1_fn<7>(c, f);
-        case 8: return shade1_fn<8>(c, f);
-        default: return shade1_fn<6>(c, f);
+        case 1: return shade1_fn<1, false>(c, f);
+        case 4: return shade1_fn<4, false>(c, f);
+        case 5: return shade1_fn<5, false>(c, f);
+        case 7: return shade1_fn<7, false>(c, f);
+        case 8: return shade1_fn<8, false>(c, f);
+        default: return shade1_fn<6, false>(c, f);
     }
 }
 // bound: the resolve pass at its g_resolve_waves occupancy target (~240 VGPRs unbounded)
@@ -1620,7 +1630,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         }
         P.tile_cost = lpt ? c.tile_cost : nullptr;
         P.tile_order = lpt && c.order_tiles == P.n_tiles ? c.tile_order : nullptr;
-        if ((rc = launch(pick_frame1(g_frame1_waves, count, fb)))) return rc;
+        if ((rc = launch(pick_frame1(g_frame1_waves, count, fb, d.pow_spec)))) return rc;
         HIP_OK(hipEventRecord(c.evm, stream));
         if (lpt) {   // the next frame on this stream dequeues this frame's slowest tiles first
             hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, c.tile_cost, c.tile_order, P.n_tiles);
@@ -1647,7 +1657,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         P.units_total = (uint32_t)P.n_tiles * 64u;
         if ((rc = launch_chain(s, c, P, count, stream, (uint64_t)P.n_tiles * 64, 64))) return rc;
     } else if (one || !wave) {
-        if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb) : pick_shade(count, d.point_only, fb, inst, d.recursive)))) return rc;
+        if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb, d.pow_spec) : pick_shade(count, d.point_only, fb, inst, d.recursive)))) return rc;
     } else {
         if ((rc = ensure_rays(c, slots, (size_t)max_sh))) return rc;
         P.ray_o = c.rays;

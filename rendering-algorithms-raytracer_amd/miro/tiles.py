@@ -3,9 +3,9 @@
 Frame batches: a step may render several frames of one size (a camera path).
 Items are id = frame * buckets_per_frame + bucket, dealt id -> rank id mod N
 over the whole batch, rendered in ONE launch pair per rank
-(mrt_render_batch_async) and gathered once per step.  BatchPipeline
-double-buffers the tile buffers so the gather of step k overlaps the render of
-step k + 1.
+(mrt_render_batch_async) and gathered once per step.  BatchPipeline keeps
+`depth` tile buffers (one HIP stream each), so the gather of step k overlaps the
+renders of the next steps and several steps' launches are in flight at once.
 
 The reference renders 32x32 buckets (src/Miro.h:55) in a dynamic OpenMP loop
 (src/Scene.cpp:90-174).  Across GPUs the buckets are dealt statically,
@@ -94,32 +94,35 @@ def batch_items(buckets_per_frame: int, n_frames: int, world: int, rank: int) ->
 
 
 class BatchPipeline:
-    """Per-step render -> gather(rank 0) -> unpack, double-buffered.
+    """Per-step render -> gather(rank 0) -> unpack, over `depth` buffers.
 
     render(items, out_tiles) enqueues this rank's items into out_tiles;
-    unpack(all_items, gathered) assembles the batch on rank 0 from ONE buffer
+    unpack(all_items, gathered, b) assembles the batch on rank 0 from ONE buffer
     holding every rank's tiles in rank order (all_items is the matching
     concatenation of the ranks' item lists).  new_tiles(k) allocates k ranks'
     worth of tiles.  Both callables are injected so the same pipeline drives
     libmrt on the GPU (RCCL) and the CPU oracle in the gloo tests.
 
-    Step k writes buffer k % 2; before step k + 2 reuses it, the gather of step
-    k is waited on (work.wait() orders the compute stream after the collective
-    on nccl; it blocks on gloo).  Rank 0 unpacks step k after enqueuing the
-    render of step k + 1, so its next render is not queued behind the
-    collective.  With `streams` (two torch.cuda.Stream), everything of buffer b
-    runs on streams[b]: consecutive steps' launches overlap on the device.
-    unpack(all_items, gathered, b) gets the buffer index, so rank 0 can keep
+    Step k writes buffer k % depth; before step k + depth reuses it, the gather
+    of step k is waited on (work.wait() orders the compute stream after the
+    collective on nccl; it blocks on gloo).  Rank 0 unpacks step k after
+    enqueuing the render of step k + 1, so its next render is not queued behind
+    the collective.  With `streams` (one torch.cuda.Stream per buffer; their
+    number sets `depth`), everything of buffer b runs on streams[b]: up to
+    `depth` steps' launches are in flight on the device at once, as the N = 1
+    frame path keeps its frames in flight, so one share's launch tail overlaps
+    the next share's start.  unpack gets the buffer index, so rank 0 can keep
     one output per buffer."""
 
-    def __init__(self, world, rank, dist, items, all_items, new_tiles, render, unpack, streams=None):
+    def __init__(self, world, rank, dist, items, all_items, new_tiles, render, unpack, streams=None, depth=2):
         self.world, self.rank, self.dist = world, rank, dist
         self.items, self.all_items = items, all_items
         self.render, self.unpack = render, unpack
         self.streams = streams
-        self.tiles = [new_tiles(1), new_tiles(1)]
-        self.recv = [new_tiles(world), new_tiles(world)] if (rank == 0 and world > 1) else None
-        self.work = [None, None]
+        self.depth = len(streams) if streams else max(1, depth)
+        self.tiles = [new_tiles(1) for _ in range(self.depth)]
+        self.recv = [new_tiles(world) for _ in range(self.depth)] if (rank == 0 and world > 1) else None
+        self.work = [None] * self.depth
         self.pending = None      # (work, buffer) of the step rank 0 has not unpacked yet
         self.k = 0
 
@@ -130,7 +133,7 @@ class BatchPipeline:
         return torch.cuda.stream(self.streams[b])
 
     def step(self):
-        b = self.k & 1
+        b = self.k % self.depth
         with self._on(b):
             if self.work[b] is not None:
                 self.work[b].wait()
@@ -159,7 +162,7 @@ class BatchPipeline:
     def flush(self):
         """Finish every outstanding gather / unpack (end of the timed region)."""
         self._drain()
-        for i in range(2):
+        for i in range(self.depth):
             if self.work[i] is not None:
                 with self._on(i):
                     self.work[i].wait()

@@ -266,11 +266,12 @@ def test_libmrt_multi_process_frame_equals_single_process(tmp_path, key, world, 
     assert np.array_equal(frame.view(np.uint32), img.rgb.view(np.uint32))
 
 
-def _split_worker(rank, world, port, W, H, steps, result_path):
+def _split_worker(rank, world, port, W, H, steps, result_path, depth=2):
     """bench.py's N > 1 headline path on the CPU: ONE frame per step, its buckets
     dealt id mod N (tiles.split_items: unpadded renders, -1-padded gather layout),
-    float tiles gathered to rank 0 through BatchPipeline (double-buffered), rank 0
-    unpacks; the renderer is the oracle (the code under test is the split)."""
+    float tiles gathered to rank 0 through BatchPipeline (`depth` buffers, as
+    bench.py keeps --inflight of them), rank 0 unpacks; the renderer is the oracle
+    (the code under test is the split)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -306,7 +307,9 @@ def _split_worker(rank, world, port, W, H, steps, result_path):
             outs.append(frame)
 
         pipe = tiles.BatchPipeline(world, rank, dist, mine, all_ids,
-                                   lambda k: torch.zeros(k * per * 1024 * 3, dtype=torch.float32), render, unpack)
+                                   lambda k: torch.zeros(k * per * 1024 * 3, dtype=torch.float32), render, unpack,
+                                   depth=depth)
+        assert len(pipe.tiles) == depth
         for _ in range(steps):
             pipe.step()
         pipe.flush()
@@ -316,13 +319,15 @@ def _split_worker(rank, world, port, W, H, steps, result_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_single_frame_split_pipeline_equals_single_rank(tmp_path, world):
+@pytest.mark.parametrize("world,depth", [(2, 2), (3, 2), (2, 4)])
+def test_single_frame_split_pipeline_equals_single_rank(tmp_path, world, depth):
     """The headline N > 1 split (bench.py --split frame) reproduces the single-rank
-    frames bit for bit, step after step (ragged frame: 7 buckets over 2 / 3 ranks)."""
-    W, H, steps = 70, 40, 3
+    frames bit for bit, step after step (ragged frame: 7 buckets over 2 / 3 ranks),
+    with 2 or 4 buffers in flight (depth 4: 6 steps, so every buffer is reused)."""
+    W, H = 70, 40
+    steps = 3 if depth == 2 else 6
     path = str(tmp_path / "frames.npy")
-    mp.start_processes(_split_worker, args=(world, _free_port(), W, H, steps, path), nprocs=world,
+    mp.start_processes(_split_worker, args=(world, _free_port(), W, H, steps, path, depth), nprocs=world,
                        start_method="spawn")
     got = np.load(path)
     assert got.shape == (steps, H, W, 3)
@@ -368,8 +373,9 @@ def test_split_path_at_one_gpu_equals_frame_path(key):
     all_items = torch.tensor(all_ids, dtype=torch.int32, device="cuda")
     camc = (_lib.mrt_camera * 1)(camera(cam)._c())
     opts = _lib.mrt_render_opts(W, H, 0, 0, 1, 0, 0)
-    out_f = [torch.zeros(H * W * 3, dtype=torch.float32, device="cuda") for _ in range(2)]
-    out_8 = [torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    K = 4   # buffers / streams in flight, as bench.py --inflight
+    out_f = [torch.zeros(H * W * 3, dtype=torch.float32, device="cuda") for _ in range(K)]
+    out_8 = [torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda") for _ in range(K)]
 
     def render(ids, out):
         _lib.check(L.mrt_render_batch_async(P.handle, camc, 1, C.byref(opts), ids.data_ptr(), len(mine),
@@ -382,11 +388,11 @@ def test_split_path_at_one_gpu_equals_frame_path(key):
 
     pipe = tiles.BatchPipeline(1, 0, None, items, all_items,
                                lambda k: torch.zeros(k * per * 1024 * 3, dtype=torch.float32, device="cuda"),
-                               render, unpack, streams=[torch.cuda.Stream(), torch.cuda.Stream()])
-    for _ in range(3):
+                               render, unpack, streams=[torch.cuda.Stream() for _ in range(K)])
+    for _ in range(2 * K + 1):
         pipe.step()
     pipe.flush()
     torch.cuda.synchronize()
-    for b in range(2):
+    for b in range(K):
         assert np.array_equal(out_f[b].cpu().numpy().reshape(H, W, 3).view(np.uint32), img.rgb.view(np.uint32))
         assert np.array_equal(out_8[b].cpu().numpy().reshape(H, W, 3), img.pixels)

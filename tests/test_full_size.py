@@ -3,8 +3,10 @@ C2, C4 and C5 were only compared at reduced sizes), and the traversal-stack
 overflow path (MRT_ERR_OVERFLOW: 16 LDS + 80 HBM entries per lane).
 
 Bars: hit ids exact everywhere; float RGB bit-exact for the configs without
-libm (C2), within 1e-4 relative per channel where pow / atan2 / acos enter
-(C4 specular, C5 dome + environment), with >99% of channels bit-exact."""
+libm (C2), within north_star's 1e-4 relative per channel where pow / atan2 / acos
+enter (C4 specular, C5 dome + environment) -- |got - ref| <= 1e-4 |ref| with no
+absolute floor, so an exact zero must stay zero -- with >99% of channels
+bit-exact.  The count of channels beyond the bar is printed (0 required)."""
 import ctypes as C
 
 import numpy as np
@@ -21,9 +23,11 @@ def need_gpu():
 
 
 def close_frac(got, ref, rtol=1e-4):
-    d = np.abs(got.astype(np.float64) - ref.astype(np.float64))
-    bad = d > rtol * np.maximum(np.abs(ref.astype(np.float64)), 1e-3)
-    return bad.sum(), (bits(got) == bits(ref)).mean()
+    """Channels beyond rtol relative (north_star: 1e-4 relative per RGB channel, no floor)
+    and the share of bit-identical channels."""
+    g, r = got.astype(np.float64), ref.astype(np.float64)
+    bad = np.abs(g - r) > rtol * np.abs(r)
+    return int(bad.sum()), float((bits(got) == bits(ref)).mean())
 
 
 @pytest.mark.gpu
@@ -46,6 +50,7 @@ def test_full_size_frame_matches_oracle(key):
         assert np.array_equal(img.pixels, ref["rgb8"])
     else:
         nbad, exact = close_frac(img.rgb, ref["rgb"])
+        print(f"{key} {W}x{H}: {nbad} channels beyond 1e-4 relative, {exact:.6f} of channels bit-exact")
         assert nbad == 0 and exact > 0.99, (nbad, exact)
 
 
