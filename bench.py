@@ -195,13 +195,13 @@ def cpu_baseline(cfg_key, seconds):
                               ior3=mat.get("ior3"))
 
     m = material(cfg["material"])
-    if cfg["mesh"] == "sponza":
-        s.add_obj(scenes.sponza_obj(), m)
+    if cfg["mesh"] in ("sponza", "sponza_large"):
+        s.add_obj(scenes.mesh_obj(cfg), m)
     elif cfg["mesh"] in ("bunny", "instances"):
         if cfg["mesh"] == "bunny":
             s.add_obj(scenes.bunny_obj(), m)
         else:   # two ProxyObject BVHs, instances alternating (as scenes.build_config)
-            blas = [s.make_blas([s.add_obj(p, m)]) for p in (scenes.dragon_obj(), scenes.buddha_obj())]
+            blas = [s.make_blas([s.add_obj(p, m)]) for p in scenes.proto_objs(cfg)]
             for i, M in enumerate(scenes.instance_transforms(**cfg["instances"])):
                 s.add_instance(blas[i % 2], M)
     else:
@@ -614,9 +614,9 @@ def main():
         # --split batch: N frames per step (work per GPU fixed)
         "scaling": "strong" if (world == 1 or split) else "weak", "vs_baseline": None, "dtype": "f32",
         "data": ("synthetic (deterministic %s stand-in, %d tris; %s.obj is not in the reference snapshot%s)"
-                 % ({"sponza": "Sponza", "bunny": "bunny", "instances": "dragon_2 / buddha_smooth"}.get(
-                     cfg["mesh"], cfg["mesh"]), scene.bvh_info["prims"],
-                    {"instances": "dragon_2.obj / buddha_smooth"}.get(cfg["mesh"], cfg["mesh"]),
+                 % ({"sponza": "Sponza", "sponza_large": "Sponza (262k variant)", "bunny": "bunny",
+                     "instances": "dragon_2 / buddha_smooth"}.get(cfg["mesh"], cfg["mesh"]), scene.bvh_info["prims"],
+                    {"instances": "dragon_2.obj / buddha_smooth", "sponza_large": "sponza"}.get(cfg["mesh"], cfg["mesh"]),
                     "; Images/Arches_E_PineTree.hdr dome / environment map" if cfg.get("env") else "")),
         "config": {"workload": cfg["name"], "config": args.config, "width": W, "height": H,
                    "spp": 1 if not adaptive else f"adaptive {cfg['subdivs'][0]}..{cfg['subdivs'][1]} subdivs, "

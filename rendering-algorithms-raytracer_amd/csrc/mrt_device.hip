@@ -399,8 +399,20 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
         }
     }
     if (COUNT && lane == 0) atomicAdd(&P.ctr[CTR_WAVE_STEPS_P], wave_steps);
-    flush_stats<COUNT, true>(P, st, nhits, lane, t0, ntiles);
-    flush_stats<COUNT, false>(P, ss, shadow_total, lane, t0, ntiles);
+    // one wall-clock record per wave (the primary span counters; the wave log counts both kinds' nodes)
+    flush_stats<COUNT, true>(P, st, nhits, lane, t0, ntiles, ss.nodes);
+    flush_stats<COUNT, false, false>(P, ss, shadow_total, lane, t0, ntiles);
+    if (!COUNT && P.done) {   // the last workgroup to finish zeroes the tile counters for the next frame
+        __syncthreads();
+        if (tid == 0) {
+            __threadfence();
+            if (atomicAdd(P.done, 1u) == gridDim.x - 1) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) atomicExch(P.queue + k * 32, 0u);
+                atomicExch(P.done, 0u);
+            }
+        }
+    }
 }
 
 // Batched Scene::trace: one lane per query ray.
@@ -548,6 +560,7 @@ struct StreamCtx {
     size_t adapt_bytes = 0;
     bool last_was_render = false;
     bool fused = false;                      // the last render ran frame1_kernel (one launch)
+    bool queue_clean = false;                // the last launch left the tile counters at zero (self-reset frame1)
     bool chain_used = false;                 // the last render's shading ran the wavefront chain engine
     uint32_t* tile_cost = nullptr;           // frame1_kernel: per-tile cycles of the last frame on this stream
     uint32_t* tile_order = nullptr;          //   and the queue order derived from them
@@ -562,6 +575,14 @@ struct StreamCtx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr;
 };
 static constexpr int kMaxStreamCtx = 16;
+
+// persistent buffers of one bucket share of mrt_render over several devices
+struct ShareBuf {
+    int32_t* items = nullptr;
+    float* tiles = nullptr;
+    size_t items_cap = 0, tiles_cap = 0;
+    hipEvent_t done = nullptr;   // the share's tiles are in the caller's gather buffer
+};
 
 struct DeviceState {
     int device = -1;
@@ -611,6 +632,11 @@ struct DeviceState {
     std::vector<StreamCtx*> ctxs;
     StreamCtx* last = nullptr;   // context of the most recent launch (stats, wave log)
     std::vector<hipStream_t> share_streams;  // mrt_render over several devices: one stream per bucket share
+    std::vector<ShareBuf*> share_bufs;       //   and its persistent item / tile buffers (+ copy-done event)
+    hipStream_t gather_stream = nullptr;     //   the caller's device: frame assembly stream,
+    float* g_tiles = nullptr;                //   every share's tiles gathered here,
+    int32_t* g_items = nullptr;              //   their bucket ids
+    size_t g_tiles_cap = 0, g_items_cap = 0;
 };
 
 // Tuning knobs (mrt_set_tuning): A/B switches for performance work.
@@ -662,6 +688,8 @@ static int g_bin_dbits = 2;       // binning key: direction cells per octahedral
 static int g_bin_obits = 2;       //   origin cells per scene-box axis = 2^obits (2 dbits + 3 obits <= 12);
                                   //   sweep of 12 pairs: (2, 2) best on P4 (-18%) and C5 (-2.6%), finer
                                   //   direction cells lose (P4 (6, 0) -11%), profiles/r03_bin_sweep.txt
+static int g_self_reset = 0;      // frame1_kernel resets its own tile counters (no per-frame fill launch on the stream):
+                                  // off -- single frame -1%, but +3% per frame with 4 in flight (profiles/r04_split_node_selfreset_ab.txt)
 static int g_tile_lpt = 0;        // frame1_kernel: tile queue ordered by the previous frame's tile costs (off: -2% single-frame latency
                                   // but +10% ms/frame with 4 frames in flight, the bench mode; profiles/r03_lpt_ab.txt)
 
@@ -684,6 +712,15 @@ static void free_device(DeviceState* d) {
     (void)hipDeviceSynchronize();   // no launch may still use the scratch below
     for (StreamCtx* c : d->ctxs) free_ctx(c);
     for (hipStream_t st : d->share_streams) (void)hipStreamDestroy(st);
+    if (d->gather_stream) (void)hipStreamDestroy(d->gather_stream);
+    for (ShareBuf* b : d->share_bufs) {
+        if (b->items) (void)hipFree(b->items);
+        if (b->tiles) (void)hipFree(b->tiles);
+        if (b->done) (void)hipEventDestroy(b->done);
+        delete b;
+    }
+    if (d->g_tiles) (void)hipFree(d->g_tiles);
+    if (d->g_items) (void)hipFree(d->g_items);
     void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts, d->tables,
                     d->gamma, d->gammaF, d->d_rgb, d->d_rgb8, d->texs, d->puv, d->uvs, d->tans, d->btans,
                     d->pflags, d->verts2};
@@ -1573,13 +1610,23 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     P.cus = d.cus;
     P.scalar_nodes = g_scalar_nodes;
     P.near_first = g_near_first > 0 ? 1 : 0;
-    HIP_OK(hipMemsetAsync(c.ctr, 0, kCtrBytes, stream));
-    unsigned int* qbase = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(c.ctr) + CTR_N * sizeof(unsigned long long));
-    P.queue = qbase;
-    const size_t pad = (size_t)g_lds_pad_kb * 1024;
-    const int items = (P.n_tiles + 3) / 4;
+    const bool inst = d.special;   // instances or alpha maps: the special-leaf kernels
+    const bool adaptive = P.min_subdivs > 1 || P.max_subdivs > 1;
+    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst && !d.recursive &&
+                     !d.has_maps;
     const size_t log_stride = (size_t)d.grid * (kWG / 64) * kLogWords;
     const bool logw = count || g_wave_log;   // wave log: count mode, or timing-only on the timed kernels
+    // The fused frame kernel can leave its tile counters at zero itself (the last
+    // workgroup to finish resets them), so the next frame on this stream needs no
+    // counter-clearing fill launch in front of it; any other launch clears them.
+    const bool self_reset = !adaptive && one && g_fused && g_self_reset && !count && !logw && !g_tile_lpt;
+    if (!(self_reset && c.queue_clean)) HIP_OK(hipMemsetAsync(c.ctr, 0, kCtrBytes, stream));
+    c.queue_clean = false;
+    unsigned int* qbase = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(c.ctr) + CTR_N * sizeof(unsigned long long));
+    P.queue = qbase;
+    P.done = nullptr;
+    const size_t pad = (size_t)g_lds_pad_kb * 1024;
+    const int items = (P.n_tiles + 3) / 4;
     if (logw) HIP_OK(hipMemsetAsync(c.wave_log, 0, 2 * log_stride * sizeof(unsigned long long), stream));
     int which = 0;
     auto launch = [&](KernelFn f) -> int {
@@ -1594,9 +1641,8 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     };
     HIP_OK(hipEventRecord(c.ev0, stream));
     const bool fb = P.fast_box != 0;
-    const bool inst = d.special;   // instances or alpha maps: the special-leaf kernels
     c.chain_used = false;
-    if (P.min_subdivs > 1 || P.max_subdivs > 1) {
+    if (adaptive) {
         HIP_OK(hipEventRecord(c.evm, stream));   // primary_ms = 0: one launch
         P.refill_min = g_adapt_refill;
         if (use_chain(s) && g_chain_adapt) {     // secondary rays: passes over the chain engine
@@ -1612,11 +1658,13 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         s.last = mrt_stats{};
         return MRT_OK;
     }
-    const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst && !d.recursive &&
-                     !d.has_maps;
     c.fused = one && g_fused;
     if (c.fused) {   // one launch: camera rays, closest hits, shading, shadow rays
         if (!want_hits) P.hits = nullptr;
+        if (self_reset) {   // the frame-1 counter line of launch slot 1 (unused by this launch) counts finished workgroups
+            P.done = qbase + 8 * 32;
+            c.queue_clean = true;
+        }
         const bool lpt = g_tile_lpt && P.mode == 0 && !count && P.sched == 2;
         if (lpt && P.n_tiles > c.tile_cap) {
             HIP_OK(hipStreamSynchronize(stream));   // the previous launch may still use them
@@ -2374,30 +2422,69 @@ static mrt_hit to_hit(const Scene& S, const float4& v) {
 
 // mrt_render over several devices: bucket b of the frame's 32x32 grid
 // (src/Scene.cpp:90-95) -> share b mod n, share k rendered on devices[k] from
-// that device's scene replica (own stream), tiles copied back and scattered into
-// the caller's frame.  Each pixel is a pure function of (scene, camera, pixel,
-// seed), so the frame is bit-identical to a one-device render.
+// that device's scene replica (own stream, persistent item / tile buffers).  The
+// frame is assembled on the caller's device: every share's float tiles are
+// copied into one gather buffer there (a peer copy over xGMI from another
+// device, a device copy from the same one), the caller's stream waits for them
+// and one unpack launch scatters them into the frame (+ Image::Map 8-bit), which
+// is copied to the caller's host buffers once.  Each pixel is a pure function of
+// (scene, camera, pixel, seed), so the frame is bit-identical to a one-device
+// render.  Hit records (want_hits, debug / parity) still come back per share.
+static int ensure_buf(void*& p, size_t& cap, size_t bytes, hipStream_t sync_on) {
+    if (bytes <= cap) return MRT_OK;
+    if (p) { HIP_OK(hipStreamSynchronize(sync_on)); (void)hipFree(p); }
+    p = nullptr; cap = 0;
+    HIP_OK(hipMalloc(&p, bytes ? bytes : 16));
+    cap = bytes;
+    return MRT_OK;
+}
 static int render_shared(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts, float* rgb, uint8_t* rgb8,
                          mrt_hit* hits) {
     Scene& S = s->impl;
     const int n = opts->n_devices, W = opts->width, H = opts->height;
     const int bx = (W + 31) / 32, bpf = bx * ((H + 31) / 32);
+    const size_t tile_f = 1024 * 3;   // floats per 32x32 bucket tile
+    int rc;
+    // the caller's device: gather buffer, item list, frame, its own stream
+    if ((rc = ensure_device(S, opts->device))) return rc;
+    DeviceState& dc = *S.dev;
+    HIP_OK(hipSetDevice(dc.device));
+    if (!dc.gather_stream) HIP_OK(hipStreamCreateWithFlags(&dc.gather_stream, hipStreamNonBlocking));
+    const hipStream_t gs = dc.gather_stream;
+    const size_t px = (size_t)W * H;
+    if (px > dc.frame_px) {
+        HIP_OK(hipStreamSynchronize(gs));
+        if (dc.d_rgb) (void)hipFree(dc.d_rgb);
+        if (dc.d_rgb8) (void)hipFree(dc.d_rgb8);
+        dc.d_rgb = nullptr; dc.d_rgb8 = nullptr; dc.frame_px = 0;
+        HIP_OK(hipMalloc((void**)&dc.d_rgb, px * 12));
+        HIP_OK(hipMalloc((void**)&dc.d_rgb8, px * 3));
+        dc.frame_px = px;
+    }
+    if ((rc = ensure_buf(reinterpret_cast<void*&>(dc.g_tiles), dc.g_tiles_cap, (size_t)bpf * tile_f * sizeof(float), gs)) ||
+        (rc = ensure_buf(reinterpret_cast<void*&>(dc.g_items), dc.g_items_cap, (size_t)bpf * sizeof(int32_t), gs)))
+        return rc;
     struct Share {
         int device = -1;
         DeviceState* d = nullptr;
         hipStream_t stream = nullptr;
-        std::vector<int32_t> items;
-        int32_t* d_items = nullptr;
-        float* d_tiles = nullptr;
-        std::vector<float> tiles;
+        ShareBuf* buf = nullptr;
+        size_t first = 0, ni = 0;   // its items' offset in the gathered list
         std::vector<float4> hitrec;
     };
     std::vector<Share> sh((size_t)n);
-    int rc = MRT_OK;
+    std::vector<int32_t> all;   // the gathered item list: share 0's buckets, then share 1's, ...
+    all.reserve((size_t)bpf);
+    for (int k = 0; k < n; k++) {
+        sh[k].first = all.size();
+        for (int b = k; b < bpf; b += n) all.push_back(b);
+        sh[k].ni = all.size() - sh[k].first;
+    }
+    HIP_OK(hipMemcpyAsync(dc.g_items, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice, gs));
+    rc = MRT_OK;
     for (int k = 0; k < n && rc == MRT_OK; k++) {
         Share& q = sh[k];
         q.device = opts->devices[k];
-        for (int b = k; b < bpf; b += n) q.items.push_back(b);
         if ((rc = ensure_device(S, q.device))) break;
         q.d = S.dev;
         int slot = 0;
@@ -2409,36 +2496,65 @@ static int render_shared(mrt_scene* s, const mrt_camera* cam, const mrt_render_o
             q.d->share_streams.push_back(st);
         }
         if (rc) break;
+        while ((int)q.d->share_bufs.size() <= slot) q.d->share_bufs.push_back(new ShareBuf());
         q.stream = q.d->share_streams[slot];
-        if (q.items.empty()) continue;
-        const size_t ni = q.items.size();
-        if (hipMalloc((void**)&q.d_items, ni * sizeof(int32_t)) != hipSuccess ||
-            hipMalloc((void**)&q.d_tiles, ni * 1024 * 3 * sizeof(float)) != hipSuccess) {
-            set_error("out of device memory (bucket shares)"); rc = MRT_ERR_HIP; break;
+        q.buf = q.d->share_bufs[slot];
+        if (!q.buf->done && hipEventCreateWithFlags(&q.buf->done, hipEventDisableTiming) != hipSuccess) {
+            set_error("event"); rc = MRT_ERR_HIP; break;
         }
-        if (hipMemcpyAsync(q.d_items, q.items.data(), ni * sizeof(int32_t), hipMemcpyHostToDevice, q.stream) != hipSuccess) {
+        if (q.ni == 0) continue;
+        const size_t tb = q.ni * tile_f * sizeof(float);
+        if ((rc = ensure_buf(reinterpret_cast<void*&>(q.buf->items), q.buf->items_cap, q.ni * sizeof(int32_t), q.stream)) ||
+            (rc = ensure_buf(reinterpret_cast<void*&>(q.buf->tiles), q.buf->tiles_cap, tb, q.stream)))
+            break;
+        if (hipMemcpyAsync(q.buf->items, all.data() + q.first, q.ni * sizeof(int32_t), hipMemcpyHostToDevice, q.stream) !=
+            hipSuccess) {
             set_error("hipMemcpyAsync"); rc = MRT_ERR_HIP; break;
         }
         mrt_render_opts o = *opts;
         o.device = q.device; o.devices = nullptr; o.n_devices = 0;
         o.want_hits = hits ? 1 : 0;
-        rc = mrt_render_batch_async(s, cam, 1, &o, q.d_items, (int32_t)ni, q.d_tiles, nullptr, q.stream);
+        if ((rc = mrt_render_batch_async(s, cam, 1, &o, q.buf->items, (int32_t)q.ni, q.buf->tiles, nullptr, q.stream))) break;
+        // the share's tiles into the caller's gather buffer: over xGMI from a peer, a device copy on the same device
+        float* dst = dc.g_tiles + q.first * tile_f;
+        hipError_t e;
+        if (q.device == dc.device) {
+            e = hipMemcpyAsync(dst, q.buf->tiles, tb, hipMemcpyDeviceToDevice, q.stream);
+        } else {
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, q.device, dc.device) == hipSuccess && can) {
+                const hipError_t pe = hipDeviceEnablePeerAccess(dc.device, 0);
+                if (pe == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+            }
+            e = hipMemcpyPeerAsync(dst, dc.device, q.buf->tiles, q.device, tb, q.stream);
+        }
+        if (e != hipSuccess || hipEventRecord(q.buf->done, q.stream) != hipSuccess) {
+            set_error(std::string("share tile copy: ") + hipGetErrorString(e)); rc = MRT_ERR_HIP; break;
+        }
+    }
+    // the caller's stream: wait for every share's tiles, one unpack, one copy back
+    if (rc == MRT_OK) {
+        HIP_OK(hipSetDevice(dc.device));
+        for (Share& q : sh)
+            if (q.ni) HIP_OK(hipStreamWaitEvent(gs, q.buf->done, 0));
+        hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)(((size_t)bpf * 1024 + 255) / 256)), dim3(256), 0, gs, dc.g_items,
+                           (int32_t)bpf, dc.g_tiles, (const uint8_t*)nullptr, W, H, bx, bpf, 1, dc.d_rgb,
+                           rgb8 ? dc.d_rgb8 : nullptr, dc.gamma);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipMemcpyAsync(rgb, dc.d_rgb, px * 12, hipMemcpyDeviceToHost, gs));
+        if (rgb8) HIP_OK(hipMemcpyAsync(rgb8, dc.d_rgb8, px * 3, hipMemcpyDeviceToHost, gs));
     }
     mrt_stats total{};
     for (int k = 0; k < n && rc == MRT_OK; k++) {
         Share& q = sh[k];
-        if (q.items.empty()) continue;
-        const size_t ni = q.items.size();
+        if (q.ni == 0) continue;
         if (hipSetDevice(q.device) != hipSuccess) { set_error("hipSetDevice"); rc = MRT_ERR_HIP; break; }
-        q.tiles.resize(ni * 1024 * 3);
-        if (hipMemcpyAsync(q.tiles.data(), q.d_tiles, q.tiles.size() * sizeof(float), hipMemcpyDeviceToHost, q.stream) != hipSuccess) {
-            set_error("hipMemcpyAsync"); rc = MRT_ERR_HIP; break;
-        }
         StreamCtx* c = nullptr;
         if ((rc = get_ctx(*q.d, q.stream, c))) break;
-        if (hits) {
-            q.hitrec.resize(ni * 1024);
-            if (hipMemcpyAsync(q.hitrec.data(), c->hitbuf, ni * 1024 * sizeof(float4), hipMemcpyDeviceToHost, q.stream) != hipSuccess) {
+        if (hits) {   // debug / parity: the share's hit records to the host
+            q.hitrec.resize(q.ni * 1024);
+            if (hipMemcpyAsync(q.hitrec.data(), c->hitbuf, q.ni * 1024 * sizeof(float4), hipMemcpyDeviceToHost, q.stream) !=
+                hipSuccess) {
                 set_error("hipMemcpyAsync"); rc = MRT_ERR_HIP; break;
             }
         }
@@ -2459,27 +2575,21 @@ static int render_shared(mrt_scene* s, const mrt_camera* cam, const mrt_render_o
         total.chain = st.chain;
         total.max_stack = std::max(total.max_stack, st.max_stack);
         if (src == MRT_ERR_OVERFLOW) rc = src;
-        // scatter the share's buckets into the frame (row 0 = bottom)
-        const uint8_t* lut = host_gamma_lut();
-        for (size_t i = 0; i < ni; i++) {
-            const int b = q.items[i], x0 = (b % bx) * 32, y0 = (b / bx) * 32;
-            for (int ly = 0; ly < 32 && y0 + ly < H; ly++)
-                for (int lx = 0; lx < 32 && x0 + lx < W; lx++) {
-                    const size_t px = (size_t)(y0 + ly) * W + x0 + lx, t = i * 1024 + ly * 32 + lx;
-                    for (int ch = 0; ch < 3; ch++) {
-                        rgb[3 * px + ch] = q.tiles[3 * t + ch];
-                        if (rgb8) rgb8[3 * px + ch] = lut[map_index(q.tiles[3 * t + ch])];
-                    }
-                    if (hits) hits[px] = to_hit(S, q.hitrec[t]);
-                }
-        }
+        if (hits)
+            for (size_t i = 0; i < q.ni; i++) {
+                const int b = all[q.first + i], x0 = (b % bx) * 32, y0 = (b / bx) * 32;
+                for (int ly = 0; ly < 32 && y0 + ly < H; ly++)
+                    for (int lx = 0; lx < 32 && x0 + lx < W; lx++)
+                        hits[(size_t)(y0 + ly) * W + x0 + lx] = to_hit(S, q.hitrec[i * 1024 + ly * 32 + lx]);
+            }
     }
+    // every share and the assembly are done before the caller's buffers are returned
     for (Share& q : sh) {
         if (q.device >= 0) (void)hipSetDevice(q.device);
         if (q.stream) (void)hipStreamSynchronize(q.stream);
-        if (q.d_items) (void)hipFree(q.d_items);
-        if (q.d_tiles) (void)hipFree(q.d_tiles);
     }
+    (void)hipSetDevice(dc.device);
+    if (hipStreamSynchronize(gs) != hipSuccess && rc == MRT_OK) { set_error("frame assembly"); rc = MRT_ERR_HIP; }
     // the scene's current replica goes back to the caller's device (mrt_trace /
     // mrt_trace_async launch on S.dev->device), not the last share's
     for (DeviceState* d : S.devs)
@@ -2578,7 +2688,8 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     if (x.last_was_render && c[CTR_TP + 3]) {   // count mode: wave ramp / tail (wall clock)
         const double us = d.wall_khz > 0 ? 1e3 / d.wall_khz : 0.0;
         for (int k = 0; k < 2; k++) {
-            const unsigned long long* t = c + (k ? CTR_TS : CTR_TP);
+            // the fused frame kernel is one launch: its span is the primary record's
+            const unsigned long long* t = c + ((k && !x.fused) ? CTR_TS : CTR_TP);
             const double s0 = (double)~t[0], s1 = (double)t[1], e0 = (double)~t[2], e1 = (double)t[3];
             float* o = k ? &S.last.shade_span_us : &S.last.primary_span_us;
             o[0] = (float)((e1 - s0) * us);   // first wave start -> last wave end
@@ -2739,6 +2850,8 @@ int mrt_set_tuning(const char* key, int value) {
         g_refill_min = value;
     } else if (k == "fused") {
         g_fused = value ? 1 : 0;
+    } else if (k == "self_reset") {
+        g_self_reset = value ? 1 : 0;
     } else if (k == "tile_lpt") {
         g_tile_lpt = value ? 1 : 0;
     } else if (k == "chain_bands") {

@@ -338,11 +338,20 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
 #pragma unroll
             for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
             m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_fast(bx, r, tMin, h.t);
+            // distinct markers end the two branches, so the compiler cannot sink their
+            // identical box tests into one block fed by 24 v_mov copies of the SGPR node:
+            // this branch reads the boxes straight from SGPRs
+#ifndef MRT_MERGE_NODE   // A/B build: the merged form (v_mov copies of the SGPR node)
+            asm volatile("; mrt: scalar node" : "+v"(m));
+#endif
         } else {
             const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
             ch = reinterpret_cast<const int4*>(q)[6];
             m = FAST ? ((ANY && c.near_first) ? box_test_fast_t(q, r, tMin, h.t, tn) : box_test_fast(q, r, tMin, h.t))
                      : box_test(q, r, tMin, h.t);
+#ifndef MRT_MERGE_NODE
+            asm volatile("; mrt: vector node" : "+v"(m));
+#endif
         }
         if (COUNT) {
             st.nodes++;
@@ -546,11 +555,17 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
 #pragma unroll
         for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
         m = c.near_first ? box_test_fast_t(bx, r, tMin, tMax, tn) : box_test_fast(bx, r, tMin, tMax);
+#ifndef MRT_MERGE_NODE
+        asm volatile("; mrt: scalar node" : "+v"(m));   // see traverse_impl
+#endif
     } else {
         const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
         ch = reinterpret_cast<const int4*>(q)[6];
         m = FAST ? (c.near_first ? box_test_fast_t(q, r, tMin, tMax, tn) : box_test_fast(q, r, tMin, tMax))
                  : box_test(q, r, tMin, tMax);
+#ifndef MRT_MERGE_NODE
+        asm volatile("; mrt: vector node" : "+v"(m));
+#endif
     }
     if (COUNT) st.nodes++;
     const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;

@@ -92,6 +92,7 @@ struct RenderParams {
     int32_t cus;                 // compute units (slot of a persistent block = blockIdx / cus)
     int32_t scalar_nodes;        // scalar fetch of wave-uniform nodes
     unsigned int* queue;         // 8 tile counters, 32 words apart (sched >= 2)
+    unsigned int* done;          // frame1_kernel: finished-workgroup counter; the last one zeroes queue (null: off)
     // cost-ordered tile queue (frame1_kernel, frame mode): dequeue rank r hands
     // out tile tile_order[r] (the previous frame's slowest tiles first, so the
     // launch drains on cheap tiles); tile_cost[t] receives this frame's cycles
@@ -1075,10 +1076,13 @@ __device__ __forceinline__ void load_tables(const uint16_t* g, uint16_t* s, int 
     __syncthreads();
 }
 
-template <bool COUNT, bool PRIMARY = false>
+// TIMES: write this wave's wall-clock record (wave log, span counters).  A fused
+// kernel flushing two ray kinds writes it once, with log_nodes -- the other kind's
+// node visits -- added to the wave log's node count.
+template <bool COUNT, bool PRIMARY = false, bool TIMES = true>
 __device__ __forceinline__ void flush_stats(const RenderParams& P, const TravStats& st, uint32_t shadow, int lane,
-                                            uint64_t t0, uint32_t tiles) {
-    if ((COUNT || P.wave_log) && lane == 0) {   // ramp / tail of the persistent waves
+                                            uint64_t t0, uint32_t tiles, uint32_t log_nodes = 0) {
+    if (TIMES && (COUNT || P.wave_log) && lane == 0) {   // ramp / tail of the persistent waves
         const uint64_t t1 = wall_clock64();
         if (P.wave_log) {
             unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6));
@@ -1095,16 +1099,17 @@ __device__ __forceinline__ void flush_stats(const RenderParams& P, const TravSta
     for (int off = 32; off > 0; off >>= 1) sh += __shfl_down(sh, off);
     if (lane == 0 && sh) atomicAdd(&P.ctr[PRIMARY ? CTR_HITS : CTR_SHADOW], sh);
     if (COUNT) {
-        unsigned long long nv = st.nodes, lv = st.leaves, uv = st.uniform;
+        unsigned long long nv = st.nodes, lv = st.leaves, uv = st.uniform, xv = log_nodes;
         int msp = st.max_sp;
         for (int off = 32; off > 0; off >>= 1) {
             nv += __shfl_down(nv, off);
             lv += __shfl_down(lv, off);
             uv += __shfl_down(uv, off);
+            xv += __shfl_down(xv, off);
             msp = max(msp, __shfl_down(msp, off));
         }
         if (lane == 0) {
-            if (P.wave_log) P.wave_log[kLogWords * ((size_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6)) + 3] = nv;
+            if (TIMES && P.wave_log) P.wave_log[kLogWords * ((size_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6)) + 3] = nv + xv;
             atomicAdd(&P.ctr[CTR_NODES], nv);
             atomicAdd(&P.ctr[CTR_LEAVES], lv);
             if (PRIMARY) {

@@ -319,6 +319,13 @@ def sponza_obj():
     return _cached("sponza_standin", sponza_standin)
 
 
+def sponza_large_obj():
+    """The 262 k-triangle Sponza variant (Crytek Sponza is 262,267
+    triangles): the same atrium at detail 2.03, 261,788 triangles, a ~16 MB hierarchy
+    -- beyond one XCD's 4 MB L2."""
+    return _cached("sponza_large_standin", lambda: sponza_standin(2.03))
+
+
 def bunny_obj():
     return _cached("bunny_standin", bunny_standin)
 
@@ -333,6 +340,18 @@ def buddha_obj():
 
 def buddha_full_obj():
     return _cached("buddha_full_standin", buddha_full_standin)
+
+
+def mesh_obj(cfg):
+    """OBJ path of a single-mesh config (sponza, sponza_large, bunny)."""
+    return {"sponza": sponza_obj, "sponza_large": sponza_large_obj, "bunny": bunny_obj}[cfg["mesh"]]()
+
+
+def proto_objs(cfg):
+    """The two ProxyObject meshes of an instanced config: the dragon stand-in and the
+    buddha stand-in, at buddha_smooth.obj's size (1,087,716 triangles) when the config
+    says buddha="full"."""
+    return dragon_obj(), (buddha_full_obj() if cfg.get("buddha") == "full" else buddha_obj())
 
 
 def sky_rgb(W=512, H=256):
@@ -393,6 +412,12 @@ CONFIGS = {
                camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
                lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
                material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza"),
+    # C3L: C3 on the 262 k-triangle Sponza variant ("also a 262 k
+    # variant"; Crytek Sponza's size): its ~16 MB hierarchy does not fit one XCD's L2
+    "C3L": dict(name="sponza stand-in, 262k variant (261,788 tris) 1920x1080 Blinn+PointLight", W=1920, H=1080,
+                camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
+                lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
+                material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza_large"),
     # A3: C3 with adaptive supersampling as the Assignment 3 scenes set it
     # (m_minSubdivs = 1, m_maxSubdivs = 4, src/Assignment3.h:31-32; noise 0.01,
     # src/Scene.cpp:20): Scene::adaptiveSampleScene, 5 to 30 eye rays per pixel
@@ -438,13 +463,13 @@ CONFIGS = {
     # alternating, seeded transforms) on a floor triangle, 3840x2160, DomeLight (power
     # 0.15, 6 samples, src/main.cpp:157-165) over Images/Arches_E_PineTree.hdr, the same
     # map as environment on missed rays; Blinn with a specular lobe
-    "C5": dict(name="dragon + buddha stand-ins instanced 64x (ProxyObject) 3840x2160, DomeLight "
+    "C5": dict(name="dragon (102k tris) + buddha (1.09M tris) stand-ins instanced 64x (ProxyObject) 3840x2160, DomeLight "
                     "(Arches_E_PineTree.hdr) 6 samples + env map",
                W=3840, H=2160, camera=dict(eye=(0.0, 10.0, 27.0), lookAt=(0.0, 0.5, 0.0), up=(0, 1, 0), fov=45.0),
                lights=[dict(type="dome", sky="arches", power=0.15, samples=6, noise=0.001)],
                env=dict(sky="arches", exposure=1.0),
                material=dict(kind="blinn", kd=(0.8, 0.8, 0.8), specExp=20.0, specAmt=0.3), bg=(0.0, 0.0, 0.2),
-               mesh="instances", instances=dict(n=64, grid=8, spacing=3.2, seed=64)),
+               mesh="instances", instances=dict(n=64, grid=8, spacing=3.2, seed=64), buddha="full"),
     # D1: image-based lighting on the C2 bunny stand-in + floor: DomeLight (power
     # 0.15, 6 samples, as src/main.cpp:157-165) over Images/Arches_E_PineTree.hdr, the
     # same map as environment on missed primary rays; Blinn with a specular lobe
@@ -537,13 +562,13 @@ def build_config(key, device=0):
         npz = os.environ.get("MRT_CORNELL_NPZ", os.path.join(root, "tests", "golden", "cornell_box_mesh.npz"))
         f = np.load(npz)
         mesh.setArrays(f["verts"], f["normals"], f["vidx"], f["nidx"])
-    elif cfg["mesh"] in ("sponza", "bunny"):
-        mesh.load(sponza_obj() if cfg["mesh"] == "sponza" else bunny_obj())
+    elif cfg["mesh"] in ("sponza", "sponza_large", "bunny"):
+        mesh.load(mesh_obj(cfg))
     if cfg["mesh"] != "instances":
         miro.makeMeshObjs(scene, mesh, material)
     else:  # two ProxyObject BVHs, 64 instances alternating (src/main.cpp proxy scenes)
         protos = []
-        for path in (dragon_obj(), buddha_obj()):
+        for path in proto_objs(cfg):
             tm = miro.TriangleMesh()
             tm.load(path)
             objs, bvh = miro.Objects(), miro.BVH()

@@ -208,8 +208,8 @@ def config_scene(key, **kw):
         return scene_pair(cfg, obj=scenes.bunny_obj(), floor=True, **kw)
     if cfg["mesh"] == "instances":
         placed = [(i % 2, M) for i, M in enumerate(scenes.instance_transforms(**cfg["instances"]))]
-        return scene_pair(cfg, floor=True, instances=((scenes.dragon_obj(), scenes.buddha_obj()), placed), **kw)
-    return scene_pair(cfg, obj=scenes.sponza_obj(), **kw)
+        return scene_pair(cfg, floor=True, instances=(scenes.proto_objs(cfg), placed), **kw)
+    return scene_pair(cfg, obj=scenes.mesh_obj(cfg), **kw)
 
 
 def bits(a):

@@ -50,7 +50,7 @@ def test_c1_cornell_matches_golden():
     assert st["shadow_rays"] == meta["C1"]["shadow_rays"]
 
 
-@pytest.mark.parametrize("key,W,H", [("C2", 128, 128), ("C3", 192, 108), ("C2", 200, 75)])
+@pytest.mark.parametrize("key,W,H", [("C2", 128, 128), ("C3", 192, 108), ("C2", 200, 75), ("C3L", 192, 108)])
 def test_configs_match_oracle(key, W, H):
     P, Osc, cam = config_scene(key)
     img, hits = render(P, cam, W, H, count_visits=True)
@@ -65,9 +65,11 @@ def test_configs_match_oracle(key, W, H):
     assert P.last_stats["primary_leaf_visits"] == ref["primary_leaf_visits"]
 
 
-def test_full_hd_sponza_rows_match_oracle():
-    """Config C3 at its full 1920x1080 size; the oracle checks bands of rows."""
-    P, Osc, cam = config_scene("C3")
+@pytest.mark.parametrize("key", ["C3", "C3L"])
+def test_full_hd_sponza_rows_match_oracle(key):
+    """Configs C3 and C3L (the 262 k-triangle variant) at their full 1920x1080
+    size; the oracle checks bands of rows."""
+    P, Osc, cam = config_scene(key)
     img, hits = render(P, cam, 1920, 1080)
     for y0 in (0, 357, 540, 1063):
         ref = Osc.render(cam, 1920, 1080, rect=(0, y0, 1920, y0 + 17), threads=8)
