@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 7
+#define MRT_ABI_VERSION 8
 
 enum {
     MRT_OK = 0,
@@ -171,6 +171,12 @@ typedef struct {
      * dispersive splits, path tracing; with adaptive supersampling as passes
      * over it) rather than one fused kernel (ABI 7) */
     int32_t chain;
+    /* chain engine: the per-stream chunk budget its last frame was cut to (bytes,
+     * at most the mrt_set_tuning("chain_mb") cap, 80% of the free memory and the
+     * stream's share of 80% of the device) and the chunks it ran (ABI 8) */
+    uint64_t chain_budget_bytes;
+    uint32_t chain_chunks;
+    int32_t reserved;
 } mrt_stats;
 
 const char* mrt_last_error(void);

@@ -201,7 +201,7 @@ typedef struct {               /* ProxyObject + ProxyMatrix (src/ProxyObject.cpp
     aabb box;                  /* ProxyObject::getAABB */
 } oro_inst;
 
-#define ORO_MAX_TEX 16
+#define ORO_MAX_TEX 64
 
 struct oro_scene {
     mesh_t* meshes; int n_meshes, cap_meshes;

@@ -556,6 +556,8 @@ struct StreamCtx {
     size_t lvl_cap = 0;                      //   floats
     void* chain = nullptr;                   // wavefront chain engine scratch (mrt_chain.hip)
     size_t chain_bytes = 0;
+    uint64_t chain_budget = 0;               // the chunk budget of its last chain-engine frame (bytes)
+    uint32_t chain_chunks = 0;               //   and the chunks that frame ran
     void* adapt = nullptr;                   // chain-engine adaptive supersampling: means, pixel lists, unit colours
     size_t adapt_bytes = 0;
     bool last_was_render = false;
@@ -1480,8 +1482,18 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     const uint64_t unit_bytes = np * path_bytes + (P0.adapt_n ? 16 : 0);
     uint64_t budget = (uint64_t)g_chain_mb << 20;
     size_t mem_free = 0, mem_total = 0;   // this stream's current chunk can be reused: count it as free
-    if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess)
+    if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess) {
         budget = std::min<uint64_t>(budget, ((uint64_t)mem_free + c.chain_bytes) / 5 * 4);
+        // every stream of this scene may hold a chunk at once: each gets at most its share of 80% of the
+        // device (frames in flight on 4 streams cannot claim the whole device between them)
+        size_t live = 1;
+        {
+            std::lock_guard<std::mutex> g(d.mu);
+            live = std::max<size_t>(1, d.ctxs.size());
+        }
+        budget = std::min<uint64_t>(budget, (uint64_t)mem_total / 5 * 4 / live);
+    }
+    c.chain_budget = budget;
     uint64_t per = std::max<uint64_t>(1, budget / unit_bytes);
     per = std::max<uint64_t>(unit_align, per / unit_align * unit_align);
     per = std::min<uint64_t>(per, (units_max + unit_align - 1) / unit_align * unit_align);
@@ -1533,6 +1545,7 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     Q.nrays = c.nrays;
     Q.max_shadow = m;
     Q.n_units = (uint32_t)per;
+    c.chain_chunks += (uint32_t)((units_max + per - 1) / per);
     for (uint64_t b = 0; b < units_max; b += per) {
         Q.unit_base = (uint32_t)b;
         if ((rc = chain_chunk(s, c, Q, count, stream, ctl, queues))) return rc;
@@ -1610,6 +1623,8 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     P.cus = d.cus;
     P.scalar_nodes = g_scalar_nodes;
     P.near_first = g_near_first > 0 ? 1 : 0;
+    c.chain_chunks = 0;
+    c.chain_budget = 0;
     const bool inst = d.special;   // instances or alpha maps: the special-leaf kernels
     const bool adaptive = P.min_subdivs > 1 || P.max_subdivs > 1;
     const bool one = g_shade1 && d.point_only && P.n_lights == 1 && P.num_paths == 1 && !P.env && !inst && !d.recursive &&
@@ -2700,6 +2715,8 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     S.last.kernel_ms = ms;
     S.last.fused = x.last_was_render && x.fused ? 1 : 0;
     S.last.chain = x.last_was_render && x.chain_used ? 1 : 0;
+    S.last.chain_budget_bytes = x.chain_budget;
+    S.last.chain_chunks = x.chain_chunks;
     *out = S.last;
     if (c[CTR_OVERFLOW]) { set_error("traversal stack overflow"); return MRT_ERR_OVERFLOW; }
     return MRT_OK;

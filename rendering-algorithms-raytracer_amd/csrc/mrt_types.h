@@ -127,6 +127,6 @@ struct CamParams {
 static constexpr int kMaxLights = 8;
 static constexpr int kMaxBatch = 16;   // cameras (frames) per batched bucket launch (kernel argument)
 static constexpr int kMaxMaterials = 64;
-static constexpr int kMaxTextures = 16;
+static constexpr int kMaxTextures = 64;   // the final scene (config FS) maps 22 textures + 2 light probes
 
 }  // namespace mrt

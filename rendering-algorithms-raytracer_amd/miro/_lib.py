@@ -9,7 +9,7 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("MRT_LIB", os.path.join(_PKG, "lib", "libmrt.so"))
 
 MRT_OK = 0
-ABI_VERSION = 7   # include/mrt.h MRT_ABI_VERSION: the struct layouts below
+ABI_VERSION = 8   # include/mrt.h MRT_ABI_VERSION: the struct layouts below
 ERRORS = {-1: "MRT_ERR_INVALID", -2: "MRT_ERR_IO", -3: "MRT_ERR_HIP", -4: "MRT_ERR_BUILD",
           -5: "MRT_ERR_NOT_BUILT", -6: "MRT_ERR_OVERFLOW", -7: "MRT_ERR_NO_DEVICE"}
 
@@ -80,7 +80,8 @@ class mrt_stats(C.Structure):
                 ("primary_span_us", C.c_float), ("primary_ramp_us", C.c_float), ("primary_tail_us", C.c_float),
                 ("shade_span_us", C.c_float), ("shade_ramp_us", C.c_float), ("shade_tail_us", C.c_float),
                 ("secondary_rays", C.c_uint64), ("shadow_wave_steps", C.c_uint64), ("shadow_node_visits", C.c_uint64),
-                ("fused", C.c_int32), ("chain", C.c_int32)]
+                ("fused", C.c_int32), ("chain", C.c_int32), ("chain_budget_bytes", C.c_uint64),
+                ("chain_chunks", C.c_uint32), ("reserved", C.c_int32)]
 
 
 _fp = C.POINTER(C.c_float)

@@ -492,6 +492,20 @@ CONFIGS = {
                extra=[("sponza_light", dict(kind="blinn", kd=(1, 1, 1), emitted=1.5, le=(1, 1, 1)))],
                material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza", num_paths=16,
                path_trace=(10, False)),
+    # FS: the reference's own final scene (makeFinalScene, src/main.cpp:132-670; miro/final_scene.py):
+    # dispersive MB glass, MB cannonball, DOF, dome light + env map, alpha-mapped translucent
+    # leaves in proxies, flowers, 40,401 grass proxies, adaptive supersampling 3..5.  The
+    # published render ("20 minutes on an i7 quadcore", webpage/aguzman_jschwarzhaupt.html:147)
+    # is 1904 x 1042.
+    "FS": dict(name="makeFinalScene (src/main.cpp:132-670) 1904x1042: dispersive MB glass, DOF, dome + env, "
+                    "alpha leaves in proxies, 42k instances, adaptive 3..5",
+               W=1904, H=1042, mesh="final",
+               camera=dict(eye=(-1.277, 0.158, 2.139), lookAt=(0.294, 0.511, 0.503), up=(0, 1, 0), fov=39.0,
+                           aperture=0.0018, focusPlane=2.0, shutterSpeed=0.1),
+               lights=[dict(type="dome", sky="final_sky", power=0.15, samples=6)],
+               material=dict(kind="blinn", kd=(0.9, 0.9, 0.9), specExp=30.0, reflectAmt=1.0, refractAmt=1.0,
+                             ior3=(1.56, 1.5, 1.5), disperse=True),
+               bg=(0.0, 0.0, 0.0), subdivs=(3, 5, 0.01)),
 }
 
 
@@ -554,6 +568,10 @@ def build_config(key, device=0):
     import miro
 
     cfg = CONFIGS[key]
+    if cfg["mesh"] == "final":   # the reference's final scene, from its own description
+        from . import final_scene
+        scene, cam = final_scene.build_product(final_scene.spec(), device=device)
+        return scene, cam, cfg
     scene = miro.Scene(device=device)
     material = make_material(cfg["material"])
     mesh = miro.TriangleMesh()

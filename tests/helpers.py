@@ -196,8 +196,20 @@ def camera(c):
     return cam
 
 
+def final_scene_pair(grid=201):
+    """(miro.Scene, OracleScene, camera dict) of the reference's final scene (config FS)."""
+    from miro import final_scene
+    import final_scene as oracle_final
+    sp = final_scene.spec(grid=grid)
+    P, _ = final_scene.build_product(sp)
+    O_, cam = oracle_final.build(sp)
+    return P, O_, cam
+
+
 def config_scene(key, **kw):
     cfg = scenes.CONFIGS[key]
+    if cfg["mesh"] == "final":
+        return final_scene_pair(**kw)
     kw.setdefault("num_paths", cfg.get("num_paths", 1))
     kw.setdefault("subdivs", cfg.get("subdivs"))
     kw.setdefault("path_trace", cfg.get("path_trace"))

@@ -94,7 +94,8 @@ def test_shim_renders_c1_like_the_oracle(tmp_path, devices):
 def write_c5_spec(path):
     cfg = scenes.CONFIGS["C5"]
     c, m, dome = cfg["camera"], cfg["material"], cfg["lights"][0]
-    lines = [f"obj {scenes.dragon_obj()}", f"obj {scenes.buddha_obj()}", f"hdr {scenes.SKIES[dome['sky']]}",
+    dragon, buddha = scenes.proto_objs(cfg)   # C5's meshes (the full-size buddha stand-in)
+    lines = [f"obj {dragon}", f"obj {buddha}", f"hdr {scenes.SKIES[dome['sky']]}",
              "camera " + " ".join(repr(float(x)) for x in (*c["eye"], *c["lookAt"], *c["up"], c["fov"])),
              "material " + " ".join(repr(float(x)) for x in (*m["kd"], m["specExp"], m["specAmt"])),
              "bg " + " ".join(repr(float(x)) for x in cfg["bg"]),

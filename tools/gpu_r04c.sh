@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round 4: GPU parity suite (C3L, full-size C5, device-side share assembly), then
-# bench lines of C3 / C3L / C5 and the single-GPU share model of the 8-GPU split.
+# Round 4: GPU parity suite (C3L, full-size C5, device-side share assembly, final
+# scene), then bench lines of C3 / C3L / C5 and the single-GPU share model of the
+# 8-GPU split.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
