@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--xgmi-gbs", type=float, default=50.0,
                     help="--share model: assumed effective RCCL point-to-point rate per xGMI link and direction (GB/s)")
     ap.add_argument("--xgmi-lat-us", type=float, default=15.0, help="--share model: assumed per-gather latency (us)")
+    ap.add_argument("--size", default="", help="WxH override of the config's frame size (exploration runs only)")
+    ap.add_argument("--latency-frames", type=int, default=5,
+                    help="single frames (nothing else in flight) timed after the run for launch_ms / frame latency")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="libmrt tuning switch (mrt_set_tuning) for A/B and profiling runs; reported in the line")
     return ap.parse_args()
@@ -121,6 +124,12 @@ def spawn(args):
 
 
 # ------------------------------------------------------------------ helpers
+def progress(msg):
+    """A progress line on stderr (long configs: a GPU run that prints nothing for
+    minutes is taken to be hung)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _camera(c):
     import miro
     cam = miro.Camera()
@@ -343,7 +352,12 @@ def main():
         k, v = kv.split("=")
         _lib.check(miro.lib().mrt_set_tuning(k.encode(), int(v)), f"tuning {k}")
         tuning[k] = int(v)
+    progress(f"building {args.config}")
     scene, cam, cfg = scenes.build_config(args.config, device=dev)
+    progress(f"built: {scene.bvh_info['prims']} world objects")
+    if args.size:   # exploration only: the line's config reports the size used
+        w_, h_ = (int(x) for x in args.size.lower().split("x"))
+        cfg = dict(cfg, W=w_, H=h_, name=cfg["name"] + f" (at {w_}x{h_})")
     W, H = cfg["W"], cfg["H"]
     L = miro.lib()
     stream = torch.cuda.current_stream()
@@ -369,7 +383,7 @@ def main():
 
     depth = max(1, args.inflight)
 
-    def make_pipe(nf, float_tiles, nsplit=None, srank=None):
+    def make_pipe(nf, float_tiles, nsplit=None, srank=None, pipe_streams=None):
         """This rank's share of an nf-frame step (items id mod N), its render /
         unpack closures and the gather pipeline over `depth` buffers and streams
         (--inflight).  nsplit / srank: the share of rank srank of an nsplit-way
@@ -402,7 +416,8 @@ def main():
         # `depth` streams: consecutive steps' launches overlap (libmrt keeps scratch per stream)
         pipe = tiles_mod.BatchPipeline(world, rank, dist, items, all_items,
                                        lambda k: torch.empty(k * per * 1024 * 3, dtype=dt, device="cuda"),
-                                       render, unpack, streams=[torch.cuda.Stream() for _ in range(depth)])
+                                       render, unpack,
+                                       streams=pipe_streams or [torch.cuda.Stream() for _ in range(depth)])
         for b in range(depth):   # per-stream scratch allocated before any timing
             with torch.cuda.stream(pipe.streams[b]):
                 render(items, pipe.tiles[b])
@@ -474,8 +489,10 @@ def main():
             _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(opts), frame[i].data_ptr(),
                                                 frame8[i].data_ptr(), streams[i].cuda_stream), "render")
         torch.cuda.synchronize()
+        progress("setup frames done; instrumented frame")
         st, (shadow_total, eye_total, second_total) = count_rays(lambda: frame_step(opts_count, serial=True))
         mine, items = None, None
+        progress("timed region")
         elapsed = timed(frame_step, lambda: None, args.steps)
     else:
         pipe, render, items, mine, _ = make_pipe(n_frames, float_tiles=split)
@@ -525,7 +542,8 @@ def main():
     # per-launch durations of the uninstrumented kernels (HIP events on the
     # launch's stream), and the latency of one frame with nothing else in flight
     prim_ms, shade_ms, lat_ms = [], [], []
-    for _ in range(5):
+    progress("latency frames")
+    for _ in range(max(1, args.latency_frames)):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         if use_frame_path:
@@ -726,15 +744,36 @@ def share_mode(args, E, widths):
                            "note": "xGMI rate and latency assumed, not measured: this box has one GPU; every "
                                    "other number in this line is measured on it"},
            "shares": {}}
+    # one set of streams for every share pipeline (libmrt keeps scratch per stream, at most 16 per scene)
+    share_streams = [torch.cuda.Stream() for _ in range(max(1, args.inflight))]
     for N in widths:
         per_rank = []
         for r in range(N):
-            pipe, render, items, mine, _ = E["make_pipe"](1, True, nsplit=N, srank=r)
+            pipe, render, items, mine, _ = E["make_pipe"](1, True, nsplit=N, srank=r, pipe_streams=share_streams)
             _, (sh, eye, sec) = E["count_rays"](lambda: render(items, pipe.tiles[0], E["opts_count"]))
             px = sum(min(32, W - (b % ((W + 31) // 32)) * 32) * min(32, H - (b // ((W + 31) // 32)) * 32) for b in mine)
             e = E["timed"](pipe.step, pipe.flush, args.steps)
             ms = e / args.steps * 1e3
+            # host issue time of the same steps (the Python loop alone, before the device drains)
+            torch.cuda.synchronize()
+            t_i = time.perf_counter()
+            for _ in range(args.steps):
+                pipe.step()
+            issue_ms = (time.perf_counter() - t_i) / args.steps * 1e3
+            pipe.flush()
+            torch.cuda.synchronize()
+            # one share launch alone (HIP events, nothing else in flight)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            alone = []
+            for _ in range(5):
+                e0.record()
+                render(items, pipe.tiles[0])
+                e1.record()
+                torch.cuda.synchronize()
+                alone.append(e0.elapsed_time(e1))
             per_rank.append({"rank": r, "buckets": len(mine), "pixels": px, "ms_per_step": round(ms, 4),
+                             "host_issue_ms_per_step": round(issue_ms, 4),
+                             "launch_alone_ms": round(float(np.median(alone)), 4),
                              "rays": (eye if E["adaptive"] else px) + sh + sec})
             del pipe
         # rank 0's unpack of the whole gathered frame (N ranks' padded float tiles)

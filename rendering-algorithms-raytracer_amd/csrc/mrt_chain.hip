@@ -332,7 +332,7 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
     if ((uint32_t)blockIdx.x * (kWG / 64) >= chunks) return;   // the block has no chunks (before any barrier)
     load_tables(P.tables, s_tab, 1024);
     const int tid = threadIdx.x, lane = tid & 63;
-    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, s_tab, s_stack + tid,
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, s_tab, s_stack + tid,
            P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
@@ -602,7 +602,7 @@ __global__ void __launch_bounds__(kWG, MINW) unit_eye_kernel(RenderParams P) {
     load_tables(P.tables, s_tab, 1024);
     const uint16_t* rsqT = P.tables + 2048;
     const int tid = threadIdx.x, lane = tid & 63;
-    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, s_tab, s_stack + tid,
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, s_tab, s_stack + tid,
            P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);

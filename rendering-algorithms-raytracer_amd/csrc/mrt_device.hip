@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
     __shared__ int32_t s_stack[kLdsStack * kWG];
     load_tables(P.tables, s_tab, 1024);
     const int tid = threadIdx.x, lane = tid & 63;
-    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, s_tab, s_stack + tid,
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, s_tab, s_stack + tid,
            P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
@@ -309,7 +309,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
     TravStats st;
@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     const uint16_t* rcpT = s_tab;
     const uint16_t* rsqT = P.tables + 2048;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
     TravStats st, ss;   // primary / shadow rays (count mode)
@@ -651,7 +651,7 @@ static int g_order = 0;           // frame-mode tile dequeue order (0 bottom-up,
 static int g_prio = 0;            // wave priority heuristic for the final tiles
 static int g_decline = 0;         // tiles per CU slot (decline heuristic), 0 = off
 static int g_wave_log = 0;        // 1: timing-only wave log on uninstrumented launches (diagnostics)
-static int g_scalar_nodes = 1;    // scalar-cache fetch of wave-uniform nodes
+static int g_scalar_nodes = 3;    // scalar-cache fetch of wave-uniform nodes (bit 0) and triangles (bit 1)
 static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
 static int g_wavefront = 1;       // general shading: gen / trace / resolve kernels instead of one fused kernel
 static int g_shadow_sched = -1;   // shadow_kernel schedule: 0 grid-stride, 1 XCD bands, 2 bands + lane refill,
@@ -2815,8 +2815,9 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "shade_waves") {
         if (value != 1 && (value < 4 || value > 8)) { set_error("shade_waves must be 1 or 4..8"); return MRT_ERR_INVALID; }
         g_shade_waves = value;
-    } else if (k == "scalar_nodes") {
-        g_scalar_nodes = value ? 1 : 0;
+    } else if (k == "scalar_nodes") {   // bit 0 nodes, bit 1 triangles (1 = round 3's nodes only)
+        if (value < 0 || value > 3) { set_error("scalar_nodes must be 0..3"); return MRT_ERR_INVALID; }
+        g_scalar_nodes = value;
     } else if (k == "decline") {
         if (value < 0 || value > 1 << 20) { set_error("decline out of range"); return MRT_ERR_INVALID; }
         g_decline = value;

@@ -61,7 +61,7 @@ struct DHit {
 struct Trav {
     const QNode* __restrict__ nodes;
     bool fast_box;            // all node boxes finite and fast box test enabled
-    bool scalar_nodes;        // scalar fetch of wave-uniform nodes (tuning)
+    int scalar_nodes;         // bit 0: scalar fetch of wave-uniform nodes, bit 1: of wave-uniform triangles (tuning)
     const DLeaf* __restrict__ leaves;
     const uint16_t* rcpT;     // LDS
     int32_t* lds;             // this lane's LDS stack column (stride kWG)
@@ -276,6 +276,37 @@ __device__ __forceinline__ DRay object_ray(const DevInstance& I, const DRay& r, 
     return make_ray(o, d, r.time);
 }
 
+// Triangle k of leaf packet `leaf` (intersect4's lane), for the active lanes of a
+// traversal's flattened leaf loop.  When every active lane tests the same
+// triangle (coherent rays on one leaf: most primary and point-light shadow steps)
+// its 36 bytes come once through the scalar cache into SGPRs, not 64 times
+// through the vector path; tri_test then reads them as SGPR operands.  Distinct
+// markers end the two branches so the compiler cannot merge them (see
+// traverse_impl's node fetch).  The same test either way.
+__device__ __forceinline__ bool tri_test_lane(const Trav& c, uint32_t leaf, int k, const DRay& r, float tMin,
+                                              float tBest, float& t, float& a, float& b) {
+    int ok;
+    const uint32_t key = (leaf << 2) | (uint32_t)k;
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+    if ((c.scalar_nodes & 2) && __ballot(key != k0) == 0) {
+        typedef const __attribute__((address_space(4))) float cfloat;
+        cfloat* q = (cfloat*)(const void*)(c.leaves[k0 >> 2].tri[k0 & 3]);
+        float T[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) T[i] = q[i];
+        ok = tri_test(T, r, tMin, tBest, t, a, b, c.rcpT) ? 1 : 0;
+#ifndef MRT_MERGE_TRI
+        asm volatile("; mrt: scalar triangle" : "+v"(ok));
+#endif
+    } else {
+        ok = tri_test(c.leaves[leaf].tri[k], r, tMin, tBest, t, a, b, c.rcpT) ? 1 : 0;
+#ifndef MRT_MERGE_TRI
+        asm volatile("; mrt: vector triangle" : "+v"(ok));
+#endif
+    }
+    return ok != 0;
+}
+
 template <bool ANY, bool COUNT, bool FAST, bool INST = false, bool BL = false>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root = 0,
                               int sp0 = 0, int32_t aoff = 0);
@@ -326,7 +357,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         // 64 copies through the vector memory path.
         const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
         float tn[4] = {0.f, 0.f, 0.f, 0.f};   // slot entry distances (any-hit near-first order)
-        if (FAST && c.scalar_nodes && __ballot(cur != c0) == 0) {
+        if (FAST && (c.scalar_nodes & 1) && __ballot(cur != c0) == 0) {
             // constant address space + uniform address -> s_load_dwordx16 (node
             // data is read-only for the whole launch)
             typedef const __attribute__((address_space(4))) float cfloat;
@@ -425,7 +456,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                              : tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT);
                     ok = ok && !alpha_rejects(c, leaf, k, a, b, aoff);
                 } else {
-                    ok = tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT);
+                    ok = tri_test_lane(c, leaf, k, r, tMin, h.t, t, a, b);
                 }
                 if (ok) {
                     if (ANY) return true;
@@ -545,7 +576,7 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
     int4 ch;
     const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
     float tn[4] = {0.f, 0.f, 0.f, 0.f};
-    if (FAST && c.scalar_nodes && __ballot(cur != c0) == 0) {   // wave-uniform node: scalar fetch
+    if (FAST && (c.scalar_nodes & 1) && __ballot(cur != c0) == 0) {   // wave-uniform node: scalar fetch
         typedef const __attribute__((address_space(4))) float cfloat;
         typedef const __attribute__((address_space(4))) int32_t cint;
         cfloat* q = (cfloat*)(const void*)(c.nodes + c0);

@@ -1180,7 +1180,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
     TravStats st;
@@ -1231,7 +1231,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade_kernel(RenderParams P) {
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
     TravStats st;
@@ -1329,7 +1329,7 @@ __global__ void __launch_bounds__(kWG, MINW) adaptive_kernel(RenderParams P) {
     const uint16_t* rcpT = s_tab;
     const uint16_t* rsqT = P.tables + 2048;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes != 0, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
     TravStats st;
