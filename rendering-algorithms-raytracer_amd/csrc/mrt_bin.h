@@ -32,6 +32,16 @@ struct BinArgs {
     uint32_t m;
     float lo[3], inv[3];      // origin cell = (o - lo) * inv, clamped to [0, 2^obits)
     int dbits, obits;         // 2 * dbits + 3 * obits <= kBinBits
+    // instance-major keys (instanced scenes' shadow rays): a ray whose pixel's primary hit
+    // lies on ProxyObject instance i gets key 1 << 11 | inst_class[i] << 4 | direction cell
+    // (inst_class: instances ranked by BLAS, then index, scaled to 7 bits), so the rays a
+    // wave (and an XCD's band) traces leave the same instance and walk one BLAS first;
+    // other rays keep the direction / origin-cell key below 1 << 11.  null: plain keys.
+    const float4* hits;       // per pixel slot (ray i's pixel = i / m): t, a, b, prim bits
+    const int32_t* hit_base;  // per instance: its first hit id (ascending)
+    const uint16_t* inst_class;
+    int32_t n_inst, n_world;
+    int bits;                 // key bits (set by bin_rays)
     uint16_t* keys;           // [n] scratch
     uint32_t* hist;           // [2^bits + 1] scratch; word 2^bits receives the valid count
     uint32_t* perm;           // [n] out: valid rays, binned

@@ -56,6 +56,21 @@ __device__ __forceinline__ uint32_t bin_key(const BinArgs& A, float4 o, float4 d
     return (((iu << A.dbits) | iv) << (3 * A.obits)) | mort;
 }
 
+// instance-major key of ray i (BinArgs::hits): 1 << 11 | class << 4 | direction cell
+// (2 x 2 bits) when its pixel's primary hit is on an instance, else the plain key
+// (which stays below 1 << 11: dbits = obits = 2)
+__device__ __forceinline__ uint32_t bin_key_inst(const BinArgs& A, uint32_t i, float4 o, float4 d) {
+    const int32_t prim = __float_as_int(A.hits[i / A.m].w);
+    if (prim < A.n_world) return bin_key(A, o, d);
+    int lo = 0, hi = A.n_inst - 1;   // the last instance whose hit_base <= prim
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (A.hit_base[mid] <= prim) lo = mid; else hi = mid - 1;
+    }
+    const uint32_t dir = bin_key(A, o, d) >> (3 * A.obits);   // the direction cell
+    return (1u << 11) | ((uint32_t)A.inst_class[lo] << (2 * A.dbits)) | dir;
+}
+
 __device__ __forceinline__ bool bin_valid(const BinArgs& A, uint32_t i) {
     if (!A.nrays) return true;
     const uint32_t px = i / A.m;
@@ -64,7 +79,7 @@ __device__ __forceinline__ bool bin_valid(const BinArgs& A, uint32_t i) {
 
 __global__ void __launch_bounds__(kBinWG) bin_count_kernel(BinArgs A) {
     __shared__ uint32_t h[1 << kBinBits];
-    const int K = 1 << (2 * A.dbits + 3 * A.obits);
+    const int K = 1 << A.bits;
     for (int i = threadIdx.x; i < K; i += kBinWG) h[i] = 0;
     __syncthreads();
     uint32_t lo, hi;
@@ -72,7 +87,7 @@ __global__ void __launch_bounds__(kBinWG) bin_count_kernel(BinArgs A) {
     for (uint32_t i = lo + threadIdx.x; i < hi; i += kBinWG) {
         uint16_t k = kBinInvalid;
         if (bin_valid(A, i)) {
-            k = (uint16_t)bin_key(A, A.o[i], A.d[i]);
+            k = (uint16_t)(A.hits ? bin_key_inst(A, i, A.o[i], A.d[i]) : bin_key(A, A.o[i], A.d[i]));
             atomicAdd(&h[k], 1u);
         }
         A.keys[i] = k;
@@ -86,7 +101,7 @@ __global__ void __launch_bounds__(kBinWG) bin_count_kernel(BinArgs A) {
 // position, the scatter's cursor) and the total
 __global__ void __launch_bounds__(1024) bin_scan_kernel(BinArgs A) {
     __shared__ uint32_t part[1024];
-    const int K = 1 << (2 * A.dbits + 3 * A.obits);
+    const int K = 1 << A.bits;
     const int per = (K + 1023) / 1024, t = threadIdx.x, b0 = t * per;
     uint32_t s = 0;
     for (int j = 0; j < per; j++)
@@ -111,7 +126,7 @@ __global__ void __launch_bounds__(1024) bin_scan_kernel(BinArgs A) {
 
 __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(BinArgs A) {
     __shared__ uint32_t h[1 << kBinBits];
-    const int K = 1 << (2 * A.dbits + 3 * A.obits);
+    const int K = 1 << A.bits;
     for (int i = threadIdx.x; i < K; i += kBinWG) h[i] = 0;
     __syncthreads();
     uint32_t lo, hi;
@@ -130,8 +145,14 @@ __global__ void __launch_bounds__(kBinWG) bin_scatter_kernel(BinArgs A) {
     }
 }
 
-int bin_rays(const BinArgs& A, int grid, hipStream_t stream) {
-    const int bits = 2 * A.dbits + 3 * A.obits;
+int bin_rays(const BinArgs& A0, int grid, hipStream_t stream) {
+    BinArgs A = A0;
+    A.bits = A.hits ? kBinBits : 2 * A.dbits + 3 * A.obits;
+    if (A.hits && (A.dbits != 2 || A.obits != 2 || A.n_inst < 1 || !A.hit_base || !A.inst_class || A.m < 1)) {
+        set_error("instance-major ray-bin keys need dbits = obits = 2 and the instance tables");
+        return MRT_ERR_INVALID;
+    }
+    const int bits = A.bits;
     if (A.dbits < 0 || A.obits < 0 || bits < 1 || bits > kBinBits) { set_error("bad ray-bin key bits"); return MRT_ERR_INVALID; }
     const int K = 1 << bits;
     hipError_t e = hipMemsetAsync(A.hist, 0, (size_t)(K + 1) * sizeof(uint32_t), stream);

@@ -326,7 +326,7 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
     const uint32_t nprev = k == 1 ? chunk_units(P) * (uint32_t)P.num_paths : P.ch_cnt[k - 1];
     // binned orders (mrt_bin.h): sh_perm lists level k - 1's valid shadow-ray slots, tr_perm
     // level k's entries; a ray's answer does not depend on which lane traces it
-    const uint32_t nB = P.sh_perm ? *P.sh_perm_n : nprev * m;
+    const uint32_t nB = P.ch_skip_shadow ? 0u : (P.sh_perm ? *P.sh_perm_n : nprev * m);   // skip: their own launch
     const uint32_t chA = (nA + 63u) >> 6, chunks = chA + ((nB + 63u) >> 6);
     const uint32_t wave_id = (uint32_t)blockIdx.x * (kWG / 64) + (uint32_t)(threadIdx.x >> 6);
     if ((uint32_t)blockIdx.x * (kWG / 64) >= chunks) return;   // the block has no chunks (before any barrier)

@@ -598,6 +598,8 @@ struct DeviceState {
     DevDome* domes = nullptr;
     DevInstance* insts = nullptr;
     int n_insts = 0, n_world = 0;
+    int32_t* inst_hit_base = nullptr;   // per instance: hit_base (ascending), for the instance-major bin keys
+    uint16_t* inst_class = nullptr;     //   and its 7-bit class (BLAS-major rank)
     DevTexture* texs = nullptr;   // material-map textures (bufs hold their data)
     uint4* puv = nullptr;         // per prim texture-coordinate indices (nullptr: no texture-mapped mesh)
     float2* uvs = nullptr;
@@ -669,6 +671,7 @@ static int g_near_first = -1;     // any-hit walks take the nearest hit child fi
                                   // -12.6%; off in the refill one, C5 +4.5%, the instanced chunked one,
                                   // C5 +15%, and the fused kernels, C3 +5%, A3 / R3 +2%)
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
+static int g_chain_shadow_refill = 1;   // instanced chain levels: shadow rays on the lane-refill kernel (FS / C5-like scenes)
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
 static int g_chain_mb = 49152;    // chain scratch per stream (MB), at most 80% of the device's free memory; larger
                                   // frames run in chunks of work items (G3: 16 GB -> 48 GB, 76.9 -> 47.2 ms per frame,
@@ -685,6 +688,7 @@ static int g_bin = -1;            // ray binning (mrt_bin.h) before tracing: bit
 static int g_chain_bands = -1;    // chain_trace_kernel: XCD-banded chunk queue (binned rays: one XCD's L2 holds its share);
                                   // -1 auto: on when the level is binned (P4 -3.4%; unbinned R3 +5.7%, G3 +3%)
 static int g_dome_replay = 1;      // dome-light resolve (2c) sums 2a's recorded samples instead of sampling again
+static int g_bin_inst = 0;        // off: C5 shade pass +0.8% (profiles/r04_c5_bin_inst_primary_waves_ab.txt); instanced scenes' shadow-ray bins: instance-major keys (the ray's origin instance, BLAS-major)
 static int g_bin_blocks = 4;      // binning launches: workgroups per CU (each reserves its range of every bin atomically)
 static int g_bin_dbits = 2;       // binning key: direction cells per octahedral axis = 2^dbits
 static int g_bin_obits = 2;       //   origin cells per scene-box axis = 2^obits (2 dbits + 3 obits <= 12);
@@ -723,7 +727,8 @@ static void free_device(DeviceState* d) {
     }
     if (d->g_tiles) (void)hipFree(d->g_tiles);
     if (d->g_items) (void)hipFree(d->g_items);
-    void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts, d->tables,
+    void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts,
+                    d->inst_hit_base, d->inst_class, d->tables,
                     d->gamma, d->gammaF, d->d_rgb, d->d_rgb8, d->texs, d->puv, d->uvs, d->tans, d->btans,
                     d->pflags, d->verts2};
     for (void* p : ptrs)
@@ -942,6 +947,16 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     }
     if ((rc = upload(d.insts, DI.data(), DI.size() * sizeof(DevInstance), total))) return rc;
     d.n_insts = (int)DI.size();
+    {   // instance-major ray-bin keys (mrt_bin.h): hit bases, and instances ranked by BLAS then index
+        std::vector<int32_t> hb(DI.size());
+        std::vector<uint32_t> order(DI.size());
+        for (size_t i = 0; i < DI.size(); i++) { hb[i] = DI[i].hit_base; order[i] = (uint32_t)i; }
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return DI[a].root < DI[b].root; });
+        std::vector<uint16_t> cls(DI.size());
+        for (size_t r = 0; r < order.size(); r++) cls[order[r]] = (uint16_t)std::min<size_t>(127, r * 128 / order.size());
+        if ((rc = upload(d.inst_hit_base, hb.data(), hb.size() * sizeof(int32_t), total))) return rc;
+        if ((rc = upload(d.inst_class, cls.data(), cls.size() * sizeof(uint16_t), total))) return rc;
+    }
     d.n_world = (int)s.obj_mesh.size();
     if ((rc = upload(d.leaves, DL.data(), DL.size() * sizeof(DLeaf), total))) return rc;
     if ((rc = upload(d.prims, PS.data(), PS.size() * sizeof(PrimShade), total))) return rc;
@@ -1206,7 +1221,9 @@ static BinArgs bin_args(const DeviceState& d, const StreamCtx& c, int which, con
     A.perm = c.bin_perm + (size_t)which * c.bin_cap;
     return A;
 }
-static const uint32_t* bin_total(const BinArgs& A) { return A.hist + (size_t(1) << (2 * A.dbits + 3 * A.obits)); }
+static const uint32_t* bin_total(const BinArgs& A) {
+    return A.hist + (size_t(1) << (A.hits ? kBinBits : 2 * A.dbits + 3 * A.obits));
+}
 static int bin_grid(const DeviceState& d, size_t n) {   // fewer blocks: fewer per-bin global atomics
     return (int)std::max<size_t>(1, std::min<size_t>((size_t)d.cus * (size_t)g_bin_blocks, (n + 255) / 256));
 }
@@ -1248,6 +1265,7 @@ static KernelFn primary_fn(bool c, bool f) {
 static KernelFn pick_primary(int w, bool c, bool f, bool inst) {
     if (inst) {   // special-leaf scenes (instances: nested BLAS walks)
         switch (g_primary_inst_waves) {
+            case 4: return primary_fn<4, true>(c, f);   // 128 VGPRs: the nested instance walk without spills
             case 5: return primary_fn<5, true>(c, f);
             case 6: return primary_fn<6, true>(c, f);
             default: return primary_fn<1, true>(c, f);
@@ -1400,6 +1418,10 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
         for (int k = 0; k < L; k++) need = std::max(need, std::max(lcap_h(k), lcap_h(k) * m));
         if ((rc = ensure_bin(c, need))) return rc;
     }
+    // instanced scenes: the levels' shadow rays on the lane-refill kernel (their own launch)
+    const bool refill_sh = inst && g_chain_shadow_refill;
+    const ShadowFn ksh = refill_sh ? pick_shadow(count, Q.fast_box != 0, true, true, d.has_alpha, g_shadow_waves) : nullptr;
+    int gsh = refill_sh ? std::max(8, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(ksh), 0))) & ~7 : 0;
     auto trace = [&](int k) -> int {   // Q.ch_level == k
         if ((bm & 2) && k < L) {
             const size_t lo = Q.ch_lofs[k], cap = lcap_h(k);
@@ -1432,13 +1454,39 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
             Q.sh_perm = B.perm;
             Q.sh_perm_n = bin_total(B);
         }
-        const int r3 = go(kt, full(kt));
+        int r3 = MRT_OK;
+        if (refill_sh) {
+            // instanced scenes: level k - 1's shadow rays on the lane-refill any-hit kernel
+            // (shadow_kernel sched 2: a finished lane takes the next ray, proxy lanes deferred
+            // onto the stack), the entries' closest hits in chain_trace below.  Same rays,
+            // same answers; level 0's ray counts of units past the chunk are zeroed at its start.
+            RenderParams S = Q;
+            const size_t sbase = (size_t)Q.ch_lofs[k - 1] * m;
+            S.ray_o = Q.ray_o + sbase;
+            S.ray_d = Q.ray_d + sbase;
+            S.occl = Q.occl + sbase;
+            S.nrays = Q.nrays + Q.ch_lofs[k - 1];
+            S.sh_count = k - 1 > 0 ? Q.ch_cnt + (k - 1) : nullptr;
+            S.near_first = 0;
+            S.queue = queues + (size_t)(L + 2 + k) * 256;
+            size_t n_rays = lcap_h(k - 1) * m;
+            int sched = 2, refill = g_refill_min;
+            void* sargs[] = {&S, &n_rays, &sched, &refill};
+            r3 = MRT_OK;
+            if (hipLaunchKernel(reinterpret_cast<const void*>(ksh), dim3(gsh), dim3(kWG), sargs, 0, stream) != hipSuccess) {
+                set_error("chain shadow launch"); r3 = MRT_ERR_HIP;
+            }
+            Q.ch_skip_shadow = 1;
+        }
+        if (r3 == MRT_OK) r3 = go(kt, full(kt));
+        Q.ch_skip_shadow = 0;
         Q.tr_perm = nullptr;
         Q.sh_perm = nullptr;
         Q.sh_perm_n = nullptr;
         return r3;
     };
     HIP_OK(hipMemsetAsync(Q.ch_cnt, 0, ctl, stream));
+    if (refill_sh) HIP_OK(hipMemsetAsync(Q.nrays + Q.ch_lofs[0], 0, lcap_h(0), stream));   // level 0: only live units' counts
     Q.queue = queues;
     if (Q.uhits) {   // adaptive pass: the chunk's eye rays and their closest hits
         const KernelFn ke = pick_unit_eye(count, Q.fast_box != 0, inst);
@@ -1505,7 +1553,7 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     if ((rc = ensure_rays(c, entries, (size_t)m))) return rc;   // every level keeps its shadow rays
     // layout: ray | ior (2 per entry) | hit | val | spawn (4 per slot) | uhits (float4), rec (float),
     // map (u32), control (counts + queues), flag (u8)
-    const size_t ctl = 256 + (size_t)(L + 2) * 1024;
+    const size_t ctl = 256 + (size_t)(2 * L + 3) * 1024;   // counts; trace + resolve queues; chain shadow-launch queues
     const uint64_t n4 = 2 * entries + 2 * entries + entries + entries + 4 * spcap + (P0.adapt_n ? per : 0);
     const uint64_t bytes = n4 * 16 + entries * (uint64_t)W * 4 + entries * (uint64_t)split * 4 + ctl + spcap;
     if (bytes > c.chain_bytes) {
@@ -1756,6 +1804,13 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
             BinArgs A = bin_args(d, c, 0, P.ray_o, P.ray_d, n_rays);
             A.nrays = P.nrays;
             A.m = (uint32_t)max_sh;
+            if (g_bin_inst && d.n_insts > 0 && A.dbits == 2 && A.obits == 2) {   // instance-major keys
+                A.hits = P.hits;
+                A.hit_base = d.inst_hit_base;
+                A.inst_class = d.inst_class;
+                A.n_inst = d.n_insts;
+                A.n_world = d.n_world;
+            }
             if ((rc = bin_rays(A, bin_grid(d, n_rays), stream))) return rc;
             P.sh_perm = A.perm;
             P.sh_perm_n = bin_total(A);
@@ -2843,7 +2898,9 @@ int mrt_set_tuning(const char* key, int value) {
         if (value < -1 || value > 2) { set_error("shadow_sched must be -1..2"); return MRT_ERR_INVALID; }
         g_shadow_sched = value;
     } else if (k == "primary_inst_waves") {
-        if (value != 1 && value != 5 && value != 6) { set_error("primary_inst_waves must be 1, 5 or 6"); return MRT_ERR_INVALID; }
+        if (value != 1 && value != 4 && value != 5 && value != 6) {
+            set_error("primary_inst_waves must be 1, 4, 5 or 6"); return MRT_ERR_INVALID;
+        }
         g_primary_inst_waves = value;
     } else if (k == "resolve_waves") {
         if (value != 1 && value != 3 && value != 4) { set_error("resolve_waves must be 1, 3 or 4"); return MRT_ERR_INVALID; }
@@ -2868,6 +2925,10 @@ int mrt_set_tuning(const char* key, int value) {
         g_refill_min = value;
     } else if (k == "fused") {
         g_fused = value ? 1 : 0;
+    } else if (k == "chain_shadow_refill") {
+        g_chain_shadow_refill = value ? 1 : 0;
+    } else if (k == "bin_inst") {
+        g_bin_inst = value ? 1 : 0;
     } else if (k == "self_reset") {
         g_self_reset = value ? 1 : 0;
     } else if (k == "tile_lpt") {

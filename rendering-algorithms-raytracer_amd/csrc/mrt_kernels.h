@@ -478,6 +478,105 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
     return hit;
 }
 
+// traverse_impl<FAST = true> for plain scenes (no instances, alpha or motion
+// blur), with the stack work on wave-uniform branches: when no lane of the wave
+// is within 4 entries of the LDS column's end, every lane pushes with four
+// unconditional LDS writes (sp advancing by the slot's bit) and pops its peeked
+// top, with no per-lane branch; only a wave holding a deep lane takes the
+// per-lane path that spills to the HBM column.  The next node is the top hit
+// child or the popped entry, chosen per lane by a select.  Same node order, same
+// boxes and triangles tested with the same t as traverse_impl, so the same
+// hits and visit counts.
+template <bool ANY, bool COUNT>
+__device__ bool traverse_fast(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
+    int sp = 0;
+    int32_t cur = 0;
+    bool hit = false;
+    while (true) {
+        const int32_t peek = c.lds[(sp > 0 && sp <= kLdsStack ? sp - 1 : 0) * kWG];
+        int m;
+        int4 ch;
+        const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
+        float tn[4] = {0.f, 0.f, 0.f, 0.f};
+        if ((c.scalar_nodes & 1) && __ballot(cur != c0) == 0) {
+            typedef const __attribute__((address_space(4))) float cfloat;
+            typedef const __attribute__((address_space(4))) int32_t cint;
+            cfloat* q = (cfloat*)(const void*)(c.nodes + c0);
+            cint* qc = (cint*)(q + 24);
+            ch = make_int4(qc[0], qc[1], qc[2], qc[3]);
+            float4 bx[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
+            m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_fast(bx, r, tMin, h.t);
+            asm volatile("; mrt: scalar node (fast walk)" : "+v"(m));
+        } else {
+            const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
+            ch = reinterpret_cast<const int4*>(q)[6];
+            m = (ANY && c.near_first) ? box_test_fast_t(q, r, tMin, h.t, tn) : box_test_fast(q, r, tMin, h.t);
+            asm volatile("; mrt: vector node (fast walk)" : "+v"(m));
+        }
+        if (COUNT) {
+            st.nodes++;
+            if (__ballot(cur != c0) == 0) st.uniform++;
+        }
+        const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
+        const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
+                           (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
+        const int inner = m & isinner;
+        int lm = m & isleaf;
+        const int top = (ANY && c.near_first && inner) ? nearest_slot(inner, tn)
+                                                       : 31 - __builtin_clz((unsigned)inner | 1u);
+        const int rest = inner & ~(1 << top);   // 0 when no inner slot was hit
+        if (__ballot(sp > kLdsStack - 4) == 0) {   // every lane has room: branch-free LDS pushes
+            c.lds[sp * kWG] = ch.x; sp += rest & 1;
+            c.lds[sp * kWG] = ch.y; sp += (rest >> 1) & 1;
+            c.lds[sp * kWG] = ch.z; sp += (rest >> 2) & 1;
+            c.lds[sp * kWG] = ch.w; sp += (rest >> 3) & 1;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if ((rest >> i) & 1)
+                    if (!stk_push(c, sp, sel4(ch, i))) { st.overflow = true; return hit; }
+        }
+        if (COUNT && sp > st.max_sp) st.max_sp = sp;
+        const int32_t nxt = sel4(ch, top);
+        if (lm) {
+            uint32_t leaf = 0;
+            int k = 0, cnt = 0;
+            while (true) {
+                if (k == cnt) {
+                    if (!lm) break;
+                    const int s = __builtin_ctz((unsigned)lm);
+                    lm &= lm - 1;
+                    const uint32_t v = ~(uint32_t)sel4(ch, s);
+                    leaf = v >> 4;
+                    cnt = (int)(v & 3u) + 1;
+                    k = 0;
+                    if (COUNT) st.leaves++;
+                }
+                float t, a, b;
+                if (tri_test_lane(c, leaf, k, r, tMin, h.t, t, a, b)) {
+                    if (ANY) return true;
+                    h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
+                    hit = true;
+                }
+                k++;
+            }
+        }
+        if (!inner && sp == 0) break;   // this lane's walk is over
+        if (__ballot(sp > kLdsStack) == 0) {   // every lane's top is in LDS: the peeked entry
+            const bool pop = inner == 0;
+            cur = pop ? peek : nxt;
+            sp -= pop ? 1 : 0;
+        } else if (inner) {
+            cur = nxt;
+        } else {
+            cur = stk_pop(c, sp);
+        }
+    }
+    return hit;
+}
+
 struct NodeData {
     float4 b[6];
     int4 ch;
@@ -775,8 +874,12 @@ __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMi
 #ifdef MRT_PREFETCH  // build variant (make variant NAME=pf EXTRA=-DMRT_PREFETCH) for A/B runs
     const bool hit = (FAST && r.finite && !INST) ? traverse_pf<ANY, COUNT>(c, r, tMin, h, st)
                                                  : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
-#else
+#elif defined(MRT_TRAV_V1)   // A/B build: round 3's walk for plain scenes too
     const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
+                                        : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
+#else
+    const bool hit = (FAST && r.finite) ? (INST ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
+                                                : traverse_fast<ANY, COUNT>(c, r, tMin, h, st))
                                         : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
 #endif
     if (!ANY && hit) {

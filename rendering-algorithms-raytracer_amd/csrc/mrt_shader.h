@@ -126,6 +126,7 @@ struct RenderParams {
     uint32_t ch_spcap;           // sparse spawn slots
     int32_t ch_split;            // spawn slots per entry: 3 where dispersive splits can occur, else 1
     int32_t ch_level;            // the level a chain launch works on
+    int32_t ch_skip_shadow;      // chain_trace: the previous level's shadow rays run in a launch of their own
     int32_t ch_levels;           // levels allocated
     uint32_t ch_lofs[kMaxLevelsP1 + 1];
     // work units of the chain engine: one eye ray of a pixel.  Without a unit

@@ -12,7 +12,7 @@ from helpers import bits, camera, config_scene
 from test_chain import CASES
 
 KNOB_DEFAULTS = dict(bin=-1, bin_dbits=2, bin_obits=2, dome_replay=1, chain=1, chain_mb=49152, chain_bands=-1,
-                     shadow_sched=-1)
+                     shadow_sched=-1, bin_inst=0, primary_inst_waves=5)
 
 
 def tuned(**knobs):
@@ -72,7 +72,7 @@ def test_bin_tuning_validates_key_bits():
 def test_binned_shadow_pass_and_dome_replay_give_identical_frames(key, W, H):
     P, _, cam = config_scene(key)
     out = runs(P, cam, W, H, [dict(dome_replay=0, bin=0), dict(), dict(bin=1), dict(bin=1, bin_dbits=6, bin_obits=0),
-                              dict(bin=1, bin_dbits=0, bin_obits=4), dict(bin=1, dome_replay=0)])
+                              dict(bin=1, bin_dbits=0, bin_obits=4), dict(bin=1, dome_replay=0), dict(bin=1, bin_inst=1)])
     assert out[0][2]["shadow_rays"] > 0
     assert_all_same(out)
 
@@ -119,3 +119,12 @@ def test_chain_trace_schedules_give_identical_frames(case):
                                 dict(bin=6, chain_bands=1), dict(bin=2), dict(bin=4, chain_bands=1)])
     assert_all_same(out)
 
+
+
+@pytest.mark.gpu
+def test_instanced_primary_occupancy_targets_give_identical_frames():
+    """The instanced primary kernel at 4 (no spills), 5, 6 waves and unbounded: the
+    same nested walks, so the same frames, hit ids and ray counts."""
+    P, _, cam = config_scene("C5")
+    out = runs(P, cam, 96, 54, [dict(primary_inst_waves=w) for w in (5, 4, 6, 1)])
+    assert_all_same(out)

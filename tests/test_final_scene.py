@@ -94,3 +94,27 @@ def test_final_scene_frame_matches_oracle(W, H):
           f"{st['primary_rays'] / (W * H):.1f} eye rays/px, {st['secondary_rays']} secondary, {st['shadow_rays']} shadow")
     assert not bad.any()
     assert exact > 0.99
+
+
+@pytest.mark.gpu
+def test_final_scene_chain_shadow_schedules_give_identical_frames():
+    """The chain levels' shadow rays of an instanced scene on the lane-refill kernel
+    (chain_shadow_refill 1, deferred proxy walks) or inside chain_trace (0): the
+    same rays and answers, so the same frame, hit ids and ray counts."""
+    if miro.device_count() < 1:
+        pytest.skip("no HIP device")
+    P, _, cam = final_scene_pair()
+    L = miro.lib()
+    out = []
+    try:
+        for v in (0, 1):
+            assert L.mrt_set_tuning(b"chain_shadow_refill", v) == 0
+            img = miro.Image(); img.resize(72, 40)
+            hits = P.raytraceImage(camera(cam), img, want_hits=True)
+            out.append((img, hits, dict(P.last_stats)))
+    finally:
+        L.mrt_set_tuning(b"chain_shadow_refill", 1)
+    (a, ha, sa), (b, hb, sb) = out
+    assert np.array_equal(ha["prim"], hb["prim"])
+    assert np.array_equal(bits(a.rgb), bits(b.rgb)) and np.array_equal(a.pixels, b.pixels)
+    assert sa["shadow_rays"] == sb["shadow_rays"] and sa["secondary_rays"] == sb["secondary_rays"]
