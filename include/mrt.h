@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 8
+#define MRT_ABI_VERSION 9
 
 enum {
     MRT_OK = 0,
@@ -75,10 +75,11 @@ typedef struct {
                                 Point light: its walk (src/PointLight.cpp:49-70) starts
                                 with sampleHit.t = distance and loops while t < distance,
                                 so it never traces -- the light casts no shadow, as the
-                                reference.  Rectangle / dome lights (the walks of
-                                src/RectangleLight.cpp:93-116, src/DomeLight.cpp:123-145):
-                                not implemented, mrt_scene_add_light returns
-                                MRT_ERR_INVALID.  0 (zero-initialised) = m_fastShadows
+                                reference.  Rectangle / dome lights: the transparency
+                                walk of src/RectangleLight.cpp:93-116 / src/DomeLight.cpp:
+                                123-145 (closest-hit rays through every hit, attenuated
+                                by refractAmt at front faces; ABI 9), rendered by the
+                                fused kernels.  0 (zero-initialised) = m_fastShadows
                                 true, the reference default (ABI 7)                   */
 } mrt_light;
 
@@ -292,6 +293,11 @@ int mrt_scene_set_material_maps(mrt_scene* s, int material, const int32_t maps[6
  * that miss return the lat-long lookup x exposure instead of the background
  * (src/Scene.cpp:236-239).  texture = -1 clears. */
 int mrt_scene_set_env_map(mrt_scene* s, int32_t texture, float exposure);
+/* Material::setEnvMap + m_envExposure (src/Material.h:19,41-42; ABI 9): a Blinn
+ * material's missed reflection / refraction / path-tracing GI rays take this map
+ * x exposure instead of the scene's (Material::getEnvironmentColor,
+ * src/Material.cpp:44-64).  An RGB / HDR texture id, or -1 = the scene's. */
+int mrt_scene_set_material_env_map(mrt_scene* s, int material, int32_t texture, float exposure);
 /* Importance tables of dome light `light` (DomeLight::setTexture,
  * src/DomeLight.cpp:8-78), for inspection: cdf_u[nu+1], func_u[nu],
  * cdf_v[nu*(nv+1)], func_v[nu*nv], func_int[nu+1] (column integrals, then the u

@@ -217,6 +217,7 @@ struct oro_scene {
     float noise;                      /* Scene::m_noiseThreshold (src/Scene.cpp:20) */
     int* mesh_blas;                  /* per mesh: owning BLAS, -1 = world geometry */
     int (*maps)[6];                   /* per material: color, normal, specular, reflect, refract, alpha map (-1) */
+    int* menv; float* menv_exp;       /* per material: Material::m_envMap (-1) / m_envExposure */
     int* groups; int n_groups;        /* world objects in add order: mesh m >= 0, instance ~i */
     struct oro_scene** blas; int n_blas;   /* ProxyObject BVHs (sub-scenes sharing the meshes) */
     oro_inst* inst; int n_inst;
@@ -255,7 +256,7 @@ void oro_scene_destroy(oro_scene* s) {
         free(s->meshes[i].uv); free(s->meshes[i].tidx); free(s->meshes[i].tan); free(s->meshes[i].btan);
         free(s->meshes[i].verts2);
     }
-    free(s->maps);
+    free(s->maps); free(s->menv); free(s->menv_exp);
     for (int i = 0; i < s->n_lights; i++) ibl_dome_free(&s->domes[i]);
     for (int i = 0; i < s->n_tex; i++) free(s->tex[i].rgb);
     for (int i = 0; i < s->n_blas; i++) { free_build(s->blas[i]); free(s->blas[i]); }
@@ -269,6 +270,10 @@ int oro_scene_add_material(oro_scene* s, const oro_material* m) {
     s->mats[s->n_mats] = *m;
     s->maps = (int(*)[6])realloc(s->maps, sizeof(int[6]) * (s->n_mats + 1));
     for (int k = 0; k < 6; k++) s->maps[s->n_mats][k] = -1;
+    s->menv = (int*)realloc(s->menv, sizeof(int) * (s->n_mats + 1));
+    s->menv_exp = (float*)realloc(s->menv_exp, sizeof(float) * (s->n_mats + 1));
+    s->menv[s->n_mats] = -1;            /* Material::Material, src/Material.cpp:4 */
+    s->menv_exp[s->n_mats] = 1.0f;
     return s->n_mats++;
 }
 int oro_scene_add_light(oro_scene* s, const oro_light* l) {
@@ -338,6 +343,16 @@ int oro_image_load(const char* path, float* data, int w, int h) {
     int ww = 0, hh = 0, tt = 0;
     return tex_image_read(path, data, w, h, &ww, &hh, &tt);
 }
+/* Material::setEnvMap + m_envExposure (src/Material.h:19,41-42), read by
+ * Material::getEnvironmentColor (src/Material.cpp:44-64) */
+int oro_scene_set_material_env_map(oro_scene* s, int material, int texture, float exposure) {
+    if (material < 0 || material >= s->n_mats || texture < -1 || texture >= s->n_tex) return -1;
+    if (texture >= 0 && tex_channels(s->tex[texture].type) != 3) return -1;
+    s->menv[material] = texture;
+    s->menv_exp[material] = exposure;
+    return 0;
+}
+
 int oro_scene_set_env_map(oro_scene* s, int texture, float exposure) {
     if (texture < -1 || texture >= s->n_tex) return -1;
     s->env_tex = texture;
@@ -1376,6 +1391,44 @@ static int trace_shadow(shade_ctx* c, v3 from, v3 L, float tMax) {
     return rc > 0;
 }
 
+/* The "full method" shadow walk of Light::m_fastShadows = false for rectangle and
+ * dome lights (src/RectangleLight.cpp:93-116, src/DomeLight.cpp:123-145):
+ * closest-hit rays (IS_PRIMARY_RAY, tMin epsilon) from the shading point along
+ * L.  sampleHit lives across the loop, so each trace is bounded by the previous
+ * hit's t (the first by t0).  At a hit the attenuation takes the hit object's
+ * refractAmt when its interpolated normal (HitInfo::getInterpolatedNormal,
+ * src/Ray.cpp:51-65: the mesh normals, in object space for a proxy hit) faces
+ * the ray, and the ray restarts at o + t * L.  The walk ends at a miss, when the
+ * summed t reaches `limit` or the attenuation falls to epsilon.  Lambert
+ * materials read as refractAmt 0 (the reference leaves Material::m_refractAmt
+ * uninitialised for them).  Every trace counts as a shadow ray. */
+static const mesh_t* hit_mesh(const oro_scene* s, const hit_t* h, int* tri);
+static float transmit(shade_ctx* c, v3 from, v3 L, float t0, float limit) {
+    float att = 1.0f, done = 0.0f, tb = t0;
+    v3 o = from;
+    while (done < limit && att > 0.001f) {
+        ray_t r = make_ray_t(o, L, c->shadow_time);
+        hit_t h = {tb, 0, 0, -1, -1};
+        uint32_t nv = 0, lv = 0;
+        int rc = bvh_intersect(c->s, &r, 0.001f, &h, &nv, &lv);
+        c->shadow_rays++; c->nodes += nv; c->leaves += lv;
+        if (rc <= 0) break;
+        int t;
+        const mesh_t* m = hit_mesh(c->s, &h, &t);
+        float cc = 1.0f - h.a - h.b;
+        v3 n0 = m->normals[m->nidx[3 * t]], n1 = m->normals[m->nidx[3 * t + 1]], n2 = m->normals[m->nidx[3 * t + 2]];
+        v3 hitN = vnormalized(vadd(vadd(vscale(n0, cc), vscale(n1, h.a)), vscale(n2, h.b)));
+        if ((double)vdot(hitN, vneg(L)) > 0.0) {
+            const oro_material* hm = &c->s->mats[m->material];
+            att *= hm->type == ORO_BLINN ? hm->refract : 0.0f;
+        }
+        o = vadd(o, vscale(L, h.t));
+        tb = h.t;
+        done += h.t;
+    }
+    return att;
+}
+
 /* PointLight::sampleLight, src/PointLight.cpp:8-81 (fast shadows; the shadow ray
  * is a closest-hit ray because of the IS_SHADOW_RAY/giBounces slot mix-up at :43,
  * which does not change the occlusion boolean). */
@@ -1413,7 +1466,7 @@ static float rect_power(const oro_light* l) {
     return l->power * surfAreaRecip;
 }
 
-/* RectangleLight::sampleLight, src/RectangleLight.cpp:42-136 (fast shadows). */
+/* RectangleLight::sampleLight, src/RectangleLight.cpp:42-136 (fast or transparent shadows). */
 static v3 rect_light(shade_ctx* c, const oro_light* l, int li, v3 from, v3 normal, v3 rVec, float* outSpec) {
     v3 v1 = V(l->v1[0], l->v1[1], l->v1[2]), v2 = V(l->v2[0], l->v2[1], l->v2[2]), v3_ = V(l->v3[0], l->v3[1], l->v3[2]);
     float power = rect_power(l);
@@ -1434,7 +1487,10 @@ static v3 rect_light(shade_ctx* c, const oro_light* l, int li, v3 from, v3 norma
             float distance = rcp_nr(distanceRecip);
             randDir = vscale(randDir, distanceRecip);
             nDotL *= distanceRecip;
-            if (l->castShadows) {
+            if (l->castShadows && l->transparent) {
+                attenuate = transmit(c, from, randDir, distance - 0.001f, distance);
+                if (attenuate == 0.0f) c->shadow_mask |= 1u << (li & 31);
+            } else if (l->castShadows) {
                 if (trace_shadow(c, from, randDir, distance - 0.001f)) { attenuate = 0.0f; c->shadow_mask |= 1u << (li & 31); }
             }
         } else {
@@ -1485,7 +1541,12 @@ static v3 dome_light(shade_ctx* c, const oro_light* l, int li, v3 from, v3 norma
         float img[3];
         ibl_lookup_dir(tex, direction.x, direction.y, direction.z, img);
         float attenuate = 1.0f;
-        if (trace_shadow(c, from, direction, 1e12f)) { attenuate = 0.0f; c->shadow_mask |= 1u << (li & 31); }
+        if (l->transparent) {
+            attenuate = transmit(c, from, direction, 1e12f, 1e12f);   /* sampleHit.t = MIRO_TMAX */
+            if (attenuate == 0.0f) c->shadow_mask |= 1u << (li & 31);
+        } else if (trace_shadow(c, from, direction, 1e12f)) {
+            attenuate = 0.0f; c->shadow_mask |= 1u << (li & 31);
+        }
         float inv = 1.0f / pdf;   /* E = m_Gain * imageSample / pdf (Vector3::operator/) */
         v3 E = V((img[0] * l->power) * inv, (img[1] * l->power) * inv, (img[2] * l->power) * inv);
         samplesDone++;
@@ -1619,8 +1680,16 @@ static v3 cosine_sample(shade_ctx* c, v3 N) {
     return vnormalized(vadd(vadd(vscale(u, cs * sqrte2), vscale(v, sn * sqrte2)), vscale(N, sqrt1_e2)));
 }
 
-/* Material::getEnvironmentColor, src/Material.cpp:44-62 (scene map or background) */
-static v3 env_color(const oro_scene* s, v3 d) {
+/* Material::getEnvironmentColor, src/Material.cpp:44-64: the material's own map
+ * (m_envMap x m_envExposure), else the scene's, else the background */
+static v3 env_color(const oro_scene* s, const oro_material* mat, v3 d) {
+    const int mi = (int)(mat - s->mats);
+    if (s->menv[mi] >= 0) {
+        float e[3];
+        const float x = s->menv_exp[mi];
+        ibl_lookup_dir(&s->tex[s->menv[mi]], d.x, d.y, d.z, e);
+        return V(e[0] * x, e[1] * x, e[2] * x);
+    }
     if (s->env_tex >= 0) {
         float e[3];
         ibl_lookup_dir(&s->tex[s->env_tex], d.x, d.y, d.z, e);
@@ -1666,7 +1735,7 @@ static v3 path_trace(shade_ctx* c, const oro_material* mat, v3 P, v3 theNormal, 
             chain_t cc = {ch.bounces, ch.gi + 1, 1, ch.level + 1, 0, ch.branch};   /* IS_PRIMARY_RAY */
             out = vadd(out, vmul(kd, shade_child(c, &gr, &nh, &child, cc)));
         } else if (mat->sample_env && s->sample_env) {
-            out = vadd(out, vmul(kd, env_color(s, randD)));
+            out = vadd(out, vmul(kd, env_color(s, mat, randD)));
         }
     } else {
         for (int i = 0; i < s->n_lights; i++) {
@@ -1779,7 +1848,7 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
                     doEnv = 0;
                 }
             }
-            if (reflectAmt * Rs > 0.0f && doEnv) Lr = vadd(Lr, vmul(ks, env_color(c->s, rVec)));
+            if (reflectAmt * Rs > 0.0f && doEnv) Lr = vadd(Lr, vmul(ks, env_color(c->s, mat, rVec)));
         } else if (refractAmt * Ts > 0.0f && disp) {
             /* dispersion (src/Blinn.cpp:275-301): one refraction ray per colour
              * channel i through m_ior[i]; each child's colour is masked to its
@@ -1808,7 +1877,7 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
                     }
                 }
             }
-            if (doEnv) Lt = vadd(Lt, vmul(ks, env_color(c->s, tVec)));
+            if (doEnv) Lt = vadd(Lt, vmul(ks, env_color(c->s, mat, tVec)));
         } else if (refractAmt * Ts > 0.0f) {
             float snellsQ = inIOR / outIOR[0];
             float sqrtPart = std_max(0.0f, sqrtf(1.0f - (snellsQ * snellsQ) * (1.0f - vDotN * vDotN)));
@@ -1826,7 +1895,7 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
                     doEnv = 0;
                 }
             }
-            if (doEnv) Lt = vadd(Lt, vmul(ks, env_color(c->s, tVec)));
+            if (doEnv) Lt = vadd(Lt, vmul(ks, env_color(c->s, mat, tVec)));
         }
     }
     Ld = vadd(Ld, V(mat->ka[0], mat->ka[1], mat->ka[2]));

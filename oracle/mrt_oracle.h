@@ -57,6 +57,8 @@ typedef struct {
     float noiseThreshold;   /* Light::m_noiseThreshold (default epsilon)       */
     int castShadows;
     int texture;            /* dome light: texture id (oro_scene_add_texture)  */
+    int transparent;        /* Light::setFastShadows(false): rect / dome lights walk
+                               through refractive hits (0 = fast shadows)       */
 } oro_light;
 
 typedef struct {
@@ -157,6 +159,10 @@ int oro_mesh_texcoords(const oro_scene* s, int mesh, int* ntc, float* uv, uint32
 int oro_mesh_set_motion(oro_scene* s, int mesh, const float* verts2);
 /* Scene::setEnvMap + setEnvExposure (src/Scene.h:23-24); texture -1 clears. */
 int oro_scene_set_env_map(oro_scene* s, int texture, float exposure);
+/* Material::setEnvMap + m_envExposure (src/Material.h:19,41-42): a Blinn
+ * material's missed reflection / refraction / GI rays take this map instead of
+ * the scene's (Material::getEnvironmentColor, src/Material.cpp:44-64); -1 clears */
+int oro_scene_set_material_env_map(oro_scene* s, int material, int texture, float exposure);
 /* DomeLight::setTexture tables of light `light` (src/DomeLight.cpp:8-78):
  * cdf_u[nu+1], func_u[nu], cdf_v[nu*(nv+1)], func_v[nu*nv], func_int[nu+1]
  * (column integrals, then the u integral), cos_u/sin_u[nu+1], cos_v/sin_v[nv+1]. */

@@ -42,7 +42,8 @@ class Material(C.Structure):
 class Light(C.Structure):
     _fields_ = [("type", C.c_int), ("pos", C.c_float * 3), ("v1", C.c_float * 3), ("v2", C.c_float * 3),
                 ("v3", C.c_float * 3), ("power", C.c_float), ("samples", C.c_int),
-                ("noiseThreshold", C.c_float), ("castShadows", C.c_int), ("texture", C.c_int)]
+                ("noiseThreshold", C.c_float), ("castShadows", C.c_int), ("texture", C.c_int),
+                ("transparent", C.c_int)]
 
 
 class Camera(C.Structure):
@@ -99,6 +100,7 @@ def _declare(L):
     L.oro_mesh_texcoords.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), _fp, _u32p]
     L.oro_mesh_set_motion.argtypes = [C.c_void_p, C.c_int, _fp]
     L.oro_scene_set_env_map.argtypes = [C.c_void_p, C.c_int, C.c_float]
+    L.oro_scene_set_material_env_map.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_float]
     L.oro_dome_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.oro_dome_export.argtypes = [C.c_void_p, C.c_int] + [_fp] * 9
     L.oro_texture_lookup_dir.argtypes = [C.c_void_p, C.c_int, C.c_int, _fp, _fp]
@@ -227,8 +229,11 @@ class OracleScene:
         self.n_lights += 1
         return self.L.oro_scene_add_light(self.h, C.byref(l))
 
-    def add_rect_light(self, v1, v2, v3, power, samples=1, noise=0.001, cast_shadows=True):
+    def add_rect_light(self, v1, v2, v3, power, samples=1, noise=0.001, cast_shadows=True, fast_shadows=True):
+        """fast_shadows False: Light::setFastShadows(false), the transparency walk of
+        src/RectangleLight.cpp:93-116."""
         l = Light()
+        l.transparent = 0 if fast_shadows else 1
         l.type = 1
         l.v1, l.v2, l.v3 = _v3(v1), _v3(v2), _v3(v3)
         l.power = power
@@ -280,9 +285,11 @@ class OracleScene:
             raise RuntimeError("oracle add_texture failed")
         return r
 
-    def add_dome_light(self, texture, power, samples=1, noise=0.001):
-        """DomeLight: setTexture(texture) + setPower (m_Gain) + setSamples."""
+    def add_dome_light(self, texture, power, samples=1, noise=0.001, fast_shadows=True):
+        """DomeLight: setTexture(texture) + setPower (m_Gain) + setSamples (fast_shadows
+        False: the transparency walk of src/DomeLight.cpp:123-145)."""
         l = Light()
+        l.transparent = 0 if fast_shadows else 1
         l.type = 2
         l.power = power
         l.samples = samples
@@ -324,6 +331,11 @@ class OracleScene:
     def set_env_map(self, texture, exposure=1.0):
         if self.L.oro_scene_set_env_map(self.h, int(texture), float(exposure)) != 0:
             raise RuntimeError("oracle set_env_map failed")
+
+    def set_material_env_map(self, material, texture, exposure=1.0):
+        """Material::setEnvMap + m_envExposure (src/Material.h:19,41-42)."""
+        if self.L.oro_scene_set_material_env_map(self.h, int(material), int(texture), float(exposure)) != 0:
+            raise RuntimeError("oracle set_material_env_map failed")
 
     def dome_export(self, light):
         nu, nv = C.c_int(), C.c_int()

@@ -67,7 +67,9 @@ __device__ __forceinline__ void unpack_state(uint32_t w, ChainState& cs, bool& e
 // ch_val flags (.w bits): the entry's ray missed (a split parent skips it); its
 // value is "nothing" (a GI ray missed without environment sampling); its value
 // is still to be folded from its children (pending), which are a split
-enum { kValMissed = 1, kValNone = 2, kValPending = 4, kValSplit = 8 };
+// value is the missed ray's direction, the parent's environment still to be looked up
+// (a material with its own environment map, Material::getEnvironmentColor)
+enum { kValMissed = 1, kValNone = 2, kValPending = 4, kValSplit = 8, kValEnvDir = 16 };
 
 __device__ __forceinline__ uint32_t lofs(const RenderParams& P, int k) { return P.ch_lofs[k]; }
 __device__ __forceinline__ uint32_t lcap(const RenderParams& P, int k) { return P.ch_lofs[k + 1] - P.ch_lofs[k]; }
@@ -457,6 +459,8 @@ __global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
                 if (MODE == kGen) {
                     P.nrays[base + e] = 0;
                     if (k + 1 < P.ch_levels) no_children(P, e);
+                } else if (env_miss && P.mat_env) {   // the fold looks up the parent material's map
+                    write_val(P, k, e, mk(d.x, d.y, d.z), kValMissed | kValEnvDir);
                 } else {
                     write_val(P, k, e, env_miss ? env_or_bg(P, mk(d.x, d.y, d.z)) : mk(0, 0, 0),
                               kValMissed | (env_miss ? 0u : kValNone));
@@ -525,7 +529,9 @@ __global__ void __launch_bounds__(kWG) chain_fold_kernel(RenderParams P) {
         v3 val;
         if (!(fl & kValSplit)) {
             const float4 c = P.ch_val[cb + map[(size_t)e * P.ch_split]];
-            val = chain_combine(P, rec, mk(c.x, c.y, c.z), (__float_as_uint(c.w) & kValNone) != 0);
+            v3 cv = mk(c.x, c.y, c.z);
+            if (__float_as_uint(c.w) & kValEnvDir) cv = mat_env(P, P.mats[__float_as_int(rec(0)) & 0xFFFF], cv);
+            val = chain_combine(P, rec, cv, (__float_as_uint(c.w) & kValNone) != 0);
         } else {
             const DevMaterial& M = P.mats[__float_as_int(rec(0)) & 0xFFFF];
             const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
@@ -543,7 +549,7 @@ __global__ void __launch_bounds__(kWG) chain_fold_kernel(RenderParams P) {
                 const float vDotN = rec(17), q = rec(18) / rec(21);
                 const float sq = std_max(0.0f, sqrtf(1.0f - (q * q) * (1.0f - vDotN * vDotN)));
                 const v3 dir2 = normalized(add(scale(rayD, q), scale(nn, q * vDotN - sq)), rsqT);
-                Lt = add(Lt, mul(ks, env_or_bg(P, dir2)));
+                Lt = add(Lt, mul(ks, mat_env(P, M, dir2)));
             }
             const v3 ka = mk(M.ka[0], M.ka[1], M.ka[2]), le = mk(M.le[0], M.le[1], M.le[2]);
             const v3 base = scale(add(add(add(z, ka), z), z), rec(1));

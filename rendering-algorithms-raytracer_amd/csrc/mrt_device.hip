@@ -628,6 +628,7 @@ struct DeviceState {
     bool dome = false;           // a dome light (incoherent shadow rays)
     int recursive = 0;           // chain shading (Shader REC): 1 reflection / refraction, 2 + path tracing
     bool disperse = false;       // a dispersive Blinn material with secondary rays: the fused (tree) engine
+    bool transparent = false;    // a rect / dome light with transparent shadows: fused kernels only
     bool pow_spec = false;       // a Blinn material with specExp != 1 (frame1 / shade1 kernels with pow)
     int wall_khz = 0;            // wall_clock64() rate
     size_t bytes = 0;
@@ -1059,6 +1060,12 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
         if (m.type == MRT_BLINN && (m.reflect > 0.f || m.refract > 0.f || m.gloss < 1.f || m.translucency > 0.01f)) d.recursive = 1;
     if (s.path_trace) d.recursive = 2;
     d.disperse = false;
+    // transparent shadows: the walk is compiled into the fused chain kernels only (it
+    // needs a closest-hit traversal in the shading, which would cost the direct
+    // kernels occupancy), and they shade a scene without secondary rays identically
+    d.transparent = false;
+    for (const DevLight& l : s.lights) d.transparent |= l.transparent != 0;
+    if (d.transparent && !d.recursive) d.recursive = 1;
     d.pow_spec = false;
     for (const DevMaterial& m : s.materials) d.pow_spec |= m.type == MRT_BLINN && m.spec_exp != 1.0f;
     for (const DevMaterial& m : s.materials)
@@ -1126,6 +1133,8 @@ static void fill_params(const Scene& s, RenderParams& P) {
     P.path_trace = s.path_trace ? 1 : 0;
     P.max_bounces = s.max_bounces;
     P.sample_env = s.sample_env ? 1 : 0;
+    P.mat_env = 0;
+    for (const DevMaterial& m : s.materials) P.mat_env |= m.env >= 0 ? 1 : 0;
 }
 
 // chain levels of the REC kernels: reflection / refraction bounces (< 5) plus
@@ -1384,9 +1393,11 @@ static uint64_t level_mult(const Scene& s, int k) {
         for (int i = 0; i < (k + 1) / 2; i++) m *= 3;
     return m;
 }
+// (Transparent shadows: the walk's answer is an attenuation, not the one bit the
+// wavefront shadow passes carry -- such scenes shade in the fused kernels.)
 static bool use_chain(const Scene& s) {
     return s.dev->recursive && g_chain && chain_levels(s) <= kMaxChainLevels && chain_shadow_rays(s) > 0 &&
-           !(s.dev->disperse && s.path_trace);
+           !(s.dev->disperse && s.path_trace) && !s.dev->transparent;
 }
 // One chunk of the engine over units [Q.unit_base, Q.unit_base + Q.n_units) of
 // Q's pass (the chunk layout -- ch_lofs, arrays -- is set by the caller).
@@ -1759,7 +1770,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     P.queue = qbase + 8 * 32;
     const int max_sh = max_shadow_rays(s);
     // secondary rays and their shadow rays depend on hits along the path: fused kernel
-    const bool wave = !one && g_wavefront && max_sh > 0 && max_sh <= kMaxWaveShadow && !d.recursive;
+    const bool wave = !one && g_wavefront && max_sh > 0 && max_sh <= kMaxWaveShadow && !d.recursive && !d.transparent;
     if (use_chain(s)) {
         c.chain_used = true;
         P.units = nullptr;
@@ -1871,6 +1882,8 @@ int mrt_scene_add_material(mrt_scene* s, const mrt_material* m) {
     memcpy(d.le, m->le, 12);
     d.emitted = m->emitted;
     d.sample_env = 1;                                                 // Material::Material, src/Material.cpp:6
+    d.env = -1;                                                       // m_envMap NULL, m_envExposure 1 (:4)
+    d.env_exposure = 1.f;
     for (int k = 0; k < 6; k++) d.maps[k] = -1;                       // no maps (src/Material.cpp:4-5)
     d.emitter = (d.emitted > 0.0f || (d.le[0] + d.le[1]) + d.le[2] > 0.0f) ? 1 : 0;   // src/Blinn.cpp:47
     if (m->type != MRT_BLINN) { d.le[0] = d.le[1] = d.le[2] = 0.f; d.emitted = 0.f; d.emitter = 0; }
@@ -1888,12 +1901,8 @@ int mrt_scene_add_light(mrt_scene* s, const mrt_light* l) {
     // Light::setFastShadows(false).  A point light's "full method" (src/PointLight.cpp:49-70)
     // sets sampleHit.t = distance and then loops while sampleHit.t < distance: it never
     // traces, so the light casts no shadow -- exactly cast_shadows = 0.  The rectangle and
-    // dome lights' transparency walks (src/RectangleLight.cpp:93-116, src/DomeLight.cpp:
-    // 123-145) are not implemented; no reference scene sets the flag.
-    if (l->transparent_shadows && l->type != MRT_POINT_LIGHT) {
-        set_error("transparent shadows (Light::setFastShadows(false)) of rectangle / dome lights are not implemented");
-        return MRT_ERR_INVALID;
-    }
+    // dome lights walk through refractive hits (src/RectangleLight.cpp:93-116,
+    // src/DomeLight.cpp:123-145; Shader::transmit).
     DevLight d;
     memset(&d, 0, sizeof d);
     d.dome = -1;
@@ -1916,7 +1925,8 @@ int mrt_scene_add_light(mrt_scene* s, const mrt_light* l) {
     memcpy(d.pos, l->pos, 12); memcpy(d.v1, l->v1, 12); memcpy(d.v2, l->v2, 12); memcpy(d.v3, l->v3, 12);
     d.samples = l->samples < 1 ? 1 : l->samples;
     d.noise = l->noise_threshold;
-    d.cast_shadows = l->cast_shadows && !l->transparent_shadows;
+    d.cast_shadows = l->cast_shadows && !(l->transparent_shadows && l->type == MRT_POINT_LIGHT);
+    d.transparent = l->transparent_shadows && l->type != MRT_POINT_LIGHT ? 1 : 0;
     d.power = l->power;
     if (l->type == MRT_RECT_LIGHT) {
         // RectangleLight::setPower (src/RectangleLight.cpp:14-40)
@@ -2068,6 +2078,20 @@ int mrt_scene_add_texture(mrt_scene* s, const float* rgb, int32_t width, int32_t
     s->impl.textures.push_back(std::move(t));
     s->impl.dev_dirty = true;
     return (int)s->impl.textures.size() - 1;
+}
+
+int mrt_scene_set_material_env_map(mrt_scene* s, int material, int32_t texture, float exposure) {
+    if (!s || material < 0 || material >= (int)s->impl.materials.size()) { set_error("bad material id"); return MRT_ERR_INVALID; }
+    if (texture < -1 || texture >= (int32_t)s->impl.textures.size() ||
+        (texture >= 0 && tex_channels(s->impl.textures[texture].type) != 3)) {
+        set_error("bad texture id (an environment map needs an RGB / HDR texture)");
+        return MRT_ERR_INVALID;
+    }
+    DevMaterial& m = s->impl.materials[(size_t)material];
+    m.env = texture;
+    m.env_exposure = exposure;
+    s->impl.dev_dirty = true;
+    return MRT_OK;
 }
 
 int mrt_scene_set_env_map(mrt_scene* s, int32_t texture, float exposure) {

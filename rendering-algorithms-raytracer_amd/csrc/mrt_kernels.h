@@ -874,12 +874,15 @@ __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMi
 #ifdef MRT_PREFETCH  // build variant (make variant NAME=pf EXTRA=-DMRT_PREFETCH) for A/B runs
     const bool hit = (FAST && r.finite && !INST) ? traverse_pf<ANY, COUNT>(c, r, tMin, h, st)
                                                  : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
-#elif defined(MRT_TRAV_V1)   // A/B build: round 3's walk for plain scenes too
-    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
-                                        : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
-#else
+#elif defined(MRT_TRAV_UNIFORM)   // A/B build (make variant NAME=uni EXTRA=-DMRT_TRAV_UNIFORM): the
+    // uniform-stack walk for plain scenes.  Round 4, interleaved on one MI355X
+    // (profiles/r04_walk_ab.txt): C3 +0.8..1.6% slower per frame, C3L 1.5% faster per
+    // launch but equal at 4 frames in flight, C2 / C4 within 0.5% -- not the default.
     const bool hit = (FAST && r.finite) ? (INST ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
                                                 : traverse_fast<ANY, COUNT>(c, r, tMin, h, st))
+                                        : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
+#else
+    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
                                         : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
 #endif
     if (!ANY && hit) {

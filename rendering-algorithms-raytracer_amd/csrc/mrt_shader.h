@@ -164,6 +164,7 @@ struct RenderParams {
     const uint8_t* pflags;
     const float4* verts2;
     int32_t has_mb;
+    int32_t mat_env;             // some material has its own environment map (Material::m_envMap)
 };
 
 // pow(spec, specExp) of Blinn::shade (src/Blinn.cpp:219-220; libm powf in the
@@ -230,10 +231,19 @@ struct LevelOut {
     bool split = false;   // dispersion: three refraction children (Shader::disp_child), not r2
 };
 
-// Material::getEnvironmentColor (src/Material.cpp:44-62): scene map or background
+// Material::getEnvironmentColor (src/Material.cpp:44-64) without a material map:
+// the scene's map or the background
 __device__ __forceinline__ v3 env_or_bg(const RenderParams& P, v3 d) {
     if (P.env) return scale(tex_lookup_dir(P.env, P.env_w, P.env_h, d.x, d.y, d.z), P.env_exposure);
     return mk(P.bg[0], P.bg[1], P.bg[2]);
+}
+// Material::getEnvironmentColor of material M: its own map x m_envExposure first
+__device__ __forceinline__ v3 mat_env(const RenderParams& P, const DevMaterial& M, v3 d) {
+    if (M.env >= 0) {
+        const DevTexture& t = P.texs[M.env];
+        return scale(tex_lookup_dir(t.data, t.W, t.H, d.x, d.y, d.z), M.env_exposure);
+    }
+    return env_or_bg(P, d);
 }
 
 // Fold a child's value into its parent level (Blinn::shade, src/Blinn.cpp:
@@ -302,6 +312,52 @@ struct Shader {
         }
     }
 
+    // The shadow walk of Light::m_fastShadows = false for rectangle / dome lights
+    // (src/RectangleLight.cpp:93-116, src/DomeLight.cpp:123-145), fused chain kernels
+    // only (the dispatcher runs such scenes there, off the wavefront passes, whose
+    // shadow answers are one bit): closest-hit rays along L, each from the previous hit
+    // point and bounded by the previous hit's t (the reference's sampleHit lives
+    // across the loop; the first bound is t0).  A hit whose interpolated normal
+    // (HitInfo::getInterpolatedNormal, src/Ray.cpp:51-65: mesh normals, object
+    // space for a proxy hit) faces the ray scales the attenuation by its
+    // material's refractAmt (0 for Lambert, which the reference leaves
+    // uninitialised).  Ends at a miss, when the summed t reaches `limit`, or at an
+    // attenuation <= epsilon.  Every trace counts as a shadow ray.
+    template <bool COUNT>
+    __device__ float transmit(v3 from, v3 L, float t0, float limit) {
+        float att = 1.0f, done = 0.0f, tb = t0;
+        v3 o = from;
+        while (done < limit && att > 0.001f) {
+            shadow_rays++;
+            const DRay r = make_ray(o, L, shadow_time);
+            DHit h{tb, 0.f, 0.f, -1};
+            if (!traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st)) break;
+            int32_t ps_i = h.prim;
+            if (INST && h.prim >= P.n_world) ps_i = inst_shade_index(h.prim, nullptr);
+            const PrimShade ps = P.prims[ps_i];
+            const float c = 1.0f - h.a - h.b;
+            const float4 n0 = P.normals[ps.n[0]], n1 = P.normals[ps.n[1]], n2 = P.normals[ps.n[2]];
+            const v3 hitN = normalized(add(add(scale(mk(n0.x, n0.y, n0.z), c), scale(mk(n1.x, n1.y, n1.z), h.a)),
+                                           scale(mk(n2.x, n2.y, n2.z), h.b)), rsqT);
+            if (dot(hitN, neg(L)) > 0.0f) {
+                const DevMaterial& M = P.mats[ps.mat];
+                att *= M.type == MRT_BLINN ? M.refract : 0.0f;
+            }
+            o = add(o, scale(L, h.t));
+            tb = h.t;
+            done += h.t;
+        }
+        return att;
+    }
+    // shadow answer of a rect / dome light sample: 0 / 1, or the transparency walk
+    template <bool COUNT>
+    __device__ float light_vis(const DevLight& l, v3 from, v3 L, float tMax, float limit) {
+        if constexpr (MODE == kFused && !POINT_ONLY && REC != 0) {
+            if (l.transparent) return transmit<COUNT>(from, L, tMax, limit);
+        }
+        return occluded<COUNT>(from, L, tMax) ? 0.0f : 1.0f;
+    }
+
     // PointLight::sampleLight, src/PointLight.cpp:8-81
     template <bool COUNT>
     __device__ float point_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec) {
@@ -325,7 +381,7 @@ struct Shader {
         return A * attenuate;
     }
 
-    // RectangleLight::sampleLight, src/RectangleLight.cpp:42-136 (fast shadows)
+    // RectangleLight::sampleLight, src/RectangleLight.cpp:42-136 (fast or transparent shadows)
     template <bool COUNT>
     __device__ v3 rect_light(const DevLight& l, v3 from, v3 normal, v3 rVec, float& outSpec) {
         v3 v1 = mk(l.v1[0], l.v1[1], l.v1[2]), v2 = mk(l.v2[0], l.v2[1], l.v2[2]), w3 = mk(l.v3[0], l.v3[1], l.v3[2]);
@@ -346,7 +402,7 @@ struct Shader {
                 falloff = rcp_nr(falloff, rcpT);
                 float dist = rcp_nr(dr, rcpT);
                 rd = scale(rd, dr);
-                if (l.cast_shadows && occluded<COUNT>(from, rd, dist - 0.001f)) att = 0.0f;
+                if (l.cast_shadows) att = light_vis<COUNT>(l, from, rd, dist - 0.001f, dist);
             } else {
                 att = 0.0f;
             }
@@ -421,7 +477,7 @@ struct Shader {
             const v3 E = scale(scale(img, l.power), inv);
             float att = 1.0f;
             if (MODE == kGen && P.lrec) P.ray_e[slot0 + nslot] = make_float4(E.x, E.y, E.z, dot(rVec, dir));
-            if (occluded<COUNT>(from, dir, 1e12f)) att = 0.0f;
+            att = light_vis<COUNT>(l, from, dir, 1e12f, 1e12f);   // sampleHit.t = MIRO_TMAX
             done++;
             recip = 1.0f / (float)done;
             const v3 Es = scale(E, recip);
@@ -451,18 +507,21 @@ struct Shader {
 
     // HitInfo::getAllInfos (normals), src/Ray.cpp:5-49
     // an instance hit (id >= n_world) names instance i's BLAS object id - hit_base
-    __device__ void normals(const DHit& h, v3& N, v3& geoN, uint32_t& mat) {
-        int32_t ps_i = h.prim, inst = -1;
-        if (INST && h.prim >= P.n_world) {
-            int lo = 0, hi = P.n_insts - 1;  // the last instance with hit_base <= id
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (P.insts[mid].hit_base <= h.prim) lo = mid;
-                else hi = mid - 1;
-            }
-            inst = lo;
-            ps_i = P.insts[lo].shade_base + (h.prim - P.insts[lo].hit_base);
+    // PrimShade index of instance hit id `prim` (and the instance)
+    __device__ int32_t inst_shade_index(int32_t prim, int* inst) const {
+        int lo = 0, hi = P.n_insts - 1;  // the last instance with hit_base <= id
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (P.insts[mid].hit_base <= prim) lo = mid;
+            else hi = mid - 1;
         }
+        if (inst) *inst = lo;
+        return P.insts[lo].shade_base + (prim - P.insts[lo].hit_base);
+    }
+    __device__ void normals(const DHit& h, v3& N, v3& geoN, uint32_t& mat) {
+        int32_t ps_i = h.prim;
+        int inst = -1;
+        if (INST && h.prim >= P.n_world) ps_i = inst_shade_index(h.prim, &inst);
         PrimShade ps = P.prims[ps_i];
         float4 A = P.verts[ps.v[0]], B = P.verts[ps.v[1]], C = P.verts[ps.v[2]];
         geoN = normalized(cross(mk(B.x - A.x, B.y - A.y, B.z - A.z), mk(C.x - A.x, C.y - A.y, C.z - A.z)), rsqT);
@@ -622,7 +681,7 @@ struct Shader {
         return normalized(add(add(scale(u, c * sqrte2), scale(v, s * sqrte2)), scale(N, sqrt1_e2)), rsqT);
     }
 
-    __device__ v3 env_color(v3 d) { return env_or_bg(P, d); }
+    __device__ v3 env_color(const DevMaterial& M, v3 d) { return mat_env(P, M, d); }
 
     // the camera ray's history: [1, 1.001, (a level-0 refraction push)] and its index
     struct IorCam {
@@ -792,7 +851,7 @@ struct Shader {
             // dispersion (src/Blinn.cpp:275-301): three refraction children, one per
             // colour channel, traced by the caller in channel order (disp_child)
             if (cs.bounces >= kMaxBounce) {   // none traced: Lt = ks * environment along channel 2's direction
-                const v3 L = add(z, mul(ks, env_color(disp_dir(rayD, n, vDotN, inIOR / M.ior3[2]))));
+                const v3 L = add(z, mul(ks, env_color(M, disp_dir(rayD, n, vDotN, inIOR / M.ior3[2]))));
                 o.val = add(add(base, scale(add(z, L), rrSpec)), le);
                 return;
             }
@@ -843,7 +902,7 @@ struct Shader {
             secondary++;
             return;
         }
-        const v3 L = add(z, mul(ks, env_color(dir)));   // Lr / Lt += m_ks * environment
+        const v3 L = add(z, mul(ks, env_color(M, dir)));   // Lr / Lt += m_ks * environment
         o.val = add(add(base, scale(refr ? add(z, L) : add(L, z), rrSpec)), le);
     }
 
@@ -909,7 +968,7 @@ struct Shader {
                     continue;
                 }
                 none = !o.env_miss;   // the missed child's value: environment, or nothing (GI, no env)
-                val = none ? z : env_color(o.dir);
+                val = none ? z : env_color(P.mats[__float_as_int(rec_fused(d)(0)) & 0xFFFF], o.dir);
                 k = d;
             }
             bool descend = false;
@@ -947,7 +1006,7 @@ struct Shader {
                 if (__float_as_int(rec(7)) == 0) {   // doEnv: no child hit
                     const v3 dir2 = disp_dir(mk(rec(11), rec(12), rec(13)), mk(rec(14), rec(15), rec(16)), rec(17),
                                              rec(18) / rec(21));
-                    Lt = add(Lt, mul(ks, env_color(dir2)));
+                    Lt = add(Lt, mul(ks, env_color(M, dir2)));
                 }
                 const v3 ka = mk(M.ka[0], M.ka[1], M.ka[2]), le = mk(M.le[0], M.le[1], M.le[2]);
                 const v3 base = scale(add(add(add(z, ka), z), z), rec(1));

@@ -72,6 +72,10 @@ struct DevMaterial {
     // a ray that is not a refraction ray splits into one refraction ray per channel
     int32_t disperse;
     float ior3[3];
+    // Material::m_envMap / m_envExposure (src/Material.h:19,41-42): the map a missed
+    // reflection / refraction / GI ray of this material takes (-1: the scene's)
+    int32_t env;
+    float env_exposure;
 };
 enum { kMapColor = 0, kMapNormal = 1, kMapSpecular = 2, kMapReflect = 3, kMapRefract = 4, kMapAlpha = 5 };
 
@@ -90,6 +94,7 @@ struct DevLight {
     float noise;
     int32_t cast_shadows;
     int32_t dome;       // dome light: index of its DevDome tables (-1 otherwise)
+    int32_t transparent;   // rect / dome: Light::m_fastShadows false, the transparency walk (fused kernels)
 };
 
 // DomeLight::setTexture products in HBM (src/DomeLight.cpp:8-78): the lat-long

@@ -140,6 +140,15 @@ class _Maps:
     def _maps(self):
         return (self.colorMap, self.normalMap, self.specularMap, self.reflectMap, self.refractMap, self.alphaMap)
 
+    # Material::setEnvMap / m_envExposure (src/Material.h:19,41-42): the map a missed
+    # reflection / refraction / GI ray of a Blinn material takes (getEnvironmentColor,
+    # src/Material.cpp:44-64); None = the scene's
+    envMap = None
+    envExposure = 1.0
+
+    def setEnvMap(self, t): self.envMap = t
+    def setEnvExposure(self, x): self.envExposure = float(x)
+
 
 class Lambert(_Maps):
     """Lambert(kd = Vector3(1), ka = Vector3(0)), src/Lambert.h:11-13."""
@@ -215,7 +224,7 @@ class _Light:
         self.power = 0.0
         self.samples = 1
         self.castShadows = True
-        self.fastShadows = True           # src/Light.h:16; False: a point light casts no shadow (its walk never traces), rect / dome lights are rejected by libmrt
+        self.fastShadows = True           # src/Light.h:16; False: a point light casts no shadow (its walk never traces), rect / dome lights walk through refractive hits
         self.noiseThreshold = 0.001
 
     def setColor(self, c): self.color = Vector3(c)
@@ -593,6 +602,9 @@ class Scene:
             if any(m is not None for m in maps):
                 arr = (C.c_int32 * 6)(*[tex_id(m) for m in maps])
                 check(L.mrt_scene_set_material_maps(self._h, mid, arr), "material maps")
+            if getattr(mat, "envMap", None) is not None:
+                check(L.mrt_scene_set_material_env_map(self._h, mid, tex_id(mat.envMap), mat.envExposure),
+                      "material env map")
 
         for light in self._lights:
             lc = light._c(tex_id(getattr(light, "texture", None)))

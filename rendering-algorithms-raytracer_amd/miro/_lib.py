@@ -9,7 +9,7 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("MRT_LIB", os.path.join(_PKG, "lib", "libmrt.so"))
 
 MRT_OK = 0
-ABI_VERSION = 8   # include/mrt.h MRT_ABI_VERSION: the struct layouts below
+ABI_VERSION = 9   # include/mrt.h MRT_ABI_VERSION: the struct layouts below
 ERRORS = {-1: "MRT_ERR_INVALID", -2: "MRT_ERR_IO", -3: "MRT_ERR_HIP", -4: "MRT_ERR_BUILD",
           -5: "MRT_ERR_NOT_BUILT", -6: "MRT_ERR_OVERFLOW", -7: "MRT_ERR_NO_DEVICE"}
 
@@ -23,7 +23,7 @@ EXPORTS = [
     "mrt_render_frame_async", "mrt_trace", "mrt_trace_async", "mrt_scene_last_stats", "mrt_rcp_nr",
     "mrt_rsqrt_nr", "mrt_set_tuning", "mrt_render_batch_async", "mrt_unpack_batch_async",
     "mrt_debug_wave_log", "mrt_device_wall_clock_khz", "mrt_hdr_info", "mrt_hdr_load", "mrt_scene_add_texture",
-    "mrt_scene_set_env_map", "mrt_scene_dome_info", "mrt_scene_dome_export", "mrt_scene_make_blas",
+    "mrt_scene_set_env_map", "mrt_scene_set_material_env_map", "mrt_scene_dome_info", "mrt_scene_dome_export", "mrt_scene_make_blas",
     "mrt_scene_add_instance", "mrt_scene_blas_info", "mrt_scene_blas_export", "mrt_scene_set_material_emission",
     "mrt_scene_set_material_sample_env", "mrt_scene_set_path_trace", "mrt_scene_prim_object",
     "mrt_image_info", "mrt_image_load", "mrt_scene_add_texture_typed", "mrt_scene_set_material_maps",
@@ -171,6 +171,7 @@ def load():
     L.mrt_scene_set_mesh_motion.argtypes = [C.c_void_p, C.c_int, _fp]
     L.mrt_scene_mesh_texcoords.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int32), _fp, C.POINTER(C.c_uint32)]
     L.mrt_scene_set_env_map.argtypes = [C.c_void_p, C.c_int32, C.c_float]
+    L.mrt_scene_set_material_env_map.argtypes = [C.c_void_p, C.c_int, C.c_int32, C.c_float]
     L.mrt_scene_dome_info.argtypes = [C.c_void_p, C.c_int32, _ip, _ip]
     L.mrt_scene_dome_export.argtypes = [C.c_void_p, C.c_int32] + [_fp] * 9
     L.mrt_scene_make_blas.argtypes = [C.c_void_p, _ip, C.c_int32]

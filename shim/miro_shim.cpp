@@ -145,7 +145,6 @@ struct Builder {
     int material(const Material* m) {
         auto it = mats.find(m);
         if (it != mats.end()) return it->second;
-        if (m->m_envMap) return MRT_ERR_INVALID;   // Material::setEnvMap: not on the C-ABI
         mrt_material mm;
         memset(&mm, 0, sizeof mm);
         int id;
@@ -189,6 +188,11 @@ struct Builder {
             any |= ids[k] >= 0;
         }
         if (any && (rc = mrt_scene_set_material_maps(s, id, ids))) return rc;
+        if (m->m_envMap) {   // Material::setEnvMap / m_envExposure (src/Material.h:19,41-42)
+            const int t = texture(m->m_envMap);
+            if (t < 0) return t;
+            if ((rc = mrt_scene_set_material_env_map(s, id, t, m->m_envExposure))) return rc;
+        }
         mats.emplace(m, id);
         return id;
     }

@@ -107,7 +107,7 @@ struct Material {
     Texture* m_reflectMap = nullptr;
     Texture* m_refractMap = nullptr;
     Texture* m_normalMap = nullptr;
-    Texture* m_envMap = nullptr;      // Material::setEnvMap: not on the C-ABI yet (preCalc rejects it)
+    Texture* m_envMap = nullptr;      // Material::setEnvMap (mrt_scene_set_material_env_map)
     float m_envExposure = 1.f;
     bool m_sampleEnv = true;
     float m_translucency = 0.f;
@@ -141,7 +141,7 @@ struct Light {
     float m_power = 0.f;
     int m_numSamples = 1;
     bool m_castShadows = true;
-    bool m_fastShadows = true;   // src/Light.h:16 (false: a point light casts no shadow, its walk never traces; rect / dome: rejected by the C-ABI)
+    bool m_fastShadows = true;   // src/Light.h:16 (false: a point light casts no shadow, its walk never traces; rect / dome walk through refractive hits)
     float m_noiseThreshold = 0.001f;
     void setPower(float f) { m_power = f; }
     void setSamples(int n) { m_numSamples = n; }

@@ -73,7 +73,13 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
     mat = cfg["material"]
     P = miro.Scene()
     O_ = O.OracleScene()
-    pm, om = materials_pair(P, O_, mat)
+    all_mats = []   # (product, oracle id, description): per-material environment maps come last
+
+    def materials_pair_(P, O_, m):
+        pm_, om_ = materials_pair(P, O_, m)
+        all_mats.append((pm_, om_, m))
+        return pm_, om_
+    pm, om = materials_pair_(P, O_, mat)
     material_maps(pm, O_, om, mat)
     for arrs in (meshes or []):
         tm = miro.TriangleMesh()
@@ -99,7 +105,7 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
             P.addObject(miro.ProxyObject(*protos[b], miro.Matrix4x4(M)))
             O_.add_instance(oblas[b], M)
     for arrs, emat in (extra or []):   # mesh arrays (+ uv, tidx), or an OBJ path
-        xm, oxm = materials_pair(P, O_, emat)
+        xm, oxm = materials_pair_(P, O_, emat)
         tm = miro.TriangleMesh()
         if isinstance(arrs, str):
             tm.load(arrs)
@@ -113,7 +119,7 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
         miro.makeMeshObjs(P, tm, xm)
         material_maps(xm, O_, oxm, emat)
     for arrs, v2, emat in (moving or []):
-        xm, oxm = materials_pair(P, O_, emat)
+        xm, oxm = materials_pair_(P, O_, emat)
         tm, tm2 = miro.TriangleMesh(), miro.TriangleMesh()
         tm.setArrays(*arrs[:4])
         tm2.setArrays(v2, *arrs[1:4])
@@ -161,13 +167,17 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
             tex, otex = texture(rgb)
             dl = miro.DomeLight(); dl.setTexture(tex); dl.setPower(l["power"])
             dl.setSamples(l.get("samples", 1)); dl.setNoiseThreshold(l.get("noise", 0.001))
+            dl.setFastShadows(l.get("fast_shadows", True))
             P.addLight(dl)
-            O_.add_dome_light(otex, l["power"], l.get("samples", 1), l.get("noise", 0.001))
+            O_.add_dome_light(otex, l["power"], l.get("samples", 1), l.get("noise", 0.001),
+                              fast_shadows=l.get("fast_shadows", True))
         else:
             rl = miro.RectangleLight(); rl.setVertices(l["v1"], l["v2"], l["v3"]); rl.setPower(l["power"])
             rl.setSamples(l.get("samples", 1)); rl.setNoiseThreshold(l.get("noise", 0.001))
+            rl.setFastShadows(l.get("fast_shadows", True))
             P.addLight(rl)
-            O_.add_rect_light(l["v1"], l["v2"], l["v3"], l["power"], l.get("samples", 1), l.get("noise", 0.001))
+            O_.add_rect_light(l["v1"], l["v2"], l["v3"], l["power"], l.get("samples", 1), l.get("noise", 0.001),
+                              fast_shadows=l.get("fast_shadows", True))
     P.setBGColor(cfg["bg"])
     O_.set_bg(cfg["bg"])
     env = cfg.get("env")
@@ -175,6 +185,11 @@ def scene_pair(cfg, meshes=None, obj=None, floor=False, lights=None, num_paths=1
         tex, otex = texture(sky(env["sky"]))
         P.setEnvMap(tex); P.setEnvExposure(env["exposure"])
         O_.set_env_map(otex, env["exposure"])
+    for pm_, om_, m in all_mats:   # Material::setEnvMap / m_envExposure
+        if m.get("env"):
+            tex, otex = texture(sky(m["env"]["sky"]))
+            pm_.setEnvMap(tex); pm_.setEnvExposure(m["env"]["exposure"])
+            O_.set_material_env_map(om_, otex, m["env"]["exposure"])
     P.setNumPaths(num_paths)
     O_.set_num_paths(num_paths)
     if path_trace is not None:

@@ -170,12 +170,12 @@ def test_shim_renders_c5_instances_dome_and_env_like_the_oracle(tmp_path):
         assert np.array_equal(got[k][hit].view(np.uint32), want[k][hit].view(np.uint32))
 
 
-def test_shim_rejects_transparent_shadows_and_material_env_maps():
+def test_c_abi_light_transparency_flag():
     """Light::setFastShadows(false): a point light's transparent-shadow walk
     (src/PointLight.cpp:49-70) never traces (it loops while sampleHit.t <
-    distance, starting at t = distance), so the C-ABI accepts it as a light that
-    casts no shadow; the rectangle / dome lights' walks have no implementation and
-    are rejected loudly (MRT_ERR_INVALID) rather than rendered with fast shadows."""
+    distance, starting at t = distance), so the C-ABI takes it as a light that
+    casts no shadow; rectangle / dome lights take the transparency walk (ABI 9,
+    tests/test_transparent.py)."""
     from miro import _lib
     L = miro.lib()
     s = L.mrt_scene_create()
@@ -185,9 +185,6 @@ def test_shim_rejects_transparent_shadows_and_material_env_maps():
         assert L.mrt_scene_add_light(s, C.byref(l)) >= 0       # point light: no shadow ray, as the reference
         r = _lib.mrt_light(1, _lib.f3((0, 0, 0)), _lib.f3((0, 2, 0)), _lib.f3((1, 2, 0)), _lib.f3((0, 2, 1)), 1.0, 1,
                            0.001, 1, -1, 1)
-        assert L.mrt_scene_add_light(s, C.byref(r)) == -1
-        assert b"transparent shadows" in L.mrt_last_error()
-        r.transparent_shadows = 0
         assert L.mrt_scene_add_light(s, C.byref(r)) >= 0
     finally:
         L.mrt_scene_destroy(s)
