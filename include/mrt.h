@@ -177,7 +177,10 @@ typedef struct {
      * stream's share of 80% of the device) and the chunks it ran (ABI 8) */
     uint64_t chain_budget_bytes;
     uint32_t chain_chunks;
-    int32_t reserved;
+    /* chunks whose level counts outgrew the capacities estimated from earlier chunks
+     * on the stream (mrt_set_tuning "chain_est"): their units were rendered again by
+     * the fused chain shading -- same frame, slower (ABI 9) */
+    int32_t chain_fallbacks;
 } mrt_stats;
 
 const char* mrt_last_error(void);

@@ -72,6 +72,9 @@ __device__ __forceinline__ void unpack_state(uint32_t w, ChainState& cs, bool& e
 enum { kValMissed = 1, kValNone = 2, kValPending = 4, kValSplit = 8, kValEnvDir = 16 };
 
 __device__ __forceinline__ uint32_t lofs(const RenderParams& P, int k) { return P.ch_lofs[k]; }
+// The chunk outgrew a level's estimated capacity: its remaining launches return at
+// once and chain_fallback_kernel renders its units instead.
+__device__ __forceinline__ bool chunk_dead(const RenderParams& P) { return P.ch_ovf != nullptr && *P.ch_ovf != 0u; }
 __device__ __forceinline__ uint32_t lcap(const RenderParams& P, int k) { return P.ch_lofs[k + 1] - P.ch_lofs[k]; }
 // level record of entry e of level k: lvl_words consecutive floats
 __device__ __forceinline__ ChainRec chain_rec(const RenderParams& P, int k, uint32_t e) {
@@ -198,6 +201,7 @@ __device__ __forceinline__ void no_children(const RenderParams& P, uint32_t e) {
 template <bool POINT_ONLY, bool INST, int REC, int MODE>
 __global__ void __launch_bounds__(kWG) chain0_kernel(RenderParams P) {
     __shared__ float s_ior[kIorCap * kWG];
+    if (chunk_dead(P)) return;
     const uint16_t* rcpT = P.tables;          // no triangle tests here: both tables from global (L1)
     const uint16_t* rsqT = P.tables + 2048;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -264,6 +268,7 @@ static constexpr int kCompactGroup = 4 * kWG;
 __global__ void __launch_bounds__(kWG) chain_compact_kernel(RenderParams P) {
     __shared__ uint32_t s_cnt[4 * (kWG / 64)];
     __shared__ uint32_t s_base;
+    if (chunk_dead(P)) return;
     const int k = P.ch_level;
     const uint32_t ne = k == 0 ? chunk_units(P) * (uint32_t)P.num_paths : P.ch_cnt[k];
     const uint32_t n = ne * (uint32_t)P.ch_split;
@@ -297,8 +302,9 @@ __global__ void __launch_bounds__(kWG) chain_compact_kernel(RenderParams P) {
             if (!f[j]) continue;
             const uint32_t e = g + (uint32_t)(j * kWG + tid);
             const uint32_t d = s_base + s_cnt[j * (kWG / 64) + wave] + rank[j];
-            if (d >= dcap) {   // cannot happen: level capacities bound the children per entry
-                atomicOr(&P.ctr[CTR_OVERFLOW], 2ull);
+            if (d >= dcap) {   // past the level's (estimated) capacity: the chunk goes to the fallback
+                if (P.ch_ovf) *P.ch_ovf = 1u;
+                else atomicOr(&P.ctr[CTR_OVERFLOW], 2ull);
                 map[e] = 0xFFFFFFFFu;
                 continue;
             }
@@ -322,6 +328,7 @@ template <bool COUNT, bool FAST, bool INST, int MINW = 1>
 __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
+    if (chunk_dead(P)) return;
     const int k = P.ch_level;
     const uint32_t nA = k < P.ch_levels ? P.ch_cnt[k] : 0u;
     const uint32_t m = (uint32_t)P.max_shadow;
@@ -432,6 +439,7 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
 template <bool POINT_ONLY, bool INST, int REC, int MODE>
 __global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
     __shared__ float s_ior[kIorCap * kWG];
+    if (chunk_dead(P)) return;
     const uint16_t* rcpT = P.tables;
     const uint16_t* rsqT = P.tables + 2048;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -514,6 +522,7 @@ __global__ void __launch_bounds__(kWG) chain_shade_kernel(RenderParams P) {
 // hit Lt takes m_ks * the environment along channel 2's direction
 // (src/Blinn.cpp:275-301, Shader::shade_path's fold).
 __global__ void __launch_bounds__(kWG) chain_fold_kernel(RenderParams P) {
+    if (chunk_dead(P)) return;
     const int k = P.ch_level;
     const uint32_t n = k == 0 ? chunk_units(P) * (uint32_t)P.num_paths : P.ch_cnt[k];
     const uint16_t* rsqT = P.tables + 2048;
@@ -564,6 +573,7 @@ __global__ void __launch_bounds__(kWG) chain_fold_kernel(RenderParams P) {
 // the environment / background.  Frame / bucket mode: float RGB + Image::Map
 // 8-bit of the pixel; adaptive passes: the unit's colour (ucol).
 __global__ void __launch_bounds__(kWG) chain_finish_kernel(RenderParams P) {
+    if (chunk_dead(P)) return;
     const uint16_t* rsqT = P.tables + 2048;
     const uint32_t np = (uint32_t)P.num_paths, n = chunk_units(P);
     for (uint32_t u = blockIdx.x * kWG + threadIdx.x; u < n; u += gridDim.x * kWG) {
@@ -653,6 +663,87 @@ __global__ void __launch_bounds__(kWG, MINW) unit_eye_kernel(RenderParams P) {
     if (st.overflow) atomicOr(&P.ctr[CTR_OVERFLOW], 1ull);
 }
 
+// End of a chunk (one block): its statistics into the frame's unless it outgrew a
+// level (the fallback counts its units then), and per level the entries per path
+// it needed (x 65536, + 1) into the stream's capacity estimates for this pass --
+// exact up to the level that overflowed, unknown (all ones) past it.
+__global__ void __launch_bounds__(64) chain_merge_kernel(RenderParams P) {
+    const int i = threadIdx.x;
+    const bool dead = chunk_dead(P);
+    if (dead && i == 0) atomicAdd(P.ctr_out + CTR_FALLBACK, 1ull);
+    if (!dead && i < CTR_N) {
+        const unsigned long long v = P.ctr[i];
+        if (i == CTR_MAXSP || (i >= CTR_TP && i < CTR_TS + 4)) atomicMax(P.ctr_out + i, v);
+        else if (i == CTR_OVERFLOW) { if (v) atomicOr(P.ctr_out + i, v); }
+        else if (v) atomicAdd(P.ctr_out + i, v);
+    }
+    if (!P.ch_est || i == 0 || i >= P.ch_levels) return;
+    const uint32_t paths = chunk_units(P) * (uint32_t)P.num_paths;
+    if (!paths) return;
+    bool known = true;   // no level above i overflowed
+    for (int k = 1; k < i; k++) known &= P.ch_cnt[k] <= lcap(P, k);
+    const uint64_t r = ((uint64_t)P.ch_cnt[i] * 65536u + paths - 1) / paths + 1;
+    atomicMax(P.ch_est + i, known ? (uint32_t)min<uint64_t>(r, 0xFFFFFFFEull) : 0xFFFFFFFFu);
+}
+
+// The units of a chunk that outgrew a level's estimated capacity, rendered by the
+// fused chain shading (Shader::shade: every path's tree depth first, the same rays,
+// draws and adds as the engine -- tests/test_chain.py) from the units' eye-ray hits,
+// written as chain_finish writes them.  Nothing to do (one uniform load) otherwise.
+template <bool POINT_ONLY, bool INST, int REC>
+__global__ void __launch_bounds__(kWG) chain_fallback_kernel(RenderParams P) {
+    __shared__ uint16_t s_tab[2048];
+    __shared__ int32_t s_stack[kLdsStack * kWG];
+    __shared__ float s_ior[kIorCap * kWG];
+    if (!chunk_dead(P)) return;
+    load_tables(P.tables, s_tab, 1024);
+    const uint16_t* rcpT = s_tab;
+    const uint16_t* rsqT = P.tables + 2048;
+    const int tid = threadIdx.x, lane = tid & 63;
+    Trav T{P.nodes, false, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
+    T.inst = P.insts;
+    trav_alpha(T, P);
+    TravStats st;
+    uint32_t shadow_total = 0, secondary_total = 0;
+    const uint32_t n = chunk_units(P);
+    for (uint32_t u = blockIdx.x * kWG + (uint32_t)tid; u < n; u += gridDim.x * kWG) {
+        const UnitPix U = unit_pixel(P, P.unit_base + u);
+        if (!U.valid) continue;
+        const float4 hv = unit_hit(P, u, U);
+        const DHit h{hv.x, hv.y, hv.z, __float_as_int(hv.w)};
+        const EyeRay er = unit_eye(P, U, rsqT);
+        v3 col;
+        if (h.prim >= 0) {
+            const CamParams& cam = P.cam[U.f];
+            Shader<POINT_ONLY, false, INST, kFused, REC> S{P, T, rcpT, rsqT, st, (uint32_t)(U.y * cam.W + U.x), 0u,
+                                                        P.seed + (uint32_t)U.f, 0, 0u};
+            S.sample = U.sample;
+            S.time = S.shadow_time = er.time;
+            S.iorS = s_ior + tid;
+            S.lvl = P.lvl + (blockIdx.x * kWG + tid);
+            col = S.template shade<false>(make_ray(er.o, er.d, er.time), h);
+            shadow_total += S.shadow_rays;
+            secondary_total += S.secondary;
+        } else {
+            col = P.env ? env_or_bg(P, er.d) : mk(P.bg[0], P.bg[1], P.bg[2]);
+        }
+        if (P.ucol) {
+            P.ucol[P.unit_base + u] = make_float4(col.x, col.y, col.z, 0.f);
+            continue;
+        }
+        if (P.out_rgb) {
+            float* o = P.out_rgb + 3 * U.slot;
+            o[0] = col.x; o[1] = col.y; o[2] = col.z;
+        }
+        if (P.out_rgb8) {
+            uint8_t* o8 = P.out_rgb8 + 3 * U.slot;
+            o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
+        }
+    }
+    flush_secondary(P, secondary_total, lane);
+    flush_stats<false>(P, st, shadow_total, lane, 0, 0);
+}
+
 // After adaptive pass n: per pixel of the pass, Scene::adaptiveSampleScene's
 // bookkeeping in the fused adaptive kernel's order -- pass 1 sets the result;
 // pass n >= 2 adds its n^2 colours in (i, j) order, forms the running mean with
@@ -739,6 +830,13 @@ KernelFn pick_unit_eye(bool c, bool f, bool inst) {
     return f ? unit_eye_kernel<true, true, false> : unit_eye_kernel<true, false, false>;
 }
 KernelFn pick_chain_compact() { return chain_compact_kernel; }
+KernelFn pick_chain_merge() { return chain_merge_kernel; }
+KernelFn pick_chain_fallback(bool po, bool inst, int rec) {
+    if (rec == 2) return po ? (inst ? chain_fallback_kernel<true, true, 2> : chain_fallback_kernel<true, false, 2>)
+                            : (inst ? chain_fallback_kernel<false, true, 2> : chain_fallback_kernel<false, false, 2>);
+    return po ? (inst ? chain_fallback_kernel<true, true, 1> : chain_fallback_kernel<true, false, 1>)
+              : (inst ? chain_fallback_kernel<false, true, 1> : chain_fallback_kernel<false, false, 1>);
+}
 KernelFn pick_chain_finish() { return chain_finish_kernel; }
 KernelFn pick_chain_fold() { return chain_fold_kernel; }
 KernelFn pick_adapt_combine() { return adapt_combine_kernel; }

@@ -75,6 +75,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
     trav_alpha(T, P);
     TravStats st;
     unsigned long long wave_steps = 0;
+    if (P.ch_ovf && *P.ch_ovf) return;   // a chain chunk past its estimated capacity (redone by its fallback)
     // chain levels: the entry count is on the device (n_rays is the capacity)
     if (P.sh_count) {
         const size_t nd = (size_t)*P.sh_count * (size_t)P.max_shadow;
@@ -560,6 +561,15 @@ struct StreamCtx {
     uint32_t chain_chunks = 0;               //   and the chunks that frame ran
     void* adapt = nullptr;                   // chain-engine adaptive supersampling: means, pixel lists, unit colours
     size_t adapt_bytes = 0;
+    // chain level capacities: per pass index (adapt_n, 0 = no supersampling) and level, the
+    // largest entries per path a chunk on this stream needed (x 65536, + 1; 0 = not seen,
+    // all ones = unknown) -- on the device (atomicMax by chain_merge), its last copy on the
+    // host (pinned, in flight until est_ev), and the host's view used to size chunks
+    uint32_t* est_dev = nullptr;
+    uint32_t* est_pinned = nullptr;
+    hipEvent_t est_ev = nullptr;
+    bool est_pending = false;
+    std::vector<uint32_t> est;
     bool last_was_render = false;
     bool fused = false;                      // the last render ran frame1_kernel (one launch)
     bool queue_clean = false;                // the last launch left the tile counters at zero (self-reset frame1)
@@ -674,6 +684,8 @@ static int g_near_first = -1;     // any-hit walks take the nearest hit child fi
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
 static int g_chain_shadow_refill = 1;   // instanced chain levels: shadow rays on the lane-refill kernel (FS / C5-like scenes)
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
+static int g_chain_est = 1;       // chain levels sized by the entries earlier chunks needed (0: worst case, 3^ceil(k/2))
+static int g_chain_est_pct = 125; //   headroom over the largest count per path seen, percent
 static int g_chain_mb = 49152;    // chain scratch per stream (MB), at most 80% of the device's free memory; larger
                                   // frames run in chunks of work items (G3: 16 GB -> 48 GB, 76.9 -> 47.2 ms per frame,
                                   // profiles/r03_g3_chain_mb_ab.txt)
@@ -707,6 +719,9 @@ static void free_ctx(StreamCtx* c) {
                     c->tile_cost, c->tile_order, c->adapt, c->bin_keys, c->bin_perm, c->bin_hist, c->ray_e, c->lrec};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (c->est_dev) (void)hipFree(c->est_dev);
+    if (c->est_pinned) (void)hipHostFree(c->est_pinned);
+    if (c->est_ev) (void)hipEventDestroy(c->est_ev);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->evm) (void)hipEventDestroy(c->evm);
@@ -1499,9 +1514,14 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
     HIP_OK(hipMemsetAsync(Q.ch_cnt, 0, ctl, stream));
     if (refill_sh) HIP_OK(hipMemsetAsync(Q.nrays + Q.ch_lofs[0], 0, lcap_h(0), stream));   // level 0: only live units' counts
     Q.queue = queues;
-    if (Q.uhits) {   // adaptive pass: the chunk's eye rays and their closest hits
+    if (Q.uhits) {   // adaptive pass: the chunk's eye rays and their closest hits (counted in the frame's
+                     // statistics: they run before any level can outgrow its capacity)
         const KernelFn ke = pick_unit_eye(count, Q.fast_box != 0, inst);
-        if ((rc = go(ke, (int)std::min<uint64_t>((uint64_t)full(ke), ((uint64_t)Q.n_units + kWG - 1) / kWG)))) return rc;
+        unsigned long long* cc = Q.ctr;
+        Q.ctr = Q.ctr_out;
+        rc = go(ke, (int)std::min<uint64_t>((uint64_t)full(ke), ((uint64_t)Q.n_units + kWG - 1) / kWG));
+        Q.ctr = cc;
+        if (rc) return rc;
     }
     Q.ch_level = 0;
     if ((rc = go(g0, ug))) return rc;                 // level 0: shadow rays + children
@@ -1521,23 +1541,61 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
         Q.ch_level = k;
         if ((rc = go(kd, full(kd)))) return rc;
     }
-    return go(kf, ug);                                 // per unit: paths averaged, pixel / unit colour
+    if ((rc = go(kf, ug))) return rc;                  // per unit: paths averaged, pixel / unit colour
+    // the chunk's statistics and capacity counts; a chunk that outgrew a level: its units again,
+    // fused (counted in the frame's statistics directly)
+    void* margs[] = {&Q};
+    HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(pick_chain_merge()), dim3(1), dim3(64), margs, 0, stream));
+    const KernelFn kfb = pick_chain_fallback(d.point_only, inst, d.recursive);
+    unsigned long long* cc = Q.ctr;
+    Q.ctr = Q.ctr_out;
+    rc = go(kfb, std::min(full(kfb), ug));
+    Q.ctr = cc;
+    return rc;
 }
 
 // The chain engine over a pass of `units_max` units (at most; the adaptive
 // passes' counts live on the device): the scratch layout for `per_chunk`
 // units, then the chunks.
+static constexpr int kEstPasses = 17;   // capacity estimates: pass index 0 (no supersampling), 1 .. 16
 static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool count, hipStream_t stream,
                         uint64_t units_max, int unit_align) {
     DeviceState& d = *s.dev;
     const int L = chain_levels(s), W = level_words(s), m = chain_shadow_rays(s), split = d.disperse ? 3 : 1;
     const uint64_t np = (uint64_t)P0.num_paths;
-    uint64_t mult_sum = 0, mult_max = 0;
-    for (int k = 0; k < L; k++) { mult_sum += level_mult(s, k); mult_max = std::max(mult_max, level_mult(s, k)); }
+    // Level capacities in entries per path x 65536.  Worst case: level k holds 3^ceil(k/2)
+    // entries per path where dispersive splits can occur, else one.  With chain_est, a level
+    // this stream has seen (this pass index) gets the largest count per path any chunk needed
+    // x chain_est_pct + 1/32: a chunk that outgrows it sets ch_ovf, its remaining launches
+    // return at once and chain_fallback renders its units with the fused chain shading --
+    // the same frame, at the fused kernel's speed for that chunk only.
+    const int pi = std::min(P0.adapt_n, kEstPasses - 1);
+    if (g_chain_est && !c.est_dev) {
+        HIP_OK(hipMalloc((void**)&c.est_dev, kEstPasses * 64 * sizeof(uint32_t)));
+        HIP_OK(hipMemsetAsync(c.est_dev, 0, kEstPasses * 64 * sizeof(uint32_t), stream));
+        HIP_OK(hipHostMalloc((void**)&c.est_pinned, kEstPasses * 64 * sizeof(uint32_t)));
+        HIP_OK(hipEventCreateWithFlags(&c.est_ev, hipEventDisableTiming));
+        c.est.assign(kEstPasses * 64, 0u);
+    }
+    if (c.est_pending && hipEventQuery(c.est_ev) == hipSuccess) {   // the last copy has landed: no wait
+        std::copy(c.est_pinned, c.est_pinned + kEstPasses * 64, c.est.begin());
+        c.est_pending = false;
+    }
+    std::vector<uint64_t> capr(L);
+    uint64_t capr_sum = 0, capr_max = 0;
+    for (int k = 0; k < L; k++) {
+        const uint64_t worst = level_mult(s, k) << 16;
+        uint64_t r = worst;
+        const uint32_t e = g_chain_est && k > 0 ? c.est[(size_t)pi * 64 + k] : 0u;
+        if (e != 0u && e != 0xFFFFFFFFu) r = std::min(worst, (uint64_t)(e - 1) * (uint64_t)g_chain_est_pct / 100 + 2048);
+        capr[k] = r;
+        capr_sum += r;
+        capr_max = std::max(capr_max, r);
+    }
     // per path over all levels: ray + ior 2 x 32 B, hit 16, value 16, record 4 W, child map 4 split,
     // shadow rays m x (32 B + occlusion byte) + ray count; sparse spawn slots 65 B x split x the widest level
     const uint64_t entry_bytes = 32 + 32 + 16 + 16 + 4 * (uint64_t)W + 4 * (uint64_t)split + (uint64_t)m * 33 + 1;
-    const uint64_t path_bytes = mult_sum * entry_bytes + mult_max * (uint64_t)split * 65;
+    const uint64_t path_bytes = (capr_sum * entry_bytes + capr_max * (uint64_t)split * 65 + 65535) >> 16;
     const uint64_t unit_bytes = np * path_bytes + (P0.adapt_n ? 16 : 0);
     uint64_t budget = (uint64_t)g_chain_mb << 20;
     size_t mem_free = 0, mem_total = 0;   // this stream's current chunk can be reused: count it as free
@@ -1556,15 +1614,25 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     uint64_t per = std::max<uint64_t>(1, budget / unit_bytes);
     per = std::max<uint64_t>(unit_align, per / unit_align * unit_align);
     per = std::min<uint64_t>(per, (units_max + unit_align - 1) / unit_align * unit_align);
-    const uint64_t paths = per * np, entries = paths * mult_sum, spcap = paths * mult_max * (uint64_t)split;
+    const uint64_t paths = per * np;
+    std::vector<uint64_t> lcap(L);
+    uint64_t entries = 0, lmax = 0;
+    for (int k = 0; k < L; k++) {
+        lcap[k] = k == 0 ? paths : std::max<uint64_t>(64, (paths * capr[k] + 65535) >> 16);
+        entries += lcap[k];
+        lmax = std::max(lmax, lcap[k]);
+    }
+    const uint64_t spcap = lmax * (uint64_t)split;
     if (entries * (uint64_t)m >= (uint64_t(1) << 32) || spcap >= (uint64_t(1) << 32)) {
         set_error("chain chunk too large"); return MRT_ERR_INVALID;
     }
     int rc;
     if ((rc = ensure_rays(c, entries, (size_t)m))) return rc;   // every level keeps its shadow rays
     // layout: ray | ior (2 per entry) | hit | val | spawn (4 per slot) | uhits (float4), rec (float),
-    // map (u32), control (counts + queues), flag (u8)
-    const size_t ctl = 256 + (size_t)(2 * L + 3) * 1024;   // counts; trace + resolve queues; chain shadow-launch queues
+    // map (u32), control (counts, trace + resolve + chain shadow-launch queues, the chunk's
+    // statistics, its overflow flag), flag (u8)
+    const size_t ctl_q = 256 + (size_t)(2 * L + 3) * 1024;
+    const size_t ctl = ctl_q + 256 + 64;
     const uint64_t n4 = 2 * entries + 2 * entries + entries + entries + 4 * spcap + (P0.adapt_n ? per : 0);
     const uint64_t bytes = n4 * 16 + entries * (uint64_t)W * 4 + entries * (uint64_t)split * 4 + ctl + spcap;
     if (bytes > c.chain_bytes) {
@@ -1585,6 +1653,10 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     Q.ch_map = reinterpret_cast<uint32_t*>(Q.ch_rec + entries * (uint64_t)W);
     Q.ch_cnt = Q.ch_map + entries * (uint64_t)split;           // 64 counts, then L + 2 queues
     unsigned int* queues = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(Q.ch_cnt) + 256);
+    Q.ctr_out = P0.ctr;
+    Q.ctr = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(Q.ch_cnt) + ctl_q);
+    Q.ch_ovf = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(Q.ch_cnt) + ctl_q + 256);
+    Q.ch_est = g_chain_est ? c.est_dev + (size_t)pi * 64 : nullptr;
     Q.ch_flag = reinterpret_cast<uint8_t*>(Q.ch_cnt) + ctl;
     Q.ch_spcap = (uint32_t)spcap;
     Q.ch_split = split;
@@ -1592,7 +1664,7 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     uint64_t off = 0;
     for (int k = 0; k <= L; k++) {
         Q.ch_lofs[k] = (uint32_t)off;
-        if (k < L) off += paths * level_mult(s, k);
+        if (k < L) off += lcap[k];
     }
     Q.lvl_words = W;
     Q.ch_bands = g_chain_bands > 0 || (g_chain_bands < 0 && (bin_mode(d) & 6));
@@ -1608,6 +1680,11 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     for (uint64_t b = 0; b < units_max; b += per) {
         Q.unit_base = (uint32_t)b;
         if ((rc = chain_chunk(s, c, Q, count, stream, ctl, queues))) return rc;
+    }
+    if (g_chain_est) {   // this pass's estimates to the host, read by a later frame once they have landed
+        HIP_OK(hipMemcpyAsync(c.est_pinned, c.est_dev, kEstPasses * 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipEventRecord(c.est_ev, stream));
+        c.est_pending = true;
     }
     return MRT_OK;
 }
@@ -2796,6 +2873,7 @@ int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     S.last.chain = x.last_was_render && x.chain_used ? 1 : 0;
     S.last.chain_budget_bytes = x.chain_budget;
     S.last.chain_chunks = x.chain_chunks;
+    S.last.chain_fallbacks = (int32_t)c[CTR_FALLBACK];
     *out = S.last;
     if (c[CTR_OVERFLOW]) { set_error("traversal stack overflow"); return MRT_ERR_OVERFLOW; }
     return MRT_OK;
@@ -2949,6 +3027,11 @@ int mrt_set_tuning(const char* key, int value) {
         g_refill_min = value;
     } else if (k == "fused") {
         g_fused = value ? 1 : 0;
+    } else if (k == "chain_est") {
+        g_chain_est = value ? 1 : 0;
+    } else if (k == "chain_est_pct") {
+        if (value < 1 || value > 100000) { set_error("chain_est_pct must be 1..100000"); return MRT_ERR_INVALID; }
+        g_chain_est_pct = value;
     } else if (k == "chain_shadow_refill") {
         g_chain_shadow_refill = value ? 1 : 0;
     } else if (k == "bin_inst") {

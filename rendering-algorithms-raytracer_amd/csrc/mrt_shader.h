@@ -19,7 +19,8 @@ enum { CTR_SHADOW = 0, CTR_NODES = 1, CTR_LEAVES = 2, CTR_MAXSP = 3, CTR_OVERFLO
        CTR_RAYS_P = 18,  // eye rays traced (adaptive supersampling; otherwise one per pixel)
        CTR_SECONDARY = 19,  // Blinn reflection / refraction rays
        CTR_WAVE_STEPS_S = 20, CTR_NODES_S = 21,  // count mode, shadow_kernel: wave loop steps, node visits
-       CTR_N = 22 };
+       CTR_FALLBACK = 22,  // chain chunks that outgrew an estimated level capacity (rendered by the fallback)
+       CTR_N = 23 };
 static constexpr int kMaxBlocksPerCU = 8;
 // wave log record: start, end, tiles, node visits, then (tile id << 40 | start tick) of the first kLogTiles
 // tiles, then the wall-clock ticks each of those tiles' dequeue took
@@ -165,6 +166,13 @@ struct RenderParams {
     const float4* verts2;
     int32_t has_mb;
     int32_t mat_env;             // some material has its own environment map (Material::m_envMap)
+    // chain chunks on estimated level capacities: ch_ovf = the chunk outgrew one (its later
+    // launches do nothing, chain_fallback_kernel renders its units); the chunk's statistics
+    // go to ctr and are added to ctr_out unless it did; ch_est = per level, the largest
+    // entries per path seen (x 65536, + 1; atomicMax) for this pass index on this stream
+    uint32_t* ch_ovf;
+    unsigned long long* ctr_out;
+    uint32_t* ch_est;
 };
 
 // pow(spec, specExp) of Blinn::shade (src/Blinn.cpp:219-220; libm powf in the
@@ -1561,6 +1569,8 @@ KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec);
 KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec);
 KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves);
 KernelFn pick_chain_compact();
+KernelFn pick_chain_merge();
+KernelFn pick_chain_fallback(bool po, bool inst, int rec);
 KernelFn pick_chain_finish();
 KernelFn pick_chain_fold();
 KernelFn pick_unit_eye(bool c, bool f, bool inst);

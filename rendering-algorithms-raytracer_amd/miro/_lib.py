@@ -81,7 +81,7 @@ class mrt_stats(C.Structure):
                 ("shade_span_us", C.c_float), ("shade_ramp_us", C.c_float), ("shade_tail_us", C.c_float),
                 ("secondary_rays", C.c_uint64), ("shadow_wave_steps", C.c_uint64), ("shadow_node_visits", C.c_uint64),
                 ("fused", C.c_int32), ("chain", C.c_int32), ("chain_budget_bytes", C.c_uint64),
-                ("chain_chunks", C.c_uint32), ("reserved", C.c_int32)]
+                ("chain_chunks", C.c_uint32), ("chain_fallbacks", C.c_int32)]
 
 
 _fp = C.POINTER(C.c_float)

@@ -163,6 +163,32 @@ def test_chain_tree_and_adaptive_chunks_equal_one_chunk(case):
     assert_same(one, many)
 
 
+@pytest.mark.parametrize("case", ["disp_cornell_mixed", "adapt_disp_env", "pt_rect_panel", "adapt_mixed_rect"])
+def test_chain_estimated_capacities_and_fallback_equal_worst_case(case):
+    """Level capacities from the counts earlier chunks needed (chain_est) give the
+    worst-case-sized frame; with the headroom cut to 1% every chunk outgrows a level
+    and the fallback (the fused chain shading over the chunk's units) must give the
+    same frame and ray counts -- in one chunk and in many."""
+    P, _, cam = CASES[case]()
+    try:
+        tuned(chain_est=0)
+        worst = render(P, cam, 48, 40)
+        tuned(chain_est=1)
+        render(P, cam, 48, 40)           # seeds this stream's estimates
+        est = render(P, cam, 48, 40)
+        tuned(chain_est_pct=1)
+        fb = render(P, cam, 48, 40)
+        tuned(chain_mb=2)
+        fb_many = render(P, cam, 48, 40)
+    finally:
+        tuned(chain_est=1, chain_est_pct=125, chain_mb=49152)
+    assert worst[2]["chain_fallbacks"] == 0 and est[2]["chain_fallbacks"] == 0
+    assert fb[2]["chain_fallbacks"] >= 1 and fb_many[2]["chain_fallbacks"] >= 1
+    for other in (est, fb, fb_many):
+        assert_same(worst, other)
+        assert other[2]["primary_rays"] == worst[2]["primary_rays"]
+
+
 def test_chain_engine_on_instances_with_mirrors():
     """ProxyObject instances (nested BLAS traversal in the trace and shadow
     kernels, inverse-transpose normals in the shading) under reflection."""

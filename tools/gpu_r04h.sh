@@ -12,3 +12,4 @@ for v in 0 1; do
     --no-cpu-baseline --tune chain_shadow_refill=$v > gpurun_out/bench_FS_small_csr$v.log 2>&1
   rc=$?; tail -1 gpurun_out/bench_FS_small_csr$v.log | cut -c1-200; [ $rc -eq 0 ] || exit $rc
 done
+bash tools/gpu_g3prof.sh
