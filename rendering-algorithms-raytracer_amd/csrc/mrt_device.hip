@@ -682,7 +682,7 @@ static int g_near_first = -1;     // any-hit walks take the nearest hit child fi
                                   // -12.6%; off in the refill one, C5 +4.5%, the instanced chunked one,
                                   // C5 +15%, and the fused kernels, C3 +5%, A3 / R3 +2%)
 static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
-static int g_chain_shadow_refill = 1;   // instanced chain levels: shadow rays on the lane-refill kernel (FS / C5-like scenes)
+static int g_chain_shadow_refill = 0;   // instanced chain levels: shadow rays on the lane-refill kernel (FS: 6% slower, profiles/r04_fs_chain_shadow_refill_ab.txt)
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
 static int g_chain_est = 1;       // chain levels sized by the entries earlier chunks needed (0: worst case, 3^ceil(k/2))
 static int g_chain_est_pct = 125; //   headroom over the largest count per path seen, percent

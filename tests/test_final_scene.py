@@ -113,7 +113,7 @@ def test_final_scene_chain_shadow_schedules_give_identical_frames():
             hits = P.raytraceImage(camera(cam), img, want_hits=True)
             out.append((img, hits, dict(P.last_stats)))
     finally:
-        L.mrt_set_tuning(b"chain_shadow_refill", 1)
+        L.mrt_set_tuning(b"chain_shadow_refill", 0)
     (a, ha, sa), (b, hb, sb) = out
     assert np.array_equal(ha["prim"], hb["prim"])
     assert np.array_equal(bits(a.rgb), bits(b.rgb)) and np.array_equal(a.pixels, b.pixels)
