@@ -1618,7 +1618,9 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     std::vector<uint64_t> lcap(L);
     uint64_t entries = 0, lmax = 0;
     for (int k = 0; k < L; k++) {
-        lcap[k] = k == 0 ? paths : std::max<uint64_t>(64, (paths * capr[k] + 65535) >> 16);
+        // whole 64-entry groups: every array's level slice stays aligned (the u64 statistics
+        // after the maps need 8-byte alignment) and a wave's 64 entries share a group
+        lcap[k] = k == 0 ? paths : std::max<uint64_t>(64, (((paths * capr[k] + 65535) >> 16) + 63) / 64 * 64);
         entries += lcap[k];
         lmax = std::max(lmax, lcap[k]);
     }
@@ -1657,6 +1659,7 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     Q.ctr = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(Q.ch_cnt) + ctl_q);
     Q.ch_ovf = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(Q.ch_cnt) + ctl_q + 256);
     Q.ch_est = g_chain_est ? c.est_dev + (size_t)pi * 64 : nullptr;
+    if (reinterpret_cast<uintptr_t>(Q.ctr) % 8 != 0) { set_error("chain layout misaligned"); return MRT_ERR_INVALID; }
     Q.ch_flag = reinterpret_cast<uint8_t*>(Q.ch_cnt) + ctl;
     Q.ch_spcap = (uint32_t)spcap;
     Q.ch_split = split;
