@@ -686,9 +686,9 @@ static int g_chain_shadow_refill = 0;   // instanced chain levels: shadow rays o
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
 static int g_chain_est = 1;       // chain levels sized by the entries earlier chunks needed (0: worst case, 3^ceil(k/2))
 static int g_chain_est_pct = 125; //   headroom over the largest count per path seen, percent
-static int g_chain_mb = 49152;    // chain scratch per stream (MB), at most 80% of the device's free memory; larger
-                                  // frames run in chunks of work items (G3: 16 GB -> 48 GB, 76.9 -> 47.2 ms per frame,
-                                  // profiles/r03_g3_chain_mb_ab.txt)
+static int g_chain_mb = 8192;     // chain scratch per stream (MB), at most 80% of the device's free memory; larger frames
+                                  // run in chunks of work items.  With estimated level capacities 8 GB costs G3 3% against
+                                  // 48 GB and R3 / P4 / FS nothing (profiles/r04_chain_mb_est_ab.txt)
 static int g_chain_adapt = 1;     // adaptive supersampling of REC scenes: passes over the chain engine (0: fused kernel)
 static int g_fused = 1;           // one point light, one path: frame1_kernel (primary + shading in one launch)
 static int g_frame1_waves = 7;    // frame1_kernel launch-bounds occupancy target: 1 (none), 5..8 (7: -0.9% per frame with

@@ -11,7 +11,7 @@ import miro
 from helpers import bits, camera, config_scene
 from test_chain import CASES
 
-KNOB_DEFAULTS = dict(bin=-1, bin_dbits=2, bin_obits=2, dome_replay=1, chain=1, chain_mb=49152, chain_bands=-1,
+KNOB_DEFAULTS = dict(bin=-1, bin_dbits=2, bin_obits=2, dome_replay=1, chain=1, chain_mb=8192, chain_bands=-1,
                      shadow_sched=-1, bin_inst=0, primary_inst_waves=5)
 
 

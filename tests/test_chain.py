@@ -86,7 +86,7 @@ def both_engines(P, cam, W, H):
         tuned(chain=1)
         chain = render(P, cam, W, H)
     finally:
-        tuned(chain=1, chain_mb=49152)
+        tuned(chain=1, chain_mb=8192)
     return fused, chain
 
 
@@ -159,7 +159,7 @@ def test_chain_tree_and_adaptive_chunks_equal_one_chunk(case):
         tuned(chain_mb=2)
         many = render(P, cam, 48, 40)
     finally:
-        tuned(chain_mb=49152)
+        tuned(chain_mb=8192)
     assert_same(one, many)
 
 
@@ -181,7 +181,7 @@ def test_chain_estimated_capacities_and_fallback_equal_worst_case(case):
         tuned(chain_mb=2)
         fb_many = render(P, cam, 48, 40)
     finally:
-        tuned(chain_est=1, chain_est_pct=125, chain_mb=49152)
+        tuned(chain_est=1, chain_est_pct=125, chain_mb=8192)
     assert worst[2]["chain_fallbacks"] == 0 and est[2]["chain_fallbacks"] == 0
     assert fb[2]["chain_fallbacks"] >= 1 and fb_many[2]["chain_fallbacks"] >= 1
     for other in (est, fb, fb_many):
@@ -209,7 +209,7 @@ def test_chain_chunks_equal_one_chunk():
         tuned(chain_mb=1)
         many = render(P, cam, 70, 50)
     finally:
-        tuned(chain_mb=49152)
+        tuned(chain_mb=8192)
     assert_same(one, many)
 
 
