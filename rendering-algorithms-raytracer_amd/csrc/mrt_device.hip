@@ -950,6 +950,12 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     append(s.nodes, s.leaves, &s.obj_inst, nullptr);
     std::vector<int32_t> blas_root(s.blas.size());
     for (size_t b = 0; b < s.blas.size(); b++) blas_root[b] = append(s.blas[b].nodes, s.blas[b].leaves, nullptr, &s.blas[b]);
+    // pad[0]: the parent node (-1 at a root) -- read only by the stackless walk (traverse_sl,
+    // an A/B build); the stack walks never look at it
+    for (QNode& q : DN) q.pad[0] = 0xFFFFFFFFu;
+    for (size_t i = 0; i < DN.size(); i++)
+        for (int k = 0; k < 4; k++)
+            if (DN[i].child[k] >= 0) DN[(size_t)DN[i].child[k]].pad[0] = (uint32_t)i;
     if ((rc = upload(d.nodes, DN.data(), DN.size() * sizeof(QNode), total))) return rc;
     std::vector<DevInstance> DI(s.instances.size());
     for (size_t i = 0; i < DI.size(); i++) {

@@ -577,6 +577,105 @@ __device__ bool traverse_fast(const Trav& c, const DRay& r, float tMin, DHit& h,
     return hit;
 }
 
+// Stackless form of traverse_impl<FAST = true> for plain scenes (A/B build
+// MRT_TRAV_STACKLESS; north_star's "stackless traversal"): no LDS or HBM stack.
+// Per depth the walk keeps the 4-bit mask of hit inner slots it has still to
+// visit (a 128-bit trail in registers); it descends into the highest hit slot,
+// and when a node has no hit inner slot it climbs back through the parent words
+// (QNode::pad[0]) to the deepest level with slots left and takes the highest of
+// them.  That is the order the stack walk pops its pushes in, with the masks of
+// the same box tests, so the same nodes are tested with the same t: the same
+// hits and visit counts.  The price is one dependent parent load per level
+// climbed instead of one LDS read per pop.
+template <bool ANY, bool COUNT>
+__device__ bool traverse_sl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
+    int32_t cur = 0;
+    int d = 0;
+    uint64_t lo = 0, hi = 0;   // trail: 4 bits per depth, depths 0-15 in lo, 16-31 in hi
+    bool hit = false;
+    while (true) {
+        int m;
+        int4 ch;
+        const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
+        float tn[4] = {0.f, 0.f, 0.f, 0.f};
+        if ((c.scalar_nodes & 1) && __ballot(cur != c0) == 0) {
+            typedef const __attribute__((address_space(4))) float cfloat;
+            typedef const __attribute__((address_space(4))) int32_t cint;
+            cfloat* q = (cfloat*)(const void*)(c.nodes + c0);
+            cint* qc = (cint*)(q + 24);
+            ch = make_int4(qc[0], qc[1], qc[2], qc[3]);
+            float4 bx[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
+            m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_fast(bx, r, tMin, h.t);
+            asm volatile("; mrt: scalar node (stackless)" : "+v"(m));
+        } else {
+            const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
+            ch = reinterpret_cast<const int4*>(q)[6];
+            m = (ANY && c.near_first) ? box_test_fast_t(q, r, tMin, h.t, tn) : box_test_fast(q, r, tMin, h.t);
+            asm volatile("; mrt: vector node (stackless)" : "+v"(m));
+        }
+        if (COUNT) {
+            st.nodes++;
+            if (__ballot(cur != c0) == 0) st.uniform++;
+        }
+        const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
+        const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
+                           (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
+        const int inner = m & isinner;
+        int lm = m & isleaf;
+        if (lm) {
+            uint32_t leaf = 0;
+            int k = 0, cnt = 0;
+            while (true) {
+                if (k == cnt) {
+                    if (!lm) break;
+                    const int s = __builtin_ctz((unsigned)lm);
+                    lm &= lm - 1;
+                    const uint32_t v = ~(uint32_t)sel4(ch, s);
+                    leaf = v >> 4;
+                    cnt = (int)(v & 3u) + 1;
+                    k = 0;
+                    if (COUNT) st.leaves++;
+                }
+                float t, a, b;
+                if (tri_test_lane(c, leaf, k, r, tMin, h.t, t, a, b)) {
+                    if (ANY) return true;
+                    h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
+                    hit = true;
+                }
+                k++;
+            }
+        }
+        if (inner) {   // descend into the highest hit slot (nearest in any-hit near-first mode)
+            const int top = (ANY && c.near_first) ? nearest_slot(inner, tn) : 31 - __builtin_clz((unsigned)inner);
+            const uint64_t rest = (uint64_t)(inner ^ (1 << top));
+            if (d >= 32) { st.overflow = true; return hit; }
+            if (d < 16) lo |= rest << (4 * d);
+            else hi |= rest << (4 * (d - 16));
+            if (COUNT && d + 1 > st.max_sp) st.max_sp = d + 1;
+            cur = sel4(ch, top);
+            d++;
+            continue;
+        }
+        // climb to the deepest level with slots left (levels below the current one are empty)
+        int e;
+        if (hi) e = 16 + (63 - __builtin_clzll(hi)) / 4;
+        else if (lo) e = (63 - __builtin_clzll(lo)) / 4;
+        else break;   // nothing left: the walk is over
+        for (; d > e; d--) cur = (int32_t)c.nodes[cur].pad[0];
+        const int sh = 4 * (e & 15);
+        const int nib = (int)(((e < 16 ? lo : hi) >> sh) & 15u);
+        const int s = 31 - __builtin_clz((unsigned)nib);
+        const uint64_t clear = ~((uint64_t)1 << (sh + s));
+        if (e < 16) lo &= clear;
+        else hi &= clear;
+        cur = c.nodes[cur].child[s];
+        d = e + 1;
+    }
+    return hit;
+}
+
 struct NodeData {
     float4 b[6];
     int4 ch;
@@ -880,6 +979,10 @@ __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMi
     // launch but equal at 4 frames in flight, C2 / C4 within 0.5% -- not the default.
     const bool hit = (FAST && r.finite) ? (INST ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
                                                 : traverse_fast<ANY, COUNT>(c, r, tMin, h, st))
+                                        : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
+#elif defined(MRT_TRAV_STACKLESS)   // A/B build (make variant NAME=sl EXTRA=-DMRT_TRAV_STACKLESS)
+    const bool hit = (FAST && r.finite) ? (INST ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
+                                                : traverse_sl<ANY, COUNT>(c, r, tMin, h, st))
                                         : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
 #else
     const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
