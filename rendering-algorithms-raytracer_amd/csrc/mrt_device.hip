@@ -352,7 +352,12 @@ template <bool COUNT, bool FAST, int MINW, bool POW>
 __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
-    load_tables(P.tables, s_tab, 1024);
+#ifdef MRT_LDS_NODES   // A/B build: the hierarchy's top nodes (host-renumbered to 0 .. MRT_LDS_NODES - 1) in LDS
+    __shared__ QNode s_top[MRT_LDS_NODES];
+    for (int i = threadIdx.x; i < MRT_LDS_NODES * 32; i += kWG)
+        reinterpret_cast<uint32_t*>(s_top)[i] = reinterpret_cast<const uint32_t*>(P.nodes)[i];
+#endif
+    load_tables(P.tables, s_tab, 1024);   // (its barrier also covers s_top)
     const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
     const uint16_t* rcpT = s_tab;
     const uint16_t* rsqT = P.tables + 2048;
@@ -360,6 +365,9 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
+#ifdef MRT_LDS_NODES
+    T.lnodes = s_top;
+#endif
     TravStats st, ss;   // primary / shadow rays (count mode)
     uint32_t nhits = 0, shadow_total = 0;
     unsigned long long wave_steps = 0;
@@ -950,6 +958,32 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     append(s.nodes, s.leaves, &s.obj_inst, nullptr);
     std::vector<int32_t> blas_root(s.blas.size());
     for (size_t b = 0; b < s.blas.size(); b++) blas_root[b] = append(s.blas[b].nodes, s.blas[b].leaves, nullptr, &s.blas[b]);
+#ifdef MRT_LDS_NODES
+    {   // A/B build: renumber the world hierarchy's first MRT_LDS_NODES nodes in breadth-first
+        // order to 0 .. MRT_LDS_NODES - 1 (frame1_kernel stages them in LDS).  Node numbers are
+        // internal to the device: the visit order follows the child slots, not the numbers.
+        const size_t nw = s.nodes.size();
+        std::vector<int32_t> bfs{0};
+        for (size_t q = 0; q < bfs.size() && bfs.size() < (size_t)MRT_LDS_NODES; q++)
+            for (int k = 0; k < 4 && bfs.size() < (size_t)MRT_LDS_NODES; k++)
+                if (DN[(size_t)bfs[q]].child[k] >= 0) bfs.push_back(DN[(size_t)bfs[q]].child[k]);
+        std::vector<int32_t> perm(DN.size(), -1);
+        for (size_t i = 0; i < bfs.size(); i++) perm[(size_t)bfs[i]] = (int32_t)i;
+        int32_t next = (int32_t)bfs.size();
+        for (size_t i = 0; i < nw; i++)
+            if (perm[i] < 0) perm[i] = next++;
+        for (size_t i = nw; i < DN.size(); i++) perm[i] = (int32_t)i;
+        std::vector<QNode> R(DN.size());
+        for (size_t i = 0; i < DN.size(); i++) {
+            QNode q = DN[i];
+            for (int k = 0; k < 4; k++)
+                if (q.child[k] >= 0) q.child[k] = perm[(size_t)q.child[k]];
+            R[(size_t)perm[i]] = q;
+        }
+        DN.swap(R);
+        for (int32_t& br : blas_root) br = perm[(size_t)br];
+    }
+#endif
     // pad[0]: the parent node (-1 at a root) -- read only by the stackless walk (traverse_sl,
     // an A/B build); the stack walks never look at it
     for (QNode& q : DN) q.pad[0] = 0xFFFFFFFFu;

@@ -82,6 +82,7 @@ struct Trav {
     const float4* verts = nullptr;
     const float4* verts2 = nullptr;
     bool near_first = false;   // any-hit walks descend into the nearest hit child first (order-free answer)
+    const QNode* lnodes = nullptr;   // A/B build MRT_LDS_NODES: the top of the hierarchy staged in LDS
 };
 
 struct TravStats {
@@ -357,6 +358,17 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         // 64 copies through the vector memory path.
         const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
         float tn[4] = {0.f, 0.f, 0.f, 0.f};   // slot entry distances (any-hit near-first order)
+#ifdef MRT_LDS_NODES   // A/B build: the first MRT_LDS_NODES nodes (the top levels, host-renumbered) from LDS
+        if (FAST && c.lnodes && c0 < MRT_LDS_NODES && __ballot(cur != c0) == 0) {
+            const QNode& nd = c.lnodes[c0];   // one wave-uniform LDS address: broadcast reads
+            ch = make_int4(nd.child[0], nd.child[1], nd.child[2], nd.child[3]);
+            float4 bx[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) bx[k] = make_float4(nd.box[4 * k], nd.box[4 * k + 1], nd.box[4 * k + 2], nd.box[4 * k + 3]);
+            m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_fast(bx, r, tMin, h.t);
+            asm volatile("; mrt: lds node" : "+v"(m));
+        } else
+#endif
         if (FAST && (c.scalar_nodes & 1) && __ballot(cur != c0) == 0) {
             // constant address space + uniform address -> s_load_dwordx16 (node
             // data is read-only for the whole launch)
