@@ -383,18 +383,23 @@ def main():
 
     depth = max(1, args.inflight)
 
-    def make_pipe(nf, float_tiles, nsplit=None, srank=None, pipe_streams=None):
+    def make_pipe(nf, float_tiles, nsplit=None, srank=None, pipe_streams=None, share_unpack="own"):
         """This rank's share of an nf-frame step (items id mod N), its render /
         unpack closures and the gather pipeline over `depth` buffers and streams
         (--inflight).  nsplit / srank: the share of rank srank of an nsplit-way
-        split rendered without the gather (bench.py --share)."""
+        split rendered without the gather (bench.py --share); share_unpack "none":
+        no unpack (a rank > 0 of the split only renders and sends), "full": rank 0's
+        unpack of all nsplit shares' tiles each step (its buffers hold nsplit shares)."""
         nsplit = world if nsplit is None else nsplit
         srank = rank if srank is None else srank
         cams_ = [cam] if nf == 1 else [_camera(c) for c in scenes.camera_path(cfg["camera"], nf)]
         cc = (_lib.mrt_camera * nf)(*[c._c() for c in cams_])
         mine, all_ids, per = tiles_mod.split_items(bpf * nf, nsplit, srank)
-        if nsplit != world:   # one share on its own: its unpadded items are the whole "gathered" buffer
+        shares = 1
+        if nsplit != world and share_unpack != "full":   # one share on its own: its unpadded items are the whole "gathered" buffer
             all_ids = mine
+        elif nsplit != world:   # rank 0 of the split: every share's (padded) tiles unpacked each step
+            shares = nsplit
         items = torch.tensor(mine, dtype=torch.int32, device="cuda")
         all_items = torch.tensor(all_ids, dtype=torch.int32, device="cuda")
         out_f = [torch.empty(nf * H * W * 3, dtype=torch.float32, device="cuda") for _ in range(depth)] \
@@ -408,6 +413,8 @@ def main():
                                                 torch.cuda.current_stream().cuda_stream), "render batch")
 
         def unpack(ids, gathered, b):
+            if share_unpack == "none":
+                return
             gf, g8 = (gathered.data_ptr(), None) if float_tiles else (None, gathered.data_ptr())
             _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(ids), gf, g8, W, H, nf,
                                                 out_f[b].data_ptr() if float_tiles else None, out_8[b].data_ptr(),
@@ -415,7 +422,7 @@ def main():
 
         # `depth` streams: consecutive steps' launches overlap (libmrt keeps scratch per stream)
         pipe = tiles_mod.BatchPipeline(world, rank, dist, items, all_items,
-                                       lambda k: torch.empty(k * per * 1024 * 3, dtype=dt, device="cuda"),
+                                       lambda k: torch.empty(k * shares * per * 1024 * 3, dtype=dt, device="cuda"),
                                        render, unpack,
                                        streams=pipe_streams or [torch.cuda.Stream() for _ in range(depth)])
         for b in range(depth):   # per-stream scratch allocated before any timing
@@ -715,10 +722,11 @@ def share_mode(args, E, widths):
 
     The whole frame first (the N = 1 frame path with --inflight streams); then, per
     split width N, every rank r's share of buckets (id mod N == r) rendered alone
-    through the split pipeline (render into float tiles + unpack of its own tiles,
-    --inflight buffers and streams, no gather), and rank 0's unpack of a whole
-    gathered frame.  The N-GPU step is modeled as
-        max(slowest share + rank 0's full-frame unpack, gather)
+    through the split pipeline (--inflight buffers and streams, no gather): ranks
+    r > 0 render into float tiles only; rank 0 renders its share and unpacks all N
+    shares' tiles into the frame every step, as it does after the gather.  The
+    N-GPU step is modeled as
+        max(rank 0's render + full unpack, slowest rank > 0, gather)
     with gather = latency + (one rank's float tiles) / (per-link xGMI rate): rank 0
     receives the N - 1 other shares over N - 1 point-to-point links at once, and the
     pipeline overlaps step k's gather with step k + 1's renders.  The xGMI rate and
@@ -749,7 +757,8 @@ def share_mode(args, E, widths):
     for N in widths:
         per_rank = []
         for r in range(N):
-            pipe, render, items, mine, _ = E["make_pipe"](1, True, nsplit=N, srank=r, pipe_streams=share_streams)
+            pipe, render, items, mine, _ = E["make_pipe"](1, True, nsplit=N, srank=r, pipe_streams=share_streams,
+                                                          share_unpack="full" if r == 0 else "none")
             _, (sh, eye, sec) = E["count_rays"](lambda: render(items, pipe.tiles[0], E["opts_count"]))
             px = sum(min(32, W - (b % ((W + 31) // 32)) * 32) * min(32, H - (b // ((W + 31) // 32)) * 32) for b in mine)
             e = E["timed"](pipe.step, pipe.flush, args.steps)
@@ -795,14 +804,15 @@ def share_mode(args, E, widths):
         unpack_ms = float(np.median(un[2:]))
         tile_bytes = per * 1024 * 3 * 4
         gather_ms = args.xgmi_lat_us * 1e-3 + tile_bytes / (args.xgmi_gbs * 1e9) * 1e3
-        slow = max(per_rank, key=lambda x: x["ms_per_step"])
-        step_ms = max(slow["ms_per_step"] + unpack_ms, gather_ms)
+        slow = max(per_rank, key=lambda x: x["ms_per_step"])   # rank 0's line includes its full unpack
+        step_ms = max(slow["ms_per_step"], gather_ms)
         out["shares"][str(N)] = {
-            "per_rank": per_rank, "slowest_rank_ms": slow["ms_per_step"],
+            "per_rank": per_rank, "slowest_rank_ms": slow["ms_per_step"], "slowest_rank": slow["rank"],
+            "rank0_render_plus_unpack_ms": per_rank[0]["ms_per_step"],
             "mean_rank_ms": round(sum(x["ms_per_step"] for x in per_rank) / N, 4),
-            "unpack_ms_rank0": round(unpack_ms, 4), "gather_bytes_per_rank": tile_bytes,
+            "unpack_ms_rank0_alone": round(unpack_ms, 4), "gather_bytes_per_rank": tile_bytes,
             "gather_ms_model": round(gather_ms, 4), "step_ms_model": round(step_ms, 4),
-            "bound": "render" if slow["ms_per_step"] + unpack_ms >= gather_ms else "gather",
+            "bound": "render" if slow["ms_per_step"] >= gather_ms else "gather",
             "predicted_mray_s": round(rays_full / (step_ms * 1e-3) / 1e6, 1),
             "predicted_speedup": round(frame_ms / step_ms, 3)}
     print(json.dumps(out), flush=True)
