@@ -47,7 +47,7 @@ NODE_B, LEAF_B = 128, 160      # QNode / DLeaf bytes (csrc/mrt_types.h)
 # rocprofv3 evidence of this round (tools/prof_all.sh + tools/prof3.py): per config and
 # bench pass, HBM bytes per launch (PMC) and the rocprof average duration at one
 # frame in flight; per kernel, the SQ / TCP latency counters
-PROFILE_FILE = os.path.join(ROOT, "profiles", "r03_profile.json")
+PROFILE_FILE = os.path.join(ROOT, "profiles", "r04_profile.json")
 CPU_CAL_FILE = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
 # kernel traces of the driver-settings runs (tools/step_trace.py): busy union per timed step
 STEP_TRACE_FILE = os.path.join(ROOT, "profiles", "r04_steptrace.json")
