@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mrt_types.h"
+
 namespace mrt {
 
 static constexpr int kBinBits = 12;                 // at most 4096 bins (16 KB LDS histogram)
@@ -41,6 +43,12 @@ struct BinArgs {
     const int32_t* hit_base;  // per instance: its first hit id (ascending)
     const uint16_t* inst_class;
     int32_t n_inst, n_world;
+    // object-space keys (bin_inst 2): 1 << 11 | BLAS bit << 10 | the Morton code of the ray
+    // origin's cell in its BLAS's box (4 cells per axis, in object space: the same region of
+    // one BLAS across every instance of it) << 4 | direction cell.  Per instance two float4:
+    // (BLAS box lo, BLAS bit), (4 / box extent, 0); the world -> object matrices from insts.
+    const float4* inst_cell;
+    const DevInstance* insts;
     int bits;                 // key bits (set by bin_rays)
     uint16_t* keys;           // [n] scratch
     uint32_t* hist;           // [2^bits + 1] scratch; word 2^bits receives the valid count

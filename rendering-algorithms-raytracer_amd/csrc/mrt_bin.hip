@@ -68,6 +68,18 @@ __device__ __forceinline__ uint32_t bin_key_inst(const BinArgs& A, uint32_t i, f
         if (A.hit_base[mid] <= prim) lo = mid; else hi = mid - 1;
     }
     const uint32_t dir = bin_key(A, o, d) >> (3 * A.obits);   // the direction cell
+    if (A.inst_cell) {   // object-space cell of the origin in its BLAS
+        const float* M = A.insts[lo].inv;
+        const float4 c0 = A.inst_cell[2 * lo], c1 = A.inst_cell[2 * lo + 1];
+        const float ox = M[0] * o.x + M[1] * o.y + M[2] * o.z + M[3];
+        const float oy = M[4] * o.x + M[5] * o.y + M[6] * o.z + M[7];
+        const float oz = M[8] * o.x + M[9] * o.y + M[10] * o.z + M[11];
+        const uint32_t cx = (uint32_t)min(3, max(0, (int)((ox - c0.x) * c1.x)));
+        const uint32_t cy = (uint32_t)min(3, max(0, (int)((oy - c0.y) * c1.y)));
+        const uint32_t cz = (uint32_t)min(3, max(0, (int)((oz - c0.z) * c1.z)));
+        const uint32_t morton = (cx & 1u) | (cy & 1u) << 1 | (cz & 1u) << 2 | (cx >> 1) << 3 | (cy >> 1) << 4 | (cz >> 1) << 5;
+        return (1u << 11) | ((c0.w != 0.f) ? 1u << 10 : 0u) | morton << 4 | dir;
+    }
     return (1u << 11) | ((uint32_t)A.inst_class[lo] << (2 * A.dbits)) | dir;
 }
 

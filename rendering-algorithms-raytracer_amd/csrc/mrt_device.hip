@@ -618,6 +618,7 @@ struct DeviceState {
     int n_insts = 0, n_world = 0;
     int32_t* inst_hit_base = nullptr;   // per instance: hit_base (ascending), for the instance-major bin keys
     uint16_t* inst_class = nullptr;     //   and its 7-bit class (BLAS-major rank)
+    float4* inst_cell = nullptr;        //   object-space bin cells: BLAS box lo + BLAS bit, 4 / extent (2 per instance)
     DevTexture* texs = nullptr;   // material-map textures (bufs hold their data)
     uint4* puv = nullptr;         // per prim texture-coordinate indices (nullptr: no texture-mapped mesh)
     float2* uvs = nullptr;
@@ -752,7 +753,7 @@ static void free_device(DeviceState* d) {
     if (d->g_tiles) (void)hipFree(d->g_tiles);
     if (d->g_items) (void)hipFree(d->g_items);
     void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts,
-                    d->inst_hit_base, d->inst_class, d->tables,
+                    d->inst_hit_base, d->inst_class, d->inst_cell, d->tables,
                     d->gamma, d->gammaF, d->d_rgb, d->d_rgb8, d->texs, d->puv, d->uvs, d->tans, d->btans,
                     d->pflags, d->verts2};
     for (void* p : ptrs)
@@ -1012,6 +1013,27 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
         for (size_t r = 0; r < order.size(); r++) cls[order[r]] = (uint16_t)std::min<size_t>(127, r * 128 / order.size());
         if ((rc = upload(d.inst_hit_base, hb.data(), hb.size() * sizeof(int32_t), total))) return rc;
         if ((rc = upload(d.inst_class, cls.data(), cls.size() * sizeof(uint16_t), total))) return rc;
+        // object-space cells: each instance's BLAS root box (its finite child boxes), 4 cells per axis
+        std::vector<float4> cell(2 * DI.size());
+        for (size_t i = 0; i < DI.size(); i++) {
+            const QNode& R = DN[(size_t)DI[i].root];
+            float lo3[3] = {0, 0, 0}, hi3[3] = {0, 0, 0};
+            bool any3[3] = {false, false, false};
+            for (int k = 0; k < 4; k++) {
+                if (R.child[k] == kEmptySlot) continue;
+                for (int a = 0; a < 3; a++) {
+                    const float l = R.box[a * 4 + k], h = R.box[12 + a * 4 + k];
+                    if (!std::isfinite(l) || !std::isfinite(h)) continue;
+                    lo3[a] = any3[a] ? std::min(lo3[a], l) : l;
+                    hi3[a] = any3[a] ? std::max(hi3[a], h) : h;
+                    any3[a] = true;
+                }
+            }
+            auto sc = [&](int a) { return hi3[a] > lo3[a] ? 4.0f / (hi3[a] - lo3[a]) : 0.0f; };
+            cell[2 * i] = make_float4(lo3[0], lo3[1], lo3[2], (float)(s.instances[i].blas & 1));
+            cell[2 * i + 1] = make_float4(sc(0), sc(1), sc(2), 0.f);
+        }
+        if ((rc = upload(d.inst_cell, cell.data(), cell.size() * sizeof(float4), total))) return rc;
     }
     d.n_world = (int)s.obj_mesh.size();
     if ((rc = upload(d.leaves, DL.data(), DL.size() * sizeof(DLeaf), total))) return rc;
@@ -1939,6 +1961,8 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
                 A.hits = P.hits;
                 A.hit_base = d.inst_hit_base;
                 A.inst_class = d.inst_class;
+                A.inst_cell = g_bin_inst == 2 ? d.inst_cell : nullptr;   // 2: object-space cells
+                A.insts = d.insts;
                 A.n_inst = d.n_insts;
                 A.n_world = d.n_world;
             }
@@ -3078,7 +3102,8 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "chain_shadow_refill") {
         g_chain_shadow_refill = value ? 1 : 0;
     } else if (k == "bin_inst") {
-        g_bin_inst = value ? 1 : 0;
+        if (value < 0 || value > 2) { set_error("bin_inst must be 0..2"); return MRT_ERR_INVALID; }
+        g_bin_inst = value;
     } else if (k == "self_reset") {
         g_self_reset = value ? 1 : 0;
     } else if (k == "tile_lpt") {

@@ -72,7 +72,7 @@ def test_bin_tuning_validates_key_bits():
 def test_binned_shadow_pass_and_dome_replay_give_identical_frames(key, W, H):
     P, _, cam = config_scene(key)
     out = runs(P, cam, W, H, [dict(dome_replay=0, bin=0), dict(), dict(bin=1), dict(bin=1, bin_dbits=6, bin_obits=0),
-                              dict(bin=1, bin_dbits=0, bin_obits=4), dict(bin=1, dome_replay=0), dict(bin=1, bin_inst=1)])
+                              dict(bin=1, bin_dbits=0, bin_obits=4), dict(bin=1, dome_replay=0), dict(bin=1, bin_inst=1), dict(bin=1, bin_inst=2)])
     assert out[0][2]["shadow_rays"] > 0
     assert_all_same(out)
 
