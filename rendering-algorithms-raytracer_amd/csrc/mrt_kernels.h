@@ -242,7 +242,12 @@ __device__ __noinline__ bool mb_tri_test(const Trav& c, int32_t prim, const DRay
 // the reference's t-ordered retry loop.  aoff: PrimShade index of the leaf's
 // prim 0 (0 in the world; an instance's shade_base inside its BLAS, whose
 // alpha-mapped triangles -- the reference's tree proxies -- are tested too).
-__device__ __noinline__ bool alpha_rejects(const Trav& c, uint32_t leaf, int k, float a, float b, int32_t aoff) {
+#ifdef MRT_ALPHA_INLINE   // A/B build: the alpha test inlined into the walks
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+bool alpha_rejects(const Trav& c, uint32_t leaf, int k, float a, float b, int32_t aoff) {
     const int32_t prim = c.leaves[leaf].prim[k] + aoff;
     const int am = c.amats[c.aprims[prim].mat].maps[kMapAlpha];
     if (am < 0) return false;
