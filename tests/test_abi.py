@@ -30,3 +30,23 @@ def test_errors_are_reported_not_raised():
     L = miro.lib()
     assert L.mrt_scene_build_bvh(None) == -1          # MRT_ERR_INVALID, no exception
     assert b"null" in L.mrt_last_error()
+
+
+def test_chain_tuning_keys_validate():
+    """The chain engine's capacity switches (round 4): estimates on / off, the
+    headroom percentage in range, the scratch budget in range; bad values are
+    rejected with an error, not clamped."""
+    L = miro.lib()
+    try:
+        assert L.mrt_set_tuning(b"chain_est", 0) == 0
+        assert L.mrt_set_tuning(b"chain_est", 1) == 0
+        assert L.mrt_set_tuning(b"chain_est_pct", 0) != 0
+        assert L.mrt_set_tuning(b"chain_est_pct", 200000) != 0
+        assert L.mrt_set_tuning(b"chain_est_pct", 150) == 0
+        assert L.mrt_set_tuning(b"chain_mb", 0) != 0
+        assert L.mrt_set_tuning(b"bin_inst", 3) != 0
+        assert L.mrt_set_tuning(b"bin_inst", 2) == 0
+    finally:
+        assert L.mrt_set_tuning(b"chain_est_pct", 125) == 0
+        assert L.mrt_set_tuning(b"bin_inst", 0) == 0
+        assert L.mrt_set_tuning(b"chain_est", 1) == 0
