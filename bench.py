@@ -701,6 +701,10 @@ def main():
                     "them, and the environment image, are stand-ins here) and a different RNG stream"}
     if region:
         out["timed_region"] = region
+    try:   # the library's embedded source hash against the sources beside it (tools/source_hash.py)
+        out["build"] = _lib.build_info(L)
+    except Exception as e:   # reported, never fatal
+        out["build"] = {"error": str(e)}
     if tuning:
         out["tuning"] = tuning
     if split_times is not None:

@@ -95,6 +95,26 @@ class MRTError(RuntimeError):
     pass
 
 
+def build_info(L=None):
+    """The source hash embedded in the loaded libmrt.so (Makefile, tools/source_hash.py)
+    next to the hash of the sources beside it: {"library": ..., "sources": ..., "match": ...}
+    ("sources" is None where the tools are not shipped)."""
+    L = L or load()
+    try:
+        lib_hash = (C.c_char * 17).in_dll(L, "mrt_source_hash").value.decode()
+    except ValueError:
+        lib_hash = None
+    src_hash = None
+    tools = os.path.join(os.path.dirname(_PKG), "tools")
+    if os.path.exists(os.path.join(tools, "source_hash.py")):
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("mrt_source_hash", os.path.join(tools, "source_hash.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        src_hash = mod.source_hash()
+    return {"library": lib_hash, "sources": src_hash, "match": lib_hash is not None and lib_hash == src_hash}
+
+
 def load():
     """Load libmrt.so (fails loudly when the HIP build is missing)."""
     global _lib
