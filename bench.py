@@ -339,11 +339,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MRT_BENCH_REHEARSE=gloo: the N > 1 path rehearsed on ONE GPU -- every rank on cuda:0, the
+    # collectives over gloo through host copies (_HostDist); its numbers mean nothing, its job
+    # is to run the multi-rank code (split pipeline, timing, the JSON line) where only one GPU is
+    rehearse = world > 1 and os.environ.get("MRT_BENCH_REHEARSE") == "gloo"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
         import datetime
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=datetime.timedelta(seconds=300))
+        if rehearse:
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
+            dist = _HostDist(dist, torch)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=datetime.timedelta(seconds=300))
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -707,6 +716,9 @@ def main():
         out["build"] = {"error": str(e)}
     if tuning:
         out["tuning"] = tuning
+    if rehearse:
+        out["rehearsal"] = (f"MRT_BENCH_REHEARSE=gloo: {world} ranks sharing ONE GPU, collectives over gloo through "
+                            f"host copies -- a run of the multi-rank code, not a measurement")
     if split_times is not None:
         out["split_times"] = split_times
     if weak is not None:
@@ -719,6 +731,43 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+class _HostDist:
+    """torch.distributed over gloo through host copies (bench rehearsal, MRT_BENCH_REHEARSE=gloo):
+    barrier, all_reduce, gather and destroy_process_group as bench.py and BatchPipeline call them,
+    on CUDA tensors.  A gather returns an already completed work object."""
+
+    def __init__(self, dist, torch):
+        self._d, self._t = dist, torch
+        self.ReduceOp = dist.ReduceOp
+
+    def barrier(self):
+        self._d.barrier()
+
+    def all_reduce(self, t, op=None):
+        h = t.cpu()
+        self._d.all_reduce(h, op=op if op is not None else self._d.ReduceOp.SUM)
+        t.copy_(h)
+
+    def gather(self, t, outs=None, dst=0, async_op=False):
+        if t.is_cuda:
+            self._t.cuda.current_stream().synchronize()
+        h = t.cpu()
+        ho = [self._t.empty_like(h) for _ in outs] if outs is not None else None
+        self._d.gather(h, ho, dst=dst)
+        if outs is not None:
+            for o, x in zip(outs, ho):
+                o.copy_(x)
+
+        class _Done:
+            @staticmethod
+            def wait():
+                return True
+        return _Done() if async_op else None
+
+    def destroy_process_group(self):
+        self._d.destroy_process_group()
 
 
 def share_mode(args, E, widths):

@@ -89,11 +89,25 @@ def test_bucket_assignment_covers_frame_once():
         assert lens == {(nb + world - 1) // world}
 
 
-def _batch_worker(rank, world, port, W, H, n_frames, steps, result_path):
+def _batch_worker(rank, world, port, W, H, n_frames, steps, result_path, host_dist=False):
     """Each step renders a batch of n_frames cameras (shifted by the step index,
-    so a buffer mix-up between steps shows) through BatchPipeline."""
+    so a buffer mix-up between steps shows) through BatchPipeline.  host_dist: the
+    collectives through bench.py's _HostDist (its one-GPU rehearsal adapter)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    D = dist
+    if host_dist:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        D = bench._HostDist(dist, torch)
+        t = torch.tensor([float(rank + 1)])
+        D.all_reduce(t)
+        assert t.item() == world * (world + 1) / 2
+        t = torch.tensor([float(rank)])
+        D.all_reduce(t, op=D.ReduceOp.MAX)
+        assert t.item() == world - 1
+        D.barrier()
     try:
         s, cam = _oracle_scene()
         bx, by = tiles.bucket_grid(W, H)
@@ -127,7 +141,7 @@ def _batch_worker(rank, world, port, W, H, n_frames, steps, result_path):
             outs.append(frames)
 
         per = len(items)
-        pipe = tiles.BatchPipeline(world, rank, dist, items, all_items,
+        pipe = tiles.BatchPipeline(world, rank, D, items, all_items,
                                    lambda k: torch.zeros(k * per * 1024 * 3, dtype=torch.float32), render, unpack)
         for _ in range(steps):
             pipe.step()
@@ -138,12 +152,12 @@ def _batch_worker(rank, world, port, W, H, n_frames, steps, result_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_batch_pipeline_frames_equal_single_rank(tmp_path, world):
+@pytest.mark.parametrize("world,host_dist", [(2, False), (3, False), (2, True)])
+def test_batch_pipeline_frames_equal_single_rank(tmp_path, world, host_dist):
     W, H, n_frames, steps = 70, 40, 2, 3
     path = str(tmp_path / "frames.npy")
-    mp.start_processes(_batch_worker, args=(world, _free_port(), W, H, n_frames, steps, path), nprocs=world,
-                       start_method="spawn")
+    mp.start_processes(_batch_worker, args=(world, _free_port(), W, H, n_frames, steps, path, host_dist),
+                       nprocs=world, start_method="spawn")
     got = np.load(path)
     assert got.shape == (steps, n_frames, H, W, 3)
     s, cam = _oracle_scene()
