@@ -241,3 +241,19 @@ def test_chain_batch_equals_frames():
         img.resize(W, H)
         P.raytraceImage(camera(cams[f]), img, seed=0x5EED + f)
         assert np.array_equal(bits(fr[f]), bits(img.rgb)), f
+
+
+@pytest.mark.parametrize("case", ["pt_rect_panel", "adapt_mixed_rect", "disp_cornell_mixed", "mixed_env_paths"])
+def test_odd_frame_sizes_match_oracle(case):
+    """1x1, 33x17 and 7x65 frames -- partial 8x8 tiles and 32x32 buckets, fewer units than one
+    wave, chain levels of a handful of entries -- through both engines against the oracle:
+    hit ids and ray counts exact, RGB within the path-tracing tolerance (1e-4 relative, libm
+    pow in Blinn's specular term; tests/test_path_trace.py)."""
+    P, O, cam = CASES[case]()
+    for W, H in ((1, 1), (33, 17), (7, 65)):
+        ref = O.render(cam, W, H)
+        for img, hits, st in both_engines(P, cam, W, H):
+            assert np.array_equal(hits["prim"], ref["hits"]["prim"]), (W, H)
+            assert st["shadow_rays"] == ref["shadow_rays"] and st["secondary_rays"] == ref["secondary_rays"], (W, H)
+            g, r = img.rgb.astype(np.float64), ref["rgb"].astype(np.float64)
+            assert not (np.abs(g - r) > 1e-4 * np.maximum(np.abs(r), 1e-3)).any(), (W, H)
