@@ -434,6 +434,25 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
             nxt = sel4(ch, top);
             have_next = true;
         }
+#ifdef MRT_NODE_TOUCH   // A/B build: touch the next node's line before this step's leaf triangles
+        // The next node is fixed by now (the kept slot, or the stack top when nothing
+        // was pushed); one dword of it loaded here brings its line towards the CU while
+        // the triangles are tested, and the load's value is only consumed after them.
+        // MRT_NODE_TOUCH 2: a wave-uniform next node is touched through the scalar cache.
+        int32_t touch_v = 0, touch_s = 0;
+        if (FAST && lm) {
+            const int32_t pn = have_next ? nxt : ((sp > sp0 && sp <= kLdsStack) ? peek : -1);
+            const int32_t p0 = __builtin_amdgcn_readfirstlane(pn);
+            if (MRT_NODE_TOUCH >= 2 && __ballot(pn != p0) == 0) {
+                if (p0 >= 0) {
+                    typedef const __attribute__((address_space(4))) int32_t cint;
+                    touch_s = ((cint*)(const void*)(c.nodes + p0))[24];
+                }
+            } else if (pn >= 0) {
+                touch_v = reinterpret_cast<const int32_t*>(c.nodes + pn)[24];
+            }
+        }
+#endif
         if (lm) {
             uint32_t leaf = 0;
             int k = 0, cnt = 0;
@@ -484,6 +503,9 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                 k++;
             }
         }
+#ifdef MRT_NODE_TOUCH
+        asm volatile("; mrt: node touch" :: "v"(touch_v), "s"(touch_s));
+#endif
         if (have_next) {
             cur = nxt;
         } else {
