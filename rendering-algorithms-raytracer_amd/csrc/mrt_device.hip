@@ -707,7 +707,10 @@ static int g_bin = -1;            // ray binning (mrt_bin.h) before tracing: bit
                                   // -1 auto (bin_mode): chain levels of path-traced scenes (P4 -18% frame; the
                                   // coherent mirror / glass levels of R3 / G3 lose their pixel order: +22% / +44%)
                                   // and the dome shadow rays of instanced scenes, in the frame shadow pass (C5 -2.6%;
-                                  // D1 +2%) and in the chain levels (FS -29% per frame, profiles/r04_fs_bin_ab.txt)
+                                  // D1 +2%) and in the chain levels (FS -29% per frame, profiles/r04_fs_bin_ab.txt),
+                                  // and the chain levels' shadow rays of dispersive scenes, whose three refraction
+                                  // children per split diverge (G3 -5% with 4 frames in flight; R3's coherent
+                                  // mirror levels +7%: off; profiles/r04_g3_bin_ab.txt)
 static int g_chain_bands = -1;    // chain_trace_kernel: XCD-banded chunk queue (binned rays: one XCD's L2 holds its share);
                                   // -1 auto: on when the level is binned (P4 -3.4%; unbinned R3 +5.7%, G3 +3%)
 static int g_dome_replay = 1;      // dome-light resolve (2c) sums 2a's recorded samples instead of sampling again
@@ -1271,7 +1274,7 @@ static int ensure_replay(StreamCtx& c, size_t n, size_t calls) {
 // The binning switches in effect for a scene (g_bin, or the auto choice).
 static int bin_mode(const DeviceState& d) {
     if (g_bin >= 0) return g_bin;
-    return (d.recursive == 2 ? 6 : 0) | (d.n_insts > 0 && d.dome ? 5 : 0);
+    return (d.recursive == 2 ? 6 : 0) | (d.n_insts > 0 && d.dome ? 5 : 0) | (d.disperse ? 4 : 0);
 }
 
 // Ray-binning scratch of a stream (mrt_bin.h) for batches of up to n rays.
