@@ -458,26 +458,68 @@ __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DL
 // Bucket tiles -> frames.  Item id = frame * buckets_per_frame + bucket; frame f
 // of the output starts at f * W * H pixels.  Float tiles (nullable) go to
 // `frames`; 8-bit pixels come from tiles8 when given, else from the LUT.
-__global__ void unpack_kernel(const int32_t* items, int32_t n_items, const float* tiles, const uint8_t* tiles8,
-                              int32_t W, int32_t H, int32_t buckets_x, int32_t buckets_per_frame, int32_t n_frames,
-                              float* frames, uint8_t* frames8, const uint8_t* gamma) {
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)n_items * 1024) return;
-    int bslot = (int)(i >> 10), p = (int)(i & 1023);
+// One 256-thread workgroup per item (a 32x32 tile), a thread per 4 consecutive
+// pixels of a tile row: 48 B of float RGB as three 16-B loads and stores and 12 B
+// of 8-bit RGB as three dword stores when the frame width is a multiple of 4
+// and the buffers are 16-B / 4-B aligned (every 4-pixel group then is too);
+// otherwise, and for groups the frame's right edge cuts, pixel by pixel.
+__global__ void __launch_bounds__(256) unpack_kernel(const int32_t* items, int32_t n_items, const float* tiles,
+                                                     const uint8_t* tiles8, int32_t W, int32_t H, int32_t buckets_x,
+                                                     int32_t buckets_per_frame, int32_t n_frames, float* frames,
+                                                     uint8_t* frames8, const uint8_t* gamma) {
+    const int bslot = blockIdx.x;
+    if (bslot >= n_items) return;
     const uint32_t id = (uint32_t)items[bslot];
     const uint32_t f = id / (uint32_t)buckets_per_frame, b = id % (uint32_t)buckets_per_frame;
-    int x = (int)(b % buckets_x) * 32 + (p & 31), y = (int)(b / buckets_x) * 32 + (p >> 5);
+    const int row = threadIdx.x >> 3, px = (threadIdx.x & 7) * 4;
+    const int x = (int)(b % buckets_x) * 32 + px, y = (int)(b / buckets_x) * 32 + row;
     if (f >= (uint32_t)n_frames || x >= W || y >= H) return;  // ids outside the batch are ignored
-    size_t q = (size_t)f * W * H + (size_t)y * W + x;
-    if (tiles && frames) {
-        frames[3 * q] = tiles[3 * i]; frames[3 * q + 1] = tiles[3 * i + 1]; frames[3 * q + 2] = tiles[3 * i + 2];
+    const size_t i = (size_t)bslot * 1024 + (size_t)(row * 32 + px);   // first pixel of the group in the tiles
+    const size_t q = (size_t)f * W * H + (size_t)y * W + x;            // ... and in the frames
+    const bool aligned = (((uintptr_t)tiles | (uintptr_t)frames) & 15) == 0 && (((uintptr_t)tiles8 | (uintptr_t)frames8) & 3) == 0;
+    if ((W & 3) == 0 && aligned) {   // x + 3 < W: the whole group, aligned
+        float v[12];
+        if (tiles) {
+            const float4* t4 = reinterpret_cast<const float4*>(tiles + 3 * i);
+            const float4 a = t4[0], c = t4[1], d = t4[2];
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y;
+            v[6] = c.z; v[7] = c.w; v[8] = d.x; v[9] = d.y; v[10] = d.z; v[11] = d.w;
+            if (frames) {
+                float4* o4 = reinterpret_cast<float4*>(frames + 3 * q);
+                o4[0] = a; o4[1] = c; o4[2] = d;
+            }
+        }
+        if (frames8) {
+            uint32_t w[3];
+            if (tiles8) {
+                const uint32_t* t = reinterpret_cast<const uint32_t*>(tiles8 + 3 * i);
+                w[0] = t[0]; w[1] = t[1]; w[2] = t[2];
+            } else {
+                uint32_t c8[12];
+#pragma unroll
+                for (int k = 0; k < 12; k++) c8[k] = map8(gamma, v[k]);
+#pragma unroll
+                for (int k = 0; k < 3; k++)
+                    w[k] = c8[4 * k] | c8[4 * k + 1] << 8 | c8[4 * k + 2] << 16 | c8[4 * k + 3] << 24;
+            }
+            uint32_t* o = reinterpret_cast<uint32_t*>(frames8 + 3 * q);
+            o[0] = w[0]; o[1] = w[1]; o[2] = w[2];
+        }
+        return;
     }
-    if (frames8) {
-        if (tiles8) {
-            frames8[3 * q] = tiles8[3 * i]; frames8[3 * q + 1] = tiles8[3 * i + 1]; frames8[3 * q + 2] = tiles8[3 * i + 2];
-        } else {
-            frames8[3 * q] = map8(gamma, tiles[3 * i]); frames8[3 * q + 1] = map8(gamma, tiles[3 * i + 1]);
-            frames8[3 * q + 2] = map8(gamma, tiles[3 * i + 2]);
+    for (int k = 0; k < 4 && x + k < W; k++) {
+        const size_t ik = i + k, qk = q + k;
+        if (tiles && frames) {
+            frames[3 * qk] = tiles[3 * ik]; frames[3 * qk + 1] = tiles[3 * ik + 1]; frames[3 * qk + 2] = tiles[3 * ik + 2];
+        }
+        if (frames8) {
+            if (tiles8) {
+                frames8[3 * qk] = tiles8[3 * ik]; frames8[3 * qk + 1] = tiles8[3 * ik + 1];
+                frames8[3 * qk + 2] = tiles8[3 * ik + 2];
+            } else {
+                frames8[3 * qk] = map8(gamma, tiles[3 * ik]); frames8[3 * qk + 1] = map8(gamma, tiles[3 * ik + 1]);
+                frames8[3 * qk + 2] = map8(gamma, tiles[3 * ik + 2]);
+            }
         }
     }
 }
@@ -2629,10 +2671,9 @@ int mrt_unpack_batch_async(const int32_t* d_items, int32_t n_items, const float*
     const bool need_lut = d_frames8 && !d_tiles8;
     if (need_lut && (!s_for_lut || !s_for_lut->impl.dev)) { set_error("rgb8 needs an uploaded scene for the LUT"); return MRT_ERR_INVALID; }
     if (n_items == 0) return MRT_OK;
-    size_t n = (size_t)n_items * 1024;
     const uint8_t* lut = need_lut ? s_for_lut->impl.dev->gamma : nullptr;
     const int bx = (width + 31) / 32, bpf = bx * ((height + 31) / 32);
-    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_items,
+    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)n_items), dim3(256), 0, (hipStream_t)stream, d_items,
                        n_items, d_tiles, d_tiles8, width, height, bx, bpf, n_frames, d_frames, d_frames8, lut);
     HIP_OK(hipGetLastError());
     return MRT_OK;
@@ -2779,7 +2820,7 @@ static int render_shared(mrt_scene* s, const mrt_camera* cam, const mrt_render_o
         HIP_OK(hipSetDevice(dc.device));
         for (Share& q : sh)
             if (q.ni) HIP_OK(hipStreamWaitEvent(gs, q.buf->done, 0));
-        hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)(((size_t)bpf * 1024 + 255) / 256)), dim3(256), 0, gs, dc.g_items,
+        hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)bpf), dim3(256), 0, gs, dc.g_items,
                            (int32_t)bpf, dc.g_tiles, (const uint8_t*)nullptr, W, H, bx, bpf, 1, dc.d_rgb,
                            rgb8 ? dc.d_rgb8 : nullptr, dc.gamma);
         HIP_OK(hipGetLastError());
