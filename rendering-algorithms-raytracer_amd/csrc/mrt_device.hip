@@ -714,6 +714,10 @@ static int g_sched = 2;           // TileSched mode 0..3 (2 measured fastest)
 static int g_order = 0;           // frame-mode tile dequeue order (0 bottom-up, 1 top-down)
 static int g_prio = 0;            // wave priority heuristic for the final tiles
 static int g_decline = 0;         // tiles per CU slot (decline heuristic), 0 = off
+static int g_batch_tpw = 2;       // bucket batches: tiles per wave the launch's grid is sized for when the batch is
+                                  // smaller than the persistent grid (a 1/4 or 1/8 split share): 2 -- C3 share model
+                                  // 2.98 -> 3.17x at N = 4, 4.69 -> 4.74x at N = 8; 4: 3.99x at N = 8
+                                  // (profiles/r04_share_tpw_ab.txt)
 static int g_wave_log = 0;        // 1: timing-only wave log on uninstrumented launches (diagnostics)
 static int g_scalar_nodes = 3;    // scalar-cache fetch of wave-uniform nodes (bit 0) and triangles (bit 1)
 static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
@@ -1888,7 +1892,10 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     P.queue = qbase;
     P.done = nullptr;
     const size_t pad = (size_t)g_lds_pad_kb * 1024;
-    const int items = (P.n_tiles + 3) / 4;
+    // workgroups: at most one per 4 tiles (a tile per wave); bucket batches (P.mode 1) may ask for
+    // g_batch_tpw tiles per wave, so a small share's waves take several tiles each
+    const int tpw = P.mode == 1 ? g_batch_tpw : 1;
+    const int items = (int)(((int64_t)P.n_tiles + 4 * tpw - 1) / (4 * tpw));
     if (logw) HIP_OK(hipMemsetAsync(c.wave_log, 0, 2 * log_stride * sizeof(unsigned long long), stream));
     int which = 0;
     auto launch = [&](KernelFn f) -> int {
@@ -3087,6 +3094,9 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "scalar_nodes") {   // bit 0 nodes, bit 1 triangles (1 = round 3's nodes only)
         if (value < 0 || value > 3) { set_error("scalar_nodes must be 0..3"); return MRT_ERR_INVALID; }
         g_scalar_nodes = value;
+    } else if (k == "batch_tpw") {
+        if (value < 1 || value > 64) { set_error("batch_tpw must be 1..64"); return MRT_ERR_INVALID; }
+        g_batch_tpw = value;
     } else if (k == "decline") {
         if (value < 0 || value > 1 << 20) { set_error("decline out of range"); return MRT_ERR_INVALID; }
         g_decline = value;

@@ -27,8 +27,14 @@ static constexpr int kMaxBlocksPerCU = 8;
 static constexpr int kLogTiles = 28;
 static constexpr int kLogWords = 4 + 2 * kLogTiles;  // 256-thread blocks: 8 waves per SIMD at most
 // counter block: CTR_N u64 statistics, then four launches x 8 work counters x 128 B
-// (primary, shade / gen, resolve, shadow_kernel's per-XCD ray queues)
+// (primary, shade / gen, resolve, shadow_kernel's per-XCD ray queues); cleared per launch
+// with one hipMemsetAsync, whose length is a multiple of 256 B so the runtime fills it with
+// one kernel (an odd length costs a second fill launch for the tail)
+#ifndef MRT_CTR_ODD
+static constexpr size_t kCtrBytes = (CTR_N * sizeof(unsigned long long) + 4 * 8 * 128 + 255) / 256 * 256;
+#else   // A/B build: round 3's unpadded length
 static constexpr size_t kCtrBytes = CTR_N * sizeof(unsigned long long) + 4 * 8 * 128;
+#endif
 // Shadow rays of the general shading path, wavefront style (ShadowMode): kernel
 // 2a runs the shading code and writes every shadow ray to its slot, kernel 2b
 // traces all of them any-hit (few registers, full occupancy), kernel 2c runs the

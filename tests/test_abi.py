@@ -50,3 +50,14 @@ def test_chain_tuning_keys_validate():
         assert L.mrt_set_tuning(b"chain_est_pct", 125) == 0
         assert L.mrt_set_tuning(b"bin_inst", 0) == 0
         assert L.mrt_set_tuning(b"chain_est", 1) == 0
+
+
+def test_batch_tiles_per_wave_key_validates():
+    """batch_tpw (tiles per wave a bucket-batch launch is sized for): 1..64, bad values rejected."""
+    L = miro.lib()
+    try:
+        assert L.mrt_set_tuning(b"batch_tpw", 0) != 0
+        assert L.mrt_set_tuning(b"batch_tpw", 65) != 0
+        assert L.mrt_set_tuning(b"batch_tpw", 1) == 0
+    finally:
+        assert L.mrt_set_tuning(b"batch_tpw", 2) == 0

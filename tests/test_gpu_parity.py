@@ -434,3 +434,40 @@ def test_wavefront_shadow_pass_equals_fused_kernel(key, W, H):
     assert np.array_equal(bits(img0.rgb), bits(img1.rgb))
     assert np.array_equal(img0.pixels, img1.pixels)
     assert st0["shadow_rays"] == st1["shadow_rays"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rect", [False, True])
+def test_batch_grid_sizing_gives_identical_tiles(rect):
+    """A small bucket batch (rank 3's share of an 8-way split) launched with grids sized for
+    1, 2, 4 and 64 tiles per wave (tuning key batch_tpw): the same tiles, bit for bit -- the
+    fused point-light kernel and the general shading path (rectangle light)."""
+    torch = pytest.importorskip("torch")
+    import ctypes as C
+    from miro import _lib
+    cfg = dict(scenes.CONFIGS["C1"])
+    lights = [dict(type="rect", v1=(3.0, 5.4, -2.5), v2=(3.0, 5.4, -3.0), v3=(2.5, 5.4, -2.5), power=15.0,
+                   samples=2, noise=0.001)] if rect else None
+    P, _, cam = scene_pair(cfg, meshes=[fixture_mesh("cornell_box")], **({"lights": lights} if rect else {}))
+    W, H = 300, 200
+    bpf = ((W + 31) // 32) * ((H + 31) // 32)
+    mine = [i for i in range(bpf) if i % 8 == 3]
+    ids = torch.tensor(mine, dtype=torch.int32, device="cuda")
+    camc = (_lib.mrt_camera * 1)(camera(cam)._c())
+    opts = _lib.mrt_render_opts(W, H, 0, 0, 0, 0, 0)
+    L = miro.lib()
+    stream = torch.cuda.current_stream().cuda_stream
+    out = []
+    try:
+        for tpw in (1, 2, 4, 64):
+            assert L.mrt_set_tuning(b"batch_tpw", tpw) == 0
+            tiles = torch.zeros(len(mine) * 1024 * 3, dtype=torch.float32, device="cuda")
+            _lib.check(L.mrt_render_batch_async(P.handle, camc, 1, C.byref(opts), ids.data_ptr(), len(mine),
+                                                tiles.data_ptr(), None, stream), "batch")
+            torch.cuda.synchronize()
+            out.append(tiles.cpu().numpy())
+    finally:
+        assert L.mrt_set_tuning(b"batch_tpw", 2) == 0
+    assert np.abs(out[0]).sum() > 0
+    for o in out[1:]:
+        assert np.array_equal(bits(o), bits(out[0]))
