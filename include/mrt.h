@@ -415,7 +415,9 @@ int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
  * direction and origin cells per axis as powers of two, 2 dbits + 3 obits <= 12),
  * "bin_blocks" 1..16 [4] (binning workgroups per CU), "dome_replay" 0/[1] (the
  * dome-light resolve pass sums the recorded samples), "chain_bands" [-1]..1
- * (XCD-banded chain trace queue; -1: on for binned levels).  Process-wide. */
+ * (XCD-banded chain trace queue; -1: on for binned levels), "batch_tpw" 1..64 [2]
+ * (tiles per wave a bucket batch smaller than the persistent grid is launched
+ * for).  Process-wide. */
 int mrt_set_tuning(const char* key, int value);
 
 /* Diagnostics: per-wave records of the last count-mode render (count_visits = 1)
