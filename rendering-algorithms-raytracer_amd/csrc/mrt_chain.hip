@@ -324,7 +324,13 @@ __global__ void __launch_bounds__(kWG) chain_compact_kernel(RenderParams P) {
 // answers of level k - 1's shadow rays (nB slots), which no longer wait for
 // each other -- a level's resolve needs its shadow answers only at the end of
 // the chunk.  Wave-uniform 64-slot chunks, the closest-hit chunks first.
-template <bool COUNT, bool FAST, bool INST, int MINW = 1>
+//
+// STEP (instanced scenes): 0 -- a shadow ray walks with traverse(), whose ProxyObject
+// lanes run their BLAS walks nested inside the world walk; 1 / 2 -- it walks with
+// anyhit_step_inst (2: alpha-mapped / motion-blurred lanes), one node per step for world
+// and BLAS nodes alike, the proxy walks deferred onto the stack (an any-hit answer does
+// not depend on the visit order), so lanes in and out of instances share every step.
+template <bool COUNT, bool FAST, bool INST, int MINW = 1, int STEP = 0>
 __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -376,8 +382,21 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
             if (ok) {
                 const float4 o = P.ray_o[sb + i], d = P.ray_d[sb + i];
                 const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
-                DHit h{o.w, 0.f, 0.f, -1};
-                P.occl[sb + i] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
+                if constexpr (INST && STEP > 0) {
+                    AnyState as;
+                    as.q = r;
+                    as.cur = 0;
+                    as.sp = 0;
+                    as.aoff = -1;
+                    bool hit = false;
+                    while (!anyhit_step_inst<COUNT, FAST, STEP == 2>(T, 0.001f, o.w, as, P.ray_o + sb, P.ray_d + sb, i,
+                                                                    hit, st)) {
+                    }
+                    P.occl[sb + i] = hit ? 1 : 0;
+                } else {
+                    DHit h{o.w, 0.f, 0.f, -1};
+                    P.occl[sb + i] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
+                }
             }
         }
         if (COUNT) {   // the chunk's wave steps: its longest ray's node visits
@@ -815,9 +834,15 @@ KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec) {
     if (rec == 2) return resolve ? chain_shade_fn<kResolve, 2>(po, inst) : chain_shade_fn<kGen, 2>(po, inst);
     return resolve ? chain_shade_fn<kResolve, 1>(po, inst) : chain_shade_fn<kGen, 1>(po, inst);
 }
-KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves) {
+KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves, int step) {
     if (waves == 8 && !c && !inst)   // occupancy target of the plain-scene trace (timed variants)
         return f ? chain_trace_kernel<false, true, false, 8> : chain_trace_kernel<false, false, false, 8>;
+    if (inst && step == 1)
+        return c ? (f ? chain_trace_kernel<true, true, true, 1, 1> : chain_trace_kernel<true, false, true, 1, 1>)
+                 : (f ? chain_trace_kernel<false, true, true, 1, 1> : chain_trace_kernel<false, false, true, 1, 1>);
+    if (inst && step == 2)
+        return c ? (f ? chain_trace_kernel<true, true, true, 1, 2> : chain_trace_kernel<true, false, true, 1, 2>)
+                 : (f ? chain_trace_kernel<false, true, true, 1, 2> : chain_trace_kernel<false, false, true, 1, 2>);
     if (inst) return c ? (f ? chain_trace_kernel<true, true, true> : chain_trace_kernel<true, false, true>)
                        : (f ? chain_trace_kernel<false, true, true> : chain_trace_kernel<false, false, true>);
     return c ? (f ? chain_trace_kernel<true, true, false> : chain_trace_kernel<true, false, false>)

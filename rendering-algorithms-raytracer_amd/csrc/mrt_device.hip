@@ -731,6 +731,7 @@ static int g_resolve_waves = 4;   // resolve pass (kernel 2c) of dome-light scen
 static int g_adapt_waves = 6;     // direct-lighting adaptive kernel occupancy target: 1 (none) or 6
                                   // (unbounded it takes 256 VGPRs, 1 wave: A3 30.7 -> 12.8 ms at 6)
 static int g_adapt_refill = 32;   // adaptive_kernel pixel refill: idle lanes that trigger a dequeue (0: tiles; 32: A3 -13%)
+static int g_chain_shadow_step = 0;   // instanced chain levels: shadow rays walk with anyhit_step_inst (deferred proxies)
 static int g_chain_trace_waves = 8;   // chain_trace_kernel occupancy target: 1 (none) or 8 (P4 -17%, R3 -3.5%)
 static int g_near_first = -1;     // any-hit walks take the nearest hit child first: 0 off, 1 on, -1 auto
                                   // (auto: on in the chunked shadow kernel of plain scenes only -- C4 shade
@@ -1473,6 +1474,8 @@ static ShadowFn shadow_fn_w(int w, bool c, bool f) {
         default: return shadow_fn<INST, REFILL, CHECK>(c, f);
     }
 }
+// check: the scene has alpha-mapped or motion-blurred lanes (child-word bit 3), which the
+// refill step must test as such
 static ShadowFn pick_shadow(bool c, bool f, bool inst, bool refill, bool check, int w) {
     if (!refill) return inst ? shadow_fn<true, false, true>(c, f) : shadow_fn_w<false, false, false>(w, c, f);
     if (!inst) return shadow_fn_w<false, true, false>(w, c, f);
@@ -1536,7 +1539,8 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
     const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive), r0 = pick_chain0(true, d.point_only, inst, d.recursive);
     const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive),
                    rk = pick_chain_shade(true, d.point_only, inst, d.recursive);
-    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, Q.fast_box != 0, inst, g_chain_trace_waves),
+    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, Q.fast_box != 0, inst, g_chain_trace_waves,
+                                                                           g_chain_shadow_step ? (d.has_alpha || d.has_mb ? 2 : 1) : 0),
                    kf = pick_chain_finish(), kd = pick_chain_fold();
     auto go = [&](KernelFn f, int g) -> int {
         void* args[] = {&Q};
@@ -1558,7 +1562,7 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
     }
     // instanced scenes: the levels' shadow rays on the lane-refill kernel (their own launch)
     const bool refill_sh = inst && g_chain_shadow_refill;
-    const ShadowFn ksh = refill_sh ? pick_shadow(count, Q.fast_box != 0, true, true, d.has_alpha, g_shadow_waves) : nullptr;
+    const ShadowFn ksh = refill_sh ? pick_shadow(count, Q.fast_box != 0, true, true, d.has_alpha || d.has_mb, g_shadow_waves) : nullptr;
     int gsh = refill_sh ? std::max(8, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(ksh), 0))) & ~7 : 0;
     auto trace = [&](int k) -> int {   // Q.ch_level == k
         if ((bm & 2) && k < L) {
@@ -1995,12 +1999,12 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         // lane refill for dome-light (incoherent) rays: D1 -7%, C5 -13% shade pass; coherent
         // area-light rays keep the bands (C4: refill +9%)
         int sched = g_shadow_sched >= 0 ? g_shadow_sched : (dome ? 2 : 1), refill = g_refill_min;
-        ShadowFn sf = pick_shadow(count, fb, inst, sched == 2, d.has_alpha, g_shadow_waves);
+        ShadowFn sf = pick_shadow(count, fb, inst, sched == 2, d.has_alpha || d.has_mb, g_shadow_waves);
         int g = std::max(1, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(sf), 0)));
         if (sched && (g & 7)) g &= ~7;          // XCD bands need a whole number of workgroups per XCD
         if (g < 8) {                            // too few workgroups for the bands: grid-stride
             sched = 0;
-            sf = pick_shadow(count, fb, inst, false, d.has_alpha, g_shadow_waves);
+            sf = pick_shadow(count, fb, inst, false, d.has_alpha || d.has_mb, g_shadow_waves);
         }
         size_t n_rays = slots * (size_t)max_sh;
         if (n_rays >= (size_t(1) << 32)) { set_error("too many wavefront shadow-ray slots (2^32)"); return MRT_ERR_INVALID; }
@@ -3138,6 +3142,8 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "adapt_refill") {
         if (value < 0 || value > 64) { set_error("adapt_refill must be 0..64"); return MRT_ERR_INVALID; }
         g_adapt_refill = value;
+    } else if (k == "chain_shadow_step") {
+        g_chain_shadow_step = value ? 1 : 0;
     } else if (k == "chain_trace_waves") {
         if (value != 1 && value != 8) { set_error("chain_trace_waves must be 1 or 8"); return MRT_ERR_INVALID; }
         g_chain_trace_waves = value;

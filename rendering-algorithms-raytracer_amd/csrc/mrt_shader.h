@@ -1573,7 +1573,7 @@ KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec, int waves);
 // defined in mrt_chain.hip: the wavefront chain engine
 KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec);
 KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec);
-KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves);
+KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves, int step);
 KernelFn pick_chain_compact();
 KernelFn pick_chain_merge();
 KernelFn pick_chain_fallback(bool po, bool inst, int rec);

@@ -21,6 +21,8 @@ import miro
 from helpers import bits, camera, final_scene_pair
 from miro import final_scene as F
 
+CHAIN_SHADOW_STEP_DEFAULT = 0   # libmrt's default (csrc/mrt_device.hip g_chain_shadow_step)
+
 
 def test_packed_data_matches_manifest():
     man = json.load(open(os.path.join(F.FINAL_DIR, "manifest.json")))
@@ -99,22 +101,26 @@ def test_final_scene_frame_matches_oracle(W, H):
 @pytest.mark.gpu
 def test_final_scene_chain_shadow_schedules_give_identical_frames():
     """The chain levels' shadow rays of an instanced scene on the lane-refill kernel
-    (chain_shadow_refill 1, deferred proxy walks) or inside chain_trace (0): the
-    same rays and answers, so the same frame, hit ids and ray counts."""
+    (chain_shadow_refill 1, deferred proxy walks), inside chain_trace with nested proxy
+    walks (0) or inside chain_trace stepping with deferred proxy walks (chain_shadow_step 1):
+    the same rays and answers, so the same frame, hit ids and ray counts."""
     if miro.device_count() < 1:
         pytest.skip("no HIP device")
     P, _, cam = final_scene_pair()
     L = miro.lib()
     out = []
     try:
-        for v in (0, 1):
-            assert L.mrt_set_tuning(b"chain_shadow_refill", v) == 0
+        for refill, step in ((0, 0), (1, 0), (0, 1)):
+            assert L.mrt_set_tuning(b"chain_shadow_refill", refill) == 0
+            assert L.mrt_set_tuning(b"chain_shadow_step", step) == 0
             img = miro.Image(); img.resize(72, 40)
             hits = P.raytraceImage(camera(cam), img, want_hits=True)
             out.append((img, hits, dict(P.last_stats)))
     finally:
         L.mrt_set_tuning(b"chain_shadow_refill", 0)
-    (a, ha, sa), (b, hb, sb) = out
-    assert np.array_equal(ha["prim"], hb["prim"])
-    assert np.array_equal(bits(a.rgb), bits(b.rgb)) and np.array_equal(a.pixels, b.pixels)
-    assert sa["shadow_rays"] == sb["shadow_rays"] and sa["secondary_rays"] == sb["secondary_rays"]
+        L.mrt_set_tuning(b"chain_shadow_step", CHAIN_SHADOW_STEP_DEFAULT)
+    a, ha, sa = out[0]
+    for b, hb, sb in out[1:]:
+        assert np.array_equal(ha["prim"], hb["prim"])
+        assert np.array_equal(bits(a.rgb), bits(b.rgb)) and np.array_equal(a.pixels, b.pixels)
+        assert sa["shadow_rays"] == sb["shadow_rays"] and sa["secondary_rays"] == sb["secondary_rays"]

@@ -252,3 +252,20 @@ def test_cannonball_motion_blur_matches_oracle():
     P, O_, _ = cannonball(shiny, num_paths=2)
     ref = gpu_vs_oracle(P, O_, dict(BALL_CAM, shutterSpeed=0.6), 96, 72)
     assert ref["secondary_rays"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chain", [False, True])
+def test_motion_blur_under_a_dome_light_matches_oracle(chain):
+    """A moving ball lit by a dome light: the dome's shadow rays take the lane-refill shadow
+    kernel (frame path) or the chain levels (mirror material), whose steps must test the
+    motion-blurred lanes at the ray's time, with no alpha map in the scene."""
+    need_gpu()
+    ball = sphere()
+    dome = [dict(type="dome", sky=(64, 32), power=0.15, samples=3, noise=0.001)]
+    mat = dict(kind="blinn", kd=(0.6, 0.5, 0.4), reflectAmt=0.7, refractAmt=0.3, ior=1.4) if chain else BALL
+    P, O_, _ = cornell(moving=[(ball, moved(ball), mat)], lights=dome)
+    ref = gpu_vs_oracle(P, O_, MB, 48, 40)
+    assert ref["shadow_rays"] > 0
+    if chain:
+        assert ref["secondary_rays"] > 0
