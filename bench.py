@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frames", type=int, default=0, help="frames per step (default: 1 at N=1, N at N>1)")
+    ap.add_argument("--settle-s", type=float, default=0.3,
+                    help="untimed rendering before the warmup steps until this many seconds have passed (clock settle)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="N = 1 frame path: frames in flight (consecutive steps alternate over this many HIP "
                          "streams, so one frame's launch tail overlaps the next frame's start)")
@@ -459,7 +461,31 @@ def main():
         return {"monotonic_ns": time.clock_gettime_ns(time.CLOCK_MONOTONIC),
                 "boottime_ns": time.clock_gettime_ns(time.CLOCK_BOOTTIME)}
 
+    settle = {}
+
     def timed(step_fn, flush, k):
+        # clock settle before the warmup: the GPU renders groups of `inflight` steps until
+        # --settle-s of wall time have passed, so clocks and caches are at their sustained
+        # state when the W warmup steps start (C3, one box: 20 steps after 5 warmups 0.444 ms
+        # per step, after 20 warmups 0.424, 100 steps 0.414)
+        # (N > 1: every rank takes the same decision from the slowest rank's clock, so all
+        # ranks run the same steps and their gathers pair up)
+        t_s, n_s = time.perf_counter(), 0
+        while True:
+            e_s = time.perf_counter() - t_s
+            if world > 1:
+                t_ = torch.tensor([e_s], dtype=torch.float64, device="cuda")
+                dist.all_reduce(t_, op=dist.ReduceOp.MAX)
+                e_s = t_.item()
+            if e_s >= args.settle_s:
+                break
+            for _ in range(max(1, inflight, depth if not use_frame_path else 1)):
+                step_fn()
+            n_s += max(1, inflight, depth if not use_frame_path else 1)
+            flush()
+            torch.cuda.synchronize()
+        if not settle:
+            settle.update({"seconds": round(time.perf_counter() - t_s, 3), "steps": n_s})
         for _ in range(args.warmup):
             step_fn()
         flush()
@@ -710,6 +736,8 @@ def main():
                     "them, and the environment image, are stand-ins here) and a different RNG stream"}
     if region:
         out["timed_region"] = region
+    if settle:   # untimed clock-settle steps before the warmup (see timed())
+        out["settle"] = settle
     try:   # the library's embedded source hash against the sources beside it (tools/source_hash.py)
         out["build"] = _lib.build_info(L)
     except Exception as e:   # reported, never fatal
