@@ -407,8 +407,7 @@ int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
  * holds), "primary_waves" 0/6/[7]/8 (occupancy target of the primary-ray kernel),
  * "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands, dynamic
  * interleaved, dynamic banded; see TileSched), "shade1" 0/[1] (specialised shading
- * kernel for one point light and one path), "lds_pad_kb" [0]..128 (extra LDS per
- * workgroup, lowers occupancy for sweeps), "fused" 0/[1] (one-launch frame kernel
+ * kernel for one point light and one path), "fused" 0/[1] (one-launch frame kernel
  * for one point light), "bin" [-1] / 0..7 (ray binning before tracing: bit 0 the
  * wavefront shadow pass, bit 1 the chain levels' closest-hit entries, bit 2 their
  * shadow rays; -1 auto), "bin_dbits" 0..6 [2] / "bin_obits" 0..4 [2] (binning key:

@@ -209,221 +209,6 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
 }
 
 
-// Shading of one primary hit for one point light and num_paths == 1 (the
-// BASELINE configs C1-C3): HitInfo::getAllInfos + Ray::getPoint, the
-// Lambert/Blinn set-up, straight-line PointLight::sampleLight with only the
-// light's three pre-shadow scalars live across the any-hit traversal, then the
-// material sums.  Same operations in the same order as Shader::shade.  r is the
-// camera ray, (ht, ha, hb, prim) its closest hit.
-// POW: some Blinn material has specExp != 1 (Blinn::shade's pow, src/Blinn.cpp:220).  Scenes
-// without one run the POW = false kernels, which carry no double-precision pow: its
-// polynomial constants, hoisted out of the tile loop, took VGPRs and scratch.
-template <bool COUNT, bool FAST, bool POW>
-__device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, TravStats& st, const DRay& r, float ht,
-                                         float ha, float hb, int prim, const uint16_t* rcpT, const uint16_t* rsqT,
-                                         uint32_t& shadow_total) {
-    const v3 rayD = mk(r.d[0], r.d[1], r.d[2]);
-    const PrimShade ps = P.prims[prim];
-    const uint32_t mi = ps.mat;
-    const bool lambert = P.mats[mi].type == MRT_LAMBERT;
-    const float4 A = P.verts[ps.v[0]], B = P.verts[ps.v[1]], C = P.verts[ps.v[2]];
-    const v3 geoN = normalized(cross(mk(B.x - A.x, B.y - A.y, B.z - A.z), mk(C.x - A.x, C.y - A.y, C.z - A.z)), rsqT);
-    const float c = 1.0f - ha - hb;
-    const float4 n0 = P.normals[ps.n[0]], n1 = P.normals[ps.n[1]], n2 = P.normals[ps.n[2]];
-    const v3 N = normalized(add(add(scale(mk(n0.x, n0.y, n0.z), c), scale(mk(n1.x, n1.y, n1.z), ha)),
-                                scale(mk(n2.x, n2.y, n2.z), hb)), rsqT);
-    const v3 from = mk(r.o[0] + ht * r.d[0], r.o[1] + ht * r.d[1], r.o[2] + ht * r.d[2]);
-    // Lambert::shade uses the shading normal and no reflection vector;
-    // Blinn::shade flips to the viewer's side (src/Blinn.cpp:150-170).
-    v3 n = N, rVec = mk(0, 0, 0);
-    if (!lambert) {
-        const v3 viewDir = neg(rayD);
-        float vDotN = dot(viewDir, N);
-        const float vDotGeoN = dot(viewDir, geoN);
-        const bool same = (vDotN * vDotGeoN) >= 0.0f;
-        n = same ? N : geoN;
-        vDotN = same ? vDotN : vDotGeoN;
-        if (vDotN < 0.0f) { vDotN = -vDotN; n = neg(n); }
-        rVec = add(rayD, scale(n, 2.0f * vDotN));
-    }
-    // PointLight::sampleLight (src/PointLight.cpp:8-81), as Shader::point_light
-    const DevLight& l = P.lights[0];
-    v3 L = sub(mk(l.pos[0], l.pos[1], l.pos[2]), from);
-    float nDotL = dot(n, L);
-    float e = 0.f, spec = 0.f;
-    if (nDotL > 0.0f) {
-        float falloff = dot(L, L);
-        const float distanceRecip = rsqrt_nr(falloff, rsqT);
-        falloff = rcp_nr(falloff, rcpT);
-        const float distance = rcp_nr(distanceRecip, rcpT);
-        L = scale(L, distanceRecip);
-        nDotL *= distanceRecip;
-        const float Aterm = (l.power * falloff) * (0.25f / 3.1415926f);
-        const float rdl = std_max(0.f, dot(rVec, L));
-        float attenuate = 1.0f;
-        if (l.cast_shadows) {
-            const DRay sr = make_ray(from, L);
-            DHit sh{distance, 0.f, 0.f, -1};
-            shadow_total++;
-            if (traverse<true, COUNT, FAST>(T, sr, 0.001f, sh, st)) attenuate = 0.0f;
-        }
-        attenuate *= nDotL;
-        spec = rdl * attenuate;
-        e = Aterm * attenuate;
-    }
-    const DevMaterial& M = P.mats[mi];
-    const v3 E = mk(e, e, e);
-    const v3 kd = mk(M.kd[0], M.kd[1], M.kd[2]), ka = mk(M.ka[0], M.ka[1], M.ka[2]);
-    v3 sh;
-    if (lambert) {
-        sh = add(add(mk(0, 0, 0), mul(E, kd)), ka);
-    } else {
-        const v3 ks = mk(M.ks[0], M.ks[1], M.ks[2]);
-        const float pw = (!POW || M.spec_exp == 1.0f) ? spec : spec_pow(spec, M.spec_exp);
-        const v3 Ls = add(mk(0, 0, 0), scale(scale(mul(E, ks), M.spec_amt), pw));
-        const v3 Ld = add(add(mk(0, 0, 0), mul(E, kd)), ka);
-        const v3 z = mk(0, 0, 0);
-        sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), mk(M.le[0], M.le[1], M.le[2]));
-    }
-    return scale(add(mk(0, 0, 0), sh), 1.0f / (float)P.num_paths);
-}
-
-__device__ __forceinline__ void write_pixel(const RenderParams& P, size_t slot, v3 col) {
-    if (P.out_rgb) {
-        float* o = P.out_rgb + 3 * slot;
-        o[0] = col.x; o[1] = col.y; o[2] = col.z;
-    }
-    if (P.out_rgb8) {
-        uint8_t* o8 = P.out_rgb8 + 3 * slot;
-        o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
-    }
-}
-
-// Kernel 2, specialised for one point light and num_paths == 1: shade1_hit of
-// every pixel's hit record (the two-launch path; frame1_kernel fuses both).
-template <bool COUNT, bool FAST, int MINW, bool POW>
-__global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
-    __shared__ uint16_t s_tab[2048];
-    __shared__ int32_t s_stack[kLdsStack * kWG];
-    load_tables(P.tables, s_tab, 1024);
-    const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
-    const uint16_t* rcpT = s_tab;           // per triangle test: LDS
-    const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
-    T.inst = P.insts;
-    trav_alpha(T, P);
-    TravStats st;
-    uint32_t shadow_total = 0;
-    TileSched ts(P, wave, lane);
-    uint32_t ntiles = 0;
-    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
-        if (P.wave_log && lane == 0 && ntiles < kLogTiles)
-        {
-            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
-            r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
-            r[4 + kLogTiles + ntiles] = ts.deq_ticks;
-        }
-        ntiles++;
-        int x, y;
-        size_t slot;
-        if (!item_pixel(P, item, lane, x, y, slot)) continue;
-        const float4 hv = P.hits[slot];
-        const int prim = __float_as_int(hv.w);
-        v3 col = mk(P.bg[0], P.bg[1], P.bg[2]);
-        if (prim >= 0) {
-            const int f = item_frame(P, item);
-            const EyeRay er = camera_ray(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
-            col = shade1_hit<COUNT, FAST, POW>(P, T, st, make_ray(er.o, er.d), hv.x, hv.y, hv.z, prim, rcpT, rsqT, shadow_total);
-        }
-        item_pixel(P, item, lane, x, y, slot);
-        write_pixel(P, slot, col);
-    }
-    flush_stats<COUNT, false>(P, st, shadow_total, lane, t0, ntiles);
-}
-
-// Kernel 1+2 fused for one point light and num_paths == 1 (C1-C3): per pixel
-// the camera ray, its closest hit, then shade1_hit (the shadow ray any-hit) in
-// the same lane -- one persistent launch per frame, no hit-record hand-off
-// (the record is written only when the caller asks for hits, P.hits != null),
-// one launch tail instead of two.  Every ray's visits and every operation are
-// those of primary_kernel + shade1_kernel, so the frame is bit-identical.
-template <bool COUNT, bool FAST, int MINW, bool POW>
-__global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
-    __shared__ uint16_t s_tab[2048];
-    __shared__ int32_t s_stack[kLdsStack * kWG];
-#ifdef MRT_LDS_NODES   // A/B build: the hierarchy's top nodes (host-renumbered to 0 .. MRT_LDS_NODES - 1) in LDS
-    __shared__ QNode s_top[MRT_LDS_NODES];
-    for (int i = threadIdx.x; i < MRT_LDS_NODES * 32; i += kWG)
-        reinterpret_cast<uint32_t*>(s_top)[i] = reinterpret_cast<const uint32_t*>(P.nodes)[i];
-#endif
-    load_tables(P.tables, s_tab, 1024);   // (its barrier also covers s_top)
-    const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
-    const uint16_t* rcpT = s_tab;
-    const uint16_t* rsqT = P.tables + 2048;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
-    T.inst = P.insts;
-    trav_alpha(T, P);
-#ifdef MRT_LDS_NODES
-    T.lnodes = s_top;
-#endif
-    TravStats st, ss;   // primary / shadow rays (count mode)
-    uint32_t nhits = 0, shadow_total = 0;
-    unsigned long long wave_steps = 0;
-    TileSched ts(P, wave, lane);
-    uint32_t ntiles = 0;
-    for (int item = ts.first(); item >= 0; item = ts.next(item)) {
-        if (P.wave_log && lane == 0 && ntiles < kLogTiles)
-        {
-            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
-            r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
-            r[4 + kLogTiles + ntiles] = ts.deq_ticks;
-        }
-        ntiles++;
-        int x, y;
-        size_t slot;
-        const uint32_t n0 = st.nodes;
-        const uint64_t tc0 = P.tile_cost ? clock64() : 0;
-        if (item_pixel(P, item, lane, x, y, slot)) {
-            const int f = item_frame(P, item);
-            const EyeRay er = camera_ray(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
-            const DRay r = make_ray(er.o, er.d);
-            DHit h{1e12f, 0.f, 0.f, -1};
-            const bool hit = traverse<false, COUNT, FAST>(T, r, 0.001f, h, st);
-            v3 col = mk(P.bg[0], P.bg[1], P.bg[2]);
-            if (hit) {
-                nhits++;
-                col = shade1_hit<COUNT, FAST, POW>(P, T, ss, r, h.t, h.a, h.b, h.prim, rcpT, rsqT, shadow_total);
-            }
-            item_pixel(P, item, lane, x, y, slot);   // recompute: keeps it out of the traversals' live set
-            if (P.hits) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
-            write_pixel(P, slot, col);
-        }
-        if (P.tile_cost && lane == 0) P.tile_cost[item] = (uint32_t)min(clock64() - tc0, (uint64_t)0xFFFFFFFFu);
-        if (COUNT) {
-            uint32_t dmax = st.nodes - n0;
-            for (int off = 32; off > 0; off >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, off));
-            wave_steps += dmax;
-        }
-    }
-    if (COUNT && lane == 0) atomicAdd(&P.ctr[CTR_WAVE_STEPS_P], wave_steps);
-    // one wall-clock record per wave (the primary span counters; the wave log counts both kinds' nodes)
-    flush_stats<COUNT, true>(P, st, nhits, lane, t0, ntiles, ss.nodes);
-    flush_stats<COUNT, false, false>(P, ss, shadow_total, lane, t0, ntiles);
-    if (!COUNT && P.done) {   // the last workgroup to finish zeroes the tile counters for the next frame
-        __syncthreads();
-        if (tid == 0) {
-            __threadfence();
-            if (atomicAdd(P.done, 1u) == gridDim.x - 1) {
-#pragma unroll
-                for (int k = 0; k < 8; k++) atomicExch(P.queue + k * 32, 0u);
-                atomicExch(P.done, 0u);
-            }
-        }
-    }
-}
-
 // Batched Scene::trace: one lane per query ray.
 template <bool ANY, bool INST = false>
 __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DLeaf* leaves, const uint16_t* tables,
@@ -524,68 +309,6 @@ __global__ void __launch_bounds__(256) unpack_kernel(const int32_t* items, int32
     }
 }
 
-// Next frame's tile queue order from this frame's tile costs, slowest first
-// (longest-processing-time-first: the launch then ends on cheap tiles, so its
-// drain -- waves finishing their last tile at falling occupancy -- is short).
-// One workgroup of 16 waves: a 64-bin histogram of the costs on a half-octave
-// scale (one copy per wave, so LDS atomics rarely collide), bin offsets, then a
-// scatter; the order inside a bin does not matter (every schedule renders the
-// same frame).  Each thread keeps kOrderBatch bins in registers, so the cost
-// loads of a batch are in flight together.
-static constexpr int kOrderBins = 64, kOrderWaves = 16, kOrderBatch = 16;
-__device__ __forceinline__ int order_bin(uint32_t c) {   // descending: costly tiles in low bins
-    if (c < 2) return kOrderBins - 1;
-    const int l = 31 - __builtin_clz(c);              // 1..31
-    const int half = (int)((c >> (l - 1)) & 1u);      // the next bit: half an octave
-    return kOrderBins - 1 - min(kOrderBins - 1, 2 * l + half - 1);
-}
-__global__ void __launch_bounds__(1024) tile_order_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
-                                                          int n) {
-    __shared__ uint32_t hist[kOrderBins * kOrderWaves];   // [bin][wave]
-    const int tid = threadIdx.x, wave = tid >> 6;
-    hist[tid] = 0;
-    __syncthreads();
-    for (int base = 0; base < n; base += 1024 * kOrderBatch) {
-        int bin[kOrderBatch];
-#pragma unroll
-        for (int j = 0; j < kOrderBatch; j++) {
-            const int i = base + j * 1024 + tid;
-            bin[j] = i < n ? order_bin(cost[i]) : -1;
-        }
-#pragma unroll
-        for (int j = 0; j < kOrderBatch; j++)
-            if (bin[j] >= 0) atomicAdd(&hist[bin[j] * kOrderWaves + wave], 1u);
-    }
-    __syncthreads();
-    {   // exclusive scan over (bin, wave) = thread tid: bins in order, waves inside a bin
-        __shared__ uint32_t part[kOrderWaves];
-        const uint32_t h = hist[tid];
-        uint32_t v = h;
-        const int lane = tid & 63;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t u = __shfl_up(v, off);
-            if (lane >= off) v += u;
-        }
-        if (lane == 63) part[wave] = v;
-        __syncthreads();
-        uint32_t before = 0;
-        for (int w = 0; w < wave; w++) before += part[w];
-        hist[tid] = before + v - h;
-    }
-    __syncthreads();
-    for (int base = 0; base < n; base += 1024 * kOrderBatch) {
-        int bin[kOrderBatch];
-#pragma unroll
-        for (int j = 0; j < kOrderBatch; j++) {
-            const int i = base + j * 1024 + tid;
-            bin[j] = i < n ? order_bin(cost[i]) : -1;
-        }
-#pragma unroll
-        for (int j = 0; j < kOrderBatch; j++)
-            if (bin[j] >= 0) order[atomicAdd(&hist[bin[j] * kOrderWaves + wave], 1u)] = (uint32_t)(base + j * 1024 + tid);
-    }
-}
-
 // ------------------------------------------------------------------ device state
 // Launch scratch of one stream: everything a render / trace launch writes
 // besides the caller's outputs.  Two launches on different streams never share
@@ -622,11 +345,7 @@ struct StreamCtx {
     std::vector<uint32_t> est;
     bool last_was_render = false;
     bool fused = false;                      // the last render ran frame1_kernel (one launch)
-    bool queue_clean = false;                // the last launch left the tile counters at zero (self-reset frame1)
     bool chain_used = false;                 // the last render's shading ran the wavefront chain engine
-    uint32_t* tile_cost = nullptr;           // frame1_kernel: per-tile cycles of the last frame on this stream
-    uint32_t* tile_order = nullptr;          //   and the queue order derived from them
-    int tile_cap = 0, order_tiles = 0;       //   capacity; tiles of the frame the order is valid for (0: none)
     uint16_t* bin_keys = nullptr;            // ray binning (mrt_bin.h): per-ray keys, two permutations
     uint32_t* bin_perm = nullptr;            //   [2][bin_cap] (0: shadow rays, 1: chain closest-hit entries)
     uint32_t* bin_hist = nullptr;            //   [2][kBinHist] bins + valid count
@@ -709,11 +428,7 @@ struct DeviceState {
 static int g_fast_box = 1;        // hardware min/max box test when its precondition holds
 static int g_primary_waves = 7;   // launch-bounds occupancy target of the primary kernel: 0 (none), 6, 7, 8
 static int g_shade_waves = 5;     // same for shade1_kernel: 1 (none), 4..8 (5: 96 VGPRs, 64 B spill; -2.5% vs 6)
-static int g_lds_pad_kb = 0;      // extra dynamic LDS per workgroup (occupancy sweeps)
 static int g_sched = 2;           // TileSched mode 0..3 (2 measured fastest)
-static int g_order = 0;           // frame-mode tile dequeue order (0 bottom-up, 1 top-down)
-static int g_prio = 0;            // wave priority heuristic for the final tiles
-static int g_decline = 0;         // tiles per CU slot (decline heuristic), 0 = off
 static int g_batch_tpw = 2;       // bucket batches: tiles per wave the launch's grid is sized for when the batch is
                                   // smaller than the persistent grid (a 1/4 or 1/8 split share): 2 -- C3 share model
                                   // 2.98 -> 3.17x at N = 4, 4.69 -> 4.74x at N = 8; 4: 3.99x at N = 8
@@ -767,16 +482,12 @@ static int g_bin_dbits = 2;       // binning key: direction cells per octahedral
 static int g_bin_obits = 2;       //   origin cells per scene-box axis = 2^obits (2 dbits + 3 obits <= 12);
                                   //   sweep of 12 pairs: (2, 2) best on P4 (-18%) and C5 (-2.6%), finer
                                   //   direction cells lose (P4 (6, 0) -11%), profiles/r03_bin_sweep.txt
-static int g_self_reset = 0;      // frame1_kernel resets its own tile counters (no per-frame fill launch on the stream):
-                                  // off -- single frame -1%, but +3% per frame with 4 in flight (profiles/r04_split_node_selfreset_ab.txt)
-static int g_tile_lpt = 0;        // frame1_kernel: tile queue ordered by the previous frame's tile costs (off: -2% single-frame latency
-                                  // but +10% ms/frame with 4 frames in flight, the bench mode; profiles/r03_lpt_ab.txt)
 
 static inline int fast_box(const DeviceState& d);
 
 static void free_ctx(StreamCtx* c) {
     void* ptrs[] = {c->gstack, c->ctr, c->wave_log, c->hitbuf, c->rays, c->occl, c->nrays, c->lvl, c->chain,
-                    c->tile_cost, c->tile_order, c->adapt, c->bin_keys, c->bin_perm, c->bin_hist, c->ray_e, c->lrec};
+                    c->adapt, c->bin_keys, c->bin_perm, c->bin_hist, c->ray_e, c->lrec};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->est_dev) (void)hipFree(c->est_dev);
@@ -1010,38 +721,6 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     append(s.nodes, s.leaves, &s.obj_inst, nullptr);
     std::vector<int32_t> blas_root(s.blas.size());
     for (size_t b = 0; b < s.blas.size(); b++) blas_root[b] = append(s.blas[b].nodes, s.blas[b].leaves, nullptr, &s.blas[b]);
-#ifdef MRT_LDS_NODES
-    {   // A/B build: renumber the world hierarchy's first MRT_LDS_NODES nodes in breadth-first
-        // order to 0 .. MRT_LDS_NODES - 1 (frame1_kernel stages them in LDS).  Node numbers are
-        // internal to the device: the visit order follows the child slots, not the numbers.
-        const size_t nw = s.nodes.size();
-        std::vector<int32_t> bfs{0};
-        for (size_t q = 0; q < bfs.size() && bfs.size() < (size_t)MRT_LDS_NODES; q++)
-            for (int k = 0; k < 4 && bfs.size() < (size_t)MRT_LDS_NODES; k++)
-                if (DN[(size_t)bfs[q]].child[k] >= 0) bfs.push_back(DN[(size_t)bfs[q]].child[k]);
-        std::vector<int32_t> perm(DN.size(), -1);
-        for (size_t i = 0; i < bfs.size(); i++) perm[(size_t)bfs[i]] = (int32_t)i;
-        int32_t next = (int32_t)bfs.size();
-        for (size_t i = 0; i < nw; i++)
-            if (perm[i] < 0) perm[i] = next++;
-        for (size_t i = nw; i < DN.size(); i++) perm[i] = (int32_t)i;
-        std::vector<QNode> R(DN.size());
-        for (size_t i = 0; i < DN.size(); i++) {
-            QNode q = DN[i];
-            for (int k = 0; k < 4; k++)
-                if (q.child[k] >= 0) q.child[k] = perm[(size_t)q.child[k]];
-            R[(size_t)perm[i]] = q;
-        }
-        DN.swap(R);
-        for (int32_t& br : blas_root) br = perm[(size_t)br];
-    }
-#endif
-    // pad[0]: the parent node (-1 at a root) -- read only by the stackless walk (traverse_sl,
-    // an A/B build); the stack walks never look at it
-    for (QNode& q : DN) q.pad[0] = 0xFFFFFFFFu;
-    for (size_t i = 0; i < DN.size(); i++)
-        for (int k = 0; k < 4; k++)
-            if (DN[i].child[k] >= 0) DN[(size_t)DN[i].child[k]].pad[0] = (uint32_t)i;
     if ((rc = upload(d.nodes, DN.data(), DN.size() * sizeof(QNode), total))) return rc;
     std::vector<DevInstance> DI(s.instances.size());
     for (size_t i = 0; i < DI.size(); i++) {
@@ -1415,38 +1094,6 @@ static KernelFn pick_primary(int w, bool c, bool f, bool inst) {
         default: return primary_fn<1>(c, f);
     }
 }
-template <int W, bool POW>
-static KernelFn shade1_fn(bool c, bool f) {
-    return c ? (f ? shade1_kernel<true, true, W, POW> : shade1_kernel<true, false, W, POW>)
-             : (f ? shade1_kernel<false, true, W, POW> : shade1_kernel<false, false, W, POW>);
-}
-template <int W, bool POW>
-static KernelFn frame1_fn(bool c, bool f) {
-    return c ? (f ? frame1_kernel<true, true, W, POW> : frame1_kernel<true, false, W, POW>)
-             : (f ? frame1_kernel<false, true, W, POW> : frame1_kernel<false, false, W, POW>);
-}
-// pow: a Blinn material with specExp != 1 (those scenes run at 6 waves, or unbounded)
-static KernelFn pick_frame1(int w, bool c, bool f, bool pow) {
-    if (pow) return w == 1 ? frame1_fn<1, true>(c, f) : frame1_fn<6, true>(c, f);
-    switch (w) {
-        case 1: return frame1_fn<1, false>(c, f);
-        case 5: return frame1_fn<5, false>(c, f);
-        case 7: return frame1_fn<7, false>(c, f);
-        case 8: return frame1_fn<8, false>(c, f);
-        default: return frame1_fn<6, false>(c, f);
-    }
-}
-static KernelFn pick_shade1(int w, bool c, bool f, bool pow) {
-    if (pow) return w == 1 ? shade1_fn<1, true>(c, f) : shade1_fn<5, true>(c, f);
-    switch (w) {
-        case 1: return shade1_fn<1, false>(c, f);
-        case 4: return shade1_fn<4, false>(c, f);
-        case 5: return shade1_fn<5, false>(c, f);
-        case 7: return shade1_fn<7, false>(c, f);
-        case 8: return shade1_fn<8, false>(c, f);
-        default: return shade1_fn<6, false>(c, f);
-    }
-}
 // bound: the resolve pass at its g_resolve_waves occupancy target (~240 VGPRs unbounded)
 template <int MODE>
 static KernelFn shade_mode_fn(bool c, bool po, bool inst, bool bound = false) {   // kGen / kResolve: no traversal, FAST unused
@@ -1787,7 +1434,6 @@ static int launch_chain(Scene& s, StreamCtx& c, const RenderParams& P0, bool cou
     }
     Q.lvl_words = W;
     Q.ch_bands = g_chain_bands > 0 || (g_chain_bands < 0 && (bin_mode(d) & 6));
-    Q.order = 0;          // chunks index work items directly
     Q.wave_log = nullptr;
     Q.ray_o = c.rays;
     Q.ray_d = c.rays + entries * (uint64_t)m;
@@ -1872,9 +1518,6 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     P.ctr = c.ctr;
     P.fast_box = fast_box(d);
     P.sched = g_sched;
-    P.order = g_order;
-    P.prio = g_prio;
-    P.decline = g_decline;
     P.cus = d.cus;
     P.scalar_nodes = g_scalar_nodes;
     P.near_first = g_near_first > 0 ? 1 : 0;
@@ -1886,16 +1529,9 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
                      !d.has_maps;
     const size_t log_stride = (size_t)d.grid * (kWG / 64) * kLogWords;
     const bool logw = count || g_wave_log;   // wave log: count mode, or timing-only on the timed kernels
-    // The fused frame kernel can leave its tile counters at zero itself (the last
-    // workgroup to finish resets them), so the next frame on this stream needs no
-    // counter-clearing fill launch in front of it; any other launch clears them.
-    const bool self_reset = !adaptive && one && g_fused && g_self_reset && !count && !logw && !g_tile_lpt;
-    if (!(self_reset && c.queue_clean)) HIP_OK(hipMemsetAsync(c.ctr, 0, kCtrBytes, stream));
-    c.queue_clean = false;
+    HIP_OK(hipMemsetAsync(c.ctr, 0, kCtrBytes, stream));
     unsigned int* qbase = reinterpret_cast<unsigned int*>(reinterpret_cast<char*>(c.ctr) + CTR_N * sizeof(unsigned long long));
     P.queue = qbase;
-    P.done = nullptr;
-    const size_t pad = (size_t)g_lds_pad_kb * 1024;
     // workgroups: at most one per 4 tiles (a tile per wave); bucket batches (P.mode 1) may ask for
     // g_batch_tpw tiles per wave, so a small share's waves take several tiles each
     const int tpw = P.mode == 1 ? g_batch_tpw : 1;
@@ -1903,13 +1539,13 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     if (logw) HIP_OK(hipMemsetAsync(c.wave_log, 0, 2 * log_stride * sizeof(unsigned long long), stream));
     int which = 0;
     auto launch = [&](KernelFn f) -> int {
-        const int g = std::max(1, std::min(std::min(d.grid, d.cus * blocks_per_cu(f, pad)), items));
+        const int g = std::max(1, std::min(std::min(d.grid, d.cus * blocks_per_cu(f, 0)), items));
         P.wave_log = logw && which < 2 ? c.wave_log + which * log_stride : nullptr;  // primary + first shade
         P.n_waves = g * (kWG / 64);
         if (logw && which < 2) c.log_waves[which] = g * (kWG / 64);
         which++;
         void* args[] = {&P};
-        HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(f), dim3(g), dim3(kWG), args, pad, stream));
+        HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(f), dim3(g), dim3(kWG), args, 0, stream));
         return MRT_OK;
     };
     HIP_OK(hipEventRecord(c.ev0, stream));
@@ -1934,29 +1570,8 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     c.fused = one && g_fused;
     if (c.fused) {   // one launch: camera rays, closest hits, shading, shadow rays
         if (!want_hits) P.hits = nullptr;
-        if (self_reset) {   // the frame-1 counter line of launch slot 1 (unused by this launch) counts finished workgroups
-            P.done = qbase + 8 * 32;
-            c.queue_clean = true;
-        }
-        const bool lpt = g_tile_lpt && P.mode == 0 && !count && P.sched == 2;
-        if (lpt && P.n_tiles > c.tile_cap) {
-            HIP_OK(hipStreamSynchronize(stream));   // the previous launch may still use them
-            if (c.tile_cost) (void)hipFree(c.tile_cost);
-            if (c.tile_order) (void)hipFree(c.tile_order);
-            c.tile_cost = c.tile_order = nullptr;
-            c.tile_cap = c.order_tiles = 0;
-            HIP_OK(hipMalloc((void**)&c.tile_cost, (size_t)P.n_tiles * sizeof(uint32_t)));
-            HIP_OK(hipMalloc((void**)&c.tile_order, (size_t)P.n_tiles * sizeof(uint32_t)));
-            c.tile_cap = P.n_tiles;
-        }
-        P.tile_cost = lpt ? c.tile_cost : nullptr;
-        P.tile_order = lpt && c.order_tiles == P.n_tiles ? c.tile_order : nullptr;
         if ((rc = launch(pick_frame1(g_frame1_waves, count, fb, d.pow_spec)))) return rc;
         HIP_OK(hipEventRecord(c.evm, stream));
-        if (lpt) {   // the next frame on this stream dequeues this frame's slowest tiles first
-            hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, stream, c.tile_cost, c.tile_order, P.n_tiles);
-            c.order_tiles = P.n_tiles;
-        }
         c.last_was_render = true;
         HIP_OK(hipGetLastError());
         HIP_OK(hipEventRecord(c.ev1, stream));
@@ -3101,16 +2716,8 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "batch_tpw") {
         if (value < 1 || value > 64) { set_error("batch_tpw must be 1..64"); return MRT_ERR_INVALID; }
         g_batch_tpw = value;
-    } else if (k == "decline") {
-        if (value < 0 || value > 1 << 20) { set_error("decline out of range"); return MRT_ERR_INVALID; }
-        g_decline = value;
     } else if (k == "wave_log") {
         g_wave_log = value ? 1 : 0;
-    } else if (k == "order") {
-        g_order = value ? 1 : 0;
-    } else if (k == "prio") {
-        if (value < 0 || value > 2) { set_error("prio must be 0..2"); return MRT_ERR_INVALID; }
-        g_prio = value;
     } else if (k == "shade1") {
         g_shade1 = value ? 1 : 0;
     } else if (k == "wavefront") {
@@ -3165,10 +2772,6 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "bin_inst") {
         if (value < 0 || value > 2) { set_error("bin_inst must be 0..2"); return MRT_ERR_INVALID; }
         g_bin_inst = value;
-    } else if (k == "self_reset") {
-        g_self_reset = value ? 1 : 0;
-    } else if (k == "tile_lpt") {
-        g_tile_lpt = value ? 1 : 0;
     } else if (k == "chain_bands") {
         if (value < -1 || value > 1) { set_error("chain_bands must be -1..1"); return MRT_ERR_INVALID; }
         g_chain_bands = value;
@@ -3192,9 +2795,6 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "sched") {
         if (value < 0 || value > 3) { set_error("sched must be 0..3"); return MRT_ERR_INVALID; }
         g_sched = value;
-    } else if (k == "lds_pad_kb") {
-        if (value < 0 || value > 128) { set_error("lds_pad_kb out of range"); return MRT_ERR_INVALID; }
-        g_lds_pad_kb = value;
     } else { set_error("unknown tuning key " + k); return MRT_ERR_INVALID; }
     return MRT_OK;
 }

@@ -82,7 +82,6 @@ struct Trav {
     const float4* verts = nullptr;
     const float4* verts2 = nullptr;
     bool near_first = false;   // any-hit walks descend into the nearest hit child first (order-free answer)
-    const QNode* lnodes = nullptr;   // A/B build MRT_LDS_NODES: the top of the hierarchy staged in LDS
 };
 
 struct TravStats {
@@ -242,11 +241,7 @@ __device__ __noinline__ bool mb_tri_test(const Trav& c, int32_t prim, const DRay
 // the reference's t-ordered retry loop.  aoff: PrimShade index of the leaf's
 // prim 0 (0 in the world; an instance's shade_base inside its BLAS, whose
 // alpha-mapped triangles -- the reference's tree proxies -- are tested too).
-#ifdef MRT_ALPHA_INLINE   // A/B build: the alpha test inlined into the walks
-__device__ __forceinline__
-#else
 __device__ __noinline__
-#endif
 bool alpha_rejects(const Trav& c, uint32_t leaf, int k, float a, float b, int32_t aoff) {
     const int32_t prim = c.leaves[leaf].prim[k] + aoff;
     const int am = c.amats[c.aprims[prim].mat].maps[kMapAlpha];
@@ -301,14 +296,10 @@ __device__ __forceinline__ bool tri_test_lane(const Trav& c, uint32_t leaf, int 
 #pragma unroll
         for (int i = 0; i < 9; i++) T[i] = q[i];
         ok = tri_test(T, r, tMin, tBest, t, a, b, c.rcpT) ? 1 : 0;
-#ifndef MRT_MERGE_TRI
         asm volatile("; mrt: scalar triangle" : "+v"(ok));
-#endif
     } else {
         ok = tri_test(c.leaves[leaf].tri[k], r, tMin, tBest, t, a, b, c.rcpT) ? 1 : 0;
-#ifndef MRT_MERGE_TRI
         asm volatile("; mrt: vector triangle" : "+v"(ok));
-#endif
     }
     return ok != 0;
 }
@@ -363,17 +354,6 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         // 64 copies through the vector memory path.
         const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
         float tn[4] = {0.f, 0.f, 0.f, 0.f};   // slot entry distances (any-hit near-first order)
-#ifdef MRT_LDS_NODES   // A/B build: the first MRT_LDS_NODES nodes (the top levels, host-renumbered) from LDS
-        if (FAST && c.lnodes && c0 < MRT_LDS_NODES && __ballot(cur != c0) == 0) {
-            const QNode& nd = c.lnodes[c0];   // one wave-uniform LDS address: broadcast reads
-            ch = make_int4(nd.child[0], nd.child[1], nd.child[2], nd.child[3]);
-            float4 bx[6];
-#pragma unroll
-            for (int k = 0; k < 6; k++) bx[k] = make_float4(nd.box[4 * k], nd.box[4 * k + 1], nd.box[4 * k + 2], nd.box[4 * k + 3]);
-            m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_fast(bx, r, tMin, h.t);
-            asm volatile("; mrt: lds node" : "+v"(m));
-        } else
-#endif
         if (FAST && (c.scalar_nodes & 1) && __ballot(cur != c0) == 0) {
             // constant address space + uniform address -> s_load_dwordx16 (node
             // data is read-only for the whole launch)
@@ -389,17 +369,13 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
             // distinct markers end the two branches, so the compiler cannot sink their
             // identical box tests into one block fed by 24 v_mov copies of the SGPR node:
             // this branch reads the boxes straight from SGPRs
-#ifndef MRT_MERGE_NODE   // A/B build: the merged form (v_mov copies of the SGPR node)
             asm volatile("; mrt: scalar node" : "+v"(m));
-#endif
         } else {
             const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
             ch = reinterpret_cast<const int4*>(q)[6];
             m = FAST ? ((ANY && c.near_first) ? box_test_fast_t(q, r, tMin, h.t, tn) : box_test_fast(q, r, tMin, h.t))
                      : box_test(q, r, tMin, h.t);
-#ifndef MRT_MERGE_NODE
             asm volatile("; mrt: vector node" : "+v"(m));
-#endif
         }
         if (COUNT) {
             st.nodes++;
@@ -434,25 +410,6 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
             nxt = sel4(ch, top);
             have_next = true;
         }
-#ifdef MRT_NODE_TOUCH   // A/B build: touch the next node's line before this step's leaf triangles
-        // The next node is fixed by now (the kept slot, or the stack top when nothing
-        // was pushed); one dword of it loaded here brings its line towards the CU while
-        // the triangles are tested, and the load's value is only consumed after them.
-        // MRT_NODE_TOUCH 2: a wave-uniform next node is touched through the scalar cache.
-        int32_t touch_v = 0, touch_s = 0;
-        if (FAST && lm) {
-            const int32_t pn = have_next ? nxt : ((sp > sp0 && sp <= kLdsStack) ? peek : -1);
-            const int32_t p0 = __builtin_amdgcn_readfirstlane(pn);
-            if (MRT_NODE_TOUCH >= 2 && __ballot(pn != p0) == 0) {
-                if (p0 >= 0) {
-                    typedef const __attribute__((address_space(4))) int32_t cint;
-                    touch_s = ((cint*)(const void*)(c.nodes + p0))[24];
-                }
-            } else if (pn >= 0) {
-                touch_v = reinterpret_cast<const int32_t*>(c.nodes + pn)[24];
-            }
-        }
-#endif
         if (lm) {
             uint32_t leaf = 0;
             int k = 0, cnt = 0;
@@ -503,9 +460,6 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                 k++;
             }
         }
-#ifdef MRT_NODE_TOUCH
-        asm volatile("; mrt: node touch" :: "v"(touch_v), "s"(touch_s));
-#endif
         if (have_next) {
             cur = nxt;
         } else {
@@ -513,289 +467,6 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
             if (sp <= kLdsStack) { cur = peek; sp--; }
             else cur = stk_pop(c, sp);
         }
-    }
-    return hit;
-}
-
-// traverse_impl<FAST = true> for plain scenes (no instances, alpha or motion
-// blur), with the stack work on wave-uniform branches: when no lane of the wave
-// is within 4 entries of the LDS column's end, every lane pushes with four
-// unconditional LDS writes (sp advancing by the slot's bit) and pops its peeked
-// top, with no per-lane branch; only a wave holding a deep lane takes the
-// per-lane path that spills to the HBM column.  The next node is the top hit
-// child or the popped entry, chosen per lane by a select.  Same node order, same
-// boxes and triangles tested with the same t as traverse_impl, so the same
-// hits and visit counts.
-template <bool ANY, bool COUNT>
-__device__ bool traverse_fast(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
-    int sp = 0;
-    int32_t cur = 0;
-    bool hit = false;
-    while (true) {
-        const int32_t peek = c.lds[(sp > 0 && sp <= kLdsStack ? sp - 1 : 0) * kWG];
-        int m;
-        int4 ch;
-        const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
-        float tn[4] = {0.f, 0.f, 0.f, 0.f};
-        if ((c.scalar_nodes & 1) && __ballot(cur != c0) == 0) {
-            typedef const __attribute__((address_space(4))) float cfloat;
-            typedef const __attribute__((address_space(4))) int32_t cint;
-            cfloat* q = (cfloat*)(const void*)(c.nodes + c0);
-            cint* qc = (cint*)(q + 24);
-            ch = make_int4(qc[0], qc[1], qc[2], qc[3]);
-            float4 bx[6];
-#pragma unroll
-            for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
-            m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_fast(bx, r, tMin, h.t);
-            asm volatile("; mrt: scalar node (fast walk)" : "+v"(m));
-        } else {
-            const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
-            ch = reinterpret_cast<const int4*>(q)[6];
-            m = (ANY && c.near_first) ? box_test_fast_t(q, r, tMin, h.t, tn) : box_test_fast(q, r, tMin, h.t);
-            asm volatile("; mrt: vector node (fast walk)" : "+v"(m));
-        }
-        if (COUNT) {
-            st.nodes++;
-            if (__ballot(cur != c0) == 0) st.uniform++;
-        }
-        const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
-        const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
-                           (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
-        const int inner = m & isinner;
-        int lm = m & isleaf;
-        const int top = (ANY && c.near_first && inner) ? nearest_slot(inner, tn)
-                                                       : 31 - __builtin_clz((unsigned)inner | 1u);
-        const int rest = inner & ~(1 << top);   // 0 when no inner slot was hit
-        if (__ballot(sp > kLdsStack - 4) == 0) {   // every lane has room: branch-free LDS pushes
-            c.lds[sp * kWG] = ch.x; sp += rest & 1;
-            c.lds[sp * kWG] = ch.y; sp += (rest >> 1) & 1;
-            c.lds[sp * kWG] = ch.z; sp += (rest >> 2) & 1;
-            c.lds[sp * kWG] = ch.w; sp += (rest >> 3) & 1;
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                if ((rest >> i) & 1)
-                    if (!stk_push(c, sp, sel4(ch, i))) { st.overflow = true; return hit; }
-        }
-        if (COUNT && sp > st.max_sp) st.max_sp = sp;
-        const int32_t nxt = sel4(ch, top);
-        if (lm) {
-            uint32_t leaf = 0;
-            int k = 0, cnt = 0;
-            while (true) {
-                if (k == cnt) {
-                    if (!lm) break;
-                    const int s = __builtin_ctz((unsigned)lm);
-                    lm &= lm - 1;
-                    const uint32_t v = ~(uint32_t)sel4(ch, s);
-                    leaf = v >> 4;
-                    cnt = (int)(v & 3u) + 1;
-                    k = 0;
-                    if (COUNT) st.leaves++;
-                }
-                float t, a, b;
-                if (tri_test_lane(c, leaf, k, r, tMin, h.t, t, a, b)) {
-                    if (ANY) return true;
-                    h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
-                    hit = true;
-                }
-                k++;
-            }
-        }
-        if (!inner && sp == 0) break;   // this lane's walk is over
-        if (__ballot(sp > kLdsStack) == 0) {   // every lane's top is in LDS: the peeked entry
-            const bool pop = inner == 0;
-            cur = pop ? peek : nxt;
-            sp -= pop ? 1 : 0;
-        } else if (inner) {
-            cur = nxt;
-        } else {
-            cur = stk_pop(c, sp);
-        }
-    }
-    return hit;
-}
-
-// Stackless form of traverse_impl<FAST = true> for plain scenes (A/B build
-// MRT_TRAV_STACKLESS; north_star's "stackless traversal"): no LDS or HBM stack.
-// Per depth the walk keeps the 4-bit mask of hit inner slots it has still to
-// visit (a 128-bit trail in registers); it descends into the highest hit slot,
-// and when a node has no hit inner slot it climbs back through the parent words
-// (QNode::pad[0]) to the deepest level with slots left and takes the highest of
-// them.  That is the order the stack walk pops its pushes in, with the masks of
-// the same box tests, so the same nodes are tested with the same t: the same
-// hits and visit counts.  The price is one dependent parent load per level
-// climbed instead of one LDS read per pop.
-template <bool ANY, bool COUNT>
-__device__ bool traverse_sl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
-    int32_t cur = 0;
-    int d = 0;
-    uint64_t lo = 0, hi = 0;   // trail: 4 bits per depth, depths 0-15 in lo, 16-31 in hi
-    bool hit = false;
-    while (true) {
-        int m;
-        int4 ch;
-        const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
-        float tn[4] = {0.f, 0.f, 0.f, 0.f};
-        if ((c.scalar_nodes & 1) && __ballot(cur != c0) == 0) {
-            typedef const __attribute__((address_space(4))) float cfloat;
-            typedef const __attribute__((address_space(4))) int32_t cint;
-            cfloat* q = (cfloat*)(const void*)(c.nodes + c0);
-            cint* qc = (cint*)(q + 24);
-            ch = make_int4(qc[0], qc[1], qc[2], qc[3]);
-            float4 bx[6];
-#pragma unroll
-            for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
-            m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_fast(bx, r, tMin, h.t);
-            asm volatile("; mrt: scalar node (stackless)" : "+v"(m));
-        } else {
-            const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
-            ch = reinterpret_cast<const int4*>(q)[6];
-            m = (ANY && c.near_first) ? box_test_fast_t(q, r, tMin, h.t, tn) : box_test_fast(q, r, tMin, h.t);
-            asm volatile("; mrt: vector node (stackless)" : "+v"(m));
-        }
-        if (COUNT) {
-            st.nodes++;
-            if (__ballot(cur != c0) == 0) st.uniform++;
-        }
-        const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
-        const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
-                           (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
-        const int inner = m & isinner;
-        int lm = m & isleaf;
-        if (lm) {
-            uint32_t leaf = 0;
-            int k = 0, cnt = 0;
-            while (true) {
-                if (k == cnt) {
-                    if (!lm) break;
-                    const int s = __builtin_ctz((unsigned)lm);
-                    lm &= lm - 1;
-                    const uint32_t v = ~(uint32_t)sel4(ch, s);
-                    leaf = v >> 4;
-                    cnt = (int)(v & 3u) + 1;
-                    k = 0;
-                    if (COUNT) st.leaves++;
-                }
-                float t, a, b;
-                if (tri_test_lane(c, leaf, k, r, tMin, h.t, t, a, b)) {
-                    if (ANY) return true;
-                    h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
-                    hit = true;
-                }
-                k++;
-            }
-        }
-        if (inner) {   // descend into the highest hit slot (nearest in any-hit near-first mode)
-            const int top = (ANY && c.near_first) ? nearest_slot(inner, tn) : 31 - __builtin_clz((unsigned)inner);
-            const uint64_t rest = (uint64_t)(inner ^ (1 << top));
-            if (d >= 32) { st.overflow = true; return hit; }
-            if (d < 16) lo |= rest << (4 * d);
-            else hi |= rest << (4 * (d - 16));
-            if (COUNT && d + 1 > st.max_sp) st.max_sp = d + 1;
-            cur = sel4(ch, top);
-            d++;
-            continue;
-        }
-        // climb to the deepest level with slots left (levels below the current one are empty)
-        int e;
-        if (hi) e = 16 + (63 - __builtin_clzll(hi)) / 4;
-        else if (lo) e = (63 - __builtin_clzll(lo)) / 4;
-        else break;   // nothing left: the walk is over
-        for (; d > e; d--) cur = (int32_t)c.nodes[cur].pad[0];
-        const int sh = 4 * (e & 15);
-        const int nib = (int)(((e < 16 ? lo : hi) >> sh) & 15u);
-        const int s = 31 - __builtin_clz((unsigned)nib);
-        const uint64_t clear = ~((uint64_t)1 << (sh + s));
-        if (e < 16) lo &= clear;
-        else hi &= clear;
-        cur = c.nodes[cur].child[s];
-        d = e + 1;
-    }
-    return hit;
-}
-
-struct NodeData {
-    float4 b[6];
-    int4 ch;
-};
-__device__ __forceinline__ NodeData load_node(const QNode* __restrict__ nodes, int32_t i) {
-    const float4* q = reinterpret_cast<const float4*>(nodes + i);
-    NodeData n;
-#pragma unroll
-    for (int k = 0; k < 6; k++) n.b[k] = q[k];
-    n.ch = reinterpret_cast<const int4*>(q)[6];
-    return n;
-}
-
-// traverse_impl<FAST = true> with the next node's fetch issued before the
-// current node's leaf triangles are tested.  The next node is fixed by the box
-// mask and the stack alone; only its box TEST needs the t the leaves may
-// lower, so the visit order (and every result) is unchanged while the node
-// fetch latency hides behind the triangle work.
-template <bool ANY, bool COUNT>
-__device__ bool traverse_pf(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
-    int sp = 0;
-    bool hit = false;
-    NodeData nd = load_node(c.nodes, 0);
-    while (true) {
-        const int32_t peek = c.lds[(sp > 0 && sp <= kLdsStack ? sp - 1 : 0) * kWG];
-        const int m = box_test_fast(nd.b, r, tMin, h.t);
-        const int4 ch = nd.ch;
-        if (COUNT) st.nodes++;
-        const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
-        const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
-                           (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
-        const int inner = m & isinner;
-        int lm = m & isleaf;
-        int32_t next = -1;
-        if (inner) {
-            const int top = 31 - __builtin_clz((unsigned)inner);
-            const int rest = inner ^ (1 << top);
-            if (rest) {
-                if (sp + 4 <= kLdsStack) {
-                    c.lds[sp * kWG] = ch.x; sp += rest & 1;
-                    c.lds[sp * kWG] = ch.y; sp += (rest >> 1) & 1;
-                    c.lds[sp * kWG] = ch.z; sp += (rest >> 2) & 1;
-                    c.lds[sp * kWG] = ch.w; sp += (rest >> 3) & 1;
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-                        if ((rest >> i) & 1)
-                            if (!stk_push(c, sp, sel4(ch, i))) { st.overflow = true; return hit; }
-                }
-                if (COUNT && sp > st.max_sp) st.max_sp = sp;
-            }
-            next = sel4(ch, top);
-        } else if (sp > 0) {
-            if (sp <= kLdsStack) { next = peek; sp--; }
-            else next = stk_pop(c, sp);
-        }
-        if (next >= 0) nd = load_node(c.nodes, next);
-        if (lm) {
-            uint32_t leaf = 0;
-            int k = 0, cnt = 0;
-            while (true) {
-                if (k == cnt) {
-                    if (!lm) break;
-                    const int s = __builtin_ctz((unsigned)lm);
-                    lm &= lm - 1;
-                    const uint32_t v = ~(uint32_t)sel4(ch, s);
-                    leaf = v >> 4;
-                    cnt = (int)(v & 3u) + 1;
-                    k = 0;
-                    if (COUNT) st.leaves++;
-                }
-                float t, a, b;
-                if (tri_test(c.leaves[leaf].tri[k], r, tMin, h.t, t, a, b, c.rcpT)) {
-                    if (ANY) return true;
-                    h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
-                    hit = true;
-                }
-                k++;
-            }
-        }
-        if (next < 0) break;
     }
     return hit;
 }
@@ -823,17 +494,13 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
 #pragma unroll
         for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
         m = c.near_first ? box_test_fast_t(bx, r, tMin, tMax, tn) : box_test_fast(bx, r, tMin, tMax);
-#ifndef MRT_MERGE_NODE
         asm volatile("; mrt: scalar node" : "+v"(m));   // see traverse_impl
-#endif
     } else {
         const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
         ch = reinterpret_cast<const int4*>(q)[6];
         m = FAST ? (c.near_first ? box_test_fast_t(q, r, tMin, tMax, tn) : box_test_fast(q, r, tMin, tMax))
                  : box_test(q, r, tMin, tMax);
-#ifndef MRT_MERGE_NODE
         asm volatile("; mrt: vector node" : "+v"(m));
-#endif
     }
     if (COUNT) st.nodes++;
     const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
@@ -1009,24 +676,8 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
 // An instance hit's id is the instance's hit_base + its BLAS object index.
 template <bool ANY, bool COUNT, bool FAST = false, bool INST = false>
 __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
-#ifdef MRT_PREFETCH  // build variant (make variant NAME=pf EXTRA=-DMRT_PREFETCH) for A/B runs
-    const bool hit = (FAST && r.finite && !INST) ? traverse_pf<ANY, COUNT>(c, r, tMin, h, st)
-                                                 : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
-#elif defined(MRT_TRAV_UNIFORM)   // A/B build (make variant NAME=uni EXTRA=-DMRT_TRAV_UNIFORM): the
-    // uniform-stack walk for plain scenes.  Round 4, interleaved on one MI355X
-    // (profiles/r04_walk_ab.txt): C3 +0.8..1.6% slower per frame, C3L 1.5% faster per
-    // launch but equal at 4 frames in flight, C2 / C4 within 0.5% -- not the default.
-    const bool hit = (FAST && r.finite) ? (INST ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
-                                                : traverse_fast<ANY, COUNT>(c, r, tMin, h, st))
-                                        : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
-#elif defined(MRT_TRAV_STACKLESS)   // A/B build (make variant NAME=sl EXTRA=-DMRT_TRAV_STACKLESS)
-    const bool hit = (FAST && r.finite) ? (INST ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
-                                                : traverse_sl<ANY, COUNT>(c, r, tMin, h, st))
-                                        : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
-#else
     const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
                                         : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
-#endif
     if (!ANY && hit) {
         h.prim = c.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3];
         if (INST && h.inst >= 0) h.prim += c.inst[h.inst].hit_base;

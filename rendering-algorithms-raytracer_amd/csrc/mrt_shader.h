@@ -90,22 +90,12 @@ struct RenderParams {
     uint32_t seed;
     int32_t fast_box;            // node boxes finite && tuning allows the hardware min/max box test
     int32_t sched;               // tile schedule (TileSched)
-    int32_t order;               // frame mode: 0 tiles bottom-up, 1 top-down (dequeue order only)
-    int32_t prio;                // 1: waves on their final tiles raise their issue priority
-    int32_t n_waves;             // waves in this launch (prio heuristic)
-    int32_t decline;             // >0: a wave in CU slot s stops taking tiles when fewer than s * decline remain
+    int32_t n_waves;             // waves in this launch
     int32_t refill_min;          // adaptive_kernel: 0 tile schedule, > 0 pixel refill at this many idle lanes
     int32_t near_first;          // any-hit walks take the nearest hit child first (their answer is order-free)
     int32_t cus;                 // compute units (slot of a persistent block = blockIdx / cus)
     int32_t scalar_nodes;        // scalar fetch of wave-uniform nodes
     unsigned int* queue;         // 8 tile counters, 32 words apart (sched >= 2)
-    unsigned int* done;          // frame1_kernel: finished-workgroup counter; the last one zeroes queue (null: off)
-    // cost-ordered tile queue (frame1_kernel, frame mode): dequeue rank r hands
-    // out tile tile_order[r] (the previous frame's slowest tiles first, so the
-    // launch drains on cheap tiles); tile_cost[t] receives this frame's cycles
-    // per tile for the next frame's order.  Either may be null.
-    const uint32_t* tile_order;
-    uint32_t* tile_cost;
     // work: 8x8 tiles
     int32_t tiles_x, n_tiles;    // frame mode: tiles_x = ceil(W/8)
     const int32_t* buckets;      // bucket mode: bucket ids (row-major bucket grid)
@@ -1071,21 +1061,12 @@ struct TileSched {
         int item = -1;
         const uint64_t q0 = P.wave_log ? wall_clock64() : 0;
         if (lane == 0) {
-            // decline: later-dispatched blocks (issue priority goes to older waves)
-            // leave the last tiles to the older, faster waves
-            const int slot = blockIdx.x / P.cus;
-            const int keep = P.decline * slot;
             while (probe < 8) {
                 const int c = (home + probe) & 7;
-                if (keep > 0 && mode == 2) {
-                    const unsigned seen = __hip_atomic_load(P.queue + c * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const long left = ((long)P.n_tiles - c + 7) / 8 - (long)seen;   // tiles left on counter c
-                    if (left * 8 < keep) { probe = 8; break; }
-                }
                 const unsigned v = atomicAdd(P.queue + c * 32, 1u);
                 const long idx = (mode == 3) ? (v < (unsigned)band ? (long)c * band + v : (long)P.n_tiles)
                                              : (long)c + 8l * v;
-                if (idx < P.n_tiles) { item = P.tile_order ? (int)P.tile_order[idx] : (int)idx; break; }
+                if (idx < P.n_tiles) { item = (int)idx; break; }
                 probe++;
             }
         }
@@ -1095,24 +1076,12 @@ struct TileSched {
     }
     // items are wave-uniform: readfirstlane puts them (and the frame / camera
     // lookups derived from them) in SGPRs
-    // prio 1: a wave whose tile is among the last n_waves handed out raises its
-    // issue priority (those tiles bound the launch); prio 2: also lowers it back
-    // to 0 before earlier tiles (reset)
-    __device__ void boost(int item) {
-        if (P.prio && item >= 0 && mode >= 2 && item_rank(item) >= P.n_tiles - P.n_waves) __builtin_amdgcn_s_setprio(3);
-        else if (P.prio == 2) __builtin_amdgcn_s_setprio(0);
-    }
-    // dequeue position of a tile under sched 2 / 3
-    __device__ int item_rank(int item) const {
-        if (mode == 3) return (item % band) * 8 + item / band;
-        return item;  // interleaved counters hand out tiles in index order overall
-    }
     __device__ int first() {
-        if (mode >= 2) { const int it = __builtin_amdgcn_readfirstlane(dequeue()); boost(it); return it; }
+        if (mode >= 2) return __builtin_amdgcn_readfirstlane(dequeue());
         return __builtin_amdgcn_readfirstlane(cur < end ? cur : -1);
     }
     __device__ int next(int item) {
-        if (mode >= 2) { const int it = __builtin_amdgcn_readfirstlane(dequeue()); boost(it); return it; }
+        if (mode >= 2) return __builtin_amdgcn_readfirstlane(dequeue());
         item += step;
         return __builtin_amdgcn_readfirstlane(item < end ? item : -1);
     }
@@ -1128,8 +1097,7 @@ __device__ __forceinline__ int item_frame(const RenderParams& P, int item) {
 // work item + lane -> pixel (x, y) and output slot
 __device__ __forceinline__ bool item_pixel(const RenderParams& P, int item, int lane, int& x, int& y, size_t& slot) {
     if (P.mode == 0) {
-        const int t = P.order ? P.n_tiles - 1 - item : item;
-        int tx = t % P.tiles_x, ty = t / P.tiles_x;
+        int tx = item % P.tiles_x, ty = item / P.tiles_x;
         x = tx * 8 + (lane & 7);
         y = ty * 8 + (lane >> 3);
         slot = (size_t)y * P.cam[0].W + x;
@@ -1566,6 +1534,10 @@ static KernelFn pick4(bool c, bool po, bool f, bool inst) {
 template <bool C, bool PO, bool F, bool I, int REC>
 struct ShadeK { static constexpr KernelFn fn = shade_kernel<C, PO, F, I, kFused, REC>; };
 
+// defined in mrt_frame.hip: the one-point-light frame / shade kernels at an
+// occupancy target w; pow: a Blinn material with specExp != 1
+KernelFn pick_frame1(int w, bool c, bool f, bool pow);
+KernelFn pick_shade1(int w, bool c, bool f, bool pow);
 // defined in mrt_rec.hip: the fused chain kernels (rec 1: reflection / refraction,
 // 2: + path tracing) and the adaptive supersampling kernels (any rec)
 KernelFn pick_shade_rec(bool c, bool po, bool f, bool inst, int rec);
