@@ -440,6 +440,7 @@ def main():
             with torch.cuda.stream(pipe.streams[b]):
                 render(items, pipe.tiles[b])
         torch.cuda.synchronize()
+        pipe.out_f, pipe.out_8 = out_f, out_8   # rank 0's assembled frames, one per buffer
         return pipe, render, items, mine, out_f
 
     def count_rays(render_count):
@@ -520,6 +521,29 @@ def main():
         _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(o), frame[i].data_ptr(),
                                             frame8[i].data_ptr(), streams[i].cuda_stream), "render")
 
+    def check_timed_frame(t_f, t_8):
+        """The last timed frame (rank 0's assembled frame at N > 1) against the same
+        camera rendered once on its own through mrt_render_frame_async, the path the
+        full-size parity tests compare with the oracle (tests/test_full_size.py):
+        sha256 of the float and 8-bit frames, after the timed region."""
+        import hashlib
+        torch.cuda.synchronize()
+        ref_f = torch.empty(H * W * 3, dtype=torch.float32, device="cuda")
+        ref_8 = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")
+        _lib.check(L.mrt_render_frame_async(scene.handle, C.byref(camc[0]), C.byref(opts), ref_f.data_ptr(),
+                                            ref_8.data_ptr(), stream.cuda_stream), "render (frame check)")
+        torch.cuda.synchronize()
+
+        def digest(a, b):
+            h = hashlib.sha256()
+            if a is not None:
+                h.update(a.reshape(-1)[:H * W * 3].cpu().numpy().tobytes())
+            h.update(b.reshape(-1)[:H * W * 3].cpu().numpy().tobytes())
+            return h.hexdigest()[:16]
+        got, ref = digest(t_f, t_8), digest(ref_f if t_f is not None else None, ref_8)
+        return {"timed_frame_sha256": got, "single_frame_sha256": ref, "equal": got == ref,
+                "compared": ("float + 8-bit" if t_f is not None else "8-bit") + " RGB of the last timed step's frame"}
+
     adaptive = bool(cfg.get("subdivs")) and max(cfg["subdivs"][:2]) > 1
     if args.share:
         share_mode(args, dict(scene=scene, cfg=cfg, W=W, H=H, bpf=bpf, L=L, _lib=_lib, tiles_mod=tiles_mod, torch=torch, np=np, make_pipe=make_pipe, count_rays=count_rays, timed=timed, frame_step=frame_step, streams=streams, frame=frame, frame8=frame8, opts=opts, opts_count=opts_count, camc=camc, adaptive=adaptive, inflight=inflight), [int(x) for x in args.share.split(",") if x.strip()])
@@ -536,10 +560,15 @@ def main():
         mine, items = None, None
         progress("timed region")
         elapsed = timed(frame_step, lambda: None, args.steps)
+        last = (nstep[0] - 1) % inflight
+        frame_check = check_timed_frame(frame[last], frame8[last])
     else:
         pipe, render, items, mine, _ = make_pipe(n_frames, float_tiles=split)
         st, (shadow_total, eye_total, second_total) = count_rays(lambda: render(items, pipe.tiles[0], opts_count))
         elapsed = timed(pipe.step, pipe.flush, args.steps)
+        last = (pipe.k - 1) % pipe.depth
+        frame_check = check_timed_frame(pipe.out_f[last] if split else None, pipe.out_8[last]) \
+            if rank == 0 and n_frames == 1 else None
     shadow_mine, eye_mine, second_mine = st["shadow_rays"], (st["primary_rays"] if adaptive else 0), st["secondary_rays"]
     primary_total = eye_total if adaptive else n_frames * W * H
     rays_per_step = primary_total + shadow_total + second_total      # all frames of the batch, all ranks
@@ -674,6 +703,37 @@ def main():
             if ent.get("code_object"):
                 latency["code_object"] = ent["code_object"]
             break
+    # SURVEY.md 8(d)'s own pricing of the same bytes: algorithmic bytes against HBM.  Above 1
+    # it is non-physical -- those node / leaf bytes are served by L1 (98% hits) and L2, and the
+    # PMC-measured DRAM-side bytes (`hbm`, per_step.hbm_frac_counters) are a few % of HBM
+    hbm_alg = {"frac_per_launch": round(achieved / HBM_PEAK_GBS, 4), "frac_per_step": round(step_gbs / HBM_PEAK_GBS, 4),
+               "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "note": "SURVEY.md 8(d) pricing (algorithmic bytes / 8 TB/s); non-physical above 1: the bytes are "
+                       "served by L1 / L2, not HBM (see hbm / per_step.hbm_frac_counters for the DRAM-side bytes)"}
+    # latency model of the one-launch frame kernel: every wave walks its tiles' rays one
+    # dependent node step at a time (a step = node fetch -> box test -> push / pop, then the
+    # step's leaf triangles); a tile costs its slowest lane's steps (count-mode wave steps,
+    # primary + shadow).  With `waves` resident waves per SIMD sharing the launch time, the
+    # time one wave spends per step is launch_ms / (wave steps / resident wave slots).
+    lat_model = None
+    wsteps = st.get("primary_wave_steps", 0) + st.get("shadow_wave_steps", 0)
+    if st.get("fused") and wsteps:
+        simds = 4 * int(torch.cuda.get_device_properties(dev).multi_processor_count)
+        waves = int(tuning.get("frame1_waves", 7))
+        per_slot = wsteps / (simds * waves)
+        ns_step = dom_ms * 1e6 / per_slot
+        lat_model = {
+            "wave_steps_per_frame": int(wsteps), "resident_wave_slots": simds * waves,
+            "steps_per_wave_slot": round(per_slot, 1), "ns_per_step_per_wave": round(ns_step, 1),
+            "cycles_per_step_at_2p4ghz": round(ns_step * 2.4, 0),
+            "l2_hit_latency_cycles": "180-225 (MI355X_MICROARCH.md, one lane, idle chip)",
+            "lane_use": round((st["primary_node_visits"] + st.get("shadow_node_visits", 0)) / (64.0 * wsteps), 4),
+            "reading": ("latency-bound: each resident wave spends ~%.0f cycles per dependent node step (one node "
+                        "fetch + box test + stack op, plus the step's triangle tests), ~1-2 cache-hit latencies; "
+                        "%d waves per SIMD overlap them, so the frame takes steps-per-slot x that step latency. Neither "
+                        "bandwidth roofline binds (L2 frac %.2f, counter HBM frac %s)."
+                        % (ns_step * 2.4, waves, achieved / L2_PEAK_GBS,
+                           "n/a" if hbm is None else "%.3f" % hbm["frac"]))}
     # primary-kernel lanes doing node work per issued wave step (adaptive: no primary launch)
     lane_util = round(st["primary_node_visits"] / (64 * st["primary_wave_steps"]), 4) if st["primary_wave_steps"] else None
     out = {
@@ -713,9 +773,13 @@ def main():
         "roofline": {"bound": "l2", "kernel": dom, "achieved": round(achieved, 1), "peak": L2_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / L2_PEAK_GBS, 4),
                      "traffic": None if dom_traffic is None else int(dom_traffic),
-                     "hbm": hbm, "tracked_profile": tracked, "latency": latency, "lane_util": lane_util,
+                     "hbm": hbm, "hbm_algorithmic": hbm_alg, "latency_model": lat_model,
+                     "tracked_profile": tracked, "latency": latency, "lane_util": lane_util,
                      "launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(dom_b),
                      "per_step": per_step,
+                     # count-mode chunks of the chain engine re-rendered by the fused fallback: their node /
+                     # leaf visits are not in the counts above, so visits_per_ray is a floor then
+                     "chain_fallbacks_in_count_frame": int(st.get("chain_fallbacks", 0)),
                      "visits_per_ray": round(st["node_visits"] / max(1, (eye_mine if adaptive else px_mine)
                                                                     + shadow_mine + second_mine), 3)},
         "launch_ms": {"primary": round(pm, 4), "shade": round(sm, 4)},
@@ -747,6 +811,8 @@ def main():
     if rehearse:
         out["rehearsal"] = (f"MRT_BENCH_REHEARSE=gloo: {world} ranks sharing ONE GPU, collectives over gloo through "
                             f"host copies -- a run of the multi-rank code, not a measurement")
+    if frame_check is not None:
+        out["frame_check"] = frame_check
     if split_times is not None:
         out["split_times"] = split_times
     if weak is not None:

@@ -66,6 +66,13 @@ static inline float std_min(float a, float b) { return b < a ? b : a; }   /* std
 static inline float std_max(float a, float b) { return a < b ? b : a; }   /* std::max */
 
 float oro_x86_rcp(float x) { return x86_rcp(x); }
+/* glibc's acosf (fn 0) / atan2f(y, x) (fn 1): the float overloads the reference
+ * calls (src/Material.h:51, src/Texture.cpp:82-93), for the device probe's test */
+int oro_libm_eval(int fn, size_t n, const float* x, const float* y, float* out) {
+    if (fn != 0 && fn != 1) return -1;
+    for (size_t i = 0; i < n; i++) out[i] = fn == 0 ? acosf(x[i]) : atan2f(y[i], x[i]);
+    return 0;
+}
 float oro_x86_rsqrt(float x) { return x86_rsqrt(x); }
 float oro_rcp_nr(float x) { return rcp_nr(x); }
 float oro_rsqrt_nr(float x) { return rsqrt_nr(x); }
@@ -290,6 +297,12 @@ int oro_scene_add_light(oro_scene* s, const oro_light* l) {
     return s->n_lights++;
 }
 void oro_scene_set_bg(oro_scene* s, float r, float g, float b) { s->bg = V(r, g, b); }
+/* libm convention (oro_ibl.h): 1 = the reference's float overloads, 0 = double rounded once */
+int oro_set_libm(int float_overloads) {
+    const int prev = oro_libm_float;
+    oro_libm_float = float_overloads ? 1 : 0;
+    return prev;
+}
 void oro_scene_set_num_paths(oro_scene* s, int n) { s->num_paths = n < 1 ? 1 : (n > 1024 ? 1024 : n); }
 int oro_scene_set_path_trace(oro_scene* s, int enable, int max_bounces, int sample_env) {
     if (max_bounces < 1 || max_bounces > 64) return -1;
@@ -1654,19 +1667,19 @@ typedef struct { int bounces, gi, secondary, level, refr, branch; } chain_t;
 
 static v3 shade_hit(shade_ctx* c, const ray_t* r, const hit_t* h, ior_list* ior, chain_t ch);
 
-/* Material::fresnel (full form, src/Material.h:47-55); sin/acos of the
- * reference's libm evaluated in double and rounded once. */
+/* Material::fresnel (full form, src/Material.h:47-55): n1*sin(acosf(cosThetaI))/n2,
+ * sinf / acosf under oro_libm_float. */
 static float fresnel(float n1, float n2, float cosThetaI) {
     const float n1CosTh = n1 * cosThetaI;
-    const float th = (float)acos((double)cosThetaI);
-    const float n1_n2SinTh = (n1 * (float)sin((double)th)) / n2;
+    const float th = oro_acos(cosThetaI);
+    const float n1_n2SinTh = (n1 * oro_sin(th)) / n2;
     const float n2CosTh = n2 * std_max(0.0f, sqrtf(1.0f - n1_n2SinTh * n1_n2SinTh));
     const float Rs = (n1CosTh - n2CosTh) / (n1CosTh + n2CosTh);
     return Rs * Rs;
 }
 
 /* Material::getCosineDistributedSamples, src/Material.cpp:14-41 (SSE path);
- * libm cos / sin evaluated in double and rounded once. */
+ * cos / sin of the float _2_PI_e1 (cosf / sinf under oro_libm_float). */
 static v3 cosine_sample(shade_ctx* c, v3 N) {
     const float e1 = next_rand(c);
     float e2 = next_rand(c);
@@ -1676,7 +1689,7 @@ static v3 cosine_sample(shade_ctx* c, v3 N) {
     float _2_PI_e1 = 2 * PI_F * e1;
     float sqrte2 = rcp_nr(rsqrt_nr(e2));
     float sqrt1_e2 = rcp_nr(rsqrt_nr(fabsf(1.0f - e2)));
-    float cs = (float)cos((double)_2_PI_e1), sn = (float)sin((double)_2_PI_e1);
+    float cs = oro_cos(_2_PI_e1), sn = oro_sin(_2_PI_e1);
     return vnormalized(vadd(vadd(vscale(u, cs * sqrte2), vscale(v, sn * sqrte2)), vscale(N, sqrt1_e2)));
 }
 
@@ -1819,8 +1832,8 @@ static v3 shade_blinn(shade_ctx* c, const oro_material* mat, const ray_t* r, con
         for (int i = 0; i < c->s->n_lights; i++) {
             float lightSpec = 0;
             v3 E = sample_light(c, i, P, theNormal, rVec, &lightSpec, ch.secondary);
-            /* libm pow of the reference, evaluated in double and rounded once */
-            float pw = (float)pow((double)lightSpec, (double)mat->specExp);
+            /* pow(lightSpec, localSpecExp) of floats, src/Blinn.cpp:219 (powf under oro_libm_float) */
+            float pw = oro_pow(lightSpec, mat->specExp);
             Ls = vadd(Ls, vscale(vscale(vmul(E, ks), specAmt), pw));
             Ld = vadd(Ld, vmul(E, kd));
         }

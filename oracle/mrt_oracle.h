@@ -90,6 +90,12 @@ void oro_scene_destroy(oro_scene* s);
 int oro_scene_add_material(oro_scene* s, const oro_material* m);
 int oro_scene_add_light(oro_scene* s, const oro_light* l);
 void oro_scene_set_bg(oro_scene* s, float r, float g, float b);
+/* libm convention of Fresnel's sin, Blinn's pow and the cosine sampler's cos / sin:
+ * 1 (default) = the float overloads the reference's source calls (glibc sinf / powf /
+ * cosf), 0 = the same functions in double, rounded once (the device's convention).
+ * atan2 / acos are glibc's atan2f / acosf either way (oro_ibl.h).  Process-wide;
+ * returns the previous setting. */
+int oro_set_libm(int float_overloads);
 void oro_scene_set_num_paths(oro_scene* s, int n);
 /* Scene::m_pathTrace / m_maxBounces / m_sampleLightFromEnv (src/Scene.h:40-64) */
 int oro_scene_set_path_trace(oro_scene* s, int enable, int max_bounces, int sample_env);
@@ -174,6 +180,8 @@ int oro_texture_lookup_dir(const oro_scene* s, int tex, int n, const float* dirs
 
 /* numerics probes (for tests) */
 float oro_x86_rcp(float x);
+/* glibc acosf(x) (fn 0) / atan2f(y, x) (fn 1) over n inputs; 0 = ok */
+int oro_libm_eval(int fn, size_t n, const float* x, const float* y, float* out);
 float oro_x86_rsqrt(float x);
 float oro_rcp_nr(float x);
 float oro_rsqrt_nr(float x);

@@ -17,6 +17,35 @@ _LIB_PATH = os.path.join(_HERE, "_build", "libmrt_oracle.so")
 _lib = None
 
 
+# libm convention of the oracle's restated sin / cos / pow calls (oro_set_libm, oro_ibl.h):
+#   "float"  -- the float overloads the reference's source resolves to under g++
+#               (sin(acosf(x)) -> sinf, pow(float, float) -> powf, cos/sin of floats ->
+#               cosf/sinf; src/Material.h:51, src/Blinn.cpp:219, src/Material.cpp:41), glibc
+#               here: the reference's own calls;
+#   "device" -- the same functions evaluated in double and rounded once, the HIP
+#               device's convention (bit-exact comparisons of everything around them).
+# atan2 / acos (src/Texture.cpp:82-93, the acosf of src/Material.h:51) are glibc's
+# atan2f / acosf in both: the device restates them bit-exactly (csrc/mrt_libm.h).
+LIBM_FLOAT, LIBM_DEVICE = "float", "device"
+_default_libm = LIBM_FLOAT
+
+
+def set_default_libm(mode):
+    """Convention for render / texture_lookup_dir calls that do not name one; returns the previous."""
+    global _default_libm
+    if mode not in (LIBM_FLOAT, LIBM_DEVICE):
+        raise ValueError(mode)
+    prev, _default_libm = _default_libm, mode
+    return prev
+
+
+def _apply_libm(mode):
+    mode = mode or _default_libm
+    if mode not in (LIBM_FLOAT, LIBM_DEVICE):
+        raise ValueError(mode)
+    lib().oro_set_libm(1 if mode == LIBM_FLOAT else 0)
+
+
 def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
@@ -80,6 +109,7 @@ def _declare(L):
     L.oro_scene_build.argtypes = [C.c_void_p]
     L.oro_qbvh_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 6
     L.oro_qbvh_export.argtypes = [C.c_void_p, _fp, _i32p, _fp, _i32p]
+    L.oro_set_libm.argtypes = [C.c_int]
     L.oro_trace.argtypes = [C.c_void_p, C.c_size_t, _fp, _fp, _fp, _fp, C.c_void_p, _u32p, _u32p]
     L.oro_render.argtypes = [C.c_void_p, C.POINTER(Camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                              _fp, _u8p, C.c_void_p, _u32p, _u64p, C.c_int]
@@ -345,7 +375,8 @@ class OracleScene:
         self.L.oro_dome_export(self.h, light, *[_p(out[k], _fp) for k in DOME_KEYS])
         return out
 
-    def texture_lookup_dir(self, texture, dirs):
+    def texture_lookup_dir(self, texture, dirs, libm=None):
+        _apply_libm(libm)
         d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
         out = np.zeros_like(d)
         if self.L.oro_texture_lookup_dir(self.h, int(texture), len(d), _p(d, _fp), _p(out, _fp)) != 0:
@@ -403,8 +434,10 @@ class OracleScene:
             raise RuntimeError(f"oracle trace failed ({r})")
         return out, nv, lv
 
-    def render(self, cam, W, H, rect=None, threads=1, want_hits=True):
-        """cam: dict(eye, lookAt, up, fov[, aperture, focusPlane, shutterSpeed]).  Returns dict of numpy arrays."""
+    def render(self, cam, W, H, rect=None, threads=1, want_hits=True, libm=None):
+        """cam: dict(eye, lookAt, up, fov[, aperture, focusPlane, shutterSpeed]).  Returns dict of numpy arrays.
+        libm: LIBM_FLOAT / LIBM_DEVICE (None: the module default, set_default_libm)."""
+        _apply_libm(libm)
         c = Camera(_v3(cam["eye"]), _v3(cam.get("up", (0, 1, 0))), _v3(cam["lookAt"]), float(cam["fov"]),
                    float(cam.get("aperture", 0.0)), float(cam.get("focusPlane", 1.0)),
                    float(cam.get("shutterSpeed", 0.001)))
@@ -424,6 +457,18 @@ class OracleScene:
                 "node_visits": int(counters[2]), "leaf_visits": int(counters[3]),
                 "primary_node_visits": int(counters[4]), "primary_leaf_visits": int(counters[5]),
                 "secondary_rays": int(counters[6])}
+
+
+def libm_eval(fn, x, y=None):
+    """glibc acosf(x) ("acos") or atan2f(y, x) ("atan2"), elementwise."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.ascontiguousarray(np.zeros_like(x) if y is None else y, np.float32)
+    out = np.empty_like(x)
+    L = lib()
+    L.oro_libm_eval.argtypes = [C.c_int, C.c_size_t, _fp, _fp, _fp]
+    if L.oro_libm_eval({"acos": 0, "atan2": 1}[fn], len(x), _p(x, _fp), _p(y, _fp), _p(out, _fp)) != 0:
+        raise ValueError(fn)
+    return out
 
 
 def x86_rcp(x):

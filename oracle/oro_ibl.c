@@ -20,6 +20,8 @@
  */
 #include "oro_ibl.h"
 
+int oro_libm_float = 1;
+
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -191,11 +193,12 @@ void ibl_lookup3(const ibl_image* t, float u, float v, float out[3]) {
     }
 }
 
-/* Texture::getLookupXYZ3, src/Texture.cpp:80-98: u = theta * 0.5 * _1_PI and
+/* Texture::getLookupXYZ3, src/Texture.cpp:80-98: atan2(z, x) and acos(y) of
+ * floats (atan2f / acosf, oro_libm_float); u = theta * 0.5 * _1_PI and
  * v = 1.0 - phi * _1_PI are evaluated in double (double literals) and rounded. */
 void ibl_lookup_dir(const ibl_image* t, float x, float y, float z, float out[3]) {
-    float theta = (float)atan2((double)z, (double)x) + PI_F;
-    float phi = (float)acos((double)y);
+    float theta = oro_atan2(z, x) + PI_F;
+    float phi = oro_acos(y);
     float u = (float)((double)theta * 0.5 * (double)INV_PI);
     float v = (float)(1.0 - (double)(phi * INV_PI));
     ibl_lookup3(t, u, v, out);

@@ -6,6 +6,8 @@
 #ifndef ORO_IBL_H
 #define ORO_IBL_H
 
+#include <math.h>
+
 typedef struct {            /* RawImage (src/RawImage.h): W*H*channels floats, row 0 = top */
     float* rgb;
     int W, H;
@@ -36,5 +38,20 @@ void ibl_lookup_dir(const ibl_image* t, float x, float y, float z, float out[3])
 int ibl_dome_init(ibl_dome* d, const ibl_image* tex);
 void ibl_dome_free(ibl_dome* d);
 float ibl_dist_sample(const ibl_dist* d, float u, float* pdf);
+
+/* The reference's libm calls on floats resolve to the float overloads under g++
+ * (`using namespace std` + <math.h>): sin(acosf(x)) -> sinf / acosf (src/Material.h:51),
+ * pow(float, float) -> powf (src/Blinn.cpp:219), atan2 / acos -> atan2f / acosf
+ * (src/Texture.cpp:82-83,92-93), cos / sin -> cosf / sinf (src/Material.cpp:41).
+ * atan2f / acosf are always glibc's (the device restates them bit-exactly).  For
+ * sinf / cosf / powf the convention is selectable (oro_set_libm): 1 (default) = glibc's
+ * float functions, the reference's own calls; 0 = the function in double, rounded once
+ * (the HIP device's convention, within 1 ulp of glibc's). */
+extern int oro_libm_float;
+static inline float oro_acos(float x) { return acosf(x); }
+static inline float oro_atan2(float y, float x) { return atan2f(y, x); }
+static inline float oro_sin(float x) { return oro_libm_float ? sinf(x) : (float)sin((double)x); }
+static inline float oro_cos(float x) { return oro_libm_float ? cosf(x) : (float)cos((double)x); }
+static inline float oro_pow(float x, float y) { return oro_libm_float ? powf(x, y) : (float)pow((double)x, (double)y); }
 
 #endif

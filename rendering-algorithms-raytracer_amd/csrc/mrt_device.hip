@@ -209,6 +209,12 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
 }
 
 
+// Numerics probe (mrt_debug_libm): the device's acosf / atan2f (mrt_libm.h).
+__global__ void __launch_bounds__(256) libm_kernel(int fn, const float* x, const float* y, size_t n, float* out) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        out[i] = fn == 0 ? fd_acosf(x[i]) : fd_atan2f(y[i], x[i]);
+}
+
 // Batched Scene::trace: one lane per query ray.
 template <bool ANY, bool INST = false>
 __global__ void __launch_bounds__(kWG) trace_kernel(const QNode* nodes, const DLeaf* leaves, const uint16_t* tables,
@@ -2797,6 +2803,33 @@ int mrt_set_tuning(const char* key, int value) {
         g_sched = value;
     } else { set_error("unknown tuning key " + k); return MRT_ERR_INVALID; }
     return MRT_OK;
+}
+
+int mrt_debug_libm(int fn, const float* x, const float* y, size_t n, float* out) {
+    if ((fn != 0 && fn != 1) || !x || !out || (fn == 1 && !y)) { set_error("bad libm probe arguments"); return MRT_ERR_INVALID; }
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) { set_error("no HIP device"); return MRT_ERR_NO_DEVICE; }
+    if (n == 0) return MRT_OK;
+    float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    const size_t b = n * sizeof(float);
+    int rc = MRT_OK;
+    auto run = [&]() -> int {
+        HIP_OK(hipMalloc((void**)&dx, b));
+        HIP_OK(hipMalloc((void**)&dy, b));
+        HIP_OK(hipMalloc((void**)&dout, b));
+        HIP_OK(hipMemcpy(dx, x, b, hipMemcpyHostToDevice));
+        if (fn == 1) HIP_OK(hipMemcpy(dy, y, b, hipMemcpyHostToDevice));
+        const int blocks = (int)std::min<size_t>((n + 255) / 256, 65536);
+        hipLaunchKernelGGL(libm_kernel, dim3(blocks), dim3(256), 0, 0, fn, dx, dy, n, dout);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipMemcpy(out, dout, b, hipMemcpyDeviceToHost));
+        return MRT_OK;
+    };
+    rc = run();
+    if (dx) (void)hipFree(dx);
+    if (dy) (void)hipFree(dy);
+    if (dout) (void)hipFree(dout);
+    return rc;
 }
 
 float mrt_rcp_nr(float x) { return rcp_nr(x, host_rcp_table()); }

@@ -57,8 +57,12 @@ __device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, T
         const float distance = rcp_nr(distanceRecip, rcpT);
         L = scale(L, distanceRecip);
         nDotL *= distanceRecip;
-        const float Aterm = (l.power * falloff) * (0.25f / 3.1415926f);
-        const float rdl = std_max(0.f, dot(rVec, L));
+        float Aterm = (l.power * falloff) * (0.25f / 3.1415926f);
+        float rdl = std_max(0.f, dot(rVec, L));
+        // Only these three scalars stay live across the shadow traversal: without the
+        // pin the compiler sinks both products below it, keeping rVec, L, falloff and
+        // the light's power live instead (4 spilled values per pixel)
+        asm volatile("" : "+v"(Aterm), "+v"(rdl), "+v"(nDotL));
         float attenuate = 1.0f;
         if (l.cast_shadows) {
             const DRay sr = make_ray(from, L);
@@ -84,7 +88,9 @@ __device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, T
         const v3 z = mk(0, 0, 0);
         sh = add(add(scale(add(add(Ld, Ls), z), 1.0f), scale(add(z, z), 1.0f)), mk(M.le[0], M.le[1], M.le[2]));
     }
-    return scale(add(mk(0, 0, 0), sh), 1.0f / (float)P.num_paths);
+    // the path average of Scene::sampleScene with num_paths == 1 (the only case
+    // these kernels run): x * (1 / 1) == x, so the scale is left out
+    return add(mk(0, 0, 0), sh);
 }
 
 __device__ __forceinline__ void write_pixel(const RenderParams& P, size_t slot, v3 col) {
@@ -161,7 +167,7 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     trav_alpha(T, P);
     TravStats st, ss;   // primary / shadow rays (count mode)
     uint32_t nhits = 0, shadow_total = 0;
-    unsigned long long wave_steps = 0;
+    unsigned long long wave_steps = 0, wave_steps_s = 0;   // count mode: per tile, the max node steps over lanes
     TileSched ts(P, wave, lane);
     uint32_t ntiles = 0;
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
@@ -174,7 +180,7 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
         ntiles++;
         int x, y;
         size_t slot;
-        const uint32_t n0 = st.nodes;
+        const uint32_t n0 = st.nodes, s0 = ss.nodes;
         if (item_pixel(P, item, lane, x, y, slot)) {
             const int f = item_frame(P, item);
             const EyeRay er = camera_ray(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
@@ -191,12 +197,24 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
             write_pixel(P, slot, col);
         }
         if (COUNT) {
-            uint32_t dmax = st.nodes - n0;
-            for (int off = 32; off > 0; off >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor(dmax, off));
+            uint32_t dmax = st.nodes - n0, smax = ss.nodes - s0;
+            for (int off = 32; off > 0; off >>= 1) {
+                dmax = max(dmax, (uint32_t)__shfl_xor(dmax, off));
+                smax = max(smax, (uint32_t)__shfl_xor(smax, off));
+            }
             wave_steps += dmax;
+            wave_steps_s += smax;
         }
     }
-    if (COUNT && lane == 0) atomicAdd(&P.ctr[CTR_WAVE_STEPS_P], wave_steps);
+    if (COUNT) {   // the shadow rays' node visits and wave steps (the latency model of bench.py)
+        unsigned long long sv = ss.nodes;
+        for (int off = 32; off > 0; off >>= 1) sv += __shfl_down(sv, off);
+        if (lane == 0) {
+            atomicAdd(&P.ctr[CTR_WAVE_STEPS_P], wave_steps);
+            atomicAdd(&P.ctr[CTR_WAVE_STEPS_S], wave_steps_s);
+            atomicAdd(&P.ctr[CTR_NODES_S], sv);
+        }
+    }
     // one wall-clock record per wave (the primary span counters; the wave log counts both kinds' nodes)
     flush_stats<COUNT, true>(P, st, nhits, lane, t0, ntiles, ss.nodes);
     flush_stats<COUNT, false, false>(P, ss, shadow_total, lane, t0, ntiles);

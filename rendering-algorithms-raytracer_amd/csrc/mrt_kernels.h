@@ -21,7 +21,7 @@ namespace mrt {
 
 static constexpr int kWG = 256;          // threads per workgroup (4 waves)
 static constexpr int kLdsStack = 16;     // stack entries per lane kept in LDS (max seen: 11)
-static constexpr int kGlobalStack = 80;  // spill entries per thread in HBM
+static constexpr int kGlobalStack = 240; // spill entries per thread in HBM: 256 in all, the reference's stack (src/BVH.cpp:1133)
 static constexpr int kTableWords = 4096; // rcp[2048] + rsqrt[2048] (u16)
 
 struct DRay {

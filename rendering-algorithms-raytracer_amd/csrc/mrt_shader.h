@@ -658,11 +658,12 @@ struct Shader {
         return scale(result, 1.0f / (float)P.num_paths);
     }
 
-    // Material::fresnel, full form (src/Material.h:47-55); the reference's libm
-    // acos / sin evaluated in double and rounded once (as in the oracle)
+    // Material::fresnel, full form (src/Material.h:47-55): n1*sin(acosf(c))/n2.
+    // acosf is glibc's (fd_acosf, bit-exact); sinf is evaluated in double and rounded
+    // once (glibc's sinf is within 0.56 ulp of that; tools/libm_parity.py)
     __device__ static float fresnel(float n1, float n2, float c) {
         const float n1CosTh = n1 * c;
-        const float th = (float)acos((double)c);
+        const float th = fd_acosf(c);
         const float n1_n2SinTh = (n1 * (float)sin((double)th)) / n2;
         const float n2CosTh = n2 * std_max(0.0f, sqrtf(1.0f - n1_n2SinTh * n1_n2SinTh));
         const float Rs = (n1CosTh - n2CosTh) / (n1CosTh + n2CosTh);
@@ -1070,7 +1071,7 @@ struct TileSched {
                 probe++;
             }
         }
-        item = __shfl(item, 0);
+        item = __builtin_amdgcn_readlane(item, 0);   // lane 0's atomic, as a scalar
         if (P.wave_log) deq_ticks = (uint32_t)(wall_clock64() - q0);
         return item;
     }

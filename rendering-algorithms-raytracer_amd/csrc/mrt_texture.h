@@ -6,13 +6,15 @@
 // src/Texture.cpp:43-125) for RGB / HDR float images (RawImage m_rawData, row 0 =
 // top scanline of the file, 3 floats per texel), and Distribution1D::sample
 // (src/DomeLight.h:31-38).  Same single-precision operations in the same order as
-// the reference; atan2 / acos (libm in the reference) are evaluated in double and
-// rounded once, as the CPU restatement does (parity with libm itself unpinned).
+// the reference; atan2 / acos of floats are the float overloads the reference
+// calls (atan2f / acosf), restated bit-exactly from glibc's fdlibm code in
+// mrt_libm.h.
 #pragma once
 #include <math.h>
 #include <stddef.h>
 #include <stdint.h>
 
+#include "mrt_libm.h"
 #include "mrt_math.h"
 
 namespace mrt {
@@ -94,12 +96,12 @@ MRT_HD float4 tex_lookup4(const float* d, int W, int H, int type, float u, float
 #endif
 
 // Texture::getLookupXYZ3 (src/Texture.cpp:80-98): direction -> (u, v).
-//   theta = atan2(z, x) + PI; phi = acos(y);
+//   theta = atan2(z, x) + PI; phi = acos(y);   (atan2f / acosf: fd_atan2f / fd_acosf)
 //   u = theta * 0.5 * _1_PI   (double arithmetic, rounded to float)
 //   v = 1.0 - phi * _1_PI     (float product, double subtraction)
 MRT_HD v3 tex_lookup_dir(const float* rgb, int W, int H, float x, float y, float z) {
-    const float theta = (float)atan2((double)z, (double)x) + kPI;
-    const float phi = (float)acos((double)y);
+    const float theta = fd_atan2f(z, x) + kPI;
+    const float phi = fd_acosf(y);
     const float u = (float)((double)theta * 0.5 * (double)kInvPI);
     const float v = (float)(1.0 - (double)(phi * kInvPI));
     return tex_lookup3(rgb, W, H, u, v);

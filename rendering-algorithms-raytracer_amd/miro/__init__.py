@@ -47,6 +47,17 @@ def rsqrt_nr(x: float) -> float:
     return float(lib().mrt_rsqrt_nr(float(x)))
 
 
+def debug_libm(fn: str, x, y=None):
+    """The device's acosf(x) ("acos") / atan2f(y, x) ("atan2") (numerics probe)."""
+    import numpy as np
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.ascontiguousarray(np.zeros_like(x) if y is None else y, np.float32)
+    out = np.empty_like(x)
+    _lib.check(lib().mrt_debug_libm({"acos": 0, "atan2": 1}[fn], x.ctypes.data, y.ctypes.data, len(x),
+                                    out.ctypes.data), "mrt_debug_libm")
+    return out
+
+
 class Vector3(tuple):
     """Plain 3-tuple with the reference's constructors: Vector3(s) or Vector3(x, y, z)."""
 

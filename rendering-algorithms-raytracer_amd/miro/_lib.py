@@ -21,7 +21,7 @@ EXPORTS = [
     "mrt_scene_build_bvh", "mrt_scene_bvh_info", "mrt_scene_bvh_export", "mrt_scene_bvh_import",
     "mrt_scene_upload", "mrt_render", "mrt_render_buckets_async", "mrt_unpack_buckets_async",
     "mrt_render_frame_async", "mrt_trace", "mrt_trace_async", "mrt_scene_last_stats", "mrt_rcp_nr",
-    "mrt_rsqrt_nr", "mrt_set_tuning", "mrt_render_batch_async", "mrt_unpack_batch_async",
+    "mrt_rsqrt_nr", "mrt_debug_libm", "mrt_set_tuning", "mrt_render_batch_async", "mrt_unpack_batch_async",
     "mrt_debug_wave_log", "mrt_device_wall_clock_khz", "mrt_hdr_info", "mrt_hdr_load", "mrt_scene_add_texture",
     "mrt_scene_set_env_map", "mrt_scene_set_material_env_map", "mrt_scene_dome_info", "mrt_scene_dome_export", "mrt_scene_make_blas",
     "mrt_scene_add_instance", "mrt_scene_blas_info", "mrt_scene_blas_export", "mrt_scene_set_material_emission",
@@ -198,6 +198,7 @@ def load():
     L.mrt_scene_add_instance.argtypes = [C.c_void_p, C.c_int32, _fp]
     L.mrt_scene_blas_info.argtypes = [C.c_void_p, C.c_int32, _ip, _ip, _ip]
     L.mrt_scene_blas_export.argtypes = [C.c_void_p, C.c_int32, _fp, _ip, _fp, _ip]
+    L.mrt_debug_libm.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
     L.mrt_rcp_nr.argtypes = [C.c_float]
     L.mrt_rcp_nr.restype = C.c_float
     L.mrt_rsqrt_nr.argtypes = [C.c_float]
