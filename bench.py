@@ -81,6 +81,10 @@ def parse():
                     help="--share model: assumed effective RCCL point-to-point rate per xGMI link and direction (GB/s)")
     ap.add_argument("--xgmi-lat-us", type=float, default=15.0, help="--share model: assumed per-gather latency (us)")
     ap.add_argument("--size", default="", help="WxH override of the config's frame size (exploration runs only)")
+    ap.add_argument("--frames-per-launch", type=int, default=1,
+                    help="strong split (N > 1, and --share): frames of the same camera each rank renders in ONE launch "
+                         "per step (its buckets of all of them dealt id mod N) and gathers at once; amortises the "
+                         "per-launch tail of a 1/N share (<= 16)")
     ap.add_argument("--latency-frames", type=int, default=5,
                     help="single frames (nothing else in flight) timed after the run for launch_ms / frame latency")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
@@ -380,7 +384,8 @@ def main():
     # secondary key of the split line.
     # (--path batch at N = 1 runs the split path on one GPU: same pipeline, N = 1)
     split = (world > 1 and args.split == "frame") or (world == 1 and args.path == "batch")
-    n_frames = 1 if (world == 1 or split) else (args.frames or min(world, 16))
+    fpl = max(1, min(16, args.frames_per_launch))
+    n_frames = (fpl if split else 1) if (world == 1 or split) else (args.frames or min(world, 16))
     bx, by = (W + 31) // 32, (H + 31) // 32
     bpf = bx * by
     use_frame_path = world == 1 and n_frames == 1 and args.path == "auto"
@@ -394,16 +399,18 @@ def main():
 
     depth = max(1, args.inflight)
 
-    def make_pipe(nf, float_tiles, nsplit=None, srank=None, pipe_streams=None, share_unpack="own"):
+    def make_pipe(nf, float_tiles, nsplit=None, srank=None, pipe_streams=None, share_unpack="own", same_camera=False):
         """This rank's share of an nf-frame step (items id mod N), its render /
         unpack closures and the gather pipeline over `depth` buffers and streams
         (--inflight).  nsplit / srank: the share of rank srank of an nsplit-way
         split rendered without the gather (bench.py --share); share_unpack "none":
         no unpack (a rank > 0 of the split only renders and sends), "full": rank 0's
-        unpack of all nsplit shares' tiles each step (its buffers hold nsplit shares)."""
+        unpack of all nsplit shares' tiles each step (its buffers hold nsplit shares).
+        same_camera: the nf frames are the headline camera's (strong split batched over
+        --frames-per-launch frames), not a camera path."""
         nsplit = world if nsplit is None else nsplit
         srank = rank if srank is None else srank
-        cams_ = [cam] if nf == 1 else [_camera(c) for c in scenes.camera_path(cfg["camera"], nf)]
+        cams_ = [cam] * nf if (nf == 1 or same_camera) else [_camera(c) for c in scenes.camera_path(cfg["camera"], nf)]
         cc = (_lib.mrt_camera * nf)(*[c._c() for c in cams_])
         mine, all_ids, per = tiles_mod.split_items(bpf * nf, nsplit, srank)
         shares = 1
@@ -563,12 +570,12 @@ def main():
         last = (nstep[0] - 1) % inflight
         frame_check = check_timed_frame(frame[last], frame8[last])
     else:
-        pipe, render, items, mine, _ = make_pipe(n_frames, float_tiles=split)
+        pipe, render, items, mine, _ = make_pipe(n_frames, float_tiles=split, same_camera=split)
         st, (shadow_total, eye_total, second_total) = count_rays(lambda: render(items, pipe.tiles[0], opts_count))
         elapsed = timed(pipe.step, pipe.flush, args.steps)
         last = (pipe.k - 1) % pipe.depth
         frame_check = check_timed_frame(pipe.out_f[last] if split else None, pipe.out_8[last]) \
-            if rank == 0 and n_frames == 1 else None
+            if rank == 0 and (n_frames == 1 or split) else None
     shadow_mine, eye_mine, second_mine = st["shadow_rays"], (st["primary_rays"] if adaptive else 0), st["secondary_rays"]
     primary_total = eye_total if adaptive else n_frames * W * H
     rays_per_step = primary_total + shadow_total + second_total      # all frames of the batch, all ranks
@@ -761,9 +768,12 @@ def main():
                    "qbvh_nodes": scene.bvh_info["nodes"], "qbvh_leaves": scene.bvh_info["leaves"],
                    "frames_in_flight": inflight,
                    "parallelism": "single GPU, whole frame" if use_frame_path else
-                   (f"one {W}x{H} frame per step split over {world} GPUs: its 32x32 buckets dealt id mod {world} "
-                    f"(src/Scene.cpp:90-174), float32 tiles, one RCCL gather of the framebuffer to rank 0 per frame, "
-                    f"consecutive frames double-buffered" if split else
+                   ((f"one {W}x{H} frame per step" if n_frames == 1 else
+                     f"{n_frames} {W}x{H} frames of one camera per step, rendered by each rank in ONE launch "
+                     f"(--frames-per-launch)") +
+                    f" split over {world} GPUs: its 32x32 buckets dealt id mod {world} "
+                    f"(src/Scene.cpp:90-174), float32 tiles, one RCCL gather of the framebuffer(s) to rank 0 per step, "
+                    f"consecutive steps double-buffered" if split else
                     f"{n_frames}-frame camera path per step, 32x32 buckets dealt id mod {world}, "
                     f"one RCCL gather of 8-bit tiles per step (double-buffered)")},
         # The traversal is bound by latency along each wave's dependent chain
@@ -878,7 +888,8 @@ def share_mode(args, E, widths):
     receives the N - 1 other shares over N - 1 point-to-point links at once, and the
     pipeline overlaps step k's gather with step k + 1's renders.  The xGMI rate and
     latency are ASSUMED (--xgmi-gbs, --xgmi-lat-us); nothing here ran on more than
-    one GPU."""
+    one GPU.  --frames-per-launch K: each share renders K frames of the camera in one
+    launch and gathers them at once (per-frame times reported)."""
     torch, np, C_ = E["torch"], E["np"], C
     scene, L, _lib, tiles_mod = E["scene"], E["L"], E["_lib"], E["tiles_mod"]
     W, H, bpf = E["W"], E["H"], E["bpf"]
@@ -901,21 +912,24 @@ def share_mode(args, E, widths):
            "shares": {}}
     # one set of streams for every share pipeline (libmrt keeps scratch per stream, at most 16 per scene)
     share_streams = [torch.cuda.Stream() for _ in range(max(1, args.inflight))]
+    K = max(1, min(16, args.frames_per_launch))   # frames per share launch (same camera)
+    out["config"]["frames_per_launch"] = K
     for N in widths:
         per_rank = []
         for r in range(N):
-            pipe, render, items, mine, _ = E["make_pipe"](1, True, nsplit=N, srank=r, pipe_streams=share_streams,
-                                                          share_unpack="full" if r == 0 else "none")
+            pipe, render, items, mine, _ = E["make_pipe"](K, True, nsplit=N, srank=r, pipe_streams=share_streams,
+                                                          share_unpack="full" if r == 0 else "none", same_camera=True)
             _, (sh, eye, sec) = E["count_rays"](lambda: render(items, pipe.tiles[0], E["opts_count"]))
-            px = sum(min(32, W - (b % ((W + 31) // 32)) * 32) * min(32, H - (b // ((W + 31) // 32)) * 32) for b in mine)
+            px = sum(min(32, W - (b % bpf % ((W + 31) // 32)) * 32) * min(32, H - (b % bpf // ((W + 31) // 32)) * 32)
+                     for b in mine)   # over the K frames of a launch
             e = E["timed"](pipe.step, pipe.flush, args.steps)
-            ms = e / args.steps * 1e3
+            ms = e / args.steps * 1e3 / K   # per frame
             # host issue time of the same steps (the Python loop alone, before the device drains)
             torch.cuda.synchronize()
             t_i = time.perf_counter()
             for _ in range(args.steps):
                 pipe.step()
-            issue_ms = (time.perf_counter() - t_i) / args.steps * 1e3
+            issue_ms = (time.perf_counter() - t_i) / args.steps * 1e3 / K
             pipe.flush()
             torch.cuda.synchronize()
             # one share launch alone (HIP events, nothing else in flight)
@@ -926,31 +940,31 @@ def share_mode(args, E, widths):
                 render(items, pipe.tiles[0])
                 e1.record()
                 torch.cuda.synchronize()
-                alone.append(e0.elapsed_time(e1))
+                alone.append(e0.elapsed_time(e1) / K)
             per_rank.append({"rank": r, "buckets": len(mine), "pixels": px, "ms_per_step": round(ms, 4),
                              "host_issue_ms_per_step": round(issue_ms, 4),
                              "launch_alone_ms": round(float(np.median(alone)), 4),
                              "rays": (eye if E["adaptive"] else px) + sh + sec})
             del pipe
         # rank 0's unpack of the whole gathered frame (N ranks' padded float tiles)
-        _, all_ids, per = tiles_mod.split_items(bpf, N, 0)
+        _, all_ids, per = tiles_mod.split_items(bpf * K, N, 0)
         ids = torch.tensor(all_ids, dtype=torch.int32, device="cuda")
         gathered = torch.zeros(len(all_ids) * 1024 * 3, dtype=torch.float32, device="cuda")
-        ff = torch.empty(W * H * 3, dtype=torch.float32, device="cuda")
-        f8 = torch.empty(W * H * 3, dtype=torch.uint8, device="cuda")
+        ff = torch.empty(K * W * H * 3, dtype=torch.float32, device="cuda")
+        f8 = torch.empty(K * W * H * 3, dtype=torch.uint8, device="cuda")
         un = []
         for _ in range(7):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(all_ids), gathered.data_ptr(), None, W, H, 1,
+            _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(all_ids), gathered.data_ptr(), None, W, H, K,
                                                 ff.data_ptr(), f8.data_ptr(), scene.handle,
                                                 torch.cuda.current_stream().cuda_stream), "unpack")
             e1.record()
             torch.cuda.synchronize()
             un.append(e0.elapsed_time(e1))
-        unpack_ms = float(np.median(un[2:]))
-        tile_bytes = per * 1024 * 3 * 4
-        gather_ms = args.xgmi_lat_us * 1e-3 + tile_bytes / (args.xgmi_gbs * 1e9) * 1e3
+        unpack_ms = float(np.median(un[2:])) / K   # per frame
+        tile_bytes = per * 1024 * 3 * 4                      # one gather: K frames' tiles
+        gather_ms = (args.xgmi_lat_us * 1e-3 + tile_bytes / (args.xgmi_gbs * 1e9) * 1e3) / K   # per frame
         slow = max(per_rank, key=lambda x: x["ms_per_step"])   # rank 0's line includes its full unpack
         step_ms = max(slow["ms_per_step"], gather_ms)
         out["shares"][str(N)] = {

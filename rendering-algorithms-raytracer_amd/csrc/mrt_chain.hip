@@ -699,17 +699,21 @@ __global__ void __launch_bounds__(64) chain_merge_kernel(RenderParams P) {
     if (!P.ch_est || i == 0 || i >= P.ch_levels) return;
     const uint32_t paths = chunk_units(P) * (uint32_t)P.num_paths;
     if (!paths) return;
-    bool known = true;   // no level above i overflowed
-    for (int k = 1; k < i; k++) known &= P.ch_cnt[k] <= lcap(P, k);
+    // a level below one that overflowed was not measured: it leaves the estimate as it
+    // is (unseen levels keep the worst-case size until a chunk measures them), so one
+    // fallback chunk never pins a level to the worst case for the scene's lifetime
+    for (int k = 1; k < i; k++)
+        if (P.ch_cnt[k] > lcap(P, k)) return;
     const uint64_t r = ((uint64_t)P.ch_cnt[i] * 65536u + paths - 1) / paths + 1;
-    atomicMax(P.ch_est + i, known ? (uint32_t)min<uint64_t>(r, 0xFFFFFFFEull) : 0xFFFFFFFFu);
+    atomicMax(P.ch_est + i, (uint32_t)min<uint64_t>(r, 0xFFFFFFFEull));
 }
 
 // The units of a chunk that outgrew a level's estimated capacity, rendered by the
 // fused chain shading (Shader::shade: every path's tree depth first, the same rays,
 // draws and adds as the engine -- tests/test_chain.py) from the units' eye-ray hits,
 // written as chain_finish writes them.  Nothing to do (one uniform load) otherwise.
-template <bool POINT_ONLY, bool INST, int REC>
+// COUNT: a count-mode frame, whose node / leaf visit statistics then include these units.
+template <bool POINT_ONLY, bool INST, int REC, bool COUNT>
 __global__ void __launch_bounds__(kWG) chain_fallback_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -740,7 +744,7 @@ __global__ void __launch_bounds__(kWG) chain_fallback_kernel(RenderParams P) {
             S.time = S.shadow_time = er.time;
             S.iorS = s_ior + tid;
             S.lvl = P.lvl + (blockIdx.x * kWG + tid);
-            col = S.template shade<false>(make_ray(er.o, er.d, er.time), h);
+            col = S.template shade<COUNT>(make_ray(er.o, er.d, er.time), h);
             shadow_total += S.shadow_rays;
             secondary_total += S.secondary;
         } else {
@@ -760,7 +764,7 @@ __global__ void __launch_bounds__(kWG) chain_fallback_kernel(RenderParams P) {
         }
     }
     flush_secondary(P, secondary_total, lane);
-    flush_stats<false>(P, st, shadow_total, lane, 0, 0);
+    flush_stats<COUNT>(P, st, shadow_total, lane, 0, 0);
 }
 
 // After adaptive pass n: per pixel of the pass, Scene::adaptiveSampleScene's
@@ -856,11 +860,15 @@ KernelFn pick_unit_eye(bool c, bool f, bool inst) {
 }
 KernelFn pick_chain_compact() { return chain_compact_kernel; }
 KernelFn pick_chain_merge() { return chain_merge_kernel; }
-KernelFn pick_chain_fallback(bool po, bool inst, int rec) {
-    if (rec == 2) return po ? (inst ? chain_fallback_kernel<true, true, 2> : chain_fallback_kernel<true, false, 2>)
-                            : (inst ? chain_fallback_kernel<false, true, 2> : chain_fallback_kernel<false, false, 2>);
-    return po ? (inst ? chain_fallback_kernel<true, true, 1> : chain_fallback_kernel<true, false, 1>)
-              : (inst ? chain_fallback_kernel<false, true, 1> : chain_fallback_kernel<false, false, 1>);
+template <bool C>
+static KernelFn chain_fallback_fn(bool po, bool inst, int rec) {
+    if (rec == 2) return po ? (inst ? chain_fallback_kernel<true, true, 2, C> : chain_fallback_kernel<true, false, 2, C>)
+                            : (inst ? chain_fallback_kernel<false, true, 2, C> : chain_fallback_kernel<false, false, 2, C>);
+    return po ? (inst ? chain_fallback_kernel<true, true, 1, C> : chain_fallback_kernel<true, false, 1, C>)
+              : (inst ? chain_fallback_kernel<false, true, 1, C> : chain_fallback_kernel<false, false, 1, C>);
+}
+KernelFn pick_chain_fallback(bool po, bool inst, int rec, bool count) {
+    return count ? chain_fallback_fn<true>(po, inst, rec) : chain_fallback_fn<false>(po, inst, rec);
 }
 KernelFn pick_chain_finish() { return chain_finish_kernel; }
 KernelFn pick_chain_fold() { return chain_fold_kernel; }

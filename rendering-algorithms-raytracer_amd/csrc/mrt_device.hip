@@ -408,6 +408,7 @@ struct DeviceState {
     size_t frame_px = 0;
     int grid = 0;                // upper bound of any launch (kMaxBlocksPerCU per CU)
     bool boxes_finite = false;
+    bool boxes_ordered = false;  // every used slot box has lo <= hi per axis (octant-ordered box test)
     float bb_lo[3] = {0, 0, 0}, bb_hi[3] = {0, 0, 0};   // world root box (ray-binning origin cells)
     int cus = 0;
     bool point_only = false;
@@ -440,7 +441,8 @@ static int g_batch_tpw = 2;       // bucket batches: tiles per wave the launch's
                                   // 2.98 -> 3.17x at N = 4, 4.69 -> 4.74x at N = 8; 4: 3.99x at N = 8
                                   // (profiles/r04_share_tpw_ab.txt)
 static int g_wave_log = 0;        // 1: timing-only wave log on uninstrumented launches (diagnostics)
-static int g_scalar_nodes = 3;    // scalar-cache fetch of wave-uniform nodes (bit 0) and triangles (bit 1)
+static int g_scalar_nodes = 7;    // scalar-cache fetch of wave-uniform nodes (bit 0) and triangles (bit 1); bit 2:
+                                  // octant-ordered box test for waves whose rays share an octant (box_test_oct)
 static int g_shade1 = 1;          // specialised shade kernel for one point light and one path
 static int g_wavefront = 1;       // general shading: gen / trace / resolve kernels instead of one fused kernel
 static int g_shadow_sched = -1;   // shadow_kernel schedule: 0 grid-stride, 1 XCD bands, 2 bands + lane refill,
@@ -846,8 +848,13 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     if (hipDeviceGetAttribute(&d.wall_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) d.wall_khz = 0;
     d.grid = d.cus * kMaxBlocksPerCU;
     d.boxes_finite = true;
-    for (const QNode& q : DN)
+    d.boxes_ordered = true;
+    for (const QNode& q : DN) {
         for (int k = 0; k < 24; k++) d.boxes_finite &= std::isfinite(q.box[k]);
+        for (int i = 0; i < 4; i++)
+            if (q.child[i] != kEmptySlot)
+                for (int a = 0; a < 3; a++) d.boxes_ordered &= q.box[a * 4 + i] <= q.box[12 + a * 4 + i];
+    }
     for (int a = 0; a < 3; a++) d.bb_lo[a] = d.bb_hi[a] = 0.f;
     if (!DN.empty()) {   // union of the root's used slot boxes (finite values only, per axis)
         bool any[3] = {false, false, false};
@@ -1315,7 +1322,7 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
     // fused (counted in the frame's statistics directly)
     void* margs[] = {&Q};
     HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(pick_chain_merge()), dim3(1), dim3(64), margs, 0, stream));
-    const KernelFn kfb = pick_chain_fallback(d.point_only, inst, d.recursive);
+    const KernelFn kfb = pick_chain_fallback(d.point_only, inst, d.recursive, count);
     unsigned long long* cc = Q.ctr;
     Q.ctr = Q.ctr_out;
     rc = go(kfb, std::min(full(kfb), ug));
@@ -1525,7 +1532,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     P.fast_box = fast_box(d);
     P.sched = g_sched;
     P.cus = d.cus;
-    P.scalar_nodes = g_scalar_nodes;
+    P.scalar_nodes = g_scalar_nodes & (d.boxes_ordered ? 7 : 3);
     P.near_first = g_near_first > 0 ? 1 : 0;
     c.chain_chunks = 0;
     c.chain_budget = 0;
@@ -2716,8 +2723,8 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "shade_waves") {
         if (value != 1 && (value < 4 || value > 8)) { set_error("shade_waves must be 1 or 4..8"); return MRT_ERR_INVALID; }
         g_shade_waves = value;
-    } else if (k == "scalar_nodes") {   // bit 0 nodes, bit 1 triangles (1 = round 3's nodes only)
-        if (value < 0 || value > 3) { set_error("scalar_nodes must be 0..3"); return MRT_ERR_INVALID; }
+    } else if (k == "scalar_nodes") {   // bit 0 nodes, bit 1 triangles (1 = round 3's nodes only), bit 2 octant box test
+        if (value < 0 || value > 7) { set_error("scalar_nodes must be 0..7"); return MRT_ERR_INVALID; }
         g_scalar_nodes = value;
     } else if (k == "batch_tpw") {
         if (value < 1 || value > 64) { set_error("batch_tpw must be 1..64"); return MRT_ERR_INVALID; }

@@ -61,7 +61,8 @@ struct DHit {
 struct Trav {
     const QNode* __restrict__ nodes;
     bool fast_box;            // all node boxes finite and fast box test enabled
-    int scalar_nodes;         // bit 0: scalar fetch of wave-uniform nodes, bit 1: of wave-uniform triangles (tuning)
+    int scalar_nodes;         // bit 0: scalar fetch of wave-uniform nodes, bit 1: of wave-uniform triangles,
+                              // bit 2: octant-ordered box test for waves whose rays share an octant (tuning)
     const DLeaf* __restrict__ leaves;
     const uint16_t* rcpT;     // LDS
     int32_t* lds;             // this lane's LDS stack column (stride kWG)
@@ -173,6 +174,53 @@ __device__ __forceinline__ int box_test_fast(const float4* bx, const DRay& r, fl
         m |= (int)(t0 <= t1) << i;
     }
     return m;
+}
+
+// box_test_fast for a ray whose direction signs are known at compile time (S bit k:
+// 1/d[k] < 0).  For 1/d >= 0 the rounded (lo - o) * (1/d) <= (hi - o) * (1/d) whenever
+// lo <= hi (rounding is monotone), so the slab minimum is the lo distance and the
+// maximum the hi one; for 1/d < 0 the other way round.  Every slot box of a built
+// hierarchy has lo <= hi on each axis (checked at upload: DeviceState::boxes_ordered),
+// and empty slots are masked by the caller, so the mask equals box_test_fast's with
+// half of its min / max work (the near / far planes are picked by register, not by
+// an instruction).
+template <int S>
+__device__ __forceinline__ int box_test_oct(const float4* bx, const DRay& r, float tMin, float tMax) {
+    const float4 nx = bx[(S & 1) ? 3 : 0], fx = bx[(S & 1) ? 0 : 3];
+    const float4 ny = bx[(S & 2) ? 4 : 1], fy = bx[(S & 2) ? 1 : 4];
+    const float4 nz = bx[(S & 4) ? 5 : 2], fz = bx[(S & 4) ? 2 : 5];
+    const float lx[4] = {nx.x, nx.y, nx.z, nx.w}, ly[4] = {ny.x, ny.y, ny.z, ny.w}, lz[4] = {nz.x, nz.y, nz.z, nz.w};
+    const float hx[4] = {fx.x, fx.y, fx.z, fx.w}, hy[4] = {fy.x, fy.y, fy.z, fy.w}, hz[4] = {fz.x, fz.y, fz.z, fz.w};
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float t0 = __builtin_fmaxf(__builtin_fmaxf((lx[i] - r.o[0]) * r.id[0], (ly[i] - r.o[1]) * r.id[1]),
+                                         __builtin_fmaxf((lz[i] - r.o[2]) * r.id[2], tMin));
+        const float t1 = __builtin_fminf(__builtin_fminf((hx[i] - r.o[0]) * r.id[0], (hy[i] - r.o[1]) * r.id[1]),
+                                         __builtin_fminf((hz[i] - r.o[2]) * r.id[2], tMax));
+        m |= (int)(t0 <= t1) << i;
+    }
+    return m;
+}
+// box_test_fast, or box_test_oct when the wave's rays share one octant (s < 8, wave-uniform)
+__device__ __forceinline__ int box_test_sel(const float4* bx, const DRay& r, float tMin, float tMax, int s) {
+    switch (s) {
+        case 0: return box_test_oct<0>(bx, r, tMin, tMax);
+        case 1: return box_test_oct<1>(bx, r, tMin, tMax);
+        case 2: return box_test_oct<2>(bx, r, tMin, tMax);
+        case 3: return box_test_oct<3>(bx, r, tMin, tMax);
+        case 4: return box_test_oct<4>(bx, r, tMin, tMax);
+        case 5: return box_test_oct<5>(bx, r, tMin, tMax);
+        case 6: return box_test_oct<6>(bx, r, tMin, tMax);
+        case 7: return box_test_oct<7>(bx, r, tMin, tMax);
+        default: return box_test_fast(bx, r, tMin, tMax);
+    }
+}
+// the wave-uniform octant of the active lanes' rays (1/d sign bits), or 8 when they differ
+__device__ __forceinline__ int wave_octant(const DRay& r) {
+    const int oct = (int)(r.id[0] < 0.f) | (int)(r.id[1] < 0.f) << 1 | (int)(r.id[2] < 0.f) << 2;
+    const int o0 = __builtin_amdgcn_readfirstlane(oct);
+    return __ballot(oct != o0) == 0 ? o0 : 8;
 }
 
 // box_test_fast that also returns each slot's entry distance (the slab max of
@@ -343,6 +391,9 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
     int sp = sp0;
     int32_t cur = root;
     bool hit = false;
+    // octant-ordered box tests (box_test_oct) when every active lane's ray has the same
+    // direction signs: most primary tiles and point-light shadow rays
+    const int soct = (FAST && !(ANY && c.near_first) && (c.scalar_nodes & 4)) ? wave_octant(r) : 8;
     while (true) {
         // stack top read at the start of the step: the LDS latency overlaps the
         // node fetch and box test (used only if this step pops)
@@ -365,7 +416,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
             float4 bx[6];
 #pragma unroll
             for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
-            m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_fast(bx, r, tMin, h.t);
+            m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_sel(bx, r, tMin, h.t, soct);
             // distinct markers end the two branches, so the compiler cannot sink their
             // identical box tests into one block fed by 24 v_mov copies of the SGPR node:
             // this branch reads the boxes straight from SGPRs
@@ -373,7 +424,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         } else {
             const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
             ch = reinterpret_cast<const int4*>(q)[6];
-            m = FAST ? ((ANY && c.near_first) ? box_test_fast_t(q, r, tMin, h.t, tn) : box_test_fast(q, r, tMin, h.t))
+            m = FAST ? ((ANY && c.near_first) ? box_test_fast_t(q, r, tMin, h.t, tn) : box_test_sel(q, r, tMin, h.t, soct))
                      : box_test(q, r, tMin, h.t);
             asm volatile("; mrt: vector node" : "+v"(m));
         }

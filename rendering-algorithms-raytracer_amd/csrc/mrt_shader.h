@@ -1549,7 +1549,7 @@ KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec);
 KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves, int step);
 KernelFn pick_chain_compact();
 KernelFn pick_chain_merge();
-KernelFn pick_chain_fallback(bool po, bool inst, int rec);
+KernelFn pick_chain_fallback(bool po, bool inst, int rec, bool count);
 KernelFn pick_chain_finish();
 KernelFn pick_chain_fold();
 KernelFn pick_unit_eye(bool c, bool f, bool inst);
