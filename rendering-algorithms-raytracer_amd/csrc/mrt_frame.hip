@@ -147,6 +147,18 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     flush_stats<COUNT, false>(P, st, shadow_total, lane, t0, ntiles);
 }
 
+// The kernel-argument block, re-read from the kernarg segment at this point: the
+// compiler can no longer keep its fields in SGPRs across the traversals (where it
+// ran out of SGPRs and spilled them to VGPR lanes); a few scalar-cache loads per
+// tile instead.
+// (The block is the kernel's only explicit argument: offset 0 of the kernarg segment.)
+__device__ __forceinline__ const RenderParams& reload_params() {
+    typedef const __attribute__((address_space(4))) RenderParams cparams;
+    cparams* p = (cparams*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const RenderParams*)p;
+}
+
 // Kernel 1+2 fused for one point light and num_paths == 1 (C1-C3): per pixel
 // the camera ray, its closest hit, then shade1_hit (the shadow ray any-hit) in
 // the same lane -- one persistent launch per frame, no hit-record hand-off
@@ -161,7 +173,7 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
     const uint16_t* rcpT = s_tab;
     const uint16_t* rsqT = P.tables + 2048;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave: an SGPR
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
@@ -171,9 +183,10 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     TileSched ts(P, wave, lane);
     uint32_t ntiles = 0;
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
-        if (P.wave_log && lane == 0 && ntiles < kLogTiles)
-        {
-            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
+        const RenderParams& PA = reload_params();   // camera, tile and diagnostics parameters
+        if (PA.wave_log && lane_id() == 0 && ntiles < kLogTiles) {
+            const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            unsigned long long* r = PA.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + w);
             r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
             r[4 + kLogTiles + ntiles] = ts.deq_ticks;
         }
@@ -181,20 +194,22 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
         int x, y;
         size_t slot;
         const uint32_t n0 = st.nodes, s0 = ss.nodes;
-        if (item_pixel(P, item, lane, x, y, slot)) {
-            const int f = item_frame(P, item);
-            const EyeRay er = camera_ray(P.cam[f], P.seed + (uint32_t)f, x, y, rsqT);
+        if (item_pixel(PA, item, lane_id(), x, y, slot)) {
+            const int f = item_frame(PA, item);
+            const EyeRay er = camera_ray(PA.cam[f], PA.seed + (uint32_t)f, x, y, rsqT);
             const DRay r = make_ray(er.o, er.d);
             DHit h{1e12f, 0.f, 0.f, -1};
             const bool hit = traverse<false, COUNT, FAST>(T, r, 0.001f, h, st);
-            v3 col = mk(P.bg[0], P.bg[1], P.bg[2]);
+            const RenderParams& PB = reload_params();   // shading parameters
+            v3 col = mk(PB.bg[0], PB.bg[1], PB.bg[2]);
             if (hit) {
                 nhits++;
-                col = shade1_hit<COUNT, FAST, POW>(P, T, ss, r, h.t, h.a, h.b, h.prim, rcpT, rsqT, shadow_total);
+                col = shade1_hit<COUNT, FAST, POW>(PB, T, ss, r, h.t, h.a, h.b, h.prim, rcpT, rsqT, shadow_total);
             }
-            item_pixel(P, item, lane, x, y, slot);   // recompute: keeps it out of the traversals' live set
-            if (P.hits) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
-            write_pixel(P, slot, col);
+            const RenderParams& PC = reload_params();   // outputs
+            item_pixel(PC, item, lane_id(), x, y, slot);   // recompute: keeps it out of the traversals' live set
+            if (PC.hits) PC.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
+            write_pixel(PC, slot, col);
         }
         if (COUNT) {
             uint32_t dmax = st.nodes - n0, smax = ss.nodes - s0;

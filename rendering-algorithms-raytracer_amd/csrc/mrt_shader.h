@@ -1036,11 +1036,15 @@ __device__ __forceinline__ uint8_t map8(const uint8_t* lut, float v) { return lu
 //   sched 3: dynamic, counter c hands out the contiguous band c (L2 locality per
 //            XCD) with the same stealing.
 // Counters are zeroed per launch; every wave sees -1 after at most 8 empty probes.
+// This lane's index in its wave (v_mbcnt): recomputed where it is used instead of
+// being held in a register across the traversals.
+__device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
 struct TileSched {
     const RenderParams& P;
-    int lane, mode, cur, step, end, home, probe, band;
+    int mode, cur, step, end, home, probe, band;
     uint32_t deq_ticks = 0;  // count mode: wall-clock ticks of the last dequeue
-    __device__ TileSched(const RenderParams& P_, int wave, int lane_) : P(P_), lane(lane_) {
+    __device__ TileSched(const RenderParams& P_, int wave, int) : P(P_) {
         mode = P.sched;
         home = blockIdx.x & 7;
         probe = 0;
@@ -1061,7 +1065,7 @@ struct TileSched {
     __device__ int dequeue() {
         int item = -1;
         const uint64_t q0 = P.wave_log ? wall_clock64() : 0;
-        if (lane == 0) {
+        if (lane_id() == 0) {
             while (probe < 8) {
                 const int c = (home + probe) & 7;
                 const unsigned v = atomicAdd(P.queue + c * 32, 1u);
