@@ -81,10 +81,11 @@ def parse():
                     help="--share model: assumed effective RCCL point-to-point rate per xGMI link and direction (GB/s)")
     ap.add_argument("--xgmi-lat-us", type=float, default=15.0, help="--share model: assumed per-gather latency (us)")
     ap.add_argument("--size", default="", help="WxH override of the config's frame size (exploration runs only)")
-    ap.add_argument("--frames-per-launch", type=int, default=1,
+    ap.add_argument("--frames-per-launch", type=int, default=0,
                     help="strong split (N > 1, and --share): frames of the same camera each rank renders in ONE launch "
                          "per step (its buckets of all of them dealt id mod N) and gathers at once; amortises the "
-                         "per-launch tail of a 1/N share (<= 16)")
+                         "per-launch tail of a 1/N share (1..16; 0 = 8: C3's 1/8 share 0.0912 -> 0.0599 ms per frame, "
+                         "profiles/r05_c3_share_model_k*.json)")
     ap.add_argument("--latency-frames", type=int, default=5,
                     help="single frames (nothing else in flight) timed after the run for launch_ms / frame latency")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
@@ -384,7 +385,7 @@ def main():
     # secondary key of the split line.
     # (--path batch at N = 1 runs the split path on one GPU: same pipeline, N = 1)
     split = (world > 1 and args.split == "frame") or (world == 1 and args.path == "batch")
-    fpl = max(1, min(16, args.frames_per_launch))
+    fpl = max(1, min(16, args.frames_per_launch or 8))
     n_frames = (fpl if split else 1) if (world == 1 or split) else (args.frames or min(world, 16))
     bx, by = (W + 31) // 32, (H + 31) // 32
     bpf = bx * by
@@ -912,7 +913,7 @@ def share_mode(args, E, widths):
            "shares": {}}
     # one set of streams for every share pipeline (libmrt keeps scratch per stream, at most 16 per scene)
     share_streams = [torch.cuda.Stream() for _ in range(max(1, args.inflight))]
-    K = max(1, min(16, args.frames_per_launch))   # frames per share launch (same camera)
+    K = max(1, min(16, args.frames_per_launch or 8))   # frames per share launch (same camera)
     out["config"]["frames_per_launch"] = K
     for N in widths:
         per_rank = []

@@ -198,7 +198,8 @@ def load():
     L.mrt_scene_add_instance.argtypes = [C.c_void_p, C.c_int32, _fp]
     L.mrt_scene_blas_info.argtypes = [C.c_void_p, C.c_int32, _ip, _ip, _ip]
     L.mrt_scene_blas_export.argtypes = [C.c_void_p, C.c_int32, _fp, _ip, _fp, _ip]
-    L.mrt_debug_libm.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+    if hasattr(L, "mrt_debug_libm"):   # (absent from round-4 builds loaded for A/B runs via MRT_LIB)
+        L.mrt_debug_libm.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
     L.mrt_rcp_nr.argtypes = [C.c_float]
     L.mrt_rcp_nr.restype = C.c_float
     L.mrt_rsqrt_nr.argtypes = [C.c_float]
