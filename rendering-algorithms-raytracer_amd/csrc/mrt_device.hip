@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
         const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
         DHit h{o.w, 0.f, 0.f, -1};
         const uint32_t n0 = st.nodes;
-        P.occl[e] = traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st) ? 1 : 0;
+        P.occl[e] = traverse<true, COUNT, FAST, INST, CHECK>(T, r, 0.001f, h, st) ? 1 : 0;
         return st.nodes - n0;
     };
     // per-XCD band of ray slots and its chunk counter (own 128-B line)
@@ -729,6 +729,7 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     append(s.nodes, s.leaves, &s.obj_inst, nullptr);
     std::vector<int32_t> blas_root(s.blas.size());
     for (size_t b = 0; b < s.blas.size(); b++) blas_root[b] = append(s.blas[b].nodes, s.blas[b].leaves, nullptr, &s.blas[b]);
+    for (QNode& q : DN) q.pad[0] = slot_kinds(q.child);   // the walks read the slot kinds (node_kinds)
     if ((rc = upload(d.nodes, DN.data(), DN.size() * sizeof(QNode), total))) return rc;
     std::vector<DevInstance> DI(s.instances.size());
     for (size_t i = 0; i < DI.size(); i++) {
@@ -1086,12 +1087,23 @@ static int blocks_per_cu(KernelFn f, size_t lds) {
     return n;
 }
 
-template <int W, bool I = false>
+template <int W, bool I = false, bool CHK = true>
 static KernelFn primary_fn(bool c, bool f) {
-    return c ? (f ? primary_kernel<true, W, true, I> : primary_kernel<true, W, false, I>)
-             : (f ? primary_kernel<false, W, true, I> : primary_kernel<false, W, false, I>);
+    return c ? (f ? primary_kernel<true, W, true, I, CHK> : primary_kernel<true, W, false, I, CHK>)
+             : (f ? primary_kernel<false, W, true, I, CHK> : primary_kernel<false, W, false, I, CHK>);
 }
-static KernelFn pick_primary(int w, bool c, bool f, bool inst) {
+// check: the special-leaf scene has alpha-mapped or motion-blurred lanes; scenes with
+// instances only take the variants without those tests (no noinline calls: C5's nested
+// instance walk at 5 waves spills 28 B instead of 256 B per lane)
+static KernelFn pick_primary(int w, bool c, bool f, bool inst, bool check = true) {
+    if (inst && !check) {
+        switch (g_primary_inst_waves) {
+            case 4: return primary_fn<4, true, false>(c, f);
+            case 6: return primary_fn<6, true, false>(c, f);
+            case 1: return primary_fn<1, true, false>(c, f);
+            default: return primary_fn<5, true, false>(c, f);
+        }
+    }
     if (inst) {   // special-leaf scenes (instances: nested BLAS walks)
         switch (g_primary_inst_waves) {
             case 4: return primary_fn<4, true>(c, f);   // 128 VGPRs: the nested instance walk without spills
@@ -1592,7 +1604,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         s.last = mrt_stats{};
         return MRT_OK;
     }
-    if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst)))) return rc;
+    if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst, d.has_alpha || d.has_mb)))) return rc;
     HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
     const int max_sh = max_shadow_rays(s);

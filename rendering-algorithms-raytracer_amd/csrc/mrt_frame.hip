@@ -147,18 +147,6 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
     flush_stats<COUNT, false>(P, st, shadow_total, lane, t0, ntiles);
 }
 
-// The kernel-argument block, re-read from the kernarg segment at this point: the
-// compiler can no longer keep its fields in SGPRs across the traversals (where it
-// ran out of SGPRs and spilled them to VGPR lanes); a few scalar-cache loads per
-// tile instead.
-// (The block is the kernel's only explicit argument: offset 0 of the kernarg segment.)
-__device__ __forceinline__ const RenderParams& reload_params() {
-    typedef const __attribute__((address_space(4))) RenderParams cparams;
-    cparams* p = (cparams*)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return *(const RenderParams*)p;
-}
-
 // Kernel 1+2 fused for one point light and num_paths == 1 (C1-C3): per pixel
 // the camera ray, its closest hit, then shade1_hit (the shadow ray any-hit) in
 // the same lane -- one persistent launch per frame, no hit-record hand-off
@@ -185,8 +173,7 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
         const RenderParams& PA = reload_params();   // camera, tile and diagnostics parameters
         if (PA.wave_log && lane_id() == 0 && ntiles < kLogTiles) {
-            const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-            unsigned long long* r = PA.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + w);
+            unsigned long long* r = PA.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
             r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
             r[4 + kLogTiles + ntiles] = ts.deq_ticks;
         }
@@ -224,15 +211,15 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     if (COUNT) {   // the shadow rays' node visits and wave steps (the latency model of bench.py)
         unsigned long long sv = ss.nodes;
         for (int off = 32; off > 0; off >>= 1) sv += __shfl_down(sv, off);
-        if (lane == 0) {
+        if (lane_id() == 0) {
             atomicAdd(&P.ctr[CTR_WAVE_STEPS_P], wave_steps);
             atomicAdd(&P.ctr[CTR_WAVE_STEPS_S], wave_steps_s);
             atomicAdd(&P.ctr[CTR_NODES_S], sv);
         }
     }
     // one wall-clock record per wave (the primary span counters; the wave log counts both kinds' nodes)
-    flush_stats<COUNT, true>(P, st, nhits, lane, t0, ntiles, ss.nodes);
-    flush_stats<COUNT, false, false>(P, ss, shadow_total, lane, t0, ntiles);
+    flush_stats<COUNT, true>(P, st, nhits, lane_id(), t0, ntiles, ss.nodes, wave);
+    flush_stats<COUNT, false, false>(P, ss, shadow_total, lane_id(), t0, ntiles, 0, wave);
 }
 
 template <int W, bool POW>

@@ -263,6 +263,24 @@ __host__ __device__ __forceinline__ int32_t leaf_child(uint32_t leaf, int count,
     return ~(int32_t)((leaf << 4) | (check ? 8u : 0u) | (proxy ? 4u : 0u) | (uint32_t)(count - 1));
 }
 
+// QNode::pad[0] of a device node: its slot kinds, set on upload from the child
+// words (mrt_device.hip, upload_scene): bits 0-3 inner child, 4-7 leaf packet,
+// 8-11 leaf packet with ProxyObject lanes.  One dword of the node's own line, read
+// instead of decoding the four child words in every step.
+__host__ __device__ __forceinline__ uint32_t slot_kinds(const int32_t child[4]) {
+    uint32_t k = 0;
+    for (int i = 0; i < 4; i++) {
+        const int32_t ch = child[i];
+        if (ch >= 0) k |= 1u << i;
+        else if (ch != kEmptySlot) k |= (1u << (4 + i)) | ((~(uint32_t)ch & 4u) ? 1u << (8 + i) : 0u);
+    }
+    return k;
+}
+__device__ __forceinline__ int node_kinds(const float4* q) { return reinterpret_cast<const int32_t*>(q)[28]; }
+__device__ __forceinline__ int kinds_inner(int k) { return k & 15; }
+__device__ __forceinline__ int kinds_leaf(int k) { return (k >> 4) & 15; }
+__device__ __forceinline__ int kinds_proxy(int k) { return (k >> 8) & 15; }
+
 // An MBObject lane of intersect4 (src/BVH.cpp:1316-1334): the triangle at the
 // ray's time, A = time * A2 + (1 - time) * A1 and the edges from the
 // interpolated B and C, then the lane's usual test.
@@ -352,20 +370,21 @@ __device__ __forceinline__ bool tri_test_lane(const Trav& c, uint32_t leaf, int 
     return ok != 0;
 }
 
-template <bool ANY, bool COUNT, bool FAST, bool INST = false, bool BL = false>
+template <bool ANY, bool COUNT, bool FAST, bool INST = false, bool BL = false, bool CHECK = true>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root = 0,
                               int sp0 = 0, int32_t aoff = 0);
 
 // One ProxyObject lane: its BLAS traversed with the object-space ray, the
 // current t as tMax, on the same stack above the caller's entries.
-template <bool ANY, bool COUNT, bool FAST>
+template <bool ANY, bool COUNT, bool FAST, bool CHECK = true>
 __device__ __forceinline__ bool proxy_hit(const Trav& c, int inst, const DRay& r, float tMin, DHit& h,
                                           TravStats& st, int sp) {
     const DevInstance& I = c.inst[inst];
     const DRay ro = object_ray(I, r, c.rcpT);
     // BLAS packets with alpha-mapped triangles (check bit): PrimShade = shade_base + BLAS object
-    if (FAST && ro.finite) return traverse_impl<ANY, COUNT, true, false, true>(c, ro, tMin, h, st, I.root, sp, I.shade_base);
-    return traverse_impl<ANY, COUNT, false, false, true>(c, ro, tMin, h, st, I.root, sp, I.shade_base);
+    if (FAST && ro.finite)
+        return traverse_impl<ANY, COUNT, true, false, true, CHECK>(c, ro, tMin, h, st, I.root, sp, I.shade_base);
+    return traverse_impl<ANY, COUNT, false, false, true, CHECK>(c, ro, tMin, h, st, I.root, sp, I.shade_base);
 }
 
 // BVH::intersect, QBVH branch (src/BVH.cpp:1128-1178).  Returns hit; h.prim is
@@ -385,7 +404,10 @@ __device__ __forceinline__ bool proxy_hit(const Trav& c, int inst, const DRay& r
 // a nested BLAS traversal (proxy_hit); root / sp0 start such a nested walk.
 // INST / BL (a BLAS walk): packets with the check bit (3) test alpha-mapped
 // lanes -- and, in the world, motion-blurred ones.
-template <bool ANY, bool COUNT, bool FAST, bool INST, bool BL>
+// CHECK = false: the scene has no alpha-mapped or motion-blurred lanes (no check bit
+// is set), so their tests -- calls of the noinline mb_tri_test / alpha_rejects, whose
+// call ABI costs the walk registers and scratch -- are compiled out.
+template <bool ANY, bool COUNT, bool FAST, bool INST, bool BL, bool CHECK>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root,
                               int sp0, int32_t aoff) {
     int sp = sp0;
@@ -398,7 +420,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         // stack top read at the start of the step: the LDS latency overlaps the
         // node fetch and box test (used only if this step pops)
         const int32_t peek = c.lds[(sp > 0 && sp <= kLdsStack ? sp - 1 : 0) * kWG];
-        int m;
+        int m, kinds;
         int4 ch;
         // Wave-uniform node (all active lanes on one node, ~70% of primary
         // steps): fetch it once through the scalar cache into SGPRs instead of
@@ -413,6 +435,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
             cfloat* q = (cfloat*)(const void*)(c.nodes + c0);
             cint* qc = (cint*)(q + 24);
             ch = make_int4(qc[0], qc[1], qc[2], qc[3]);
+            kinds = qc[4];
             float4 bx[6];
 #pragma unroll
             for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
@@ -424,6 +447,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         } else {
             const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
             ch = reinterpret_cast<const int4*>(q)[6];
+            kinds = node_kinds(q);
             m = FAST ? ((ANY && c.near_first) ? box_test_fast_t(q, r, tMin, h.t, tn) : box_test_sel(q, r, tMin, h.t, soct))
                      : box_test(q, r, tMin, h.t);
             asm volatile("; mrt: vector node" : "+v"(m));
@@ -432,11 +456,8 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
             st.nodes++;
             if (__ballot(cur != c0) == 0) st.uniform++;  // all active lanes of the wave on one node
         }
-        const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
-        const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
-                           (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
-        const int inner = m & isinner;
-        int lm = m & isleaf;
+        const int inner = m & kinds_inner(kinds);
+        int lm = m & kinds_leaf(kinds);
         bool have_next = false;
         int32_t nxt = 0;
         if (inner) {
@@ -474,14 +495,14 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                     leaf = v >> 4;
                     cnt = (int)(v & 3u) + 1;
                     k = 0;
-                    check = (INST || BL) && (v & 8u);
+                    check = CHECK && (INST || BL) && (v & 8u);
                     if (COUNT) st.leaves++;
                     if (INST && (v & 4u)) {
                         for (int j = 0; j < cnt; j++) {
                             const int32_t pm = c.leaves[leaf].prim[j];
                             if (pm > -2) continue;  // a triangle lane
                             DHit hi{h.t, 0.f, 0.f, -1};
-                            const bool ph = proxy_hit<ANY, COUNT, FAST>(c, -2 - pm, r, tMin, hi, st, sp);
+                            const bool ph = proxy_hit<ANY, COUNT, FAST, CHECK>(c, -2 - pm, r, tMin, hi, st, sp);
                             if (st.overflow) return hit;
                             if (ph) {
                                 if (ANY) return true;
@@ -493,7 +514,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                 }
                 float t, a, b;
                 bool ok;
-                if ((INST || BL) && check) {   // alpha-mapped / motion-blurred lanes
+                if (CHECK && (INST || BL) && check) {   // alpha-mapped / motion-blurred lanes
                     const int32_t pm = c.leaves[leaf].prim[k];
                     ok = (!BL && pm >= 0 && c.pflags && (c.pflags[pm] & 1u))
                              ? mb_tri_test(c, pm, r, tMin, h.t, t, a, b)
@@ -531,7 +552,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
 template <bool COUNT, bool FAST>
 __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float tMin, float tMax, int32_t& cur,
                                             int& sp, bool& hit, TravStats& st) {
-    int m;
+    int m, kinds;
     int4 ch;
     const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
     float tn[4] = {0.f, 0.f, 0.f, 0.f};
@@ -541,6 +562,7 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
         cfloat* q = (cfloat*)(const void*)(c.nodes + c0);
         cint* qc = (cint*)(q + 24);
         ch = make_int4(qc[0], qc[1], qc[2], qc[3]);
+        kinds = qc[4];
         float4 bx[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) bx[k] = make_float4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
@@ -549,16 +571,14 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
     } else {
         const float4* q = reinterpret_cast<const float4*>(c.nodes + cur);
         ch = reinterpret_cast<const int4*>(q)[6];
+        kinds = node_kinds(q);
         m = FAST ? (c.near_first ? box_test_fast_t(q, r, tMin, tMax, tn) : box_test_fast(q, r, tMin, tMax))
                  : box_test(q, r, tMin, tMax);
         asm volatile("; mrt: vector node" : "+v"(m));
     }
     if (COUNT) st.nodes++;
-    const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
-    const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
-                       (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
-    const int inner = m & isinner;
-    int lm = m & isleaf;
+    const int inner = m & kinds_inner(kinds);
+    int lm = m & kinds_leaf(kinds);
     bool have_next = false;
     int32_t nxt = 0;
     if (inner) {
@@ -648,22 +668,18 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
     const DRay& q = s.q;
     const float4* qn = reinterpret_cast<const float4*>(c.nodes + s.cur);
     const int4 ch = reinterpret_cast<const int4*>(qn)[6];
+    const int kinds = node_kinds(qn);
     float tn[4] = {0.f, 0.f, 0.f, 0.f};
     const bool fast = FAST && q.finite;
     const int m = fast ? (c.near_first ? box_test_fast_t(qn, q, tMin, tMax, tn) : box_test_fast(qn, q, tMin, tMax))
                        : box_test(qn, q, tMin, tMax);
     if (COUNT) st.nodes++;
-    const int isinner = (int)(ch.x >= 0) | (int)(ch.y >= 0) << 1 | (int)(ch.z >= 0) << 2 | (int)(ch.w >= 0) << 3;
-    const int isleaf = (int)(ch.x < 0 && ch.x != kEmptySlot) | (int)(ch.y < 0 && ch.y != kEmptySlot) << 1 |
-                       (int)(ch.z < 0 && ch.z != kEmptySlot) << 2 | (int)(ch.w < 0 && ch.w != kEmptySlot) << 3;
-    const int inner = m & isinner;
-    int lm = m & isleaf;
+    const int inner = m & kinds_inner(kinds);
+    int lm = m & kinds_leaf(kinds);
     // a hit leaf packet with proxy lanes: its instance walks run before the
     // descent (all hit inner children go onto the stack below them), so deferred
     // proxies never pile up along the path -- the stack stays near 4 per level
-    bool proxies = false;
-#pragma unroll
-    for (int i = 0; i < 4; i++) proxies |= ((lm >> i) & 1) && (~(uint32_t)sel4(ch, i) & 4u);
+    const bool proxies = (lm & kinds_proxy(kinds)) != 0;
     bool have_next = false;
     int32_t nxt = 0;
     if (inner) {
@@ -725,10 +741,10 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
 // whose origin and 1/d are finite; any other ray takes the exact loop.  A
 // closest hit's packed slot is resolved to the global prim id here.
 // An instance hit's id is the instance's hit_base + its BLAS object index.
-template <bool ANY, bool COUNT, bool FAST = false, bool INST = false>
+template <bool ANY, bool COUNT, bool FAST = false, bool INST = false, bool CHECK = true>
 __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
-    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST>(c, r, tMin, h, st)
-                                        : traverse_impl<ANY, COUNT, false, INST>(c, r, tMin, h, st);
+    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST, false, CHECK>(c, r, tMin, h, st)
+                                        : traverse_impl<ANY, COUNT, false, INST, false, CHECK>(c, r, tMin, h, st);
     if (!ANY && hit) {
         h.prim = c.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3];
         if (INST && h.inst >= 0) h.prim += c.inst[h.inst].hit_base;

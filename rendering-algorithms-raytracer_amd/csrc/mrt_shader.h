@@ -1036,6 +1036,18 @@ __device__ __forceinline__ uint8_t map8(const uint8_t* lut, float v) { return lu
 //   sched 3: dynamic, counter c hands out the contiguous band c (L2 locality per
 //            XCD) with the same stealing.
 // Counters are zeroed per launch; every wave sees -1 after at most 8 empty probes.
+// The kernel-argument block, re-read from the kernarg segment at this point: the
+// compiler can no longer keep its fields in SGPRs across the traversals (where it
+// ran out of SGPRs and spilled them to VGPR lanes); a few scalar-cache loads per
+// tile instead.
+// (The block is the kernel's only explicit argument: offset 0 of the kernarg segment.)
+__device__ __forceinline__ const RenderParams& reload_params() {
+    typedef const __attribute__((address_space(4))) RenderParams cparams;
+    cparams* p = (cparams*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const RenderParams*)p;
+}
+
 // This lane's index in its wave (v_mbcnt): recomputed where it is used instead of
 // being held in a register across the traversals.
 __device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -1128,11 +1140,12 @@ __device__ __forceinline__ void load_tables(const uint16_t* g, uint16_t* s, int 
 // node visits -- added to the wave log's node count.
 template <bool COUNT, bool PRIMARY = false, bool TIMES = true>
 __device__ __forceinline__ void flush_stats(const RenderParams& P, const TravStats& st, uint32_t shadow, int lane,
-                                            uint64_t t0, uint32_t tiles, uint32_t log_nodes = 0) {
+                                            uint64_t t0, uint32_t tiles, uint32_t log_nodes = 0, int wave = -1) {
     if (TIMES && (COUNT || P.wave_log) && lane == 0) {   // ramp / tail of the persistent waves
         const uint64_t t1 = wall_clock64();
         if (P.wave_log) {
-            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6));
+            const int w = wave >= 0 ? wave : (int)(threadIdx.x >> 6);   // (wave: the caller's scalar index)
+            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + w);
             r[0] = t0; r[1] = t1; r[2] = tiles;
         }
         unsigned long long* c = P.ctr + (PRIMARY ? CTR_TP : CTR_TS);
@@ -1156,7 +1169,8 @@ __device__ __forceinline__ void flush_stats(const RenderParams& P, const TravSta
             msp = max(msp, __shfl_down(msp, off));
         }
         if (lane == 0) {
-            if (TIMES && P.wave_log) P.wave_log[kLogWords * ((size_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6)) + 3] = nv + xv;
+            if (TIMES && P.wave_log)
+                P.wave_log[kLogWords * ((size_t)blockIdx.x * (kWG / 64) + (wave >= 0 ? wave : (int)(threadIdx.x >> 6))) + 3] = nv + xv;
             atomicAdd(&P.ctr[CTR_NODES], nv);
             atomicAdd(&P.ctr[CTR_LEAVES], lv);
             if (PRIMARY) {
@@ -1218,7 +1232,8 @@ __device__ __forceinline__ EyeRay camera_ray(const CamParams& cam, uint32_t seed
 
 // Kernel 1: Camera::eyeRayAdaptive + closest-hit BVH::intersect per pixel.
 // Writes the HitInfo record (t, a, b, prim) to P.hits[slot].
-template <bool COUNT, int MINW, bool FAST, bool INST = false>
+// CHECK: the special-leaf scene has alpha-mapped or motion-blurred lanes (false: instances only)
+template <bool COUNT, int MINW, bool FAST, bool INST = false, bool CHECK = true>
 __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -1226,7 +1241,9 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
     const uint16_t* rcpT = s_tab;           // per triangle test: LDS
     const uint16_t* rsqT = P.tables + 2048; // a few per pixel: global (L1-resident)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // (lane / wave indices and the tile's parameters are recomputed / re-read where
+    // used, so they hold no registers across the traversal: see frame1_kernel)
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
@@ -1236,9 +1253,9 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     TileSched ts(P, wave, lane);
     uint32_t ntiles = 0;
     for (int item = ts.first(); item >= 0; item = ts.next(item)) {
-        if (P.wave_log && lane == 0 && ntiles < kLogTiles)
-        {
-            unsigned long long* r = P.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
+        const RenderParams& PA = reload_params();
+        if (PA.wave_log && lane_id() == 0 && ntiles < kLogTiles) {
+            unsigned long long* r = PA.wave_log + kLogWords * ((size_t)blockIdx.x * (kWG / 64) + wave);
             r[4 + ntiles] = ((unsigned long long)item << 40) | (wall_clock64() & ((1ull << 40) - 1));
             r[4 + kLogTiles + ntiles] = ts.deq_ticks;
         }
@@ -1246,15 +1263,16 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
         int x, y;
         size_t slot;
         const uint32_t n0 = st.nodes;
-        if (item_pixel(P, item, lane, x, y, slot)) {
-            const int f = item_frame(P, item);
-            const CamParams& cam = P.cam[f];
-            const EyeRay er = camera_ray(cam, P.seed + (uint32_t)f, x, y, rsqT);
+        if (item_pixel(PA, item, lane_id(), x, y, slot)) {
+            const int f = item_frame(PA, item);
+            const CamParams& cam = PA.cam[f];
+            const EyeRay er = camera_ray(cam, PA.seed + (uint32_t)f, x, y, rsqT);
             DRay r = make_ray(er.o, er.d, er.time);
             DHit h{1e12f, 0.f, 0.f, -1};
-            if (!traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st)) h.prim = -1;
-            item_pixel(P, item, lane, x, y, slot);  // recompute: keeps it out of the traversal's live set
-            P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(h.prim));
+            if (!traverse<false, COUNT, FAST, INST, CHECK>(T, r, 0.001f, h, st)) h.prim = -1;
+            const RenderParams& PC = reload_params();
+            item_pixel(PC, item, lane_id(), x, y, slot);  // recompute: keeps it out of the traversal's live set
+            PC.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(h.prim));
             nhits += h.prim >= 0 ? 1u : 0u;  // wave-reduced in flush_stats
         }
         if (COUNT) {

@@ -7,7 +7,8 @@ namespace mrt {
 // 4-wide node, one 128-B line.  SoA boxes exactly as QBVH_Node
 // (reference src/BVH.h:83-109): minX[4] minY[4] minZ[4] maxX[4] maxY[4] maxZ[4].
 // child[i] >= 0: inner node index; child[i] == INT32_MIN: empty slot;
-// otherwise ~child[i] is a leaf-packet index.
+// otherwise ~child[i] is a leaf-packet index.  The device copy keeps its slot kinds
+// in pad[0] (slot_kinds, mrt_kernels.h).
 struct alignas(16) QNode {
     float box[24];
     int32_t child[4];
