@@ -397,6 +397,10 @@ int mrt_trace(mrt_scene* s, const float* o, const float* d, const float* tmin, c
 int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const float* d_tmin,
                     const float* d_tmax, size_t n, int any_hit, mrt_hit* d_out, void* stream);
 
+/* The walk of the scene's last one-light frame on its current device: *lds_nodes = 1
+ * when it ran the LDS top-node walk (tuning "lds_nodes"), 0 when not, -1 before any. */
+int mrt_scene_walk_info(const mrt_scene* s, int32_t* lds_nodes);
+
 /* Counters of the last render on this scene (ray counts, visits, kernel time). */
 int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
 
@@ -407,7 +411,9 @@ int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
  * holds), "primary_waves" 0/6/[7]/8 (occupancy target of the primary-ray kernel),
  * "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands, dynamic
  * interleaved, dynamic banded; see TileSched), "shade1" 0/[1] (specialised shading
- * kernel for one point light and one path), "fused" 0/[1] (one-launch frame kernel
+ * kernel for one point light and one path), "lds_nodes" [-1]..1 (the frame kernel's
+ * LDS top-node walk: [0] off, 1 on; C2 -4%, C3 +9% with 4 frames in flight), "scalar_nodes" 0..[7] (bit 0 scalar fetch of wave-uniform nodes, bit 1 of
+ * wave-uniform triangles, bit 2 octant-ordered box test), "fused" 0/[1] (one-launch frame kernel
  * for one point light), "bin" [-1] / 0..7 (ray binning before tracing: bit 0 the
  * wavefront shadow pass, bit 1 the chain levels' closest-hit entries, bit 2 their
  * shadow rays; -1 auto), "bin_dbits" 0..6 [2] / "bin_obits" 0..4 [2] (binning key:

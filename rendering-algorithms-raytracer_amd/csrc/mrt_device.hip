@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cmath>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -409,6 +410,8 @@ struct DeviceState {
     int grid = 0;                // upper bound of any launch (kMaxBlocksPerCU per CU)
     bool boxes_finite = false;
     bool boxes_ordered = false;  // every used slot box has lo <= hi per axis (octant-ordered box test)
+    bool lds_ok = false;         // the world hierarchy has kLdsNodes nodes for the LDS top-node walk (renumbered)
+    std::atomic<int> lds_pick{-1};   // the last one-light frame ran the LDS top-node walk: 1 yes, 0 no, -1 none yet
     float bb_lo[3] = {0, 0, 0}, bb_hi[3] = {0, 0, 0};   // world root box (ray-binning origin cells)
     int cus = 0;
     bool point_only = false;
@@ -470,6 +473,9 @@ static int g_chain_mb = 8192;     // chain scratch per stream (MB), at most 80% 
                                   // 48 GB and R3 / P4 / FS nothing (profiles/r04_chain_mb_est_ab.txt)
 static int g_chain_adapt = 1;     // adaptive supersampling of REC scenes: passes over the chain engine (0: fused kernel)
 static int g_fused = 1;           // one point light, one path: frame1_kernel (primary + shading in one launch)
+static int g_lds_nodes = 0;       // frame1_kernel's LDS top-node walk (LN), 0 off / 1 on: with 4 frames in flight C2
+                                  // -4.1%, C3 +9%, C3L +11% (profiles/r05_lds_nodes_ab_*.txt); no probe separated them
+                                  // reliably (single-frame kernel times are equal on C2), so it is off unless asked for
 static int g_frame1_waves = 7;    // frame1_kernel launch-bounds occupancy target: 1 (none), 5..8 (7: -0.9% per frame with
                                   // 4 frames in flight, +0.8% single-frame latency; profiles/r03_c3_scalar_waves_ab.txt)
 static int g_bin = -1;            // ray binning (mrt_bin.h) before tracing: bit 0 the wavefront shadow pass (kernel 2b),
@@ -729,6 +735,39 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     append(s.nodes, s.leaves, &s.obj_inst, nullptr);
     std::vector<int32_t> blas_root(s.blas.size());
     for (size_t b = 0; b < s.blas.size(); b++) blas_root[b] = append(s.blas[b].nodes, s.blas[b].leaves, nullptr, &s.blas[b]);
+    // The world hierarchy's first kLdsNodes nodes in breadth-first order get device
+    // numbers 0 .. kLdsNodes - 1 (frame1_kernel<LN> stages them in LDS).  Device node
+    // numbers are internal: the visit order follows the child slots, not the numbers.
+    const size_t nw = s.nodes.size();
+    d.lds_ok = nw >= (size_t)kLdsNodes;
+    if (d.lds_ok) {
+        // (an imported hierarchy may share a node between parents: each is numbered once)
+        std::vector<int32_t> bfs{0};
+        std::vector<int32_t> perm(DN.size(), -1);
+        perm[0] = 0;
+        for (size_t q = 0; q < bfs.size() && bfs.size() < (size_t)kLdsNodes; q++)
+            for (int k = 0; k < 4 && bfs.size() < (size_t)kLdsNodes; k++) {
+                const int32_t ch = DN[(size_t)bfs[q]].child[k];
+                if (ch >= 0 && (size_t)ch < nw && perm[(size_t)ch] < 0) {
+                    perm[(size_t)ch] = (int32_t)bfs.size();
+                    bfs.push_back(ch);
+                }
+            }
+        d.lds_ok = bfs.size() == (size_t)kLdsNodes;
+        int32_t next = (int32_t)bfs.size();
+        for (size_t i = 0; i < nw; i++)
+            if (perm[i] < 0) perm[i] = next++;
+        for (size_t i = nw; i < DN.size(); i++) perm[i] = (int32_t)i;
+        std::vector<QNode> R(DN.size());
+        for (size_t i = 0; i < DN.size(); i++) {
+            QNode q = DN[i];
+            for (int k = 0; k < 4; k++)
+                if (q.child[k] >= 0) q.child[k] = perm[(size_t)q.child[k]];
+            R[(size_t)perm[i]] = q;
+        }
+        DN.swap(R);
+        for (int32_t& br : blas_root) br = perm[(size_t)br];
+    }
     for (QNode& q : DN) q.pad[0] = slot_kinds(q.child);   // the walks read the slot kinds (node_kinds)
     if ((rc = upload(d.nodes, DN.data(), DN.size() * sizeof(QNode), total))) return rc;
     std::vector<DevInstance> DI(s.instances.size());
@@ -1595,7 +1634,10 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
     c.fused = one && g_fused;
     if (c.fused) {   // one launch: camera rays, closest hits, shading, shadow rays
         if (!want_hits) P.hits = nullptr;
-        if ((rc = launch(pick_frame1(g_frame1_waves, count, fb, d.pow_spec)))) return rc;
+        // LDS top-node walk (tuning "lds_nodes"; both walks give the same bits)
+        const bool ln = fb && d.lds_ok && g_lds_nodes > 0;
+        d.lds_pick = ln ? 1 : 0;
+        if ((rc = launch(pick_frame1(g_frame1_waves, count, fb, d.pow_spec, ln)))) return rc;
         HIP_OK(hipEventRecord(c.evm, stream));
         c.last_was_render = true;
         HIP_OK(hipGetLastError());
@@ -2581,6 +2623,14 @@ int mrt_render(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
     return MRT_OK;
 }
 
+int mrt_scene_walk_info(const mrt_scene* cs, int32_t* lds_nodes) {
+    if (!cs) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    const Scene& S = cs->impl;
+    const DeviceState* d = S.dev;
+    if (lds_nodes) *lds_nodes = d ? (int32_t)d->lds_pick.load() : -1;
+    return MRT_OK;
+}
+
 int mrt_scene_last_stats(const mrt_scene* cs, mrt_stats* out) {
     if (!cs || !out) { set_error("bad argument"); return MRT_ERR_INVALID; }
     mrt_scene* s = const_cast<mrt_scene*>(cs);
@@ -2814,6 +2864,9 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "bin_obits") {
         if (value < 0 || value > 4) { set_error("bin_obits must be 0..4"); return MRT_ERR_INVALID; }
         g_bin_obits = value;
+    } else if (k == "lds_nodes") {
+        if (value < 0 || value > 1) { set_error("lds_nodes must be 0 or 1"); return MRT_ERR_INVALID; }
+        g_lds_nodes = value;
     } else if (k == "frame1_waves") {
         if (value != 1 && (value < 5 || value > 8)) { set_error("frame1_waves must be 1 or 5..8"); return MRT_ERR_INVALID; }
         g_frame1_waves = value;

@@ -17,7 +17,7 @@ namespace mrt {
 // POW: some Blinn material has specExp != 1 (Blinn::shade's pow, src/Blinn.cpp:220).  Scenes
 // without one run the POW = false kernels, which carry no double-precision pow: its
 // polynomial constants, hoisted out of the tile loop, took VGPRs and scratch.
-template <bool COUNT, bool FAST, bool POW>
+template <bool COUNT, bool FAST, bool POW, bool LN = false>
 __device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, TravStats& st, const DRay& r, float ht,
                                          float ha, float hb, int prim, const uint16_t* rcpT, const uint16_t* rsqT,
                                          uint32_t& shadow_total) {
@@ -68,7 +68,7 @@ __device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, T
             const DRay sr = make_ray(from, L);
             DHit sh{distance, 0.f, 0.f, -1};
             shadow_total++;
-            if (traverse<true, COUNT, FAST>(T, sr, 0.001f, sh, st)) attenuate = 0.0f;
+            if (traverse<true, COUNT, FAST, false, true, LN>(T, sr, 0.001f, sh, st)) attenuate = 0.0f;
         }
         attenuate *= nDotL;
         spec = rdl * attenuate;
@@ -153,11 +153,18 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
 // (the record is written only when the caller asks for hits, P.hits != null),
 // one launch tail instead of two.  Every ray's visits and every operation are
 // those of primary_kernel + shade1_kernel, so the frame is bit-identical.
-template <bool COUNT, bool FAST, int MINW, bool POW>
+// LN: the hierarchy's top kLdsNodes nodes are staged in LDS (+8 KB per workgroup)
+// and both walks read their wave-uniform visits from there (traverse_impl); the
+// host runs it where a probe measured it faster (launch_render, lds_nodes).
+template <bool COUNT, bool FAST, int MINW, bool POW, bool LN = false>
 __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
-    load_tables(P.tables, s_tab, 1024);
+    __shared__ QNode s_top[LN ? kLdsNodes : 1];
+    if (LN)   // (the host runs LN only on hierarchies of at least kLdsNodes nodes)
+        for (int i = threadIdx.x; i < kLdsNodes * 32; i += kWG)
+            reinterpret_cast<uint32_t*>(s_top)[i] = reinterpret_cast<const uint32_t*>(P.nodes)[i];
+    load_tables(P.tables, s_tab, 1024);   // (its barrier also covers s_top)
     const uint64_t t0 = (COUNT || P.wave_log) ? wall_clock64() : 0;
     const uint16_t* rcpT = s_tab;
     const uint16_t* rsqT = P.tables + 2048;
@@ -165,6 +172,7 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     Trav T{P.nodes, P.fast_box != 0, P.scalar_nodes, P.leaves, rcpT, s_stack + tid, P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
+    if (LN) T.lnodes = s_top;
     TravStats st, ss;   // primary / shadow rays (count mode)
     uint32_t nhits = 0, shadow_total = 0;
     unsigned long long wave_steps = 0, wave_steps_s = 0;   // count mode: per tile, the max node steps over lanes
@@ -186,12 +194,12 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
             const EyeRay er = camera_ray(PA.cam[f], PA.seed + (uint32_t)f, x, y, rsqT);
             const DRay r = make_ray(er.o, er.d);
             DHit h{1e12f, 0.f, 0.f, -1};
-            const bool hit = traverse<false, COUNT, FAST>(T, r, 0.001f, h, st);
+            const bool hit = traverse<false, COUNT, FAST, false, true, LN>(T, r, 0.001f, h, st);
             const RenderParams& PB = reload_params();   // shading parameters
             v3 col = mk(PB.bg[0], PB.bg[1], PB.bg[2]);
             if (hit) {
                 nhits++;
-                col = shade1_hit<COUNT, FAST, POW>(PB, T, ss, r, h.t, h.a, h.b, h.prim, rcpT, rsqT, shadow_total);
+                col = shade1_hit<COUNT, FAST, POW, LN>(PB, T, ss, r, h.t, h.a, h.b, h.prim, rcpT, rsqT, shadow_total);
             }
             const RenderParams& PC = reload_params();   // outputs
             item_pixel(PC, item, lane_id(), x, y, slot);   // recompute: keeps it out of the traversals' live set
@@ -227,21 +235,26 @@ static KernelFn shade1_fn(bool c, bool f) {
     return c ? (f ? shade1_kernel<true, true, W, POW> : shade1_kernel<true, false, W, POW>)
              : (f ? shade1_kernel<false, true, W, POW> : shade1_kernel<false, false, W, POW>);
 }
-template <int W, bool POW>
+template <int W, bool POW, bool LN>
 static KernelFn frame1_fn(bool c, bool f) {
-    return c ? (f ? frame1_kernel<true, true, W, POW> : frame1_kernel<true, false, W, POW>)
-             : (f ? frame1_kernel<false, true, W, POW> : frame1_kernel<false, false, W, POW>);
+    return c ? (f ? frame1_kernel<true, true, W, POW, LN> : frame1_kernel<true, false, W, POW, LN>)
+             : (f ? frame1_kernel<false, true, W, POW, LN> : frame1_kernel<false, false, W, POW, LN>);
 }
-// pow: a Blinn material with specExp != 1 (those scenes run at 6 waves, or unbounded)
-KernelFn pick_frame1(int w, bool c, bool f, bool pow) {
-    if (pow) return w == 1 ? frame1_fn<1, true>(c, f) : frame1_fn<6, true>(c, f);
+template <bool LN>
+static KernelFn pick_frame1_ln(int w, bool c, bool f, bool pow) {
+    if (pow) return w == 1 ? frame1_fn<1, true, LN>(c, f) : frame1_fn<6, true, LN>(c, f);
     switch (w) {
-        case 1: return frame1_fn<1, false>(c, f);
-        case 5: return frame1_fn<5, false>(c, f);
-        case 7: return frame1_fn<7, false>(c, f);
-        case 8: return frame1_fn<8, false>(c, f);
-        default: return frame1_fn<6, false>(c, f);
+        case 1: return frame1_fn<1, false, LN>(c, f);
+        case 5: return frame1_fn<5, false, LN>(c, f);
+        case 7: return frame1_fn<7, false, LN>(c, f);
+        case 8: return frame1_fn<8, false, LN>(c, f);
+        default: return frame1_fn<6, false, LN>(c, f);
     }
+}
+// pow: a Blinn material with specExp != 1 (those scenes run at 6 waves, or unbounded);
+// ln: the LDS top-node walk
+KernelFn pick_frame1(int w, bool c, bool f, bool pow, bool ln) {
+    return ln ? pick_frame1_ln<true>(w, c, f, pow) : pick_frame1_ln<false>(w, c, f, pow);
 }
 KernelFn pick_shade1(int w, bool c, bool f, bool pow) {
     if (pow) return w == 1 ? shade1_fn<1, true>(c, f) : shade1_fn<5, true>(c, f);

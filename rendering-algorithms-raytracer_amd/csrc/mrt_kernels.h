@@ -23,6 +23,7 @@ static constexpr int kWG = 256;          // threads per workgroup (4 waves)
 static constexpr int kLdsStack = 16;     // stack entries per lane kept in LDS (max seen: 11)
 static constexpr int kGlobalStack = 240; // spill entries per thread in HBM: 256 in all, the reference's stack (src/BVH.cpp:1133)
 static constexpr int kTableWords = 4096; // rcp[2048] + rsqrt[2048] (u16)
+static constexpr int kLdsNodes = 64;     // LN walks: the world hierarchy's first 64 nodes (breadth first) staged in LDS
 
 struct DRay {
     float o[3], d[3], id[3];
@@ -83,6 +84,7 @@ struct Trav {
     const float4* verts = nullptr;
     const float4* verts2 = nullptr;
     bool near_first = false;   // any-hit walks descend into the nearest hit child first (order-free answer)
+    const QNode* lnodes = nullptr;   // LN walks: nodes 0 .. kLdsNodes - 1 (the hierarchy's top levels) in LDS
 };
 
 struct TravStats {
@@ -370,7 +372,7 @@ __device__ __forceinline__ bool tri_test_lane(const Trav& c, uint32_t leaf, int 
     return ok != 0;
 }
 
-template <bool ANY, bool COUNT, bool FAST, bool INST = false, bool BL = false, bool CHECK = true>
+template <bool ANY, bool COUNT, bool FAST, bool INST = false, bool BL = false, bool CHECK = true, bool LN = false>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root = 0,
                               int sp0 = 0, int32_t aoff = 0);
 
@@ -407,7 +409,11 @@ __device__ __forceinline__ bool proxy_hit(const Trav& c, int inst, const DRay& r
 // CHECK = false: the scene has no alpha-mapped or motion-blurred lanes (no check bit
 // is set), so their tests -- calls of the noinline mb_tri_test / alpha_rejects, whose
 // call ABI costs the walk registers and scratch -- are compiled out.
-template <bool ANY, bool COUNT, bool FAST, bool INST, bool BL, bool CHECK>
+// LN: wave-uniform visits of the hierarchy's top nodes (index < kLdsNodes, renumbered
+// breadth first on upload) read them from LDS (c.lnodes, one broadcast address)
+// instead of the scalar cache -- faster where the top levels end most rays (the
+// walk is per scene, chosen by a probe: mrt_device.hip, lds_nodes).
+template <bool ANY, bool COUNT, bool FAST, bool INST, bool BL, bool CHECK, bool LN>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root,
                               int sp0, int32_t aoff) {
     int sp = sp0;
@@ -427,7 +433,16 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
         // 64 copies through the vector memory path.
         const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
         float tn[4] = {0.f, 0.f, 0.f, 0.f};   // slot entry distances (any-hit near-first order)
-        if (FAST && (c.scalar_nodes & 1) && __ballot(cur != c0) == 0) {
+        if (LN && FAST && c0 < kLdsNodes && __ballot(cur != c0) == 0) {
+            const QNode& nd = c.lnodes[c0];   // one wave-uniform LDS address: broadcast reads
+            ch = make_int4(nd.child[0], nd.child[1], nd.child[2], nd.child[3]);
+            kinds = (int)nd.pad[0];
+            float4 bx[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) bx[k] = make_float4(nd.box[4 * k], nd.box[4 * k + 1], nd.box[4 * k + 2], nd.box[4 * k + 3]);
+            m = (ANY && c.near_first) ? box_test_fast_t(bx, r, tMin, h.t, tn) : box_test_sel(bx, r, tMin, h.t, soct);
+            asm volatile("; mrt: lds node" : "+v"(m));
+        } else if (FAST && (c.scalar_nodes & 1) && __ballot(cur != c0) == 0) {
             // constant address space + uniform address -> s_load_dwordx16 (node
             // data is read-only for the whole launch)
             typedef const __attribute__((address_space(4))) float cfloat;
@@ -741,9 +756,9 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
 // whose origin and 1/d are finite; any other ray takes the exact loop.  A
 // closest hit's packed slot is resolved to the global prim id here.
 // An instance hit's id is the instance's hit_base + its BLAS object index.
-template <bool ANY, bool COUNT, bool FAST = false, bool INST = false, bool CHECK = true>
+template <bool ANY, bool COUNT, bool FAST = false, bool INST = false, bool CHECK = true, bool LN = false>
 __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
-    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST, false, CHECK>(c, r, tMin, h, st)
+    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST, false, CHECK, LN>(c, r, tMin, h, st)
                                         : traverse_impl<ANY, COUNT, false, INST, false, CHECK>(c, r, tMin, h, st);
     if (!ANY && hit) {
         h.prim = c.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3];

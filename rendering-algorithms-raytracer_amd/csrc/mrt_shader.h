@@ -1559,7 +1559,7 @@ struct ShadeK { static constexpr KernelFn fn = shade_kernel<C, PO, F, I, kFused,
 
 // defined in mrt_frame.hip: the one-point-light frame / shade kernels at an
 // occupancy target w; pow: a Blinn material with specExp != 1
-KernelFn pick_frame1(int w, bool c, bool f, bool pow);
+KernelFn pick_frame1(int w, bool c, bool f, bool pow, bool ln);
 KernelFn pick_shade1(int w, bool c, bool f, bool pow);
 // defined in mrt_rec.hip: the fused chain kernels (rec 1: reflection / refraction,
 // 2: + path tracing) and the adaptive supersampling kernels (any rec)

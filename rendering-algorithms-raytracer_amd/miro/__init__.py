@@ -704,6 +704,13 @@ class Scene:
         self.last_stats = self.stats()
         return hits
 
+    def walk_info(self):
+        """The walk of this scene's last one-light frame: {"lds_nodes": 1 (LDS top-node walk),
+        0 (plain), -1 (none yet)}."""
+        ln = C.c_int32()
+        check(lib().mrt_scene_walk_info(self.handle, C.byref(ln)), "walk_info")
+        return {"lds_nodes": int(ln.value)}
+
     def stats(self):
         st = _lib.mrt_stats()
         check(lib().mrt_scene_last_stats(self.handle, C.byref(st)), "stats")

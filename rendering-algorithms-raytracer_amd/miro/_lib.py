@@ -27,7 +27,7 @@ EXPORTS = [
     "mrt_scene_add_instance", "mrt_scene_blas_info", "mrt_scene_blas_export", "mrt_scene_set_material_emission",
     "mrt_scene_set_material_sample_env", "mrt_scene_set_path_trace", "mrt_scene_prim_object",
     "mrt_image_info", "mrt_image_load", "mrt_scene_add_texture_typed", "mrt_scene_set_material_maps",
-    "mrt_scene_mesh_set_texcoords", "mrt_scene_mesh_texcoords", "mrt_scene_set_mesh_motion",
+    "mrt_scene_mesh_set_texcoords", "mrt_scene_mesh_texcoords", "mrt_scene_set_mesh_motion", "mrt_scene_walk_info",
 ]
 
 
@@ -198,6 +198,8 @@ def load():
     L.mrt_scene_add_instance.argtypes = [C.c_void_p, C.c_int32, _fp]
     L.mrt_scene_blas_info.argtypes = [C.c_void_p, C.c_int32, _ip, _ip, _ip]
     L.mrt_scene_blas_export.argtypes = [C.c_void_p, C.c_int32, _fp, _ip, _fp, _ip]
+    if hasattr(L, "mrt_scene_walk_info"):
+        L.mrt_scene_walk_info.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
     if hasattr(L, "mrt_debug_libm"):   # (absent from round-4 builds loaded for A/B runs via MRT_LIB)
         L.mrt_debug_libm.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
     L.mrt_rcp_nr.argtypes = [C.c_float]
