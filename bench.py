@@ -824,7 +824,7 @@ def main():
                             f"host copies -- a run of the multi-rank code, not a measurement")
     if frame_check is not None:
         out["frame_check"] = frame_check
-    if st.get("fused"):   # the frame kernel's walk: LDS top-node walk chosen per scene by a probe frame
+    if st.get("fused"):   # the frame kernel's walk (LDS top nodes only with tuning lds_nodes 1)
         out["walk"] = scene.walk_info()
     if split_times is not None:
         out["split_times"] = split_times
