@@ -718,30 +718,46 @@ def main():
                "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "note": "SURVEY.md 8(d) pricing (algorithmic bytes / 8 TB/s); non-physical above 1: the bytes are "
                        "served by L1 / L2, not HBM (see hbm / per_step.hbm_frac_counters for the DRAM-side bytes)"}
-    # latency model of the one-launch frame kernel: every wave walks its tiles' rays one
-    # dependent node step at a time (a step = node fetch -> box test -> push / pop, then the
-    # step's leaf triangles); a tile costs its slowest lane's steps (count-mode wave steps,
-    # primary + shadow).  With `waves` resident waves per SIMD sharing the launch time, the
-    # time one wave spends per step is launch_ms / (wave steps / resident wave slots).
+    # latency model of the one-launch frame kernel.  Every wave walks its tiles' rays one
+    # dependent node step at a time (a step = node fetch -> box test -> stack op, plus the
+    # step's leaf triangles, for the whole wave); count mode counts those wave steps.  The
+    # launch's SIMD-cycles divided by them give the SIMD time one wave step costs; the
+    # tracked profile's VALU instruction count (SQ_INSTS_VALU, 2 cycles per wave64 op on a
+    # SIMD-32, MI355X_MICROARCH.md) gives the part of it spent issuing VALU, and the rest is
+    # latency the other resident waves did not cover.
     lat_model = None
     wsteps = st.get("primary_wave_steps", 0) + st.get("shadow_wave_steps", 0)
     if st.get("fused") and wsteps:
         simds = 4 * int(torch.cuda.get_device_properties(dev).multi_processor_count)
         waves = int(tuning.get("frame1_waves", 7))
-        per_slot = wsteps / (simds * waves)
-        ns_step = dom_ms * 1e6 / per_slot
+        clk = float((latency or {}).get("clock_ghz") or 2.4)
+        simd_cyc = dom_ms * 1e-3 * clk * 1e9 * simds / wsteps
         lat_model = {
-            "wave_steps_per_frame": int(wsteps), "resident_wave_slots": simds * waves,
-            "steps_per_wave_slot": round(per_slot, 1), "ns_per_step_per_wave": round(ns_step, 1),
-            "cycles_per_step_at_2p4ghz": round(ns_step * 2.4, 0),
-            "l2_hit_latency_cycles": "180-225 (MI355X_MICROARCH.md, one lane, idle chip)",
-            "lane_use": round((st["primary_node_visits"] + st.get("shadow_node_visits", 0)) / (64.0 * wsteps), 4),
-            "reading": ("latency-bound: each resident wave spends ~%.0f cycles per dependent node step (one node "
-                        "fetch + box test + stack op, plus the step's triangle tests), ~1-2 cache-hit latencies; "
-                        "%d waves per SIMD overlap them, so the frame takes steps-per-slot x that step latency. Neither "
-                        "bandwidth roofline binds (L2 frac %.2f, counter HBM frac %s)."
-                        % (ns_step * 2.4, waves, achieved / L2_PEAK_GBS,
-                           "n/a" if hbm is None else "%.3f" % hbm["frac"]))}
+            "wave_steps_per_frame": int(wsteps), "resident_waves": simds * waves, "waves_per_simd": waves,
+            "steps_per_wave": round(wsteps / (simds * waves), 1), "clock_ghz": clk,
+            "simd_cycles_per_wave_step": round(simd_cyc, 1),
+            "wave_cycles_per_step": round(simd_cyc * waves, 0),
+            "lane_use": round((st["primary_node_visits"] + st.get("shadow_node_visits", 0)) / (64.0 * wsteps), 4)}
+        vpw = (latency or {}).get("valu_insts_per_wave")
+        if vpw and (latency or {}).get("waves"):
+            valu_step = vpw * latency["waves"] / wsteps
+            lat_model.update({
+                "valu_insts_per_wave_step": round(valu_step, 1),
+                "valu_issue_cycles_per_step": round(2 * valu_step, 1),
+                "valu_issue_share": round(2 * valu_step / simd_cyc, 3),
+                "uncovered_latency_cycles_per_step": round(simd_cyc - 2 * valu_step, 1),
+                "source": "valu counts from the tracked profile (%s)" % (prof or {}).get("source")})
+            lat_model["reading"] = (
+                "latency-bound with VALU issue second: a SIMD spends %.0f cycles per wave step, %.0f%% of them "
+                "issuing its %.0f VALU instructions (2 cycles each); in the other %.0f cycles all %d resident waves "
+                "wait on their dependent node / triangle fetches (L1 / L2 hits, 180-225+ cycles each, "
+                "MI355X_MICROARCH.md). Bandwidth is not the bound: L2 frac %.2f, counter HBM frac %s."
+                % (simd_cyc, 100 * 2 * valu_step / simd_cyc, valu_step, simd_cyc - 2 * valu_step, waves,
+                   achieved / L2_PEAK_GBS, "n/a" if hbm is None else "%.3f" % hbm["frac"]))
+        else:
+            lat_model["reading"] = ("a SIMD spends %.0f cycles per wave step (%d waves resident); no tracked VALU "
+                                    "counts for this config, so the issue / latency split is not given"
+                                    % (simd_cyc, waves))
     # primary-kernel lanes doing node work per issued wave step (adaptive: no primary launch)
     lane_util = round(st["primary_node_visits"] / (64 * st["primary_wave_steps"]), 4) if st["primary_wave_steps"] else None
     out = {

@@ -437,7 +437,8 @@ int mrt_device_wall_clock_khz(const mrt_scene* s);
 
 /* Numerics probes (x86 RCPSS/RSQRTSS emulation + one Newton step, SSE.h:67-101). */
 /* The device's acosf(x) (fn 0) / atan2f(y, x) (fn 1) over n host inputs (a kernel on
- * the current device; glibc's fdlibm code restated, csrc/mrt_libm.h). */
+ * the current device; glibc's fdlibm code restated, csrc/mrt_libm.h), or its rcp_nr(x)
+ * (fn 2: the RCPSS emulation and Newton step of every triangle test; y unused). */
 int mrt_debug_libm(int fn, const float* x, const float* y, size_t n, float* out);
 float mrt_rcp_nr(float x);
 float mrt_rsqrt_nr(float x);

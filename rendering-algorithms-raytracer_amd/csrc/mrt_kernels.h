@@ -133,7 +133,9 @@ __device__ __forceinline__ bool tri_test(const float* __restrict__ T, const DRay
     const float b = inv * (r.d[0] * qx + (r.d[1] * qy + r.d[2] * qz));
     const float t = inv * (e1x * qx + (e1y * qy + e1z * qz));
     ot = t; oa = a; ob = b;
-    return (a >= 0.0f) & (a <= 1.0f) & (b >= 0.0f) & (b <= 1.0f) & ((a + b) <= 1.0f) & (t >= tMin) & (t < tBest);
+    // the reference's a <= 1 and b <= 1 lanes are implied: with a, b >= 0 (so neither is
+    // NaN), a + b rounds to at least max(a, b), so (a + b) <= 1 bounds both
+    return (a >= 0.0f) & (b >= 0.0f) & ((a + b) <= 1.0f) & (t >= tMin) & (t < tBest);
 }
 
 // QBVH_Node::intersect (src/BVH.cpp:391-414) -> 4-bit hit mask.

@@ -40,16 +40,21 @@ MRT_HD uint32_t tbl_bits(uint16_t e) { return 0x3F000000u | ((uint32_t)e << 11);
 
 // RCPSS emulation; T = 2048-entry packed rcp table.  Written as a select chain
 // (lowest priority first) so device code has no divergent branches; the table
-// index is in range for every input.
+// index is in range for every input.  On |x| bits a = u & 0x7FFFFFFF: a normal x
+// (exponent e in 1..252) gives exponent 253 - e and the entry's 12 mantissa bits,
+// formed as (s | 253 << 23 | entry << 11) - (e << 23) (no borrow reaches the
+// mantissa or the sign); e >= 253 (and inf) -> +-0; zero / denormal -> +-inf;
+// NaN -> quiet NaN.  (Round 5: 5 fewer VALU ops per triangle test than testing e
+// and m separately; exhaustively equal, tests/test_numerics.py.)
 MRT_HD float x86_rcp(float x, const uint16_t* T) {
-    const uint32_t u = f2u(x), s = u & 0x80000000u, e = (u >> 23) & 0xFFu, m = u & 0x7FFFFFu;
-    uint32_t t = tbl_bits(T[m >> 12]);
+    const uint32_t u = f2u(x), a = u & 0x7FFFFFFFu, s = u & 0x80000000u;
+    uint32_t t = T[(a >> 12) & 0x7FFu];
     MRT_OPAQUE(t);
-    const int re = 253 - (int)e;                                   // 126 - (e - 127)
-    uint32_t r = re <= 0 ? s : (s | ((uint32_t)re << 23) | (t & 0x7FFFFFu));
-    r = e == 0u ? (s | 0x7F800000u) : r;                          // zero / denormal -> inf
+    uint32_t r = (s | 0x7E800000u | (t << 11)) - (a & 0x7F800000u);
+    r = a >= 0x7E800000u ? s : r;                                  // e >= 253: below FLT_MIN -> +-0; inf -> +-0
+    r = a < 0x00800000u ? (s | 0x7F800000u) : r;                  // zero / denormal -> +-inf
     MRT_OPAQUE(r);
-    r = e == 0xFFu ? (m ? (u | 0x00400000u) : s) : r;              // NaN -> quiet, inf -> 0
+    r = a > 0x7F800000u ? (u | 0x00400000u) : r;                  // NaN -> quiet
     return u2f(r);
 }
 

@@ -1,11 +1,12 @@
 #!/bin/bash
-# Same-box A/B: this build (libmrt.so) against round 4's (libmrt_r04.so, built from
-# commit 981f1bb into the lib directory) on each config of $CONFIGS, alternated twice;
-# then tuning A/Bs given as "CFG:key=v1,v2" words in $TUNES.
+# Same-box A/B of library builds: the libraries named in $LIBS (default: this build,
+# libmrt.so, against round 4's libmrt_r04.so built from commit 981f1bb; libmrt_prev.so =
+# a build of the last commit, from a git worktree) on each config of $CONFIGS,
+# alternated twice; then tuning A/Bs given as "CFG:key=v1,v2" words in $TUNES.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export MRT_SCENE_CACHE=/tmp/mrt_scenes
-for c in ${CONFIGS:-C3}; do for i in 1 2; do for L in libmrt libmrt_r04; do
+for c in ${CONFIGS:-C3}; do for i in 1 2; do for L in ${LIBS:-libmrt libmrt_r04}; do
   echo "== $c $L run $i"
   AB_CONFIG=$c MRT_LIB=rendering-algorithms-raytracer_amd/lib/$L.so timeout -k 10 240 python tools/ab_bench.py \
       --rounds ${ROUNDS:-4} 2>&1 | grep -E "^\{" || exit 1
