@@ -127,6 +127,12 @@ __device__ __forceinline__ bool tri_test(const float* __restrict__ T, const DRay
     const float inv = rcp_nr(det, rcpT);
     const float tx = r.o[0] - ax, ty = r.o[1] - ay, tz = r.o[2] - az;
     const float a = inv * (tx * px + (ty * py + tz * pz));
+    // no active lane has a in [0, 1] (most tests of a packet the wave's rays miss):
+    // the wave skips b and t -- every lane's answer is "no hit" either way
+    if (__ballot((a >= 0.0f) & (a <= 1.0f)) == 0) {
+        ot = a; oa = a; ob = a;
+        return false;
+    }
     const float qx = ty * e0z - tz * e0y;
     const float qy = -1.0f * (tx * e0z - tz * e0x);
     const float qz = tx * e0y - ty * e0x;
