@@ -9,10 +9,10 @@ export MRT_SCENE_CACHE=/tmp/mrt_scenes
 for c in ${CONFIGS:-C3}; do for i in 1 2; do for L in ${LIBS:-libmrt libmrt_r04}; do
   echo "== $c $L run $i"
   AB_CONFIG=$c MRT_LIB=rendering-algorithms-raytracer_amd/lib/$L.so timeout -k 10 240 python tools/ab_bench.py \
-      --rounds ${ROUNDS:-4} 2>&1 | grep -E "^\{" || exit 1
+      --rounds ${ROUNDS:-4} 2>&1 | grep -E "^(\{|variant)" || exit 1
 done; done; done
 for t in $TUNES; do
   c=${t%%:*}; kv=${t#*:}
   echo "== $c $kv"
-  AB_CONFIG=$c timeout -k 10 300 python tools/ab_bench.py $kv --rounds ${ROUNDS:-4} 2>&1 | grep -E "^\{" || exit 1
+  AB_CONFIG=$c timeout -k 10 300 python tools/ab_bench.py $kv --rounds ${ROUNDS:-4} 2>&1 | grep -E "^(\{|variant)" || exit 1
 done
