@@ -738,6 +738,10 @@ def main():
             "simd_cycles_per_wave_step": round(simd_cyc, 1),
             "wave_cycles_per_step": round(simd_cyc * waves, 0),
             "lane_use": round((st["primary_node_visits"] + st.get("shadow_node_visits", 0)) / (64.0 * wsteps), 4)}
+        # the timed steps keep several frames in flight, so the launch tails overlap: the same
+        # wave steps over ms_per_step (per frame) give the steady-state SIMD time per step
+        pipe_cyc = elapsed / args.steps / max(1, n_frames) * clk * 1e9 * simds / wsteps
+        lat_model["pipelined_simd_cycles_per_wave_step"] = round(pipe_cyc, 1)
         vpw = (latency or {}).get("valu_insts_per_wave")
         if vpw and (latency or {}).get("waves"):
             valu_step = vpw * latency["waves"] / wsteps
@@ -745,14 +749,17 @@ def main():
                 "valu_insts_per_wave_step": round(valu_step, 1),
                 "valu_issue_cycles_per_step": round(2 * valu_step, 1),
                 "valu_issue_share": round(2 * valu_step / simd_cyc, 3),
+                "pipelined_valu_issue_share": round(2 * valu_step / pipe_cyc, 3),
                 "uncovered_latency_cycles_per_step": round(simd_cyc - 2 * valu_step, 1),
                 "source": "valu counts from the tracked profile (%s)" % (prof or {}).get("source")})
             lat_model["reading"] = (
-                "latency-bound with VALU issue second: a SIMD spends %.0f cycles per wave step, %.0f%% of them "
-                "issuing its %.0f VALU instructions (2 cycles each); in the other %.0f cycles all %d resident waves "
-                "wait on their dependent node / triangle fetches (L1 / L2 hits, 180-225+ cycles each, "
-                "MI355X_MICROARCH.md). Bandwidth is not the bound: L2 frac %.2f, counter HBM frac %s."
-                % (simd_cyc, 100 * 2 * valu_step / simd_cyc, valu_step, simd_cyc - 2 * valu_step, waves,
+                "one launch alone: a SIMD spends %.0f cycles per wave step, %.0f%% of them issuing its %.0f VALU "
+                "instructions (2 cycles each) and the rest with all %d resident waves waiting on dependent node / "
+                "triangle fetches (L1 / L2 hits, 180-225+ cycles each, MI355X_MICROARCH.md) or in the launch's "
+                "ramp and tail. In the timed steps (frames in flight, tails overlapped) a step costs %.0f SIMD "
+                "cycles, %.0f%% of them VALU issue: the frame is bound by VALU issue first and dependent-fetch "
+                "latency second. Bandwidth is not the bound: L2 frac %.2f, counter HBM frac %s."
+                % (simd_cyc, 100 * 2 * valu_step / simd_cyc, valu_step, waves, pipe_cyc, 100 * 2 * valu_step / pipe_cyc,
                    achieved / L2_PEAK_GBS, "n/a" if hbm is None else "%.3f" % hbm["frac"]))
         else:
             lat_model["reading"] = ("a SIMD spends %.0f cycles per wave step (%d waves resident); no tracked VALU "
