@@ -409,8 +409,8 @@ int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
  * bands + lane refill), "refill_min" 1..64 [40] (idle lanes that trigger a refill),
  * "fast_box" 0/[1] (hardware min/max slab test when its finiteness precondition
  * holds), "primary_waves" 0/6/[7]/8 (occupancy target of the primary-ray kernel),
- * "sched" 0..4 [2] (tile schedule: static grid-stride, static XCD bands, dynamic
- * interleaved, dynamic banded, dynamic interleaved by 16-tile groups; see TileSched), "shade1" 0/[1] (specialised shading
+ * "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands, dynamic
+ * interleaved, dynamic banded; see TileSched), "shade1" 0/[1] (specialised shading
  * kernel for one point light and one path), "lds_nodes" 0..1 (the frame kernel's
  * LDS top-node walk: [0] off, 1 on; C2 -4%, C3 +9% with 4 frames in flight), "scalar_nodes" 0..[7] (bit 0 scalar fetch of wave-uniform nodes, bit 1 of
  * wave-uniform triangles, bit 2 octant-ordered box test), "fused" 0/[1] (one-launch frame kernel

@@ -440,7 +440,7 @@ struct DeviceState {
 static int g_fast_box = 1;        // hardware min/max box test when its precondition holds
 static int g_primary_waves = 7;   // launch-bounds occupancy target of the primary kernel: 0 (none), 6, 7, 8
 static int g_shade_waves = 5;     // same for shade1_kernel: 1 (none), 4..8 (5: 96 VGPRs, 64 B spill; -2.5% vs 6)
-static int g_sched = 2;           // TileSched mode 0..4 (2: counter c hands out items c, c + 8, ...; 4: groups of 16)
+static int g_sched = 2;           // TileSched mode 0..3 (2 measured fastest)
 static int g_batch_tpw = 2;       // bucket batches: tiles per wave the launch's grid is sized for when the batch is
                                   // smaller than the persistent grid (a 1/4 or 1/8 split share): 2 -- C3 share model
                                   // 2.98 -> 3.17x at N = 4, 4.69 -> 4.74x at N = 8; 4: 3.99x at N = 8
@@ -2873,7 +2873,7 @@ int mrt_set_tuning(const char* key, int value) {
         if (value != 1 && (value < 5 || value > 8)) { set_error("frame1_waves must be 1 or 5..8"); return MRT_ERR_INVALID; }
         g_frame1_waves = value;
     } else if (k == "sched") {
-        if (value < 0 || value > 4) { set_error("sched must be 0..4"); return MRT_ERR_INVALID; }
+        if (value < 0 || value > 3) { set_error("sched must be 0..3"); return MRT_ERR_INVALID; }
         g_sched = value;
     } else { set_error("unknown tuning key " + k); return MRT_ERR_INVALID; }
     return MRT_OK;

@@ -1081,13 +1081,8 @@ struct TileSched {
             while (probe < 8) {
                 const int c = (home + probe) & 7;
                 const unsigned v = atomicAdd(P.queue + c * 32, 1u);
-                // mode 4: counter c hands out whole groups of 16 consecutive items (a 128-pixel
-                // strip of 8x8 tiles, or one 32x32 bucket), groups c, c + 8, ...; its workgroups
-                // sit on XCD c, so the output lines a group writes are written back by one L2
-                // instead of being shared between the L2s of neighbouring tiles' XCDs
                 const long idx = (mode == 3) ? (v < (unsigned)band ? (long)c * band + v : (long)P.n_tiles)
-                                 : (mode == 4) ? (((long)c + 8l * (long)(v >> 4)) << 4) + (long)(v & 15u)
-                                               : (long)c + 8l * v;
+                                             : (long)c + 8l * v;
                 if (idx < P.n_tiles) { item = (int)idx; break; }
                 probe++;
             }
