@@ -398,8 +398,11 @@ int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const floa
                     const float* d_tmax, size_t n, int any_hit, mrt_hit* d_out, void* stream);
 
 /* The walk of the scene's last one-light frame on its current device: *lds_nodes = 1
- * when it ran the LDS top-node walk (tuning "lds_nodes"), 0 when not, -1 before any. */
-int mrt_scene_walk_info(const mrt_scene* s, int32_t* lds_nodes);
+ * when it ran the LDS top-node walk (tuning "lds_nodes"), 0 when not, -1 before any;
+ * *walk_exits = the frame kernel's walk-loop form, 1 (one exit) or 2 (a second exit on
+ * stack overflow), picked per scene by a probe of single frames (tuning "walk_exit"),
+ * -1 before it ran.  Both forms give the same bits. */
+int mrt_scene_walk_info(const mrt_scene* s, int32_t* lds_nodes, int32_t* walk_exits);
 
 /* Counters of the last render on this scene (ray counts, visits, kernel time). */
 int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
@@ -409,7 +412,8 @@ int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
  * bands + lane refill), "refill_min" 1..64 [40] (idle lanes that trigger a refill),
  * "fast_box" 0/[1] (hardware min/max slab test when its finiteness precondition
  * holds), "primary_waves" 0/6/[7]/8 (occupancy target of the primary-ray kernel),
- * "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands, dynamic
+ * "walk_exit" [-1]..1 (the frame kernel's walk loop: auto by a per-scene probe, two
+ * exits, one exit), "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands, dynamic
  * interleaved, dynamic banded; see TileSched), "shade1" 0/[1] (specialised shading
  * kernel for one point light and one path), "lds_nodes" 0..1 (the frame kernel's
  * LDS top-node walk: [0] off, 1 on; C2 -4%, C3 +9% with 4 frames in flight), "scalar_nodes" 0..[7] (bit 0 scalar fetch of wave-uniform nodes, bit 1 of

@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
         const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
         DHit h{o.w, 0.f, 0.f, -1};
         const uint32_t n0 = st.nodes;
-        P.occl[e] = traverse<true, COUNT, FAST, INST, CHECK>(T, r, 0.001f, h, st) ? 1 : 0;
+        P.occl[e] = traverse<true, COUNT, FAST, INST, CHECK, false, !INST>(T, r, 0.001f, h, st) ? 1 : 0;
         return st.nodes - n0;
     };
     // per-XCD band of ray slots and its chunk counter (own 128-B line)
@@ -414,6 +414,7 @@ struct DeviceState {
     bool boxes_ordered = false;  // every used slot box has lo <= hi per axis (octant-ordered box test)
     bool lds_ok = false;         // the world hierarchy has kLdsNodes nodes for the LDS top-node walk (renumbered)
     std::atomic<int> lds_pick{-1};   // the last one-light frame ran the LDS top-node walk: 1 yes, 0 no, -1 none yet
+    std::atomic<int> exit_pick{-1};  // frame1_kernel's walk loop for this scene: 1 one exit, 0 two, -1 not probed yet
     float bb_lo[3] = {0, 0, 0}, bb_hi[3] = {0, 0, 0};   // world root box (ray-binning origin cells)
     int cus = 0;
     bool point_only = false;
@@ -475,6 +476,9 @@ static int g_chain_mb = 8192;     // chain scratch per stream (MB), at most 80% 
                                   // 48 GB and R3 / P4 / FS nothing (profiles/r04_chain_mb_est_ab.txt)
 static int g_chain_adapt = 1;     // adaptive supersampling of REC scenes: passes over the chain engine (0: fused kernel)
 static int g_fused = 1;           // one point light, one path: frame1_kernel (primary + shading in one launch)
+static int g_walk_exit = -1;      // frame1_kernel's walk loop: 1 one exit (the overflow empties the stack), 0 two
+                                  // (the overflow returns); -1 auto: a probe of single frames on the scene's first
+                                  // fused render picks (one exit: C3 -7%, C3L -1%; two: C2 -12%, r05_walk_exit_ab.txt)
 static int g_lds_nodes = 0;       // frame1_kernel's LDS top-node walk (LN), 0 off / 1 on: with 4 frames in flight C2
                                   // -4.1%, C3 +9%, C3L +11% (profiles/r05_lds_nodes_ab_*.txt); no probe separated them
                                   // reliably (single-frame kernel times are equal on C2), so it is off unless asked for
@@ -1128,15 +1132,17 @@ static int blocks_per_cu(KernelFn f, size_t lds) {
     return n;
 }
 
-template <int W, bool I = false, bool CHK = true>
+template <int W, bool I = false, bool CHK = true, bool X = false>
 static KernelFn primary_fn(bool c, bool f) {
-    return c ? (f ? primary_kernel<true, W, true, I, CHK> : primary_kernel<true, W, false, I, CHK>)
-             : (f ? primary_kernel<false, W, true, I, CHK> : primary_kernel<false, W, false, I, CHK>);
+    return c ? (f ? primary_kernel<true, W, true, I, CHK, X> : primary_kernel<true, W, false, I, CHK, X>)
+             : (f ? primary_kernel<false, W, true, I, CHK, X> : primary_kernel<false, W, false, I, CHK, X>);
 }
 // check: the special-leaf scene has alpha-mapped or motion-blurred lanes; scenes with
 // instances only take the variants without those tests (no noinline calls: C5's nested
 // instance walk at 5 waves spills 28 B instead of 256 B per lane)
-static KernelFn pick_primary(int w, bool c, bool f, bool inst, bool check = true) {
+// xone: the one-exit walk loop (non-instanced scenes; the instanced walk keeps its exits:
+// C5's primary launch measured 36% slower with one)
+static KernelFn pick_primary(int w, bool c, bool f, bool inst, bool check = true, bool xone = false) {
     if (inst && !check) {
         switch (g_primary_inst_waves) {
             case 4: return primary_fn<4, true, false>(c, f);
@@ -1151,6 +1157,14 @@ static KernelFn pick_primary(int w, bool c, bool f, bool inst, bool check = true
             case 5: return primary_fn<5, true>(c, f);
             case 6: return primary_fn<6, true>(c, f);
             default: return primary_fn<1, true>(c, f);
+        }
+    }
+    if (xone) {
+        switch (w) {
+            case 6: return primary_fn<6, false, true, true>(c, f);
+            case 7: return primary_fn<7, false, true, true>(c, f);
+            case 8: return primary_fn<8, false, true, true>(c, f);
+            default: return primary_fn<1, false, true, true>(c, f);
         }
     }
     switch (w) {
@@ -1614,6 +1628,34 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(f), dim3(g), dim3(kWG), args, 0, stream));
         return MRT_OK;
     };
+    // the walk loop's exit form (same bits either way; traverse_impl XONE): tuning "walk_exit",
+    // or a probe on this stream the first time the scene renders a timed frame here -- three
+    // single launches of each form, alternating, the faster minimum wins (a one-time host
+    // wait).  Returns 0 / 1, -1 (not probed: count mode), -2 on a HIP failure (rc set).
+    auto exit_form = [&](bool may_probe, auto pick) -> int {
+        int wx = g_walk_exit >= 0 ? g_walk_exit : d.exit_pick.load();
+        if (wx >= 0 || count || !may_probe) return wx;
+        hipEvent_t ea = nullptr, eb = nullptr;
+        if (hipEventCreate(&ea) != hipSuccess || hipEventCreate(&eb) != hipSuccess) rc = MRT_ERR_HIP;
+        float best[2] = {1e30f, 1e30f};
+        for (int rep = 0; rep < 3 && rc == MRT_OK; rep++)
+            for (int v = 0; v < 2 && rc == MRT_OK; v++) {
+                float ms = 0.f;
+                if (hipMemsetAsync(c.ctr, 0, kCtrBytes, stream) != hipSuccess ||
+                    hipEventRecord(ea, stream) != hipSuccess) { rc = MRT_ERR_HIP; break; }
+                if ((rc = launch(pick(v)))) break;
+                if (hipEventRecord(eb, stream) != hipSuccess || hipEventSynchronize(eb) != hipSuccess ||
+                    hipEventElapsedTime(&ms, ea, eb) != hipSuccess) { rc = MRT_ERR_HIP; break; }
+                best[v] = std::min(best[v], ms);
+            }
+        if (ea) (void)hipEventDestroy(ea);
+        if (eb) (void)hipEventDestroy(eb);
+        if (rc == MRT_OK && hipMemsetAsync(c.ctr, 0, kCtrBytes, stream) != hipSuccess) rc = MRT_ERR_HIP;
+        if (rc) { set_error("walk exit probe failed"); return -2; }
+        wx = best[1] <= best[0] ? 1 : 0;
+        d.exit_pick = wx;
+        return wx;
+    };
     HIP_OK(hipEventRecord(c.ev0, stream));
     const bool fb = P.fast_box != 0;
     c.chain_used = false;
@@ -1639,7 +1681,10 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         // LDS top-node walk (tuning "lds_nodes"; both walks give the same bits)
         const bool ln = fb && d.lds_ok && g_lds_nodes > 0;
         d.lds_pick = ln ? 1 : 0;
-        if ((rc = launch(pick_frame1(g_frame1_waves, count, fb, d.pow_spec, ln)))) return rc;
+        const int wx = exit_form(!ln, [&](int v) { return pick_frame1(g_frame1_waves, false, fb, d.pow_spec, v); });
+        if (wx == -2) return rc;
+        const int walk = ln ? 2 : (wx < 0 ? 1 : wx);
+        if ((rc = launch(pick_frame1(g_frame1_waves, count, fb, d.pow_spec, walk)))) return rc;
         HIP_OK(hipEventRecord(c.evm, stream));
         c.last_was_render = true;
         HIP_OK(hipGetLastError());
@@ -1648,7 +1693,10 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         s.last = mrt_stats{};
         return MRT_OK;
     }
-    if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst, d.has_alpha || d.has_mb)))) return rc;
+    const bool chk = d.has_alpha || d.has_mb;
+    const int px = exit_form(!inst, [&](int v) { return pick_primary(g_primary_waves, false, fb, inst, chk, v != 0); });
+    if (px == -2) return rc;
+    if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst, chk, px == 1)))) return rc;
     HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
     const int max_sh = max_shadow_rays(s);
@@ -2625,11 +2673,15 @@ int mrt_render(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
     return MRT_OK;
 }
 
-int mrt_scene_walk_info(const mrt_scene* cs, int32_t* lds_nodes) {
+int mrt_scene_walk_info(const mrt_scene* cs, int32_t* lds_nodes, int32_t* walk_exits) {
     if (!cs) { set_error("bad argument"); return MRT_ERR_INVALID; }
     const Scene& S = cs->impl;
     const DeviceState* d = S.dev;
     if (lds_nodes) *lds_nodes = d ? (int32_t)d->lds_pick.load() : -1;
+    if (walk_exits) {
+        const int x = g_walk_exit >= 0 ? g_walk_exit : (d ? d->exit_pick.load() : -1);
+        *walk_exits = x < 0 ? -1 : (x ? 1 : 2);
+    }
     return MRT_OK;
 }
 
@@ -2866,6 +2918,9 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "bin_obits") {
         if (value < 0 || value > 4) { set_error("bin_obits must be 0..4"); return MRT_ERR_INVALID; }
         g_bin_obits = value;
+    } else if (k == "walk_exit") {
+        if (value < -1 || value > 1) { set_error("walk_exit must be -1..1"); return MRT_ERR_INVALID; }
+        g_walk_exit = value;
     } else if (k == "lds_nodes") {
         if (value < 0 || value > 1) { set_error("lds_nodes must be 0 or 1"); return MRT_ERR_INVALID; }
         g_lds_nodes = value;

@@ -17,7 +17,7 @@ namespace mrt {
 // POW: some Blinn material has specExp != 1 (Blinn::shade's pow, src/Blinn.cpp:220).  Scenes
 // without one run the POW = false kernels, which carry no double-precision pow: its
 // polynomial constants, hoisted out of the tile loop, took VGPRs and scratch.
-template <bool COUNT, bool FAST, bool POW, bool LN = false>
+template <bool COUNT, bool FAST, bool POW, int WALK = 1>
 __device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, TravStats& st, const DRay& r, float ht,
                                          float ha, float hb, int prim, const uint16_t* rcpT, const uint16_t* rsqT,
                                          uint32_t& shadow_total) {
@@ -68,7 +68,7 @@ __device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, T
             const DRay sr = make_ray(from, L);
             DHit sh{distance, 0.f, 0.f, -1};
             shadow_total++;
-            if (traverse<true, COUNT, FAST, false, true, LN>(T, sr, 0.001f, sh, st)) attenuate = 0.0f;
+            if (traverse<true, COUNT, FAST, false, true, WALK == 2, WALK != 0>(T, sr, 0.001f, sh, st)) attenuate = 0.0f;
         }
         attenuate *= nDotL;
         spec = rdl * attenuate;
@@ -155,9 +155,12 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
 // those of primary_kernel + shade1_kernel, so the frame is bit-identical.
 // LN: the hierarchy's top kLdsNodes nodes are staged in LDS (+8 KB per workgroup)
 // and both walks read their wave-uniform visits from there (traverse_impl); the
-// host runs it where a probe measured it faster (launch_render, lds_nodes).
-template <bool COUNT, bool FAST, int MINW, bool POW, bool LN = false>
+// host runs it when asked (tuning "lds_nodes").
+// WALK (traverse_impl): 0 the walk loop with a second exit (stack overflow returns), 1 one
+// exit (XONE), 2 one exit + LN.  Same bits either way; the host picks 0 / 1 per scene.
+template <bool COUNT, bool FAST, int MINW, bool POW, int WALK = 1>
 __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
+    constexpr bool LN = WALK == 2;
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
     __shared__ QNode s_top[LN ? kLdsNodes : 1];
@@ -194,12 +197,12 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
             const EyeRay er = camera_ray(PA.cam[f], PA.seed + (uint32_t)f, x, y, rsqT);
             const DRay r = make_ray(er.o, er.d);
             DHit h{1e12f, 0.f, 0.f, -1};
-            const bool hit = traverse<false, COUNT, FAST, false, true, LN>(T, r, 0.001f, h, st);
+            const bool hit = traverse<false, COUNT, FAST, false, true, LN, WALK != 0>(T, r, 0.001f, h, st);
             const RenderParams& PB = reload_params();   // shading parameters
             v3 col = mk(PB.bg[0], PB.bg[1], PB.bg[2]);
             if (hit) {
                 nhits++;
-                col = shade1_hit<COUNT, FAST, POW, LN>(PB, T, ss, r, h.t, h.a, h.b, h.prim, rcpT, rsqT, shadow_total);
+                col = shade1_hit<COUNT, FAST, POW, WALK>(PB, T, ss, r, h.t, h.a, h.b, h.prim, rcpT, rsqT, shadow_total);
             }
             const RenderParams& PC = reload_params();   // outputs
             item_pixel(PC, item, lane_id(), x, y, slot);   // recompute: keeps it out of the traversals' live set
@@ -235,26 +238,27 @@ static KernelFn shade1_fn(bool c, bool f) {
     return c ? (f ? shade1_kernel<true, true, W, POW> : shade1_kernel<true, false, W, POW>)
              : (f ? shade1_kernel<false, true, W, POW> : shade1_kernel<false, false, W, POW>);
 }
-template <int W, bool POW, bool LN>
+template <int W, bool POW, int WALK>
 static KernelFn frame1_fn(bool c, bool f) {
-    return c ? (f ? frame1_kernel<true, true, W, POW, LN> : frame1_kernel<true, false, W, POW, LN>)
-             : (f ? frame1_kernel<false, true, W, POW, LN> : frame1_kernel<false, false, W, POW, LN>);
+    return c ? (f ? frame1_kernel<true, true, W, POW, WALK> : frame1_kernel<true, false, W, POW, WALK>)
+             : (f ? frame1_kernel<false, true, W, POW, WALK> : frame1_kernel<false, false, W, POW, WALK>);
 }
-template <bool LN>
-static KernelFn pick_frame1_ln(int w, bool c, bool f, bool pow) {
-    if (pow) return w == 1 ? frame1_fn<1, true, LN>(c, f) : frame1_fn<6, true, LN>(c, f);
+template <int WALK>
+static KernelFn pick_frame1_walk(int w, bool c, bool f, bool pow) {
+    if (pow) return w == 1 ? frame1_fn<1, true, WALK>(c, f) : frame1_fn<6, true, WALK>(c, f);
     switch (w) {
-        case 1: return frame1_fn<1, false, LN>(c, f);
-        case 5: return frame1_fn<5, false, LN>(c, f);
-        case 7: return frame1_fn<7, false, LN>(c, f);
-        case 8: return frame1_fn<8, false, LN>(c, f);
-        default: return frame1_fn<6, false, LN>(c, f);
+        case 1: return frame1_fn<1, false, WALK>(c, f);
+        case 5: return frame1_fn<5, false, WALK>(c, f);
+        case 7: return frame1_fn<7, false, WALK>(c, f);
+        case 8: return frame1_fn<8, false, WALK>(c, f);
+        default: return frame1_fn<6, false, WALK>(c, f);
     }
 }
 // pow: a Blinn material with specExp != 1 (those scenes run at 6 waves, or unbounded);
-// ln: the LDS top-node walk
-KernelFn pick_frame1(int w, bool c, bool f, bool pow, bool ln) {
-    return ln ? pick_frame1_ln<true>(w, c, f, pow) : pick_frame1_ln<false>(w, c, f, pow);
+// walk: 0 two-exit walk loop, 1 one exit, 2 one exit + the LDS top-node walk
+KernelFn pick_frame1(int w, bool c, bool f, bool pow, int walk) {
+    return walk == 2 ? pick_frame1_walk<2>(w, c, f, pow)
+                     : walk == 0 ? pick_frame1_walk<0>(w, c, f, pow) : pick_frame1_walk<1>(w, c, f, pow);
 }
 KernelFn pick_shade1(int w, bool c, bool f, bool pow) {
     if (pow) return w == 1 ? shade1_fn<1, true>(c, f) : shade1_fn<5, true>(c, f);

@@ -380,7 +380,8 @@ __device__ __forceinline__ bool tri_test_lane(const Trav& c, uint32_t leaf, int 
     return ok != 0;
 }
 
-template <bool ANY, bool COUNT, bool FAST, bool INST = false, bool BL = false, bool CHECK = true, bool LN = false>
+template <bool ANY, bool COUNT, bool FAST, bool INST = false, bool BL = false, bool CHECK = true, bool LN = false,
+          bool XONE = true>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root = 0,
                               int sp0 = 0, int32_t aoff = 0);
 
@@ -392,9 +393,11 @@ __device__ __forceinline__ bool proxy_hit(const Trav& c, int inst, const DRay& r
     const DevInstance& I = c.inst[inst];
     const DRay ro = object_ray(I, r, c.rcpT);
     // BLAS packets with alpha-mapped triangles (check bit): PrimShade = shade_base + BLAS object
+    // (the nested walk keeps the two-exit loop: C5's primary launch measured 37% slower with
+    // one exit, traverse_impl XONE)
     if (FAST && ro.finite)
-        return traverse_impl<ANY, COUNT, true, false, true, CHECK>(c, ro, tMin, h, st, I.root, sp, I.shade_base);
-    return traverse_impl<ANY, COUNT, false, false, true, CHECK>(c, ro, tMin, h, st, I.root, sp, I.shade_base);
+        return traverse_impl<ANY, COUNT, true, false, true, CHECK, false, false>(c, ro, tMin, h, st, I.root, sp, I.shade_base);
+    return traverse_impl<ANY, COUNT, false, false, true, CHECK, false, false>(c, ro, tMin, h, st, I.root, sp, I.shade_base);
 }
 
 // BVH::intersect, QBVH branch (src/BVH.cpp:1128-1178).  Returns hit; h.prim is
@@ -421,7 +424,7 @@ __device__ __forceinline__ bool proxy_hit(const Trav& c, int inst, const DRay& r
 // breadth first on upload) read them from LDS (c.lnodes, one broadcast address)
 // instead of the scalar cache -- faster where the top levels end most rays (the
 // walk is per scene, chosen by a probe: mrt_device.hip, lds_nodes).
-template <bool ANY, bool COUNT, bool FAST, bool INST, bool BL, bool CHECK, bool LN>
+template <bool ANY, bool COUNT, bool FAST, bool INST, bool BL, bool CHECK, bool LN, bool XONE>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root,
                               int sp0, int32_t aoff) {
     int sp = sp0;
@@ -488,6 +491,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
             // near-first mode takes the nearest instead (its answer is order-free)
             const int top = (FAST && ANY && c.near_first) ? nearest_slot(inner, tn) : 31 - __builtin_clz((unsigned)inner);
             const int rest = inner ^ (1 << top);
+            bool ovf = false;
             if (rest) {
                 if (sp + 4 <= kLdsStack) {
                     c.lds[sp * kWG] = ch.x; sp += rest & 1;
@@ -495,15 +499,27 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                     c.lds[sp * kWG] = ch.z; sp += (rest >> 2) & 1;
                     c.lds[sp * kWG] = ch.w; sp += (rest >> 3) & 1;
                 } else {
+                    bool pushed = true;
 #pragma unroll
                     for (int i = 0; i < 4; i++)
-                        if ((rest >> i) & 1)
-                            if (!stk_push(c, sp, sel4(ch, i))) { st.overflow = true; return hit; }
+                        if ((rest >> i) & 1) pushed = pushed && stk_push(c, sp, sel4(ch, i));
+                    // overflow (flagged).  XONE: the walk ends at the loop's one exit (the pop
+                    // test below, with the stack emptied) instead of returning from here --
+                    // an extra exit of the divergent loop costs exec-mask bookkeeping in every
+                    // step (SALU -19% per step, C3 -7%, C4 -6%), but the two-exit form measured
+                    // faster on the bunny scenes (C2 +13% with one exit): frame1_kernel picks
+                    // per scene (mrt_device.hip, exit probe)
+                    if (!pushed) {
+                        st.overflow = true;
+                        if (!XONE) return hit;
+                        sp = sp0;
+                        ovf = true;
+                    }
                 }
                 if (COUNT && sp > st.max_sp) st.max_sp = sp;
             }
             nxt = sel4(ch, top);
-            have_next = true;
+            have_next = !ovf;
         }
         if (lm) {
             uint32_t leaf = 0;
@@ -547,7 +563,7 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                     ok = tri_test_lane(c, leaf, k, r, tMin, h.t, t, a, b);
                 }
                 if (ok) {
-                    if (ANY) return true;
+                    if (ANY) return true;   // (an any-hit walk: returning here measured faster than a flag)
                     h.t = t; h.a = a; h.b = b; h.prim = (int32_t)((leaf << 2) | (uint32_t)k);
                     if (INST) h.inst = -1;
                     hit = true;
@@ -764,10 +780,14 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
 // whose origin and 1/d are finite; any other ray takes the exact loop.  A
 // closest hit's packed slot is resolved to the global prim id here.
 // An instance hit's id is the instance's hit_base + its BLAS object index.
-template <bool ANY, bool COUNT, bool FAST = false, bool INST = false, bool CHECK = true, bool LN = false>
+// XONE: the one-exit walk loop (traverse_impl) -- on where measured faster: frame1_kernel /
+// primary_kernel per scene (host probe), the shadow and adaptive kernels of plain scenes
+// (C4 -6%, A3 -4%); off in the chain engine (P4 +21%, R3 +4% with it) and nested BLAS walks
+template <bool ANY, bool COUNT, bool FAST = false, bool INST = false, bool CHECK = true, bool LN = false,
+          bool XONE = false>
 __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
-    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST, false, CHECK, LN>(c, r, tMin, h, st)
-                                        : traverse_impl<ANY, COUNT, false, INST, false, CHECK>(c, r, tMin, h, st);
+    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST, false, CHECK, LN, XONE>(c, r, tMin, h, st)
+                                        : traverse_impl<ANY, COUNT, false, INST, false, CHECK, false, XONE>(c, r, tMin, h, st);
     if (!ANY && hit) {
         h.prim = c.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3];
         if (INST && h.inst >= 0) h.prim += c.inst[h.inst].hit_base;

@@ -312,7 +312,7 @@ struct Shader {
         } else {
             DRay r = make_ray(from, L, shadow_time);
             DHit h{tMax, 0.f, 0.f, -1};
-            return traverse<true, COUNT, FAST, INST>(T, r, 0.001f, h, st);
+            return traverse<true, COUNT, FAST, INST, true, false, !INST>(T, r, 0.001f, h, st);
         }
     }
 
@@ -1233,7 +1233,8 @@ __device__ __forceinline__ EyeRay camera_ray(const CamParams& cam, uint32_t seed
 // Kernel 1: Camera::eyeRayAdaptive + closest-hit BVH::intersect per pixel.
 // Writes the HitInfo record (t, a, b, prim) to P.hits[slot].
 // CHECK: the special-leaf scene has alpha-mapped or motion-blurred lanes (false: instances only)
-template <bool COUNT, int MINW, bool FAST, bool INST = false, bool CHECK = true>
+// XONE: the walk loop's exit form (traverse_impl; same bits), picked per scene by the host
+template <bool COUNT, int MINW, bool FAST, bool INST = false, bool CHECK = true, bool XONE = false>
 __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
     __shared__ uint16_t s_tab[2048];
     __shared__ int32_t s_stack[kLdsStack * kWG];
@@ -1269,7 +1270,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
             const EyeRay er = camera_ray(cam, PA.seed + (uint32_t)f, x, y, rsqT);
             DRay r = make_ray(er.o, er.d, er.time);
             DHit h{1e12f, 0.f, 0.f, -1};
-            if (!traverse<false, COUNT, FAST, INST, CHECK>(T, r, 0.001f, h, st)) h.prim = -1;
+            if (!traverse<false, COUNT, FAST, INST, CHECK, false, XONE>(T, r, 0.001f, h, st)) h.prim = -1;
             const RenderParams& PC = reload_params();
             item_pixel(PC, item, lane_id(), x, y, slot);  // recompute: keeps it out of the traversal's live set
             PC.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(h.prim));
@@ -1433,7 +1434,7 @@ __global__ void __launch_bounds__(kWG, MINW) adaptive_kernel(RenderParams P) {
         DHit h{1e12f, 0.f, 0.f, -1};
         v3 col;
         eye_rays++;
-        const bool hit = traverse<false, COUNT, FAST, INST>(T, r, 0.001f, h, st);
+        const bool hit = traverse<false, COUNT, FAST, INST, true, false, !INST>(T, r, 0.001f, h, st);
         if (sample == 0) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
         if (hit) {
             eye_hits++;
@@ -1559,7 +1560,7 @@ struct ShadeK { static constexpr KernelFn fn = shade_kernel<C, PO, F, I, kFused,
 
 // defined in mrt_frame.hip: the one-point-light frame / shade kernels at an
 // occupancy target w; pow: a Blinn material with specExp != 1
-KernelFn pick_frame1(int w, bool c, bool f, bool pow, bool ln);
+KernelFn pick_frame1(int w, bool c, bool f, bool pow, int walk);
 KernelFn pick_shade1(int w, bool c, bool f, bool pow);
 // defined in mrt_rec.hip: the fused chain kernels (rec 1: reflection / refraction,
 // 2: + path tracing) and the adaptive supersampling kernels (any rec)

@@ -707,10 +707,11 @@ class Scene:
 
     def walk_info(self):
         """The walk of this scene's last one-light frame: {"lds_nodes": 1 (LDS top-node walk),
-        0 (plain), -1 (none yet)}."""
-        ln = C.c_int32()
-        check(lib().mrt_scene_walk_info(self.handle, C.byref(ln)), "walk_info")
-        return {"lds_nodes": int(ln.value)}
+        0 (plain), -1 (none yet); "walk_exits": 1 or 2 (the walk loop's form, picked per scene
+        by a probe), -1 (not probed yet)}."""
+        ln, wx = C.c_int32(-1), C.c_int32(-1)
+        check(lib().mrt_scene_walk_info(self.handle, C.byref(ln), C.byref(wx)), "walk_info")
+        return {"lds_nodes": int(ln.value), "walk_exits": int(wx.value)}
 
     def stats(self):
         st = _lib.mrt_stats()

@@ -199,7 +199,7 @@ def load():
     L.mrt_scene_blas_info.argtypes = [C.c_void_p, C.c_int32, _ip, _ip, _ip]
     L.mrt_scene_blas_export.argtypes = [C.c_void_p, C.c_int32, _fp, _ip, _fp, _ip]
     if hasattr(L, "mrt_scene_walk_info"):
-        L.mrt_scene_walk_info.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+        L.mrt_scene_walk_info.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     if hasattr(L, "mrt_debug_libm"):   # (absent from round-4 builds loaded for A/B runs via MRT_LIB)
         L.mrt_debug_libm.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
     L.mrt_rcp_nr.argtypes = [C.c_float]
