@@ -705,7 +705,9 @@ def main():
     # latency evidence of the pass's longest kernel (SQ wave-state shares, VALU busy,
     # L2 requests per vector load): why neither bandwidth roofline binds
     latency = None
-    for kname, ent in sorted(((prof or {}).get("kernels") or {}).items(), key=lambda kv: -kv[1].get("avg_us", 0)):
+    # (the pass's most-dispatched kernel: the timed instantiation, not the walk-exit probe's few launches)
+    for kname, ent in sorted(((prof or {}).get("kernels") or {}).items(),
+                             key=lambda kv: (-kv[1].get("dispatches", 0), -kv[1].get("avg_us", 0))):
         if kname in (ppass.get("kernels") or []) and ent.get("latency"):
             latency = dict(ent["latency"], kernel=kname)
             if ent.get("code_object"):
