@@ -356,7 +356,9 @@ __global__ void __launch_bounds__(kWG, MINW) chain_trace_kernel(RenderParams P) 
     const uint8_t* nrays = P.nrays + lofs(P, k - 1);
     const uint32_t np = (uint32_t)P.num_paths;
     unsigned long long wave_steps = 0;
-    auto chunk = [&](uint32_t c) {   // one 64-slot chunk, one ray per lane
+    // (always inlined: as a call from the two schedules below it takes the RenderParams out
+    // of the kernarg segment, a 2288-B private copy per lane)
+    auto chunk = [&](uint32_t c) __attribute__((always_inline)) {   // one 64-slot chunk, one ray per lane
         const uint32_t n0 = st.nodes;
         if (c < chA) {   // closest hit of entry e
             uint32_t e = (c << 6) + (uint32_t)lane;

@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
         return e64 < n_rays && e < nr32 && e - px * m < (uint32_t)P.nrays[px];
     };
     auto slot_at = [&](size_t c) -> size_t { return perm ? (size_t)perm[c] : c; };
-    auto trace_one = [&](size_t e) {
+    auto trace_one = [&](size_t e) __attribute__((always_inline)) {   // (inlined: see chain_trace_kernel)
         const float4 o = P.ray_o[e], d = P.ray_d[e];
         const DRay r = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
         DHit h{o.w, 0.f, 0.f, -1};

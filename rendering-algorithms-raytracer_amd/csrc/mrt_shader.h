@@ -686,7 +686,9 @@ struct Shader {
         return normalized(add(add(scale(u, c * sqrte2), scale(v, s * sqrte2)), scale(N, sqrt1_e2)), rsqT);
     }
 
-    __device__ v3 env_color(const DevMaterial& M, v3 d) { return mat_env(P, M, d); }
+    // (forced inline: as a call it takes the Shader's reference to the kernel's RenderParams
+    // out of the kernarg segment -- a 2288-B private copy per lane, R3's REC kernels 2x slower)
+    __device__ __forceinline__ v3 env_color(const DevMaterial& M, v3 d) { return mat_env(P, M, d); }
 
     // the camera ray's history: [1, 1.001, (a level-0 refraction push)] and its index
     struct IorCam {
@@ -1056,7 +1058,7 @@ struct TileSched {
     const RenderParams& P;
     int mode, cur, step, end, home, probe, band;
     uint32_t deq_ticks = 0;  // count mode: wall-clock ticks of the last dequeue
-    __device__ TileSched(const RenderParams& P_, int wave, int) : P(P_) {
+    __device__ __forceinline__ TileSched(const RenderParams& P_, int wave, int) : P(P_) {
         mode = P.sched;
         home = blockIdx.x & 7;
         probe = 0;
@@ -1074,7 +1076,7 @@ struct TileSched {
             end = P.n_tiles;
         }
     }
-    __device__ int dequeue() {
+    __device__ __forceinline__ int dequeue() {
         int item = -1;
         const uint64_t q0 = P.wave_log ? wall_clock64() : 0;
         if (lane_id() == 0) {
@@ -1093,11 +1095,11 @@ struct TileSched {
     }
     // items are wave-uniform: readfirstlane puts them (and the frame / camera
     // lookups derived from them) in SGPRs
-    __device__ int first() {
+    __device__ __forceinline__ int first() {
         if (mode >= 2) return __builtin_amdgcn_readfirstlane(dequeue());
         return __builtin_amdgcn_readfirstlane(cur < end ? cur : -1);
     }
-    __device__ int next(int item) {
+    __device__ __forceinline__ int next(int item) {
         if (mode >= 2) return __builtin_amdgcn_readfirstlane(dequeue());
         item += step;
         return __builtin_amdgcn_readfirstlane(item < end ? item : -1);
@@ -1408,7 +1410,7 @@ __global__ void __launch_bounds__(kWG, MINW) adaptive_kernel(RenderParams P) {
     v3 result = mk(0, 0, 0), cur = mk(0, 0, 0);
     int level = 1, i = 0, j = 0;
     // start pixel `lane_` of work item `item` (false: outside the frame)
-    auto start = [&](int item, int lane_) {
+    auto start = [&](int item, int lane_) __attribute__((always_inline)) {
         if (!item_pixel(P, item, lane_, x, y, slot)) return false;
         f = item_frame(P, item);
         seed = P.seed + (uint32_t)f;
@@ -1420,7 +1422,9 @@ __global__ void __launch_bounds__(kWG, MINW) adaptive_kernel(RenderParams P) {
         return true;
     };
     // one eye ray of the lane's pixel; true when the pixel is done (written)
-    auto step = [&]() {
+    // (always inlined: called from both schedules below, it became a call, and a call takes
+    // the RenderParams out of the kernarg segment -- 2288 B of scratch per lane, A3 2x slower)
+    auto step = [&]() __attribute__((always_inline)) {
         const CamParams& cam = P.cam[f];
         float x0 = 0.5f, x1 = 0.5f, y0 = 0.5f, y1 = 0.5f;
         if (level > 1) {
