@@ -51,6 +51,8 @@ PROFILE_FILE = os.path.join(ROOT, "profiles", "r05_profile.json")
 CPU_CAL_FILE = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
 # kernel traces of the driver-settings runs (tools/step_trace.py): busy union per timed step
 STEP_TRACE_FILE = os.path.join(ROOT, "profiles", "r05_steptrace.json")
+# N > 1 split: frames of the camera path per step when --frames-per-launch is not given
+DEFAULT_FPL = 1
 
 
 def parse():
@@ -81,11 +83,15 @@ def parse():
                     help="--share model: assumed effective RCCL point-to-point rate per xGMI link and direction (GB/s)")
     ap.add_argument("--xgmi-lat-us", type=float, default=15.0, help="--share model: assumed per-gather latency (us)")
     ap.add_argument("--size", default="", help="WxH override of the config's frame size (exploration runs only)")
+    ap.add_argument("--assemble", choices=["ipc", "gather"], default="ipc",
+                    help="N > 1 split (and --share): ipc = every rank writes its buckets straight into rank 0's frames "
+                         "through an IPC mapping (mrt_ipc_open) and one barrier per step marks the frame whole, no gather "
+                         "or unpack (falls back to gather when a rank cannot map them); gather = packed float tiles, one "
+                         "RCCL gather to rank 0 and its unpack")
     ap.add_argument("--frames-per-launch", type=int, default=0,
-                    help="strong split (N > 1, and --share): frames of the same camera each rank renders in ONE launch "
-                         "per step (its buckets of all of them dealt id mod N) and gathers at once; amortises the "
-                         "per-launch tail of a 1/N share (1..16; 0 = 8: C3's 1/8 share 0.0912 -> 0.0599 ms per frame, "
-                         "profiles/r05_c3_share_model_k*.json)")
+                    help="strong split (N > 1, and --share): frames per step, the first K frames of the config's "
+                         "camera path (distinct cameras; frame 0 = the headline camera), each rank's buckets of all of "
+                         "them rendered in ONE launch; K > 1 is reported as batched (1..16; 0 = DEFAULT_FPL)")
     ap.add_argument("--latency-frames", type=int, default=5,
                     help="single frames (nothing else in flight) timed after the run for launch_ms / frame latency")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
@@ -385,7 +391,7 @@ def main():
     # secondary key of the split line.
     # (--path batch at N = 1 runs the split path on one GPU: same pipeline, N = 1)
     split = (world > 1 and args.split == "frame") or (world == 1 and args.path == "batch")
-    fpl = max(1, min(16, args.frames_per_launch or 8))
+    fpl = max(1, min(16, args.frames_per_launch or DEFAULT_FPL))
     n_frames = (fpl if split else 1) if (world == 1 or split) else (args.frames or min(world, 16))
     bx, by = (W + 31) // 32, (H + 31) // 32
     bpf = bx * by
@@ -400,19 +406,18 @@ def main():
 
     depth = max(1, args.inflight)
 
-    def make_pipe(nf, float_tiles, nsplit=None, srank=None, pipe_streams=None, share_unpack="own", same_camera=False):
+    def make_pipe(nf, float_tiles, nsplit=None, srank=None, pipe_streams=None, share_unpack="own"):
         """This rank's share of an nf-frame step (items id mod N), its render /
         unpack closures and the gather pipeline over `depth` buffers and streams
         (--inflight).  nsplit / srank: the share of rank srank of an nsplit-way
         split rendered without the gather (bench.py --share); share_unpack "none":
         no unpack (a rank > 0 of the split only renders and sends), "full": rank 0's
         unpack of all nsplit shares' tiles each step (its buffers hold nsplit shares).
-        same_camera: the nf frames are the headline camera's (strong split batched over
-        --frames-per-launch frames), not a camera path."""
+        The nf frames are the first nf frames of the config's camera path (frame 0 is
+        the headline camera)."""
         nsplit = world if nsplit is None else nsplit
         srank = rank if srank is None else srank
-        cams_ = [cam] * nf if (nf == 1 or same_camera) else [_camera(c) for c in scenes.camera_path(cfg["camera"], nf)]
-        cc = (_lib.mrt_camera * nf)(*[c._c() for c in cams_])
+        cc = path_cameras(nf)
         mine, all_ids, per = tiles_mod.split_items(bpf * nf, nsplit, srank)
         shares = 1
         if nsplit != world and share_unpack != "full":   # one share on its own: its unpadded items are the whole "gathered" buffer
@@ -450,6 +455,92 @@ def main():
         torch.cuda.synchronize()
         pipe.out_f, pipe.out_8 = out_f, out_8   # rank 0's assembled frames, one per buffer
         return pipe, render, items, mine, out_f
+
+    def path_cameras(nf):
+        """mrt_camera[nf]: the first nf frames of the config's camera path (frame 0 = the headline camera)."""
+        cams_ = [cam] if nf == 1 else [_camera(c) for c in scenes.camera_path(cfg["camera"], nf)]
+        return (_lib.mrt_camera * nf)(*[c._c() for c in cams_])
+
+    def make_ipc_pipe(nf, nsplit=None, srank=None, pipe_streams=None):
+        """The split with direct writes (--assemble ipc): rank 0 owns `depth` frame buffers
+        (nf frames each, float + 8-bit), exports them (mrt_ipc_export), every rank maps
+        them (mrt_ipc_open) and renders its buckets of each step straight into buffer
+        k % depth (mrt_render_batch_frames_async); one stream-ordered all-reduce of one
+        int per step is the frame-end barrier (tiles.FramePipeline).  nsplit / srank: one
+        rank's share rendered alone on this GPU into local frames (--share: no barrier).
+        Returns (pipe, render(b, opts), mine, frames) or raises when a rank cannot map."""
+        nsplit = world if nsplit is None else nsplit
+        srank = rank if srank is None else srank
+        cc = path_cameras(nf)
+        mine = tiles_mod.rank_buckets(bpf * nf, nsplit, srank)
+        items = torch.tensor(mine, dtype=torch.int32, device="cuda")
+        alone = nsplit != world
+        owner = alone or rank == 0
+        own = [(torch.empty(nf * H * W * 3, dtype=torch.float32, device="cuda"),
+                torch.empty(nf * H * W * 3, dtype=torch.uint8, device="cuda")) for _ in range(depth)] if owner else None
+        ptrs, opened, err = [], [], ""
+        if alone or world == 1:
+            ptrs = [(f.data_ptr(), f8.data_ptr()) for f, f8 in own]
+        else:
+            obj = [None]
+            if rank == 0:
+                try:
+                    hs = []
+                    for f, f8 in own:
+                        for t in (f, f8):
+                            h = _lib.mrt_ipc_handle()
+                            _lib.check(L.mrt_ipc_export(C.c_void_p(t.data_ptr()), C.byref(h)), "ipc export")
+                            hs.append(bytes(h))
+                    obj = [hs]
+                except Exception as e:   # reported through the agreement below
+                    err = repr(e)
+            dist.broadcast_object_list(obj, src=0)
+            try:
+                if rank == 0:
+                    ptrs = [(f.data_ptr(), f8.data_ptr()) for f, f8 in own]
+                elif obj[0] is None:
+                    err = "rank 0 could not export its frames"
+                else:
+                    for i in range(depth):
+                        pair = []
+                        for j in range(2):
+                            h = _lib.mrt_ipc_handle.from_buffer_copy(obj[0][2 * i + j])
+                            p = C.c_void_p()
+                            _lib.check(L.mrt_ipc_open(C.byref(h), dev, C.byref(p)), "ipc open")
+                            pair.append(p.value)
+                            opened.append(p.value)
+                        ptrs.append(tuple(pair))
+            except Exception as e:
+                err = repr(e)
+            # every rank takes the same decision: all mapped, or all fall back
+            ok = torch.tensor([0.0 if err else 1.0], dtype=torch.float64, device="cuda")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if ok.item() < 1.0:
+                for p in opened:
+                    L.mrt_ipc_close(C.c_void_p(p))
+                raise RuntimeError(err or "another rank could not map rank 0's frames")
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+        def render(b, o=opts):
+            _lib.check(L.mrt_render_batch_frames_async(scene.handle, cc, nf, C.byref(o), items.data_ptr(), len(mine),
+                                                       ptrs[b][0], ptrs[b][1],
+                                                       torch.cuda.current_stream().cuda_stream), "render frames")
+
+        def barrier():
+            if alone or world == 1:
+                return None
+            return dist.all_reduce(flag, async_op=True)
+
+        pipe = tiles_mod.FramePipeline(world if not alone else 1, rank if not alone else 0, render, barrier, None,
+                                       streams=pipe_streams or [torch.cuda.Stream() for _ in range(depth)])
+        for b in range(depth):   # per-stream scratch allocated before any timing
+            with torch.cuda.stream(pipe.streams[b]):
+                render(b)
+        torch.cuda.synchronize()
+        if not alone and world > 1:
+            dist.barrier()
+        pipe.own, pipe.opened, pipe.items_n = own, opened, len(mine)
+        return pipe, render, mine, own
 
     def count_rays(render_count):
         """Rays of one step over all ranks from an instrumented launch (+ this rank's stats)."""
@@ -553,8 +644,9 @@ def main():
                 "compared": ("float + 8-bit" if t_f is not None else "8-bit") + " RGB of the last timed step's frame"}
 
     adaptive = bool(cfg.get("subdivs")) and max(cfg["subdivs"][:2]) > 1
+    assemble = None
     if args.share:
-        share_mode(args, dict(scene=scene, cfg=cfg, W=W, H=H, bpf=bpf, L=L, _lib=_lib, tiles_mod=tiles_mod, torch=torch, np=np, make_pipe=make_pipe, count_rays=count_rays, timed=timed, frame_step=frame_step, streams=streams, frame=frame, frame8=frame8, opts=opts, opts_count=opts_count, camc=camc, adaptive=adaptive, inflight=inflight), [int(x) for x in args.share.split(",") if x.strip()])
+        share_mode(args, dict(scene=scene, cfg=cfg, W=W, H=H, bpf=bpf, L=L, _lib=_lib, tiles_mod=tiles_mod, torch=torch, np=np, make_pipe=make_pipe, make_ipc_pipe=make_ipc_pipe, count_rays=count_rays, timed=timed, frame_step=frame_step, streams=streams, frame=frame, frame8=frame8, opts=opts, opts_count=opts_count, camc=camc, adaptive=adaptive, inflight=inflight), [int(x) for x in args.share.split(",") if x.strip()])
         return
     if use_frame_path:
         # setup: every in-flight stream renders once, so libmrt's per-stream scratch
@@ -571,42 +663,72 @@ def main():
         last = (nstep[0] - 1) % inflight
         frame_check = check_timed_frame(frame[last], frame8[last])
     else:
-        pipe, render, items, mine, _ = make_pipe(n_frames, float_tiles=split, same_camera=split)
-        st, (shadow_total, eye_total, second_total) = count_rays(lambda: render(items, pipe.tiles[0], opts_count))
-        elapsed = timed(pipe.step, pipe.flush, args.steps)
-        last = (pipe.k - 1) % pipe.depth
-        frame_check = check_timed_frame(pipe.out_f[last] if split else None, pipe.out_8[last]) \
-            if rank == 0 and (n_frames == 1 or split) else None
+        assemble = "gather"
+        if split and args.assemble == "ipc":
+            try:
+                pipe, render_b, mine, own = make_ipc_pipe(n_frames)
+                assemble = "ipc"
+            except Exception as e:   # every rank took the same decision (make_ipc_pipe)
+                assemble = f"gather (ipc unavailable: {e})"
+                progress(f"IPC frame mapping failed ({e}); the split gathers tiles instead")
+        if assemble == "ipc":
+            def render_one(o=opts):
+                render_b(0, o)
+            items = None
+            st, (shadow_total, eye_total, second_total) = count_rays(lambda: render_one(opts_count))
+            elapsed = timed(pipe.step, pipe.flush, args.steps)
+            last = (pipe.k - 1) % pipe.depth
+            frame_check = check_timed_frame(own[last][0], own[last][1]) if rank == 0 else None
+        else:
+            pipe, render, items, mine, _ = make_pipe(n_frames, float_tiles=split)
+
+            def render_one(o=opts):
+                render(items, pipe.tiles[0], o)
+            st, (shadow_total, eye_total, second_total) = count_rays(lambda: render_one(opts_count))
+            elapsed = timed(pipe.step, pipe.flush, args.steps)
+            last = (pipe.k - 1) % pipe.depth
+            frame_check = check_timed_frame(pipe.out_f[last] if split else None, pipe.out_8[last]) \
+                if rank == 0 and (n_frames == 1 or split) else None
     shadow_mine, eye_mine, second_mine = st["shadow_rays"], (st["primary_rays"] if adaptive else 0), st["secondary_rays"]
     primary_total = eye_total if adaptive else n_frames * W * H
     rays_per_step = primary_total + shadow_total + second_total      # all frames of the batch, all ranks
     hits_px = st["primary_hits"]
 
-    # N > 1: per-rank render and gather times of the split (median of 5, each
-    # alone: render = HIP events of one launch on this rank's stream, gather =
-    # one RCCL gather of the tile buffer between barriers), and the weak-scaling
-    # batch of N frames per step as the secondary key
+    # N > 1: per-rank render and assembly times of the split (median of 5, each
+    # alone: render = HIP events of one launch on this rank's stream; ipc: one frame-end
+    # barrier (all-reduce of one int) between barriers, gather: one RCCL gather of the
+    # tile buffer), and the weak-scaling batch of N frames per step as the secondary key
     split_times, weak = None, None
     if world > 1 and split:
         r_ms, g_ms = [], []
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
         for _ in range(5):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             dist.barrier()
             e0.record()
-            render(items, pipe.tiles[0])
+            render_one()
             e1.record()
             torch.cuda.synchronize()
             r_ms.append(e0.elapsed_time(e1))
             dist.barrier()
             tg = time.perf_counter()
-            dist.gather(pipe.tiles[0], list(pipe.recv[0].chunk(world)) if rank == 0 else None, dst=0)
+            if assemble == "ipc":
+                dist.all_reduce(flag)
+            else:
+                dist.gather(pipe.tiles[0], list(pipe.recv[0].chunk(world)) if rank == 0 else None, dst=0)
             torch.cuda.synchronize()
             g_ms.append((time.perf_counter() - tg) * 1e3)
         t_ = torch.tensor([float(np.median(r_ms)), float(np.median(g_ms))], dtype=torch.float64, device="cuda")
         dist.all_reduce(t_, op=dist.ReduceOp.MAX)
-        split_times = {"render_ms_max_rank": round(t_[0].item(), 4), "gather_ms": round(t_[1].item(), 4),
-                       "gather_bytes_per_rank": int(pipe.tiles[0].numel() * 4)}
+        if assemble == "ipc":
+            split_times = {"render_ms_max_rank": round(t_[0].item(), 4), "barrier_ms": round(t_[1].item(), 4),
+                           "assemble": "ipc: every rank's kernel stores its buckets' pixels into rank 0's frames "
+                                       "(mrt_ipc_open mapping, xGMI); no gather, no unpack",
+                           "remote_bytes_per_rank_max": int(max(0, len(mine)) * 1024 * 15)}
+        else:
+            split_times = {"render_ms_max_rank": round(t_[0].item(), 4), "gather_ms": round(t_[1].item(), 4),
+                           "assemble": assemble, "gather_bytes_per_rank": int(pipe.tiles[0].numel() * 4)}
         nf_w = args.frames or min(world, 16)
         wpipe, wrender, witems, _, _ = make_pipe(nf_w, float_tiles=False)
         _, (wsh, weye, wsec) = count_rays(lambda: wrender(witems, wpipe.tiles[0], opts_count))
@@ -628,12 +750,17 @@ def main():
         if use_frame_path:
             frame_step(opts, serial=True)
         else:
-            render(items, pipe.tiles[0])
+            render_one()
         torch.cuda.synchronize()
         lat_ms.append((time.perf_counter() - t1) * 1e3)
         s2 = scene.stats()
         prim_ms.append(s2["primary_ms"])
         shade_ms.append(s2["shade_ms"])
+    if split and world > 1 and assemble == "ipc":   # unmap rank 0's frames once every rank is done with them
+        torch.cuda.synchronize()
+        dist.barrier()
+        for p_ in pipe.opened:
+            L.mrt_ipc_close(C.c_void_p(p_))
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -795,11 +922,15 @@ def main():
                    "frames_in_flight": inflight,
                    "parallelism": "single GPU, whole frame" if use_frame_path else
                    ((f"one {W}x{H} frame per step" if n_frames == 1 else
-                     f"{n_frames} {W}x{H} frames of one camera per step, rendered by each rank in ONE launch "
-                     f"(--frames-per-launch)") +
-                    f" split over {world} GPUs: its 32x32 buckets dealt id mod {world} "
-                    f"(src/Scene.cpp:90-174), float32 tiles, one RCCL gather of the framebuffer(s) to rank 0 per step, "
-                    f"consecutive steps double-buffered" if split else
+                     f"batched: {n_frames} {W}x{H} frames of the camera path per step (distinct cameras), rendered "
+                     f"by each rank in ONE launch (--frames-per-launch)") +
+                    f" split over {world} GPUs: its 32x32 buckets dealt id mod {world} (src/Scene.cpp:90-174), " +
+                    ("each rank's kernel stores its pixels straight into rank 0's frames through an IPC mapping, one "
+                     "frame-end barrier (all-reduce of one int) per step, no gather or unpack"
+                     if assemble == "ipc" else
+                     "float32 tiles, one RCCL gather of the framebuffer(s) to rank 0 per step" +
+                     ("" if assemble == "gather" else f" [{assemble}]")) +
+                    f", consecutive steps pipelined over {depth} buffers" if split else
                     f"{n_frames}-frame camera path per step, 32x32 buckets dealt id mod {world}, "
                     f"one RCCL gather of 8-bit tiles per step (double-buffered)")},
         # The traversal is bound by latency along each wave's dependent chain
@@ -877,10 +1008,24 @@ class _HostDist:
     def barrier(self):
         self._d.barrier()
 
-    def all_reduce(self, t, op=None):
+    def all_reduce(self, t, op=None, async_op=False):
+        if t.is_cuda:   # stream order: the collective follows this rank's enqueued work
+            self._t.cuda.current_stream().synchronize()
         h = t.cpu()
         self._d.all_reduce(h, op=op if op is not None else self._d.ReduceOp.SUM)
         t.copy_(h)
+        return self._done() if async_op else None
+
+    def broadcast_object_list(self, obj, src=0):
+        self._d.broadcast_object_list(obj, src=src)
+
+    @staticmethod
+    def _done():
+        class _Done:
+            @staticmethod
+            def wait():
+                return True
+        return _Done()
 
     def gather(self, t, outs=None, dst=0, async_op=False):
         if t.is_cuda:
@@ -907,20 +1052,26 @@ def share_mode(args, E, widths):
 
     The whole frame first (the N = 1 frame path with --inflight streams); then, per
     split width N, every rank r's share of buckets (id mod N == r) rendered alone
-    through the split pipeline (--inflight buffers and streams, no gather): ranks
-    r > 0 render into float tiles only; rank 0 renders its share and unpacks all N
-    shares' tiles into the frame every step, as it does after the gather.  The
-    N-GPU step is modeled as
-        max(rank 0's render + full unpack, slowest rank > 0, gather)
-    with gather = latency + (one rank's float tiles) / (per-link xGMI rate): rank 0
-    receives the N - 1 other shares over N - 1 point-to-point links at once, and the
-    pipeline overlaps step k's gather with step k + 1's renders.  The xGMI rate and
+    through the split pipeline (--inflight buffers and streams).
+
+    --assemble ipc (default): every share renders straight into frames
+    (mrt_render_batch_frames_async), as a rank does into rank 0's mapped frames; no
+    unpack anywhere.  The N-GPU step is modeled as
+        max(slowest rank's render, one rank's frame bytes / per-link xGMI rate,
+            barrier latency / (buffers - 1))
+    -- the kernel stores of rank r > 0 cross one xGMI link into rank 0 (each rank its
+    own link), and the per-step barrier of step k only gates the render of step
+    k + buffers - 1.  --assemble gather: ranks r > 0 render into float tiles; rank 0
+    renders its share and unpacks all N shares' tiles every step, as after the
+    gather; step = max(rank 0's render + full unpack, slowest rank > 0, gather) with
+    gather = latency + one rank's float tiles / per-link rate.  The xGMI rate and
     latency are ASSUMED (--xgmi-gbs, --xgmi-lat-us); nothing here ran on more than
-    one GPU.  --frames-per-launch K: each share renders K frames of the camera in one
-    launch and gathers them at once (per-frame times reported)."""
+    one GPU.  --frames-per-launch K: each share renders the first K frames of the
+    camera path in one launch per step (per-frame times reported)."""
     torch, np, C_ = E["torch"], E["np"], C
     scene, L, _lib, tiles_mod = E["scene"], E["L"], E["_lib"], E["tiles_mod"]
     W, H, bpf = E["W"], E["H"], E["bpf"]
+    ipc = args.assemble == "ipc"
     for i in range(E["inflight"]):
         _lib.check(L.mrt_render_frame_async(scene.handle, C_.byref(E["camc"][0]), C_.byref(E["opts"]),
                                             E["frame"][i].data_ptr(), E["frame8"][i].data_ptr(),
@@ -932,23 +1083,35 @@ def share_mode(args, E, widths):
     frame_ms = e_full / args.steps * 1e3
     out = {"metric": f"modeled strong-split curve from single-GPU share measurements [{args.config}]",
            "config": {"workload": E["cfg"]["name"], "config": args.config, "width": W, "height": H,
-                      "buckets": bpf, "inflight": E["inflight"], "steps": args.steps, "warmup": args.warmup},
+                      "buckets": bpf, "inflight": E["inflight"], "steps": args.steps, "warmup": args.warmup,
+                      "assemble": args.assemble},
            "frame": {"ms_per_step": round(frame_ms, 4), "mray_s": round(rays_full / (frame_ms * 1e-3) / 1e6, 1)},
-           "assumptions": {"xgmi_gbs_per_link": args.xgmi_gbs, "gather_latency_us": args.xgmi_lat_us,
+           "assumptions": {"xgmi_gbs_per_link": args.xgmi_gbs,
+                           ("barrier_latency_us" if ipc else "gather_latency_us"): args.xgmi_lat_us,
                            "note": "xGMI rate and latency assumed, not measured: this box has one GPU; every "
                                    "other number in this line is measured on it"},
            "shares": {}}
     # one set of streams for every share pipeline (libmrt keeps scratch per stream, at most 16 per scene)
-    share_streams = [torch.cuda.Stream() for _ in range(max(1, args.inflight))]
-    K = max(1, min(16, args.frames_per_launch or 8))   # frames per share launch (same camera)
+    share_streams = [torch.cuda.Stream() for _ in range(max(2, args.inflight))]
+    K = max(1, min(16, args.frames_per_launch or DEFAULT_FPL))   # frames per share launch (camera path)
     out["config"]["frames_per_launch"] = K
+    bxs = (W + 31) // 32
     for N in widths:
         per_rank = []
         for r in range(N):
-            pipe, render, items, mine, _ = E["make_pipe"](K, True, nsplit=N, srank=r, pipe_streams=share_streams,
-                                                          share_unpack="full" if r == 0 else "none", same_camera=True)
-            _, (sh, eye, sec) = E["count_rays"](lambda: render(items, pipe.tiles[0], E["opts_count"]))
-            px = sum(min(32, W - (b % bpf % ((W + 31) // 32)) * 32) * min(32, H - (b % bpf // ((W + 31) // 32)) * 32)
+            if ipc:
+                pipe, render_b, mine, _ = E["make_ipc_pipe"](K, nsplit=N, srank=r, pipe_streams=share_streams)
+
+                def render_one(o=E["opts"]):
+                    render_b(0, o)
+            else:
+                pipe, render, items, mine, _ = E["make_pipe"](K, True, nsplit=N, srank=r, pipe_streams=share_streams,
+                                                              share_unpack="full" if r == 0 else "none")
+
+                def render_one(o=E["opts"]):
+                    render(items, pipe.tiles[0], o)
+            _, (sh, eye, sec) = E["count_rays"](lambda: render_one(E["opts_count"]))
+            px = sum(min(32, W - (b % bpf % bxs) * 32) * min(32, H - (b % bpf // bxs) * 32)
                      for b in mine)   # over the K frames of a launch
             e = E["timed"](pipe.step, pipe.flush, args.steps)
             ms = e / args.steps * 1e3 / K   # per frame
@@ -965,7 +1128,7 @@ def share_mode(args, E, widths):
             alone = []
             for _ in range(5):
                 e0.record()
-                render(items, pipe.tiles[0])
+                render_one()
                 e1.record()
                 torch.cuda.synchronize()
                 alone.append(e0.elapsed_time(e1) / K)
@@ -974,36 +1137,46 @@ def share_mode(args, E, widths):
                              "launch_alone_ms": round(float(np.median(alone)), 4),
                              "rays": (eye if E["adaptive"] else px) + sh + sec})
             del pipe
-        # rank 0's unpack of the whole gathered frame (N ranks' padded float tiles)
-        _, all_ids, per = tiles_mod.split_items(bpf * K, N, 0)
-        ids = torch.tensor(all_ids, dtype=torch.int32, device="cuda")
-        gathered = torch.zeros(len(all_ids) * 1024 * 3, dtype=torch.float32, device="cuda")
-        ff = torch.empty(K * W * H * 3, dtype=torch.float32, device="cuda")
-        f8 = torch.empty(K * W * H * 3, dtype=torch.uint8, device="cuda")
-        un = []
-        for _ in range(7):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(all_ids), gathered.data_ptr(), None, W, H, K,
-                                                ff.data_ptr(), f8.data_ptr(), scene.handle,
-                                                torch.cuda.current_stream().cuda_stream), "unpack")
-            e1.record()
-            torch.cuda.synchronize()
-            un.append(e0.elapsed_time(e1))
-        unpack_ms = float(np.median(un[2:])) / K   # per frame
-        tile_bytes = per * 1024 * 3 * 4                      # one gather: K frames' tiles
-        gather_ms = (args.xgmi_lat_us * 1e-3 + tile_bytes / (args.xgmi_gbs * 1e9) * 1e3) / K   # per frame
-        slow = max(per_rank, key=lambda x: x["ms_per_step"])   # rank 0's line includes its full unpack
-        step_ms = max(slow["ms_per_step"], gather_ms)
-        out["shares"][str(N)] = {
-            "per_rank": per_rank, "slowest_rank_ms": slow["ms_per_step"], "slowest_rank": slow["rank"],
-            "rank0_render_plus_unpack_ms": per_rank[0]["ms_per_step"],
-            "mean_rank_ms": round(sum(x["ms_per_step"] for x in per_rank) / N, 4),
-            "unpack_ms_rank0_alone": round(unpack_ms, 4), "gather_bytes_per_rank": tile_bytes,
-            "gather_ms_model": round(gather_ms, 4), "step_ms_model": round(step_ms, 4),
-            "bound": "render" if slow["ms_per_step"] >= gather_ms else "gather",
-            "predicted_mray_s": round(rays_full / (step_ms * 1e-3) / 1e6, 1),
-            "predicted_speedup": round(frame_ms / step_ms, 3)}
+        slow = max(per_rank, key=lambda x: x["ms_per_step"])
+        if ipc:
+            # rank r > 0's pixels cross its xGMI link as stores: float RGB + RGB8 per pixel, per frame
+            link_b = max(x["pixels"] for x in per_rank[1:]) * 15 / K if N > 1 else 0
+            link_ms = link_b / (args.xgmi_gbs * 1e9) * 1e3
+            bar_ms = args.xgmi_lat_us * 1e-3 / max(1, len(share_streams) - 1) / K
+            step_ms = max(slow["ms_per_step"], link_ms, bar_ms)
+            bound = "render" if step_ms == slow["ms_per_step"] else ("xgmi stores" if step_ms == link_ms else "barrier")
+            rec = {"remote_bytes_per_link_per_frame": int(link_b), "link_ms_model": round(link_ms, 4),
+                   "barrier_ms_model": round(bar_ms, 4)}
+        else:
+            # rank 0's unpack of the whole gathered frame (N ranks' padded float tiles)
+            _, all_ids, per = tiles_mod.split_items(bpf * K, N, 0)
+            ids = torch.tensor(all_ids, dtype=torch.int32, device="cuda")
+            gathered = torch.zeros(len(all_ids) * 1024 * 3, dtype=torch.float32, device="cuda")
+            ff = torch.empty(K * W * H * 3, dtype=torch.float32, device="cuda")
+            f8 = torch.empty(K * W * H * 3, dtype=torch.uint8, device="cuda")
+            un = []
+            for _ in range(7):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                _lib.check(L.mrt_unpack_batch_async(ids.data_ptr(), len(all_ids), gathered.data_ptr(), None, W, H, K,
+                                                    ff.data_ptr(), f8.data_ptr(), scene.handle,
+                                                    torch.cuda.current_stream().cuda_stream), "unpack")
+                e1.record()
+                torch.cuda.synchronize()
+                un.append(e0.elapsed_time(e1))
+            unpack_ms = float(np.median(un[2:])) / K   # per frame
+            tile_bytes = per * 1024 * 3 * 4                      # one gather: K frames' tiles
+            gather_ms = (args.xgmi_lat_us * 1e-3 + tile_bytes / (args.xgmi_gbs * 1e9) * 1e3) / K   # per frame
+            step_ms = max(slow["ms_per_step"], gather_ms)   # rank 0's line includes its full unpack
+            bound = "render" if slow["ms_per_step"] >= gather_ms else "gather"
+            rec = {"rank0_render_plus_unpack_ms": per_rank[0]["ms_per_step"], "unpack_ms_rank0_alone": round(unpack_ms, 4),
+                   "gather_bytes_per_rank": tile_bytes, "gather_ms_model": round(gather_ms, 4)}
+        out["shares"][str(N)] = dict(
+            {"per_rank": per_rank, "slowest_rank_ms": slow["ms_per_step"], "slowest_rank": slow["rank"],
+             "mean_rank_ms": round(sum(x["ms_per_step"] for x in per_rank) / N, 4)}, **rec,
+            step_ms_model=round(step_ms, 4), bound=bound,
+            predicted_mray_s=round(rays_full / (step_ms * 1e-3) / 1e6, 1),
+            predicted_speedup=round(frame_ms / step_ms, 3))
     print(json.dumps(out), flush=True)
 
 

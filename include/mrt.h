@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MRT_ABI_VERSION 9
+#define MRT_ABI_VERSION 10
 
 enum {
     MRT_OK = 0,
@@ -384,6 +384,30 @@ int mrt_render_batch_async(mrt_scene* s, const mrt_camera* cams, int32_t n_cams,
 int mrt_unpack_batch_async(const int32_t* d_items, int32_t n_items, const float* d_tiles, const uint8_t* d_tiles8,
                            int32_t width, int32_t height, int32_t n_frames, float* d_frames, uint8_t* d_frames8,
                            const mrt_scene* s_for_lut, void* stream);
+/* ---- the batch render written straight into frames (ABI 10): the same items and
+ * launches as mrt_render_batch_async, but each pixel goes to its place in n_cams
+ * consecutive W*H frames (frame f at offset f*W*H*3 of d_frames / d_frames8, either
+ * may be NULL, not both); pixels outside the frame and items of frames >= n_cams
+ * write nothing.  With the frames of another process mapped by mrt_ipc_open, every
+ * rank of the multi-GPU split writes its buckets into rank 0's frame directly: the
+ * frame is complete when every rank's launch is (a stream-ordered barrier), with no
+ * gather and no unpack (src/Scene.cpp:90-174's bucket loop, one image for all). */
+int mrt_render_batch_frames_async(mrt_scene* s, const mrt_camera* cams, int32_t n_cams, const mrt_render_opts* opts,
+                                  const int32_t* d_items, int32_t n_items, float* d_frames, uint8_t* d_frames8,
+                                  void* stream);
+/* Device memory shared between processes (hipIpcGetMemHandle / hipIpcOpenMemHandle):
+ * mrt_ipc_export describes the allocation holding d_ptr (any pointer into a device
+ * allocation, e.g. a torch tensor's data) and d_ptr's offset in it; mrt_ipc_open maps
+ * it in this process for `device` (peer access enabled) and returns the same byte;
+ * mrt_ipc_close unmaps a pointer mrt_ipc_open returned.  The handle is plain bytes
+ * (send it to the other ranks over any channel). */
+typedef struct {
+    uint8_t handle[64];
+    uint64_t offset, size;
+} mrt_ipc_handle;
+int mrt_ipc_export(const void* d_ptr, mrt_ipc_handle* out);
+int mrt_ipc_open(const mrt_ipc_handle* h, int device, void** d_ptr);
+int mrt_ipc_close(void* d_ptr);
 /* Whole frame straight into device buffers (N = 1 fast path, no tiles). */
 int mrt_render_frame_async(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts,
                            float* d_rgb, uint8_t* d_rgb8, void* stream);

@@ -616,14 +616,7 @@ __global__ void __launch_bounds__(kWG) chain_finish_kernel(RenderParams P) {
             P.ucol[P.unit_base + u] = make_float4(col.x, col.y, col.z, 0.f);
             continue;
         }
-        if (P.out_rgb) {
-            float* o = P.out_rgb + 3 * U.slot;
-            o[0] = col.x; o[1] = col.y; o[2] = col.z;
-        }
-        if (P.out_rgb8) {
-            uint8_t* o8 = P.out_rgb8 + 3 * U.slot;
-            o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
-        }
+        store_rgb(P, U.slot, col);
     }
 }
 
@@ -756,14 +749,7 @@ __global__ void __launch_bounds__(kWG) chain_fallback_kernel(RenderParams P) {
             P.ucol[P.unit_base + u] = make_float4(col.x, col.y, col.z, 0.f);
             continue;
         }
-        if (P.out_rgb) {
-            float* o = P.out_rgb + 3 * U.slot;
-            o[0] = col.x; o[1] = col.y; o[2] = col.z;
-        }
-        if (P.out_rgb8) {
-            uint8_t* o8 = P.out_rgb8 + 3 * U.slot;
-            o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
-        }
+        store_rgb(P, U.slot, col);
     }
     flush_secondary(P, secondary_total, lane);
     flush_stats<COUNT>(P, st, shadow_total, lane, 0, 0);
@@ -810,14 +796,7 @@ __global__ void __launch_bounds__(kWG) adapt_combine_kernel(RenderParams P) {
             P.next_units[atomicAdd(P.next_cnt, 1u)] = id;
             continue;
         }
-        if (P.out_rgb) {
-            float* o = P.out_rgb + 3 * slot;
-            o[0] = result.x; o[1] = result.y; o[2] = result.z;
-        }
-        if (P.out_rgb8) {
-            uint8_t* o8 = P.out_rgb8 + 3 * slot;
-            o8[0] = map8(P.gamma, result.x); o8[1] = map8(P.gamma, result.y); o8[2] = map8(P.gamma, result.z);
-        }
+        store_rgb(P, slot, result);
     }
 }
 

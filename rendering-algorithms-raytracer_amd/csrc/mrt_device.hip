@@ -2368,9 +2368,10 @@ int mrt_render_frame_async(mrt_scene* s, const mrt_camera* cam, const mrt_render
     return rc;
 }
 
-int mrt_render_batch_async(mrt_scene* s, const mrt_camera* cams, int32_t n_cams, const mrt_render_opts* opts,
-                           const int32_t* d_items, int32_t n_items, float* d_tiles, uint8_t* d_tiles8, void* stream) {
-    if (!s || !cams || !opts || n_items < 0 || (n_items && !d_items) || (!d_tiles && !d_tiles8)) {
+static int render_batch(mrt_scene* s, const mrt_camera* cams, int32_t n_cams, const mrt_render_opts* opts,
+                        const int32_t* d_items, int32_t n_items, float* d_out, uint8_t* d_out8, void* stream,
+                        bool frame_out) {
+    if (!s || !cams || !opts || n_items < 0 || (n_items && !d_items) || (!d_out && !d_out8)) {
         set_error("bad argument"); return MRT_ERR_INVALID;
     }
     if (n_cams < 1 || n_cams > kMaxBatch) { set_error("n_cams must be 1..16"); return MRT_ERR_INVALID; }
@@ -2384,17 +2385,77 @@ int mrt_render_batch_async(mrt_scene* s, const mrt_camera* cams, int32_t n_cams,
         if ((rc = host_camera(cams + f, opts->width, opts->height, P.cam[f]))) return rc;
     P.seed = opts->seed ? opts->seed : 0x5EEDu;
     P.mode = 1;
+    P.frame_out = frame_out ? 1 : 0;
     P.buckets = d_items;
     P.buckets_x = (opts->width + 31) / 32;
     P.buckets_per_frame = P.buckets_x * ((opts->height + 31) / 32);
     P.n_cams = n_cams;
     P.n_tiles = n_items * 16;
-    P.out_rgb = d_tiles;
-    P.out_rgb8 = d_tiles8;
+    P.out_rgb = d_out;
+    P.out_rgb8 = d_out8;
     if (n_items == 0) return MRT_OK;
     rc = launch_render(S, P, (size_t)n_items * 1024, opts->count_visits != 0, (hipStream_t)stream, opts->want_hits != 0);
     S.last.primary_rays = 0;
     return rc;
+}
+
+int mrt_render_batch_async(mrt_scene* s, const mrt_camera* cams, int32_t n_cams, const mrt_render_opts* opts,
+                           const int32_t* d_items, int32_t n_items, float* d_tiles, uint8_t* d_tiles8, void* stream) {
+    return render_batch(s, cams, n_cams, opts, d_items, n_items, d_tiles, d_tiles8, stream, false);
+}
+
+int mrt_render_batch_frames_async(mrt_scene* s, const mrt_camera* cams, int32_t n_cams, const mrt_render_opts* opts,
+                                  const int32_t* d_items, int32_t n_items, float* d_frames, uint8_t* d_frames8,
+                                  void* stream) {
+    return render_batch(s, cams, n_cams, opts, d_items, n_items, d_frames, d_frames8, stream, true);
+}
+
+// ---- device memory shared between processes (the multi-GPU split's frame assembly)
+int mrt_ipc_export(const void* d_ptr, mrt_ipc_handle* out) {
+    if (!d_ptr || !out) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    HIP_OK(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)d_ptr));
+    hipIpcMemHandle_t h;
+    HIP_OK(hipIpcGetMemHandle(&h, (void*)base));
+    static_assert(sizeof(h) <= sizeof(out->handle), "hipIpcMemHandle_t does not fit mrt_ipc_handle");
+    memset(out, 0, sizeof(*out));
+    memcpy(out->handle, &h, sizeof(h));
+    out->offset = (uint64_t)((const char*)d_ptr - (const char*)base);
+    out->size = (uint64_t)size;
+    return MRT_OK;
+}
+
+static std::mutex g_ipc_mu;
+static std::vector<std::pair<void*, void*>> g_ipc_maps;   // (pointer handed out, mapping base)
+
+int mrt_ipc_open(const mrt_ipc_handle* h, int device, void** d_ptr) {
+    if (!h || !d_ptr || h->offset > h->size) { set_error("bad argument"); return MRT_ERR_INVALID; }
+    HIP_OK(hipSetDevice(device));
+    hipIpcMemHandle_t hh;
+    memcpy(&hh, h->handle, sizeof(hh));
+    void* base = nullptr;
+    HIP_OK(hipIpcOpenMemHandle(&base, hh, hipIpcMemLazyEnablePeerAccess));
+    *d_ptr = (char*)base + h->offset;
+    std::lock_guard<std::mutex> g(g_ipc_mu);
+    g_ipc_maps.emplace_back(*d_ptr, base);
+    return MRT_OK;
+}
+
+int mrt_ipc_close(void* d_ptr) {
+    void* base = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_ipc_mu);
+        for (size_t i = 0; i < g_ipc_maps.size(); i++)
+            if (g_ipc_maps[i].first == d_ptr) {
+                base = g_ipc_maps[i].second;
+                g_ipc_maps.erase(g_ipc_maps.begin() + (long)i);
+                break;
+            }
+    }
+    if (!base) { set_error("not a pointer from mrt_ipc_open"); return MRT_ERR_INVALID; }
+    HIP_OK(hipIpcCloseMemHandle(base));
+    return MRT_OK;
 }
 
 int mrt_render_buckets_async(mrt_scene* s, const mrt_camera* cam, const mrt_render_opts* opts, const int32_t* d_buckets,

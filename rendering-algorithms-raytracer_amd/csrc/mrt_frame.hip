@@ -93,17 +93,6 @@ __device__ __forceinline__ v3 shade1_hit(const RenderParams& P, const Trav& T, T
     return add(mk(0, 0, 0), sh);
 }
 
-__device__ __forceinline__ void write_pixel(const RenderParams& P, size_t slot, v3 col) {
-    if (P.out_rgb) {
-        float* o = P.out_rgb + 3 * slot;
-        o[0] = col.x; o[1] = col.y; o[2] = col.z;
-    }
-    if (P.out_rgb8) {
-        uint8_t* o8 = P.out_rgb8 + 3 * slot;
-        o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
-    }
-}
-
 // Kernel 2, specialised for one point light and num_paths == 1: shade1_hit of
 // every pixel's hit record (the two-launch path; frame1_kernel fuses both).
 template <bool COUNT, bool FAST, int MINW, bool POW>
@@ -142,7 +131,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
             col = shade1_hit<COUNT, FAST, POW>(P, T, st, make_ray(er.o, er.d), hv.x, hv.y, hv.z, prim, rcpT, rsqT, shadow_total);
         }
         item_pixel(P, item, lane, x, y, slot);
-        write_pixel(P, slot, col);
+        store_rgb(P, slot, col);
     }
     flush_stats<COUNT, false>(P, st, shadow_total, lane, t0, ntiles);
 }
@@ -207,7 +196,7 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
             const RenderParams& PC = reload_params();   // outputs
             item_pixel(PC, item, lane_id(), x, y, slot);   // recompute: keeps it out of the traversals' live set
             if (PC.hits) PC.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
-            write_pixel(PC, slot, col);
+            store_rgb(PC, slot, col);
         }
         if (COUNT) {
             uint32_t dmax = st.nodes - n0, smax = ss.nodes - s0;

@@ -103,7 +103,8 @@ struct RenderParams {
     int32_t buckets_per_frame;   // bucket mode: id = frame * buckets_per_frame + bucket
     int32_t n_cams;              // bucket mode: frames (cameras) in the batch
     int32_t mode;                // 0 frame, 1 buckets
-    float* out_rgb;              // frame: W*H*3; buckets: n_buckets*1024*3 (nullable)
+    int32_t frame_out;           // buckets: outputs are n_cams consecutive W*H frames, not tiles (store_rgb)
+    float* out_rgb;              // frame: W*H*3; buckets: n_buckets*1024*3, or n_cams*W*H*3 with frame_out (nullable)
     uint8_t* out_rgb8;           // same slots as out_rgb (nullable)
     float4* hits;                // per slot: t, a, b, prim bits (kernel 1 -> kernel 2)
     // wavefront chain engine (mrt_chain.hip; REC scenes on the frame / bucket
@@ -1132,6 +1133,33 @@ __device__ __forceinline__ bool item_pixel(const RenderParams& P, int item, int 
     return x < P.cam[0].W && y < P.cam[0].H;
 }
 
+// Store a pixel's linear RGB (before Image::Map) and its 8-bit Map (src/Image.cpp:19-35,
+// 71-87) at its slot.  Frame mode and bucket tiles: the slot is the output index.  With
+// frame_out (mrt_render_batch_frames_async) a bucket slot's pixel goes straight to its
+// place in frame f of n_cams consecutive W*H frames -- e.g. rank 0's frame mapped into
+// this process (mrt_ipc_open), so a rank of the multi-GPU split writes its buckets
+// where they belong and no gather / unpack follows; pixels outside the frame and
+// items of frames >= n_cams write nothing.
+__device__ __forceinline__ void store_rgb(const RenderParams& P, size_t slot, v3 col) {
+    if (P.frame_out) {
+        const uint32_t id = (uint32_t)P.buckets[slot >> 10];
+        const uint32_t bpf = (uint32_t)P.buckets_per_frame, f = id / bpf, b = id % bpf;
+        const int x = (int)(b % (uint32_t)P.buckets_x) * 32 + (int)(slot & 31);
+        const int y = (int)(b / (uint32_t)P.buckets_x) * 32 + (int)((slot >> 5) & 31);
+        const int W = P.cam[0].W, H = P.cam[0].H;
+        if (f >= (uint32_t)P.n_cams || x >= W || y >= H) return;
+        slot = ((size_t)f * H + y) * W + x;
+    }
+    if (P.out_rgb) {
+        float* o = P.out_rgb + 3 * slot;
+        o[0] = col.x; o[1] = col.y; o[2] = col.z;
+    }
+    if (P.out_rgb8) {
+        uint8_t* o8 = P.out_rgb8 + 3 * slot;
+        o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
+    }
+}
+
 __device__ __forceinline__ void load_tables(const uint16_t* g, uint16_t* s, int words32) {
     for (int i = threadIdx.x; i < words32; i += kWG) reinterpret_cast<uint32_t*>(s)[i] = reinterpret_cast<const uint32_t*>(g)[i];
     __syncthreads();
@@ -1349,14 +1377,7 @@ __global__ void __launch_bounds__(kWG, MINW) shade_kernel(RenderParams P) {
             col = mk(P.bg[0], P.bg[1], P.bg[2]);
         }
         if (MODE == kGen) continue;
-        if (P.out_rgb) {
-            float* o = P.out_rgb + 3 * slot;
-            o[0] = col.x; o[1] = col.y; o[2] = col.z;
-        }
-        if (P.out_rgb8) {
-            uint8_t* o8 = P.out_rgb8 + 3 * slot;
-            o8[0] = map8(P.gamma, col.x); o8[1] = map8(P.gamma, col.y); o8[2] = map8(P.gamma, col.z);
-        }
+        store_rgb(P, slot, col);
     }
     flush_secondary(P, secondary_total, lane);
     flush_stats<COUNT>(P, st, MODE == kResolve ? 0u : shadow_total, lane, t0, ntiles);
@@ -1476,14 +1497,7 @@ __global__ void __launch_bounds__(kWG, MINW) adaptive_kernel(RenderParams P) {
             level++;
         }
         if ((level <= P.max_subdivs && !cut) || level <= P.min_subdivs) return false;
-        if (P.out_rgb) {
-            float* o = P.out_rgb + 3 * slot;
-            o[0] = result.x; o[1] = result.y; o[2] = result.z;
-        }
-        if (P.out_rgb8) {
-            uint8_t* o8 = P.out_rgb8 + 3 * slot;
-            o8[0] = map8(P.gamma, result.x); o8[1] = map8(P.gamma, result.y); o8[2] = map8(P.gamma, result.z);
-        }
+        store_rgb(P, slot, result);
         return true;
     };
     if (P.refill_min <= 0) {

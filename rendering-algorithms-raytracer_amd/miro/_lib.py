@@ -9,7 +9,7 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("MRT_LIB", os.path.join(_PKG, "lib", "libmrt.so"))
 
 MRT_OK = 0
-ABI_VERSION = 9   # include/mrt.h MRT_ABI_VERSION: the struct layouts below
+ABI_VERSION = 10   # include/mrt.h MRT_ABI_VERSION: the struct layouts below
 ERRORS = {-1: "MRT_ERR_INVALID", -2: "MRT_ERR_IO", -3: "MRT_ERR_HIP", -4: "MRT_ERR_BUILD",
           -5: "MRT_ERR_NOT_BUILT", -6: "MRT_ERR_OVERFLOW", -7: "MRT_ERR_NO_DEVICE"}
 
@@ -28,6 +28,7 @@ EXPORTS = [
     "mrt_scene_set_material_sample_env", "mrt_scene_set_path_trace", "mrt_scene_prim_object",
     "mrt_image_info", "mrt_image_load", "mrt_scene_add_texture_typed", "mrt_scene_set_material_maps",
     "mrt_scene_mesh_set_texcoords", "mrt_scene_mesh_texcoords", "mrt_scene_set_mesh_motion", "mrt_scene_walk_info",
+    "mrt_render_batch_frames_async", "mrt_ipc_export", "mrt_ipc_open", "mrt_ipc_close",
 ]
 
 
@@ -63,6 +64,10 @@ class mrt_bvh_info(C.Structure):
     _fields_ = [("nodes", C.c_int32), ("leaves", C.c_int32), ("prims", C.c_int32), ("bin_nodes", C.c_int32),
                 ("bin_leaves", C.c_int32), ("max_depth", C.c_int32), ("build_ms", C.c_double),
                 ("device_bytes", C.c_uint64)]
+
+
+class mrt_ipc_handle(C.Structure):
+    _fields_ = [("handle", C.c_uint8 * 64), ("offset", C.c_uint64), ("size", C.c_uint64)]
 
 
 class mrt_render_opts(C.Structure):
@@ -171,6 +176,12 @@ def load():
                                          C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
     L.mrt_unpack_batch_async.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                                          C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mrt_render_batch_frames_async.argtypes = [C.c_void_p, C.POINTER(mrt_camera), C.c_int32,
+                                                C.POINTER(mrt_render_opts), C.c_void_p, C.c_int32, C.c_void_p,
+                                                C.c_void_p, C.c_void_p]
+    L.mrt_ipc_export.argtypes = [C.c_void_p, C.POINTER(mrt_ipc_handle)]
+    L.mrt_ipc_open.argtypes = [C.POINTER(mrt_ipc_handle), C.c_int, C.POINTER(C.c_void_p)]
+    L.mrt_ipc_close.argtypes = [C.c_void_p]
     L.mrt_render_frame_async.argtypes = [C.c_void_p, C.POINTER(mrt_camera), C.POINTER(mrt_render_opts),
                                          C.c_void_p, C.c_void_p, C.c_void_p]
     L.mrt_trace.argtypes = [C.c_void_p, _fp, _fp, _fp, _fp, C.c_size_t, C.c_int, C.c_void_p]

@@ -167,3 +167,83 @@ class BatchPipeline:
                 with self._on(i):
                     self.work[i].wait()
                 self.work[i] = None
+
+
+class FramePipeline:
+    """Per-step render straight into rank 0's frames -> one frame-end barrier.
+
+    The frames live on rank 0 (`depth` buffers); every rank has them mapped
+    (mrt_ipc_export / mrt_ipc_open on the GPU: rank r's pixels cross xGMI as the
+    kernel stores them) and render(b) enqueues this rank's buckets of the step
+    straight into buffer b (mrt_render_batch_frames_async) -- no tile buffers, no
+    gather, no unpack.  barrier() is a stream-ordered collective (an all-reduce of
+    one int, async) that completes once every rank's render of the step has
+    completed, i.e. when rank 0's frame b is whole.  consume(b), on rank 0 only
+    and optional, runs on buffer b's stream once its frame is whole (e.g. a copy
+    out, a display).
+
+    Ordering, with streams (one per buffer): step k renders into b = k % depth on
+    streams[b] after the barrier of step k - depth + 1 has completed, and rank 0
+    joins barrier j only after consume(j - 1) has run.  So that barrier implies
+    that every rank finished step k - depth + 1 and that rank 0 consumed step
+    k - depth, the last user of buffer b.  Up to depth - 1 steps' launches are in
+    flight at once.  Without streams (gloo on the CPU) every call completes in
+    order and the same code runs."""
+
+    def __init__(self, world, rank, render, barrier, consume=None, streams=None, depth=2):
+        self.world, self.rank = world, rank
+        self.render, self.barrier, self.consume = render, barrier, consume
+        self.streams = streams
+        self.depth = len(streams) if streams else max(2, depth)
+        if self.depth < 2:
+            raise ValueError("FramePipeline needs at least 2 buffers")
+        self.works = {}          # step -> barrier work
+        self.consumed = -1       # last step rank 0 consumed
+        self.ev = None           # rank 0: event after the last consume (GPU streams)
+        self.k = 0
+
+    def _on(self, b):
+        if self.streams is None:
+            return contextlib.nullcontext()
+        import torch
+        return torch.cuda.stream(self.streams[b])
+
+    def _consume(self, j):
+        """rank 0: step j's frame is whole after its barrier; consume it on its stream."""
+        with self._on(j % self.depth):
+            w = self.works.get(j)
+            if w is not None:
+                w.wait()
+            if self.consume is not None:
+                self.consume(j % self.depth)
+            if self.streams is not None:
+                import torch
+                self.ev = torch.cuda.Event()
+                self.ev.record()
+        self.consumed = j
+
+    def step(self):
+        k, d = self.k, self.depth
+        b = k % d
+        if self.rank == 0 and self.consume is not None and k >= 1 and self.consumed < k - 1:
+            self._consume(k - 1)
+        with self._on(b):
+            w = self.works.pop(k - d + 1, None)
+            if w is not None:
+                w.wait()
+            self.render(b)
+            if self.rank == 0 and self.ev is not None:   # barrier k only after consume(k - 1)
+                import torch
+                torch.cuda.current_stream().wait_event(self.ev)
+            self.works[k] = self.barrier()
+        self.k += 1
+
+    def flush(self):
+        """Every outstanding step whole (and consumed on rank 0)."""
+        if self.rank == 0 and self.consume is not None:
+            for j in range(self.consumed + 1, self.k):
+                self._consume(j)
+        for j, w in sorted(self.works.items()):
+            with self._on(j % self.depth):
+                w.wait()
+        self.works.clear()

@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
     L = miro.lib()
     missing = [s for s in declared_symbols() if not hasattr(L, s)]
     assert not missing, missing
-    assert L.mrt_abi_version() == 9
+    assert L.mrt_abi_version() == 10
 
 
 def test_errors_are_reported_not_raised():

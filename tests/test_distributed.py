@@ -410,3 +410,187 @@ def test_split_path_at_one_gpu_equals_frame_path(key):
     for b in range(K):
         assert np.array_equal(out_f[b].cpu().numpy().reshape(H, W, 3).view(np.uint32), img.rgb.view(np.uint32))
         assert np.array_equal(out_8[b].cpu().numpy().reshape(H, W, 3), img.pixels)
+
+
+def _frame_pipeline_worker(rank, world, port, W, H, steps, depth, result_path):
+    """FramePipeline on the CPU: rank 0's `depth` frames are a shared memory-mapped
+    file (the stand-in for the IPC mapping), every rank writes its buckets of a
+    step straight into frame k % depth, the barrier is a gloo all-reduce, and rank
+    0 consumes (copies out) each frame once it is whole; the renderer is the oracle."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, cam = _oracle_scene()
+        bx, by = tiles.bucket_grid(W, H)
+        mine = tiles.rank_buckets(bx * by, world, rank)
+        frames = np.lib.format.open_memmap(result_path + ".frames", mode="r+", dtype=np.float32,
+                                           shape=(depth, H, W, 3))
+        cams = scenes.camera_path(cam, steps, step_deg=4.0)
+        state = {"k": 0}
+        outs = []
+
+        def render(b):
+            k = state["k"]
+            state["k"] += 1
+            for i in mine:
+                x0, y0 = (i % bx) * 32, (i // bx) * 32
+                r = s.render(cams[k], W, H, rect=(x0, y0, x0 + 32, y0 + 32), want_hits=False)
+                h, w = min(32, H - y0), min(32, W - x0)
+                frames[b, y0:y0 + h, x0:x0 + w] = r["rgb"][y0:y0 + h, x0:x0 + w]
+            frames.flush()
+
+        def barrier():
+            return dist.all_reduce(torch.zeros(1), async_op=True)
+
+        def consume(b):
+            outs.append(np.array(frames[b]))
+
+        pipe = tiles.FramePipeline(world, rank, render, barrier, consume if rank == 0 else None, depth=depth)
+        for _ in range(steps):
+            pipe.step()
+        pipe.flush()
+        if rank == 0:
+            np.save(result_path, np.stack(outs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,depth", [(2, 2), (3, 3)])
+def test_frame_pipeline_direct_writes_equal_single_rank(tmp_path, world, depth):
+    """bench.py's IPC split (--assemble ipc): ranks write their buckets straight into
+    rank 0's frames, one barrier per step, rank 0 consumes each frame when whole --
+    every consumed frame equals the single-rank render of its camera, with buffers
+    reused (steps > depth) and a ragged bucket grid."""
+    W, H = 70, 40
+    steps = 5
+    path = str(tmp_path / "frames.npy")
+    np.lib.format.open_memmap(path + ".frames", mode="w+", dtype=np.float32, shape=(depth, H, W, 3)).flush()
+    mp.start_processes(_frame_pipeline_worker, args=(world, _free_port(), W, H, steps, depth, path), nprocs=world,
+                       start_method="spawn")
+    got = np.load(path)
+    assert got.shape == (steps, H, W, 3)
+    s, cam = _oracle_scene()
+    for k, c in enumerate(scenes.camera_path(cam, steps, step_deg=4.0)):
+        ref = s.render(c, W, H, want_hits=False)["rgb"]
+        assert np.array_equal(got[k].view(np.uint32), ref.view(np.uint32)), k
+
+
+def _ipc_worker(rank, world, port, key, W, H, steps, K, result_path):
+    """libmrt's IPC split on ONE device: rank 0 allocates the frames, exports them
+    (mrt_ipc_export), every other process maps them (mrt_ipc_open) and renders its
+    buckets of K camera-path frames per step straight into them
+    (mrt_render_batch_frames_async); a gloo all-reduce after each rank's stream
+    has drained is the frame-end barrier; rank 0 copies every whole step out."""
+    import ctypes as C
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import conftest  # noqa: F401  (paths)
+        import miro
+        from miro import _lib
+        from helpers import config_scene, camera
+        torch.cuda.set_device(0)
+        P, _, cam = config_scene(key)
+        L = miro.lib()
+        depth = 2
+        bpf = int(np.prod(tiles.bucket_grid(W, H)))
+        mine = tiles.rank_buckets(bpf * K, world, rank)
+        d_items = torch.tensor(mine, dtype=torch.int32, device="cuda")
+        if rank == 0:
+            own = [(torch.full((K * H * W * 3,), -1.0, dtype=torch.float32, device="cuda"),
+                    torch.zeros(K * H * W * 3, dtype=torch.uint8, device="cuda")) for _ in range(depth)]
+            hs = []
+            for f, f8 in own:
+                for t in (f, f8):
+                    h = _lib.mrt_ipc_handle()
+                    _lib.check(L.mrt_ipc_export(C.c_void_p(t.data_ptr()), C.byref(h)), "ipc export")
+                    hs.append(bytes(h))
+            obj = [hs]
+        else:
+            obj = [None]
+        dist.broadcast_object_list(obj, src=0)
+        ptrs, opened = [], []
+        for i in range(depth):
+            if rank == 0:
+                ptrs.append((own[i][0].data_ptr(), own[i][1].data_ptr()))
+                continue
+            pair = []
+            for j in range(2):
+                h = _lib.mrt_ipc_handle.from_buffer_copy(obj[0][2 * i + j])
+                p = C.c_void_p()
+                _lib.check(L.mrt_ipc_open(C.byref(h), 0, C.byref(p)), "ipc open")
+                pair.append(p.value)
+                opened.append(p.value)
+            ptrs.append(tuple(pair))
+        opts = _lib.mrt_render_opts(W, H, 0, 0, 1, 0, 0)
+        state = {"k": 0}
+        outs = []
+
+        def render(b):
+            k = state["k"]
+            state["k"] += 1
+            cams = [camera(c)._c() for c in scenes.camera_path(cam, K * steps, step_deg=3.0)[k * K:(k + 1) * K]]
+            cc = (_lib.mrt_camera * K)(*cams)
+            _lib.check(L.mrt_render_batch_frames_async(P.handle, cc, K, C.byref(opts), d_items.data_ptr(), len(mine),
+                                                       ptrs[b][0], ptrs[b][1],
+                                                       torch.cuda.current_stream().cuda_stream), "render frames")
+
+        def barrier():
+            torch.cuda.current_stream().synchronize()
+            return dist.all_reduce(torch.zeros(1), async_op=True)
+
+        def consume(b):
+            outs.append((own[b][0].cpu().numpy().reshape(K, H, W, 3), own[b][1].cpu().numpy().reshape(K, H, W, 3)))
+
+        pipe = tiles.FramePipeline(world, rank, render, barrier, consume if rank == 0 else None, depth=depth)
+        for _ in range(steps):
+            pipe.step()
+        pipe.flush()
+        torch.cuda.synchronize()
+        dist.barrier()
+        for p in opened:
+            _lib.check(L.mrt_ipc_close(C.c_void_p(p)), "ipc close")
+        if rank == 0:
+            np.save(result_path, np.stack([o[0] for o in outs]))
+            np.save(result_path + "8.npy", np.stack([o[1] for o in outs]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key,world,W,H,K", [("C3", 2, 200, 120, 1), ("C4", 3, 130, 70, 2), ("C5", 2, 160, 90, 2)])
+def test_ipc_split_frames_equal_single_process(tmp_path, key, world, W, H, K):
+    """every rank of the split writes its buckets into rank 0's
+    frames through an IPC mapping (processes sharing cuda:0 here; xGMI peers on a
+    node), no gather and no unpack.  Every frame of every step equals one
+    mrt_render_frame_async of its camera (seed + f within a step), float and 8-bit,
+    with frame buffers reused across steps."""
+    import ctypes as C
+    import miro
+    from miro import _lib
+    from helpers import config_scene, camera
+    if miro.device_count() < 1:
+        pytest.skip("no HIP device")
+    steps = 3
+    path = str(tmp_path / "frames.npy")
+    mp.start_processes(_ipc_worker, args=(world, _free_port(), key, W, H, steps, K, path), nprocs=world,
+                       start_method="spawn")
+    got, got8 = np.load(path), np.load(path + "8.npy")
+    assert got.shape == (steps, K, H, W, 3)
+    P, _, cam = config_scene(key)
+    L = miro.lib()
+    cams = scenes.camera_path(cam, K * steps, step_deg=3.0)
+    f = torch.empty(H * W * 3, dtype=torch.float32, device="cuda")
+    f8 = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")
+    for k in range(steps):
+        for j in range(K):
+            o = _lib.mrt_render_opts(W, H, 0, 0, 1, 0, 0x5EED + j)
+            cc = camera(cams[k * K + j])._c()
+            _lib.check(L.mrt_render_frame_async(P.handle, C.byref(cc), C.byref(o), f.data_ptr(), f8.data_ptr(), None),
+                       "render")
+            torch.cuda.synchronize()
+            ref, ref8 = f.cpu().numpy().reshape(H, W, 3), f8.cpu().numpy().reshape(H, W, 3)
+            assert np.array_equal(got[k, j].view(np.uint32), ref.view(np.uint32)), (k, j)
+            assert np.array_equal(got8[k, j], ref8), (k, j)

@@ -6,7 +6,8 @@ Every frame is compared whole (every row, every pixel):
 - hit ids, t, a, b and the shadow-ray count exact;
 - C2 / C3 / C3L (no libm on their path): float RGB and 8-bit RGB bit-exact against
   the oracle under the reference's own libm convention (oracle.LIBM_FLOAT);
-- C4 / C5 / D1 (Blinn pow, dome and environment lookups): bit-exact against the
+- C4 / C5 / D1 (Blinn pow, dome and environment lookups), and the secondary-ray
+  configs R3 / G3 / P4 (Fresnel, dispersion, path tracing): bit-exact against the
   oracle under the device's convention for sinf / cosf / powf (LIBM_DEVICE: double,
   rounded once; atan2f / acosf are glibc's bit for bit in both, csrc/mrt_libm.h), and
   within north_star's 1e-4 relative per channel -- |got - ref| <= 1e-4 |ref|, no
@@ -65,6 +66,45 @@ def test_full_size_frame_matches_oracle(key):
     assert nbad == 0, (key, nbad, exact)
     dev = Osc.render(cam, W, H, threads=16, want_hits=False, libm=O.LIBM_DEVICE)
     assert dev["shadow_rays"] == ref["shadow_rays"]
+    assert np.array_equal(bits(img.rgb), bits(dev["rgb"])), f"{key}: float RGB differs from the device-convention oracle"
+    assert np.array_equal(img.pixels, dev["rgb8"])
+
+
+SECONDARY = {"R3": (1920, 1080), "G3": (1920, 1080), "P4": (512, 512)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", sorted(SECONDARY))
+def test_full_size_secondary_rays_vs_reference_libm(key):
+    """The BASELINE-size frames of the secondary-ray configs (Fresnel's sin(acosf),
+    src/Material.h:47-55; dispersion, src/Blinn.cpp:169-185; path tracing's cosine
+    sampler cos / sin, src/Material.cpp:14-42) against the oracle under the
+    reference's own libm convention (LIBM_FLOAT: glibc's float overloads) within
+    north_star's 1e-4 relative per channel, and bit-exact against the device
+    convention (LIBM_DEVICE).  Primary hit ids and t / a / b are exact under both.
+    Under LIBM_FLOAT a path whose direction moves by an ulp may reach other
+    surfaces, so its secondary / shadow ray counts are printed, not required equal
+    (tools/libm_parity.py records the same comparison on the CPU,
+    profiles/r06_libm_parity.json)."""
+    need_gpu()
+    P, Osc, cam = config_scene(key)
+    W, H = SECONDARY[key]
+    img = miro.Image(); img.resize(W, H)
+    hits = P.raytraceImage(camera(cam), img, want_hits=True)
+    ref = Osc.render(cam, W, H, threads=16, libm=O.LIBM_FLOAT)
+    assert np.array_equal(hits["prim"], ref["hits"]["prim"]), f"{key}: primary hit ids differ"
+    hit = ref["hits"]["prim"] >= 0
+    for k in ("t", "a", "b"):
+        assert np.array_equal(bits(hits[k][hit]), bits(ref["hits"][k][hit])), f"{key}: hit {k} differs"
+    nbad, exact = close_frac(img.rgb, ref["rgb"])
+    st = P.last_stats
+    print(f"{key} {W}x{H} vs the reference's libm convention: {nbad} channels beyond 1e-4 relative, "
+          f"{exact:.6f} of channels bit-exact, {int((img.pixels != ref['rgb8']).any(axis=2).sum())} 8-bit pixels "
+          f"differ; shadow rays {st['shadow_rays']} / {ref['shadow_rays']}, secondary rays "
+          f"{st['secondary_rays']} / {ref['secondary_rays']} (device / reference convention)")
+    assert nbad == 0, (key, nbad, exact)
+    dev = Osc.render(cam, W, H, threads=16, want_hits=False, libm=O.LIBM_DEVICE)
+    assert st["shadow_rays"] == dev["shadow_rays"] and st["secondary_rays"] == dev["secondary_rays"]
     assert np.array_equal(bits(img.rgb), bits(dev["rgb"])), f"{key}: float RGB differs from the device-convention oracle"
     assert np.array_equal(img.pixels, dev["rgb8"])
 

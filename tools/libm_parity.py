@@ -1,12 +1,14 @@
 """CPU-only: how far the reference's libm convention moves each config's frame.
 
-The HIP device evaluates the reference's libm calls (Fresnel's sin(acosf), Blinn's
-pow, the lat-long lookups' atan2 / acos, the cosine sampler's cos / sin) in double
-and rounds once; the reference's source resolves them to the float overloads
-(glibc sinf / acosf / powf / atan2f / cosf).  The oracle restates both
-(oracle.LIBM_DEVICE / LIBM_FLOAT).  The device's frames equal the LIBM_DEVICE
-oracle bit for bit (tests/), so LIBM_FLOAT vs LIBM_DEVICE here is exactly the
-device-vs-reference-convention difference, per config:
+The reference's source resolves its libm calls (Fresnel's sin(acosf), Blinn's pow, the
+lat-long lookups' atan2 / acos, the cosine sampler's cos / sin) to the float overloads
+(glibc sinf / acosf / powf / atan2f / cosf).  The HIP device evaluates atan2f / acosf
+with the bit-exact fdlibm restatement of csrc/mrt_libm.h (glibc's own values), and only
+sinf / cosf / powf in double, rounded once.  The oracle restates both conventions
+(oracle.LIBM_DEVICE: the device's sinf / cosf / powf; LIBM_FLOAT: glibc's -- atan2f /
+acosf are glibc's in both).  The device's frames equal the LIBM_DEVICE oracle bit for
+bit (tests/), so LIBM_FLOAT vs LIBM_DEVICE here is exactly the device-vs-reference-
+convention difference, per config:
 
     python3 tools/libm_parity.py [--threads 8] [--out profiles/r05_libm_parity.json] [KEY[:WxH] ...]
 

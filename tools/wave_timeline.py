@@ -64,6 +64,8 @@ def main():
         log, khz = scene.wave_log(k)
         out[name + "_full"] = log
         log = log[:, :4]
+        if len(log) == 0:   # (the one-launch frame kernel has no shade launch)
+            continue
         t0 = log[:, 0].astype(np.float64)
         t1 = log[:, 1].astype(np.float64)
         base = t0.min()
