@@ -65,9 +65,11 @@ def parse():
     ap.add_argument("--frames", type=int, default=0, help="frames per step (default: 1 at N=1, N at N>1)")
     ap.add_argument("--settle-s", type=float, default=0.3,
                     help="untimed rendering before the warmup steps until this many seconds have passed (clock settle)")
-    ap.add_argument("--inflight", type=int, default=4,
+    ap.add_argument("--inflight", type=int, default=0,
                     help="N = 1 frame path: frames in flight (consecutive steps alternate over this many HIP "
-                         "streams, so one frame's launch tail overlaps the next frame's start)")
+                         "streams and hardware queues, so one frame's launch tail overlaps the next frame's "
+                         "start); 0 = the config's `inflight` (4, or 8 where a few heavy tiles set the frame's "
+                         "latency: C2, C4)")
     ap.add_argument("--path", choices=["auto", "batch"], default="auto",
                     help="batch: use the bucket-batch path even for one frame on one GPU (A/B)")
     ap.add_argument("--split", choices=["frame", "batch"], default="frame",
@@ -337,6 +339,15 @@ def profile_evidence(config):
 # ------------------------------------------------------------------ worker
 def main():
     args = parse()
+    if not args.inflight:   # the config's frames in flight (miro.scenes imports no torch / HIP)
+        sys.path.insert(0, os.path.join(ROOT, "rendering-algorithms-raytracer_amd"))
+        from miro import scenes as _scenes
+        args.inflight = int(_scenes.CONFIGS[args.config].get("inflight", 4))
+    # hardware queues of this process's HIP runtime (read when HIP initialises, so before
+    # torch is imported): one per frame in flight.  With HIP's default 4 the N = 1 pipeline
+    # holds at most 4 frames, so a frame whose latency is set by a few heavy tiles caps
+    # the step at latency / 4 (C2: 0.2011 -> 0.1644 ms per step with 8)
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(min(32, max(4, args.inflight))))
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(spawn(args))
@@ -471,13 +482,14 @@ def main():
         Returns (pipe, render(b, opts), mine, frames) or raises when a rank cannot map."""
         nsplit = world if nsplit is None else nsplit
         srank = rank if srank is None else srank
+        nb = len(pipe_streams) if pipe_streams else max(2, depth)   # frame buffers (FramePipeline needs 2)
         cc = path_cameras(nf)
         mine = tiles_mod.rank_buckets(bpf * nf, nsplit, srank)
         items = torch.tensor(mine, dtype=torch.int32, device="cuda")
         alone = nsplit != world
         owner = alone or rank == 0
         own = [(torch.empty(nf * H * W * 3, dtype=torch.float32, device="cuda"),
-                torch.empty(nf * H * W * 3, dtype=torch.uint8, device="cuda")) for _ in range(depth)] if owner else None
+                torch.empty(nf * H * W * 3, dtype=torch.uint8, device="cuda")) for _ in range(nb)] if owner else None
         ptrs, opened, err = [], [], ""
         if alone or world == 1:
             ptrs = [(f.data_ptr(), f8.data_ptr()) for f, f8 in own]
@@ -501,7 +513,7 @@ def main():
                 elif obj[0] is None:
                     err = "rank 0 could not export its frames"
                 else:
-                    for i in range(depth):
+                    for i in range(nb):
                         pair = []
                         for j in range(2):
                             h = _lib.mrt_ipc_handle.from_buffer_copy(obj[0][2 * i + j])
@@ -532,8 +544,8 @@ def main():
             return dist.all_reduce(flag, async_op=True)
 
         pipe = tiles_mod.FramePipeline(world if not alone else 1, rank if not alone else 0, render, barrier, None,
-                                       streams=pipe_streams or [torch.cuda.Stream() for _ in range(depth)])
-        for b in range(depth):   # per-stream scratch allocated before any timing
+                                       streams=pipe_streams or [torch.cuda.Stream() for _ in range(nb)])
+        for b in range(nb):   # per-stream scratch allocated before any timing
             with torch.cuda.stream(pipe.streams[b]):
                 render(b)
         torch.cuda.synchronize()

@@ -423,34 +423,41 @@ int mrt_trace_async(mrt_scene* s, const float* d_o, const float* d_d, const floa
 
 /* The walk of the scene's last one-light frame on its current device: *lds_nodes = 1
  * when it ran the LDS top-node walk (tuning "lds_nodes"), 0 when not, -1 before any;
- * *walk_exits = the frame kernel's walk-loop form, 1 (one exit) or 2 (a second exit on
- * stack overflow), picked per scene by a probe of single frames (tuning "walk_exit"),
- * -1 before it ran.  Both forms give the same bits. */
+ * *walk_exits = the walk loop's form of the frame / primary kernels, 1 (one exit: a
+ * stack overflow empties the stack and leaves at the pop test; the default) or 2 (a
+ * second exit on overflow; tuning "walk_exit" 0).  Both forms give the same bits. */
 int mrt_scene_walk_info(const mrt_scene* s, int32_t* lds_nodes, int32_t* walk_exits);
 
 /* Counters of the last render on this scene (ray counts, visits, kernel time). */
 int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
 
-/* Performance A/B switches (no effect on results; defaults in brackets):
- * "shadow_sched" [-1]..2 (wavefront shadow rays: auto, grid-stride, XCD bands,
- * bands + lane refill), "refill_min" 1..64 [40] (idle lanes that trigger a refill),
- * "fast_box" 0/[1] (hardware min/max slab test when its finiteness precondition
- * holds), "primary_waves" 0/6/[7]/8 (occupancy target of the primary-ray kernel),
- * "walk_exit" [-1]..1 (the frame kernel's walk loop: auto by a per-scene probe, two
- * exits, one exit), "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands, dynamic
- * interleaved, dynamic banded; see TileSched), "shade1" 0/[1] (specialised shading
- * kernel for one point light and one path), "lds_nodes" 0..1 (the frame kernel's
- * LDS top-node walk: [0] off, 1 on; C2 -4%, C3 +9% with 4 frames in flight), "scalar_nodes" 0..[7] (bit 0 scalar fetch of wave-uniform nodes, bit 1 of
- * wave-uniform triangles, bit 2 octant-ordered box test), "fused" 0/[1] (one-launch frame kernel
- * for one point light), "bin" [-1] / 0..7 (ray binning before tracing: bit 0 the
- * wavefront shadow pass, bit 1 the chain levels' closest-hit entries, bit 2 their
- * shadow rays; -1 auto), "bin_dbits" 0..6 [2] / "bin_obits" 0..4 [2] (binning key:
- * direction and origin cells per axis as powers of two, 2 dbits + 3 obits <= 12),
- * "bin_blocks" 1..16 [4] (binning workgroups per CU), "dome_replay" 0/[1] (the
- * dome-light resolve pass sums the recorded samples), "chain_bands" [-1]..1
- * (XCD-banded chain trace queue; -1: on for binned levels), "batch_tpw" 1..64 [2]
- * (tiles per wave a bucket batch smaller than the persistent grid is launched
- * for).  Process-wide. */
+/* Performance A/B switches (no effect on results; defaults in brackets).  Each key is
+ * either selected by a default path or exercised by the GPU tests (round 6 removed the
+ * rest, with their kernel instantiations; their A/B records stay in profiles/):
+ * "fast_box" 0/[1] (hardware min/max slab test when its finiteness precondition holds),
+ * "scalar_nodes" 0..[7] (bit 0 scalar fetch of wave-uniform nodes, bit 1 of wave-uniform
+ * triangles, bit 2 octant-ordered box test), "walk_exit" 0/[1] (the frame / primary
+ * kernels' walk loop: two exits, one exit), "lds_nodes" [0]/1 (the frame kernel's LDS
+ * top-node walk), "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands,
+ * dynamic interleaved, dynamic banded; see TileSched), "fused" 0/[1] (one-launch frame
+ * kernel for one point light), "shade1" 0/[1] (specialised shading kernel for one point
+ * light and one path), "frame1_waves" 1/5/6/[7]/8 and "primary_waves" 0/6/[7]/8 and
+ * "primary_inst_waves" 1/4/[5]/6 (occupancy targets), "wavefront" 0/[1] (gen / shadow /
+ * resolve passes instead of the fused shading kernel), "shadow_sched" [-1]..2 (wavefront
+ * shadow rays: auto, grid-stride, XCD bands, bands + lane refill), "near_first" [-1]..1
+ * (any-hit walks descend into the nearest hit child first), "dome_replay" 0/[1] (the
+ * dome-light resolve pass sums the recorded samples), "bin" [-1] / 0..7 (ray binning
+ * before tracing: bit 0 the wavefront shadow pass, bit 1 the chain levels' closest-hit
+ * entries, bit 2 their shadow rays; -1 auto), "bin_dbits" 0..6 [2] / "bin_obits" 0..4 [2]
+ * (binning key: direction and origin cells per axis as powers of two, 2 dbits + 3 obits
+ * <= 12), "bin_inst" [0]..2 (instance-major shadow-ray bin keys), "chain" 0/[1] (the
+ * wavefront chain engine for secondary rays), "chain_bands" [-1]..1 (XCD-banded chain
+ * trace queue; -1: on for binned levels), "chain_est" 0/[1] / "chain_est_pct" [125] /
+ * "chain_mb" [8192] (chain level capacities and scratch budget), "chain_shadow_step"
+ * [0]/1 and "chain_shadow_refill" [0]/1 (instanced chain levels' shadow walks),
+ * "adapt_refill" 0..64 [32] (adaptive pixel refill), "batch_tpw" 1..64 [2] (tiles per
+ * wave a bucket batch smaller than the persistent grid is launched for), "wave_log"
+ * [0]/1 (timing-only wave log, diagnostics).  Process-wide. */
 int mrt_set_tuning(const char* key, int value);
 
 /* Diagnostics: per-wave records of the last count-mode render (count_visits = 1)

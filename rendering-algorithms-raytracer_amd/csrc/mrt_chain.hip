@@ -819,8 +819,8 @@ KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec) {
     if (rec == 2) return resolve ? chain_shade_fn<kResolve, 2>(po, inst) : chain_shade_fn<kGen, 2>(po, inst);
     return resolve ? chain_shade_fn<kResolve, 1>(po, inst) : chain_shade_fn<kGen, 1>(po, inst);
 }
-KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves, int step) {
-    if (waves == 8 && !c && !inst)   // occupancy target of the plain-scene trace (timed variants)
+KernelFn pick_chain_trace(bool c, bool f, bool inst, int step) {
+    if (!c && !inst)   // occupancy target of the plain-scene trace (timed variants)
         return f ? chain_trace_kernel<false, true, false, 8> : chain_trace_kernel<false, false, false, 8>;
     if (inst && step == 1)
         return c ? (f ? chain_trace_kernel<true, true, true, 1, 1> : chain_trace_kernel<true, false, true, 1, 1>)

@@ -74,6 +74,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
            P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
+    if (INST && REFILL) { T.cleaves = P.cleaves; T.cverts = P.verts; }
     TravStats st;
     unsigned long long wave_steps = 0;
     if (P.ch_ovf && *P.ch_ovf) return;   // a chain chunk past its estimated capacity (redone by its fallback)
@@ -378,6 +379,7 @@ struct DeviceState {
     int device = -1;
     QNode* nodes = nullptr;
     DLeaf* leaves = nullptr;
+    uint4* cleaves = nullptr;     // compact leaf packets: per lane the triangle's 3 vertex indices (tuning compact_leaves)
     PrimShade* prims = nullptr;
     float4* verts = nullptr;
     float4* normals = nullptr;
@@ -414,7 +416,6 @@ struct DeviceState {
     bool boxes_ordered = false;  // every used slot box has lo <= hi per axis (octant-ordered box test)
     bool lds_ok = false;         // the world hierarchy has kLdsNodes nodes for the LDS top-node walk (renumbered)
     std::atomic<int> lds_pick{-1};   // the last one-light frame ran the LDS top-node walk: 1 yes, 0 no, -1 none yet
-    std::atomic<int> exit_pick{-1};  // frame1_kernel's walk loop for this scene: 1 one exit, 0 two, -1 not probed yet
     float bb_lo[3] = {0, 0, 0}, bb_hi[3] = {0, 0, 0};   // world root box (ray-binning origin cells)
     int cus = 0;
     bool point_only = false;
@@ -440,7 +441,7 @@ struct DeviceState {
 // Tuning knobs (mrt_set_tuning): A/B switches for performance work.
 static int g_fast_box = 1;        // hardware min/max box test when its precondition holds
 static int g_primary_waves = 7;   // launch-bounds occupancy target of the primary kernel: 0 (none), 6, 7, 8
-static int g_shade_waves = 5;     // same for shade1_kernel: 1 (none), 4..8 (5: 96 VGPRs, 64 B spill; -2.5% vs 6)
+// shade1_kernel (the two-launch one-light shading) runs at 5 waves: 96 VGPRs, -2.5% vs 6 (round 2)
 static int g_sched = 2;           // TileSched mode 0..3 (2 measured fastest)
 static int g_batch_tpw = 2;       // bucket batches: tiles per wave the launch's grid is sized for when the batch is
                                   // smaller than the persistent grid (a 1/4 or 1/8 split share): 2 -- C3 share model
@@ -453,20 +454,19 @@ static int g_shade1 = 1;          // specialised shade kernel for one point ligh
 static int g_wavefront = 1;       // general shading: gen / trace / resolve kernels instead of one fused kernel
 static int g_shadow_sched = -1;   // shadow_kernel schedule: 0 grid-stride, 1 XCD bands, 2 bands + lane refill,
                                   // -1 auto: refill for dome-light (incoherent) rays, else bands
-static int g_shadow_waves = 8;    // shadow_kernel launch-bounds occupancy: 1 (none), 7, 8 (8: C4 / C5 -5.5%)
+// shadow_kernel's launch-bounds occupancy target is 8 waves (C4 / C5 -5.5% against none)
 static int g_primary_inst_waves = 5;   // primary kernel of special-leaf scenes: 1 (none), 5, 6 (r02: 6 beat 1 by 5% on C5;
                                        // r03: 5 = 6 within 0.3% with binned shadow rays, and 96 VGPRs spill less)
-static int g_resolve_waves = 4;   // resolve pass (kernel 2c) of dome-light scenes: 1 (none), 3 (special-leaf only), 4
-static int g_adapt_waves = 6;     // direct-lighting adaptive kernel occupancy target: 1 (none) or 6
-                                  // (unbounded it takes 256 VGPRs, 1 wave: A3 30.7 -> 12.8 ms at 6)
+// the resolve pass (kernel 2c) of dome-light scenes runs at 4 waves (D1 -4%, C5 -1.2 ms);
+// the direct-lighting adaptive kernel at 6 (unbounded it takes 256 VGPRs: A3 30.7 -> 12.8 ms)
 static int g_adapt_refill = 32;   // adaptive_kernel pixel refill: idle lanes that trigger a dequeue (0: tiles; 32: A3 -13%)
 static int g_chain_shadow_step = 0;   // instanced chain levels: shadow rays walk with anyhit_step_inst (deferred proxies)
-static int g_chain_trace_waves = 8;   // chain_trace_kernel occupancy target: 1 (none) or 8 (P4 -17%, R3 -3.5%)
+// chain_trace_kernel of plain scenes runs at 8 waves (P4 -17%, R3 -3.5% against none)
 static int g_near_first = -1;     // any-hit walks take the nearest hit child first: 0 off, 1 on, -1 auto
                                   // (auto: on in the chunked shadow kernel of plain scenes only -- C4 shade
                                   // -12.6%; off in the refill one, C5 +4.5%, the instanced chunked one,
                                   // C5 +15%, and the fused kernels, C3 +5%, A3 / R3 +2%)
-static int g_refill_min = 40;     // lane refill: idle lanes of a wave that trigger a dequeue
+static constexpr int kRefillMin = 40;   // lane refill: idle lanes of a wave that trigger a dequeue
 static int g_chain_shadow_refill = 0;   // instanced chain levels: shadow rays on the lane-refill kernel (FS: 6% slower, profiles/r04_fs_chain_shadow_refill_ab.txt)
 static int g_chain = 1;           // REC scenes: wavefront chain engine (mrt_chain.hip) instead of the fused kernel
 static int g_chain_est = 1;       // chain levels sized by the entries earlier chunks needed (0: worst case, 3^ceil(k/2))
@@ -474,14 +474,18 @@ static int g_chain_est_pct = 125; //   headroom over the largest count per path 
 static int g_chain_mb = 8192;     // chain scratch per stream (MB), at most 80% of the device's free memory; larger frames
                                   // run in chunks of work items.  With estimated level capacities 8 GB costs G3 3% against
                                   // 48 GB and R3 / P4 / FS nothing (profiles/r04_chain_mb_est_ab.txt)
-static int g_chain_adapt = 1;     // adaptive supersampling of REC scenes: passes over the chain engine (0: fused kernel)
 static int g_fused = 1;           // one point light, one path: frame1_kernel (primary + shading in one launch)
-static int g_walk_exit = -1;      // frame1_kernel's walk loop: 1 one exit (the overflow empties the stack), 0 two
-                                  // (the overflow returns); -1 auto: a probe of single frames on the scene's first
-                                  // fused render picks (one exit: C3 -7%, C3L -1%; two: C2 -12%, r05_walk_exit_ab.txt)
+static int g_walk_exit = 1;       // the walk loop of frame1_kernel / primary_kernel: 1 one exit (a stack overflow
+                                  // empties the stack and leaves at the pop test), 0 two (the overflow returns).
+                                  // One exit issues 19% fewer SALU per wave step (C3 -7%, C4 -6%); round 5's
+                                  // 12-16% loss on the bunny scenes was the frame latency of a few heavy
+                                  // top-row tiles with only 4 frames in flight (walk exit), gone
+                                  // with 8 hardware queues: one exit everywhere, no probe (round 6)
 static int g_lds_nodes = 0;       // frame1_kernel's LDS top-node walk (LN), 0 off / 1 on: with 4 frames in flight C2
                                   // -4.1%, C3 +9%, C3L +11% (profiles/r05_lds_nodes_ab_*.txt); no probe separated them
                                   // reliably (single-frame kernel times are equal on C2), so it is off unless asked for
+static int g_compact_leaves = 0;  // instanced any-hit shadow walks (lane refill) read compact leaf packets: the
+                                  // three vertex indices per lane and the shared vertices (A/B, round 6)
 static int g_frame1_waves = 7;    // frame1_kernel launch-bounds occupancy target: 1 (none), 5..8 (7: -0.9% per frame with
                                   // 4 frames in flight, +0.8% single-frame latency; profiles/r03_c3_scalar_waves_ab.txt)
 static int g_bin = -1;            // ray binning (mrt_bin.h) before tracing: bit 0 the wavefront shadow pass (kernel 2b),
@@ -497,7 +501,7 @@ static int g_chain_bands = -1;    // chain_trace_kernel: XCD-banded chunk queue 
                                   // -1 auto: on when the level is binned (P4 -3.4%; unbinned R3 +5.7%, G3 +3%)
 static int g_dome_replay = 1;      // dome-light resolve (2c) sums 2a's recorded samples instead of sampling again
 static int g_bin_inst = 0;        // off: C5 shade pass +0.8% (profiles/r04_c5_bin_inst_primary_waves_ab.txt); instanced scenes' shadow-ray bins: instance-major keys (the ray's origin instance, BLAS-major)
-static int g_bin_blocks = 4;      // binning launches: workgroups per CU (each reserves its range of every bin atomically)
+static constexpr int kBinBlocks = 4;   // binning launches: workgroups per CU (each reserves its range of every bin atomically)
 static int g_bin_dbits = 2;       // binning key: direction cells per octahedral axis = 2^dbits
 static int g_bin_obits = 2;       //   origin cells per scene-box axis = 2^obits (2 dbits + 3 obits <= 12);
                                   //   sweep of 12 pairs: (2, 2) best on P4 (-18%) and C5 (-2.6%), finer
@@ -534,7 +538,7 @@ static void free_device(DeviceState* d) {
     }
     if (d->g_tiles) (void)hipFree(d->g_tiles);
     if (d->g_items) (void)hipFree(d->g_items);
-    void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts,
+    void* ptrs[] = {d->nodes, d->leaves, d->cleaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts,
                     d->inst_hit_base, d->inst_class, d->inst_cell, d->tables,
                     d->gamma, d->gammaF, d->d_rgb, d->d_rgb8, d->texs, d->puv, d->uvs, d->tans, d->btans,
                     d->pflags, d->verts2};
@@ -701,6 +705,7 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     if (n_leaves >= (size_t(1) << 27)) { set_error("too many leaf packets"); return MRT_ERR_OVERFLOW; }
     std::vector<QNode> DN;
     std::vector<DLeaf> DL;
+    std::vector<uint4> CL;   // compact leaf packets (parallel to DL)
     auto append = [&](const std::vector<QNode>& nodes, const std::vector<QLeaf>& leaves,
                       const std::vector<int32_t>* oi, const Blas* B) -> int32_t {
         const int32_t nb = (int32_t)DN.size(), lb = (int32_t)DL.size();
@@ -733,6 +738,17 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
                 for (int c = 0; c < 9; c++) D.tri[k][c] = L.t[4 * c + k];
                 const int32_t pi = proxy_of(L.prim[k]);
                 D.prim[k] = pi >= 0 ? -2 - pi : L.prim[k];
+                // the lane's vertices (make_leaf: A = v0, e0 = v1 - v0, e1 = v2 - v0), as global vertex
+                // indices; proxy and motion-blurred lanes (no triangle data in the packet) and empty lanes: 0
+                uint4 ix = make_uint4(0u, 0u, 0u, 0u);
+                const int32_t p = L.prim[k];
+                const int32_t mesh = p < 0 || pi >= 0 ? -1 : B ? B->obj_mesh[(size_t)p] : (oi && !mb_obj(p)) ? s.obj_mesh[(size_t)p] : -1;
+                if (mesh >= 0) {
+                    const size_t tri = (size_t)(B ? B->obj_tri[(size_t)p] : s.obj_tri[(size_t)p]);
+                    const uint32_t* f = &s.meshes[(size_t)mesh].vidx[3 * tri];
+                    ix = make_uint4(vbase[(size_t)mesh] + f[0], vbase[(size_t)mesh] + f[1], vbase[(size_t)mesh] + f[2], 0u);
+                }
+                CL.push_back(ix);
             }
             DL.push_back(D);
         }
@@ -821,6 +837,7 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     }
     d.n_world = (int)s.obj_mesh.size();
     if ((rc = upload(d.leaves, DL.data(), DL.size() * sizeof(DLeaf), total))) return rc;
+    if ((rc = upload(d.cleaves, CL.data(), CL.size() * sizeof(uint4), total))) return rc;
     if ((rc = upload(d.prims, PS.data(), PS.size() * sizeof(PrimShade), total))) return rc;
     if ((rc = upload(d.verts, V.data(), V.size() * sizeof(float4), total))) return rc;
     if ((rc = upload(d.normals, N.data(), N.size() * sizeof(float4), total))) return rc;
@@ -993,6 +1010,7 @@ static void fill_params(const Scene& s, RenderParams& P) {
     P.env_h = d.env ? s.textures[s.env_tex].H : 0;
     P.env_exposure = s.env_exposure;
     P.gstride = d.gthreads;
+    P.cleaves = g_compact_leaves ? d.cleaves : nullptr;
     P.bg[0] = s.bg[0]; P.bg[1] = s.bg[1]; P.bg[2] = s.bg[2];
     P.n_lights = (int32_t)s.lights.size();
     P.num_paths = s.num_paths;
@@ -1100,7 +1118,7 @@ static const uint32_t* bin_total(const BinArgs& A) {
     return A.hist + (size_t(1) << (A.hits ? kBinBits : 2 * A.dbits + 3 * A.obits));
 }
 static int bin_grid(const DeviceState& d, size_t n) {   // fewer blocks: fewer per-bin global atomics
-    return (int)std::max<size_t>(1, std::min<size_t>((size_t)d.cus * (size_t)g_bin_blocks, (n + 255) / 256));
+    return (int)std::max<size_t>(1, std::min<size_t>((size_t)d.cus * (size_t)kBinBlocks, (n + 255) / 256));
 }
 
 static int ensure_slots(StreamCtx& c, size_t slots) {
@@ -1174,14 +1192,13 @@ static KernelFn pick_primary(int w, bool c, bool f, bool inst, bool check = true
         default: return primary_fn<1>(c, f);
     }
 }
-// bound: the resolve pass at its g_resolve_waves occupancy target (~240 VGPRs unbounded)
+// bound: the dome-light resolve pass at 4 waves (~240 VGPRs unbounded)
 template <int MODE>
 static KernelFn shade_mode_fn(bool c, bool po, bool inst, bool bound = false) {   // kGen / kResolve: no traversal, FAST unused
-    if (!c && MODE == kResolve && bound && g_resolve_waves == 4) {
+    if (!c && MODE == kResolve && bound) {
         if (inst) return shade_kernel<false, false, false, true, MODE, 0, 4>;
         return po ? shade_kernel<false, true, false, false, MODE, 0, 4> : shade_kernel<false, false, false, false, MODE, 0, 4>;
     }
-    if (inst && !c && MODE == kResolve && bound && g_resolve_waves == 3) return shade_kernel<false, false, false, true, MODE, 0, 3>;
     if (inst) return c ? shade_kernel<true, false, false, true, MODE> : shade_kernel<false, false, false, true, MODE>;
     if (po) return c ? shade_kernel<true, true, false, false, MODE> : shade_kernel<false, true, false, false, MODE>;
     return c ? shade_kernel<true, false, false, false, MODE> : shade_kernel<false, false, false, false, MODE>;
@@ -1194,19 +1211,13 @@ static ShadowFn shadow_fn(bool c, bool f) {
              : (f ? shadow_kernel<false, true, INST, REFILL, CHECK, MINW> : shadow_kernel<false, false, INST, REFILL, CHECK, MINW>);
 }
 template <bool INST, bool REFILL, bool CHECK>
-static ShadowFn shadow_fn_w(int w, bool c, bool f) {
-    switch (w) {
-        case 7: return shadow_fn<INST, REFILL, CHECK, 7>(c, f);
-        case 8: return shadow_fn<INST, REFILL, CHECK, 8>(c, f);
-        default: return shadow_fn<INST, REFILL, CHECK>(c, f);
-    }
-}
+static ShadowFn shadow_fn_w(bool c, bool f) { return shadow_fn<INST, REFILL, CHECK, 8>(c, f); }
 // check: the scene has alpha-mapped or motion-blurred lanes (child-word bit 3), which the
 // refill step must test as such
-static ShadowFn pick_shadow(bool c, bool f, bool inst, bool refill, bool check, int w) {
-    if (!refill) return inst ? shadow_fn<true, false, true>(c, f) : shadow_fn_w<false, false, false>(w, c, f);
-    if (!inst) return shadow_fn_w<false, true, false>(w, c, f);
-    return check ? shadow_fn<true, true, true>(c, f) : shadow_fn_w<true, true, false>(w, c, f);
+static ShadowFn pick_shadow(bool c, bool f, bool inst, bool refill, bool check) {
+    if (!refill) return inst ? shadow_fn<true, false, true>(c, f) : shadow_fn_w<false, false, false>(c, f);
+    if (!inst) return shadow_fn_w<false, true, false>(c, f);
+    return check ? shadow_fn<true, true, true>(c, f) : shadow_fn_w<true, true, false>(c, f);
 }
 // shadow rays per pixel at most: num_paths x (1 per point light, m_numSamples per area / dome light)
 static int max_shadow_rays(const Scene& s) {
@@ -1266,7 +1277,7 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
     const KernelFn g0 = pick_chain0(false, d.point_only, inst, d.recursive), r0 = pick_chain0(true, d.point_only, inst, d.recursive);
     const KernelFn gk = pick_chain_shade(false, d.point_only, inst, d.recursive),
                    rk = pick_chain_shade(true, d.point_only, inst, d.recursive);
-    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, Q.fast_box != 0, inst, g_chain_trace_waves,
+    const KernelFn kc = pick_chain_compact(), kt = pick_chain_trace(count, Q.fast_box != 0, inst,
                                                                            g_chain_shadow_step ? (d.has_alpha || d.has_mb ? 2 : 1) : 0),
                    kf = pick_chain_finish(), kd = pick_chain_fold();
     auto go = [&](KernelFn f, int g) -> int {
@@ -1289,7 +1300,7 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
     }
     // instanced scenes: the levels' shadow rays on the lane-refill kernel (their own launch)
     const bool refill_sh = inst && g_chain_shadow_refill;
-    const ShadowFn ksh = refill_sh ? pick_shadow(count, Q.fast_box != 0, true, true, d.has_alpha || d.has_mb, g_shadow_waves) : nullptr;
+    const ShadowFn ksh = refill_sh ? pick_shadow(count, Q.fast_box != 0, true, true, d.has_alpha || d.has_mb) : nullptr;
     int gsh = refill_sh ? std::max(8, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(ksh), 0))) & ~7 : 0;
     auto trace = [&](int k) -> int {   // Q.ch_level == k
         if ((bm & 2) && k < L) {
@@ -1339,7 +1350,7 @@ static int chain_chunk(Scene& s, StreamCtx& c, RenderParams& Q, bool count, hipS
             S.near_first = 0;
             S.queue = queues + (size_t)(L + 2 + k) * 256;
             size_t n_rays = lcap_h(k - 1) * m;
-            int sched = 2, refill = g_refill_min;
+            int sched = 2, refill = kRefillMin;
             void* sargs[] = {&S, &n_rays, &sched, &refill};
             r3 = MRT_OK;
             if (hipLaunchKernel(reinterpret_cast<const void*>(ksh), dim3(gsh), dim3(kWG), sargs, 0, stream) != hipSuccess) {
@@ -1628,44 +1639,16 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         HIP_OK(hipLaunchKernel(reinterpret_cast<const void*>(f), dim3(g), dim3(kWG), args, 0, stream));
         return MRT_OK;
     };
-    // the walk loop's exit form (same bits either way; traverse_impl XONE): tuning "walk_exit",
-    // or a probe on this stream the first time the scene renders a timed frame here -- three
-    // single launches of each form, alternating, the faster minimum wins (a one-time host
-    // wait).  Returns 0 / 1, -1 (not probed: count mode), -2 on a HIP failure (rc set).
-    auto exit_form = [&](bool may_probe, auto pick) -> int {
-        int wx = g_walk_exit >= 0 ? g_walk_exit : d.exit_pick.load();
-        if (wx >= 0 || count || !may_probe) return wx;
-        hipEvent_t ea = nullptr, eb = nullptr;
-        if (hipEventCreate(&ea) != hipSuccess || hipEventCreate(&eb) != hipSuccess) rc = MRT_ERR_HIP;
-        float best[2] = {1e30f, 1e30f};
-        for (int rep = 0; rep < 3 && rc == MRT_OK; rep++)
-            for (int v = 0; v < 2 && rc == MRT_OK; v++) {
-                float ms = 0.f;
-                if (hipMemsetAsync(c.ctr, 0, kCtrBytes, stream) != hipSuccess ||
-                    hipEventRecord(ea, stream) != hipSuccess) { rc = MRT_ERR_HIP; break; }
-                if ((rc = launch(pick(v)))) break;
-                if (hipEventRecord(eb, stream) != hipSuccess || hipEventSynchronize(eb) != hipSuccess ||
-                    hipEventElapsedTime(&ms, ea, eb) != hipSuccess) { rc = MRT_ERR_HIP; break; }
-                best[v] = std::min(best[v], ms);
-            }
-        if (ea) (void)hipEventDestroy(ea);
-        if (eb) (void)hipEventDestroy(eb);
-        if (rc == MRT_OK && hipMemsetAsync(c.ctr, 0, kCtrBytes, stream) != hipSuccess) rc = MRT_ERR_HIP;
-        if (rc) { set_error("walk exit probe failed"); return -2; }
-        wx = best[1] <= best[0] ? 1 : 0;
-        d.exit_pick = wx;
-        return wx;
-    };
     HIP_OK(hipEventRecord(c.ev0, stream));
     const bool fb = P.fast_box != 0;
     c.chain_used = false;
     if (adaptive) {
         HIP_OK(hipEventRecord(c.evm, stream));   // primary_ms = 0: one launch
         P.refill_min = g_adapt_refill;
-        if (use_chain(s) && g_chain_adapt) {     // secondary rays: passes over the chain engine
+        if (use_chain(s)) {     // secondary rays: passes over the chain engine
             c.chain_used = true;
             if ((rc = launch_chain_adaptive(s, c, P, count, stream))) return rc;
-        } else if ((rc = launch(pick_adaptive(count, d.point_only, fb, inst, d.recursive, g_adapt_waves)))) {
+        } else if ((rc = launch(pick_adaptive(count, d.point_only, fb, inst, d.recursive)))) {
             return rc;
         }
         c.last_was_render = true;
@@ -1681,9 +1664,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         // LDS top-node walk (tuning "lds_nodes"; both walks give the same bits)
         const bool ln = fb && d.lds_ok && g_lds_nodes > 0;
         d.lds_pick = ln ? 1 : 0;
-        const int wx = exit_form(!ln, [&](int v) { return pick_frame1(g_frame1_waves, false, fb, d.pow_spec, v); });
-        if (wx == -2) return rc;
-        const int walk = ln ? 2 : (wx < 0 ? 1 : wx);
+        const int walk = ln ? 2 : g_walk_exit;
         if ((rc = launch(pick_frame1(g_frame1_waves, count, fb, d.pow_spec, walk)))) return rc;
         HIP_OK(hipEventRecord(c.evm, stream));
         c.last_was_render = true;
@@ -1694,9 +1675,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         return MRT_OK;
     }
     const bool chk = d.has_alpha || d.has_mb;
-    const int px = exit_form(!inst, [&](int v) { return pick_primary(g_primary_waves, false, fb, inst, chk, v != 0); });
-    if (px == -2) return rc;
-    if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst, chk, px == 1)))) return rc;
+    if ((rc = launch(pick_primary(g_primary_waves, count, fb, inst, chk, g_walk_exit == 1)))) return rc;
     HIP_OK(hipEventRecord(c.evm, stream));
     P.queue = qbase + 8 * 32;
     const int max_sh = max_shadow_rays(s);
@@ -1710,7 +1689,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         P.units_total = (uint32_t)P.n_tiles * 64u;
         if ((rc = launch_chain(s, c, P, count, stream, (uint64_t)P.n_tiles * 64, 64))) return rc;
     } else if (one || !wave) {
-        if ((rc = launch(one ? pick_shade1(g_shade_waves, count, fb, d.pow_spec) : pick_shade(count, d.point_only, fb, inst, d.recursive)))) return rc;
+        if ((rc = launch(one ? pick_shade1(count, fb, d.pow_spec) : pick_shade(count, d.point_only, fb, inst, d.recursive)))) return rc;
     } else {
         if ((rc = ensure_rays(c, slots, (size_t)max_sh))) return rc;
         P.ray_o = c.rays;
@@ -1730,13 +1709,13 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         if ((rc = launch(shade_mode_fn<kGen>(count, d.point_only, inst)))) return rc;
         // lane refill for dome-light (incoherent) rays: D1 -7%, C5 -13% shade pass; coherent
         // area-light rays keep the bands (C4: refill +9%)
-        int sched = g_shadow_sched >= 0 ? g_shadow_sched : (dome ? 2 : 1), refill = g_refill_min;
-        ShadowFn sf = pick_shadow(count, fb, inst, sched == 2, d.has_alpha || d.has_mb, g_shadow_waves);
+        int sched = g_shadow_sched >= 0 ? g_shadow_sched : (dome ? 2 : 1), refill = kRefillMin;
+        ShadowFn sf = pick_shadow(count, fb, inst, sched == 2, d.has_alpha || d.has_mb);
         int g = std::max(1, std::min(d.grid, d.cus * blocks_per_cu(reinterpret_cast<KernelFn>(sf), 0)));
         if (sched && (g & 7)) g &= ~7;          // XCD bands need a whole number of workgroups per XCD
         if (g < 8) {                            // too few workgroups for the bands: grid-stride
             sched = 0;
-            sf = pick_shadow(count, fb, inst, false, d.has_alpha || d.has_mb, g_shadow_waves);
+            sf = pick_shadow(count, fb, inst, false, d.has_alpha || d.has_mb);
         }
         size_t n_rays = slots * (size_t)max_sh;
         if (n_rays >= (size_t(1) << 32)) { set_error("too many wavefront shadow-ray slots (2^32)"); return MRT_ERR_INVALID; }
@@ -2740,8 +2719,7 @@ int mrt_scene_walk_info(const mrt_scene* cs, int32_t* lds_nodes, int32_t* walk_e
     const DeviceState* d = S.dev;
     if (lds_nodes) *lds_nodes = d ? (int32_t)d->lds_pick.load() : -1;
     if (walk_exits) {
-        const int x = g_walk_exit >= 0 ? g_walk_exit : (d ? d->exit_pick.load() : -1);
-        *walk_exits = x < 0 ? -1 : (x ? 1 : 2);
+        *walk_exits = g_walk_exit ? 1 : 2;
     }
     return MRT_OK;
 }
@@ -2897,9 +2875,6 @@ int mrt_set_tuning(const char* key, int value) {
     else if (k == "primary_waves") {
         if (value != 0 && value != 1 && (value < 6 || value > 8)) { set_error("primary_waves must be 0 or 6..8"); return MRT_ERR_INVALID; }
         g_primary_waves = value;
-    } else if (k == "shade_waves") {
-        if (value != 1 && (value < 4 || value > 8)) { set_error("shade_waves must be 1 or 4..8"); return MRT_ERR_INVALID; }
-        g_shade_waves = value;
     } else if (k == "scalar_nodes") {   // bit 0 nodes, bit 1 triangles (1 = round 3's nodes only), bit 2 octant box test
         if (value < 0 || value > 7) { set_error("scalar_nodes must be 0..7"); return MRT_ERR_INVALID; }
         g_scalar_nodes = value;
@@ -2914,8 +2889,6 @@ int mrt_set_tuning(const char* key, int value) {
         g_wavefront = value ? 1 : 0;
     } else if (k == "chain") {
         g_chain = value ? 1 : 0;
-    } else if (k == "chain_adapt") {
-        g_chain_adapt = value ? 1 : 0;
     } else if (k == "chain_mb") {
         if (value < 1 || value > 1 << 20) { set_error("chain_mb out of range"); return MRT_ERR_INVALID; }
         g_chain_mb = value;
@@ -2927,29 +2900,14 @@ int mrt_set_tuning(const char* key, int value) {
             set_error("primary_inst_waves must be 1, 4, 5 or 6"); return MRT_ERR_INVALID;
         }
         g_primary_inst_waves = value;
-    } else if (k == "resolve_waves") {
-        if (value != 1 && value != 3 && value != 4) { set_error("resolve_waves must be 1, 3 or 4"); return MRT_ERR_INVALID; }
-        g_resolve_waves = value;
-    } else if (k == "shadow_waves") {
-        if (value != 1 && value != 7 && value != 8) { set_error("shadow_waves must be 1, 7 or 8"); return MRT_ERR_INVALID; }
-        g_shadow_waves = value;
-    } else if (k == "adapt_waves") {
-        if (value != 1 && value != 6) { set_error("adapt_waves must be 1 or 6"); return MRT_ERR_INVALID; }
-        g_adapt_waves = value;
     } else if (k == "adapt_refill") {
         if (value < 0 || value > 64) { set_error("adapt_refill must be 0..64"); return MRT_ERR_INVALID; }
         g_adapt_refill = value;
     } else if (k == "chain_shadow_step") {
         g_chain_shadow_step = value ? 1 : 0;
-    } else if (k == "chain_trace_waves") {
-        if (value != 1 && value != 8) { set_error("chain_trace_waves must be 1 or 8"); return MRT_ERR_INVALID; }
-        g_chain_trace_waves = value;
     } else if (k == "near_first") {
         if (value < -1 || value > 1) { set_error("near_first must be -1..1"); return MRT_ERR_INVALID; }
         g_near_first = value;
-    } else if (k == "refill_min") {
-        if (value < 1 || value > 64) { set_error("refill_min must be 1..64"); return MRT_ERR_INVALID; }
-        g_refill_min = value;
     } else if (k == "fused") {
         g_fused = value ? 1 : 0;
     } else if (k == "chain_est") {
@@ -2970,9 +2928,6 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "bin") {
         if (value < -1 || value > 7) { set_error("bin must be -1 (auto) or 0..7"); return MRT_ERR_INVALID; }
         g_bin = value;
-    } else if (k == "bin_blocks") {
-        if (value < 1 || value > 16) { set_error("bin_blocks must be 1..16"); return MRT_ERR_INVALID; }
-        g_bin_blocks = value;
     } else if (k == "bin_dbits") {   // the pair is checked when a batch is binned (2 dbits + 3 obits = 1..12)
         if (value < 0 || value > 6) { set_error("bin_dbits must be 0..6"); return MRT_ERR_INVALID; }
         g_bin_dbits = value;
@@ -2980,8 +2935,11 @@ int mrt_set_tuning(const char* key, int value) {
         if (value < 0 || value > 4) { set_error("bin_obits must be 0..4"); return MRT_ERR_INVALID; }
         g_bin_obits = value;
     } else if (k == "walk_exit") {
-        if (value < -1 || value > 1) { set_error("walk_exit must be -1..1"); return MRT_ERR_INVALID; }
+        if (value < 0 || value > 1) { set_error("walk_exit must be 0 or 1"); return MRT_ERR_INVALID; }
         g_walk_exit = value;
+    } else if (k == "compact_leaves") {
+        if (value < 0 || value > 1) { set_error("compact_leaves must be 0 or 1"); return MRT_ERR_INVALID; }
+        g_compact_leaves = value;
     } else if (k == "lds_nodes") {
         if (value < 0 || value > 1) { set_error("lds_nodes must be 0 or 1"); return MRT_ERR_INVALID; }
         g_lds_nodes = value;

@@ -249,15 +249,6 @@ KernelFn pick_frame1(int w, bool c, bool f, bool pow, int walk) {
     return walk == 2 ? pick_frame1_walk<2>(w, c, f, pow)
                      : walk == 0 ? pick_frame1_walk<0>(w, c, f, pow) : pick_frame1_walk<1>(w, c, f, pow);
 }
-KernelFn pick_shade1(int w, bool c, bool f, bool pow) {
-    if (pow) return w == 1 ? shade1_fn<1, true>(c, f) : shade1_fn<5, true>(c, f);
-    switch (w) {
-        case 1: return shade1_fn<1, false>(c, f);
-        case 4: return shade1_fn<4, false>(c, f);
-        case 5: return shade1_fn<5, false>(c, f);
-        case 7: return shade1_fn<7, false>(c, f);
-        case 8: return shade1_fn<8, false>(c, f);
-        default: return shade1_fn<6, false>(c, f);
-    }
-}
+// (the two-launch path: fused = 0, or a caller that wants hit records) at 5 waves
+KernelFn pick_shade1(bool c, bool f, bool pow) { return pow ? shade1_fn<5, true>(c, f) : shade1_fn<5, false>(c, f); }
 }  // namespace mrt

@@ -23,13 +23,8 @@ static KernelFn adapt_direct(bool po, bool f, bool inst) {
     return f ? adaptive_kernel<false, false, true, false, REC, W> : adaptive_kernel<false, false, false, false, REC, W>;
 }
 
-KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec, int waves) {
-    if (rec == 0 && !c) {
-        switch (waves) {
-            case 6: return adapt_direct<6>(po, f, inst);   // 4 / 5 measured 6% / 1% slower on A3
-            default: break;
-        }
-    }
+KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec) {
+    if (rec == 0 && !c) return adapt_direct<6>(po, f, inst);   // 4 / 5 waves measured 6% / 1% slower on A3
     // (REC 1 / 2 kernels bounded to 2 or 3 waves still end at one: no variants)
     if (rec == 2) return pick4<AdaptK, 2>(c, po, f, inst);
     if (rec == 1) return pick4<AdaptK, 1>(c, po, f, inst);

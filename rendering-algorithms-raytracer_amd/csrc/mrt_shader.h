@@ -50,6 +50,7 @@ struct RenderParams {
     const DLeaf* leaves;
     const PrimShade* prims;
     const float4* verts;
+    const uint4* cleaves;        // compact leaf packets (tuning "compact_leaves"): per lane the 3 vertex indices
     const float4* normals;
     const DevMaterial* mats;
     const DevLight* lights;
@@ -1579,15 +1580,15 @@ struct ShadeK { static constexpr KernelFn fn = shade_kernel<C, PO, F, I, kFused,
 // defined in mrt_frame.hip: the one-point-light frame / shade kernels at an
 // occupancy target w; pow: a Blinn material with specExp != 1
 KernelFn pick_frame1(int w, bool c, bool f, bool pow, int walk);
-KernelFn pick_shade1(int w, bool c, bool f, bool pow);
+KernelFn pick_shade1(bool c, bool f, bool pow);
 // defined in mrt_rec.hip: the fused chain kernels (rec 1: reflection / refraction,
 // 2: + path tracing) and the adaptive supersampling kernels (any rec)
 KernelFn pick_shade_rec(bool c, bool po, bool f, bool inst, int rec);
-KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec, int waves);
+KernelFn pick_adaptive(bool c, bool po, bool f, bool inst, int rec);
 // defined in mrt_chain.hip: the wavefront chain engine
 KernelFn pick_chain0(bool resolve, bool po, bool inst, int rec);
 KernelFn pick_chain_shade(bool resolve, bool po, bool inst, int rec);
-KernelFn pick_chain_trace(bool c, bool f, bool inst, int waves, int step);
+KernelFn pick_chain_trace(bool c, bool f, bool inst, int step);
 KernelFn pick_chain_compact();
 KernelFn pick_chain_merge();
 KernelFn pick_chain_fallback(bool po, bool inst, int rec, bool count);

@@ -707,8 +707,8 @@ class Scene:
 
     def walk_info(self):
         """The walk of this scene's last one-light frame: {"lds_nodes": 1 (LDS top-node walk),
-        0 (plain), -1 (none yet); "walk_exits": 1 or 2 (the walk loop's form, picked per scene
-        by a probe), -1 (not probed yet)}."""
+        0 (plain), -1 (none yet); "walk_exits": 1 or 2 (the walk loop's form: one exit unless
+        tuning "walk_exit" 0 asks for the two-exit loop)}."""
         ln, wx = C.c_int32(-1), C.c_int32(-1)
         check(lib().mrt_scene_walk_info(self.handle, C.byref(ln), C.byref(wx)), "walk_info")
         return {"lds_nodes": int(ln.value), "walk_exits": int(wx.value)}

@@ -406,7 +406,10 @@ CONFIGS = {
     "C2": dict(name="bunny stand-in (69.5k tris) 1024x1024 Blinn+PointLight", W=1024, H=1024,
                camera=dict(eye=(0.0, 5.0, 15.0), lookAt=(0.0, 0.0, 0.0), up=(0, 1, 0), fov=45.0),
                lights=[dict(type="point", pos=(10.0, 20.0, 10.0), power=1000.0)],
-               material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="bunny"),
+               material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="bunny",
+               # bench.py frames in flight (one HIP stream and hardware queue each): the frame's latency is set by
+               # a few heavy top-row tiles, so 4 in flight cap the step at latency / 4 (walk exit)
+               inflight=8),
     # C3: Sponza stand-in 1920x1080, Blinn kd=1, PointLight (0,10,0) 200
     "C3": dict(name="sponza stand-in (~66k tris) 1920x1080 Blinn+PointLight", W=1920, H=1080,
                camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
@@ -458,7 +461,7 @@ CONFIGS = {
                lights=[dict(type="rect", v1=(8.0, 10.0, 2.0), v2=(8.0, 10.0, -2.0), v3=(-8.0, 10.0, 2.0),
                             power=1.5, samples=1, noise=0.001)],
                material=dict(kind="blinn", kd=(1, 1, 1), specExp=8.0, specAmt=0.25), bg=(0.0, 0.0, 0.2),
-               mesh="sponza", num_paths=16),
+               mesh="sponza", num_paths=16, inflight=8),   # 8 frames in flight: -3.5% per step (r06 hwq2)
     # C5: dragon + buddha stand-ins instanced 64x via ProxyObject (two BLASes,
     # alternating, seeded transforms) on a floor triangle, 3840x2160, DomeLight (power
     # 0.15, 6 samples, src/main.cpp:157-165) over Images/Arches_E_PineTree.hdr, the same

@@ -185,7 +185,7 @@ def test_every_kernel_path_is_exact(knobs):
         assert P.last_stats["shadow_rays"] == ref["shadow_rays"]
     finally:
         for k, v in dict(shade1=1, fast_box=1, sched=2, primary_waves=7, scalar_nodes=7, wavefront=1, fused=1,
-                         frame1_waves=7, walk_exit=-1, lds_nodes=0).items():   # the library's defaults
+                         frame1_waves=7, walk_exit=1, lds_nodes=0).items():   # the library's defaults
             L.mrt_set_tuning(k.encode(), v)
 
 
