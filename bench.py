@@ -52,7 +52,7 @@ CPU_CAL_FILE = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
 # kernel traces of the driver-settings runs (tools/step_trace.py): busy union per timed step
 STEP_TRACE_FILE = os.path.join(ROOT, "profiles", "r05_steptrace.json")
 # N > 1 split: frames of the camera path per step when --frames-per-launch is not given
-DEFAULT_FPL = 1
+DEFAULT_FPL = 8
 
 
 def parse():
@@ -90,6 +90,10 @@ def parse():
                          "through an IPC mapping (mrt_ipc_open) and one barrier per step marks the frame whole, no gather "
                          "or unpack (falls back to gather when a rank cannot map them); gather = packed float tiles, one "
                          "RCCL gather to rank 0 and its unpack")
+    ap.add_argument("--split-float", action="store_true",
+                    help="N > 1 split with --assemble ipc: rank 0's frames also hold the float RGB before Image::Map "
+                         "(12 more bytes per pixel across xGMI); by default the split assembles the reference's "
+                         "framebuffer, the 8-bit Image (src/Image.cpp:19-35)")
     ap.add_argument("--frames-per-launch", type=int, default=0,
                     help="strong split (N > 1, and --share): frames per step, the first K frames of the config's "
                          "camera path (distinct cameras; frame 0 = the headline camera), each rank's buckets of all of "
@@ -474,7 +478,8 @@ def main():
 
     def make_ipc_pipe(nf, nsplit=None, srank=None, pipe_streams=None):
         """The split with direct writes (--assemble ipc): rank 0 owns `depth` frame buffers
-        (nf frames each, float + 8-bit), exports them (mrt_ipc_export), every rank maps
+        (nf frames each: the 8-bit framebuffer, Image::m_pixels, and with --split-float the
+        float frame before Image::Map), exports them (mrt_ipc_export), every rank maps
         them (mrt_ipc_open) and renders its buckets of each step straight into buffer
         k % depth (mrt_render_batch_frames_async); one stream-ordered all-reduce of one
         int per step is the frame-end barrier (tiles.FramePipeline).  nsplit / srank: one
@@ -488,18 +493,25 @@ def main():
         items = torch.tensor(mine, dtype=torch.int32, device="cuda")
         alone = nsplit != world
         owner = alone or rank == 0
-        own = [(torch.empty(nf * H * W * 3, dtype=torch.float32, device="cuda"),
+        # per buffer: (float frames or None, 8-bit frames)
+        own = [(torch.empty(nf * H * W * 3, dtype=torch.float32, device="cuda") if args.split_float else None,
                 torch.empty(nf * H * W * 3, dtype=torch.uint8, device="cuda")) for _ in range(nb)] if owner else None
         ptrs, opened, err = [], [], ""
+
+        def ptr(t):
+            return None if t is None else t.data_ptr()
         if alone or world == 1:
-            ptrs = [(f.data_ptr(), f8.data_ptr()) for f, f8 in own]
+            ptrs = [(ptr(f), ptr(f8)) for f, f8 in own]
         else:
             obj = [None]
             if rank == 0:
                 try:
                     hs = []
-                    for f, f8 in own:
-                        for t in (f, f8):
+                    for pair in own:
+                        for t in pair:
+                            if t is None:
+                                hs.append(None)
+                                continue
                             h = _lib.mrt_ipc_handle()
                             _lib.check(L.mrt_ipc_export(C.c_void_p(t.data_ptr()), C.byref(h)), "ipc export")
                             hs.append(bytes(h))
@@ -509,14 +521,18 @@ def main():
             dist.broadcast_object_list(obj, src=0)
             try:
                 if rank == 0:
-                    ptrs = [(f.data_ptr(), f8.data_ptr()) for f, f8 in own]
+                    ptrs = [(ptr(f), ptr(f8)) for f, f8 in own]
                 elif obj[0] is None:
                     err = "rank 0 could not export its frames"
                 else:
                     for i in range(nb):
                         pair = []
                         for j in range(2):
-                            h = _lib.mrt_ipc_handle.from_buffer_copy(obj[0][2 * i + j])
+                            hb = obj[0][2 * i + j]
+                            if hb is None:
+                                pair.append(None)
+                                continue
+                            h = _lib.mrt_ipc_handle.from_buffer_copy(hb)
                             p = C.c_void_p()
                             _lib.check(L.mrt_ipc_open(C.byref(h), dev, C.byref(p)), "ipc open")
                             pair.append(p.value)
@@ -691,6 +707,7 @@ def main():
             elapsed = timed(pipe.step, pipe.flush, args.steps)
             last = (pipe.k - 1) % pipe.depth
             frame_check = check_timed_frame(own[last][0], own[last][1]) if rank == 0 else None
+            out_bytes_px = 3 + (12 if args.split_float else 0)
         else:
             pipe, render, items, mine, _ = make_pipe(n_frames, float_tiles=split)
 
@@ -737,10 +754,39 @@ def main():
             split_times = {"render_ms_max_rank": round(t_[0].item(), 4), "barrier_ms": round(t_[1].item(), 4),
                            "assemble": "ipc: every rank's kernel stores its buckets' pixels into rank 0's frames "
                                        "(mrt_ipc_open mapping, xGMI); no gather, no unpack",
-                           "remote_bytes_per_rank_max": int(max(0, len(mine)) * 1024 * 15)}
+                           "framebuffer": "RGB8 (Image::m_pixels)" + (" + float RGB" if args.split_float else ""),
+                           "remote_bytes_per_rank_max": int(max(0, len(mine)) * 1024 * out_bytes_px)}
         else:
             split_times = {"render_ms_max_rank": round(t_[0].item(), 4), "gather_ms": round(t_[1].item(), 4),
                            "assemble": assemble, "gather_bytes_per_rank": int(pipe.tiles[0].numel() * 4)}
+        # the same split at ONE frame per step (frames_per_step 1: strong scaling of a single frame,
+        # whose 1/N share cannot fill the GPU)
+        single = None
+        if n_frames > 1:
+            try:
+                if assemble == "ipc":
+                    spipe, srender_b, smine, _ = make_ipc_pipe(1)
+
+                    def srender_one(o=opts):
+                        srender_b(0, o)
+                else:
+                    spipe, srender, sitems, smine, _ = make_pipe(1, float_tiles=True)
+
+                    def srender_one(o=opts):
+                        srender(sitems, spipe.tiles[0], o)
+                _, (ssh, seye, ssec) = count_rays(lambda: srender_one(opts_count))
+                s_rays = (seye if adaptive else W * H) + ssh + ssec
+                se = timed(spipe.step, spipe.flush, args.steps)
+                single = {"value": round(s_rays * args.steps / se / 1e6, 2), "unit": "Mray/s", "scaling": "strong",
+                          "frames_per_step": 1, "steps": args.steps, "ms_per_step": round(se / args.steps * 1e3, 4),
+                          "split": "one frame (the headline camera) per step, the same split and assembly"}
+                if assemble == "ipc":
+                    torch.cuda.synchronize()
+                    dist.barrier()
+                    for p_ in spipe.opened:
+                        L.mrt_ipc_close(C.c_void_p(p_))
+            except Exception as e:   # reported, never fatal
+                single = {"error": repr(e)}
         nf_w = args.frames or min(world, 16)
         wpipe, wrender, witems, _, _ = make_pipe(nf_w, float_tiles=False)
         _, (wsh, weye, wsec) = count_rays(lambda: wrender(witems, wpipe.tiles[0], opts_count))
@@ -783,7 +829,9 @@ def main():
     chain = scenes.chain_level(cfg)
     one_light = (len(cfg["lights"]) == 1 and cfg["lights"][0]["type"] == "point" and cfg.get("num_paths", 1) == 1
                  and not cfg.get("env") and chain == 0 and not cfg.get("extra"))
-    b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=use_frame_path or split,
+    # float RGB is written by the frame path and the split's tiles; the IPC split writes the 8-bit framebuffer only
+    float_out = use_frame_path or (split and (assemble != "ipc" or args.split_float))
+    b_prim, b_shade = kernel_bytes(st, px_mine, hits_mine, float_out=float_out,
                                    wavefront=not one_light and chain == 0)
     if chain:   # each secondary / GI hit gathers its PrimShade + 3 vertices + 3 normals (+ its level record)
         b_shade += second_mine * (16 + 32 + 3 * 16 + 3 * 16 + 12)
@@ -796,7 +844,7 @@ def main():
         dom, dom_key, dom_ms = ("frame1_kernel (camera rays + closest hit + shading + any-hit shadow rays, "
                                 "one launch)"), "primary", pm
         dom_b = (st["node_visits"] * NODE_B + st["leaf_visits"] * LEAF_B
-                 + px_mine * ((12 if use_frame_path or split else 0) + 3) + hits_px * (32 + 3 * 16 + 3 * 16))
+                 + px_mine * ((12 if float_out else 0) + 3) + hits_px * (32 + 3 * 16 + 3 * 16))
     elif adaptive and st.get("chain"):   # adaptive passes, each a chain-engine tree walk (G3)
         dom, dom_key, dom_ms, dom_b = ("chain engine, adaptive passes (per pass: unit_eye + per level chain gen + compact "
                                        "+ chain_trace + resolve, per-level folds, adapt_combine)"), "shade", sm, b_shade
@@ -998,6 +1046,8 @@ def main():
         out["split_times"] = split_times
     if weak is not None:
         out["weak"] = weak
+    if world > 1 and split and n_frames > 1:
+        out["single_frame"] = single
     if not args.no_cpu_baseline and world == 1:
         try:
             out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
@@ -1151,8 +1201,9 @@ def share_mode(args, E, widths):
             del pipe
         slow = max(per_rank, key=lambda x: x["ms_per_step"])
         if ipc:
-            # rank r > 0's pixels cross its xGMI link as stores: float RGB + RGB8 per pixel, per frame
-            link_b = max(x["pixels"] for x in per_rank[1:]) * 15 / K if N > 1 else 0
+            # rank r > 0's pixels cross its xGMI link as stores, per frame
+            bpp = 3 + (12 if args.split_float else 0)   # RGB8 framebuffer (+ float RGB with --split-float)
+            link_b = max(x["pixels"] for x in per_rank[1:]) * bpp / K if N > 1 else 0
             link_ms = link_b / (args.xgmi_gbs * 1e9) * 1e3
             bar_ms = args.xgmi_lat_us * 1e-3 / max(1, len(share_streams) - 1) / K
             step_ms = max(slow["ms_per_step"], link_ms, bar_ms)

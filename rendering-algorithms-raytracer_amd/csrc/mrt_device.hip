@@ -74,7 +74,6 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
            P.gstack + (blockIdx.x * kWG + tid), P.gstride};
     T.inst = P.insts;
     trav_alpha(T, P);
-    if (INST && REFILL) { T.cleaves = P.cleaves; T.cverts = P.verts; }
     TravStats st;
     unsigned long long wave_steps = 0;
     if (P.ch_ovf && *P.ch_ovf) return;   // a chain chunk past its estimated capacity (redone by its fallback)
@@ -90,7 +89,11 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
     const uint32_t m = (uint32_t)P.max_shadow, nr32 = (uint32_t)n_rays;
     auto valid = [&](size_t e64) {
         if (perm) return e64 < n_rays;
-        const uint32_t e = (uint32_t)e64, px = e / m;
+        // m through an empty asm: the division's reciprocal is formed here, per dequeue, instead of
+        // once before the loop and held across the walk (it was the kernel's one spilled value)
+        uint32_t mm = m;
+        asm volatile("" : "+s"(mm));
+        const uint32_t e = (uint32_t)e64, px = e / mm;
         return e64 < n_rays && e < nr32 && e - px * m < (uint32_t)P.nrays[px];
     };
     auto slot_at = [&](size_t c) -> size_t { return perm ? (size_t)perm[c] : c; };
@@ -151,7 +154,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
     } else {   // lane refill
         bool exhausted = false;   // wave-uniform
         bool active = false;
-        size_t e = 0;
+        uint32_t e = 0;   // the lane's ray slot (n_rays < 2^32, checked on the host): one VGPR, not two
         float tmax = 0.f;
         AnyState as{};
         for (;;) {
@@ -165,7 +168,7 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
                     const size_t c = first + (size_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                     if (c < end && valid(c)) {
-                        e = slot_at(c);
+                        e = (uint32_t)slot_at(c);
                         const float4 o = P.ray_o[e], d = P.ray_d[e];
                         as.q = make_ray(mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), d.w);
                         tmax = o.w;
@@ -379,7 +382,6 @@ struct DeviceState {
     int device = -1;
     QNode* nodes = nullptr;
     DLeaf* leaves = nullptr;
-    uint4* cleaves = nullptr;     // compact leaf packets: per lane the triangle's 3 vertex indices (tuning compact_leaves)
     PrimShade* prims = nullptr;
     float4* verts = nullptr;
     float4* normals = nullptr;
@@ -457,7 +459,8 @@ static int g_shadow_sched = -1;   // shadow_kernel schedule: 0 grid-stride, 1 XC
 // shadow_kernel's launch-bounds occupancy target is 8 waves (C4 / C5 -5.5% against none)
 static int g_primary_inst_waves = 5;   // primary kernel of special-leaf scenes: 1 (none), 5, 6 (r02: 6 beat 1 by 5% on C5;
                                        // r03: 5 = 6 within 0.3% with binned shadow rays, and 96 VGPRs spill less)
-// the resolve pass (kernel 2c) of dome-light scenes runs at 4 waves (D1 -4%, C5 -1.2 ms);
+// the resolve pass (kernel 2c) of dome-light scenes runs at 4 waves (D1 -4%, C5 -1.2 ms against none;
+// special-leaf scenes at 3, without scratch);
 // the direct-lighting adaptive kernel at 6 (unbounded it takes 256 VGPRs: A3 30.7 -> 12.8 ms)
 static int g_adapt_refill = 32;   // adaptive_kernel pixel refill: idle lanes that trigger a dequeue (0: tiles; 32: A3 -13%)
 static int g_chain_shadow_step = 0;   // instanced chain levels: shadow rays walk with anyhit_step_inst (deferred proxies)
@@ -484,8 +487,6 @@ static int g_walk_exit = 1;       // the walk loop of frame1_kernel / primary_ke
 static int g_lds_nodes = 0;       // frame1_kernel's LDS top-node walk (LN), 0 off / 1 on: with 4 frames in flight C2
                                   // -4.1%, C3 +9%, C3L +11% (profiles/r05_lds_nodes_ab_*.txt); no probe separated them
                                   // reliably (single-frame kernel times are equal on C2), so it is off unless asked for
-static int g_compact_leaves = 0;  // instanced any-hit shadow walks (lane refill) read compact leaf packets: the
-                                  // three vertex indices per lane and the shared vertices (A/B, round 6)
 static int g_frame1_waves = 7;    // frame1_kernel launch-bounds occupancy target: 1 (none), 5..8 (7: -0.9% per frame with
                                   // 4 frames in flight, +0.8% single-frame latency; profiles/r03_c3_scalar_waves_ab.txt)
 static int g_bin = -1;            // ray binning (mrt_bin.h) before tracing: bit 0 the wavefront shadow pass (kernel 2b),
@@ -538,7 +539,7 @@ static void free_device(DeviceState* d) {
     }
     if (d->g_tiles) (void)hipFree(d->g_tiles);
     if (d->g_items) (void)hipFree(d->g_items);
-    void* ptrs[] = {d->nodes, d->leaves, d->cleaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts,
+    void* ptrs[] = {d->nodes, d->leaves, d->prims, d->verts, d->normals, d->mats, d->lights, d->domes, d->insts,
                     d->inst_hit_base, d->inst_class, d->inst_cell, d->tables,
                     d->gamma, d->gammaF, d->d_rgb, d->d_rgb8, d->texs, d->puv, d->uvs, d->tans, d->btans,
                     d->pflags, d->verts2};
@@ -705,7 +706,6 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     if (n_leaves >= (size_t(1) << 27)) { set_error("too many leaf packets"); return MRT_ERR_OVERFLOW; }
     std::vector<QNode> DN;
     std::vector<DLeaf> DL;
-    std::vector<uint4> CL;   // compact leaf packets (parallel to DL)
     auto append = [&](const std::vector<QNode>& nodes, const std::vector<QLeaf>& leaves,
                       const std::vector<int32_t>* oi, const Blas* B) -> int32_t {
         const int32_t nb = (int32_t)DN.size(), lb = (int32_t)DL.size();
@@ -738,17 +738,6 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
                 for (int c = 0; c < 9; c++) D.tri[k][c] = L.t[4 * c + k];
                 const int32_t pi = proxy_of(L.prim[k]);
                 D.prim[k] = pi >= 0 ? -2 - pi : L.prim[k];
-                // the lane's vertices (make_leaf: A = v0, e0 = v1 - v0, e1 = v2 - v0), as global vertex
-                // indices; proxy and motion-blurred lanes (no triangle data in the packet) and empty lanes: 0
-                uint4 ix = make_uint4(0u, 0u, 0u, 0u);
-                const int32_t p = L.prim[k];
-                const int32_t mesh = p < 0 || pi >= 0 ? -1 : B ? B->obj_mesh[(size_t)p] : (oi && !mb_obj(p)) ? s.obj_mesh[(size_t)p] : -1;
-                if (mesh >= 0) {
-                    const size_t tri = (size_t)(B ? B->obj_tri[(size_t)p] : s.obj_tri[(size_t)p]);
-                    const uint32_t* f = &s.meshes[(size_t)mesh].vidx[3 * tri];
-                    ix = make_uint4(vbase[(size_t)mesh] + f[0], vbase[(size_t)mesh] + f[1], vbase[(size_t)mesh] + f[2], 0u);
-                }
-                CL.push_back(ix);
             }
             DL.push_back(D);
         }
@@ -837,7 +826,6 @@ static int upload_scene(Scene& s, DeviceState& d, int device) {
     }
     d.n_world = (int)s.obj_mesh.size();
     if ((rc = upload(d.leaves, DL.data(), DL.size() * sizeof(DLeaf), total))) return rc;
-    if ((rc = upload(d.cleaves, CL.data(), CL.size() * sizeof(uint4), total))) return rc;
     if ((rc = upload(d.prims, PS.data(), PS.size() * sizeof(PrimShade), total))) return rc;
     if ((rc = upload(d.verts, V.data(), V.size() * sizeof(float4), total))) return rc;
     if ((rc = upload(d.normals, N.data(), N.size() * sizeof(float4), total))) return rc;
@@ -1010,7 +998,6 @@ static void fill_params(const Scene& s, RenderParams& P) {
     P.env_h = d.env ? s.textures[s.env_tex].H : 0;
     P.env_exposure = s.env_exposure;
     P.gstride = d.gthreads;
-    P.cleaves = g_compact_leaves ? d.cleaves : nullptr;
     P.bg[0] = s.bg[0]; P.bg[1] = s.bg[1]; P.bg[2] = s.bg[2];
     P.n_lights = (int32_t)s.lights.size();
     P.num_paths = s.num_paths;
@@ -1196,7 +1183,9 @@ static KernelFn pick_primary(int w, bool c, bool f, bool inst, bool check = true
 template <int MODE>
 static KernelFn shade_mode_fn(bool c, bool po, bool inst, bool bound = false) {   // kGen / kResolve: no traversal, FAST unused
     if (!c && MODE == kResolve && bound) {
-        if (inst) return shade_kernel<false, false, false, true, MODE, 0, 4>;
+        // special-leaf scenes at 3 waves: 168 VGPRs and no scratch (152 B / 40 spills at 4 waves);
+        // C5's resolve pass -0.7% (profiles/r06_c5_resolve_waves_ab.txt)
+        if (inst) return shade_kernel<false, false, false, true, MODE, 0, 3>;
         return po ? shade_kernel<false, true, false, false, MODE, 0, 4> : shade_kernel<false, false, false, false, MODE, 0, 4>;
     }
     if (inst) return c ? shade_kernel<true, false, false, true, MODE> : shade_kernel<false, false, false, true, MODE>;
@@ -2937,9 +2926,6 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "walk_exit") {
         if (value < 0 || value > 1) { set_error("walk_exit must be 0 or 1"); return MRT_ERR_INVALID; }
         g_walk_exit = value;
-    } else if (k == "compact_leaves") {
-        if (value < 0 || value > 1) { set_error("compact_leaves must be 0 or 1"); return MRT_ERR_INVALID; }
-        g_compact_leaves = value;
     } else if (k == "lds_nodes") {
         if (value < 0 || value > 1) { set_error("lds_nodes must be 0 or 1"); return MRT_ERR_INVALID; }
         g_lds_nodes = value;

@@ -85,10 +85,6 @@ struct Trav {
     const float4* verts2 = nullptr;
     bool near_first = false;   // any-hit walks descend into the nearest hit child first (order-free answer)
     const QNode* lnodes = nullptr;   // LN walks: nodes 0 .. kLdsNodes - 1 (the hierarchy's top levels) in LDS
-    // compact leaf packets (anyhit_step_inst): lane k of leaf l = cleaves[4 l + k], the triangle's three
-    // vertex indices into cverts; nullptr: the 160-B DLeaf triangles
-    const uint4* cleaves = nullptr;
-    const float4* cverts = nullptr;
 };
 
 struct TravStats {
@@ -681,21 +677,6 @@ __device__ __forceinline__ bool anyhit_step(const Trav& c, const DRay& r, float 
 // world ray is rebuilt from its slot (one ray in registers, not two).  Every
 // box and triangle test is traverse_impl's.  CHECK: the scene has alpha-mapped
 // or motion-blurred lanes (child-word bit 3).
-// intersect4's lane k of leaf `leaf` from a compact packet: the triangle's vertices
-// A, B, C by index, its edges recomputed as buildTriBundle stores them -- e0 = B - A,
-// e1 = C - A, single float subtractions of the same loaded vertices
-// (src/BVH.cpp:86-94; host_build.cpp make_leaf) -- so the nine values, and every
-// test after them, are the DLeaf packet's bit for bit.  A ProxyObject / MBObject
-// lane's indices are 0 (a degenerate triangle: det = 0 rejects it, as the zero
-// triangle does; such lanes are never tested here).
-__device__ __forceinline__ bool tri_test_compact(const Trav& c, uint32_t leaf, int k, const DRay& r, float tMin,
-                                                 float tBest, float& t, float& a, float& b) {
-    const uint4 ix = c.cleaves[(size_t)leaf * 4 + (uint32_t)k];
-    const float4 A = c.cverts[ix.x], B = c.cverts[ix.y], C = c.cverts[ix.z];
-    const float T[9] = {A.x, A.y, A.z, B.x - A.x, B.y - A.y, B.z - A.z, C.x - A.x, C.y - A.y, C.z - A.z};
-    return tri_test(T, r, tMin, tBest, t, a, b, c.rcpT);
-}
-
 struct AnyState {
     DRay q;        // the current ray: the world ray, or the object-space ray inside an instance
     int32_t cur;   // node to visit; -1: leave the instance; <= -2: enter instance -2 - cur
@@ -704,7 +685,7 @@ struct AnyState {
 };
 template <bool COUNT, bool FAST, bool CHECK>
 __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, float tMax, AnyState& s,
-                                                 const float4* ray_o, const float4* ray_d, size_t e, bool& hit,
+                                                 const float4* ray_o, const float4* ray_d, uint32_t e, bool& hit,
                                                  TravStats& st) {
     // Leaving and entering an instance share the step with the node visit that
     // follows, so every lane runs the same box test in every step (no step in
@@ -783,8 +764,6 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
                          ? mb_tri_test(c, pm, q, tMin, tMax, t, a, b)
                          : tri_test(c.leaves[leaf].tri[k], q, tMin, tMax, t, a, b, c.rcpT);
                 ok = ok && !alpha_rejects(c, leaf, k, a, b, s.aoff < 0 ? 0 : s.aoff);
-            } else if (c.cleaves) {
-                ok = tri_test_compact(c, leaf, k, q, tMin, tMax, t, a, b);
             } else {
                 ok = tri_test(c.leaves[leaf].tri[k], q, tMin, tMax, t, a, b, c.rcpT);
             }

@@ -50,7 +50,6 @@ struct RenderParams {
     const DLeaf* leaves;
     const PrimShade* prims;
     const float4* verts;
-    const uint4* cleaves;        // compact leaf packets (tuning "compact_leaves"): per lane the 3 vertex indices
     const float4* normals;
     const DevMaterial* mats;
     const DevLight* lights;

@@ -244,6 +244,8 @@ class FramePipeline:
             for j in range(self.consumed + 1, self.k):
                 self._consume(j)
         for j, w in sorted(self.works.items()):
+            if w is None:   # (a share rendered alone: no barrier)
+                continue
             with self._on(j % self.depth):
                 w.wait()
         self.works.clear()
