@@ -471,9 +471,10 @@ int mrt_debug_wave_log(const mrt_scene* s, int launch, uint64_t* out, int32_t ma
 int mrt_device_wall_clock_khz(const mrt_scene* s);
 
 /* Numerics probes (x86 RCPSS/RSQRTSS emulation + one Newton step, SSE.h:67-101). */
-/* The device's acosf(x) (fn 0) / atan2f(y, x) (fn 1) over n host inputs (a kernel on
- * the current device; glibc's fdlibm code restated, csrc/mrt_libm.h), or its rcp_nr(x)
- * (fn 2: the RCPSS emulation and Newton step of every triangle test; y unused). */
+/* The device's acosf(x) (fn 0) / atan2f(y, x) (fn 1) / sinf(x) (fn 3) / cosf(x) (fn 4) /
+ * powf(x, y) (fn 5) over n host inputs (a kernel on the current device; glibc's code
+ * restated, csrc/mrt_libm.h), or its rcp_nr(x) (fn 2: the RCPSS emulation and Newton step
+ * of every triangle test; y unused). */
 int mrt_debug_libm(int fn, const float* x, const float* y, size_t n, float* out);
 float mrt_rcp_nr(float x);
 float mrt_rsqrt_nr(float x);

@@ -66,11 +66,14 @@ static inline float std_min(float a, float b) { return b < a ? b : a; }   /* std
 static inline float std_max(float a, float b) { return a < b ? b : a; }   /* std::max */
 
 float oro_x86_rcp(float x) { return x86_rcp(x); }
-/* glibc's acosf (fn 0) / atan2f(y, x) (fn 1): the float overloads the reference
- * calls (src/Material.h:51, src/Texture.cpp:82-93), for the device probe's test */
+/* glibc's acosf (fn 0) / atan2f(y, x) (fn 1) / sinf (3) / cosf (4) / powf(x, y) (5): the
+ * float overloads the reference calls (src/Material.h:51, src/Texture.cpp:82-93,
+ * src/Material.cpp:41, src/Blinn.cpp:219), for the device probe's test */
 int oro_libm_eval(int fn, size_t n, const float* x, const float* y, float* out) {
-    if (fn != 0 && fn != 1) return -1;
-    for (size_t i = 0; i < n; i++) out[i] = fn == 0 ? acosf(x[i]) : atan2f(y[i], x[i]);
+    if (fn < 0 || fn > 5 || fn == 2) return -1;
+    for (size_t i = 0; i < n; i++)
+        out[i] = fn == 0 ? acosf(x[i]) : fn == 1 ? atan2f(y[i], x[i]) : fn == 3 ? sinf(x[i]) : fn == 4 ? cosf(x[i])
+                                                                                             : powf(x[i], y[i]);
     return 0;
 }
 float oro_x86_rsqrt(float x) { return x86_rsqrt(x); }

@@ -22,18 +22,20 @@ _lib = None
 #               (sin(acosf(x)) -> sinf, pow(float, float) -> powf, cos/sin of floats ->
 #               cosf/sinf; src/Material.h:51, src/Blinn.cpp:219, src/Material.cpp:41), glibc
 #               here: the reference's own calls;
-#   "device" -- the same functions evaluated in double and rounded once, the HIP
-#               device's convention (bit-exact comparisons of everything around them).
+#   "double" -- the same functions evaluated in double and rounded once (round 5's
+#               device convention; tools/libm_parity.py measures how far it moves a
+#               frame).
 # atan2 / acos (src/Texture.cpp:82-93, the acosf of src/Material.h:51) are glibc's
-# atan2f / acosf in both: the device restates them bit-exactly (csrc/mrt_libm.h).
-LIBM_FLOAT, LIBM_DEVICE = "float", "device"
+# atan2f / acosf in both.  The HIP device restates all five glibc functions bit for
+# bit (csrc/mrt_libm.h; since round 6 sinf / cosf / powf too), so it equals "float".
+LIBM_FLOAT, LIBM_DOUBLE = "float", "double"
 _default_libm = LIBM_FLOAT
 
 
 def set_default_libm(mode):
     """Convention for render / texture_lookup_dir calls that do not name one; returns the previous."""
     global _default_libm
-    if mode not in (LIBM_FLOAT, LIBM_DEVICE):
+    if mode not in (LIBM_FLOAT, LIBM_DOUBLE):
         raise ValueError(mode)
     prev, _default_libm = _default_libm, mode
     return prev
@@ -41,7 +43,7 @@ def set_default_libm(mode):
 
 def _apply_libm(mode):
     mode = mode or _default_libm
-    if mode not in (LIBM_FLOAT, LIBM_DEVICE):
+    if mode not in (LIBM_FLOAT, LIBM_DOUBLE):
         raise ValueError(mode)
     lib().oro_set_libm(1 if mode == LIBM_FLOAT else 0)
 
@@ -436,7 +438,7 @@ class OracleScene:
 
     def render(self, cam, W, H, rect=None, threads=1, want_hits=True, libm=None):
         """cam: dict(eye, lookAt, up, fov[, aperture, focusPlane, shutterSpeed]).  Returns dict of numpy arrays.
-        libm: LIBM_FLOAT / LIBM_DEVICE (None: the module default, set_default_libm)."""
+        libm: LIBM_FLOAT / LIBM_DOUBLE (None: the module default, set_default_libm)."""
         _apply_libm(libm)
         c = Camera(_v3(cam["eye"]), _v3(cam.get("up", (0, 1, 0))), _v3(cam["lookAt"]), float(cam["fov"]),
                    float(cam.get("aperture", 0.0)), float(cam.get("focusPlane", 1.0)),
@@ -460,13 +462,14 @@ class OracleScene:
 
 
 def libm_eval(fn, x, y=None):
-    """glibc acosf(x) ("acos") or atan2f(y, x) ("atan2"), elementwise."""
+    """glibc acosf(x) ("acos"), atan2f(y, x) ("atan2"), sinf / cosf(x) ("sin" / "cos") or
+    powf(x, y) ("pow"), elementwise."""
     x = np.ascontiguousarray(x, np.float32)
     y = np.ascontiguousarray(np.zeros_like(x) if y is None else y, np.float32)
     out = np.empty_like(x)
     L = lib()
     L.oro_libm_eval.argtypes = [C.c_int, C.c_size_t, _fp, _fp, _fp]
-    if L.oro_libm_eval({"acos": 0, "atan2": 1}[fn], len(x), _p(x, _fp), _p(y, _fp), _p(out, _fp)) != 0:
+    if L.oro_libm_eval({"acos": 0, "atan2": 1, "sin": 3, "cos": 4, "pow": 5}[fn], len(x), _p(x, _fp), _p(y, _fp), _p(out, _fp)) != 0:
         raise ValueError(fn)
     return out
 

@@ -214,12 +214,14 @@ __global__ void __launch_bounds__(kWG, MINW) shadow_kernel(RenderParams P, size_
 }
 
 
-// Numerics probe (mrt_debug_libm): the device's acosf / atan2f (mrt_libm.h) and
-// rcp_nr (RCPSS emulation + Newton step, mrt_math.h; table from global memory).
+// Numerics probe (mrt_debug_libm): the device's acosf / atan2f / sinf / cosf / powf
+// (mrt_libm.h) and rcp_nr (RCPSS emulation + Newton step, mrt_math.h; table from global
+// memory).
 __global__ void __launch_bounds__(256) libm_kernel(int fn, const float* x, const float* y, size_t n, float* out,
                                                    const uint16_t* rcpT) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
-        out[i] = fn == 0 ? fd_acosf(x[i]) : fn == 1 ? fd_atan2f(y[i], x[i]) : rcp_nr(x[i], rcpT);
+        out[i] = fn == 0 ? fd_acosf(x[i]) : fn == 1 ? fd_atan2f(y[i], x[i]) : fn == 2 ? rcp_nr(x[i], rcpT)
+               : fn == 3 ? gl_sinf(x[i]) : fn == 4 ? gl_cosf(x[i]) : gl_powf(x[i], y[i]);
 }
 
 // Batched Scene::trace: one lane per query ray.
@@ -2940,7 +2942,7 @@ int mrt_set_tuning(const char* key, int value) {
 }
 
 int mrt_debug_libm(int fn, const float* x, const float* y, size_t n, float* out) {
-    if (fn < 0 || fn > 2 || !x || !out || (fn == 1 && !y)) { set_error("bad libm probe arguments"); return MRT_ERR_INVALID; }
+    if (fn < 0 || fn > 5 || !x || !out || ((fn == 1 || fn == 5) && !y)) { set_error("bad libm probe arguments"); return MRT_ERR_INVALID; }
     int nd = 0;
     if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) { set_error("no HIP device"); return MRT_ERR_NO_DEVICE; }
     if (n == 0) return MRT_OK;
@@ -2954,7 +2956,7 @@ int mrt_debug_libm(int fn, const float* x, const float* y, size_t n, float* out)
         HIP_OK(hipMalloc((void**)&dout, b));
         HIP_OK(hipMalloc((void**)&dt, 2048 * sizeof(uint16_t)));
         HIP_OK(hipMemcpy(dx, x, b, hipMemcpyHostToDevice));
-        if (fn == 1) HIP_OK(hipMemcpy(dy, y, b, hipMemcpyHostToDevice));
+        if (fn == 1 || fn == 5) HIP_OK(hipMemcpy(dy, y, b, hipMemcpyHostToDevice));
         HIP_OK(hipMemcpy(dt, host_rcp_table(), 2048 * sizeof(uint16_t), hipMemcpyHostToDevice));
         const int blocks = (int)std::min<size_t>((n + 255) / 256, 65536);
         hipLaunchKernelGGL(libm_kernel, dim3(blocks), dim3(256), 0, 0, fn, dx, dy, n, dout, dt);

@@ -45,7 +45,9 @@ MRT_HD uint32_t tbl_bits(uint16_t e) { return 0x3F000000u | ((uint32_t)e << 11);
 // formed as (s | 253 << 23 | entry << 11) - (e << 23) (no borrow reaches the
 // mantissa or the sign); e >= 253 (and inf) -> +-0; zero / denormal -> +-inf;
 // NaN -> quiet NaN.  (Round 5: 5 fewer VALU ops per triangle test than testing e
-// and m separately; exhaustively equal, tests/test_numerics.py.)
+// and m separately; equal to the table emulation on every 61st float bit pattern on the
+// CPU and every 257th on the GPU, tests/test_numerics.py; the tables themselves are
+// checked against the live instructions on all 2^32 inputs, tools/gen_x86_tables.c.)
 MRT_HD float x86_rcp(float x, const uint16_t* T) {
     const uint32_t u = f2u(x), a = u & 0x7FFFFFFFu, s = u & 0x80000000u;
     uint32_t t = T[(a >> 12) & 0x7FFu];

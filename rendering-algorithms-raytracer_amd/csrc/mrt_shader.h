@@ -172,12 +172,10 @@ struct RenderParams {
     uint32_t* ch_est;
 };
 
-// pow(spec, specExp) of Blinn::shade (src/Blinn.cpp:219-220; libm powf in the
-// reference).  Evaluated in double and rounded once: the correctly rounded
-// result in all but a vanishing fraction of inputs, where libm powf (<= 1 ulp)
-// may differ by one ulp -- the configs with specAmt > 0 are therefore checked
-// against the oracle to 1e-4 relative (north_star), everything else bit-exact.
-__device__ __forceinline__ float spec_pow(float x, float e) { return (float)pow((double)x, (double)e); }
+// pow(spec, specExp) of Blinn::shade (src/Blinn.cpp:219-220): glibc's powf, which the
+// reference's float call resolves to, restated bit for bit (gl_powf, mrt_libm.h; round 6 --
+// round 5 evaluated it in double and rounded once, within 1 ulp of glibc's)
+__device__ __forceinline__ float spec_pow(float x, float e) { return gl_powf(x, e); }
 
 // operator*(Matrix4x4, Vector3) (src/Matrix4x4.h:693-704) on rows 0-2 of T (stride 4)
 __device__ __forceinline__ v3 xform_dir3(const float* T, v3 u) {
@@ -659,20 +657,20 @@ struct Shader {
         return scale(result, 1.0f / (float)P.num_paths);
     }
 
-    // Material::fresnel, full form (src/Material.h:47-55): n1*sin(acosf(c))/n2.
-    // acosf is glibc's (fd_acosf, bit-exact); sinf is evaluated in double and rounded
-    // once (glibc's sinf is within 0.56 ulp of that; tools/libm_parity.py)
+    // Material::fresnel, full form (src/Material.h:47-55): n1*sin(acosf(c))/n2, glibc's
+    // acosf and sinf restated bit for bit (fd_acosf, gl_sinf: mrt_libm.h)
     __device__ static float fresnel(float n1, float n2, float c) {
         const float n1CosTh = n1 * c;
         const float th = fd_acosf(c);
-        const float n1_n2SinTh = (n1 * (float)sin((double)th)) / n2;
+        const float n1_n2SinTh = (n1 * gl_sinf(th)) / n2;
         const float n2CosTh = n2 * std_max(0.0f, sqrtf(1.0f - n1_n2SinTh * n1_n2SinTh));
         const float Rs = (n1CosTh - n2CosTh) / (n1CosTh + n2CosTh);
         return Rs * Rs;
     }
 
     // Material::getCosineDistributedSamples (src/Material.cpp:14-41): two draws,
-    // RSQRTSS/RCPSS square roots, libm cos / sin in double rounded once
+    // RSQRTSS/RCPSS square roots, glibc's cosf / sinf of the float 2 pi e1 (gl_cosf /
+    // gl_sinf, bit for bit)
     __device__ v3 cosine_sample(v3 N) {
         const float e1 = next_rand();
         float e2 = next_rand();
@@ -683,7 +681,7 @@ struct Shader {
         const float t = (2.0f * 3.1415926f) * e1;
         const float sqrte2 = rcp_nr(rsqrt_nr(e2, rsqT), rcpT);
         const float sqrt1_e2 = rcp_nr(rsqrt_nr(fabsf(1.0f - e2), rsqT), rcpT);
-        const float c = (float)cos((double)t), s = (float)sin((double)t);
+        const float c = gl_cosf(t), s = gl_sinf(t);
         return normalized(add(add(scale(u, c * sqrte2), scale(v, s * sqrte2)), scale(N, sqrt1_e2)), rsqT);
     }
 

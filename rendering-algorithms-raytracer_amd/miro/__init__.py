@@ -48,13 +48,13 @@ def rsqrt_nr(x: float) -> float:
 
 
 def debug_libm(fn: str, x, y=None):
-    """The device's acosf(x) ("acos") / atan2f(y, x) ("atan2") / rcp_nr(x) ("rcp_nr")
-    (numerics probe)."""
+    """The device's acosf(x) ("acos") / atan2f(y, x) ("atan2") / sinf(x) ("sin") / cosf(x)
+    ("cos") / powf(x, y) ("pow") / rcp_nr(x) ("rcp_nr") (numerics probe)."""
     import numpy as np
     x = np.ascontiguousarray(x, np.float32)
     y = np.ascontiguousarray(np.zeros_like(x) if y is None else y, np.float32)
     out = np.empty_like(x)
-    _lib.check(lib().mrt_debug_libm({"acos": 0, "atan2": 1, "rcp_nr": 2}[fn], x.ctypes.data, y.ctypes.data, len(x),
+    _lib.check(lib().mrt_debug_libm({"acos": 0, "atan2": 1, "rcp_nr": 2, "sin": 3, "cos": 4, "pow": 5}[fn], x.ctypes.data, y.ctypes.data, len(x),
                                     out.ctypes.data), "mrt_debug_libm")
     return out
 

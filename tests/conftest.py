@@ -23,14 +23,11 @@ def golden():
 
 
 @pytest.fixture(scope="session", autouse=True)
-def _oracle_device_libm():
-    """The oracle's default libm convention is the reference's (glibc sinf / cosf / powf,
-    oracle.LIBM_FLOAT).  The bit-exact GPU-vs-oracle tests compare under the device's
-    convention for those three functions (double, rounded once: oracle.LIBM_DEVICE) --
-    atan2f / acosf are glibc's in both (csrc/mrt_libm.h).  Tests that compare against
-    the reference's convention pass libm=oracle.LIBM_FLOAT explicitly and hold the
-    north_star tolerance (tests/test_full_size.py, tests/test_final_scene.py)."""
+def _oracle_reference_libm():
+    """Every GPU-vs-oracle comparison uses the reference's libm convention (glibc's atan2f /
+    acosf / sinf / cosf / powf, oracle.LIBM_FLOAT): the device restates those five functions
+    bit for bit (csrc/mrt_libm.h, pinned by tests/test_libm.py)."""
     import oracle
-    prev = oracle.set_default_libm(oracle.LIBM_DEVICE)
+    prev = oracle.set_default_libm(oracle.LIBM_FLOAT)
     yield
     oracle.set_default_libm(prev)

@@ -1,11 +1,15 @@
-"""The reference's float libm calls on the lookup / Fresnel path (atan2f / acosf,
-src/Texture.cpp:82-93, src/Material.h:51) against the device's restatement of glibc's
-fdlibm code (csrc/mrt_libm.h).
+"""The reference's float libm calls (atan2f / acosf of the lat-long lookups,
+src/Texture.cpp:82-93; sinf(acosf(c)) of Fresnel, src/Material.h:51; cosf / sinf of the
+cosine sampler, src/Material.cpp:41; powf of Blinn's specular lobe, src/Blinn.cpp:219)
+against the device's restatements of glibc 2.35 (csrc/mrt_libm.h: fdlibm atan2f / acosf;
+the optimized-routines sinf / cosf / powf of the x86-64 FMA build).
 
-CPU: the restatement, compiled for the host with the device's flags (-ffp-contract=off),
-equals the host libm on every one of the 2^32 acosf inputs and on 2^24 seeded atan2f
-pairs plus the special values.  GPU: the same functions run on the device (the
-mrt_debug_libm probe) equal the oracle's glibc calls on 2^22 inputs each."""
+CPU: the restatements, compiled for the host with the device's flags (-ffp-contract=off;
+the FMA build's contractions are explicit fma() calls), equal the host libm on every one
+of the 2^32 acosf, sinf and cosf inputs, on 2^24 seeded atan2f pairs plus the special
+values, and on powf over 2^22 seeded pairs, the special values and every float in [0, 1]
+for the specular exponents of the scenes.  GPU: the same functions on the device
+(the mrt_debug_libm probe) equal the oracle's glibc calls on 2^22 inputs each."""
 import os
 import subprocess
 
@@ -38,13 +42,43 @@ def test_acosf_all_inputs(harness):
     assert sum(int(o.split()[1]) for o in outs) == 1 << 32
 
 
+@pytest.mark.parametrize("fn", ["sin", "cos"])
+def test_sincosf_all_inputs(harness, fn):
+    """sinf / cosf over all 2^32 bit patterns (every reduction branch: the polynomial
+    below pi / 4, reduce_fast below 120, reduce_large above), 8 ranges side by side."""
+    step = 1 << 29
+    procs = [subprocess.Popen([harness, fn, str(lo), str(lo + step)], stdout=subprocess.PIPE, text=True)
+             for lo in range(0, 1 << 32, step)]
+    outs = [p.communicate()[0] for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o
+    assert sum(int(o.split()[1]) for o in outs) == 1 << 32
+
+
+def test_powf_pairs(harness):
+    out = subprocess.run([harness, "pow", str(1 << 22), "4242"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+
+
+def test_powf_unit_interval(harness):
+    """powf(x, e) for every float in [0, 1] (the lobe's base, r.l clamped at 0) and the
+    specular exponents the scenes use, 8 ranges side by side."""
+    hi = 0x3F800001
+    step = -(-hi // 8)
+    procs = [subprocess.Popen([harness, "powx", str(lo), str(min(hi, lo + step)), "2", "8", "10", "32"],
+                              stdout=subprocess.PIPE, text=True) for lo in range(0, hi, step)]
+    outs = [p.communicate()[0] for p in procs]
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o
+
+
 def test_atan2f_pairs(harness):
     out = subprocess.run([harness, "atan2", str(1 << 24), "12345"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fn", ["acos", "atan2"])
+@pytest.mark.parametrize("fn", ["acos", "atan2", "sin", "cos", "pow"])
 def test_device_libm_equals_glibc(fn):
     if miro.device_count() < 1:
         pytest.skip("no HIP device")
@@ -55,6 +89,17 @@ def test_device_libm_equals_glibc(fn):
         x = np.concatenate([pos.view(np.float32), (pos | 0x80000000).view(np.float32),
                             rng.uniform(-1.1, 1.1, n).astype(np.float32)])
         y = np.zeros_like(x)
+    elif fn in ("sin", "cos"):   # every 2^10-th bit pattern (both signs, every branch), then [0, 2 pi)
+        pos = np.arange(0, 0x7F800000, 1024, dtype=np.uint32)
+        x = np.concatenate([pos.view(np.float32), (pos | 0x80000000).view(np.float32),
+                            (2 * np.pi * rng.random(n)).astype(np.float32)])
+        y = np.zeros_like(x)
+    elif fn == "pow":   # the lobe's domain (x in [0, 1], the scenes' exponents), then seeded pairs
+        xs = rng.random(n).astype(np.float32)
+        es = rng.choice(np.array([2, 8, 10, 32, 1.5, 100], np.float32), n)
+        u = rng.integers(0, 1 << 32, size=(2, n), dtype=np.uint64).astype(np.uint32)
+        x = np.concatenate([xs, u[0].view(np.float32)])
+        y = np.concatenate([es, u[1].view(np.float32)])
     else:
         u = rng.integers(0, 1 << 32, size=(2, n), dtype=np.uint64).astype(np.uint32)
         y, x = u[0].view(np.float32), u[1].view(np.float32)

@@ -1,14 +1,13 @@
-"""CPU-only: how far the reference's libm convention moves each config's frame.
+"""CPU-only: how far a libm evaluated in double and rounded once moves each config's frame
+against the reference's own calls.
 
 The reference's source resolves its libm calls (Fresnel's sin(acosf), Blinn's pow, the
 lat-long lookups' atan2 / acos, the cosine sampler's cos / sin) to the float overloads
-(glibc sinf / acosf / powf / atan2f / cosf).  The HIP device evaluates atan2f / acosf
-with the bit-exact fdlibm restatement of csrc/mrt_libm.h (glibc's own values), and only
-sinf / cosf / powf in double, rounded once.  The oracle restates both conventions
-(oracle.LIBM_DEVICE: the device's sinf / cosf / powf; LIBM_FLOAT: glibc's -- atan2f /
-acosf are glibc's in both).  The device's frames equal the LIBM_DEVICE oracle bit for
-bit (tests/), so LIBM_FLOAT vs LIBM_DEVICE here is exactly the device-vs-reference-
-convention difference, per config:
+(glibc sinf / acosf / powf / atan2f / cosf).  Round 5's device evaluated sinf / cosf / powf
+in double and rounded once (oracle.LIBM_DOUBLE); since round 6 it restates all five glibc
+functions bit for bit (csrc/mrt_libm.h), i.e. it equals oracle.LIBM_FLOAT.  This tool
+keeps the comparison of the two conventions (profiles/r06_libm_parity.json: round 5's
+device convention against the reference's, per config):
 
     python3 tools/libm_parity.py [--threads 8] [--out profiles/r05_libm_parity.json] [KEY[:WxH] ...]
 
@@ -38,7 +37,7 @@ DEFAULT = ["C3:1920x1080", "C4:1920x1080", "D1:1024x1024", "R3:1920x1080", "G3:9
 def compare(key, W, H, threads):
     _, Osc, cam = config_scene(key)
     t0 = time.time()
-    dev = Osc.render(cam, W, H, threads=threads, libm=O.LIBM_DEVICE)
+    dev = Osc.render(cam, W, H, threads=threads, libm=O.LIBM_DOUBLE)
     ref = Osc.render(cam, W, H, threads=threads, libm=O.LIBM_FLOAT)
     g, r = dev["rgb"].astype(np.float64), ref["rgb"].astype(np.float64)
     bad = np.abs(g - r) > 1e-4 * np.abs(r)
@@ -72,7 +71,7 @@ def main():
         rows.append(row)
     if a.out:
         with open(a.out, "w") as f:
-            json.dump({"note": "oracle LIBM_DEVICE (== the device, bit for bit) vs LIBM_FLOAT (the reference's "
+            json.dump({"note": "oracle LIBM_DOUBLE (round 5's device convention) vs LIBM_FLOAT (the reference's "
                                "float overloads, glibc); tools/libm_parity.py", "rows": rows}, f, indent=1)
 
 
