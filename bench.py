@@ -47,10 +47,10 @@ NODE_B, LEAF_B = 128, 160      # QNode / DLeaf bytes (csrc/mrt_types.h)
 # rocprofv3 evidence of this round (tools/prof_all.sh + tools/prof3.py): per config and
 # bench pass, HBM bytes per launch (PMC) and the rocprof average duration at one
 # frame in flight; per kernel, the SQ / TCP latency counters
-PROFILE_FILE = os.path.join(ROOT, "profiles", "r05_profile.json")
+PROFILE_FILE = os.path.join(ROOT, "profiles", "r06_profile.json")
 CPU_CAL_FILE = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
 # kernel traces of the driver-settings runs (tools/step_trace.py): busy union per timed step
-STEP_TRACE_FILE = os.path.join(ROOT, "profiles", "r05_steptrace.json")
+STEP_TRACE_FILE = os.path.join(ROOT, "profiles", "r06_steptrace.json")
 # N > 1 split: frames of the camera path per step when --frames-per-launch is not given
 DEFAULT_FPL = 8
 
@@ -320,7 +320,7 @@ def _scene_setup(scene):
 
 
 def step_trace_evidence(config):
-    """This config's tracked kernel trace of a driver-settings run (profiles/r05_steptrace.json,
+    """This config's tracked kernel trace of a driver-settings run (profiles/r06_steptrace.json,
     tools/step_trace.py): kernel-busy union per timed step, overlap, per-step fraction."""
     if not os.path.exists(STEP_TRACE_FILE):
         return None
@@ -333,7 +333,7 @@ def step_trace_evidence(config):
 
 
 def profile_evidence(config):
-    """This config's tracked rocprofv3 record (profiles/r05_profile.json): per pass
+    """This config's tracked rocprofv3 record (profiles/r06_profile.json): per pass
     {hbm_bytes, avg_us, kernels}, per kernel {latency, code_object, ...}, source."""
     if not os.path.exists(PROFILE_FILE):
         return None

@@ -229,7 +229,7 @@ def summarise(cfg, d):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root", nargs="?", default="gpurun_out/prof3")
-    ap.add_argument("--round", default="r05")
+    ap.add_argument("--round", default="r06")
     ap.add_argument("--objs", nargs="*", default=sorted(glob.glob(os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "rendering-algorithms-raytracer_amd", "lib", "build",
         "mrt_*.o"))))

@@ -13,7 +13,7 @@ CONFIGS = ["C3", "C2", "C3L", "C4", "D1", "C5", "A3", "R3", "P4", "G3", "FS"]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--round", default="r05")
+    ap.add_argument("--round", default="r06")
     ap.add_argument("--prev", default="r04", help="round whose tracked lines give the last column")
     a = ap.parse_args()
     print("| config | Mray/s | ms / frame | frame latency | frac (L2, live) | frac (tracked rocprof avg) | "
