@@ -476,6 +476,13 @@ def main():
         cams_ = [cam] if nf == 1 else [_camera(c) for c in scenes.camera_path(cfg["camera"], nf)]
         return (_lib.mrt_camera * nf)(*[c._c() for c in cams_])
 
+    def hip_rt():
+        """The HIP runtime torch and libmrt share (one per process)."""
+        lib_ = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+        h_ = C.CDLL(lib_ if os.path.exists(lib_) else "libamdhip64.so")
+        h_.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        return h_
+
     def make_ipc_pipe(nf, nsplit=None, srank=None, pipe_streams=None):
         """The split with direct writes (--assemble ipc): rank 0 owns `depth` frame buffers
         (nf frames each: the 8-bit framebuffer, Image::m_pixels, and with --split-float the
@@ -535,8 +542,14 @@ def main():
                             h = _lib.mrt_ipc_handle.from_buffer_copy(hb)
                             p = C.c_void_p()
                             _lib.check(L.mrt_ipc_open(C.byref(h), dev, C.byref(p)), "ipc open")
-                            pair.append(p.value)
                             opened.append(p.value)
+                            # the mapping must be usable before a kernel stores through it: a 4-byte
+                            # copy from it through the HIP runtime (an error here falls back to the
+                            # gather; a bad mapping met by a kernel would fault instead)
+                            probe = (C.c_uint8 * 4)()
+                            if hip_rt().hipMemcpy(probe, C.c_void_p(p.value), C.c_size_t(4), 2) != 0:   # DtoH
+                                raise RuntimeError("rank 0's frame mapped but not readable from this device")
+                            pair.append(p.value)
                         ptrs.append(tuple(pair))
             except Exception as e:
                 err = repr(e)
