@@ -457,3 +457,38 @@ def test_batch_grid_sizing_gives_identical_tiles(rect):
     assert np.abs(out[0]).sum() > 0
     for o in out[1:]:
         assert np.array_equal(bits(o), bits(out[0]))
+
+
+@pytest.mark.parametrize("key", ["C3", "C4", "C5", "R3", "A3", "G3"])
+def test_batch_frames_equal_per_camera_frames(key):
+    """mrt_render_batch_frames_async (ABI 10, the IPC split's render): a camera-path batch
+    whose items come shuffled, with duplicates and ids past the batch, written straight
+    into frame-layout buffers -- through every engine (one-light frame kernel, wavefront
+    shadow pass, instanced dome light, chain engine for secondary rays, adaptive passes,
+    dispersion); frame f equals a single-frame render of camera f with seed default + f,
+    float and 8-bit, and no pixel outside the batch's items is touched (ragged size)."""
+    torch = pytest.importorskip("torch")
+    import ctypes as C
+    from miro import _lib
+    P, _, cam = config_scene(key)
+    W, H, F = 100, 70, 2
+    cams = scenes.camera_path(cam, F, step_deg=5.0)
+    bpf = ((W + 31) // 32) * ((H + 31) // 32)
+    order = np.random.default_rng(11).permutation(bpf * F).tolist()
+    order += order[:3] + [bpf * F + 1]                 # duplicates and an id past the batch (skipped)
+    ids = torch.tensor(order, dtype=torch.int32, device="cuda")
+    frames = torch.full((F * H * W * 3,), -7.0, dtype=torch.float32, device="cuda")
+    frames8 = torch.zeros(F * H * W * 3, dtype=torch.uint8, device="cuda")
+    camc = (_lib.mrt_camera * F)(*[camera(c)._c() for c in cams])
+    opts = _lib.mrt_render_opts(W, H, 0, 0, 1, 0, 0)
+    L = miro.lib()
+    _lib.check(L.mrt_render_batch_frames_async(P.handle, camc, F, C.byref(opts), ids.data_ptr(), len(order),
+                                               frames.data_ptr(), frames8.data_ptr(),
+                                               torch.cuda.current_stream().cuda_stream), "batch frames")
+    torch.cuda.synchronize()
+    fr = frames.cpu().numpy().reshape(F, H, W, 3)
+    fr8 = frames8.cpu().numpy().reshape(F, H, W, 3)
+    for f in range(F):
+        img, _ = render(P, cams[f], W, H, seed=0x5EED + f)
+        assert np.array_equal(bits(fr[f]), bits(img.rgb)), (key, f)
+        assert np.array_equal(fr8[f], img.pixels), (key, f)
