@@ -16,7 +16,10 @@ CONFIGS="${CONFIGS:-C3 C2 C4 D1 C5 A3 R3 P4 G3}"
 for cfg in $CONFIGS; do
     rm -rf "$OUT/$cfg"
     mkdir -p "$OUT/$cfg"
-    timeout -s KILL ${LIMIT:-300} rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$cfg/trace" -o run \
+    # the config's frames in flight as hardware queues (bench.py sets them itself, but under rocprofv3 the
+    # HIP runtime starts before bench.py runs, so the variable has to be in the environment already)
+    q=$(python3 -c "import sys; sys.path.insert(0, 'rendering-algorithms-raytracer_amd'); from miro import scenes; print(max(4, scenes.CONFIGS['$cfg'].get('inflight', 4)))")
+    GPU_MAX_HW_QUEUES=$q timeout -s KILL ${LIMIT:-300} rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$cfg/trace" -o run \
         -- python3 bench.py --gpus 1 --config "$cfg" --steps 20 --warmup 5 --no-cpu-baseline $BENCH_EXTRA \
         > "$OUT/$cfg/bench.log" 2>&1
     rc=$?
