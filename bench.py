@@ -351,7 +351,14 @@ def main():
     # torch is imported): one per frame in flight.  With HIP's default 4 the N = 1 pipeline
     # holds at most 4 frames, so a frame whose latency is set by a few heavy tiles caps
     # the step at latency / 4 (C2: 0.2011 -> 0.1644 ms per step with 8)
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(min(32, max(4, args.inflight))))
+    # (the GPU box's environment sets GPU_MAX_HW_QUEUES=4, HIP's default, so a larger need replaces it)
+    want_q = min(32, max(4, args.inflight))
+    try:
+        have_q = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+    except ValueError:
+        have_q = 0
+    if have_q < want_q:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(spawn(args))
