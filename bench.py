@@ -999,7 +999,7 @@ def main():
                    "frames_per_step": n_frames, "rays_per_step": rays_per_step, "shadow_rays": shadow_total,
                    "secondary_rays": second_total,
                    "qbvh_nodes": scene.bvh_info["nodes"], "qbvh_leaves": scene.bvh_info["leaves"],
-                   "frames_in_flight": inflight,
+                   "frames_in_flight": inflight, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                    "parallelism": "single GPU, whole frame" if use_frame_path else
                    ((f"one {W}x{H} frame per step" if n_frames == 1 else
                      f"batched: {n_frames} {W}x{H} frames of the camera path per step (distinct cameras), rendered "
