@@ -343,9 +343,9 @@ def profile_evidence(config):
 # ------------------------------------------------------------------ worker
 def main():
     args = parse()
-    if not args.inflight:   # the config's frames in flight (miro.scenes imports no torch / HIP)
-        sys.path.insert(0, os.path.join(ROOT, "rendering-algorithms-raytracer_amd"))
-        from miro import scenes as _scenes
+    sys.path.insert(0, os.path.join(ROOT, "rendering-algorithms-raytracer_amd"))
+    from miro import scenes as _scenes   # (imports no torch / HIP)
+    if not args.inflight:   # the config's frames in flight
         args.inflight = int(_scenes.CONFIGS[args.config].get("inflight", 4))
     # hardware queues of this process's HIP runtime (read when HIP initialises, so before
     # torch is imported): one per frame in flight.  With HIP's default 4 the N = 1 pipeline
@@ -391,11 +391,14 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
-    tuning = {}
+    # the config's own switches (miro/scenes.py "tune": a measured per-scene choice, e.g. C3's
+    # nested camera-ray walk), then --tune on top; both reported in the line
+    tuning = dict(_scenes.CONFIGS[args.config].get("tune", {}))
     for kv in args.tune:
         k, v = kv.split("=")
-        _lib.check(miro.lib().mrt_set_tuning(k.encode(), int(v)), f"tuning {k}")
         tuning[k] = int(v)
+    for k, v in tuning.items():
+        _lib.check(miro.lib().mrt_set_tuning(k.encode(), int(v)), f"tuning {k}")
     progress(f"building {args.config}")
     scene, cam, cfg = scenes.build_config(args.config, device=dev)
     progress(f"built: {scene.bvh_info['prims']} world objects")
@@ -1062,6 +1065,7 @@ def main():
         out["frame_check"] = frame_check
     if st.get("fused"):   # the frame kernel's walk (LDS top nodes only with tuning lds_nodes 1)
         out["walk"] = scene.walk_info()
+        out["walk"]["latch"] = "nested" if tuning.get("walk_latch", 1) == 0 else "one"
     if split_times is not None:
         out["split_times"] = split_times
     if weak is not None:

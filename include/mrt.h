@@ -437,7 +437,8 @@ int mrt_scene_last_stats(const mrt_scene* s, mrt_stats* out);
  * "fast_box" 0/[1] (hardware min/max slab test when its finiteness precondition holds),
  * "scalar_nodes" 0..[7] (bit 0 scalar fetch of wave-uniform nodes, bit 1 of wave-uniform
  * triangles, bit 2 octant-ordered box test), "walk_exit" 0/[1] (the frame / primary
- * kernels' walk loop: two exits, one exit), "lds_nodes" [0]/1 (the frame kernel's LDS
+ * kernels' walk loop: two exits, one exit), "walk_latch" 0/[1] (the frame kernel's
+ * camera-ray walk: nested latches, one latch), "lds_nodes" [0]/1 (the frame kernel's LDS
  * top-node walk), "sched" 0..3 [2] (tile schedule: static grid-stride, static XCD bands,
  * dynamic interleaved, dynamic banded; see TileSched), "fused" 0/[1] (one-launch frame
  * kernel for one point light), "shade1" 0/[1] (specialised shading kernel for one point

@@ -486,6 +486,10 @@ static int g_walk_exit = 1;       // the walk loop of frame1_kernel / primary_ke
                                   // 12-16% loss on the bunny scenes was the frame latency of a few heavy
                                   // top-row tiles with only 4 frames in flight (walk exit), gone
                                   // with 8 hardware queues: one exit everywhere, no probe (round 6)
+static int g_walk_latch = 1;      // frame1_kernel's camera-ray walk: 1 one latch (the popping lanes pick their next node
+                                  // by select in the same step), 0 nested (two latches: lanes that pop wait for the
+                                  // wave's longest descent).  Round-6 A/B (profiles/r06_walk_latch_ab.txt): one latch
+                                  // C2 -11%, C3L -4.4%, C3 +1.5%; config C3 runs 0 (miro/scenes.py)
 static int g_lds_nodes = 0;       // frame1_kernel's LDS top-node walk (LN), 0 off / 1 on: with 4 frames in flight C2
                                   // -4.1%, C3 +9%, C3L +11% (profiles/r05_lds_nodes_ab_*.txt); no probe separated them
                                   // reliably (single-frame kernel times are equal on C2), so it is off unless asked for
@@ -1655,7 +1659,7 @@ static int launch_render(Scene& s, RenderParams& P, size_t slots, bool count, hi
         // LDS top-node walk (tuning "lds_nodes"; both walks give the same bits)
         const bool ln = fb && d.lds_ok && g_lds_nodes > 0;
         d.lds_pick = ln ? 1 : 0;
-        const int walk = ln ? 2 : g_walk_exit;
+        const int walk = ln ? 2 : g_walk_exit == 0 ? 0 : g_walk_latch ? 3 : 1;
         if ((rc = launch(pick_frame1(g_frame1_waves, count, fb, d.pow_spec, walk)))) return rc;
         HIP_OK(hipEventRecord(c.evm, stream));
         c.last_was_render = true;
@@ -2925,6 +2929,9 @@ int mrt_set_tuning(const char* key, int value) {
     } else if (k == "bin_obits") {
         if (value < 0 || value > 4) { set_error("bin_obits must be 0..4"); return MRT_ERR_INVALID; }
         g_bin_obits = value;
+    } else if (k == "walk_latch") {
+        if (value < 0 || value > 1) { set_error("walk_latch must be 0 or 1"); return MRT_ERR_INVALID; }
+        g_walk_latch = value;
     } else if (k == "walk_exit") {
         if (value < 0 || value > 1) { set_error("walk_exit must be 0 or 1"); return MRT_ERR_INVALID; }
         g_walk_exit = value;

@@ -146,7 +146,8 @@ __global__ void __launch_bounds__(kWG, MINW) shade1_kernel(RenderParams P) {
 // and both walks read their wave-uniform visits from there (traverse_impl); the
 // host runs it when asked (tuning "lds_nodes").
 // WALK (traverse_impl): 0 the walk loop with a second exit (stack overflow returns), 1 one
-// exit (XONE), 2 one exit + LN.  Same bits either way; the host picks 0 / 1 per scene.
+// exit (XONE), 2 one exit + LN, 3 one exit and one latch (OL) for the camera rays' walk.
+// Same bits either way; the host runs 3 unless tuned (walk_exit, walk_latch, lds_nodes).
 template <bool COUNT, bool FAST, int MINW, bool POW, int WALK = 1>
 __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
     constexpr bool LN = WALK == 2;
@@ -186,7 +187,7 @@ __global__ void __launch_bounds__(kWG, MINW) frame1_kernel(RenderParams P) {
             const EyeRay er = camera_ray(PA.cam[f], PA.seed + (uint32_t)f, x, y, rsqT);
             const DRay r = make_ray(er.o, er.d);
             DHit h{1e12f, 0.f, 0.f, -1};
-            const bool hit = traverse<false, COUNT, FAST, false, true, LN, WALK != 0>(T, r, 0.001f, h, st);
+            const bool hit = traverse<false, COUNT, FAST, false, true, LN, WALK != 0, WALK == 3>(T, r, 0.001f, h, st);
             const RenderParams& PB = reload_params();   // shading parameters
             v3 col = mk(PB.bg[0], PB.bg[1], PB.bg[2]);
             if (hit) {
@@ -244,10 +245,14 @@ static KernelFn pick_frame1_walk(int w, bool c, bool f, bool pow) {
     }
 }
 // pow: a Blinn material with specExp != 1 (those scenes run at 6 waves, or unbounded);
-// walk: 0 two-exit walk loop, 1 one exit, 2 one exit + the LDS top-node walk
+// walk: 0 two-exit walk loop, 1 one exit, 2 one exit + the LDS top-node walk, 3 one exit + one latch
 KernelFn pick_frame1(int w, bool c, bool f, bool pow, int walk) {
-    return walk == 2 ? pick_frame1_walk<2>(w, c, f, pow)
-                     : walk == 0 ? pick_frame1_walk<0>(w, c, f, pow) : pick_frame1_walk<1>(w, c, f, pow);
+    switch (walk) {
+        case 0: return pick_frame1_walk<0>(w, c, f, pow);
+        case 2: return pick_frame1_walk<2>(w, c, f, pow);
+        case 3: return pick_frame1_walk<3>(w, c, f, pow);
+        default: return pick_frame1_walk<1>(w, c, f, pow);
+    }
 }
 // (the two-launch path: fused = 0, or a caller that wants hit records) at 5 waves
 KernelFn pick_shade1(bool c, bool f, bool pow) { return pow ? shade1_fn<5, true>(c, f) : shade1_fn<5, false>(c, f); }

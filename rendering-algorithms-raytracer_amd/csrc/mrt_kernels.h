@@ -381,7 +381,7 @@ __device__ __forceinline__ bool tri_test_lane(const Trav& c, uint32_t leaf, int 
 }
 
 template <bool ANY, bool COUNT, bool FAST, bool INST = false, bool BL = false, bool CHECK = true, bool LN = false,
-          bool XONE = true>
+          bool XONE = true, bool OL = false>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root = 0,
                               int sp0 = 0, int32_t aoff = 0);
 
@@ -422,9 +422,9 @@ __device__ __forceinline__ bool proxy_hit(const Trav& c, int inst, const DRay& r
 // call ABI costs the walk registers and scratch -- are compiled out.
 // LN: wave-uniform visits of the hierarchy's top nodes (index < kLdsNodes, renumbered
 // breadth first on upload) read them from LDS (c.lnodes, one broadcast address)
-// instead of the scalar cache -- faster where the top levels end most rays (the
-// walk is per scene, chosen by a probe: mrt_device.hip, lds_nodes).
-template <bool ANY, bool COUNT, bool FAST, bool INST, bool BL, bool CHECK, bool LN, bool XONE>
+// instead of the scalar cache -- faster where the top levels end most rays (tuning
+// lds_nodes, off by default: mrt_device.hip).
+template <bool ANY, bool COUNT, bool FAST, bool INST, bool BL, bool CHECK, bool LN, bool XONE, bool OL>
 __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st, int32_t root,
                               int sp0, int32_t aoff) {
     int sp = sp0;
@@ -436,7 +436,8 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
     while (true) {
         // stack top read at the start of the step: the LDS latency overlaps the
         // node fetch and box test (used only if this step pops)
-        const int32_t peek = c.lds[(sp > 0 && sp <= kLdsStack ? sp - 1 : 0) * kWG];
+        // (entry min(sp - 1, kLdsStack - 1) as unsigned: an in-column address for every sp)
+        const int32_t peek = c.lds[__builtin_elementwise_min((uint32_t)(sp - 1), (uint32_t)(kLdsStack - 1)) * kWG];
         int m, kinds;
         int4 ch;
         // Wave-uniform node (all active lanes on one node, ~70% of primary
@@ -506,9 +507,8 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                     // overflow (flagged).  XONE: the walk ends at the loop's one exit (the pop
                     // test below, with the stack emptied) instead of returning from here --
                     // an extra exit of the divergent loop costs exec-mask bookkeeping in every
-                    // step (SALU -19% per step, C3 -7%, C4 -6%), but the two-exit form measured
-                    // faster on the bunny scenes (C2 +13% with one exit): frame1_kernel picks
-                    // per scene (mrt_device.hip, exit probe)
+                    // step (SALU -19% per step, C3 -7%, C4 -6%); the two-exit form stays as
+                    // tuning walk_exit 0 (round 6: the bunny scenes' tail effect)
                     if (!pushed) {
                         st.overflow = true;
                         if (!XONE) return hit;
@@ -571,7 +571,23 @@ __device__ bool traverse_impl(const Trav& c, const DRay& r, float tMin, DHit& h,
                 k++;
             }
         }
-        if (have_next) {
+        if (OL) {
+            // One back edge (OL): the next node is nxt or the popped entry, chosen by select
+            // (the LDS top was read at the step's start; a pop from the global column, like the
+            // walk's end, sits behind one compare).  With a branch per case the loop has two
+            // latches, which the compiler's structurisation nests: lanes that pop wait until
+            // every lane of the wave has ended its descent (§4, "walk loop latches").
+            int32_t g = peek;
+            // one compare for both rare cases: sp == sp0 (the walk is done) or sp > kLdsStack
+            // (sp >= sp0 always; a walk entered above kLdsStack pops from the global column only)
+            const uint32_t lds_left = sp0 < kLdsStack ? (uint32_t)(kLdsStack - sp0) : 0u;
+            if (!have_next && (uint32_t)(sp - 1 - sp0) >= lds_left) {
+                if (sp == sp0) break;
+                g = c.gstk[(size_t)(sp - 1 - kLdsStack) * c.gstride];
+            }
+            cur = have_next ? nxt : g;
+            sp -= have_next ? 0 : 1;
+        } else if (have_next) {
             cur = nxt;
         } else {
             if (sp == sp0) break;
@@ -780,14 +796,18 @@ __device__ __forceinline__ bool anyhit_step_inst(const Trav& c, float tMin, floa
 // whose origin and 1/d are finite; any other ray takes the exact loop.  A
 // closest hit's packed slot is resolved to the global prim id here.
 // An instance hit's id is the instance's hit_base + its BLAS object index.
-// XONE: the one-exit walk loop (traverse_impl) -- on where measured faster: frame1_kernel /
-// primary_kernel per scene (host probe), the shadow and adaptive kernels of plain scenes
-// (C4 -6%, A3 -4%); off in the chain engine (P4 +21%, R3 +4% with it) and nested BLAS walks
+// XONE: the one-exit walk loop (traverse_impl) -- frame1_kernel, primary_kernel and the
+// shadow and adaptive kernels of plain scenes (C4 -6%, A3 -4%); off in the chain engine
+// (P4 +21%, R3 +4% with it) and nested BLAS walks.
+// OL: the one-latch loop end (traverse_impl) -- the closest-hit walks of primary_kernel and
+// the adaptive kernel of plain scenes, and frame1_kernel's unless the host picks the nested
+// form (tuning walk_latch 0); any-hit walks and the chain engine keep the nested form
+// (round 6 A/B).
 template <bool ANY, bool COUNT, bool FAST = false, bool INST = false, bool CHECK = true, bool LN = false,
-          bool XONE = false>
+          bool XONE = false, bool OL = false>
 __device__ __forceinline__ bool traverse(const Trav& c, const DRay& r, float tMin, DHit& h, TravStats& st) {
-    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST, false, CHECK, LN, XONE>(c, r, tMin, h, st)
-                                        : traverse_impl<ANY, COUNT, false, INST, false, CHECK, false, XONE>(c, r, tMin, h, st);
+    const bool hit = (FAST && r.finite) ? traverse_impl<ANY, COUNT, true, INST, false, CHECK, LN, XONE, OL>(c, r, tMin, h, st)
+                                        : traverse_impl<ANY, COUNT, false, INST, false, CHECK, false, XONE, OL>(c, r, tMin, h, st);
     if (!ANY && hit) {
         h.prim = c.leaves[(uint32_t)h.prim >> 2].prim[h.prim & 3];
         if (INST && h.inst >= 0) h.prim += c.inst[h.inst].hit_base;

@@ -38,25 +38,42 @@ MRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 // 12-bit packed table entry -> float bits in [0.5, 1)
 MRT_HD uint32_t tbl_bits(uint16_t e) { return 0x3F000000u | ((uint32_t)e << 11); }
 
-// RCPSS emulation; T = 2048-entry packed rcp table.  Written as a select chain
-// (lowest priority first) so device code has no divergent branches; the table
-// index is in range for every input.  On |x| bits a = u & 0x7FFFFFFF: a normal x
-// (exponent e in 1..252) gives exponent 253 - e and the entry's 12 mantissa bits,
-// formed as (s | 253 << 23 | entry << 11) - (e << 23) (no borrow reaches the
-// mantissa or the sign); e >= 253 (and inf) -> +-0; zero / denormal -> +-inf;
-// NaN -> quiet NaN.  (Round 5: 5 fewer VALU ops per triangle test than testing e
-// and m separately; equal to the table emulation on every 61st float bit pattern on the
-// CPU and every 257th on the GPU, tests/test_numerics.py; the tables themselves are
-// checked against the live instructions on all 2^32 inputs, tools/gen_x86_tables.c.)
-MRT_HD float x86_rcp(float x, const uint16_t* T) {
-    const uint32_t u = f2u(x), a = u & 0x7FFFFFFFu, s = u & 0x80000000u;
-    uint32_t t = T[(a >> 12) & 0x7FFu];
-    MRT_OPAQUE(t);
-    uint32_t r = (s | 0x7E800000u | (t << 11)) - (a & 0x7F800000u);
+// RCPSS emulation; T = 2048-entry packed rcp table; the table index is in range for
+// every input.  On |x| bits a = u & 0x7FFFFFFF: a normal x (exponent e in 1..252)
+// gives exponent 253 - e and the entry's 12 mantissa bits; e >= 253 (and inf) ->
+// +-0; zero / denormal -> +-inf; NaN -> quiet NaN.  (Equal to the table emulation on
+// all 2^32 float bit patterns on the CPU, tests/native/rcp_sweep.c at stride 1, every
+// 61st in the CPU suite and every 257th on the GPU, tests/test_numerics.py; the tables
+// themselves are checked against the live instructions on all 2^32 inputs,
+// tools/gen_x86_tables.c.)
+// The exponent classes outside 1..252 (zero / denormal, e >= 253, inf, NaN): the
+// select chain over the normal-path value r, which it leaves as is for a normal x.
+MRT_HD uint32_t x86_rcp_special(uint32_t u, uint32_t r) {
+    const uint32_t a = u & 0x7FFFFFFFu, s = u & 0x80000000u;
     r = a >= 0x7E800000u ? s : r;                                  // e >= 253: below FLT_MIN -> +-0; inf -> +-0
     r = a < 0x00800000u ? (s | 0x7F800000u) : r;                  // zero / denormal -> +-inf
-    MRT_OPAQUE(r);
     r = a > 0x7F800000u ? (u | 0x00400000u) : r;                  // NaN -> quiet
+    return r;
+}
+// Normal x: ((253 << 23 | entry << 11) - (e << 23)) | sign (no borrow reaches the sign).
+// The device takes the select chain only when some lane of the wave needs it (one
+// compare per test; a triangle test's det is almost never outside the normal range),
+// instead of three compare + select pairs, each select waiting on its compare, per
+// triangle test (round 6: -8 VALU instructions and -3 wait states per test).
+MRT_HD float x86_rcp(float x, const uint16_t* T) {
+    const uint32_t u = f2u(x), ex = u & 0x7F800000u;
+    uint32_t t = T[(u >> 12) & 0x7FFu];
+    MRT_OPAQUE(t);
+    uint32_t r = ((0x7E800000u | (t << 11)) - ex) | (u & 0x80000000u);
+    const bool special = ex - 0x00800000u >= 0x7E000000u;        // e == 0 or e >= 253
+#ifdef __HIP_DEVICE_COMPILE__
+    if (__ballot(special) != 0) {
+        r = x86_rcp_special(u, r);
+        asm volatile("; mrt: rcp special" : "+v"(r));   // keeps the chain in its branch
+    }
+#else
+    if (special) r = x86_rcp_special(u, r);
+#endif
     return u2f(r);
 }
 

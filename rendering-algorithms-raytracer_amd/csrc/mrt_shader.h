@@ -1298,7 +1298,7 @@ __global__ void __launch_bounds__(kWG, MINW) primary_kernel(RenderParams P) {
             const EyeRay er = camera_ray(cam, PA.seed + (uint32_t)f, x, y, rsqT);
             DRay r = make_ray(er.o, er.d, er.time);
             DHit h{1e12f, 0.f, 0.f, -1};
-            if (!traverse<false, COUNT, FAST, INST, CHECK, false, XONE>(T, r, 0.001f, h, st)) h.prim = -1;
+            if (!traverse<false, COUNT, FAST, INST, CHECK, false, XONE, XONE && !INST>(T, r, 0.001f, h, st)) h.prim = -1;
             const RenderParams& PC = reload_params();
             item_pixel(PC, item, lane_id(), x, y, slot);  // recompute: keeps it out of the traversal's live set
             PC.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(h.prim));
@@ -1457,7 +1457,7 @@ __global__ void __launch_bounds__(kWG, MINW) adaptive_kernel(RenderParams P) {
         DHit h{1e12f, 0.f, 0.f, -1};
         v3 col;
         eye_rays++;
-        const bool hit = traverse<false, COUNT, FAST, INST, true, false, !INST>(T, r, 0.001f, h, st);
+        const bool hit = traverse<false, COUNT, FAST, INST, true, false, !INST, !INST>(T, r, 0.001f, h, st);
         if (sample == 0) P.hits[slot] = make_float4(h.t, h.a, h.b, __int_as_float(hit ? h.prim : -1));
         if (hit) {
             eye_hits++;

@@ -414,7 +414,10 @@ CONFIGS = {
     "C3": dict(name="sponza stand-in (~66k tris) 1920x1080 Blinn+PointLight", W=1920, H=1080,
                camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),
                lights=[dict(type="point", pos=(0.0, 10.0, 0.0), power=200.0)],
-               material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza"),
+               material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="sponza",
+               # the frame kernel's camera-ray walk with nested latches: 1.5% faster here than one
+               # latch, which the other scenes run (C2 -11%, C3L -4.4%; DESIGN.md §4, walk latches)
+               tune={"walk_latch": 0}),
     # C3L: C3 on the 262 k-triangle Sponza variant ("also a 262 k
     # variant"; Crytek Sponza's size): its ~16 MB hierarchy does not fit one XCD's L2
     "C3L": dict(name="sponza stand-in, 262k variant (261,788 tris) 1920x1080 Blinn+PointLight", W=1920, H=1080,

@@ -65,12 +65,13 @@ def test_batch_tiles_per_wave_key_validates():
 
 def test_walk_tuning_keys_validate():
     """Traversal switches: walk_exit (0 two exits, 1 one exit -- the default; round 6 removed
-    the per-scene probe, -1), lds_nodes
+    the per-scene probe, -1), walk_latch (0 nested, 1 one latch -- the default), lds_nodes
     (0 / 1), scalar_nodes (bit mask 0..7); bad values rejected with an error; the walk info
     entry rejects a null scene."""
     L = miro.lib()
     try:
-        for k, good, bad in ((b"walk_exit", (0, 1), (-1, 2)), (b"lds_nodes", (0, 1), (-1, 2)),
+        for k, good, bad in ((b"walk_exit", (0, 1), (-1, 2)), (b"walk_latch", (0, 1), (-1, 2)),
+                             (b"lds_nodes", (0, 1), (-1, 2)),
                              (b"scalar_nodes", (0, 7), (-1, 8))):
             for v in good:
                 assert L.mrt_set_tuning(k, v) == 0, (k, v)
@@ -78,5 +79,5 @@ def test_walk_tuning_keys_validate():
                 assert L.mrt_set_tuning(k, v) != 0, (k, v)
         assert L.mrt_scene_walk_info(None, None, None) != 0
     finally:
-        for k, v in ((b"walk_exit", 1), (b"lds_nodes", 0), (b"scalar_nodes", 7)):
+        for k, v in ((b"walk_exit", 1), (b"walk_latch", 1), (b"lds_nodes", 0), (b"scalar_nodes", 7)):
             assert L.mrt_set_tuning(k, v) == 0

@@ -36,12 +36,22 @@ def close_frac(got, ref, rtol=1e-4):
 @pytest.mark.gpu
 @pytest.mark.parametrize("key", ["C2", "C3", "C3L", "C4", "C5", "D1"])
 def test_full_size_frame_matches_oracle(key):
+    """Under the config's own tuning (bench.py's: C3's nested camera-ray walk; the others the
+    library defaults), so every benched kernel form is the one compared here."""
     need_gpu()
     P, Osc, cam = config_scene(key)
     from miro import scenes
     W, H = scenes.CONFIGS[key]["W"], scenes.CONFIGS[key]["H"]
     img = miro.Image(); img.resize(W, H)
-    hits = P.raytraceImage(camera(cam), img, want_hits=True)
+    tune = scenes.CONFIGS[key].get("tune", {})
+    L = miro.lib()
+    try:
+        for k, v in tune.items():
+            assert L.mrt_set_tuning(k.encode(), v) == 0
+        hits = P.raytraceImage(camera(cam), img, want_hits=True)
+    finally:
+        for k in tune:
+            assert L.mrt_set_tuning(k.encode(), {"walk_latch": 1}[k]) == 0   # the library default
     ref = Osc.render(cam, W, H, threads=16, libm=O.LIBM_FLOAT)
     assert np.array_equal(hits["prim"], ref["hits"]["prim"]), f"{key}: primary hit ids differ"
     hit = ref["hits"]["prim"] >= 0

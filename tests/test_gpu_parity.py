@@ -165,11 +165,13 @@ def test_edge_cases():
                                    dict(fused=1, frame1_waves=8, fast_box=0), dict(fused=1, frame1_waves=1, sched=0),
                                    dict(fused=1, walk_exit=0), dict(fused=1, walk_exit=1),
                                    dict(fused=0, walk_exit=0, primary_waves=7), dict(fused=0, walk_exit=1, primary_waves=7),
-                                   dict(fused=1, lds_nodes=1), dict(fused=1, lds_nodes=1, frame1_waves=8)])
+                                   dict(fused=1, lds_nodes=1), dict(fused=1, lds_nodes=1, frame1_waves=8),
+                                   dict(fused=1, walk_latch=0), dict(fused=1, walk_latch=1, sched=3),
+                                   dict(fused=1, walk_latch=0, walk_exit=0)])
 def test_every_kernel_path_is_exact(knobs):
     """Performance switches must not change a single bit (fused vs split shading,
     one-launch frame1_kernel vs primary + shade1 launches, hardware vs select box
-    test, XCD schedule, occupancy build, the walk loop's exit form)."""
+    test, XCD schedule, occupancy build, the walk loop's exit form and latches)."""
     L = miro.lib()
     try:
         for k, v in knobs.items():
@@ -185,7 +187,7 @@ def test_every_kernel_path_is_exact(knobs):
         assert P.last_stats["shadow_rays"] == ref["shadow_rays"]
     finally:
         for k, v in dict(shade1=1, fast_box=1, sched=2, primary_waves=7, scalar_nodes=7, wavefront=1, fused=1,
-                         frame1_waves=7, walk_exit=1, lds_nodes=0).items():   # the library's defaults
+                         frame1_waves=7, walk_exit=1, walk_latch=1, lds_nodes=0).items():   # the library's defaults
             L.mrt_set_tuning(k.encode(), v)
 
 
