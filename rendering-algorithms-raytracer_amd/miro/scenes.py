@@ -409,7 +409,10 @@ CONFIGS = {
                material=dict(kind="blinn", kd=(1, 1, 1)), bg=(0.0, 0.0, 0.2), mesh="bunny",
                # bench.py frames in flight (one HIP stream and hardware queue each): the frame's latency is set by
                # a few heavy top-row tiles, so 4 in flight cap the step at latency / 4 (walk exit)
-               inflight=8),
+               inflight=8,
+               # the frame kernel at 6 waves per SIMD: 6% faster here than the default 7 (C3 / C3L: 7 faster by
+               # 1-2%; profiles/r06_walk_latch_ab.txt)
+               tune={"frame1_waves": 6}),
     # C3: Sponza stand-in 1920x1080, Blinn kd=1, PointLight (0,10,0) 200
     "C3": dict(name="sponza stand-in (~66k tris) 1920x1080 Blinn+PointLight", W=1920, H=1080,
                camera=dict(eye=(8.0, 1.5, 1.0), lookAt=(0.0, 2.5, -1.0), up=(0, 1, 0), fov=55.0),

@@ -36,8 +36,8 @@ def close_frac(got, ref, rtol=1e-4):
 @pytest.mark.gpu
 @pytest.mark.parametrize("key", ["C2", "C3", "C3L", "C4", "C5", "D1"])
 def test_full_size_frame_matches_oracle(key):
-    """Under the config's own tuning (bench.py's: C3's nested camera-ray walk; the others the
-    library defaults), so every benched kernel form is the one compared here."""
+    """Under the config's own tuning (bench.py's: C3's nested camera-ray walk, C2's 6-wave frame
+    kernel; the others the library defaults), so every benched kernel form is compared here."""
     need_gpu()
     P, Osc, cam = config_scene(key)
     from miro import scenes
@@ -51,7 +51,7 @@ def test_full_size_frame_matches_oracle(key):
         hits = P.raytraceImage(camera(cam), img, want_hits=True)
     finally:
         for k in tune:
-            assert L.mrt_set_tuning(k.encode(), {"walk_latch": 1}[k]) == 0   # the library default
+            assert L.mrt_set_tuning(k.encode(), {"walk_latch": 1, "frame1_waves": 7}[k]) == 0   # the defaults
     ref = Osc.render(cam, W, H, threads=16, libm=O.LIBM_FLOAT)
     assert np.array_equal(hits["prim"], ref["hits"]["prim"]), f"{key}: primary hit ids differ"
     hit = ref["hits"]["prim"] >= 0
