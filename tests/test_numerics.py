@@ -99,7 +99,8 @@ def test_product_rcp_sweep_matches_oracle(tmp_path):
 
 @pytest.mark.gpu
 def test_device_rcp_matches_oracle():
-    """The device's rcp_nr (mrt_debug_libm fn 2) against the oracle on every 257th bit
+    """(All 2^32 inputs: tools/rcp_device_sweep.py, profiles/r06_rcp_device_sweep.txt.)
+    The device's rcp_nr (mrt_debug_libm fn 2) against the oracle on every 257th bit
     pattern (16.7 M inputs, all exponents, zeros, denormals, infinities, NaNs)."""
     if miro.device_count() < 1:
         pytest.skip("no HIP device")
