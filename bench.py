@@ -1065,7 +1065,10 @@ def main():
         out["frame_check"] = frame_check
     if st.get("fused"):   # the frame kernel's walk (LDS top nodes only with tuning lds_nodes 1)
         out["walk"] = scene.walk_info()
-        out["walk"]["latch"] = "nested" if tuning.get("walk_latch", 1) == 0 else "one"
+        # the camera-ray walk's loop end (mrt_device.hip: one latch unless tuned off, or the
+        # two-exit / LDS top-node walks, which are nested)
+        one = tuning.get("walk_latch", 1) != 0 and out["walk"]["walk_exits"] == 1 and out["walk"]["lds_nodes"] != 1
+        out["walk"]["latch"] = "one" if one else "nested"
     if split_times is not None:
         out["split_times"] = split_times
     if weak is not None:
